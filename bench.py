@@ -1,0 +1,267 @@
+#!/usr/bin/env python3
+"""Benchmark: CRC32C verify GiB/s (device-resident), 512 B chunks over 128 MiB
+HDFS blocks (BASELINE.json metric).
+
+One STEP = one verify pass of the hot path over this rank's whole batch:
+1024 blocks x 128 MiB (128 GiB) of splitmix64 data generated on device,
+expected per-chunk CRCs in wire (big-endian) order, 1 in 65537 chunks
+corrupted; output = mismatch bitmap + first bad chunk per block.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
+
+Ranks shard independent blocks (no data-path collective, scaling "weak");
+RCCL all-reduce only aggregates {bytes, mismatches} (sum) and time (max).
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+BLOCK = 128 << 20
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# SURVEY.md 8c pinned digests (reference-generated): _hdfs_crc32c(0, LE crc array)
+PINNED = {(0, 512): 0xF2590C08, (1, 512): 0xEB636035, (0, 4096): 0xB77BAB49, (1, 4096): 0xEF4F7B33}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--blocks", type=int, default=1024, help="128 MiB blocks per GPU")
+    ap.add_argument("--chunk", type=int, default=512)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-extra", action="store_true", help="skip compute/mixed side measurements")
+    ap.add_argument("--cpu-gib", type=float, default=2.0, help="CPU baseline sample size")
+    return ap.parse_args()
+
+
+class Dist:
+    """torch.distributed (nccl = RCCL over xGMI) only when launched as N ranks."""
+
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.torch = None
+        if self.world > 1:
+            import torch
+            import torch.distributed as dist
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            torch.cuda.set_device(self.local)
+            dist.init_process_group("nccl")
+            self.torch, self.dist = torch, dist
+
+    def barrier(self):
+        if self.torch:
+            self.dist.barrier(device_ids=[self.local])
+
+    def allreduce(self, vals, op):
+        if not self.torch:
+            return vals
+        t = self.torch.tensor(vals, dtype=self.torch.float64, device=f"cuda:{self.local}")
+        self.dist.all_reduce(t, op=getattr(self.dist.ReduceOp, op))
+        return t.tolist()
+
+    def close(self):
+        if self.torch:
+            self.dist.destroy_process_group()
+
+
+def cpu_baseline(sample_gib):
+    """Reference CPU path timed on this host (rank 0, N=1): the reference's own
+    _hdfs_sse42_crc32c compiled from its sources (oracle/_ref) when present,
+    else the oracle's SSE4.2 restatement.  A reported baseline, not the target."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import ctypes
+
+    from oracle import Oracle, Reference, have_reference
+    o = Oracle()
+    nbytes = int(sample_gib * (1 << 30)) // BLOCK * BLOCK
+    t0 = time.time()
+    data = o.splitmix(nbytes // 8, 0, 0).view("uint8")
+    gen_s = time.time() - t0
+    if have_reference():
+        ext = Reference().sse42_addr
+        kind, fn, label = "reference", "ext", "_hdfs_sse42_crc32c (src/crc32c_sse42.c built from /root/reference)"
+    else:
+        ext, kind, fn, label = None, "port", "hw", "oracle SSE4.2 3-way restatement"
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    s1, crc1 = o.bench_chunks(data, 512, 1, fn, ext)
+    passes = 8
+    tn = 0.0
+    for _ in range(passes):
+        s, _ = o.bench_chunks(data, 512, threads, fn, ext)
+        tn += s
+    # cross-check one block against the pinned digest
+    dig = o.crc32c(0, crc1[: BLOCK // 512].view("uint8"), "hw")
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    gib = nbytes / (1 << 30)
+    return {
+        "value": round(gib * passes / tn, 2),
+        "unit": "GiB/s",
+        "cores": threads,
+        "kind": kind,
+        "sample": f"{label}; per-512B-chunk CRCs over {gib:.0f} GiB splitmix64 (blocks 0..{nbytes // BLOCK - 1}), "
+                  f"{threads} threads x {passes} passes; single core {gib / s1:.2f} GiB/s",
+        "single_core_value": round(gib / s1, 3),
+        "cpu_model": model or platform.processor(),
+        "nproc": os.cpu_count(),
+        "digest_ok": dig == PINNED[(0, 512)],
+        "datagen_s": round(gen_s, 2),
+    }
+
+
+def main():
+    args = parse()
+    d = Dist()
+    import hadoofus_amd as h
+
+    h.load()
+    arch, ncu = h.device_info()
+    B, cs = args.blocks, args.chunk
+    per = BLOCK // cs
+    g_block0 = d.rank * B
+    stream = h.stream_create()
+
+    data = h.DeviceBuffer(B * BLOCK)
+    crcs = h.DeviceBuffer(B * (BLOCK // 512) * 4)
+    bms = h.DeviceBuffer(B * (BLOCK // 512) // 8)
+    h.fill_splitmix64(data.ptr, B * BLOCK // 8, 0, g_block0 << 24, None)
+
+    def segs(chunk_of, flags, with_bitmap):
+        out, off_c, off_b = [], 0, 0
+        for b in range(B):
+            c = chunk_of(b)
+            n = BLOCK // c
+            out.append(h.Segment(data=data.ptr + b * BLOCK, len=BLOCK, chunk_size=c, flags=flags, crc_init=0,
+                                 crcs=crcs.ptr + off_c * 4, bitmap=(bms.ptr + off_b // 8) if with_bitmap else None))
+            off_c += n
+            off_b += n
+        return out
+
+    extra = {}
+    # Digest check of the hot kernel's output on the pinned blocks (rank 0 owns blocks 0 and 1).
+    digest_ok = None
+    if d.rank == 0 and B >= 2:
+        digest_ok = True
+        for c in (512, 4096):
+            p = h.Plan(h.MODE_COMPUTE, segs(lambda b: c, 0, False)[:2])
+            p.execute()
+            for blk in (0, 1):
+                got = h.stream_crc_dev(0, crcs.ptr + blk * (BLOCK // c) * 4, (BLOCK // c) * 4)
+                digest_ok &= got == PINNED[(blk, c)]
+            p.destroy()
+
+    # C2: compute-only (also produces the expected wire CRCs for C3).
+    comp = h.Plan(h.MODE_COMPUTE, segs(lambda b: cs, h.SEG_BE, False))
+    comp.execute()
+    if not args.no_extra:
+        ms = comp.time(3, stream)
+        extra["compute_gibps"] = round(B * BLOCK / (ms * 1e-3) / (1 << 30), 1)
+        comp.execute()  # restore expected CRCs (identical) on the default stream
+    h.stream_sync(None)
+
+    # Corrupt 1 in 65537 chunks (global chunk index), then verify.
+    for b in range(B):
+        h.corrupt(data.ptr + b * BLOCK, BLOCK, cs, (g_block0 + b) * per, 65537, 7919, None)
+    h.stream_sync(None)
+    first = (g_block0 * per + 65536) // 65537 * 65537
+    expect_bad = max(0, ((g_block0 + B) * per - 1 - first) // 65537 + 1) if first < (g_block0 + B) * per else 0
+
+    ver = h.Plan(h.MODE_VERIFY, segs(lambda b: cs, h.SEG_BE, True))
+    for _ in range(args.warmup):
+        ver.execute(stream)
+    h.stream_sync(stream)
+    _, m = ver.results(stream)
+    parity_ok = m == expect_bad
+
+    ver.set_timing(True)
+    d.barrier()
+    h.stream_sync(stream)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ver.execute(stream)
+    h.stream_sync(stream)
+    d.barrier()
+    t1 = time.perf_counter()
+    kms, nlaunch = ver.kernel_ms()
+    first_bad, m = ver.results(stream)
+    parity_ok &= m == expect_bad
+    elapsed = t1 - t0
+
+    if not args.no_extra:
+        # C5: mixed bytesPerChecksum 512/1024/2048/4096 in one launch (compute + verify)
+        mixc = h.Plan(h.MODE_COMPUTE, segs(lambda b: 512 << (b % 4), h.SEG_BE, False))
+        mixc.execute(stream)
+        mixv = h.Plan(h.MODE_VERIFY, segs(lambda b: 512 << (b % 4), h.SEG_BE, True))
+        mixv.execute(stream)
+        ms = mixv.time(3, stream)
+        _, mm = mixv.results(stream)
+        extra["mixed_verify_gibps"] = round(B * BLOCK / (ms * 1e-3) / (1 << 30), 1)
+        extra["mixed_mismatches"] = int(mm)
+        mixc.destroy()
+        mixv.destroy()
+
+    tot_bytes, tot_mism, ok = d.allreduce([float(B * BLOCK * args.steps), float(m), float(parity_ok)], "SUM")
+    (t_max,) = d.allreduce([elapsed], "MAX")
+    n = d.world
+
+    if d.rank == 0:
+        gib_s = tot_bytes / t_max / (1 << 30)
+        nbytes = B * BLOCK
+        alg = nbytes + 4 * nbytes / cs + nbytes / (8 * cs)  # data + expected CRCs + bitmap
+        k_avg_s = kms / max(1, nlaunch) * 1e-3
+        achieved = alg / k_avg_s / 1e9
+        line = {
+            "metric": "CRC32C verify GiB/s (device-resident), 512B chunks over 128MiB HDFS blocks",
+            "value": round(gib_s, 1),
+            "unit": "GiB/s",
+            "n_gpus": n,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(t_max / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic",
+            "config": {
+                "workload": "C3 verify: 128MiB HDFS blocks of splitmix64 data, 512B chunks, BE wire CRCs, "
+                            "1/65537 chunks corrupted, bitmap + first-bad out",
+                "blocks_per_gpu": B, "block_bytes": BLOCK, "chunk_size": cs,
+                "bytes_per_gpu_per_step": nbytes, "parallelism": f"shard{n}",
+            },
+            "roofline": {
+                "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+                "kernel": "crc32c_tiles_kernel<verify>", "kernel_avg_ms": round(k_avg_s * 1e3, 3),
+                "alg_bytes_per_launch": int(alg),
+            },
+            "parity": {"mismatches": int(tot_mism), "expected_per_gpu": int(expect_bad),
+                       "all_ranks_ok": ok == n, "pinned_digests_ok": digest_ok},
+            "device": {"arch": arch, "cus": ncu},
+            "extra": extra,
+        }
+        if n == 1 and not args.no_cpu:
+            line["cpu_baseline"] = cpu_baseline(args.cpu_gib)
+        print(json.dumps(line), flush=True)
+    d.close()
+
+
+if __name__ == "__main__":
+    main()

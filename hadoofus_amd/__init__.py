@@ -1,0 +1,37 @@
+"""hadoofus_amd -- MI355X-native CRC32C chunk engine for hadoofus's datanode path.
+
+The product is the C-ABI shared library ``hadoofus_amd/lib/libhadoofus_crc32c.so``
+(include/hadoofus_crc32c.h, include/crc32c.h).  This package is a thin ctypes
+mirror of that ABI used by the tests and bench; it has no compute of its own
+and no fallback: if the library or a gfx950 device is missing, calls fail.
+"""
+from .crc32c import (  # noqa: F401
+    LIB_PATH,
+    CSUM_NULL,
+    CSUM_CRC32,
+    CSUM_CRC32C,
+    ERR_BAD_CHECKSUM,
+    ERR_CRC_LEN,
+    ERR_PACKET_SIZE,
+    ERR_UNSUPPORTED_CHECKSUM,
+    MODE_COMPUTE,
+    MODE_VERIFY,
+    SEG_BE,
+    SEG_RAW,
+    CRC32CError,
+    DeviceBuffer,
+    Plan,
+    Segment,
+    crc32c,
+    compose_crcs,
+    corrupt,
+    fill_splitmix64,
+    stream_create,
+    stream_sync,
+    device_info,
+    load,
+    stream_crc_dev,
+    verify_crcdata,
+)
+
+__all__ = [n for n in dir() if not n.startswith("_")]

@@ -1,0 +1,54 @@
+"""Build libhadoofus_crc32c.so in-tree for gfx950 (MI355X) with hipcc.
+
+The shared library is the product: the C ABI of include/hadoofus_crc32c.h and
+the drop-in symbols of include/crc32c.h.  It is built in-tree so the .so
+travels with the repository snapshot to the GPU box.
+"""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+INCLUDE = os.path.join(ROOT, "include")
+LIBDIR = os.path.join(HERE, "lib")
+LIB = os.path.join(LIBDIR, "libhadoofus_crc32c.so")
+SOURCES = ["crc32c_kernels.hip", "crc32c_engine.cpp"]
+HEADERS = ["crc32c_internal.h", "crc32c_tables.h"]
+ARCH = os.environ.get("HADOOFUS_OFFLOAD_ARCH", "gfx950")
+
+
+def _hipcc():
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
+        if c and (os.path.isabs(c) and os.path.exists(c) or not os.path.isabs(c)):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def _stale():
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
+    deps += [os.path.join(INCLUDE, "hadoofus_crc32c.h"), os.path.join(INCLUDE, "crc32c.h")]
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force=False, verbose=False):
+    if not force and not _stale():
+        return LIB
+    os.makedirs(LIBDIR, exist_ok=True)
+    tmp = LIB + ".tmp"
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-Wall", "-Wno-unused-function", f"-I{INCLUDE}", f"-I{CSRC}",
+           "-o", tmp] + [os.path.join(CSRC, f) for f in SOURCES]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.check_call(cmd)
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

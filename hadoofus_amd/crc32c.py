@@ -1,0 +1,263 @@
+"""ctypes mirror of include/hadoofus_crc32c.h.
+
+Function names follow the reference's interface for this path:
+  crc32c(crc, buf)                 <- _hdfs_crc32c (src/crc32c.h:13)
+  verify_crcdata(region, ...)      <- _verify_crcdata (src/datanode.c:2931-2963)
+  compose_crcs(iovecs, chunk)      <- CRC loop of _compose_data_packet_header
+                                      (src/datanode.c:2814-2860)
+plus the additive device batch API (Plan / Segment) and device-memory helpers.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libhadoofus_crc32c.so")
+
+# include/objects.h:169-175
+CSUM_NULL, CSUM_CRC32, CSUM_CRC32C = 0, 1, 2
+# include/objects.h:21-113 (enum hdfs_error_numeric values)
+ERR_UNSUPPORTED_CHECKSUM = 8
+ERR_PACKET_SIZE = 25
+ERR_CRC_LEN = 26
+ERR_BAD_CHECKSUM = 29
+MODE_COMPUTE, MODE_VERIFY = 0, 1
+SEG_BE, SEG_RAW = 1, 2
+
+_u32, _u64, _vp, _sz, _int = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+
+
+class CRC32CError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"hadoofus_crc32c error {code}: {msg}")
+        self.code = code
+
+
+class Segment(ctypes.Structure):
+    """struct hdfs_crc32c_segment."""
+    _fields_ = [
+        ("data", _vp),
+        ("len", _u64),
+        ("chunk_size", _u32),
+        ("flags", _u32),
+        ("crc_init", _u32),
+        ("reserved", _u32),
+        ("crcs", _vp),
+        ("bitmap", _vp),
+    ]
+
+
+_lib = None
+
+
+def _bind(lib, name, res, args):
+    f = getattr(lib, name)
+    f.restype = res
+    f.argtypes = args
+    return f
+
+
+def load(path=LIB_PATH):
+    """Load the product library (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise ImportError(f"{path} not built; run `python -m hadoofus_amd.build` "
+                          "(or __graft_entry__.build())")
+    lib = ctypes.CDLL(path)
+    for n in ("_hdfs_crc32c", "_hdfs_sse42_crc32c", "_hdfs_sw_crc32c"):
+        _bind(lib, n, _u32, [_u32, _vp, ctypes.c_uint])
+    _bind(lib, "hdfs_crc32c_last_error", ctypes.c_char_p, [])
+    _bind(lib, "hdfs_crc32c_init", _int, [_int])
+    _bind(lib, "hdfs_crc32c_device_info", _int, [_int, ctypes.c_char_p, _sz, ctypes.POINTER(_int)])
+    _bind(lib, "hdfs_crc32c_plan_create", _int, [ctypes.POINTER(_vp), _int, ctypes.POINTER(Segment), _sz])
+    _bind(lib, "hdfs_crc32c_plan_execute", _int, [_vp, _vp])
+    _bind(lib, "hdfs_crc32c_plan_results", _int, [_vp, _vp, ctypes.POINTER(_u32), _sz, ctypes.POINTER(_u64)])
+    _bind(lib, "hdfs_crc32c_plan_set_timing", _int, [_vp, _int])
+    _bind(lib, "hdfs_crc32c_plan_kernel_ms", _int, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_int)])
+    _bind(lib, "hdfs_crc32c_plan_stats", _int, [_vp, ctypes.POINTER(_u64), ctypes.POINTER(_u64), ctypes.POINTER(_u64)])
+    _bind(lib, "hdfs_crc32c_plan_destroy", None, [_vp])
+    _bind(lib, "hdfs_crc32c_plan_time", _int, [_vp, _vp, _int, ctypes.POINTER(ctypes.c_double)])
+    _bind(lib, "hdfs_crc32c_stream_dev", _int, [_u32, _vp, _u64, ctypes.POINTER(_u32)])
+    _bind(lib, "hdfs_crc32c_verify_crcdata", _int,
+          [_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _int, ctypes.POINTER(ctypes.c_int32)])
+    _bind(lib, "hdfs_crc32c_compose_crcs", _int,
+          [ctypes.POINTER(_vp), ctypes.POINTER(_sz), _int, _sz, _u32, _vp])
+    _bind(lib, "hdfs_crc32c_dev_alloc", _int, [ctypes.POINTER(_vp), _u64])
+    _bind(lib, "hdfs_crc32c_dev_free", _int, [_vp])
+    _bind(lib, "hdfs_crc32c_memcpy", _int, [_vp, _vp, _u64, _int])
+    _bind(lib, "hdfs_crc32c_memset", _int, [_vp, _int, _u64])
+    _bind(lib, "hdfs_crc32c_stream_create", _int, [ctypes.POINTER(_vp)])
+    _bind(lib, "hdfs_crc32c_stream_destroy", _int, [_vp])
+    _bind(lib, "hdfs_crc32c_stream_sync", _int, [_vp])
+    _bind(lib, "hdfs_crc32c_fill_splitmix64", _int, [_vp, _u64, _u64, _u64, _vp])
+    _bind(lib, "hdfs_crc32c_corrupt", _int, [_vp, _u64, _u32, _u64, _u64, _u64, _vp])
+    _lib = lib
+    return lib
+
+
+def _check(rc):
+    if rc != 0:
+        raise CRC32CError(rc, load().hdfs_crc32c_last_error().decode(errors="replace"))
+
+
+def _host(buf):
+    if isinstance(buf, np.ndarray):
+        a = np.ascontiguousarray(buf)
+        return a, a.ctypes.data, a.nbytes
+    a = np.frombuffer(memoryview(buf).cast("B"), dtype=np.uint8)
+    return a, (a.ctypes.data if a.nbytes else None), a.nbytes
+
+
+def device_info(device=-1):
+    arch = ctypes.create_string_buffer(64)
+    ncu = _int(0)
+    _check(load().hdfs_crc32c_device_info(device, arch, 64, ctypes.byref(ncu)))
+    return arch.value.decode(), ncu.value
+
+
+def crc32c(crc, buf, entry="_hdfs_crc32c"):
+    """_hdfs_crc32c(crc, buf, len) on host memory (src/crc32c.h:13)."""
+    keep, p, n = _host(buf)
+    return getattr(load(), entry)(crc & 0xFFFFFFFF, p, n)
+
+
+def stream_crc_dev(crc, dptr, nbytes):
+    out = _u32(0)
+    _check(load().hdfs_crc32c_stream_dev(crc & 0xFFFFFFFF, dptr, nbytes, ctypes.byref(out)))
+    return out.value
+
+
+def verify_crcdata(region, chunksize, crcdlen, dlen, ctype=CSUM_CRC32C):
+    """_verify_crcdata on a host packet region [BE crcs | data].
+
+    Returns (err, first_bad): err 0 on success or the reference error number
+    (ERR_CRC_LEN / ERR_BAD_CHECKSUM / ...); negative values are engine errors."""
+    keep, p, n = _host(region)
+    fb = ctypes.c_int32(-1)
+    rc = load().hdfs_crc32c_verify_crcdata(p, chunksize, crcdlen, dlen, ctype, ctypes.byref(fb))
+    if rc < 0:
+        _check(rc)
+    return rc, fb.value
+
+
+def compose_crcs(iovecs, chunk=512):
+    """BE CRC bytes for the concatenation of host fragments (write path)."""
+    arrs = [_host(v) for v in iovecs]
+    total = sum(a[2] for a in arrs)
+    n = len(arrs)
+    bases = (_vp * max(n, 1))(*[a[1] for a in arrs])
+    lens = (_sz * max(n, 1))(*[a[2] for a in arrs])
+    out = np.zeros(((total + chunk - 1) // chunk) * 4, dtype=np.uint8)
+    if total:
+        _check(load().hdfs_crc32c_compose_crcs(bases, lens, n, total, chunk, out.ctypes.data))
+    return out.tobytes()
+
+
+class DeviceBuffer:
+    """hipMalloc'd memory owned by the engine's device."""
+
+    def __init__(self, nbytes):
+        self.nbytes = int(nbytes)
+        p = _vp()
+        _check(load().hdfs_crc32c_dev_alloc(ctypes.byref(p), self.nbytes))
+        self.ptr = p.value
+
+    def upload(self, host, offset=0):
+        keep, p, n = _host(host)
+        assert offset + n <= self.nbytes
+        if n:
+            _check(load().hdfs_crc32c_memcpy(self.ptr + offset, p, n, 0))
+
+    def download(self, nbytes=None, offset=0, dtype=np.uint8):
+        nbytes = self.nbytes - offset if nbytes is None else nbytes
+        out = np.empty(nbytes, dtype=np.uint8)
+        if nbytes:
+            _check(load().hdfs_crc32c_memcpy(out.ctypes.data, self.ptr + offset, nbytes, 1))
+        return out.view(dtype)
+
+    def fill(self, value=0):
+        _check(load().hdfs_crc32c_memset(self.ptr, value, self.nbytes))
+
+    def free(self):
+        if self.ptr:
+            load().hdfs_crc32c_dev_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Plan:
+    """Batch compute/verify plan over a list of Segment descriptors."""
+
+    def __init__(self, mode, segments):
+        self.mode = mode
+        self.nseg = len(segments)
+        arr = (Segment * max(1, self.nseg))(*segments)
+        self._segs = arr
+        p = _vp()
+        _check(load().hdfs_crc32c_plan_create(ctypes.byref(p), mode, arr, self.nseg))
+        self.ptr = p.value
+
+    def execute(self, stream=None):
+        _check(load().hdfs_crc32c_plan_execute(self.ptr, stream))
+
+    def results(self, stream=None):
+        fb = (_u32 * max(1, self.nseg))()
+        m = _u64(0)
+        _check(load().hdfs_crc32c_plan_results(self.ptr, stream, fb, self.nseg, ctypes.byref(m)))
+        return list(fb)[: self.nseg], m.value
+
+    def set_timing(self, on=True):
+        _check(load().hdfs_crc32c_plan_set_timing(self.ptr, 1 if on else 0))
+
+    def kernel_ms(self):
+        t = ctypes.c_double(0)
+        n = _int(0)
+        _check(load().hdfs_crc32c_plan_kernel_ms(self.ptr, ctypes.byref(t), ctypes.byref(n)))
+        return t.value, n.value
+
+    def stats(self):
+        a, b, c = _u64(), _u64(), _u64()
+        _check(load().hdfs_crc32c_plan_stats(self.ptr, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
+        return {"main_bytes": a.value, "generic_bytes": b.value, "nchunks": c.value}
+
+    def time(self, iters, stream=None):
+        ms = ctypes.c_double(0)
+        _check(load().hdfs_crc32c_plan_time(self.ptr, stream, iters, ctypes.byref(ms)))
+        return ms.value
+
+    def destroy(self):
+        if self.ptr:
+            load().hdfs_crc32c_plan_destroy(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:
+            pass
+
+
+def stream_create():
+    s = _vp()
+    _check(load().hdfs_crc32c_stream_create(ctypes.byref(s)))
+    return s.value
+
+
+def stream_sync(s):
+    _check(load().hdfs_crc32c_stream_sync(s))
+
+
+def fill_splitmix64(dptr, nwords, seed=0, g0=0, stream=None):
+    _check(load().hdfs_crc32c_fill_splitmix64(dptr, nwords, seed, g0, stream))
+
+
+def corrupt(dptr, nbytes, chunk, chunk0, modulus=65537, bitmul=7919, stream=None):
+    _check(load().hdfs_crc32c_corrupt(dptr, nbytes, chunk, chunk0, modulus, bitmul, stream))

@@ -1,0 +1,653 @@
+// Host engine + C ABI of libhadoofus_crc32c.so (declared in
+// include/hadoofus_crc32c.h and include/crc32c.h).
+//
+// Replaces the reference's CRC32C dispatcher src/crc32c.c:55-110 (ifunc /
+// constructor backend selection) with a per-device engine: tables are built
+// once per device (the analogue of the constructors src/crc32c_sw.c:73 and
+// src/crc32c_sse42.c:204), segment tables are uploaded once per plan, and
+// every CRC is computed by the gfx950 kernels in crc32c_kernels.hip.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "crc32c_internal.h"
+#include "crc32c_tables.h"
+#include "hadoofus_crc32c.h"
+
+namespace hdfs_crc32c {
+
+hipError_t launch_tiles(int mode, int grid, const SegDev *segs, uint32_t nseg, uint64_t total_rounds,
+                        const uint32_t *gtab, uint32_t *first_bad, unsigned long long *mism,
+                        hipStream_t stream);
+hipError_t launch_generic(int mode, const SegDev *segs, uint32_t nseg, uint64_t total_gtiles,
+                          const uint32_t *gtab, uint32_t *first_bad, unsigned long long *mism,
+                          hipStream_t stream);
+hipError_t launch_combine(const uint32_t *raws, uint64_t nraw, uint32_t cs, uint64_t len,
+                          const uint32_t *pow2, uint32_t reg0, uint32_t *acc, hipStream_t stream);
+hipError_t launch_fill(uint64_t *out, uint64_t nwords, uint64_t seed, uint64_t g0, hipStream_t stream);
+hipError_t launch_corrupt(uint8_t *data, uint64_t len, uint32_t cs, uint64_t chunk0, uint64_t modulus,
+                          uint64_t bitmul, hipStream_t stream);
+
+namespace {
+
+thread_local char g_err[512] = "";
+
+int fail(int code, const char *fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+#define HIPCHK(expr)                                                                   \
+  do {                                                                                 \
+    hipError_t e_ = (expr);                                                            \
+    if (e_ != hipSuccess)                                                              \
+      return fail(HDFS_CRC32C_EHIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_),    \
+                  __FILE__, __LINE__);                                                 \
+  } while (0)
+
+constexpr int kMaxDev = 64;
+constexpr uint32_t kStreamPiece = 4096;          // stream CRC: raw CRC per 4 KiB piece
+constexpr size_t kStageCap = size_t(64) << 20;   // host->device staging for one-shots
+
+struct DevCtx {
+  bool ready = false;
+  int dev = -1;
+  int num_cu = 0;
+  char arch[64] = "";
+  uint32_t *d_tab_main = nullptr;
+  uint32_t *d_tab_pow2 = nullptr;
+  hipStream_t stream = nullptr;
+  // one-shot scratch (guarded by mu)
+  uint8_t *h_stage = nullptr;
+  uint8_t *d_stage = nullptr;
+  uint32_t *d_raw = nullptr;
+  size_t raw_cap = 0;
+  SegDev *d_seg = nullptr;
+  uint32_t *d_small = nullptr;  // [0] acc, [1] first_bad, [2..3] mismatches
+  std::mutex mu;
+};
+
+DevCtx g_ctx[kMaxDev];
+std::mutex g_init_mu;
+
+struct DeviceGuard {
+  int prev = -1;
+  bool changed = false;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) == hipSuccess && prev != dev) {
+      changed = hipSetDevice(dev) == hipSuccess;
+    }
+  }
+  ~DeviceGuard() {
+    if (changed) (void)hipSetDevice(prev);
+  }
+};
+
+int ctx_init(int device, DevCtx **out) {
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess || ndev <= 0)
+    return fail(HDFS_CRC32C_ENODEV, "no HIP device visible (%s)",
+                e != hipSuccess ? hipGetErrorString(e) : "count 0");
+  if (device < 0) {
+    if (hipGetDevice(&device) != hipSuccess) device = 0;
+  }
+  if (device >= ndev || device >= kMaxDev)
+    return fail(HDFS_CRC32C_ENODEV, "device %d out of range (%d visible)", device, ndev);
+  DevCtx &c = g_ctx[device];
+  if (c.ready) {
+    *out = &c;
+    return HDFS_CRC32C_OK;
+  }
+  std::lock_guard<std::mutex> lk(g_init_mu);
+  if (c.ready) {
+    *out = &c;
+    return HDFS_CRC32C_OK;
+  }
+  hipDeviceProp_t prop;
+  HIPCHK(hipGetDeviceProperties(&prop, device));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(HDFS_CRC32C_ENODEV, "device %d is %s; this engine is built for gfx950 (MI355X) only",
+                device, prop.gcnArchName);
+  DeviceGuard g(device);
+  c.dev = device;
+  c.num_cu = prop.multiProcessorCount;
+  std::snprintf(c.arch, sizeof(c.arch), "%s", prop.gcnArchName);
+
+  // Tables (cf. the reference's load-time constructors).
+  std::vector<uint32_t> main(kTabMainWords), pow2(kTabPow2Words);
+  uint32_t t[4][256];
+  make_slicing4(t);
+  std::memcpy(main.data(), t, sizeof(t));
+  for (int k = 1; k <= 7; k++)
+    zeros_byte_tables(zeros_op(64ull * k), main.data() + kTabSliceWords + (k - 1) * 1024);
+  Gf2 op = zeros_op(1);
+  for (uint32_t b = 0; b < kPow2Levels; b++) {
+    zeros_byte_tables(op, pow2.data() + b * 1024);
+    op = op.compose(op);
+  }
+  HIPCHK(hipMalloc(&c.d_tab_main, main.size() * 4));
+  HIPCHK(hipMalloc(&c.d_tab_pow2, pow2.size() * 4));
+  HIPCHK(hipMemcpy(c.d_tab_main, main.data(), main.size() * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(c.d_tab_pow2, pow2.data(), pow2.size() * 4, hipMemcpyHostToDevice));
+  // Blocking stream: it serialises with the legacy NULL stream, so the
+  // synchronous helpers (hipMemcpy/hipMemset) see prior plan work.
+  HIPCHK(hipStreamCreate(&c.stream));
+  HIPCHK(hipHostMalloc(&c.h_stage, kStageCap, hipHostMallocDefault));
+  HIPCHK(hipMalloc(&c.d_stage, kStageCap));
+  HIPCHK(hipMalloc(&c.d_seg, sizeof(SegDev)));
+  HIPCHK(hipMalloc(&c.d_small, 64));
+  c.ready = true;
+  *out = &c;
+  return HDFS_CRC32C_OK;
+}
+
+// Split a segment between the tiled kernel and the generic kernel.
+// Tiled: data 16-B aligned, chunk_size a multiple of 512, full chunks only.
+void classify(SegDev &s, uint64_t &rounds, uint64_t &gtiles) {
+  const uint64_t ntiles = (uint64_t(s.nchunks) + kTileChunks - 1) / kTileChunks;
+  const bool eligible = s.nchunks > 0 && (reinterpret_cast<uintptr_t>(s.data) & 15u) == 0 &&
+                        s.chunk_size % kRoundBytes == 0;
+  const bool partial = s.len % s.chunk_size != 0;
+  if (eligible) {
+    s.main_tiles = static_cast<uint32_t>(partial ? ntiles - 1 : ntiles);
+    s.gen_tiles = partial ? 1u : 0u;
+  } else {
+    s.main_tiles = 0;
+    s.gen_tiles = static_cast<uint32_t>(ntiles);
+  }
+  s.round_start = rounds;
+  s.gtile_start = gtiles;
+  rounds += uint64_t(s.main_tiles) * (s.chunk_size / kRoundBytes);
+  gtiles += s.gen_tiles;
+}
+
+int fill_seg(const hdfs_crc32c_segment &in, int mode, SegDev &s, size_t idx) {
+  if (in.chunk_size == 0) return fail(HDFS_CRC32C_EINVAL, "segment %zu: chunk_size 0", idx);
+  const uint64_t nch = (in.len + in.chunk_size - 1) / in.chunk_size;
+  if (nch > 0xFFFFFFF0ull) return fail(HDFS_CRC32C_EINVAL, "segment %zu: too many chunks", idx);
+  if (in.len && !in.data) return fail(HDFS_CRC32C_EINVAL, "segment %zu: null data", idx);
+  if (nch && !in.crcs) return fail(HDFS_CRC32C_EINVAL, "segment %zu: null crcs", idx);
+  if (mode == HDFS_CRC32C_MODE_VERIFY && nch && !in.bitmap)
+    return fail(HDFS_CRC32C_EINVAL, "segment %zu: verify needs a bitmap", idx);
+  if (mode == HDFS_CRC32C_MODE_VERIFY && (in.flags & HDFS_CRC32C_SEG_RAW))
+    return fail(HDFS_CRC32C_EINVAL, "segment %zu: RAW flag is compute-only", idx);
+  if (in.flags & ~(HDFS_CRC32C_SEG_BE | HDFS_CRC32C_SEG_RAW))
+    return fail(HDFS_CRC32C_EINVAL, "segment %zu: unknown flags 0x%x", idx, in.flags);
+  std::memset(&s, 0, sizeof(s));
+  s.data = static_cast<const uint8_t *>(in.data);
+  s.len = in.len;
+  s.crcs = static_cast<uint32_t *>(in.crcs);
+  s.bitmap = in.bitmap;
+  s.chunk_size = in.chunk_size;
+  s.flags = in.flags;
+  s.nchunks = static_cast<uint32_t>(nch);
+  s.reg_init = (in.flags & HDFS_CRC32C_SEG_RAW) ? 0u : ~in.crc_init;
+  return HDFS_CRC32C_OK;
+}
+
+bool device_accessible(const void *p) {
+  if (!p) return true;
+  hipPointerAttribute_t a;
+  hipError_t e = hipPointerGetAttributes(&a, p);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.devicePointer != nullptr;
+}
+
+int launch_all(DevCtx &c, int mode, const SegDev *d_segs, uint32_t nseg, uint64_t rounds,
+               uint64_t gtiles, uint32_t *d_fb, unsigned long long *d_mism, hipStream_t st,
+               hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr) {
+  if (mode == kModeVerify) {
+    HIPCHK(hipMemsetAsync(d_fb, 0xFF, sizeof(uint32_t) * (nseg ? nseg : 1), st));
+    HIPCHK(hipMemsetAsync(d_mism, 0, sizeof(unsigned long long), st));
+  }
+  if (rounds) {
+    // >= 16 rounds per wave (16 waves per block) before adding blocks.
+    uint64_t want = (rounds + 255) / 256;
+    int grid = static_cast<int>(want < 1 ? 1 : (want > uint64_t(c.num_cu) ? c.num_cu : want));
+    if (ev0) HIPCHK(hipEventRecord(ev0, st));
+    HIPCHK(launch_tiles(mode, grid, d_segs, nseg, rounds, c.d_tab_main, d_fb, d_mism, st));
+    if (ev1) HIPCHK(hipEventRecord(ev1, st));
+  }
+  if (gtiles) HIPCHK(launch_generic(mode, d_segs, nseg, gtiles, c.d_tab_main, d_fb, d_mism, st));
+  return HDFS_CRC32C_OK;
+}
+
+// CRC of one device buffer continuing from crc (caller holds c.mu).
+int stream_crc_locked(DevCtx &c, uint32_t crc, const void *dbuf, uint64_t len, uint32_t *out) {
+  if (len == 0) {
+    *out = crc;
+    return HDFS_CRC32C_OK;
+  }
+  const uint64_t nraw = (len + kStreamPiece - 1) / kStreamPiece;
+  if (nraw > c.raw_cap) {
+    if (c.d_raw) HIPCHK(hipFree(c.d_raw));
+    c.d_raw = nullptr;
+    size_t cap = 1024;
+    while (cap < nraw) cap *= 2;
+    HIPCHK(hipMalloc(&c.d_raw, cap * 4));
+    c.raw_cap = cap;
+  }
+  hdfs_crc32c_segment in = {dbuf, len, kStreamPiece, HDFS_CRC32C_SEG_RAW, 0, 0, c.d_raw, nullptr};
+  SegDev s;
+  int rc = fill_seg(in, HDFS_CRC32C_MODE_COMPUTE, s, 0);
+  if (rc) return rc;
+  uint64_t rounds = 0, gtiles = 0;
+  classify(s, rounds, gtiles);
+  HIPCHK(hipMemcpyAsync(c.d_seg, &s, sizeof(s), hipMemcpyHostToDevice, c.stream));
+  rc = launch_all(c, kModeCompute, c.d_seg, 1, rounds, gtiles, nullptr, nullptr, c.stream);
+  if (rc) return rc;
+  HIPCHK(hipMemsetAsync(c.d_small, 0, 4, c.stream));
+  HIPCHK(launch_combine(c.d_raw, nraw, kStreamPiece, len, c.d_tab_pow2, ~crc, c.d_small, c.stream));
+  uint32_t acc = 0;
+  HIPCHK(hipMemcpyAsync(&acc, c.d_small, 4, hipMemcpyDeviceToHost, c.stream));
+  HIPCHK(hipStreamSynchronize(c.stream));
+  *out = ~acc;
+  return HDFS_CRC32C_OK;
+}
+
+int stream_crc_any(uint32_t crc, const void *buf, uint64_t len, uint32_t *out) {
+  DevCtx *c = nullptr;
+  int rc = ctx_init(-1, &c);
+  if (rc) return rc;
+  DeviceGuard g(c->dev);
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (len == 0) {
+    *out = crc;
+    return HDFS_CRC32C_OK;
+  }
+  if (device_accessible(buf)) return stream_crc_locked(*c, crc, buf, len, out);
+  const uint8_t *p = static_cast<const uint8_t *>(buf);
+  while (len) {
+    const size_t n = len < kStageCap ? size_t(len) : kStageCap;
+    std::memcpy(c->h_stage, p, n);
+    HIPCHK(hipMemcpyAsync(c->d_stage, c->h_stage, n, hipMemcpyHostToDevice, c->stream));
+    rc = stream_crc_locked(*c, crc, c->d_stage, n, &crc);
+    if (rc) return rc;
+    p += n;
+    len -= n;
+  }
+  *out = crc;
+  return HDFS_CRC32C_OK;
+}
+
+[[noreturn]] void die(const char *who) {
+  std::fprintf(stderr, "%s: MI355X CRC32C engine unavailable: %s\n", who, g_err);
+  std::abort();
+}
+
+}  // namespace
+}  // namespace hdfs_crc32c
+
+using namespace hdfs_crc32c;
+
+struct hdfs_crc32c_plan {
+  int dev = -1;
+  int mode = 0;
+  uint32_t nseg = 0;
+  SegDev *d_segs = nullptr;
+  uint32_t *d_first_bad = nullptr;
+  unsigned long long *d_mism = nullptr;
+  uint64_t rounds = 0, gtiles = 0, main_bytes = 0, gen_bytes = 0, nchunks = 0;
+  bool timing = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
+};
+
+extern "C" {
+
+const char *hdfs_crc32c_last_error(void) { return g_err; }
+
+int hdfs_crc32c_init(int device) {
+  DevCtx *c = nullptr;
+  return ctx_init(device, &c);
+}
+
+int hdfs_crc32c_device_info(int device, char *arch, size_t arch_len, int *num_cu) {
+  DevCtx *c = nullptr;
+  int rc = ctx_init(device, &c);
+  if (rc) return rc;
+  if (arch && arch_len) std::snprintf(arch, arch_len, "%s", c->arch);
+  if (num_cu) *num_cu = c->num_cu;
+  return HDFS_CRC32C_OK;
+}
+
+uint32_t _hdfs_crc32c(uint32_t crc, const void *buf, unsigned len) {
+  uint32_t out = 0;
+  if (len == 0) return crc;
+  if (stream_crc_any(crc, buf, len, &out)) die("_hdfs_crc32c");
+  return out;
+}
+
+uint32_t _hdfs_sse42_crc32c(uint32_t crc, const void *buf, unsigned len) {
+  uint32_t out = 0;
+  if (len == 0) return crc;
+  if (stream_crc_any(crc, buf, len, &out)) die("_hdfs_sse42_crc32c");
+  return out;
+}
+
+uint32_t _hdfs_sw_crc32c(uint32_t crc, const void *buf, unsigned len) {
+  uint32_t out = 0;
+  if (len == 0) return crc;
+  if (stream_crc_any(crc, buf, len, &out)) die("_hdfs_sw_crc32c");
+  return out;
+}
+
+int hdfs_crc32c_stream_dev(uint32_t crc, const void *dbuf, uint64_t len, uint32_t *out) {
+  if (!out) return fail(HDFS_CRC32C_EINVAL, "null out");
+  if (len && !dbuf) return fail(HDFS_CRC32C_EINVAL, "null buffer");
+  return stream_crc_any(crc, dbuf, len, out);
+}
+
+int hdfs_crc32c_plan_create(hdfs_crc32c_plan **plan, int mode, const hdfs_crc32c_segment *segs,
+                            size_t nseg) {
+  if (!plan) return fail(HDFS_CRC32C_EINVAL, "null plan pointer");
+  *plan = nullptr;
+  if (mode != HDFS_CRC32C_MODE_COMPUTE && mode != HDFS_CRC32C_MODE_VERIFY)
+    return fail(HDFS_CRC32C_EINVAL, "bad mode %d", mode);
+  if (nseg && !segs) return fail(HDFS_CRC32C_EINVAL, "null segment table");
+  if (nseg > 0xFFFFFFF0u) return fail(HDFS_CRC32C_EINVAL, "too many segments");
+  DevCtx *c = nullptr;
+  int rc = ctx_init(-1, &c);
+  if (rc) return rc;
+  DeviceGuard g(c->dev);
+  std::vector<SegDev> host(nseg ? nseg : 1);
+  uint64_t rounds = 0, gtiles = 0, main_bytes = 0, gen_bytes = 0, nch = 0;
+  for (size_t i = 0; i < nseg; i++) {
+    rc = fill_seg(segs[i], mode, host[i], i);
+    if (rc) return rc;
+    if (!device_accessible(segs[i].data) || !device_accessible(segs[i].crcs) ||
+        !device_accessible(segs[i].bitmap))
+      return fail(HDFS_CRC32C_EINVAL, "segment %zu: pointer is not device-accessible memory", i);
+    classify(host[i], rounds, gtiles);
+    const uint64_t mb = std::min<uint64_t>(segs[i].len, uint64_t(host[i].main_tiles) * kTileChunks *
+                                                            segs[i].chunk_size);
+    main_bytes += mb;
+    gen_bytes += segs[i].len - mb;
+    nch += host[i].nchunks;
+  }
+  auto *p = new hdfs_crc32c_plan;
+  p->dev = c->dev;
+  p->mode = mode;
+  p->nseg = static_cast<uint32_t>(nseg);
+  p->rounds = rounds;
+  p->gtiles = gtiles;
+  p->main_bytes = main_bytes;
+  p->gen_bytes = gen_bytes;
+  p->nchunks = nch;
+  hipError_t e = hipMalloc(&p->d_segs, sizeof(SegDev) * host.size());
+  if (e == hipSuccess) e = hipMemcpy(p->d_segs, host.data(), sizeof(SegDev) * host.size(), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMalloc(&p->d_first_bad, sizeof(uint32_t) * host.size());
+  if (e == hipSuccess) e = hipMalloc(&p->d_mism, sizeof(unsigned long long));
+  if (e != hipSuccess) {
+    hdfs_crc32c_plan_destroy(p);
+    return fail(HDFS_CRC32C_ENOMEM, "plan allocation: %s", hipGetErrorString(e));
+  }
+  *plan = p;
+  return HDFS_CRC32C_OK;
+}
+
+int hdfs_crc32c_plan_execute(hdfs_crc32c_plan *p, void *stream) {
+  if (!p) return fail(HDFS_CRC32C_EINVAL, "null plan");
+  DevCtx &c = g_ctx[p->dev];
+  DeviceGuard g(p->dev);
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : c.stream;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (p->timing && p->rounds) {
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    p->events.emplace_back(e0, e1);
+  }
+  return launch_all(c, p->mode, p->d_segs, p->nseg, p->rounds, p->gtiles, p->d_first_bad, p->d_mism,
+                    st, e0, e1);
+}
+
+int hdfs_crc32c_plan_results(hdfs_crc32c_plan *p, void *stream, uint32_t *first_bad, size_t nseg,
+                             uint64_t *mismatches) {
+  if (!p) return fail(HDFS_CRC32C_EINVAL, "null plan");
+  if (p->mode != HDFS_CRC32C_MODE_VERIFY) return fail(HDFS_CRC32C_EINVAL, "not a verify plan");
+  DevCtx &c = g_ctx[p->dev];
+  DeviceGuard g(p->dev);
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : c.stream;
+  HIPCHK(hipStreamSynchronize(st));
+  if (first_bad && nseg) {
+    const size_t n = nseg < p->nseg ? nseg : p->nseg;
+    HIPCHK(hipMemcpy(first_bad, p->d_first_bad, n * 4, hipMemcpyDeviceToHost));
+  }
+  if (mismatches) {
+    unsigned long long m = 0;
+    HIPCHK(hipMemcpy(&m, p->d_mism, 8, hipMemcpyDeviceToHost));
+    *mismatches = m;
+  }
+  return HDFS_CRC32C_OK;
+}
+
+int hdfs_crc32c_plan_set_timing(hdfs_crc32c_plan *p, int on) {
+  if (!p) return fail(HDFS_CRC32C_EINVAL, "null plan");
+  p->timing = on != 0;
+  return HDFS_CRC32C_OK;
+}
+
+int hdfs_crc32c_plan_kernel_ms(hdfs_crc32c_plan *p, double *total_ms, int *launches) {
+  if (!p) return fail(HDFS_CRC32C_EINVAL, "null plan");
+  DeviceGuard g(p->dev);
+  double tot = 0;
+  int n = 0;
+  for (auto &ev : p->events) {
+    HIPCHK(hipEventSynchronize(ev.second));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, ev.first, ev.second));
+    tot += ms;
+    n++;
+    (void)hipEventDestroy(ev.first);
+    (void)hipEventDestroy(ev.second);
+  }
+  p->events.clear();
+  if (total_ms) *total_ms = tot;
+  if (launches) *launches = n;
+  return HDFS_CRC32C_OK;
+}
+
+int hdfs_crc32c_plan_stats(const hdfs_crc32c_plan *p, uint64_t *main_bytes, uint64_t *generic_bytes,
+                           uint64_t *nchunks) {
+  if (!p) return fail(HDFS_CRC32C_EINVAL, "null plan");
+  if (main_bytes) *main_bytes = p->main_bytes;
+  if (generic_bytes) *generic_bytes = p->gen_bytes;
+  if (nchunks) *nchunks = p->nchunks;
+  return HDFS_CRC32C_OK;
+}
+
+void hdfs_crc32c_plan_destroy(hdfs_crc32c_plan *p) {
+  if (!p) return;
+  DeviceGuard g(p->dev);
+  for (auto &ev : p->events) {
+    (void)hipEventDestroy(ev.first);
+    (void)hipEventDestroy(ev.second);
+  }
+  if (p->d_segs) (void)hipFree(p->d_segs);
+  if (p->d_first_bad) (void)hipFree(p->d_first_bad);
+  if (p->d_mism) (void)hipFree(p->d_mism);
+  delete p;
+}
+
+int hdfs_crc32c_plan_time(hdfs_crc32c_plan *p, void *stream, int iters, double *ms_per_iter) {
+  if (!p || iters <= 0) return fail(HDFS_CRC32C_EINVAL, "bad plan/iters");
+  DevCtx &c = g_ctx[p->dev];
+  DeviceGuard g(p->dev);
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : c.stream;
+  hipEvent_t a, b;
+  HIPCHK(hipEventCreate(&a));
+  HIPCHK(hipEventCreate(&b));
+  HIPCHK(hipEventRecord(a, st));
+  for (int i = 0; i < iters; i++) {
+    int rc = hdfs_crc32c_plan_execute(p, st);
+    if (rc) return rc;
+  }
+  HIPCHK(hipEventRecord(b, st));
+  HIPCHK(hipEventSynchronize(b));
+  float ms = 0;
+  HIPCHK(hipEventElapsedTime(&ms, a, b));
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  if (ms_per_iter) *ms_per_iter = ms / iters;
+  return HDFS_CRC32C_OK;
+}
+
+int hdfs_crc32c_verify_crcdata(const void *crcdata, int32_t chunksize, int32_t crcdlen, int32_t dlen,
+                               int ctype, int32_t *first_bad) {
+  if (first_bad) *first_bad = -1;
+  if (ctype == HDFS_CRC32C_CSUM_CRC32)
+    return fail(HDFS_CRC32C_ERR_DATANODE_UNSUPPORTED_CHECKSUM, "CRC32 (zlib) not implemented yet");
+  if (ctype != HDFS_CRC32C_CSUM_CRC32C) return fail(HDFS_CRC32C_EINVAL, "bad checksum type %d", ctype);
+  if (chunksize <= 0 || dlen < 0 || crcdlen < 0)
+    return fail(HDFS_CRC32C_ERR_DATANODE_PACKET_SIZE, "bad packet sizes");
+  const int64_t nch = (int64_t(dlen) + chunksize - 1) / chunksize;
+  if (int64_t(crcdlen) != nch * 4)
+    return fail(HDFS_CRC32C_ERR_DATANODE_CRC_LEN, "crcdlen %d != %lld", crcdlen, (long long)(nch * 4));
+  if (dlen == 0) return HDFS_CRC32C_OK;
+  if (!crcdata) return fail(HDFS_CRC32C_EINVAL, "null packet region");
+  DevCtx *c = nullptr;
+  int rc = ctx_init(-1, &c);
+  if (rc) return rc;
+  DeviceGuard g(c->dev);
+  std::lock_guard<std::mutex> lk(c->mu);
+  const size_t off_crc = (size_t(dlen) + 255) & ~size_t(255);
+  const size_t off_bm = off_crc + ((size_t(crcdlen) + 255) & ~size_t(255));
+  const size_t bm_len = size_t((nch + 7) / 8);
+  if (off_bm + bm_len > kStageCap) return fail(HDFS_CRC32C_EINVAL, "packet larger than staging");
+  const uint8_t *region = static_cast<const uint8_t *>(crcdata);
+  std::memcpy(c->h_stage, region + crcdlen, size_t(dlen));  // data (16-B aligned on device)
+  std::memcpy(c->h_stage + off_crc, region, size_t(crcdlen));
+  HIPCHK(hipMemcpyAsync(c->d_stage, c->h_stage, off_bm, hipMemcpyHostToDevice, c->stream));
+  hdfs_crc32c_segment in = {c->d_stage, uint64_t(dlen), uint32_t(chunksize), HDFS_CRC32C_SEG_BE, 0, 0,
+                            c->d_stage + off_crc, c->d_stage + off_bm};
+  SegDev s;
+  rc = fill_seg(in, HDFS_CRC32C_MODE_VERIFY, s, 0);
+  if (rc) return rc;
+  uint64_t rounds = 0, gtiles = 0;
+  classify(s, rounds, gtiles);
+  HIPCHK(hipMemcpyAsync(c->d_seg, &s, sizeof(s), hipMemcpyHostToDevice, c->stream));
+  uint32_t *d_fb = c->d_small + 1;
+  auto *d_m = reinterpret_cast<unsigned long long *>(c->d_small + 2);
+  rc = launch_all(*c, kModeVerify, c->d_seg, 1, rounds, gtiles, d_fb, d_m, c->stream);
+  if (rc) return rc;
+  uint32_t fb = 0;
+  HIPCHK(hipMemcpyAsync(&fb, d_fb, 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (fb != 0xFFFFFFFFu) {
+    if (first_bad) *first_bad = int32_t(fb);
+    return fail(HDFS_CRC32C_ERR_DATANODE_BAD_CHECKSUM, "chunk %u: bad checksum", fb);
+  }
+  return HDFS_CRC32C_OK;
+}
+
+int hdfs_crc32c_compose_crcs(const void *const *iov_base, const size_t *iov_len, int iovcnt, size_t total,
+                             uint32_t chunk, void *crc_be_out) {
+  if (chunk == 0) return fail(HDFS_CRC32C_EINVAL, "chunk 0");
+  if (total == 0) return HDFS_CRC32C_OK;
+  if (!iov_base || !iov_len || iovcnt <= 0 || !crc_be_out) return fail(HDFS_CRC32C_EINVAL, "bad iovecs");
+  const size_t nch = (total + chunk - 1) / chunk;
+  const size_t off_crc = (total + 255) & ~size_t(255);
+  DevCtx *c = nullptr;
+  int rc = ctx_init(-1, &c);
+  if (rc) return rc;
+  if (off_crc + nch * 4 > kStageCap) return fail(HDFS_CRC32C_EINVAL, "packet larger than staging");
+  DeviceGuard g(c->dev);
+  std::lock_guard<std::mutex> lk(c->mu);
+  size_t have = 0;
+  for (int k = 0; k < iovcnt && have < total; k++) {
+    const size_t n = iov_len[k] < total - have ? iov_len[k] : total - have;
+    if (n && !iov_base[k]) return fail(HDFS_CRC32C_EINVAL, "null iovec %d", k);
+    std::memcpy(c->h_stage + have, iov_base[k], n);
+    have += n;
+  }
+  if (have != total) return fail(HDFS_CRC32C_EINVAL, "iovecs hold %zu of %zu bytes", have, total);
+  HIPCHK(hipMemcpyAsync(c->d_stage, c->h_stage, total, hipMemcpyHostToDevice, c->stream));
+  hdfs_crc32c_segment in = {c->d_stage, total, chunk, HDFS_CRC32C_SEG_BE, 0, 0, c->d_stage + off_crc, nullptr};
+  SegDev s;
+  rc = fill_seg(in, HDFS_CRC32C_MODE_COMPUTE, s, 0);
+  if (rc) return rc;
+  uint64_t rounds = 0, gtiles = 0;
+  classify(s, rounds, gtiles);
+  HIPCHK(hipMemcpyAsync(c->d_seg, &s, sizeof(s), hipMemcpyHostToDevice, c->stream));
+  rc = launch_all(*c, kModeCompute, c->d_seg, 1, rounds, gtiles, nullptr, nullptr, c->stream);
+  if (rc) return rc;
+  HIPCHK(hipMemcpyAsync(crc_be_out, c->d_stage + off_crc, nch * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return HDFS_CRC32C_OK;
+}
+
+int hdfs_crc32c_dev_alloc(void **dptr, uint64_t bytes) {
+  DevCtx *c = nullptr;
+  int rc = ctx_init(-1, &c);
+  if (rc) return rc;
+  DeviceGuard g(c->dev);
+  hipError_t e = hipMalloc(dptr, bytes ? bytes : 1);
+  if (e != hipSuccess) return fail(HDFS_CRC32C_ENOMEM, "hipMalloc(%llu): %s", (unsigned long long)bytes,
+                                   hipGetErrorString(e));
+  return HDFS_CRC32C_OK;
+}
+
+int hdfs_crc32c_dev_free(void *dptr) {
+  HIPCHK(hipFree(dptr));
+  return HDFS_CRC32C_OK;
+}
+
+int hdfs_crc32c_memcpy(void *dst, const void *src, uint64_t bytes, int kind) {
+  hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice : kind == 1 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
+  HIPCHK(hipMemcpy(dst, src, bytes, k));
+  return HDFS_CRC32C_OK;
+}
+
+int hdfs_crc32c_memset(void *dptr, int value, uint64_t bytes) {
+  HIPCHK(hipMemset(dptr, value, bytes));
+  return HDFS_CRC32C_OK;
+}
+
+int hdfs_crc32c_stream_create(void **stream) {
+  DevCtx *c = nullptr;
+  int rc = ctx_init(-1, &c);
+  if (rc) return rc;
+  hipStream_t s;
+  HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  *stream = s;
+  return HDFS_CRC32C_OK;
+}
+
+int hdfs_crc32c_stream_destroy(void *stream) {
+  HIPCHK(hipStreamDestroy(static_cast<hipStream_t>(stream)));
+  return HDFS_CRC32C_OK;
+}
+
+int hdfs_crc32c_stream_sync(void *stream) {
+  HIPCHK(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+  return HDFS_CRC32C_OK;
+}
+
+int hdfs_crc32c_fill_splitmix64(void *dptr, uint64_t nwords, uint64_t seed, uint64_t g0, void *stream) {
+  HIPCHK(launch_fill(static_cast<uint64_t *>(dptr), nwords, seed, g0, static_cast<hipStream_t>(stream)));
+  return HDFS_CRC32C_OK;
+}
+
+int hdfs_crc32c_corrupt(void *dptr, uint64_t len, uint32_t chunk, uint64_t chunk0, uint64_t modulus,
+                        uint64_t bitmul, void *stream) {
+  if (!chunk || !modulus) return fail(HDFS_CRC32C_EINVAL, "chunk/modulus 0");
+  if (!len) return HDFS_CRC32C_OK;
+  HIPCHK(launch_corrupt(static_cast<uint8_t *>(dptr), len, chunk, chunk0, modulus, bitmul,
+                        static_cast<hipStream_t>(stream)));
+  return HDFS_CRC32C_OK;
+}
+
+}  // extern "C"

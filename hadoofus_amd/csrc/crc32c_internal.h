@@ -1,0 +1,58 @@
+// Internal structures shared by the gfx950 kernels and the host engine.
+// Not part of the public C ABI (include/hadoofus_crc32c.h).
+#pragma once
+#include <cstdint>
+
+namespace hdfs_crc32c {
+
+// Segment flags (also mirrored as HDFS_CRC32C_SEG_* in the public header).
+enum : uint32_t {
+  kSegBigEndian = 1u,  // crcs[] are in wire byte order (src/util.h:68-92)
+  kSegRaw = 2u,        // write the raw register (init 0, no final inversion)
+};
+
+enum Mode : int { kModeCompute = 0, kModeVerify = 1 };
+
+// One entry of the device-resident segment table.  A segment is one chunk
+// stream with one bytesPerChecksum (src/datanode.c:2186); chunk i covers
+// bytes [i*cs, min((i+1)*cs, len)).  Chunks are grouped in TILES of 8
+// (tile t = chunks 8t..8t+7), which is also the bitmap byte they own.
+struct SegDev {
+  const uint8_t *data;   // device pointer
+  uint64_t len;          // bytes
+  uint32_t *crcs;        // compute: out; verify: expected in
+  uint8_t *bitmap;       // verify: out, one bit per chunk, byte t per tile t
+  uint64_t round_start;  // global index of this segment's first main-path round
+  uint64_t gtile_start;  // global index of this segment's first generic tile
+  uint32_t chunk_size;   // bytes per checksum
+  uint32_t flags;        // kSeg*
+  uint32_t nchunks;      // ceil(len / chunk_size)
+  uint32_t main_tiles;   // tiles [0, main_tiles) run on the tiled kernel
+  uint32_t gen_tiles;    // tiles [main_tiles, main_tiles+gen_tiles) run generic
+  uint32_t reg_init;     // register value each chunk starts from (~crc_init, or 0 if raw)
+};
+
+// LDS image of the tiled kernel (bytes).
+//  [0, 128 KiB)          slicing-by-4 tables, each replicated 32x so that
+//                        lane l always reads bank l (conflict-free)
+//  [128 KiB, +28 KiB)    Z_{64k} byte tables, k = 1..7 (lane combine; k = 7
+//                        doubles as the 448-byte jump between rounds)
+constexpr uint32_t kLdsSliceBytes = 131072;
+constexpr uint32_t kLdsZposBytes = 7 * 4096;
+constexpr uint32_t kLdsBytes = kLdsSliceBytes + kLdsZposBytes;  // 159744
+constexpr uint32_t kLdsWords = kLdsBytes / 4;
+
+// Global table blob consumed by the kernels (u32 words).
+//  [0, 1024)       t0..t3 (t_k at k*256)
+//  [1024, 8192)    Z_{64k}[m][e] for k = 1..7 (k-1)*1024 + m*256 + e
+constexpr uint32_t kTabSliceWords = 1024;
+constexpr uint32_t kTabZposWords = 7 * 1024;
+constexpr uint32_t kTabMainWords = kTabSliceWords + kTabZposWords;
+// Power-of-two zero operators for the stream combine: Z_{2^b}, b < 48.
+constexpr uint32_t kPow2Levels = 48;
+constexpr uint32_t kTabPow2Words = kPow2Levels * 1024;
+
+constexpr uint32_t kRoundBytes = 512;  // sub-chunk handled by 8 lanes per round
+constexpr uint32_t kTileChunks = 8;
+
+}  // namespace hdfs_crc32c

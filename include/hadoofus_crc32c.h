@@ -1,0 +1,143 @@
+/*
+ * hadoofus_crc32c.h -- C ABI of the MI355X-native CRC32C engine
+ * (libhadoofus_crc32c.so, built from hadoofus_amd/csrc/).
+ *
+ * Two layers:
+ *
+ * 1. DROP-IN: the three symbols of the reference's private header
+ *    src/crc32c.h:13-24 (also declared, with the reference's include guard,
+ *    in include/crc32c.h so src/datanode.c:16 compiles unchanged).  Same
+ *    semantics: pre/post inversion inside, crc=0 starts, chaining by passing
+ *    the previous return value, len==0 returns crc, any alignment, total
+ *    function.  All three run on the GPU engine; with no usable GPU they
+ *    abort() with a message (there is no CPU fallback).
+ *
+ * 2. BATCH (additive): per-chunk compute / verify over a table of chunk
+ *    streams in device memory, the shape of the two datanode loops
+ *    (src/datanode.c:2814-2860 write compute, src/datanode.c:2931-2963 read
+ *    verify), plus host-memory mirrors of those two loops.
+ *
+ * No HIP or torch types appear in the signatures: streams are passed as
+ * `void *` (a hipStream_t, NULL = the engine's own stream).
+ */
+#ifndef HADOOFUS_CRC32C_H
+#define HADOOFUS_CRC32C_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- 1. drop-in (replaces src/crc32c.h:13, :17, :24) -------------------- */
+uint32_t _hdfs_crc32c(uint32_t crc, const void *buf, unsigned len);
+uint32_t _hdfs_sse42_crc32c(uint32_t crc, const void *buf, unsigned len);
+uint32_t _hdfs_sw_crc32c(uint32_t crc, const void *buf, unsigned len);
+
+/* ---- status codes ------------------------------------------------------- */
+#define HDFS_CRC32C_OK 0
+#define HDFS_CRC32C_EINVAL (-1)   /* bad argument / descriptor */
+#define HDFS_CRC32C_ENODEV (-2)   /* no usable gfx950 device / HIP runtime */
+#define HDFS_CRC32C_ENOMEM (-3)   /* device or pinned allocation failed */
+#define HDFS_CRC32C_EHIP (-4)     /* HIP runtime error (see last_error) */
+/* Datanode-level results reuse the reference's enum hdfs_error_numeric
+ * values (include/objects.h:21-113; checked by compiling that header). */
+#define HDFS_CRC32C_ERR_DATANODE_UNSUPPORTED_CHECKSUM 8
+#define HDFS_CRC32C_ERR_DATANODE_PACKET_SIZE 25
+#define HDFS_CRC32C_ERR_DATANODE_CRC_LEN 26
+#define HDFS_CRC32C_ERR_DATANODE_BAD_CHECKSUM 29
+
+/* enum hdfs_checksum_type (include/objects.h:169-175) */
+#define HDFS_CRC32C_CSUM_NULL 0
+#define HDFS_CRC32C_CSUM_CRC32 1
+#define HDFS_CRC32C_CSUM_CRC32C 2
+
+const char *hdfs_crc32c_last_error(void);
+/* Initialise the engine on `device` (-1: the calling thread's current HIP
+ * device).  Called implicitly by every entry point. */
+int hdfs_crc32c_init(int device);
+/* gfx arch string of the engine's device, e.g. "gfx950". */
+int hdfs_crc32c_device_info(int device, char *arch, size_t arch_len, int *num_cu);
+
+/* ---- 2. batch API -------------------------------------------------------- */
+#define HDFS_CRC32C_MODE_COMPUTE 0
+#define HDFS_CRC32C_MODE_VERIFY 1
+
+#define HDFS_CRC32C_SEG_BE 1u   /* crcs[] in wire (big-endian) order, src/util.h:68-92 */
+#define HDFS_CRC32C_SEG_RAW 2u  /* compute: raw register (init 0, no final inversion) */
+
+/* One chunk stream: chunk i = bytes [i*chunk_size, min((i+1)*chunk_size, len))
+ * of `data`; the last chunk may be partial (src/datanode.c:2946). */
+typedef struct hdfs_crc32c_segment {
+	const void *data;      /* device pointer */
+	uint64_t len;          /* bytes */
+	uint32_t chunk_size;   /* bytesPerChecksum, > 0 */
+	uint32_t flags;        /* HDFS_CRC32C_SEG_* */
+	uint32_t crc_init;     /* value each chunk's CRC starts from (reference: 0) */
+	uint32_t reserved;
+	void *crcs;            /* device u32[nchunks]: compute out / verify expected in */
+	uint8_t *bitmap;       /* verify: device out, ceil(nchunks/8) bytes, bit i = chunk i bad */
+} hdfs_crc32c_segment;
+
+typedef struct hdfs_crc32c_plan hdfs_crc32c_plan;
+
+/* Validate the segment table and upload it to the device (done once). */
+int hdfs_crc32c_plan_create(hdfs_crc32c_plan **plan, int mode,
+    const hdfs_crc32c_segment *segs, size_t nseg);
+/* Enqueue one pass over every chunk of every segment on `stream`
+ * (graph-capturable: no allocation or synchronisation inside). */
+int hdfs_crc32c_plan_execute(hdfs_crc32c_plan *plan, void *stream);
+/* Verify plans: wait for the stream and return the first bad chunk of each
+ * segment (UINT32_MAX if none) and the total number of bad chunks. */
+int hdfs_crc32c_plan_results(hdfs_crc32c_plan *plan, void *stream,
+    uint32_t *first_bad, size_t nseg, uint64_t *mismatches);
+/* Optional device-side timing of the tiled kernel (HIP events recorded on
+ * the execute stream around each launch). */
+int hdfs_crc32c_plan_set_timing(hdfs_crc32c_plan *plan, int on);
+int hdfs_crc32c_plan_kernel_ms(hdfs_crc32c_plan *plan, double *total_ms, int *launches);
+/* Bytes per pass the tiled and generic kernels cover (for roofline maths). */
+int hdfs_crc32c_plan_stats(const hdfs_crc32c_plan *plan, uint64_t *main_bytes,
+    uint64_t *generic_bytes, uint64_t *nchunks);
+void hdfs_crc32c_plan_destroy(hdfs_crc32c_plan *plan);
+
+/* CRC of one arbitrary device buffer continuing from `crc` (the
+ * _hdfs_crc32c contract on device memory); synchronous. */
+int hdfs_crc32c_stream_dev(uint32_t crc, const void *dbuf, uint64_t len, uint32_t *out);
+
+/* ---- datanode mirrors on host memory (synchronous) ---------------------- */
+/* _verify_crcdata (src/datanode.c:2931-2963) plus the CRC-length framing
+ * check of _process_recv_packet (src/datanode.c:2441-2442) on a packet region
+ * [crcdlen bytes of BE CRCs | dlen bytes of data].  Returns 0, or
+ * HDFS_CRC32C_ERR_DATANODE_{CRC_LEN,BAD_CHECKSUM,UNSUPPORTED_CHECKSUM}, or a
+ * negative HDFS_CRC32C_E* status; *first_bad = first mismatching chunk or -1. */
+int hdfs_crc32c_verify_crcdata(const void *crcdata, int32_t chunksize, int32_t crcdlen,
+    int32_t dlen, int ctype, int32_t *first_bad);
+/* CRC loop of _compose_data_packet_header (src/datanode.c:2814-2860):
+ * ceil(total/chunk) big-endian CRCs of the concatenation of iovcnt
+ * fragments (CRCs chain across fragment boundaries). */
+int hdfs_crc32c_compose_crcs(const void *const *iov_base, const size_t *iov_len, int iovcnt,
+    size_t total, uint32_t chunk, void *crc_be_out);
+
+/* ---- device memory + synthetic data helpers (bench / tests) ------------- */
+int hdfs_crc32c_dev_alloc(void **dptr, uint64_t bytes);
+int hdfs_crc32c_dev_free(void *dptr);
+int hdfs_crc32c_memcpy(void *dst, const void *src, uint64_t bytes, int kind /* 0 h2d, 1 d2h, 2 d2d */);
+int hdfs_crc32c_memset(void *dptr, int value, uint64_t bytes);
+int hdfs_crc32c_stream_create(void **stream);
+int hdfs_crc32c_stream_destroy(void *stream);
+int hdfs_crc32c_stream_sync(void *stream);
+/* w[k] = splitmix64(seed, g0 + k), k < nwords (SURVEY.md 8c data). */
+int hdfs_crc32c_fill_splitmix64(void *dptr, uint64_t nwords, uint64_t seed, uint64_t g0, void *stream);
+/* Flip bit (i*bitmul) mod (8*chunk_len) of every chunk whose global index
+ * i = chunk0 + local satisfies i % modulus == 0. */
+int hdfs_crc32c_corrupt(void *dptr, uint64_t len, uint32_t chunk, uint64_t chunk0,
+    uint64_t modulus, uint64_t bitmul, void *stream);
+/* Elapsed device time of `iters` back-to-back plan executions on `stream`
+ * measured with HIP events (ms per execution). */
+int hdfs_crc32c_plan_time(hdfs_crc32c_plan *plan, void *stream, int iters, double *ms_per_iter);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HADOOFUS_CRC32C_H */

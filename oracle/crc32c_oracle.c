@@ -1,0 +1,478 @@
+/*
+ * crc32c_oracle.c -- CPU ORACLE for the hadoofus CRC32C hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in hadoofus_amd/ links, loads or calls
+ * this file; only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+ * leg do, and only as the checker (or the timed CPU baseline), never as the
+ * thing that is measured or shipped.
+ *
+ * This is our own restatement of the reference's algorithms (nothing copied);
+ * every function cites the reference file:line it follows
+ * (paths relative to alexsmith1612/hadoofus, mounted at /root/reference):
+ *
+ *   oracle_crc32c_sw      <- src/crc32c_sw.c:63 (poly), :72-94 (tables),
+ *                            :97-127 (slicing-by-8 little-endian loop),
+ *                            :207-213 (_hdfs_sw_crc32c entry)
+ *   oracle_crc32c_hw      <- src/crc32c_sse42.c:80-81 (LONG/SHORT),
+ *                            :99-200 (GF(2) zeros operator + shift tables),
+ *                            :214-381 (3-way interleaved crc32q loop)
+ *   oracle_verify_crcdata <- src/datanode.c:2931-2963 (_verify_crcdata) and
+ *                            the framing check of src/datanode.c:2438-2446
+ *   oracle_compose_crcs   <- src/datanode.c:2814-2860 (write-path CRC loop,
+ *                            chained across iovec fragments)
+ *   oracle_zeros/combine  <- src/crc32c_sse42.c:99-200 generalised to any n
+ *
+ * Parity is PINNED: tests/test_oracle.py checks every function here against
+ * the reference's own KATs (tests/t_unit.c:146-217) and against golden
+ * vectors produced by the reference compiled unchanged from /root/reference
+ * (oracle/_ref, recipe in oracle/Makefile, generator oracle/gen_golden.py).
+ */
+#include <stddef.h>
+#include <stdint.h>
+#include <string.h>
+#include <pthread.h>
+#include <time.h>
+
+#define ORACLE_POLY 0x82f63b78u /* src/crc32c_sw.c:63 */
+
+/* ------------------------------------------------------------------ */
+/* Software slicing-by-8 (src/crc32c_sw.c:72-127)                      */
+/* ------------------------------------------------------------------ */
+static uint32_t sw_tab[8][256];
+static int sw_ready;
+
+static void sw_init(void)
+{
+	for (uint32_t n = 0; n < 256; n++) {
+		uint32_t c = n;
+		for (int k = 0; k < 8; k++)
+			c = (c >> 1) ^ (ORACLE_POLY & (0u - (c & 1u)));
+		sw_tab[0][n] = c;
+	}
+	for (uint32_t n = 0; n < 256; n++) {
+		uint32_t c = sw_tab[0][n];
+		for (int t = 1; t < 8; t++) {
+			c = sw_tab[0][c & 0xff] ^ (c >> 8);
+			sw_tab[t][n] = c;
+		}
+	}
+	sw_ready = 1;
+}
+
+__attribute__((constructor)) static void oracle_ctor(void) { sw_init(); }
+
+uint32_t oracle_crc32c_sw(uint32_t crc, const void *buf, size_t len)
+{
+	const uint8_t *p = buf;
+	uint32_t c = ~crc;
+
+	while (len && ((uintptr_t)p & 7)) {
+		c = sw_tab[0][(c ^ *p++) & 0xff] ^ (c >> 8);
+		len--;
+	}
+	while (len >= 8) {
+		uint64_t w;
+		memcpy(&w, p, 8);
+		w ^= c;
+		c = sw_tab[7][w & 0xff] ^ sw_tab[6][(w >> 8) & 0xff] ^
+		    sw_tab[5][(w >> 16) & 0xff] ^ sw_tab[4][(w >> 24) & 0xff] ^
+		    sw_tab[3][(w >> 32) & 0xff] ^ sw_tab[2][(w >> 40) & 0xff] ^
+		    sw_tab[1][(w >> 48) & 0xff] ^ sw_tab[0][w >> 56];
+		p += 8;
+		len -= 8;
+	}
+	while (len--)
+		c = sw_tab[0][(c ^ *p++) & 0xff] ^ (c >> 8);
+	return ~c;
+}
+
+/* Bitwise definition; the slowest and most obviously-correct form. */
+uint32_t oracle_crc32c_bitwise(uint32_t crc, const void *buf, size_t len)
+{
+	const uint8_t *p = buf;
+	uint32_t c = ~crc;
+	while (len--) {
+		c ^= *p++;
+		for (int k = 0; k < 8; k++)
+			c = (c >> 1) ^ (ORACLE_POLY & (0u - (c & 1u)));
+	}
+	return ~c;
+}
+
+/* ------------------------------------------------------------------ */
+/* GF(2) "append n zero bytes" operator (src/crc32c_sse42.c:99-200)   */
+/* Works on the raw (pre-inverted) register.                           */
+/* ------------------------------------------------------------------ */
+static uint32_t gf2_times(const uint32_t *mat, uint32_t vec)
+{
+	uint32_t sum = 0;
+	while (vec) {
+		if (vec & 1)
+			sum ^= *mat;
+		vec >>= 1;
+		mat++;
+	}
+	return sum;
+}
+
+static void gf2_square(uint32_t *sq, const uint32_t *mat)
+{
+	for (int n = 0; n < 32; n++)
+		sq[n] = gf2_times(mat, mat[n]);
+}
+
+/* Operator for n zero BYTES, any n (the reference builds powers of two only;
+ * this is the same squaring ladder applied per set bit of n). */
+void oracle_zeros_op(uint32_t op[32], uint64_t nbytes)
+{
+	uint32_t pow[32], tmp[32], acc[32];
+	/* identity */
+	for (int i = 0; i < 32; i++)
+		acc[i] = 1u << i;
+	/* operator for one zero bit */
+	pow[0] = ORACLE_POLY;
+	for (int i = 1; i < 32; i++)
+		pow[i] = 1u << (i - 1);
+	/* square 3 times: one zero byte */
+	gf2_square(tmp, pow);
+	gf2_square(pow, tmp);
+	gf2_square(tmp, pow);
+	memcpy(pow, tmp, sizeof(pow));
+	while (nbytes) {
+		if (nbytes & 1) {
+			for (int i = 0; i < 32; i++)
+				tmp[i] = gf2_times(pow, acc[i]);
+			memcpy(acc, tmp, sizeof(acc));
+		}
+		nbytes >>= 1;
+		if (nbytes) {
+			gf2_square(tmp, pow);
+			memcpy(pow, tmp, sizeof(pow));
+		}
+	}
+	memcpy(op, acc, sizeof(acc));
+}
+
+uint32_t oracle_zeros_apply(uint32_t reg, uint64_t nbytes)
+{
+	uint32_t op[32];
+	oracle_zeros_op(op, nbytes);
+	return gf2_times(op, reg);
+}
+
+/* c(A||B) from c(A), c(B), |B| -- public (conditioned) CRC values. */
+uint32_t oracle_crc32c_combine(uint32_t crcA, uint32_t crcB, uint64_t lenB)
+{
+	/* raw registers: regA = ~crcA ; CRC(~0, A||B) = Z_lenB(~crcA) ^ raw(B)
+	 * and c(B) = ~(Z_lenB(~0) ^ raw(B)). */
+	uint32_t zA = oracle_zeros_apply(~crcA, lenB);
+	uint32_t zI = oracle_zeros_apply(~0u, lenB);
+	return ~(zA ^ zI ^ ~crcB);
+}
+
+/* Byte tables for an operator: zt[m][e] = op(e << 8m). */
+static void zeros_tables(uint32_t zt[4][256], uint64_t nbytes)
+{
+	uint32_t op[32];
+	oracle_zeros_op(op, nbytes);
+	for (uint32_t e = 0; e < 256; e++)
+		for (int m = 0; m < 4; m++)
+			zt[m][e] = gf2_times(op, e << (8 * m));
+}
+
+static inline uint32_t zshift(uint32_t zt[4][256], uint32_t c)
+{
+	return zt[0][c & 0xff] ^ zt[1][(c >> 8) & 0xff] ^ zt[2][(c >> 16) & 0xff] ^
+	    zt[3][c >> 24];
+}
+
+/* ------------------------------------------------------------------ */
+/* SSE4.2 3-way interleaved restatement (src/crc32c_sse42.c:214-381)   */
+/* ------------------------------------------------------------------ */
+#if defined(__x86_64__)
+#define HW_LONG 128  /* src/crc32c_sse42.c:80 */
+#define HW_SHORT 64  /* src/crc32c_sse42.c:81 */
+static uint32_t hw_long[4][256], hw_2long[4][256], hw_short[4][256], hw_2short[4][256];
+static int hw_ready;
+
+__attribute__((constructor)) static void oracle_hw_ctor(void)
+{
+	zeros_tables(hw_long, HW_LONG);
+	zeros_tables(hw_2long, 2 * HW_LONG);
+	zeros_tables(hw_short, HW_SHORT);
+	zeros_tables(hw_2short, 2 * HW_SHORT);
+	hw_ready = 1;
+}
+
+__attribute__((target("sse4.2")))
+static inline uint64_t c8(uint64_t c, uint8_t b) { return __builtin_ia32_crc32qi((uint32_t)c, b); }
+__attribute__((target("sse4.2")))
+static inline uint64_t c64(uint64_t c, uint64_t w) { return __builtin_ia32_crc32di(c, w); }
+
+__attribute__((target("sse4.2")))
+uint32_t oracle_crc32c_hw(uint32_t crc, const void *buf, size_t len)
+{
+	const uint8_t *p = buf;
+	uint64_t s0 = (uint32_t)~crc, s1, s2, acc;
+
+	while (len && ((uintptr_t)p & 7)) {
+		s0 = c8(s0, *p++);
+		len--;
+	}
+	/* three streams of LONG bytes, merged with the zeros operator */
+	acc = 0;
+	while (len >= 3 * HW_LONG) {
+		const uint8_t *end = p + HW_LONG;
+		s1 = 0;
+		s2 = 0;
+		do {
+			uint64_t a, b, c;
+			memcpy(&a, p, 8);
+			memcpy(&b, p + HW_LONG, 8);
+			memcpy(&c, p + 2 * HW_LONG, 8);
+			s0 = c64(s0, a);
+			s1 = c64(s1, b);
+			s2 = c64(s2, c);
+			p += 8;
+		} while (p < end);
+		acc = zshift(hw_long, (uint32_t)acc) ^ (uint32_t)s0;
+		s1 = zshift(hw_long, (uint32_t)s1);
+		acc = zshift(hw_2long, (uint32_t)acc) ^ (uint32_t)s1;
+		s0 = s2;
+		p += 2 * HW_LONG;
+		len -= 3 * HW_LONG;
+	}
+	s0 ^= acc;
+	acc = 0;
+	while (len >= 3 * HW_SHORT) {
+		const uint8_t *end = p + HW_SHORT;
+		s1 = 0;
+		s2 = 0;
+		do {
+			uint64_t a, b, c;
+			memcpy(&a, p, 8);
+			memcpy(&b, p + HW_SHORT, 8);
+			memcpy(&c, p + 2 * HW_SHORT, 8);
+			s0 = c64(s0, a);
+			s1 = c64(s1, b);
+			s2 = c64(s2, c);
+			p += 8;
+		} while (p < end);
+		acc = zshift(hw_short, (uint32_t)acc) ^ (uint32_t)s0;
+		s1 = zshift(hw_short, (uint32_t)s1);
+		acc = zshift(hw_2short, (uint32_t)acc) ^ (uint32_t)s1;
+		s0 = s2;
+		p += 2 * HW_SHORT;
+		len -= 3 * HW_SHORT;
+	}
+	s0 ^= acc;
+	while (len >= 8) {
+		uint64_t a;
+		memcpy(&a, p, 8);
+		s0 = c64(s0, a);
+		p += 8;
+		len -= 8;
+	}
+	while (len--)
+		s0 = c8(s0, *p++);
+	return ~(uint32_t)s0;
+}
+
+int oracle_have_hw(void)
+{
+	unsigned a, b, c, d;
+	__asm__("cpuid" : "=a"(a), "=b"(b), "=c"(c), "=d"(d) : "a"(1), "c"(0));
+	return (c >> 20) & 1; /* src/crc32c.c:20-28 */
+}
+#else
+uint32_t oracle_crc32c_hw(uint32_t crc, const void *buf, size_t len)
+{
+	return oracle_crc32c_sw(crc, buf, len);
+}
+int oracle_have_hw(void) { return 0; }
+#endif
+
+/* ------------------------------------------------------------------ */
+/* Datanode call sites                                                 */
+/* ------------------------------------------------------------------ */
+static inline uint32_t be32dec(const uint8_t *p) /* src/util.h:68-80 */
+{
+	return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+
+static inline void be32enc(uint8_t *p, uint32_t v) /* src/util.h:82-92 */
+{
+	p[0] = v >> 24;
+	p[1] = v >> 16;
+	p[2] = v >> 8;
+	p[3] = v;
+}
+
+/* Reference error numbers (include/objects.h:21-113, values checked by
+ * compiling the reference header in this container). */
+#define ORACLE_ERR_CRC_LEN 26
+#define ORACLE_ERR_BAD_CHECKSUM 29
+
+/*
+ * _verify_crcdata (src/datanode.c:2931-2963) on [BE crcs (crcdlen) | data
+ * (dlen)] for CRC32C, preceded by the CRC-length framing check of
+ * _process_recv_packet (src/datanode.c:2441-2442).  Returns 0, or the
+ * reference error number; *first_bad receives the first mismatching chunk
+ * (-1 if none), which is where the reference's loop returns.
+ */
+int oracle_verify_crcdata(const void *crcdata, int32_t chunksize, int32_t crcdlen,
+    int32_t dlen, int32_t *first_bad)
+{
+	const uint8_t *crcs = crcdata;
+	const uint8_t *data = crcs + crcdlen;
+	*first_bad = -1;
+	if (crcdlen != ((dlen + chunksize - 1) / chunksize) * 4)
+		return ORACLE_ERR_CRC_LEN;
+	for (int32_t i = 0; i < (dlen + chunksize - 1) / chunksize; i++) {
+		int32_t clen = dlen - i * chunksize;
+		if (clen > chunksize)
+			clen = chunksize;
+		uint32_t crc = oracle_crc32c_sw(0, data + (size_t)i * chunksize, clen);
+		if (crc != be32dec(crcs + 4 * (size_t)i)) {
+			*first_bad = i;
+			return ORACLE_ERR_BAD_CHECKSUM;
+		}
+	}
+	return 0;
+}
+
+/*
+ * Write-path loop of _compose_data_packet_header (src/datanode.c:2814-2860):
+ * one BE CRC per CHUNK of the packet, chained across the iovec fragments
+ * (iov_base[k], iov_len[k]).  Writes ceil(total/chunk) * 4 bytes.
+ */
+void oracle_compose_crcs(const void *const *iov_base, const size_t *iov_len, int iovcnt,
+    size_t total, uint32_t chunk, void *crc_be_out)
+{
+	uint8_t *out = crc_be_out;
+	size_t nch = (total + chunk - 1) / chunk;
+	int k = 0;
+	size_t off = 0;
+	for (size_t i = 0; i < nch; i++) {
+		uint32_t crc = 0;
+		size_t clen = total - i * chunk;
+		if (clen > chunk)
+			clen = chunk;
+		while (clen > 0 && k < iovcnt) {
+			size_t t = iov_len[k] - off;
+			if (t > clen)
+				t = clen;
+			crc = oracle_crc32c_sw(crc, (const uint8_t *)iov_base[k] + off, t);
+			clen -= t;
+			off += t;
+			if (off == iov_len[k]) {
+				k++;
+				off = 0;
+			}
+		}
+		be32enc(out + 4 * i, crc);
+	}
+}
+
+/* Per-chunk CRCs (LE u32 out) of a buffer; the last chunk may be partial. */
+void oracle_chunk_crcs(const void *data, uint64_t len, uint32_t chunk, uint32_t *out, int use_hw)
+{
+	const uint8_t *p = data;
+	uint64_t nch = (len + chunk - 1) / chunk;
+	for (uint64_t i = 0; i < nch; i++) {
+		uint64_t clen = len - i * chunk;
+		if (clen > chunk)
+			clen = chunk;
+		out[i] = use_hw ? oracle_crc32c_hw(0, p + i * chunk, clen)
+				: oracle_crc32c_sw(0, p + i * chunk, clen);
+	}
+}
+
+/* ------------------------------------------------------------------ */
+/* Synthetic data: LE u64 words w[g] = splitmix64(seed,g) */
+/* ------------------------------------------------------------------ */
+static inline uint64_t splitmix64(uint64_t seed, uint64_t g)
+{
+	uint64_t z = seed + (g + 1) * 0x9E3779B97F4A7C15ull;
+	z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+	z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+	return z ^ (z >> 31);
+}
+
+void oracle_splitmix_fill(uint64_t *out, uint64_t nwords, uint64_t seed, uint64_t g0)
+{
+	for (uint64_t k = 0; k < nwords; k++)
+		out[k] = splitmix64(seed, g0 + k);
+}
+
+/* ------------------------------------------------------------------ */
+/* CPU baseline timing (bench.py cpu_baseline leg): per-chunk CRCs over  */
+/* [data, data+len) split into contiguous chunk ranges, one per thread.  */
+/* fn: 0 = oracle sw, 1 = oracle hw (sse4.2 restatement), 2 = external  */
+/* function pointer (the reference's own _hdfs_sse42_crc32c from _ref).  */
+/* ------------------------------------------------------------------ */
+typedef uint32_t (*crc_fn_t)(uint32_t, const void *, unsigned);
+
+struct bench_arg {
+	const uint8_t *data;
+	uint64_t c0, c1;
+	uint32_t chunk;
+	int fn;
+	crc_fn_t ext;
+	uint32_t *out;
+	uint64_t len;
+};
+
+static void *bench_worker(void *vp)
+{
+	struct bench_arg *a = vp;
+	for (uint64_t i = a->c0; i < a->c1; i++) {
+		uint64_t clen = a->len - i * a->chunk;
+		if (clen > a->chunk)
+			clen = a->chunk;
+		const uint8_t *p = a->data + i * a->chunk;
+		uint32_t c;
+		if (a->fn == 2)
+			c = a->ext(0, p, (unsigned)clen);
+		else if (a->fn == 1)
+			c = oracle_crc32c_hw(0, p, clen);
+		else
+			c = oracle_crc32c_sw(0, p, clen);
+		a->out[i] = c;
+	}
+	return NULL;
+}
+
+/* Returns wall seconds. */
+double oracle_bench_chunks(const void *data, uint64_t len, uint32_t chunk, int nthreads,
+    int fn, void *ext_fn, uint32_t *out)
+{
+	uint64_t nch = (len + chunk - 1) / chunk;
+	pthread_t th[256];
+	struct bench_arg args[256];
+	struct timespec t0, t1;
+	if (nthreads < 1)
+		nthreads = 1;
+	if (nthreads > 256)
+		nthreads = 256;
+	clock_gettime(CLOCK_MONOTONIC, &t0);
+	for (int t = 0; t < nthreads; t++) {
+		args[t].data = data;
+		args[t].c0 = nch * t / nthreads;
+		args[t].c1 = nch * (t + 1) / nthreads;
+		args[t].chunk = chunk;
+		args[t].fn = fn;
+		args[t].ext = (crc_fn_t)ext_fn;
+		args[t].out = out;
+		args[t].len = len;
+		if (nthreads == 1)
+			bench_worker(&args[t]);
+		else
+			pthread_create(&th[t], NULL, bench_worker, &args[t]);
+	}
+	if (nthreads > 1)
+		for (int t = 0; t < nthreads; t++)
+			pthread_join(th[t], NULL);
+	clock_gettime(CLOCK_MONOTONIC, &t1);
+	return (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
+}

@@ -1,0 +1,248 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the committed
+golden fixtures (made by the reference, oracle/gen_golden.py) and against the
+CPU oracle on the same seeded inputs.  Bit-exact everywhere (integer work)."""
+import numpy as np
+import pytest
+
+from oracle import splitmix64_np
+
+pytestmark = pytest.mark.gpu
+
+SWEEP_DATA = splitmix64_np(1024 + 8, seed=7).view(np.uint8)
+
+
+def _dev(engine, host):
+    buf = engine.DeviceBuffer(max(1, host.nbytes))
+    buf.upload(host)
+    return buf
+
+
+def _chunk_plan(engine, dbuf, nbytes, cs, mode, crcs_dev, flags=0, bitmap=None, crc_init=0, offset=0):
+    seg = engine.Segment(data=dbuf.ptr + offset, len=nbytes, chunk_size=cs, flags=flags,
+                         crc_init=crc_init, crcs=crcs_dev.ptr, bitmap=bitmap.ptr if bitmap else None)
+    return engine.Plan(mode, [seg])
+
+
+# --- drop-in symbols (src/crc32c.h) against tests/t_unit.c KATs -------------
+def test_kats_dropin(engine, golden):
+    for k in golden["kats"]:
+        b = bytes.fromhex(k["hex"])
+        for entry in ("_hdfs_crc32c", "_hdfs_sse42_crc32c", "_hdfs_sw_crc32c"):
+            assert engine.crc32c(0, b, entry) == k["crc"], (entry, k["len"], k["source"])
+
+
+def test_chaining_dropin(engine, oracle):
+    rng = np.random.default_rng(3)
+    a = rng.integers(0, 256, 3001, dtype=np.uint8)
+    b = rng.integers(0, 256, 777, dtype=np.uint8)
+    whole = oracle.crc32c(0, np.concatenate([a, b]))
+    assert engine.crc32c(engine.crc32c(0, a), b) == whole
+    assert engine.crc32c(0x12345678, b"") == 0x12345678  # len 0 returns crc
+
+
+def test_edge_sweep_host_and_device(engine, golden):
+    sweep = golden["sweep"]
+    dbuf = _dev(engine, SWEEP_DATA)
+    lens = list(range(0, 600)) + list(range(600, 4097, 37)) + [4095, 4096]
+    for off in range(8):
+        for n in lens:
+            cin = (0x9E3779B9 * (n + 1) + off) & 0xFFFFFFFF
+            if off in (0, 3):  # host-memory drop-in path
+                assert engine.crc32c(0, SWEEP_DATA[off:off + n]) == sweep[0, off, n], (off, n)
+            # device pointer at every alignment, chained crc_in
+            assert engine.stream_crc_dev(cin, dbuf.ptr + off, n) == sweep[1, off, n], (off, n)
+
+
+# --- batch compute against golden per-chunk arrays --------------------------
+@pytest.mark.parametrize("cs", [512, 1024, 2048, 4096])
+@pytest.mark.parametrize("kind", ["full", "ragged"])
+def test_chunk_crcs_golden(engine, golden, cs, kind):
+    host = splitmix64_np(1 << 17, seed=0).view(np.uint8)
+    n = host.nbytes if kind == "full" else host.nbytes - 123
+    want = golden["chunks"][f"{kind}_{cs}"]
+    dbuf = _dev(engine, host[:n])
+    out = engine.DeviceBuffer(want.nbytes)
+    p = _chunk_plan(engine, dbuf, n, cs, engine.MODE_COMPUTE, out)
+    p.execute()
+    got = out.download(dtype=np.uint32)
+    np.testing.assert_array_equal(got, want)
+    # wire order
+    pb = _chunk_plan(engine, dbuf, n, cs, engine.MODE_COMPUTE, out, flags=engine.SEG_BE)
+    pb.execute()
+    np.testing.assert_array_equal(out.download(dtype=">u4").astype(np.uint32), want)
+
+
+@pytest.mark.parametrize("nchunks", [1, 7, 8, 9, 15, 16, 17, 63, 64, 65, 1000, 4097])
+@pytest.mark.parametrize("cs", [512, 1536, 4096])
+def test_tiled_shapes_vs_oracle(engine, oracle, nchunks, cs):
+    rng = np.random.default_rng(nchunks * 31 + cs)
+    host = rng.integers(0, 256, nchunks * cs, dtype=np.uint8)
+    dbuf = _dev(engine, host)
+    out = engine.DeviceBuffer(nchunks * 4)
+    for cin in (0, 0xDEADBEEF):
+        p = _chunk_plan(engine, dbuf, host.nbytes, cs, engine.MODE_COMPUTE, out, crc_init=cin)
+        assert p.stats()["generic_bytes"] == 0
+        p.execute()
+        got = out.download(dtype=np.uint32)
+        if cin == 0:
+            want = oracle.chunk_crcs(host, cs)
+        else:
+            want = np.array([oracle.crc32c(cin, host[i * cs:(i + 1) * cs]) for i in range(nchunks)], np.uint32)
+        np.testing.assert_array_equal(got, want)
+
+
+def test_generic_path_unaligned_and_odd_sizes(engine, oracle):
+    rng = np.random.default_rng(11)
+    host = rng.integers(0, 256, 300000, dtype=np.uint8)
+    dbuf = _dev(engine, host)
+    for off, n, cs in [(1, 100000, 512), (3, 65536, 512), (8, 70001, 4096), (0, 99999, 100),
+                       (0, 5000, 1), (5, 12345, 777), (0, 1, 512), (13, 512, 512)]:
+        nch = (n + cs - 1) // cs
+        out = engine.DeviceBuffer(nch * 4)
+        p = _chunk_plan(engine, dbuf, n, cs, engine.MODE_COMPUTE, out, offset=off)
+        p.execute()
+        want = oracle.chunk_crcs(host[off:off + n], cs)
+        np.testing.assert_array_equal(out.download(dtype=np.uint32), want, err_msg=f"{off},{n},{cs}")
+
+
+def _mixed_segments(engine, rng, nseg=24):
+    """A C5-like table: chunk sizes 512<<(i%4), ragged tails, one unaligned
+    and one empty segment, all in one plan."""
+    specs = []
+    for i in range(nseg):
+        cs = 512 << (i % 4)
+        n = int(rng.integers(0, 40)) * cs + (int(rng.integers(1, cs)) if i % 5 == 2 else 0)
+        specs.append((cs, n, 1 if i == 7 else 0))
+    specs.append((512, 0, 0))
+    total = sum(n + 256 for _, n, _ in specs)
+    host = rng.integers(0, 256, total, dtype=np.uint8)
+    dbuf = _dev(engine, host)
+    offs, o = [], 0
+    for cs, n, mis in specs:
+        offs.append(o + mis)
+        o += n + 256 - (n % 256)
+        o = (o + 255) // 256 * 256
+    return specs, offs, host, dbuf
+
+
+def test_mixed_segment_plan_compute_and_verify(engine, oracle):
+    rng = np.random.default_rng(21)
+    specs, offs, host, dbuf = _mixed_segments(engine, rng)
+    nch = [(n + cs - 1) // cs for cs, n, _ in specs]
+    crc_bufs = [engine.DeviceBuffer(max(4, c * 4)) for c in nch]
+    bm_bufs = [engine.DeviceBuffer(max(4, (c + 7) // 8)) for c in nch]
+    segs = [engine.Segment(data=dbuf.ptr + off, len=n, chunk_size=cs, flags=engine.SEG_BE, crc_init=0,
+                           crcs=cb.ptr, bitmap=None)
+            for (cs, n, _), off, cb in zip(specs, offs, crc_bufs)]
+    p = engine.Plan(engine.MODE_COMPUTE, segs)
+    p.execute()
+    wants = []
+    for (cs, n, _), off, cb, c in zip(specs, offs, crc_bufs, nch):
+        want = oracle.chunk_crcs(host[off:off + n], cs)
+        wants.append(want)
+        np.testing.assert_array_equal(cb.download(c * 4, dtype=">u4").astype(np.uint32), want)
+    # verify the same table after corrupting chosen chunks
+    bad = {}
+    for si, ((cs, n, _), off, c) in enumerate(zip(specs, offs, nch)):
+        if c and si % 3 == 0:
+            picks = sorted(set(int(x) for x in rng.integers(0, c, 3)))
+            bad[si] = picks
+            for ci in picks:
+                clen = min(cs, n - ci * cs)
+                bit = int(rng.integers(0, 8 * clen))
+                host[off + ci * cs + bit // 8] ^= np.uint8(1 << (bit % 8))
+    dbuf.upload(host)
+    vsegs = [engine.Segment(data=s.data, len=s.len, chunk_size=s.chunk_size, flags=engine.SEG_BE,
+                            crc_init=0, crcs=s.crcs, bitmap=bb.ptr) for s, bb in zip(segs, bm_bufs)]
+    vp = engine.Plan(engine.MODE_VERIFY, vsegs)
+    vp.execute()
+    first_bad, mism = vp.results()
+    assert mism == sum(len(v) for v in bad.values())
+    for si, c in enumerate(nch):
+        exp_bits = np.zeros((c + 7) // 8 * 8, dtype=np.uint8)
+        for ci in bad.get(si, []):
+            exp_bits[ci] = 1
+        got = np.unpackbits(bm_bufs[si].download((c + 7) // 8), bitorder="little")
+        np.testing.assert_array_equal(got[: exp_bits.size], exp_bits, err_msg=str(si))
+        assert first_bad[si] == (bad[si][0] if si in bad else 0xFFFFFFFF)
+
+
+# --- datanode mirrors on host memory ----------------------------------------
+def test_verify_crcdata_golden(engine, golden):
+    for case in golden["verify"]:
+        region = bytes.fromhex(case["region_hex"])
+        cs, dlen = case["chunk_size"], case["dlen"]
+        nch = (dlen + cs - 1) // cs
+        err, fb = engine.verify_crcdata(region, cs, nch * 4, dlen)
+        assert fb == case["first_bad"], case["mismatch"]
+        assert err == (engine.ERR_BAD_CHECKSUM if case["mismatch"] else 0)
+        if nch:
+            assert engine.verify_crcdata(region, cs, nch * 4 + 4, dlen)[0] == engine.ERR_CRC_LEN
+    assert engine.verify_crcdata(b"\0" * 8, 512, 4, 512, ctype=engine.CSUM_CRC32)[0] == \
+        engine.ERR_UNSUPPORTED_CHECKSUM
+
+
+def test_compose_crcs_vs_oracle(engine, oracle):
+    rng = np.random.default_rng(8)
+    data = rng.integers(0, 256, 65536 + 300, dtype=np.uint8).tobytes()
+    for cuts in ([0, 65536 + 300], [0, 1, 100, 513, 40000, 65836], [0, 65536]):
+        frags = [data[a:b] for a, b in zip(cuts[:-1], cuts[1:])]
+        assert engine.compose_crcs(frags, 512) == oracle.compose_crcs(frags, 512)
+
+
+# --- large inputs: stream CRC and the pinned full-block digests ---------------
+def test_stream_crc_large(engine, oracle):
+    host = splitmix64_np(8 << 20, seed=99).view(np.uint8)  # 64 MiB
+    dbuf = _dev(engine, host)
+    for n in (host.nbytes, host.nbytes - 4095, 12345679):
+        assert engine.stream_crc_dev(0, dbuf.ptr, n) == oracle.crc32c(0, host[:n], "hw")
+    assert engine.crc32c(7, host[:5000001]) == oracle.crc32c(7, host[:5000001], "hw")
+
+
+def test_block_digests_on_device(engine, oracle, golden):
+    """128 MiB blocks generated on device by formula; digests pinned by the
+    reference."""
+    hc = engine
+    blk_bytes = 128 << 20
+    dbuf = engine.DeviceBuffer(blk_bytes)
+    for blk in (0, 1):
+        hc.fill_splitmix64(dbuf.ptr, blk_bytes // 8, 0, blk << 24)
+        for cs in (512, 1024, 2048, 4096):
+            out = engine.DeviceBuffer(blk_bytes // cs * 4)
+            p = _chunk_plan(engine, dbuf, blk_bytes, cs, engine.MODE_COMPUTE, out)
+            p.execute()
+            arr = out.download(dtype=np.uint32)
+            want = golden["blocks"][f"block{blk}_{cs}"]
+            assert int(arr[0]) == want["crc0"], (blk, cs)
+            assert oracle.crc32c(0, arr.view(np.uint8), "hw") == want["digest"], (blk, cs)
+            # the same digest on device (stream CRC of the device CRC array)
+            assert engine.stream_crc_dev(0, out.ptr, out.nbytes) == want["digest"]
+
+
+def test_verify_roundtrip_corruption_pattern(engine):
+    """Size-independent property used at full bench scale: compute -> corrupt
+    (i % 65537 == 0) -> verify finds exactly the corrupted chunks."""
+    hc = engine
+    nblk, blk = 4, 128 << 20
+    cs = 512
+    dbuf = engine.DeviceBuffer(nblk * blk)
+    hc.fill_splitmix64(dbuf.ptr, nblk * blk // 8, 0, 0)
+    crcs = engine.DeviceBuffer(nblk * blk // cs * 4)
+    bms = engine.DeviceBuffer(nblk * blk // cs // 8)
+    per = blk // cs
+    segs = [engine.Segment(data=dbuf.ptr + b * blk, len=blk, chunk_size=cs, flags=engine.SEG_BE,
+                           crc_init=0, crcs=crcs.ptr + b * per * 4, bitmap=bms.ptr + b * per // 8)
+            for b in range(nblk)]
+    engine.Plan(engine.MODE_COMPUTE, segs).execute()
+    for b in range(nblk):
+        hc.corrupt(dbuf.ptr + b * blk, blk, cs, b * per, 65537, 7919)
+    vp = engine.Plan(engine.MODE_VERIFY, segs)
+    vp.execute()
+    first_bad, mism = vp.results()
+    expected = [i for i in range(nblk * per) if i % 65537 == 0]
+    assert mism == len(expected)
+    bits = np.unpackbits(bms.download(), bitorder="little")
+    assert list(np.nonzero(bits)[0]) == expected
+    for b in range(nblk):
+        mine = [i - b * per for i in expected if b * per <= i < (b + 1) * per]
+        assert first_bad[b] == (mine[0] if mine else 0xFFFFFFFF)
