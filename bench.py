@@ -170,16 +170,17 @@ def main():
     # C2: compute-only (also produces the expected wire CRCs for C3).
     comp = h.Plan(h.MODE_COMPUTE, segs(lambda b: cs, h.SEG_BE, False))
     comp.execute()
+    h.device_sync()
     if not args.no_extra:
         ms = comp.time(3, stream)
         extra["compute_gibps"] = round(B * BLOCK / (ms * 1e-3) / (1 << 30), 1)
-        comp.execute()  # restore expected CRCs (identical) on the default stream
-    h.stream_sync(None)
+        extra["probe_read_GBps"] = round(h.probe_read(data.ptr, B * BLOCK, 3, stream), 1)
+    h.device_sync()
 
     # Corrupt 1 in 65537 chunks (global chunk index), then verify.
     for b in range(B):
         h.corrupt(data.ptr + b * BLOCK, BLOCK, cs, (g_block0 + b) * per, 65537, 7919, None)
-    h.stream_sync(None)
+    h.device_sync()
     first = (g_block0 * per + 65536) // 65537 * 65537
     expect_bad = max(0, ((g_block0 + B) * per - 1 - first) // 65537 + 1) if first < (g_block0 + B) * per else 0
 
@@ -190,7 +191,7 @@ def main():
     _, m = ver.results(stream)
     parity_ok = m == expect_bad
 
-    ver.set_timing(True)
+    ver.set_timing(max(2, args.steps))
     d.barrier()
     h.stream_sync(stream)
     t0 = time.perf_counter()

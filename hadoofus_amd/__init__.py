@@ -29,6 +29,10 @@ from .crc32c import (  # noqa: F401
     stream_create,
     stream_sync,
     device_info,
+    device_sync,
+    probe_read,
+    set_tile_order,
+    set_tuning,
     load,
     stream_crc_dev,
     verify_crcdata,

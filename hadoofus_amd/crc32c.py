@@ -94,6 +94,10 @@ def load(path=LIB_PATH):
     _bind(lib, "hdfs_crc32c_stream_sync", _int, [_vp])
     _bind(lib, "hdfs_crc32c_fill_splitmix64", _int, [_vp, _u64, _u64, _u64, _vp])
     _bind(lib, "hdfs_crc32c_corrupt", _int, [_vp, _u64, _u32, _u64, _u64, _u64, _vp])
+    _bind(lib, "hdfs_crc32c_device_sync", _int, [])
+    _bind(lib, "hdfs_crc32c_set_tile_order", _int, [_int])
+    _bind(lib, "hdfs_crc32c_probe_read", _int, [_vp, _u64, _vp, _int, ctypes.POINTER(ctypes.c_double)])
+    _bind(lib, "hdfs_crc32c_set_tuning", _int, [_int, _vp])
     _lib = lib
     return lib
 
@@ -261,3 +265,22 @@ def fill_splitmix64(dptr, nwords, seed=0, g0=0, stream=None):
 
 def corrupt(dptr, nbytes, chunk, chunk0, modulus=65537, bitmul=7919, stream=None):
     _check(load().hdfs_crc32c_corrupt(dptr, nbytes, chunk, chunk0, modulus, bitmul, stream))
+
+
+def device_sync():
+    _check(load().hdfs_crc32c_device_sync())
+
+
+def set_tile_order(order):
+    _check(load().hdfs_crc32c_set_tile_order(order))
+
+
+def probe_read(dptr, nbytes, iters=3, stream=None):
+    """Measured streaming-read GB/s (the empirical roofline)."""
+    g = ctypes.c_double(0)
+    _check(load().hdfs_crc32c_probe_read(dptr, nbytes, stream, iters, ctypes.byref(g)))
+    return g.value
+
+
+def set_tuning(nt_loads=0, diag_ptr=None):
+    _check(load().hdfs_crc32c_set_tuning(nt_loads, diag_ptr))

@@ -23,9 +23,11 @@
 
 namespace hdfs_crc32c {
 
-hipError_t launch_tiles(int mode, int grid, const SegDev *segs, uint32_t nseg, uint64_t total_rounds,
-                        const uint32_t *gtab, uint32_t *first_bad, unsigned long long *mism,
+hipError_t launch_tiles(int mode, int order, int nt, int grid, const SegDev *segs, uint32_t nseg,
+                        uint64_t total_rounds, uint64_t total_tiles, const uint32_t *gtab,
+                        uint32_t *first_bad, unsigned long long *mism, unsigned long long *diag,
                         hipStream_t stream);
+hipError_t launch_probe_read(const uint8_t *p, uint64_t nbytes, uint32_t *out, int grid, hipStream_t stream);
 hipError_t launch_generic(int mode, const SegDev *segs, uint32_t nseg, uint64_t total_gtiles,
                           const uint32_t *gtab, uint32_t *first_bad, unsigned long long *mism,
                           hipStream_t stream);
@@ -79,6 +81,16 @@ struct DevCtx {
 
 DevCtx g_ctx[kMaxDev];
 std::mutex g_init_mu;
+// Wave -> tile assignment of the tiled kernel: 0 contiguous slices, 1 interleaved.
+int env_int(const char *name, int dflt) {
+  const char *e = std::getenv(name);
+  return e ? std::atoi(e) : dflt;
+}
+int g_tile_order = env_int("HDFS_CRC32C_TILE_ORDER", 1);
+// Data-stream load policy of the tiled kernel: 0 default, 1 nontemporal.
+int g_nt_loads = env_int("HDFS_CRC32C_NT", 1);
+// Diagnostic per-wave timestamps (device buffer, 3 x u64 per wave) or null.
+unsigned long long *g_diag = nullptr;
 
 struct DeviceGuard {
   int prev = -1;
@@ -154,7 +166,7 @@ int ctx_init(int device, DevCtx **out) {
 
 // Split a segment between the tiled kernel and the generic kernel.
 // Tiled: data 16-B aligned, chunk_size a multiple of 512, full chunks only.
-void classify(SegDev &s, uint64_t &rounds, uint64_t &gtiles) {
+void classify(SegDev &s, uint64_t &rounds, uint64_t &gtiles, uint64_t &mtiles) {
   const uint64_t ntiles = (uint64_t(s.nchunks) + kTileChunks - 1) / kTileChunks;
   const bool eligible = s.nchunks > 0 && (reinterpret_cast<uintptr_t>(s.data) & 15u) == 0 &&
                         s.chunk_size % kRoundBytes == 0;
@@ -168,6 +180,8 @@ void classify(SegDev &s, uint64_t &rounds, uint64_t &gtiles) {
   }
   s.round_start = rounds;
   s.gtile_start = gtiles;
+  s.mtile_start = mtiles;
+  mtiles += s.main_tiles;
   rounds += uint64_t(s.main_tiles) * (s.chunk_size / kRoundBytes);
   gtiles += s.gen_tiles;
 }
@@ -208,8 +222,8 @@ bool device_accessible(const void *p) {
 }
 
 int launch_all(DevCtx &c, int mode, const SegDev *d_segs, uint32_t nseg, uint64_t rounds,
-               uint64_t gtiles, uint32_t *d_fb, unsigned long long *d_mism, hipStream_t st,
-               hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr) {
+               uint64_t mtiles, uint64_t gtiles, uint32_t *d_fb, unsigned long long *d_mism,
+               hipStream_t st, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr) {
   if (mode == kModeVerify) {
     HIPCHK(hipMemsetAsync(d_fb, 0xFF, sizeof(uint32_t) * (nseg ? nseg : 1), st));
     HIPCHK(hipMemsetAsync(d_mism, 0, sizeof(unsigned long long), st));
@@ -219,7 +233,8 @@ int launch_all(DevCtx &c, int mode, const SegDev *d_segs, uint32_t nseg, uint64_
     uint64_t want = (rounds + 255) / 256;
     int grid = static_cast<int>(want < 1 ? 1 : (want > uint64_t(c.num_cu) ? c.num_cu : want));
     if (ev0) HIPCHK(hipEventRecord(ev0, st));
-    HIPCHK(launch_tiles(mode, grid, d_segs, nseg, rounds, c.d_tab_main, d_fb, d_mism, st));
+    HIPCHK(launch_tiles(mode, g_tile_order, g_nt_loads, grid, d_segs, nseg, rounds, mtiles,
+                        c.d_tab_main, d_fb, d_mism, g_diag, st));
     if (ev1) HIPCHK(hipEventRecord(ev1, st));
   }
   if (gtiles) HIPCHK(launch_generic(mode, d_segs, nseg, gtiles, c.d_tab_main, d_fb, d_mism, st));
@@ -245,10 +260,10 @@ int stream_crc_locked(DevCtx &c, uint32_t crc, const void *dbuf, uint64_t len, u
   SegDev s;
   int rc = fill_seg(in, HDFS_CRC32C_MODE_COMPUTE, s, 0);
   if (rc) return rc;
-  uint64_t rounds = 0, gtiles = 0;
-  classify(s, rounds, gtiles);
+  uint64_t rounds = 0, gtiles = 0, mtiles = 0;
+  classify(s, rounds, gtiles, mtiles);
   HIPCHK(hipMemcpyAsync(c.d_seg, &s, sizeof(s), hipMemcpyHostToDevice, c.stream));
-  rc = launch_all(c, kModeCompute, c.d_seg, 1, rounds, gtiles, nullptr, nullptr, c.stream);
+  rc = launch_all(c, kModeCompute, c.d_seg, 1, rounds, mtiles, gtiles, nullptr, nullptr, c.stream);
   if (rc) return rc;
   HIPCHK(hipMemsetAsync(c.d_small, 0, 4, c.stream));
   HIPCHK(launch_combine(c.d_raw, nraw, kStreamPiece, len, c.d_tab_pow2, ~crc, c.d_small, c.stream));
@@ -301,9 +316,10 @@ struct hdfs_crc32c_plan {
   SegDev *d_segs = nullptr;
   uint32_t *d_first_bad = nullptr;
   unsigned long long *d_mism = nullptr;
-  uint64_t rounds = 0, gtiles = 0, main_bytes = 0, gen_bytes = 0, nchunks = 0;
+  uint64_t rounds = 0, mtiles = 0, gtiles = 0, main_bytes = 0, gen_bytes = 0, nchunks = 0;
   bool timing = false;
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> events;  // pre-created pool
+  size_t next_event = 0;
 };
 
 extern "C" {
@@ -364,14 +380,14 @@ int hdfs_crc32c_plan_create(hdfs_crc32c_plan **plan, int mode, const hdfs_crc32c
   if (rc) return rc;
   DeviceGuard g(c->dev);
   std::vector<SegDev> host(nseg ? nseg : 1);
-  uint64_t rounds = 0, gtiles = 0, main_bytes = 0, gen_bytes = 0, nch = 0;
+  uint64_t rounds = 0, gtiles = 0, mtiles = 0, main_bytes = 0, gen_bytes = 0, nch = 0;
   for (size_t i = 0; i < nseg; i++) {
     rc = fill_seg(segs[i], mode, host[i], i);
     if (rc) return rc;
     if (!device_accessible(segs[i].data) || !device_accessible(segs[i].crcs) ||
         !device_accessible(segs[i].bitmap))
       return fail(HDFS_CRC32C_EINVAL, "segment %zu: pointer is not device-accessible memory", i);
-    classify(host[i], rounds, gtiles);
+    classify(host[i], rounds, gtiles, mtiles);
     const uint64_t mb = std::min<uint64_t>(segs[i].len, uint64_t(host[i].main_tiles) * kTileChunks *
                                                             segs[i].chunk_size);
     main_bytes += mb;
@@ -383,6 +399,7 @@ int hdfs_crc32c_plan_create(hdfs_crc32c_plan **plan, int mode, const hdfs_crc32c
   p->mode = mode;
   p->nseg = static_cast<uint32_t>(nseg);
   p->rounds = rounds;
+  p->mtiles = mtiles;
   p->gtiles = gtiles;
   p->main_bytes = main_bytes;
   p->gen_bytes = gen_bytes;
@@ -406,12 +423,18 @@ int hdfs_crc32c_plan_execute(hdfs_crc32c_plan *p, void *stream) {
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : c.stream;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (p->timing && p->rounds) {
-    HIPCHK(hipEventCreate(&e0));
-    HIPCHK(hipEventCreate(&e1));
-    p->events.emplace_back(e0, e1);
+    if (p->next_event == p->events.size()) {  // pool exhausted: grow (outside any timed loop
+      hipEvent_t a, b;                         // when set_timing pre-sized it)
+      HIPCHK(hipEventCreate(&a));
+      HIPCHK(hipEventCreate(&b));
+      p->events.emplace_back(a, b);
+    }
+    e0 = p->events[p->next_event].first;
+    e1 = p->events[p->next_event].second;
+    p->next_event++;
   }
-  return launch_all(c, p->mode, p->d_segs, p->nseg, p->rounds, p->gtiles, p->d_first_bad, p->d_mism,
-                    st, e0, e1);
+  return launch_all(c, p->mode, p->d_segs, p->nseg, p->rounds, p->mtiles, p->gtiles, p->d_first_bad,
+                    p->d_mism, st, e0, e1);
 }
 
 int hdfs_crc32c_plan_results(hdfs_crc32c_plan *p, void *stream, uint32_t *first_bad, size_t nseg,
@@ -436,7 +459,16 @@ int hdfs_crc32c_plan_results(hdfs_crc32c_plan *p, void *stream, uint32_t *first_
 
 int hdfs_crc32c_plan_set_timing(hdfs_crc32c_plan *p, int on) {
   if (!p) return fail(HDFS_CRC32C_EINVAL, "null plan");
-  p->timing = on != 0;
+  DeviceGuard g(p->dev);
+  p->timing = on > 0;
+  // on > 1: pre-create that many event pairs so no hipEventCreate runs
+  // inside the caller's timed loop.
+  while (on > 1 && p->events.size() < size_t(on)) {
+    hipEvent_t a, b;
+    HIPCHK(hipEventCreate(&a));
+    HIPCHK(hipEventCreate(&b));
+    p->events.emplace_back(a, b);
+  }
   return HDFS_CRC32C_OK;
 }
 
@@ -445,16 +477,15 @@ int hdfs_crc32c_plan_kernel_ms(hdfs_crc32c_plan *p, double *total_ms, int *launc
   DeviceGuard g(p->dev);
   double tot = 0;
   int n = 0;
-  for (auto &ev : p->events) {
+  for (size_t i = 0; i < p->next_event; i++) {
+    auto &ev = p->events[i];
     HIPCHK(hipEventSynchronize(ev.second));
     float ms = 0;
     HIPCHK(hipEventElapsedTime(&ms, ev.first, ev.second));
     tot += ms;
     n++;
-    (void)hipEventDestroy(ev.first);
-    (void)hipEventDestroy(ev.second);
   }
-  p->events.clear();
+  p->next_event = 0;
   if (total_ms) *total_ms = tot;
   if (launches) *launches = n;
   return HDFS_CRC32C_OK;
@@ -536,12 +567,12 @@ int hdfs_crc32c_verify_crcdata(const void *crcdata, int32_t chunksize, int32_t c
   SegDev s;
   rc = fill_seg(in, HDFS_CRC32C_MODE_VERIFY, s, 0);
   if (rc) return rc;
-  uint64_t rounds = 0, gtiles = 0;
-  classify(s, rounds, gtiles);
+  uint64_t rounds = 0, gtiles = 0, mtiles = 0;
+  classify(s, rounds, gtiles, mtiles);
   HIPCHK(hipMemcpyAsync(c->d_seg, &s, sizeof(s), hipMemcpyHostToDevice, c->stream));
   uint32_t *d_fb = c->d_small + 1;
   auto *d_m = reinterpret_cast<unsigned long long *>(c->d_small + 2);
-  rc = launch_all(*c, kModeVerify, c->d_seg, 1, rounds, gtiles, d_fb, d_m, c->stream);
+  rc = launch_all(*c, kModeVerify, c->d_seg, 1, rounds, mtiles, gtiles, d_fb, d_m, c->stream);
   if (rc) return rc;
   uint32_t fb = 0;
   HIPCHK(hipMemcpyAsync(&fb, d_fb, 4, hipMemcpyDeviceToHost, c->stream));
@@ -579,10 +610,10 @@ int hdfs_crc32c_compose_crcs(const void *const *iov_base, const size_t *iov_len,
   SegDev s;
   rc = fill_seg(in, HDFS_CRC32C_MODE_COMPUTE, s, 0);
   if (rc) return rc;
-  uint64_t rounds = 0, gtiles = 0;
-  classify(s, rounds, gtiles);
+  uint64_t rounds = 0, gtiles = 0, mtiles = 0;
+  classify(s, rounds, gtiles, mtiles);
   HIPCHK(hipMemcpyAsync(c->d_seg, &s, sizeof(s), hipMemcpyHostToDevice, c->stream));
-  rc = launch_all(*c, kModeCompute, c->d_seg, 1, rounds, gtiles, nullptr, nullptr, c->stream);
+  rc = launch_all(*c, kModeCompute, c->d_seg, 1, rounds, mtiles, gtiles, nullptr, nullptr, c->stream);
   if (rc) return rc;
   HIPCHK(hipMemcpyAsync(crc_be_out, c->d_stage + off_crc, nch * 4, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
@@ -647,6 +678,47 @@ int hdfs_crc32c_corrupt(void *dptr, uint64_t len, uint32_t chunk, uint64_t chunk
   if (!len) return HDFS_CRC32C_OK;
   HIPCHK(launch_corrupt(static_cast<uint8_t *>(dptr), len, chunk, chunk0, modulus, bitmul,
                         static_cast<hipStream_t>(stream)));
+  return HDFS_CRC32C_OK;
+}
+
+int hdfs_crc32c_device_sync(void) {
+  HIPCHK(hipDeviceSynchronize());
+  return HDFS_CRC32C_OK;
+}
+
+int hdfs_crc32c_set_tuning(int nt_loads, void *diag) {
+  g_nt_loads = nt_loads ? 1 : 0;
+  g_diag = static_cast<unsigned long long *>(diag);
+  return HDFS_CRC32C_OK;
+}
+
+int hdfs_crc32c_set_tile_order(int order) {
+  if (order != 0 && order != 1) return fail(HDFS_CRC32C_EINVAL, "tile order must be 0 or 1");
+  g_tile_order = order;
+  return HDFS_CRC32C_OK;
+}
+
+int hdfs_crc32c_probe_read(const void *dptr, uint64_t bytes, void *stream, int iters, double *gbps) {
+  if (!dptr || !bytes || iters <= 0 || !gbps) return fail(HDFS_CRC32C_EINVAL, "bad probe args");
+  DevCtx *c = nullptr;
+  int rc = ctx_init(-1, &c);
+  if (rc) return rc;
+  DeviceGuard g(c->dev);
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : c->stream;
+  hipEvent_t a, b;
+  HIPCHK(hipEventCreate(&a));
+  HIPCHK(hipEventCreate(&b));
+  HIPCHK(launch_probe_read(static_cast<const uint8_t *>(dptr), bytes, c->d_small, c->num_cu * 2, st));
+  HIPCHK(hipEventRecord(a, st));
+  for (int i = 0; i < iters; i++)
+    HIPCHK(launch_probe_read(static_cast<const uint8_t *>(dptr), bytes, c->d_small, c->num_cu * 2, st));
+  HIPCHK(hipEventRecord(b, st));
+  HIPCHK(hipEventSynchronize(b));
+  float ms = 0;
+  HIPCHK(hipEventElapsedTime(&ms, a, b));
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  *gbps = double(bytes) * iters / (ms * 1e-3) / 1e9;
   return HDFS_CRC32C_OK;
 }
 

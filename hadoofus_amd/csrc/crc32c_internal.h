@@ -24,6 +24,7 @@ struct SegDev {
   uint8_t *bitmap;       // verify: out, one bit per chunk, byte t per tile t
   uint64_t round_start;  // global index of this segment's first main-path round
   uint64_t gtile_start;  // global index of this segment's first generic tile
+  uint64_t mtile_start;  // global index of this segment's first main-path tile
   uint32_t chunk_size;   // bytes per checksum
   uint32_t flags;        // kSeg*
   uint32_t nchunks;      // ceil(len / chunk_size)

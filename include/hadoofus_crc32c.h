@@ -93,7 +93,8 @@ int hdfs_crc32c_plan_execute(hdfs_crc32c_plan *plan, void *stream);
 int hdfs_crc32c_plan_results(hdfs_crc32c_plan *plan, void *stream,
     uint32_t *first_bad, size_t nseg, uint64_t *mismatches);
 /* Optional device-side timing of the tiled kernel (HIP events recorded on
- * the execute stream around each launch). */
+ * the execute stream around each launch).  on > 1 pre-creates that many
+ * event pairs; kernel_ms sums and resets the recorded launches. */
 int hdfs_crc32c_plan_set_timing(hdfs_crc32c_plan *plan, int on);
 int hdfs_crc32c_plan_kernel_ms(hdfs_crc32c_plan *plan, double *total_ms, int *launches);
 /* Bytes per pass the tiled and generic kernels cover (for roofline maths). */
@@ -136,6 +137,19 @@ int hdfs_crc32c_corrupt(void *dptr, uint64_t len, uint32_t chunk, uint64_t chunk
 /* Elapsed device time of `iters` back-to-back plan executions on `stream`
  * measured with HIP events (ms per execution). */
 int hdfs_crc32c_plan_time(hdfs_crc32c_plan *plan, void *stream, int iters, double *ms_per_iter);
+/* hipDeviceSynchronize on the engine's device. */
+int hdfs_crc32c_device_sync(void);
+/* Tiled-kernel schedule: 0 static per-wave slices, 1 workgroup-dynamic (default)
+ * (waves of a workgroup take tiles from an LDS counter).  Env
+ * HDFS_CRC32C_TILE_ORDER. */
+int hdfs_crc32c_set_tile_order(int order);
+/* Tuning / diagnostics: nt_loads=1 (default) streams chunk data with nontemporal loads
+ * (env HDFS_CRC32C_NT); diag = device u64[3 * waves] receiving per-wave
+ * start/end s_memrealtime stamps and rounds processed (NULL = off). */
+int hdfs_crc32c_set_tuning(int nt_loads, void *diag);
+/* Empirical streaming-read bandwidth of `bytes` at dptr (GB/s, 1e9 B/s):
+ * fully coalesced 16-B-per-lane loads, no compute; the measured roofline. */
+int hdfs_crc32c_probe_read(const void *dptr, uint64_t bytes, void *stream, int iters, double *gbps);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,79 @@
+"""A/B timing of tiled-kernel variants in ONE process (interleaved rounds),
+the streaming-read probe (empirical roofline), and a per-wave timestamp
+diagnostic (tail imbalance).  GPU box only."""
+import json
+import os
+import statistics
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import hadoofus_amd as h  # noqa: E402
+
+BLOCK = 128 << 20
+B = int(os.environ.get("BLOCKS", "1024"))
+cs = 512
+h.load()
+data = h.DeviceBuffer(B * BLOCK)
+crcs = h.DeviceBuffer(B * BLOCK // cs * 4)
+bms = h.DeviceBuffer(B * BLOCK // cs // 8)
+h.fill_splitmix64(data.ptr, B * BLOCK // 8, 0, 0)
+h.device_sync()
+out = {"blocks": B}
+out["probe_read_GBps"] = [round(h.probe_read(data.ptr, B * BLOCK, 3), 1) for _ in range(3)]
+segs = [h.Segment(data=data.ptr + b * BLOCK, len=BLOCK, chunk_size=cs, flags=h.SEG_BE, crc_init=0,
+                  crcs=crcs.ptr + b * (BLOCK // cs) * 4, bitmap=bms.ptr + b * (BLOCK // cs) // 8) for b in range(B)]
+comp = h.Plan(h.MODE_COMPUTE, segs)
+ver = h.Plan(h.MODE_VERIFY, segs)
+comp.execute()
+h.device_sync()
+VARIANTS = [(0, 1), (1, 1), (1, 0)]  # (order, nt)
+res = {}
+for rnd in range(4):
+    for order, nt in VARIANTS:
+        h.set_tile_order(order)
+        h.set_tuning(nt, None)
+        for name, p in (("compute", comp), ("verify", ver)):
+            ms = p.time(3)
+            res.setdefault(f"{name}_o{order}_nt{nt}", []).append(B * BLOCK / (ms * 1e-3) / 1e9)
+fb, m = ver.results()
+out["verify_mismatches"] = m
+for k, v in res.items():
+    out[k + "_GBps_median"] = round(statistics.median(v), 1)
+# per-wave timestamps for the default variant
+nwaves = 256 * 16
+diag = h.DeviceBuffer(nwaves * 3 * 8)
+for order, nt in VARIANTS:
+    h.set_tile_order(order)
+    h.set_tuning(nt, diag.ptr)
+    diag.fill(0)
+    ver.execute()
+    h.device_sync()
+    d = diag.download(dtype=np.uint64).reshape(nwaves, 3).astype(np.float64)
+    st, en, nr = d[:, 0], d[:, 1], d[:, 2]
+    ok = en > 0
+    t0 = st[ok].min()
+    span = (en[ok].max() - t0) / 100.0  # 100 MHz ticks -> us
+    out[f"diag_o{order}_nt{nt}"] = {
+        "span_us": round(span, 1),
+        "wave_end_p50_us": round(float(np.percentile(en[ok] - t0, 50)) / 100, 1),
+        "wave_end_p05_us": round(float(np.percentile(en[ok] - t0, 5)) / 100, 1),
+        "wave_start_max_us": round(float((st[ok] - t0).max()) / 100, 1),
+        "rounds_min_max": [int(nr[ok].min()), int(nr[ok].max())],
+        "tail_loss_frac": round(float(1 - (en[ok] - t0).mean() / 100 / span), 4),
+    }
+    e = ((en - t0) / 100.0).reshape(-1, 16)  # [block][wave]
+    blk_max, blk_min = e.max(1), e.min(1)
+    xcd = np.arange(e.shape[0]) % 8
+    out[f"diag_o{order}_nt{nt}"].update({
+        "within_block_spread_us_median": round(float(np.median(blk_max - blk_min)), 1),
+        "block_end_max_p05_p50_p95_us": [round(float(np.percentile(blk_max, q)), 1) for q in (5, 50, 95)],
+        "xcd_mean_block_end_us": [round(float(blk_max[xcd == x].mean()), 1) for x in range(8)],
+        "wave_in_block_mean_end_us": [round(float(v), 1) for v in e.mean(0)],
+    })
+    np.save(os.path.join(ROOT, "gpurun_out", f"diag_o{order}_nt{nt}.npy"), d)
+h.set_tuning(0, None)
+h.set_tile_order(0)
+print(json.dumps(out))
