@@ -10,8 +10,9 @@ corrupted; output = mismatch bitmap + first bad chunk per block.
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
 
-Ranks shard independent blocks (no data-path collective, scaling "weak");
-RCCL all-reduce only aggregates {bytes, mismatches} (sum) and time (max).
+Ranks shard independent blocks (hadoofus_amd/shard.py: no data-path
+collective, scaling "weak"); one RCCL all-reduce aggregates {bytes,
+mismatches, ok} (sum) and time (max).
 Prints ONE JSON line on rank 0.
 """
 import argparse
@@ -41,38 +42,6 @@ def parse():
     ap.add_argument("--no-extra", action="store_true", help="skip compute/mixed side measurements")
     ap.add_argument("--cpu-gib", type=float, default=2.0, help="CPU baseline sample size")
     return ap.parse_args()
-
-
-class Dist:
-    """torch.distributed (nccl = RCCL over xGMI) only when launched as N ranks."""
-
-    def __init__(self):
-        self.world = int(os.environ.get("WORLD_SIZE", "1"))
-        self.rank = int(os.environ.get("RANK", "0"))
-        self.local = int(os.environ.get("LOCAL_RANK", "0"))
-        self.torch = None
-        if self.world > 1:
-            import torch
-            import torch.distributed as dist
-            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            torch.cuda.set_device(self.local)
-            dist.init_process_group("nccl")
-            self.torch, self.dist = torch, dist
-
-    def barrier(self):
-        if self.torch:
-            self.dist.barrier(device_ids=[self.local])
-
-    def allreduce(self, vals, op):
-        if not self.torch:
-            return vals
-        t = self.torch.tensor(vals, dtype=self.torch.float64, device=f"cuda:{self.local}")
-        self.dist.all_reduce(t, op=getattr(self.dist.ReduceOp, op))
-        return t.tolist()
-
-    def close(self):
-        if self.torch:
-            self.dist.destroy_process_group()
 
 
 def cpu_baseline(sample_gib):
@@ -128,14 +97,17 @@ def cpu_baseline(sample_gib):
 
 def main():
     args = parse()
-    d = Dist()
+    from hadoofus_amd import shard
+    # torch (and with it the HIP runtime it ships) is imported before the
+    # engine library only when launched as ranks; both then share one runtime.
+    d = shard.Collective("nccl") if shard.launched_by_torchrun() else shard.Local()
     import hadoofus_amd as h
 
     h.load()
     arch, ncu = h.device_info()
     B, cs = args.blocks, args.chunk
     per = BLOCK // cs
-    g_block0 = d.rank * B
+    g_block0, B = shard.rank_blocks(d.rank, d.world, B)
     stream = h.stream_create()
 
     data = h.DeviceBuffer(B * BLOCK)
@@ -181,8 +153,7 @@ def main():
     for b in range(B):
         h.corrupt(data.ptr + b * BLOCK, BLOCK, cs, (g_block0 + b) * per, 65537, 7919, None)
     h.device_sync()
-    first = (g_block0 * per + 65536) // 65537 * 65537
-    expect_bad = max(0, ((g_block0 + B) * per - 1 - first) // 65537 + 1) if first < (g_block0 + B) * per else 0
+    expect_bad = shard.expected_bad(g_block0, B, per, 65537)
 
     ver = h.Plan(h.MODE_VERIFY, segs(lambda b: cs, h.SEG_BE, True))
     for _ in range(args.warmup):
@@ -218,8 +189,7 @@ def main():
         mixc.destroy()
         mixv.destroy()
 
-    tot_bytes, tot_mism, ok = d.allreduce([float(B * BLOCK * args.steps), float(m), float(parity_ok)], "SUM")
-    (t_max,) = d.allreduce([elapsed], "MAX")
+    tot_bytes, tot_mism, ok, t_max = d.aggregate(B * BLOCK * args.steps, m, parity_ok, elapsed)
     n = d.world
 
     if d.rank == 0:

@@ -5,7 +5,7 @@ The product is the C-ABI shared library ``hadoofus_amd/lib/libhadoofus_crc32c.so
 mirror of that ABI used by the tests and bench; it has no compute of its own
 and no fallback: if the library or a gfx950 device is missing, calls fail.
 """
-from .crc32c import (  # noqa: F401
+from .abi import (  # noqa: F401
     LIB_PATH,
     CSUM_NULL,
     CSUM_CRC32,
@@ -24,6 +24,9 @@ from .crc32c import (  # noqa: F401
     Segment,
     crc32c,
     compose_crcs,
+    compute_host,
+    verify_host,
+    PinnedBuffer,
     corrupt,
     fill_splitmix64,
     stream_create,

@@ -98,6 +98,11 @@ def load(path=LIB_PATH):
     _bind(lib, "hdfs_crc32c_set_tile_order", _int, [_int])
     _bind(lib, "hdfs_crc32c_probe_read", _int, [_vp, _u64, _vp, _int, ctypes.POINTER(ctypes.c_double)])
     _bind(lib, "hdfs_crc32c_set_tuning", _int, [_int, _vp])
+    _bind(lib, "hdfs_crc32c_compute_host", _int, [_vp, _u64, _u32, _u32, _u32, _vp, _u64])
+    _bind(lib, "hdfs_crc32c_verify_host", _int,
+          [_vp, _u64, _u32, _u32, _u32, _vp, _vp, _u64, ctypes.POINTER(_u64), ctypes.POINTER(_u64)])
+    _bind(lib, "hdfs_crc32c_host_alloc", _int, [ctypes.POINTER(_vp), _u64])
+    _bind(lib, "hdfs_crc32c_host_free", _int, [_vp])
     _lib = lib
     return lib
 
@@ -181,6 +186,11 @@ class DeviceBuffer:
         if nbytes:
             _check(load().hdfs_crc32c_memcpy(out.ctypes.data, self.ptr + offset, nbytes, 1))
         return out.view(dtype)
+
+    def copy_to(self, host_ptr, nbytes=None, offset=0):
+        """D2H into caller-owned host memory (e.g. a PinnedBuffer)."""
+        nbytes = self.nbytes - offset if nbytes is None else nbytes
+        _check(load().hdfs_crc32c_memcpy(host_ptr, self.ptr + offset, nbytes, 1))
 
     def fill(self, value=0):
         _check(load().hdfs_crc32c_memset(self.ptr, value, self.nbytes))
@@ -284,3 +294,41 @@ def probe_read(dptr, nbytes, iters=3, stream=None):
 
 def set_tuning(nt_loads=0, diag_ptr=None):
     _check(load().hdfs_crc32c_set_tuning(nt_loads, diag_ptr))
+
+
+def compute_host(data, chunk_size, flags=0, crc_init=0, piece_bytes=0):
+    """Per-chunk CRCs of a host buffer via the pipelined H2D path."""
+    keep, p, n = _host(data)
+    nch = (n + chunk_size - 1) // chunk_size
+    out = np.zeros(max(1, nch), dtype=np.uint32)
+    _check(load().hdfs_crc32c_compute_host(p, n, chunk_size, flags, crc_init, out.ctypes.data, piece_bytes))
+    return out[:nch]
+
+
+def verify_host(data, chunk_size, crcs, flags=0, crc_init=0, piece_bytes=0, want_bitmap=True):
+    """-> (first_bad or None, mismatches, bitmap bytes or None)."""
+    keep, p, n = _host(data)
+    ck, cp, cn = _host(crcs)
+    nch = (n + chunk_size - 1) // chunk_size
+    assert cn >= nch * 4
+    bm = np.zeros(max(1, (nch + 7) // 8), dtype=np.uint8) if want_bitmap else None
+    fb, m = _u64(0), _u64(0)
+    _check(load().hdfs_crc32c_verify_host(p, n, chunk_size, flags, crc_init, cp,
+                                          bm.ctypes.data if bm is not None else None, piece_bytes,
+                                          ctypes.byref(fb), ctypes.byref(m)))
+    return (None if fb.value == 2**64 - 1 else fb.value), m.value, (bm[:(nch + 7) // 8] if bm is not None else None)
+
+
+class PinnedBuffer:
+    """Page-locked host memory (hipHostMalloc) viewed as a numpy array."""
+
+    def __init__(self, nbytes):
+        p = _vp()
+        _check(load().hdfs_crc32c_host_alloc(ctypes.byref(p), int(nbytes)))
+        self.ptr, self.nbytes = p.value, int(nbytes)
+        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * self.nbytes).from_address(self.ptr))
+
+    def free(self):
+        if self.ptr:
+            load().hdfs_crc32c_host_free(self.ptr)
+            self.ptr = None

@@ -76,6 +76,18 @@ struct DevCtx {
   size_t raw_cap = 0;
   SegDev *d_seg = nullptr;
   uint32_t *d_small = nullptr;  // [0] acc, [1] first_bad, [2..3] mismatches
+  // host pipeline (guarded by mu): two staging slots on two streams
+  hipStream_t copy_stream = nullptr, comp_stream = nullptr;
+  hipEvent_t ev_copy[2] = {nullptr, nullptr}, ev_comp[2] = {nullptr, nullptr};
+  uint8_t *p_data[2] = {nullptr, nullptr};
+  uint32_t *p_crc[2] = {nullptr, nullptr};
+  uint8_t *p_bm[2] = {nullptr, nullptr};
+  size_t p_cap = 0;        // bytes per data slot
+  size_t p_chunk_cap = 0;  // chunks per CRC slot
+  SegDev *p_segs = nullptr;
+  uint32_t *p_fb = nullptr;
+  unsigned long long *p_mism = nullptr;
+  size_t p_npieces_cap = 0;
   std::mutex mu;
 };
 
@@ -223,14 +235,15 @@ bool device_accessible(const void *p) {
 
 int launch_all(DevCtx &c, int mode, const SegDev *d_segs, uint32_t nseg, uint64_t rounds,
                uint64_t mtiles, uint64_t gtiles, uint32_t *d_fb, unsigned long long *d_mism,
-               hipStream_t st, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr) {
-  if (mode == kModeVerify) {
+               hipStream_t st, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, bool reset = true) {
+  if (mode == kModeVerify && reset) {
     HIPCHK(hipMemsetAsync(d_fb, 0xFF, sizeof(uint32_t) * (nseg ? nseg : 1), st));
     HIPCHK(hipMemsetAsync(d_mism, 0, sizeof(unsigned long long), st));
   }
   if (rounds) {
-    // >= 16 rounds per wave (16 waves per block) before adding blocks.
-    uint64_t want = (rounds + 255) / 256;
+    // >= 4 rounds per wave (16 waves per block) before adding blocks: each
+    // block pays a ~156 KiB LDS table fill.
+    uint64_t want = (rounds + 63) / 64;
     int grid = static_cast<int>(want < 1 ? 1 : (want > uint64_t(c.num_cu) ? c.num_cu : want));
     if (ev0) HIPCHK(hipEventRecord(ev0, st));
     HIPCHK(launch_tiles(mode, g_tile_order, g_nt_loads, grid, d_segs, nseg, rounds, mtiles,
@@ -296,6 +309,164 @@ int stream_crc_any(uint32_t crc, const void *buf, uint64_t len, uint32_t *out) {
     len -= n;
   }
   *out = crc;
+  return HDFS_CRC32C_OK;
+}
+
+bool is_pinned_host(const void *p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeHost || a.devicePointer != nullptr;
+}
+
+struct HostRegistration {
+  const void *p = nullptr;
+  ~HostRegistration() {
+    if (p) (void)hipHostUnregister(const_cast<void *>(p));
+  }
+  int ensure(const void *ptr, size_t n) {
+    if (!ptr || !n || is_pinned_host(ptr)) return HDFS_CRC32C_OK;
+    HIPCHK(hipHostRegister(const_cast<void *>(ptr), n, hipHostRegisterDefault));
+    p = ptr;
+    return HDFS_CRC32C_OK;
+  }
+};
+
+int pipe_reserve(DevCtx &c, size_t piece, uint32_t cs, size_t npieces) {
+  if (!c.copy_stream) {
+    HIPCHK(hipStreamCreateWithFlags(&c.copy_stream, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&c.comp_stream, hipStreamNonBlocking));
+    for (int b = 0; b < 2; b++) {
+      HIPCHK(hipEventCreateWithFlags(&c.ev_copy[b], hipEventDisableTiming));
+      HIPCHK(hipEventCreateWithFlags(&c.ev_comp[b], hipEventDisableTiming));
+    }
+  }
+  if (piece > c.p_cap) {
+    for (int b = 0; b < 2; b++) {
+      if (c.p_data[b]) HIPCHK(hipFree(c.p_data[b]));
+      c.p_data[b] = nullptr;
+    }
+    c.p_cap = 0;
+    for (int b = 0; b < 2; b++) HIPCHK(hipMalloc(&c.p_data[b], piece));
+    c.p_cap = piece;
+  }
+  const size_t chunks = (piece + cs - 1) / cs;
+  if (chunks > c.p_chunk_cap) {
+    for (int b = 0; b < 2; b++) {
+      if (c.p_crc[b]) HIPCHK(hipFree(c.p_crc[b]));
+      if (c.p_bm[b]) HIPCHK(hipFree(c.p_bm[b]));
+      c.p_crc[b] = nullptr;
+      c.p_bm[b] = nullptr;
+    }
+    c.p_chunk_cap = 0;
+    for (int b = 0; b < 2; b++) {
+      HIPCHK(hipMalloc(&c.p_crc[b], chunks * 4));
+      HIPCHK(hipMalloc(&c.p_bm[b], chunks / 8 + 8));
+    }
+    c.p_chunk_cap = chunks;
+  }
+  if (npieces > c.p_npieces_cap) {
+    if (c.p_segs) HIPCHK(hipFree(c.p_segs));
+    if (c.p_fb) HIPCHK(hipFree(c.p_fb));
+    c.p_segs = nullptr;
+    c.p_fb = nullptr;
+    HIPCHK(hipMalloc(&c.p_segs, npieces * sizeof(SegDev)));
+    HIPCHK(hipMalloc(&c.p_fb, npieces * sizeof(uint32_t)));
+    if (!c.p_mism) HIPCHK(hipMalloc(&c.p_mism, sizeof(unsigned long long)));
+    c.p_npieces_cap = npieces;
+  }
+  return HDFS_CRC32C_OK;
+}
+
+// Host-resident pass: pieces of `piece` bytes go H2D on the copy stream into
+// one of two device slots while the other slot is verified/computed on the
+// compute stream; results go D2H behind each kernel.
+int host_pipeline(int mode, const uint8_t *data, uint64_t len, uint32_t cs, uint32_t flags,
+                  uint32_t crc_init, void *crcs, uint8_t *bitmap, uint64_t piece_req,
+                  uint64_t *first_bad, uint64_t *mismatches) {
+  if (first_bad) *first_bad = UINT64_MAX;
+  if (mismatches) *mismatches = 0;
+  if (!cs) return fail(HDFS_CRC32C_EINVAL, "chunk_size 0");
+  if (!len) return HDFS_CRC32C_OK;
+  if (!data || !crcs) return fail(HDFS_CRC32C_EINVAL, "null host buffer");
+  if (flags & ~(HDFS_CRC32C_SEG_BE | HDFS_CRC32C_SEG_RAW)) return fail(HDFS_CRC32C_EINVAL, "bad flags");
+  if (mode == kModeVerify && (flags & HDFS_CRC32C_SEG_RAW)) return fail(HDFS_CRC32C_EINVAL, "RAW is compute-only");
+  const uint64_t unit = uint64_t(cs) * 8;  // pieces hold whole tiles: bitmap bytes never straddle
+  uint64_t piece = piece_req ? piece_req : (uint64_t(64) << 20);
+  piece = piece < unit ? unit : piece / unit * unit;
+  const uint64_t nch = (len + cs - 1) / cs;
+  if (nch > 0xFFFFFFF0ull) return fail(HDFS_CRC32C_EINVAL, "too many chunks");
+  const uint64_t npieces = (len + piece - 1) / piece;
+  DevCtx *cp = nullptr;
+  int rc = ctx_init(-1, &cp);
+  if (rc) return rc;
+  DevCtx &c = *cp;
+  DeviceGuard g(c.dev);
+  std::lock_guard<std::mutex> lk(c.mu);
+  rc = pipe_reserve(c, piece, cs, npieces);
+  if (rc) return rc;
+  HostRegistration reg_d, reg_c, reg_b;
+  if ((rc = reg_d.ensure(data, len)) || (rc = reg_c.ensure(crcs, nch * 4)) ||
+      (mode == kModeVerify && bitmap && (rc = reg_b.ensure(bitmap, (nch + 7) / 8))))
+    return rc;
+  // Per-piece descriptors (uploaded once).
+  std::vector<SegDev> segs(npieces);
+  std::vector<uint64_t> rounds(npieces), mt(npieces), gt(npieces);
+  for (uint64_t i = 0; i < npieces; i++) {
+    const uint64_t off = i * piece, n = std::min(piece, len - off);
+    const int b = int(i & 1);
+    hdfs_crc32c_segment in = {c.p_data[b], n, cs, flags, crc_init, 0, c.p_crc[b], c.p_bm[b]};
+    rc = fill_seg(in, mode, segs[i], size_t(i));
+    if (rc) return rc;
+    uint64_t r = 0, m = 0, gg = 0;
+    classify(segs[i], r, gg, m);
+    rounds[i] = r;
+    mt[i] = m;
+    gt[i] = gg;
+  }
+  HIPCHK(hipMemcpyAsync(c.p_segs, segs.data(), npieces * sizeof(SegDev), hipMemcpyHostToDevice, c.comp_stream));
+  if (mode == kModeVerify) {
+    HIPCHK(hipMemsetAsync(c.p_fb, 0xFF, npieces * 4, c.comp_stream));
+    HIPCHK(hipMemsetAsync(c.p_mism, 0, 8, c.comp_stream));
+  }
+  HIPCHK(hipEventRecord(c.ev_comp[0], c.comp_stream));
+  HIPCHK(hipEventRecord(c.ev_comp[1], c.comp_stream));
+  uint8_t *hc = static_cast<uint8_t *>(crcs);
+  for (uint64_t i = 0; i < npieces; i++) {
+    const int b = int(i & 1);
+    const uint64_t off = i * piece, n = std::min(piece, len - off);
+    const uint64_t c0 = off / cs, nc = (n + cs - 1) / cs;
+    HIPCHK(hipStreamWaitEvent(c.copy_stream, c.ev_comp[b], 0));  // slot free
+    HIPCHK(hipMemcpyAsync(c.p_data[b], data + off, n, hipMemcpyHostToDevice, c.copy_stream));
+    if (mode == kModeVerify)
+      HIPCHK(hipMemcpyAsync(c.p_crc[b], hc + c0 * 4, nc * 4, hipMemcpyHostToDevice, c.copy_stream));
+    HIPCHK(hipEventRecord(c.ev_copy[b], c.copy_stream));
+    HIPCHK(hipStreamWaitEvent(c.comp_stream, c.ev_copy[b], 0));
+    rc = launch_all(c, mode, c.p_segs + i, 1, rounds[i], mt[i], gt[i], c.p_fb + i, c.p_mism, c.comp_stream,
+                    nullptr, nullptr, false);
+    if (rc) return rc;
+    if (mode == kModeCompute)
+      HIPCHK(hipMemcpyAsync(hc + c0 * 4, c.p_crc[b], nc * 4, hipMemcpyDeviceToHost, c.comp_stream));
+    else if (bitmap)
+      HIPCHK(hipMemcpyAsync(bitmap + c0 / 8, c.p_bm[b], (nc + 7) / 8, hipMemcpyDeviceToHost, c.comp_stream));
+    HIPCHK(hipEventRecord(c.ev_comp[b], c.comp_stream));
+  }
+  HIPCHK(hipStreamSynchronize(c.comp_stream));
+  HIPCHK(hipStreamSynchronize(c.copy_stream));
+  if (mode == kModeVerify) {
+    std::vector<uint32_t> fb(npieces);
+    unsigned long long m = 0;
+    HIPCHK(hipMemcpy(fb.data(), c.p_fb, npieces * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&m, c.p_mism, 8, hipMemcpyDeviceToHost));
+    if (mismatches) *mismatches = m;
+    for (uint64_t i = 0; i < npieces; i++)
+      if (fb[i] != 0xFFFFFFFFu) {
+        if (first_bad) *first_bad = i * (piece / cs) + fb[i];
+        break;
+      }
+  }
   return HDFS_CRC32C_OK;
 }
 
@@ -678,6 +849,34 @@ int hdfs_crc32c_corrupt(void *dptr, uint64_t len, uint32_t chunk, uint64_t chunk
   if (!len) return HDFS_CRC32C_OK;
   HIPCHK(launch_corrupt(static_cast<uint8_t *>(dptr), len, chunk, chunk0, modulus, bitmul,
                         static_cast<hipStream_t>(stream)));
+  return HDFS_CRC32C_OK;
+}
+
+int hdfs_crc32c_compute_host(const void *data, uint64_t len, uint32_t chunk_size, uint32_t flags,
+                              uint32_t crc_init, void *crcs_out, uint64_t piece_bytes) {
+  return host_pipeline(kModeCompute, static_cast<const uint8_t *>(data), len, chunk_size, flags, crc_init,
+                       crcs_out, nullptr, piece_bytes, nullptr, nullptr);
+}
+
+int hdfs_crc32c_verify_host(const void *data, uint64_t len, uint32_t chunk_size, uint32_t flags,
+                             uint32_t crc_init, const void *crcs, uint8_t *bitmap_out, uint64_t piece_bytes,
+                             uint64_t *first_bad, uint64_t *mismatches) {
+  return host_pipeline(kModeVerify, static_cast<const uint8_t *>(data), len, chunk_size, flags, crc_init,
+                       const_cast<void *>(crcs), bitmap_out, piece_bytes, first_bad, mismatches);
+}
+
+int hdfs_crc32c_host_alloc(void **p, uint64_t bytes) {
+  DevCtx *c = nullptr;
+  int rc = ctx_init(-1, &c);
+  if (rc) return rc;
+  hipError_t e = hipHostMalloc(p, bytes ? bytes : 1, hipHostMallocDefault);
+  if (e != hipSuccess) return fail(HDFS_CRC32C_ENOMEM, "hipHostMalloc(%llu): %s", (unsigned long long)bytes,
+                                   hipGetErrorString(e));
+  return HDFS_CRC32C_OK;
+}
+
+int hdfs_crc32c_host_free(void *p) {
+  HIPCHK(hipHostFree(p));
   return HDFS_CRC32C_OK;
 }
 

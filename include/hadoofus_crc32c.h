@@ -120,6 +120,23 @@ int hdfs_crc32c_verify_crcdata(const void *crcdata, int32_t chunksize, int32_t c
 int hdfs_crc32c_compose_crcs(const void *const *iov_base, const size_t *iov_len, int iovcnt,
     size_t total, uint32_t chunk, void *crc_be_out);
 
+/* ---- host-resident streaming (pipelined H2D / kernel / D2H) -------------- */
+/* Per-chunk CRCs of a HOST buffer: pieces of piece_bytes (0 = 64 MiB, rounded
+ * to whole 8-chunk tiles) are copied H2D on a copy stream into one of two
+ * device slots while the other slot runs on a compute stream; CRCs come back
+ * D2H behind each kernel.  Pageable buffers are host-registered for the call.
+ * crcs_out: host u32[ceil(len/chunk_size)], wire order if HDFS_CRC32C_SEG_BE. */
+int hdfs_crc32c_compute_host(const void *data, uint64_t len, uint32_t chunk_size, uint32_t flags,
+    uint32_t crc_init, void *crcs_out, uint64_t piece_bytes);
+/* Verify a HOST buffer against host expected CRCs; optional host bitmap out;
+ * *first_bad = first bad chunk (UINT64_MAX if none), *mismatches = count. */
+int hdfs_crc32c_verify_host(const void *data, uint64_t len, uint32_t chunk_size, uint32_t flags,
+    uint32_t crc_init, const void *crcs, uint8_t *bitmap_out, uint64_t piece_bytes,
+    uint64_t *first_bad, uint64_t *mismatches);
+/* Pinned (page-locked) host memory for zero-copy-staging pipelines. */
+int hdfs_crc32c_host_alloc(void **p, uint64_t bytes);
+int hdfs_crc32c_host_free(void *p);
+
 /* ---- device memory + synthetic data helpers (bench / tests) ------------- */
 int hdfs_crc32c_dev_alloc(void **dptr, uint64_t bytes);
 int hdfs_crc32c_dev_free(void *dptr);

@@ -48,7 +48,7 @@ def test_exports_every_declared_symbol(libpath):
 def test_segment_struct_layout():
     import ctypes
 
-    from hadoofus_amd.crc32c import Segment
+    from hadoofus_amd.abi import Segment
     assert ctypes.sizeof(Segment) == 48
     assert Segment.crcs.offset == 32 and Segment.bitmap.offset == 40
 

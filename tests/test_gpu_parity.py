@@ -246,3 +246,35 @@ def test_verify_roundtrip_corruption_pattern(engine):
     for b in range(nblk):
         mine = [i - b * per for i in expected if b * per <= i < (b + 1) * per]
         assert first_bad[b] == (mine[0] if mine else 0xFFFFFFFF)
+
+
+# --- host-resident pipeline (H2D / kernel / D2H overlapped) --------------------
+@pytest.mark.parametrize("cs,n,piece", [(512, 3 << 20, 1 << 20), (512, (3 << 20) + 777, 1 << 20),
+                                        (4096, 5 << 20, 0), (1000, 2_000_003, 64000), (512, 100, 0)])
+def test_host_pipeline_vs_oracle(engine, oracle, cs, n, piece):
+    rng = np.random.default_rng(n % 1000 + cs)
+    host = rng.integers(0, 256, n, dtype=np.uint8)
+    want = oracle.chunk_crcs(host, cs)
+    got = engine.compute_host(host, cs, piece_bytes=piece)
+    np.testing.assert_array_equal(got, want)
+    be = engine.compute_host(host, cs, flags=engine.SEG_BE, piece_bytes=piece)
+    np.testing.assert_array_equal(be.byteswap(), want)
+    # verify: clean, then with corruptions in several pieces
+    fb, m, bm = engine.verify_host(host, cs, be, flags=engine.SEG_BE, piece_bytes=piece)
+    assert fb is None and m == 0 and not bm.any()
+    nch = want.size
+    bad = sorted(set(int(x) for x in rng.integers(0, nch, 4)))
+    for ci in bad:
+        host[ci * cs + int(rng.integers(0, min(cs, n - ci * cs)))] ^= 0x20
+    fb, m, bm = engine.verify_host(host, cs, be, flags=engine.SEG_BE, piece_bytes=piece)
+    assert fb == bad[0] and m == len(bad)
+    assert list(np.nonzero(np.unpackbits(bm, bitorder="little"))[0]) == bad
+
+
+def test_host_pipeline_pinned(engine, oracle):
+    n, cs = 24 << 20, 512
+    pin = engine.PinnedBuffer(n)
+    pin.array[:] = np.random.default_rng(2).integers(0, 256, n, dtype=np.uint8)
+    want = oracle.chunk_crcs(pin.array, cs)
+    np.testing.assert_array_equal(engine.compute_host(pin.array, cs, piece_bytes=4 << 20), want)
+    pin.free()
