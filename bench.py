@@ -41,7 +41,30 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-extra", action="store_true", help="skip compute/mixed side measurements")
     ap.add_argument("--cpu-gib", type=float, default=2.0, help="CPU baseline sample size")
+    ap.add_argument("--mixed", action="store_true",
+                    help="also time C5 (mixed 512/1024/2048/4096 bytesPerChecksum in one launch)")
     return ap.parse_args()
+
+
+def pmc_traffic(kernel, nbytes, chunk):
+    """HBM traffic per launch from the committed rocprofv3 PMC passes
+    (tools/pmc_traffic.py -> profiles/<round>/pmc_traffic.json): the measured
+    bytes-per-payload-byte ratio of the same kernel and chunk size, scaled to
+    this launch.  None when no matching profile is committed."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json"))):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        k = d.get("kernels", {}).get(kernel)
+        if k and d.get("chunk_size") == chunk:
+            best = (f, k)
+    if not best:
+        return None, None
+    f, k = best
+    return int(k["traffic_bytes_per_payload_byte"] * nbytes), os.path.relpath(f, ROOT)
 
 
 def cpu_baseline(sample_gib):
@@ -176,7 +199,7 @@ def main():
     parity_ok &= m == expect_bad
     elapsed = t1 - t0
 
-    if not args.no_extra:
+    if args.mixed:
         # C5: mixed bytesPerChecksum 512/1024/2048/4096 in one launch (compute + verify)
         mixc = h.Plan(h.MODE_COMPUTE, segs(lambda b: 512 << (b % 4), h.SEG_BE, False))
         mixc.execute(stream)
@@ -198,6 +221,7 @@ def main():
         alg = nbytes + 4 * nbytes / cs + nbytes / (8 * cs)  # data + expected CRCs + bitmap
         k_avg_s = kms / max(1, nlaunch) * 1e-3
         achieved = alg / k_avg_s / 1e9
+        traffic, traffic_src = pmc_traffic("verify", nbytes, cs)
         line = {
             "metric": "CRC32C verify GiB/s (device-resident), 512B chunks over 128MiB HDFS blocks",
             "value": round(gib_s, 1),
@@ -219,7 +243,8 @@ def main():
             },
             "roofline": {
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+                "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
                 "kernel": "crc32c_tiles_kernel<verify>", "kernel_avg_ms": round(k_avg_s * 1e3, 3),
                 "alg_bytes_per_launch": int(alg),
             },

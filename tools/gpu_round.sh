@@ -18,3 +18,7 @@ step h2d timeout -k 10 600 python tools/h2d_bench.py > gpurun_out/${TAG}_h2d.jso
 cat gpurun_out/${TAG}_h2d.json
 step prof timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu > gpurun_out/${TAG}_prof.log 2>&1
 grep -h crc32c_tiles gpurun_out/${TAG}_prof/run_kernel_stats.csv | cut -c1-220
+step pmc timeout -k 10 900 python tools/pmc_traffic.py ${ROUND:-r01} > gpurun_out/${TAG}_pmc.json 2> gpurun_out/${TAG}_pmc.err
+cat gpurun_out/${TAG}_pmc.json
+step mixed timeout -k 10 600 python bench.py --no-cpu --mixed --steps 5 > gpurun_out/${TAG}_mixed.json 2> gpurun_out/${TAG}_mixed.err
+cat gpurun_out/${TAG}_mixed.json
