@@ -82,3 +82,22 @@ def test_product_does_not_import_oracle():
             if f.endswith((".py", ".cpp", ".hip", ".h")):
                 txt = open(os.path.join(dp, f)).read()
                 assert "oracle" not in txt.replace("no oracle", ""), f
+
+
+def build_consumer(tmp_path, libpath):
+    """Compile + link the drop-in consumer (tests/consumer/t_unit_dropin.c)."""
+    exe = tmp_path / "t_unit_dropin"
+    libdir = os.path.dirname(libpath)
+    subprocess.check_call(["gcc", "-std=gnu99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+                           os.path.join(ROOT, "tests", "consumer", "t_unit_dropin.c"), "-o", str(exe),
+                           "-L", libdir, "-Wl,-rpath," + libdir, "-lhadoofus_crc32c"])
+    import json
+    kats = json.load(open(os.path.join(ROOT, "tests", "golden", "kats.json")))["kats"]
+    txt = tmp_path / "kats.txt"
+    txt.write_text("".join(f"{k['len']} {k['crc']:08x} {k['hex'] or '-'}\n" for k in kats))
+    return exe, txt
+
+
+def test_dropin_consumer_links(tmp_path, libpath):
+    exe, txt = build_consumer(tmp_path, libpath)
+    assert exe.exists() and txt.read_text().count("\n") >= 7

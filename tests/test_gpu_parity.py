@@ -278,3 +278,16 @@ def test_host_pipeline_pinned(engine, oracle):
     want = oracle.chunk_crcs(pin.array, cs)
     np.testing.assert_array_equal(engine.compute_host(pin.array, cs, piece_bytes=4 << 20), want)
     pin.free()
+
+
+def test_dropin_consumer_runs(engine, tmp_path):
+    """A C consumer compiled against include/crc32c.h and linked with the
+    engine passes the reference's KATs through all three drop-in symbols."""
+    import subprocess
+
+    from hadoofus_amd import build
+    from test_abi import build_consumer
+    exe, txt = build_consumer(tmp_path, build.LIB)
+    p = subprocess.run([str(exe), str(txt)], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "0 failures" in p.stdout
