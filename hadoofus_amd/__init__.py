@@ -36,6 +36,8 @@ from .abi import (  # noqa: F401
     probe_read,
     set_tile_order,
     set_tuning,
+    set_probe,
+    set_depth,
     load,
     stream_crc_dev,
     verify_crcdata,

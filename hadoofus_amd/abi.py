@@ -98,6 +98,8 @@ def load(path=LIB_PATH):
     _bind(lib, "hdfs_crc32c_set_tile_order", _int, [_int])
     _bind(lib, "hdfs_crc32c_probe_read", _int, [_vp, _u64, _vp, _int, ctypes.POINTER(ctypes.c_double)])
     _bind(lib, "hdfs_crc32c_set_tuning", _int, [_int, _vp])
+    _bind(lib, "hdfs_crc32c_set_probe", _int, [_int, _int, _int])
+    _bind(lib, "hdfs_crc32c_set_depth", _int, [_int])
     _bind(lib, "hdfs_crc32c_compute_host", _int, [_vp, _u64, _u32, _u32, _u32, _vp, _u64])
     _bind(lib, "hdfs_crc32c_verify_host", _int,
           [_vp, _u64, _u32, _u32, _u32, _vp, _vp, _u64, ctypes.POINTER(_u64), ctypes.POINTER(_u64)])
@@ -332,3 +334,11 @@ class PinnedBuffer:
         if self.ptr:
             load().hdfs_crc32c_host_free(self.ptr)
             self.ptr = None
+
+
+def set_probe(variant=0, grid_per_cu=2, block=1024):
+    _check(load().hdfs_crc32c_set_probe(variant, grid_per_cu, block))
+
+
+def set_depth(depth):
+    _check(load().hdfs_crc32c_set_depth(depth))

@@ -23,11 +23,12 @@
 
 namespace hdfs_crc32c {
 
-hipError_t launch_tiles(int mode, int order, int nt, int grid, const SegDev *segs, uint32_t nseg,
+hipError_t launch_tiles(int mode, int order, int nt, int depth, int grid, const SegDev *segs, uint32_t nseg,
                         uint64_t total_rounds, uint64_t total_tiles, const uint32_t *gtab,
                         uint32_t *first_bad, unsigned long long *mism, unsigned long long *diag,
                         hipStream_t stream);
-hipError_t launch_probe_read(const uint8_t *p, uint64_t nbytes, uint32_t *out, int grid, hipStream_t stream);
+hipError_t launch_probe_read(const uint8_t *p, uint64_t nbytes, uint32_t *out, int grid, int block, int variant,
+                             hipStream_t stream);
 hipError_t launch_generic(int mode, const SegDev *segs, uint32_t nseg, uint64_t total_gtiles,
                           const uint32_t *gtab, uint32_t *first_bad, unsigned long long *mism,
                           hipStream_t stream);
@@ -101,6 +102,8 @@ int env_int(const char *name, int dflt) {
 int g_tile_order = env_int("HDFS_CRC32C_TILE_ORDER", 1);
 // Data-stream load policy of the tiled kernel: 0 default, 1 nontemporal.
 int g_nt_loads = env_int("HDFS_CRC32C_NT", 1);
+// Rounds in flight per wave + 1 (register buffers of the tiled kernel): 3 or 4.
+int g_depth = env_int("HDFS_CRC32C_DEPTH", 3);
 // Diagnostic per-wave timestamps (device buffer, 3 x u64 per wave) or null.
 unsigned long long *g_diag = nullptr;
 
@@ -246,7 +249,7 @@ int launch_all(DevCtx &c, int mode, const SegDev *d_segs, uint32_t nseg, uint64_
     uint64_t want = (rounds + 63) / 64;
     int grid = static_cast<int>(want < 1 ? 1 : (want > uint64_t(c.num_cu) ? c.num_cu : want));
     if (ev0) HIPCHK(hipEventRecord(ev0, st));
-    HIPCHK(launch_tiles(mode, g_tile_order, g_nt_loads, grid, d_segs, nseg, rounds, mtiles,
+    HIPCHK(launch_tiles(mode, g_tile_order, g_nt_loads, g_depth, grid, d_segs, nseg, rounds, mtiles,
                         c.d_tab_main, d_fb, d_mism, g_diag, st));
     if (ev1) HIPCHK(hipEventRecord(ev1, st));
   }
@@ -885,6 +888,12 @@ int hdfs_crc32c_device_sync(void) {
   return HDFS_CRC32C_OK;
 }
 
+int hdfs_crc32c_set_depth(int depth) {
+  if (depth != 3 && depth != 4) return fail(HDFS_CRC32C_EINVAL, "depth must be 3 or 4");
+  g_depth = depth;
+  return HDFS_CRC32C_OK;
+}
+
 int hdfs_crc32c_set_tuning(int nt_loads, void *diag) {
   g_nt_loads = nt_loads ? 1 : 0;
   g_diag = static_cast<unsigned long long *>(diag);
@@ -894,6 +903,15 @@ int hdfs_crc32c_set_tuning(int nt_loads, void *diag) {
 int hdfs_crc32c_set_tile_order(int order) {
   if (order != 0 && order != 1) return fail(HDFS_CRC32C_EINVAL, "tile order must be 0 or 1");
   g_tile_order = order;
+  return HDFS_CRC32C_OK;
+}
+
+int g_probe_variant = 0, g_probe_grid_per_cu = 2, g_probe_block = 1024;
+
+int hdfs_crc32c_set_probe(int variant, int grid_per_cu, int block) {
+  g_probe_variant = variant;
+  g_probe_grid_per_cu = grid_per_cu > 0 ? grid_per_cu : 2;
+  g_probe_block = block > 0 ? block : 1024;
   return HDFS_CRC32C_OK;
 }
 
@@ -907,10 +925,12 @@ int hdfs_crc32c_probe_read(const void *dptr, uint64_t bytes, void *stream, int i
   hipEvent_t a, b;
   HIPCHK(hipEventCreate(&a));
   HIPCHK(hipEventCreate(&b));
-  HIPCHK(launch_probe_read(static_cast<const uint8_t *>(dptr), bytes, c->d_small, c->num_cu * 2, st));
+  HIPCHK(launch_probe_read(static_cast<const uint8_t *>(dptr), bytes, c->d_small, c->num_cu * g_probe_grid_per_cu,
+                           g_probe_block, g_probe_variant, st));
   HIPCHK(hipEventRecord(a, st));
   for (int i = 0; i < iters; i++)
-    HIPCHK(launch_probe_read(static_cast<const uint8_t *>(dptr), bytes, c->d_small, c->num_cu * 2, st));
+    HIPCHK(launch_probe_read(static_cast<const uint8_t *>(dptr), bytes, c->d_small, c->num_cu * g_probe_grid_per_cu,
+                           g_probe_block, g_probe_variant, st));
   HIPCHK(hipEventRecord(b, st));
   HIPCHK(hipEventSynchronize(b));
   float ms = 0;

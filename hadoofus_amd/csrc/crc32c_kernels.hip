@@ -7,9 +7,11 @@
 //
 // Tiled kernel, per wave and per ROUND (4 KiB = 512 B of each of 8 chunks):
 //   1. four fully coalesced global_load_dwordx4 (1 KiB each); lane L of
-//      load k holds 16-B piece p = 64k + L of the round;
-//   2. a 4x4 in-register transpose (two DPP quad_perm exchanges) leaves each
-//      lane with 64 CONTIGUOUS bytes (quad q = 16*(L&3) + (L>>2));
+//      load k holds 16-B piece p = 64k + 4*(L&15) + (L>>4) of the round
+//      (a lane permutation inside each contiguous 1 KiB);
+//   2. an in-register transpose of two v_permlane16_swap / v_permlane32_swap
+//      stages (register bit <-> lane bit 4, then 5) leaves lane L with the
+//      64 CONTIGUOUS bytes of quad L (chunk L>>3, position L&7);
 //   3. 16 serial slicing-by-4 steps; every table read is one v_perm_b32 (the
 //      byte goes straight into the LDS address) + one conflict-free ds_read:
 //      the tables are replicated 32x so lane l always hits bank l;
@@ -59,12 +61,16 @@ DEV uint32_t swizzle(uint32_t v) {
 // t_{3-j}; v_perm_b32 drops byte j into bits [15:8] of the lane's base
 // address (entry stride 256 B, lane stride 4 B, byte 2 selects the 64 KiB
 // table pair), so each lookup costs one VALU op and one ds_read_b32.
-DEV uint32_t slice4(const uint32_t *lds, uint32_t x, uint32_t lb0, uint32_t lb1) {
+DEV uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); }
+
+// The step also folds in the NEXT data word: returns t0^t1^t2^t3^next with
+// two v_bitop3_b32 (3-input XOR), so a step is 4 v_perm + 2 VALU + 4 ds_read.
+DEV uint32_t slice4(const uint32_t *lds, uint32_t x, uint32_t next, uint32_t lb0, uint32_t lb1) {
   const uint32_t a0 = __builtin_amdgcn_perm(x, lb0, 0x0C020400u);
   const uint32_t a1 = __builtin_amdgcn_perm(x, lb0, 0x0C020500u);
   const uint32_t a2 = __builtin_amdgcn_perm(x, lb1, 0x0C020600u);
   const uint32_t a3 = __builtin_amdgcn_perm(x, lb1, 0x0C020700u);
-  return lds_at(lds, a0) ^ lds_at(lds, a1 + 128u) ^ lds_at(lds, a2) ^ lds_at(lds, a3 + 128u);
+  return xor3(xor3(lds_at(lds, a0), lds_at(lds, a1 + 128u), lds_at(lds, a2)), lds_at(lds, a3 + 128u), next);
 }
 
 // Apply a zero-byte operator stored as 4 x 256 byte tables at word `base`.
@@ -74,18 +80,28 @@ DEV uint32_t zshift(const uint32_t *lds, uint32_t base, uint32_t x) {
          t[768u + (x >> 24)];
 }
 
-// Exchange register-index bit with lane bit (0: partner = lane^1, 1: lane^2).
-template <int CTRL, int STRIDE>
-DEV void exchange(uint32_t (&d)[16], bool hi) {
+// In-register 4x4 transpose of a round: register bit 0 <-> lane bit 4
+// (v_permlane16_swap: odd 16-lane rows of one register trade places with
+// even rows of the other), then register bit 1 <-> lane bit 5
+// (v_permlane32_swap: upper 32 lanes of one with lower 32 of the other).
+// One instruction moves two registers: 16 per round for 16 dwords.
+DEV void transpose(uint32_t (&d)[16]) {
 #pragma unroll
-  for (int k = 0; k < 4; k++) {
-    if (k & STRIDE) continue;
+  for (int c = 0; c < 4; c++) {
 #pragma unroll
-    for (int c = 0; c < 4; c++) {
-      const uint32_t a = d[k * 4 + c], b = d[(k + STRIDE) * 4 + c];
-      const uint32_t pa = dpp<CTRL>(a), pb = dpp<CTRL>(b);
-      d[k * 4 + c] = hi ? pb : a;
-      d[(k + STRIDE) * 4 + c] = hi ? b : pa;
+    for (int k = 0; k < 4; k += 2) {
+      const auto r = __builtin_amdgcn_permlane16_swap(d[k * 4 + c], d[(k + 1) * 4 + c], false, false);
+      d[k * 4 + c] = r[0];
+      d[(k + 1) * 4 + c] = r[1];
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      const auto r = __builtin_amdgcn_permlane32_swap(d[k * 4 + c], d[(k + 2) * 4 + c], false, false);
+      d[k * 4 + c] = r[0];
+      d[(k + 2) * 4 + c] = r[1];
     }
   }
 }
@@ -180,20 +196,21 @@ DEV uint64_t tile_at_round(SegP segs, uint32_t nseg, uint64_t r, uint64_t total_
 }
 
 // Issue the loads of one round: four fully coalesced 1 KiB dwordx4 loads
-// (lanes 0-31 / 32-63 cover sub-chunks 2k / 2k+1) plus, in verify mode, the
+// (lanes with bit 3 clear / set cover sub-chunks 2k / 2k+1, in the permuted
+// lane order the permlane transpose expects) plus, in verify mode, the
 // expected CRC of the lane's chunk.  Unconditional (addresses clamped into
 // the tile) so the vector-memory count is static and the compiler's
 // s_waitcnt vmcnt(N) for the round being processed stays counted.
 template <int MODE, int NT>
-DEV void issue(uint32_t (&d)[16], uint32_t &exp, const Cursor c, SegP segs, uint32_t half, uint32_t l31,
+DEV void issue(uint32_t (&d)[16], uint32_t &exp, const Cursor c, SegP segs, uint32_t hsel, uint32_t loff,
                uint32_t qg) {
   const uint32_t cs = segs[c.seg].chunk_size;
   const uint32_t last = min(kTileChunks, segs[c.seg].nchunks - c.tile * kTileChunks) - 1u;
   const uint8_t *p = segs[c.seg].data + static_cast<uint64_t>(c.tile) * kTileChunks * cs +
-                     static_cast<uint64_t>(c.r) * kRoundBytes + 16u * l31;
+                     static_cast<uint64_t>(c.r) * kRoundBytes + loff;
 #pragma unroll
   for (int k = 0; k < 4; k++) {
-    const uint32_t g = min(2u * k + half, last);
+    const uint32_t g = min(2u * k + hsel, last);
     const u32x4 v = NT ? gload16_nt(p + static_cast<uint64_t>(g) * cs) : gload16(p + static_cast<uint64_t>(g) * cs);
     d[4 * k + 0] = v.x;
     d[4 * k + 1] = v.y;
@@ -204,8 +221,7 @@ DEV void issue(uint32_t (&d)[16], uint32_t &exp, const Cursor c, SegP segs, uint
 }
 
 struct LaneConst {
-  uint32_t lane, half, l31, lb0, lb1, qi, qg, zk, zbase, z448;
-  bool b0, b1;
+  uint32_t lane, hsel, loff, lb0, lb1, qi, qg, zk, zbase, z448;
 };
 
 // Process one round held in d[] for cursor c; st is the lane's running
@@ -213,42 +229,56 @@ struct LaneConst {
 template <int MODE>
 DEV void process(const uint32_t *lds, uint32_t (&d)[16], uint32_t exp, const Cursor c, SegP segs, uint32_t &st,
                  const LaneConst &L, uint32_t *__restrict__ first_bad, unsigned long long *__restrict__ mism) {
-  exchange<0xB1, 1>(d, L.b0);  // quad_perm [1,0,3,2]: register bit 0 <-> lane bit 0
-  exchange<0x4E, 2>(d, L.b1);  // quad_perm [2,3,0,1]: register bit 1 <-> lane bit 1
+  transpose(d);
   if (c.r == 0) st = (L.qi == 0) ? segs[c.seg].reg_init : 0u;
   else st = zshift(lds, L.z448, st);
+  uint32_t x = st ^ d[0];
 #pragma unroll
-  for (int w = 0; w < 16; w++) st = slice4(lds, st ^ d[w], L.lb0, L.lb1);
-  if (c.r + 1 != segs[c.seg].chunk_size / kRoundBytes) return;
-
+  for (int w = 0; w < 15; w++) x = slice4(lds, x, d[w + 1], L.lb0, L.lb1);
+  st = slice4(lds, x, 0u, L.lb0, L.lb1);
+  // Finalize only after a tile's last round; the finalize itself issues no
+  // vector-memory op (LDS and swizzles only).  The result store below runs
+  // every round, by every lane, through a bounds-checked buffer descriptor:
+  // its size is 0 unless this is a valid last round, and lanes that must not
+  // write get an out-of-range offset, so the hardware drops them.  Every
+  // round therefore issues exactly the same vector-memory ops (4 loads,
+  // [1 expected-CRC load], 1 store) and the compiler's vmcnt waits stay exact.
+  const bool last = c.valid && (c.r + 1 == segs[c.seg].chunk_size / kRoundBytes);
   const uint32_t flags = segs[c.seg].flags;
   const uint32_t nch = min(kTileChunks, segs[c.seg].nchunks - c.tile * kTileChunks);
-  uint32_t v = L.zk ? zshift(lds, L.zbase, st) : st;
-  v ^= swizzle<0x101F>(v);  // xor lane 4
-  v ^= swizzle<0x201F>(v);  // xor lane 8
-  v ^= swizzle<0x401F>(v);  // xor lane 16
-  const uint32_t out = (flags & kSegRaw) ? v : ~v;
-  const bool leader = (L.qi == 0) && (L.qg < nch);
-  const uint32_t chunk = c.tile * kTileChunks + L.qg;
-  if (MODE == kModeCompute) {
-    if (leader) gstore32(segs[c.seg].crcs + chunk, (flags & kSegBigEndian) ? __builtin_bswap32(out) : out);
-  } else {
-    const uint32_t e = (flags & kSegBigEndian) ? __builtin_bswap32(exp) : exp;
-    const uint64_t m = __ballot(leader && e != out);
-    if (L.lane == 0) {
-      uint32_t byte = 0;
+  const bool leader = last && (L.qi == 0) && (L.qg < nch);
+  uint32_t out = 0, byte = 0;
+  if (last) {
+    uint32_t v = L.zk ? zshift(lds, L.zbase, st) : st;
+    v ^= swizzle<0x041F>(v);  // xor lane 1
+    v ^= swizzle<0x081F>(v);  // xor lane 2
+    v ^= swizzle<0x101F>(v);  // xor lane 4
+    out = (flags & kSegRaw) ? v : ~v;
+    if (MODE == kModeVerify) {
+      const uint32_t e = (flags & kSegBigEndian) ? __builtin_bswap32(exp) : exp;
+      const uint64_t m = __ballot(leader && e != out);
 #pragma unroll
-      for (int g = 0; g < 8; g++) byte |= static_cast<uint32_t>((m >> ((g >> 1) | ((g & 1) << 5))) & 1u) << g;
-      gstore8(segs[c.seg].bitmap + c.tile, static_cast<uint8_t>(byte));
-      if (byte) {
-        atomicMin(&first_bad[c.seg], c.tile * kTileChunks + __builtin_ctz(byte));
-        atomicAdd(mism, static_cast<unsigned long long>(__builtin_popcount(byte)));
-      }
+      for (int g = 0; g < 8; g++) byte |= static_cast<uint32_t>((m >> (8 * g)) & 1u) << g;
+    }
+  }
+  byte = rfl(byte);
+  if (MODE == kModeCompute) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        segs[c.seg].crcs + c.tile * kTileChunks, 0, last ? static_cast<int>(nch * 4u) : 0, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b32((flags & kSegBigEndian) ? __builtin_bswap32(out) : out, rs,
+                                          leader ? L.qg * 4u : 0x80000000u, 0, 0);
+  } else {
+    const __amdgpu_buffer_rsrc_t rb =
+        __builtin_amdgcn_make_buffer_rsrc(segs[c.seg].bitmap + c.tile, 0, last ? 1 : 0, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(byte), rb, L.lane == 0 ? 0u : 0x80000000u, 0, 0);
+    if (byte && L.lane == 0) {  // rare: only tiles with a mismatch
+      atomicMin(&first_bad[c.seg], c.tile * kTileChunks + __builtin_ctz(byte));
+      atomicAdd(mism, static_cast<unsigned long long>(__builtin_popcount(byte)));
     }
   }
 }
 
-template <int MODE, int ORDER, int NT>
+template <int MODE, int ORDER, int NT, int DEPTH>
 __global__ __launch_bounds__(1024) void crc32c_tiles_kernel(
     const SegDev *__restrict__ segs, uint32_t nseg, uint64_t total_rounds, uint64_t total_tiles,
     const uint32_t *__restrict__ gtab, uint32_t *__restrict__ first_bad,
@@ -267,17 +297,15 @@ __global__ __launch_bounds__(1024) void crc32c_tiles_kernel(
 
   LaneConst L;
   L.lane = threadIdx.x & 63u;
-  L.half = L.lane >> 5;
-  L.l31 = L.lane & 31u;
-  L.lb0 = L.l31 * 4u;
-  L.lb1 = 65536u + L.l31 * 4u;
-  L.qi = (L.lane >> 2) & 7u;             // 64-B position within the chunk's 512-B round
-  L.qg = 2u * (L.lane & 3u) + L.half;    // chunk within the tile after the transpose
+  L.hsel = (L.lane >> 3) & 1u;                              // load: odd sub-chunk of each 1 KiB
+  L.loff = 16u * (4u * (L.lane & 7u) + (L.lane >> 4));      // load: byte offset in the sub-chunk
+  L.lb0 = (L.lane & 31u) * 4u;
+  L.lb1 = 65536u + (L.lane & 31u) * 4u;
+  L.qi = L.lane & 7u;                    // 64-B position within the chunk's 512-B round
+  L.qg = L.lane >> 3;                    // chunk within the tile after the transpose
   L.zk = 7u - L.qi;
   L.zbase = kLdsSliceBytes / 4 + (L.zk ? L.zk - 1u : 0u) * 1024u;
   L.z448 = kLdsSliceBytes / 4 + 6u * 1024u;
-  L.b0 = L.lane & 1u;
-  L.b1 = L.lane & 2u;
 
   const uint32_t wpb = blockDim.x >> 6;
   const uint32_t wave = rfl(blockIdx.x * wpb + (threadIdx.x >> 6));
@@ -325,33 +353,68 @@ __global__ __launch_bounds__(1024) void crc32c_tiles_kernel(
     return;
   }
 
-  // Three round buffers in rotation: while one round is processed the next
-  // two are in flight (12 KiB per wave, 192 KiB per CU at 16 waves).
-  uint32_t A[16], B[16], C[16];
-  uint32_t eA = 0, eB = 0, eC = 0, st = 0;
-  Cursor c1 = advance<ORDER>(c0, sg, nseg, w);
-  Cursor c2 = advance<ORDER>(c1, sg, nseg, w);
-  issue<MODE, NT>(A, eA, c0, sg, L.half, L.l31, L.qg);
-  issue<MODE, NT>(B, eB, c1, sg, L.half, L.l31, L.qg);
-  issue<MODE, NT>(C, eC, c2, sg, L.half, L.l31, L.qg);
-  // One exit test per iteration (after all three issues): a structured CFG
-  // keeps the vmcnt bookkeeping exact (every path issues the same loads in
-  // the same order); c0 is always valid at the top of an iteration.
-  for (;;) {
-    process<MODE>(lds, A, eA, c0, sg, st, L, first_bad, mism);
-    const Cursor c3 = advance<ORDER>(c2, sg, nseg, w);
-    issue<MODE, NT>(A, eA, c3, sg, L.half, L.l31, L.qg);
-    if (c1.valid) process<MODE>(lds, B, eB, c1, sg, st, L, first_bad, mism);
-    const Cursor c4 = advance<ORDER>(c3, sg, nseg, w);
-    issue<MODE, NT>(B, eB, c4, sg, L.half, L.l31, L.qg);
-    if (c2.valid) process<MODE>(lds, C, eC, c2, sg, st, L, first_bad, mism);
-    const Cursor c5 = advance<ORDER>(c4, sg, nseg, w);
-    issue<MODE, NT>(C, eC, c5, sg, L.half, L.l31, L.qg);
-    nrounds += 1u + (c1.valid ? 1u : 0u) + (c2.valid ? 1u : 0u);
-    if (!c3.valid) break;
-    c0 = c3;
-    c1 = c4;
-    c2 = c5;
+  // DEPTH round buffers in rotation: while one round is processed the next
+  // DEPTH-1 are in flight (DEPTH 4: 16 KiB per wave, 256 KiB per CU).
+  // One exit test per iteration (after all issues) and no memory op under a
+  // condition: every path issues the same vector-memory ops in the same
+  // order, so the vmcnt bookkeeping stays exact.  c0 is always valid at the
+  // top of an iteration; rounds of an exhausted cursor are processed with
+  // their stores dropped.
+  uint32_t st = 0;
+  if constexpr (DEPTH == 3) {
+    uint32_t A[16], B[16], C[16];
+    uint32_t eA = 0, eB = 0, eC = 0;
+    Cursor c1 = advance<ORDER>(c0, sg, nseg, w);
+    Cursor c2 = advance<ORDER>(c1, sg, nseg, w);
+    issue<MODE, NT>(A, eA, c0, sg, L.hsel, L.loff, L.qg);
+    issue<MODE, NT>(B, eB, c1, sg, L.hsel, L.loff, L.qg);
+    issue<MODE, NT>(C, eC, c2, sg, L.hsel, L.loff, L.qg);
+    for (;;) {
+      process<MODE>(lds, A, eA, c0, sg, st, L, first_bad, mism);
+      const Cursor c3 = advance<ORDER>(c2, sg, nseg, w);
+      issue<MODE, NT>(A, eA, c3, sg, L.hsel, L.loff, L.qg);
+      process<MODE>(lds, B, eB, c1, sg, st, L, first_bad, mism);  // no-op store if c1 is exhausted
+      const Cursor c4 = advance<ORDER>(c3, sg, nseg, w);
+      issue<MODE, NT>(B, eB, c4, sg, L.hsel, L.loff, L.qg);
+      process<MODE>(lds, C, eC, c2, sg, st, L, first_bad, mism);
+      const Cursor c5 = advance<ORDER>(c4, sg, nseg, w);
+      issue<MODE, NT>(C, eC, c5, sg, L.hsel, L.loff, L.qg);
+      nrounds += 1u + (c1.valid ? 1u : 0u) + (c2.valid ? 1u : 0u);
+      if (!c3.valid) break;
+      c0 = c3;
+      c1 = c4;
+      c2 = c5;
+    }
+  } else {
+    uint32_t A[16], B[16], C[16], D[16];
+    uint32_t eA = 0, eB = 0, eC = 0, eD = 0;
+    Cursor c1 = advance<ORDER>(c0, sg, nseg, w);
+    Cursor c2 = advance<ORDER>(c1, sg, nseg, w);
+    Cursor c3 = advance<ORDER>(c2, sg, nseg, w);
+    issue<MODE, NT>(A, eA, c0, sg, L.hsel, L.loff, L.qg);
+    issue<MODE, NT>(B, eB, c1, sg, L.hsel, L.loff, L.qg);
+    issue<MODE, NT>(C, eC, c2, sg, L.hsel, L.loff, L.qg);
+    issue<MODE, NT>(D, eD, c3, sg, L.hsel, L.loff, L.qg);
+    for (;;) {
+      process<MODE>(lds, A, eA, c0, sg, st, L, first_bad, mism);
+      const Cursor c4 = advance<ORDER>(c3, sg, nseg, w);
+      issue<MODE, NT>(A, eA, c4, sg, L.hsel, L.loff, L.qg);
+      process<MODE>(lds, B, eB, c1, sg, st, L, first_bad, mism);
+      const Cursor c5 = advance<ORDER>(c4, sg, nseg, w);
+      issue<MODE, NT>(B, eB, c5, sg, L.hsel, L.loff, L.qg);
+      process<MODE>(lds, C, eC, c2, sg, st, L, first_bad, mism);
+      const Cursor c6 = advance<ORDER>(c5, sg, nseg, w);
+      issue<MODE, NT>(C, eC, c6, sg, L.hsel, L.loff, L.qg);
+      process<MODE>(lds, D, eD, c3, sg, st, L, first_bad, mism);
+      const Cursor c7 = advance<ORDER>(c6, sg, nseg, w);
+      issue<MODE, NT>(D, eD, c7, sg, L.hsel, L.loff, L.qg);
+      nrounds += 1u + (c1.valid ? 1u : 0u) + (c2.valid ? 1u : 0u) + (c3.valid ? 1u : 0u);
+      if (!c4.valid) break;
+      c0 = c4;
+      c1 = c5;
+      c2 = c6;
+      c3 = c7;
+    }
   }
   if (diag && L.lane == 0) {
     diag[3 * wave + 1] = __builtin_amdgcn_s_memrealtime();
@@ -506,45 +569,93 @@ __global__ __launch_bounds__(256) void corrupt_kernel(uint8_t *__restrict__ data
 // ---------------------------------------------------------------------------
 // Host-side launchers (used by crc32c_engine.cpp).
 // ---------------------------------------------------------------------------
-hipError_t launch_tiles(int mode, int order, int nt, int grid, const SegDev *segs, uint32_t nseg,
+hipError_t launch_tiles(int mode, int order, int nt, int depth, int grid, const SegDev *segs, uint32_t nseg,
                         uint64_t total_rounds, uint64_t total_tiles, const uint32_t *gtab,
                         uint32_t *first_bad, unsigned long long *mism, unsigned long long *diag,
                         hipStream_t stream) {
-#define HDFS_LAUNCH(M, O, N)                                                                          \
-  hipLaunchKernelGGL((crc32c_tiles_kernel<M, O, N>), dim3(grid), dim3(1024), 0, stream, segs, nseg,  \
+#define HDFS_LAUNCH(M, O, N, D)                                                                        \
+  hipLaunchKernelGGL((crc32c_tiles_kernel<M, O, N, D>), dim3(grid), dim3(1024), 0, stream, segs, nseg,  \
                      total_rounds, total_tiles, gtab, first_bad, mism, diag)
-#define HDFS_LAUNCH_O(M, N) \
-  do { if (order) HDFS_LAUNCH(M, 1, N); else HDFS_LAUNCH(M, 0, N); } while (0)
-  if (mode == kModeVerify) {
-    if (nt) HDFS_LAUNCH_O(kModeVerify, 1); else HDFS_LAUNCH_O(kModeVerify, 0);
-  } else {
-    if (nt) HDFS_LAUNCH_O(kModeCompute, 1); else HDFS_LAUNCH_O(kModeCompute, 0);
-  }
-#undef HDFS_LAUNCH_O
+#define HDFS_LAUNCH_M(M)                                                   \
+  do {                                                                     \
+    if (depth == 4) HDFS_LAUNCH(M, 1, 1, 4);                               \
+    else if (order && nt) HDFS_LAUNCH(M, 1, 1, 3);                         \
+    else if (order) HDFS_LAUNCH(M, 1, 0, 3);                               \
+    else if (nt) HDFS_LAUNCH(M, 0, 1, 3);                                  \
+    else HDFS_LAUNCH(M, 0, 0, 3);                                          \
+  } while (0)
+  if (mode == kModeVerify) HDFS_LAUNCH_M(kModeVerify);
+  else HDFS_LAUNCH_M(kModeCompute);
+#undef HDFS_LAUNCH_M
 #undef HDFS_LAUNCH
   return hipGetLastError();
 }
 
-// Streaming-read probe: the empirical HBM read roofline for this access
-// width (16 B per lane, fully coalesced, 4 loads in flight per lane).
+// Streaming-read probe: the empirical HBM read roofline for 16-B-per-lane
+// fully coalesced loads, no compute.  NLOAD loads in flight per lane, NT =
+// nontemporal policy.
+template <int NLOAD, int NT, int PERM = 0>
 __global__ __launch_bounds__(1024) void probe_read_kernel(const uint8_t *__restrict__ p, uint64_t nbytes,
                                                           uint32_t *__restrict__ out) {
   const uint64_t n16 = nbytes / 16;
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
-  uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  // PERM: lanes of a wave read the wave's 1 KiB in the permuted order
+  // 4*(lane&15) + (lane>>4) (still one contiguous 1 KiB per instruction).
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t l2 = PERM ? (4u * (lane & 15u) + (lane >> 4)) : lane;
+  uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + (threadIdx.x & ~63u) + l2;
   u32x4 acc = {0u, 0u, 0u, 0u};
-  for (; i + 3 * stride < n16; i += 4 * stride) {
-    const u32x4 a = gload16(p + 16 * i), b = gload16(p + 16 * (i + stride));
-    const u32x4 c = gload16(p + 16 * (i + 2 * stride)), d = gload16(p + 16 * (i + 3 * stride));
-    acc ^= a ^ b ^ c ^ d;
+  for (; i + (NLOAD - 1) * stride < n16; i += NLOAD * stride) {
+    u32x4 v[NLOAD];
+#pragma unroll
+    for (int k = 0; k < NLOAD; k++) v[k] = NT ? gload16_nt(p + 16 * (i + k * stride)) : gload16(p + 16 * (i + k * stride));
+#pragma unroll
+    for (int k = 0; k < NLOAD; k++) acc ^= v[k];
   }
   for (; i < n16; i += stride) acc ^= gload16(p + 16 * i);
   const uint32_t v = acc.x ^ acc.y ^ acc.z ^ acc.w;
   if (v == 0x9E3779B9u) out[0] = v;  // keeps the loads live; practically never stores
 }
 
-hipError_t launch_probe_read(const uint8_t *p, uint64_t nbytes, uint32_t *out, int grid, hipStream_t stream) {
-  hipLaunchKernelGGL(probe_read_kernel, dim3(grid), dim3(1024), 0, stream, p, nbytes, out);
+// Same, but each lane reads 64 CONTIGUOUS bytes per quad (4 loads at +0/16/
+// 32/48): per instruction the wave touches a 4 KiB span with a 64-B lane
+// stride.  NQUAD quads in flight per lane.
+template <int NQUAD>
+__global__ __launch_bounds__(1024) void probe_quad_kernel(const uint8_t *__restrict__ p, uint64_t nbytes,
+                                                          uint32_t *__restrict__ out) {
+  const uint64_t n64 = nbytes / 64;
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  u32x4 acc = {0u, 0u, 0u, 0u};
+  for (; i + (NQUAD - 1) * stride < n64; i += NQUAD * stride) {
+    u32x4 v[NQUAD][4];
+#pragma unroll
+    for (int m = 0; m < NQUAD; m++)
+#pragma unroll
+      for (int k = 0; k < 4; k++) v[m][k] = gload16_nt(p + 64 * (i + m * stride) + 16 * k);
+#pragma unroll
+    for (int m = 0; m < NQUAD; m++)
+#pragma unroll
+      for (int k = 0; k < 4; k++) acc ^= v[m][k];
+  }
+  const uint32_t v = acc.x ^ acc.y ^ acc.z ^ acc.w;
+  if (v == 0x9E3779B9u) out[0] = v;
+}
+
+hipError_t launch_probe_read(const uint8_t *p, uint64_t nbytes, uint32_t *out, int grid, int block, int variant,
+                             hipStream_t stream) {
+  switch (variant) {
+    case 1: hipLaunchKernelGGL((probe_read_kernel<4, 1>), dim3(grid), dim3(block), 0, stream, p, nbytes, out); break;
+    case 2: hipLaunchKernelGGL((probe_read_kernel<8, 0>), dim3(grid), dim3(block), 0, stream, p, nbytes, out); break;
+    case 3: hipLaunchKernelGGL((probe_read_kernel<8, 1>), dim3(grid), dim3(block), 0, stream, p, nbytes, out); break;
+    case 4: hipLaunchKernelGGL((probe_read_kernel<16, 1>), dim3(grid), dim3(block), 0, stream, p, nbytes, out); break;
+    case 5: hipLaunchKernelGGL((probe_quad_kernel<1>), dim3(grid), dim3(block), 0, stream, p, nbytes, out); break;
+    case 6: hipLaunchKernelGGL((probe_quad_kernel<2>), dim3(grid), dim3(block), 0, stream, p, nbytes, out); break;
+    case 7: hipLaunchKernelGGL((probe_quad_kernel<4>), dim3(grid), dim3(block), 0, stream, p, nbytes, out); break;
+    case 8: hipLaunchKernelGGL((probe_read_kernel<16, 1, 1>), dim3(grid), dim3(block), 0, stream, p, nbytes, out); break;
+    case 9: hipLaunchKernelGGL((probe_read_kernel<4, 1, 1>), dim3(grid), dim3(block), 0, stream, p, nbytes, out); break;
+    default: hipLaunchKernelGGL((probe_read_kernel<4, 0>), dim3(grid), dim3(block), 0, stream, p, nbytes, out);
+  }
   return hipGetLastError();
 }
 

@@ -164,9 +164,15 @@ int hdfs_crc32c_set_tile_order(int order);
  * (env HDFS_CRC32C_NT); diag = device u64[3 * waves] receiving per-wave
  * start/end s_memrealtime stamps and rounds processed (NULL = off). */
 int hdfs_crc32c_set_tuning(int nt_loads, void *diag);
+/* Register round buffers per wave of the tiled kernel (3 or 4; depth-1
+ * rounds stay in flight while one is processed).  Env HDFS_CRC32C_DEPTH. */
+int hdfs_crc32c_set_depth(int depth);
 /* Empirical streaming-read bandwidth of `bytes` at dptr (GB/s, 1e9 B/s):
  * fully coalesced 16-B-per-lane loads, no compute; the measured roofline. */
 int hdfs_crc32c_probe_read(const void *dptr, uint64_t bytes, void *stream, int iters, double *gbps);
+/* Probe shape (diagnostics): variant 0..4 = {4 loads, 4 nt, 8, 8 nt, 16 nt}
+ * in flight per lane; grid = grid_per_cu x CUs blocks of `block` threads. */
+int hdfs_crc32c_set_probe(int variant, int grid_per_cu, int block);
 
 #ifdef __cplusplus
 }
