@@ -100,6 +100,7 @@ def load(path=LIB_PATH):
     _bind(lib, "hdfs_crc32c_set_tuning", _int, [_int, _vp])
     _bind(lib, "hdfs_crc32c_set_probe", _int, [_int, _int, _int])
     _bind(lib, "hdfs_crc32c_set_depth", _int, [_int])
+    _bind(lib, "hdfs_crc32c_set_store_policy", _int, [_int])
     _bind(lib, "hdfs_crc32c_compute_host", _int, [_vp, _u64, _u32, _u32, _u32, _vp, _u64])
     _bind(lib, "hdfs_crc32c_verify_host", _int,
           [_vp, _u64, _u32, _u32, _u32, _vp, _vp, _u64, ctypes.POINTER(_u64), ctypes.POINTER(_u64)])
@@ -342,3 +343,7 @@ def set_probe(variant=0, grid_per_cu=2, block=1024):
 
 def set_depth(depth):
     _check(load().hdfs_crc32c_set_depth(depth))
+
+
+def set_store_policy(policy):
+    _check(load().hdfs_crc32c_set_store_policy(policy))

@@ -26,7 +26,7 @@ namespace hdfs_crc32c {
 hipError_t launch_tiles(int mode, int order, int nt, int depth, int grid, const SegDev *segs, uint32_t nseg,
                         uint64_t total_rounds, uint64_t total_tiles, const uint32_t *gtab,
                         uint32_t *first_bad, unsigned long long *mism, unsigned long long *diag,
-                        hipStream_t stream);
+                        uint32_t store_policy, uint32_t *gctr, hipStream_t stream);
 hipError_t launch_probe_read(const uint8_t *p, uint64_t nbytes, uint32_t *out, int grid, int block, int variant,
                              hipStream_t stream);
 hipError_t launch_generic(int mode, const SegDev *segs, uint32_t nseg, uint64_t total_gtiles,
@@ -87,6 +87,7 @@ struct DevCtx {
   size_t p_chunk_cap = 0;  // chunks per CRC slot
   SegDev *p_segs = nullptr;
   uint32_t *p_fb = nullptr;
+  uint32_t *p_gctr = nullptr;  // [2], one per slot
   unsigned long long *p_mism = nullptr;
   size_t p_npieces_cap = 0;
   std::mutex mu;
@@ -99,11 +100,14 @@ int env_int(const char *name, int dflt) {
   const char *e = std::getenv(name);
   return e ? std::atoi(e) : dflt;
 }
-int g_tile_order = env_int("HDFS_CRC32C_TILE_ORDER", 1);
+int g_tile_order = env_int("HDFS_CRC32C_TILE_ORDER", 2);
 // Data-stream load policy of the tiled kernel: 0 default, 1 nontemporal.
 int g_nt_loads = env_int("HDFS_CRC32C_NT", 1);
 // Rounds in flight per wave + 1 (register buffers of the tiled kernel): 3 or 4.
 int g_depth = env_int("HDFS_CRC32C_DEPTH", 3);
+// Result-store policy of the tiled kernel: 0 default, 1 nontemporal,
+// 2 diagnostic only (drops the compute-mode CRC stores).
+uint32_t g_store_policy = uint32_t(env_int("HDFS_CRC32C_STORE", 0));
 // Diagnostic per-wave timestamps (device buffer, 3 x u64 per wave) or null.
 unsigned long long *g_diag = nullptr;
 
@@ -173,7 +177,7 @@ int ctx_init(int device, DevCtx **out) {
   HIPCHK(hipHostMalloc(&c.h_stage, kStageCap, hipHostMallocDefault));
   HIPCHK(hipMalloc(&c.d_stage, kStageCap));
   HIPCHK(hipMalloc(&c.d_seg, sizeof(SegDev)));
-  HIPCHK(hipMalloc(&c.d_small, 64));
+  HIPCHK(hipMalloc(&c.d_small, 64));  // [0] acc [1] first_bad [2..3] mism [8] pool counter
   c.ready = true;
   *out = &c;
   return HDFS_CRC32C_OK;
@@ -238,7 +242,8 @@ bool device_accessible(const void *p) {
 
 int launch_all(DevCtx &c, int mode, const SegDev *d_segs, uint32_t nseg, uint64_t rounds,
                uint64_t mtiles, uint64_t gtiles, uint32_t *d_fb, unsigned long long *d_mism,
-               hipStream_t st, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, bool reset = true) {
+               uint32_t *d_gctr, hipStream_t st, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr,
+               bool reset = true) {
   if (mode == kModeVerify && reset) {
     HIPCHK(hipMemsetAsync(d_fb, 0xFF, sizeof(uint32_t) * (nseg ? nseg : 1), st));
     HIPCHK(hipMemsetAsync(d_mism, 0, sizeof(unsigned long long), st));
@@ -248,9 +253,10 @@ int launch_all(DevCtx &c, int mode, const SegDev *d_segs, uint32_t nseg, uint64_
     // block pays a ~156 KiB LDS table fill.
     uint64_t want = (rounds + 63) / 64;
     int grid = static_cast<int>(want < 1 ? 1 : (want > uint64_t(c.num_cu) ? c.num_cu : want));
+    if (g_tile_order == 2) HIPCHK(hipMemsetAsync(d_gctr, 0, sizeof(uint32_t), st));
     if (ev0) HIPCHK(hipEventRecord(ev0, st));
     HIPCHK(launch_tiles(mode, g_tile_order, g_nt_loads, g_depth, grid, d_segs, nseg, rounds, mtiles,
-                        c.d_tab_main, d_fb, d_mism, g_diag, st));
+                        c.d_tab_main, d_fb, d_mism, g_diag, g_store_policy, d_gctr, st));
     if (ev1) HIPCHK(hipEventRecord(ev1, st));
   }
   if (gtiles) HIPCHK(launch_generic(mode, d_segs, nseg, gtiles, c.d_tab_main, d_fb, d_mism, st));
@@ -279,7 +285,7 @@ int stream_crc_locked(DevCtx &c, uint32_t crc, const void *dbuf, uint64_t len, u
   uint64_t rounds = 0, gtiles = 0, mtiles = 0;
   classify(s, rounds, gtiles, mtiles);
   HIPCHK(hipMemcpyAsync(c.d_seg, &s, sizeof(s), hipMemcpyHostToDevice, c.stream));
-  rc = launch_all(c, kModeCompute, c.d_seg, 1, rounds, mtiles, gtiles, nullptr, nullptr, c.stream);
+  rc = launch_all(c, kModeCompute, c.d_seg, 1, rounds, mtiles, gtiles, nullptr, nullptr, c.d_small + 8, c.stream);
   if (rc) return rc;
   HIPCHK(hipMemsetAsync(c.d_small, 0, 4, c.stream));
   HIPCHK(launch_combine(c.d_raw, nraw, kStreamPiece, len, c.d_tab_pow2, ~crc, c.d_small, c.stream));
@@ -378,6 +384,7 @@ int pipe_reserve(DevCtx &c, size_t piece, uint32_t cs, size_t npieces) {
     HIPCHK(hipMalloc(&c.p_segs, npieces * sizeof(SegDev)));
     HIPCHK(hipMalloc(&c.p_fb, npieces * sizeof(uint32_t)));
     if (!c.p_mism) HIPCHK(hipMalloc(&c.p_mism, sizeof(unsigned long long)));
+    if (!c.p_gctr) HIPCHK(hipMalloc(&c.p_gctr, 64));
     c.p_npieces_cap = npieces;
   }
   return HDFS_CRC32C_OK;
@@ -447,8 +454,8 @@ int host_pipeline(int mode, const uint8_t *data, uint64_t len, uint32_t cs, uint
       HIPCHK(hipMemcpyAsync(c.p_crc[b], hc + c0 * 4, nc * 4, hipMemcpyHostToDevice, c.copy_stream));
     HIPCHK(hipEventRecord(c.ev_copy[b], c.copy_stream));
     HIPCHK(hipStreamWaitEvent(c.comp_stream, c.ev_copy[b], 0));
-    rc = launch_all(c, mode, c.p_segs + i, 1, rounds[i], mt[i], gt[i], c.p_fb + i, c.p_mism, c.comp_stream,
-                    nullptr, nullptr, false);
+    rc = launch_all(c, mode, c.p_segs + i, 1, rounds[i], mt[i], gt[i], c.p_fb + i, c.p_mism, c.p_gctr + b,
+                    c.comp_stream, nullptr, nullptr, false);
     if (rc) return rc;
     if (mode == kModeCompute)
       HIPCHK(hipMemcpyAsync(hc + c0 * 4, c.p_crc[b], nc * 4, hipMemcpyDeviceToHost, c.comp_stream));
@@ -490,6 +497,7 @@ struct hdfs_crc32c_plan {
   SegDev *d_segs = nullptr;
   uint32_t *d_first_bad = nullptr;
   unsigned long long *d_mism = nullptr;
+  uint32_t *d_gctr = nullptr;  // tiled-kernel pool counter (schedule 2)
   uint64_t rounds = 0, mtiles = 0, gtiles = 0, main_bytes = 0, gen_bytes = 0, nchunks = 0;
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> events;  // pre-created pool
@@ -582,6 +590,7 @@ int hdfs_crc32c_plan_create(hdfs_crc32c_plan **plan, int mode, const hdfs_crc32c
   if (e == hipSuccess) e = hipMemcpy(p->d_segs, host.data(), sizeof(SegDev) * host.size(), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMalloc(&p->d_first_bad, sizeof(uint32_t) * host.size());
   if (e == hipSuccess) e = hipMalloc(&p->d_mism, sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMalloc(&p->d_gctr, 64);
   if (e != hipSuccess) {
     hdfs_crc32c_plan_destroy(p);
     return fail(HDFS_CRC32C_ENOMEM, "plan allocation: %s", hipGetErrorString(e));
@@ -608,7 +617,7 @@ int hdfs_crc32c_plan_execute(hdfs_crc32c_plan *p, void *stream) {
     p->next_event++;
   }
   return launch_all(c, p->mode, p->d_segs, p->nseg, p->rounds, p->mtiles, p->gtiles, p->d_first_bad,
-                    p->d_mism, st, e0, e1);
+                    p->d_mism, p->d_gctr, st, e0, e1);
 }
 
 int hdfs_crc32c_plan_results(hdfs_crc32c_plan *p, void *stream, uint32_t *first_bad, size_t nseg,
@@ -684,6 +693,7 @@ void hdfs_crc32c_plan_destroy(hdfs_crc32c_plan *p) {
   if (p->d_segs) (void)hipFree(p->d_segs);
   if (p->d_first_bad) (void)hipFree(p->d_first_bad);
   if (p->d_mism) (void)hipFree(p->d_mism);
+  if (p->d_gctr) (void)hipFree(p->d_gctr);
   delete p;
 }
 
@@ -746,7 +756,7 @@ int hdfs_crc32c_verify_crcdata(const void *crcdata, int32_t chunksize, int32_t c
   HIPCHK(hipMemcpyAsync(c->d_seg, &s, sizeof(s), hipMemcpyHostToDevice, c->stream));
   uint32_t *d_fb = c->d_small + 1;
   auto *d_m = reinterpret_cast<unsigned long long *>(c->d_small + 2);
-  rc = launch_all(*c, kModeVerify, c->d_seg, 1, rounds, mtiles, gtiles, d_fb, d_m, c->stream);
+  rc = launch_all(*c, kModeVerify, c->d_seg, 1, rounds, mtiles, gtiles, d_fb, d_m, c->d_small + 8, c->stream);
   if (rc) return rc;
   uint32_t fb = 0;
   HIPCHK(hipMemcpyAsync(&fb, d_fb, 4, hipMemcpyDeviceToHost, c->stream));
@@ -787,7 +797,7 @@ int hdfs_crc32c_compose_crcs(const void *const *iov_base, const size_t *iov_len,
   uint64_t rounds = 0, gtiles = 0, mtiles = 0;
   classify(s, rounds, gtiles, mtiles);
   HIPCHK(hipMemcpyAsync(c->d_seg, &s, sizeof(s), hipMemcpyHostToDevice, c->stream));
-  rc = launch_all(*c, kModeCompute, c->d_seg, 1, rounds, mtiles, gtiles, nullptr, nullptr, c->stream);
+  rc = launch_all(*c, kModeCompute, c->d_seg, 1, rounds, mtiles, gtiles, nullptr, nullptr, c->d_small + 8, c->stream);
   if (rc) return rc;
   HIPCHK(hipMemcpyAsync(crc_be_out, c->d_stage + off_crc, nch * 4, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
@@ -888,6 +898,12 @@ int hdfs_crc32c_device_sync(void) {
   return HDFS_CRC32C_OK;
 }
 
+int hdfs_crc32c_set_store_policy(int policy) {
+  if (policy < 0 || policy > 3) return fail(HDFS_CRC32C_EINVAL, "store policy 0..3");
+  g_store_policy = uint32_t(policy);
+  return HDFS_CRC32C_OK;
+}
+
 int hdfs_crc32c_set_depth(int depth) {
   if (depth != 3 && depth != 4) return fail(HDFS_CRC32C_EINVAL, "depth must be 3 or 4");
   g_depth = depth;
@@ -901,7 +917,7 @@ int hdfs_crc32c_set_tuning(int nt_loads, void *diag) {
 }
 
 int hdfs_crc32c_set_tile_order(int order) {
-  if (order != 0 && order != 1) return fail(HDFS_CRC32C_EINVAL, "tile order must be 0 or 1");
+  if (order < 0 || order > 2) return fail(HDFS_CRC32C_EINVAL, "tile order must be 0, 1 or 2");
   g_tile_order = order;
   return HDFS_CRC32C_OK;
 }

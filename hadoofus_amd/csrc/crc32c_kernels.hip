@@ -134,18 +134,59 @@ struct Cursor {
 //    split leaves the oldest waves idle for the last ~15 % of the kernel.
 //    The LDS atomic counts in lgkmcnt, never in the vmcnt that orders the
 //    data prefetch.
+//  ORDER 2 (two-phase): as ORDER 1 over the first kPhase1Num/kPhase1Den of
+//    the rounds; the remaining tiles form a global pool of kUnit-tile units
+//    that workgroups claim with one global atomic each once their own slice
+//    is done (published to the workgroup's other waves through an LDS slot).
+//    The pool absorbs the cross-workgroup / cross-XCD speed spread; its
+//    atomics only happen at the end, off the hot loop.
+constexpr uint32_t kUnit = 256;       // tiles per global pool unit
+constexpr uint32_t kSlots = 8;        // LDS slots for published units
+constexpr uint64_t kPhase1Num = 23, kPhase1Den = 25;  // 92 % static
+
 struct Sched {
-  uint64_t r1;      // ORDER 0: end of the wave's round slice
-  uint64_t gfirst;  // ORDER 1: first global tile of the workgroup
-  uint32_t nk;      // ORDER 1: tiles of the workgroup
-  uint32_t *ctr;    // ORDER 1: LDS tile counter
+  uint64_t r1;       // ORDER 0: end of the wave's round slice
+  uint64_t gfirst;   // ORDER 1/2: first global tile of the workgroup's slice
+  uint32_t nk;       // ORDER 1/2: tiles of the workgroup's slice
+  uint32_t *ctr;     // ORDER 1/2: LDS ticket counter
   uint32_t lane;
+  uint64_t p2first;  // ORDER 2: first global tile of the pool
+  uint64_t ntiles;   // ORDER 2: total tiles
+  uint32_t *gctr;    // ORDER 2: global unit counter (zeroed per launch)
+  uint64_t *slots;   // ORDER 2: LDS [kSlots] of (unit + 1) << 32 | global unit
 };
 
 DEV uint32_t grab(const Sched &w) {
   uint32_t k = 0;
   if (w.lane == 0) k = atomicAdd(w.ctr, 1u);
   return rfl(k);
+}
+
+// Ticket -> global tile.  Tickets below nk are the workgroup's own slice;
+// later tickets walk the pool unit by unit.
+template <int ORDER>
+DEV bool ticket_tile(const Sched &w, uint32_t t, uint64_t &g) {
+  if (t < w.nk) {
+    g = w.gfirst + t;
+    return true;
+  }
+  if (ORDER != 2) return false;
+  const uint32_t j = t - w.nk, u = j / kUnit, o = j % kUnit, s = u % kSlots;
+  if (o == 0) {  // first ticket of local unit u: claim a pool unit and publish it
+    uint32_t gu = 0;
+    if (w.lane == 0) gu = atomicAdd(w.gctr, 1u);
+    gu = rfl(gu);
+    if (w.lane == 0)
+      __hip_atomic_store(&w.slots[s], (uint64_t(u + 1) << 32) | gu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  uint64_t v;
+  for (;;) {  // the publisher is a running wave that already holds ticket u*kUnit
+    v = __hip_atomic_load(&w.slots[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (rfl(static_cast<uint32_t>(v >> 32)) == u + 1) break;
+    __builtin_amdgcn_s_sleep(2);
+  }
+  g = w.p2first + uint64_t(rfl(static_cast<uint32_t>(v))) * kUnit + o;
+  return g < w.ntiles;
 }
 
 // Global tile g -> (segment, tile), walking forward from segment s.
@@ -163,13 +204,21 @@ DEV Cursor advance(Cursor c, SegP segs, uint32_t nseg, const Sched &w) {
     c.r++;
     return c;
   }
-  if (ORDER == 1) {
-    const uint32_t k = grab(w);
-    if (k >= w.nk) {
+  if (ORDER != 0) {
+    uint64_t g;
+    if (!ticket_tile<ORDER>(w, grab(w), g)) {
       c.valid = false;
       return c;
     }
-    return locate(segs, c.seg, w.gfirst + k);
+    if (ORDER == 2 && g < segs[c.seg].mtile_start) {  // pool tiles may lie behind the slice
+      uint32_t lo = 0, hi = nseg;
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (segs[mid].mtile_start <= g) lo = mid; else hi = mid;
+      }
+      return locate(segs, lo, g);
+    }
+    return locate(segs, c.seg, g);
   }
   uint32_t s = c.seg, t = c.tile + 1;
   while (s < nseg && t >= segs[s].main_tiles) {
@@ -222,6 +271,7 @@ DEV void issue(uint32_t (&d)[16], uint32_t &exp, const Cursor c, SegP segs, uint
 
 struct LaneConst {
   uint32_t lane, hsel, loff, lb0, lb1, qi, qg, zk, zbase, z448;
+  uint32_t store_policy;  // 0 default, 1 nontemporal, 2 diagnostic: drop result stores
 };
 
 // Process one round held in d[] for cursor c; st is the lane's running
@@ -263,13 +313,24 @@ DEV void process(const uint32_t *lds, uint32_t (&d)[16], uint32_t exp, const Cur
   }
   byte = rfl(byte);
   if (MODE == kModeCompute) {
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        segs[c.seg].crcs + c.tile * kTileChunks, 0, last ? static_cast<int>(nch * 4u) : 0, 0x00020000);
-    __builtin_amdgcn_raw_buffer_store_b32((flags & kSegBigEndian) ? __builtin_bswap32(out) : out, rs,
-                                          leader ? L.qg * 4u : 0x80000000u, 0, 0);
+    const bool keep = last && L.store_policy != 2;
+    const uint32_t val = (flags & kSegBigEndian) ? __builtin_bswap32(out) : out;
+    if (L.store_policy == 3) {
+      // diagnostic: 128-B full-line write per tile (crcs must hold 16 B per chunk)
+      const __amdgpu_buffer_rsrc_t r4 = __builtin_amdgcn_make_buffer_rsrc(
+          segs[c.seg].crcs + c.tile * kTileChunks * 4, 0, last ? static_cast<int>(nch * 16u) : 0, 0x00020000);
+      u32x4 v4 = {val, val, val, val};
+      __builtin_amdgcn_raw_buffer_store_b128(v4, r4, leader ? L.qg * 16u : 0x80000000u, 0, 0);
+    } else {
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          segs[c.seg].crcs + c.tile * kTileChunks, 0, keep ? static_cast<int>(nch * 4u) : 0, 0x00020000);
+      const uint32_t off = leader ? L.qg * 4u : 0x80000000u;
+      if (L.store_policy == 1) __builtin_amdgcn_raw_buffer_store_b32(val, rs, off, 0, 2);  // nt
+      else __builtin_amdgcn_raw_buffer_store_b32(val, rs, off, 0, 0);
+    }
   } else {
-    const __amdgpu_buffer_rsrc_t rb =
-        __builtin_amdgcn_make_buffer_rsrc(segs[c.seg].bitmap + c.tile, 0, last ? 1 : 0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+        segs[c.seg].bitmap + c.tile, 0, (last && L.store_policy != 2) ? 1 : 0, 0x00020000);
     __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(byte), rb, L.lane == 0 ? 0u : 0x80000000u, 0, 0);
     if (byte && L.lane == 0) {  // rare: only tiles with a mismatch
       atomicMin(&first_bad[c.seg], c.tile * kTileChunks + __builtin_ctz(byte));
@@ -282,10 +343,12 @@ template <int MODE, int ORDER, int NT, int DEPTH>
 __global__ __launch_bounds__(1024) void crc32c_tiles_kernel(
     const SegDev *__restrict__ segs, uint32_t nseg, uint64_t total_rounds, uint64_t total_tiles,
     const uint32_t *__restrict__ gtab, uint32_t *__restrict__ first_bad,
-    unsigned long long *__restrict__ mism, unsigned long long *__restrict__ diag) {
-  __shared__ uint32_t lds[kLdsWords + 1];  // + workgroup tile counter
+    unsigned long long *__restrict__ mism, unsigned long long *__restrict__ diag, uint32_t store_policy,
+    uint32_t *__restrict__ gctr) {
+  // + ticket counter, pad, kSlots 64-bit pool slots
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords + 2 + 2 * kSlots];
 
-  if (threadIdx.x == 0) lds[kLdsWords] = 0u;
+  if (threadIdx.x < 2 + 2 * kSlots) lds[kLdsWords + threadIdx.x] = 0u;
   // LDS image: word (P*16384 + e*64 + h*32 + l) = t_{3-(2P+h)}[e] for all 32 l.
   for (uint32_t idx = threadIdx.x; idx < kLdsSliceBytes / 4; idx += blockDim.x) {
     const uint32_t P = idx >> 14, e = (idx >> 6) & 255u, h = (idx >> 5) & 1u;
@@ -296,6 +359,7 @@ __global__ __launch_bounds__(1024) void crc32c_tiles_kernel(
   __syncthreads();
 
   LaneConst L;
+  L.store_policy = store_policy;
   L.lane = threadIdx.x & 63u;
   L.hsel = (L.lane >> 3) & 1u;                              // load: odd sub-chunk of each 1 KiB
   L.loff = 16u * (4u * (L.lane & 7u) + (L.lane >> 4));      // load: byte offset in the sub-chunk
@@ -333,13 +397,17 @@ __global__ __launch_bounds__(1024) void crc32c_tiles_kernel(
       }
     }
   } else {
-    const uint64_t b0 = rfl64(total_rounds * blockIdx.x / gridDim.x);
-    const uint64_t b1 = rfl64(total_rounds * (blockIdx.x + 1) / gridDim.x);
+    const uint64_t r_static = ORDER == 2 ? total_rounds * kPhase1Num / kPhase1Den : total_rounds;
+    const uint64_t b0 = rfl64(r_static * blockIdx.x / gridDim.x);
+    const uint64_t b1 = rfl64(r_static * (blockIdx.x + 1) / gridDim.x);
     w.gfirst = tile_at_round(sg, nseg, b0, total_tiles);
     w.nk = static_cast<uint32_t>(tile_at_round(sg, nseg, b1, total_tiles) - w.gfirst);
-    const uint32_t k = grab(w);
-    if (k < w.nk) {
-      const uint64_t g = w.gfirst + k;
+    w.p2first = tile_at_round(sg, nseg, r_static, total_tiles);
+    w.ntiles = total_tiles;
+    w.gctr = gctr;
+    w.slots = reinterpret_cast<uint64_t *>(&lds[kLdsWords + 2]);
+    uint64_t g;
+    if (ticket_tile<ORDER>(w, grab(w), g)) {
       uint32_t lo = 0, hi = nseg;
       while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
@@ -572,13 +640,14 @@ __global__ __launch_bounds__(256) void corrupt_kernel(uint8_t *__restrict__ data
 hipError_t launch_tiles(int mode, int order, int nt, int depth, int grid, const SegDev *segs, uint32_t nseg,
                         uint64_t total_rounds, uint64_t total_tiles, const uint32_t *gtab,
                         uint32_t *first_bad, unsigned long long *mism, unsigned long long *diag,
-                        hipStream_t stream) {
+                        uint32_t store_policy, uint32_t *gctr, hipStream_t stream) {
 #define HDFS_LAUNCH(M, O, N, D)                                                                        \
   hipLaunchKernelGGL((crc32c_tiles_kernel<M, O, N, D>), dim3(grid), dim3(1024), 0, stream, segs, nseg,  \
-                     total_rounds, total_tiles, gtab, first_bad, mism, diag)
+                     total_rounds, total_tiles, gtab, first_bad, mism, diag, store_policy, gctr)
 #define HDFS_LAUNCH_M(M)                                                   \
   do {                                                                     \
-    if (depth == 4) HDFS_LAUNCH(M, 1, 1, 4);                               \
+    if (order == 2) HDFS_LAUNCH(M, 2, 1, 3);                               \
+    else if (depth == 4) HDFS_LAUNCH(M, 1, 1, 4);                          \
     else if (order && nt) HDFS_LAUNCH(M, 1, 1, 3);                         \
     else if (order) HDFS_LAUNCH(M, 1, 0, 3);                               \
     else if (nt) HDFS_LAUNCH(M, 0, 1, 3);                                  \

@@ -156,7 +156,8 @@ int hdfs_crc32c_corrupt(void *dptr, uint64_t len, uint32_t chunk, uint64_t chunk
 int hdfs_crc32c_plan_time(hdfs_crc32c_plan *plan, void *stream, int iters, double *ms_per_iter);
 /* hipDeviceSynchronize on the engine's device. */
 int hdfs_crc32c_device_sync(void);
-/* Tiled-kernel schedule: 0 static per-wave slices, 1 workgroup-dynamic (default)
+/* Tiled-kernel schedule: 0 static per-wave slices, 1 workgroup-dynamic,
+ * 2 (default) workgroup-dynamic over 92 % + a global pool of 256-tile units
  * (waves of a workgroup take tiles from an LDS counter).  Env
  * HDFS_CRC32C_TILE_ORDER. */
 int hdfs_crc32c_set_tile_order(int order);
@@ -167,6 +168,10 @@ int hdfs_crc32c_set_tuning(int nt_loads, void *diag);
 /* Register round buffers per wave of the tiled kernel (3 or 4; depth-1
  * rounds stay in flight while one is processed).  Env HDFS_CRC32C_DEPTH. */
 int hdfs_crc32c_set_depth(int depth);
+/* Compute-mode result store policy: 0 default, 1 nontemporal, 2 diagnostic
+ * (stores dropped; output undefined -- timing experiments only).
+ * Env HDFS_CRC32C_STORE. */
+int hdfs_crc32c_set_store_policy(int policy);
 /* Empirical streaming-read bandwidth of `bytes` at dptr (GB/s, 1e9 B/s):
  * fully coalesced 16-B-per-lane loads, no compute; the measured roofline. */
 int hdfs_crc32c_probe_read(const void *dptr, uint64_t bytes, void *stream, int iters, double *gbps);

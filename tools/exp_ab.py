@@ -29,7 +29,7 @@ comp = h.Plan(h.MODE_COMPUTE, segs)
 ver = h.Plan(h.MODE_VERIFY, segs)
 comp.execute()
 h.device_sync()
-VARIANTS = [(1, 1, 3), (1, 1, 4)]  # (order, nt, depth)
+VARIANTS = [(1, 1, 3), (2, 1, 3)]  # (order, nt, depth)
 res = {}
 for rnd in range(4):
     for order, nt, depth in VARIANTS:
@@ -46,7 +46,7 @@ for k, v in res.items():
 # per-wave timestamps for the default variant
 nwaves = 256 * 16
 diag = h.DeviceBuffer(nwaves * 3 * 8)
-for order, nt, depth in VARIANTS:
+for order, nt, depth in list(VARIANTS)[::-1] + list(VARIANTS):
     h.set_tile_order(order)
     h.set_depth(depth)
     h.set_tuning(nt, diag.ptr)
