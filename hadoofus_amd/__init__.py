@@ -18,6 +18,7 @@ from .abi import (  # noqa: F401
     MODE_VERIFY,
     SEG_BE,
     SEG_RAW,
+    SEG_CRC32,
     CRC32CError,
     DeviceBuffer,
     Plan,
@@ -41,6 +42,7 @@ from .abi import (  # noqa: F401
     set_store_policy,
     load,
     stream_crc_dev,
+    stream_ex,
     verify_crcdata,
 )
 

@@ -23,7 +23,7 @@ ERR_PACKET_SIZE = 25
 ERR_CRC_LEN = 26
 ERR_BAD_CHECKSUM = 29
 MODE_COMPUTE, MODE_VERIFY = 0, 1
-SEG_BE, SEG_RAW = 1, 2
+SEG_BE, SEG_RAW, SEG_CRC32 = 1, 2, 4
 
 _u32, _u64, _vp, _sz, _int = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
 
@@ -81,10 +81,11 @@ def load(path=LIB_PATH):
     _bind(lib, "hdfs_crc32c_plan_destroy", None, [_vp])
     _bind(lib, "hdfs_crc32c_plan_time", _int, [_vp, _vp, _int, ctypes.POINTER(ctypes.c_double)])
     _bind(lib, "hdfs_crc32c_stream_dev", _int, [_u32, _vp, _u64, ctypes.POINTER(_u32)])
+    _bind(lib, "hdfs_crc32c_stream_ex", _int, [_int, _u32, _vp, _u64, ctypes.POINTER(_u32)])
     _bind(lib, "hdfs_crc32c_verify_crcdata", _int,
           [_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _int, ctypes.POINTER(ctypes.c_int32)])
     _bind(lib, "hdfs_crc32c_compose_crcs", _int,
-          [ctypes.POINTER(_vp), ctypes.POINTER(_sz), _int, _sz, _u32, _vp])
+          [ctypes.POINTER(_vp), ctypes.POINTER(_sz), _int, _sz, _u32, _int, _vp])
     _bind(lib, "hdfs_crc32c_dev_alloc", _int, [ctypes.POINTER(_vp), _u64])
     _bind(lib, "hdfs_crc32c_dev_free", _int, [_vp])
     _bind(lib, "hdfs_crc32c_memcpy", _int, [_vp, _vp, _u64, _int])
@@ -155,7 +156,16 @@ def verify_crcdata(region, chunksize, crcdlen, dlen, ctype=CSUM_CRC32C):
     return rc, fb.value
 
 
-def compose_crcs(iovecs, chunk=512):
+def stream_ex(ctype, crc, buf):
+    """CRC of a host buffer (bytes / numpy) continuing from crc: ctype
+    CSUM_CRC32C is _hdfs_crc32c, CSUM_CRC32 is zlib.crc32."""
+    keep, p, n = _host(buf)
+    out = _u32(0)
+    _check(load().hdfs_crc32c_stream_ex(ctype, crc & 0xFFFFFFFF, p if n else None, n, ctypes.byref(out)))
+    return out.value
+
+
+def compose_crcs(iovecs, chunk=512, ctype=CSUM_CRC32C):
     """BE CRC bytes for the concatenation of host fragments (write path)."""
     arrs = [_host(v) for v in iovecs]
     total = sum(a[2] for a in arrs)
@@ -164,7 +174,7 @@ def compose_crcs(iovecs, chunk=512):
     lens = (_sz * max(n, 1))(*[a[2] for a in arrs])
     out = np.zeros(((total + chunk - 1) // chunk) * 4, dtype=np.uint8)
     if total:
-        _check(load().hdfs_crc32c_compose_crcs(bases, lens, n, total, chunk, out.ctypes.data))
+        _check(load().hdfs_crc32c_compose_crcs(bases, lens, n, total, chunk, ctype, out.ctypes.data))
     return out.tobytes()
 
 

@@ -67,8 +67,9 @@ struct DevCtx {
   int dev = -1;
   int num_cu = 0;
   char arch[64] = "";
-  uint32_t *d_tab_main = nullptr;
-  uint32_t *d_tab_pow2 = nullptr;
+  // table sets per checksum type: [0] CRC32C, [1] CRC32 (zlib polynomial)
+  uint32_t *d_tab_main_t[2] = {nullptr, nullptr};
+  uint32_t *d_tab_pow2_t[2] = {nullptr, nullptr};
   hipStream_t stream = nullptr;
   // one-shot scratch (guarded by mu)
   uint8_t *h_stage = nullptr;
@@ -155,22 +156,26 @@ int ctx_init(int device, DevCtx **out) {
   c.num_cu = prop.multiProcessorCount;
   std::snprintf(c.arch, sizeof(c.arch), "%s", prop.gcnArchName);
 
-  // Tables (cf. the reference's load-time constructors).
-  std::vector<uint32_t> main(kTabMainWords), pow2(kTabPow2Words);
-  uint32_t t[4][256];
-  make_slicing4(t);
-  std::memcpy(main.data(), t, sizeof(t));
-  for (int k = 1; k <= 7; k++)
-    zeros_byte_tables(zeros_op(64ull * k), main.data() + kTabSliceWords + (k - 1) * 1024);
-  Gf2 op = zeros_op(1);
-  for (uint32_t b = 0; b < kPow2Levels; b++) {
-    zeros_byte_tables(op, pow2.data() + b * 1024);
-    op = op.compose(op);
+  // Tables (cf. the reference's load-time constructors), one set per
+  // checksum polynomial: CRC32C and zlib's CRC32 (src/datanode.c:2940-2952).
+  for (int ct = 0; ct < 2; ct++) {
+    const uint32_t poly = ct == 0 ? kPoly : kPolyZlib;
+    std::vector<uint32_t> main(kTabMainWords), pow2(kTabPow2Words);
+    uint32_t t[4][256];
+    make_slicing4(t, poly);
+    std::memcpy(main.data(), t, sizeof(t));
+    for (int k = 1; k <= 7; k++)
+      zeros_byte_tables(zeros_op(64ull * k, poly), main.data() + kTabSliceWords + (k - 1) * 1024);
+    Gf2 op = zeros_op(1, poly);
+    for (uint32_t b = 0; b < kPow2Levels; b++) {
+      zeros_byte_tables(op, pow2.data() + b * 1024);
+      op = op.compose(op);
+    }
+    HIPCHK(hipMalloc(&c.d_tab_main_t[ct], main.size() * 4));
+    HIPCHK(hipMalloc(&c.d_tab_pow2_t[ct], pow2.size() * 4));
+    HIPCHK(hipMemcpy(c.d_tab_main_t[ct], main.data(), main.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c.d_tab_pow2_t[ct], pow2.data(), pow2.size() * 4, hipMemcpyHostToDevice));
   }
-  HIPCHK(hipMalloc(&c.d_tab_main, main.size() * 4));
-  HIPCHK(hipMalloc(&c.d_tab_pow2, pow2.size() * 4));
-  HIPCHK(hipMemcpy(c.d_tab_main, main.data(), main.size() * 4, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(c.d_tab_pow2, pow2.data(), pow2.size() * 4, hipMemcpyHostToDevice));
   // Blocking stream: it serialises with the legacy NULL stream, so the
   // synchronous helpers (hipMemcpy/hipMemset) see prior plan work.
   HIPCHK(hipStreamCreate(&c.stream));
@@ -215,7 +220,7 @@ int fill_seg(const hdfs_crc32c_segment &in, int mode, SegDev &s, size_t idx) {
     return fail(HDFS_CRC32C_EINVAL, "segment %zu: verify needs a bitmap", idx);
   if (mode == HDFS_CRC32C_MODE_VERIFY && (in.flags & HDFS_CRC32C_SEG_RAW))
     return fail(HDFS_CRC32C_EINVAL, "segment %zu: RAW flag is compute-only", idx);
-  if (in.flags & ~(HDFS_CRC32C_SEG_BE | HDFS_CRC32C_SEG_RAW))
+  if (in.flags & ~(HDFS_CRC32C_SEG_BE | HDFS_CRC32C_SEG_RAW | HDFS_CRC32C_SEG_CRC32))
     return fail(HDFS_CRC32C_EINVAL, "segment %zu: unknown flags 0x%x", idx, in.flags);
   std::memset(&s, 0, sizeof(s));
   s.data = static_cast<const uint8_t *>(in.data);
@@ -229,6 +234,9 @@ int fill_seg(const hdfs_crc32c_segment &in, int mode, SegDev &s, size_t idx) {
   return HDFS_CRC32C_OK;
 }
 
+// Table set of a segment: 0 = CRC32C, 1 = CRC32 (zlib polynomial).
+inline int seg_ctype(uint32_t flags) { return (flags & HDFS_CRC32C_SEG_CRC32) ? 1 : 0; }
+
 bool device_accessible(const void *p) {
   if (!p) return true;
   hipPointerAttribute_t a;
@@ -240,10 +248,11 @@ bool device_accessible(const void *p) {
   return a.devicePointer != nullptr;
 }
 
+// ctype: 0 = CRC32C, 1 = CRC32 (zlib polynomial) -- selects the table set.
 int launch_all(DevCtx &c, int mode, const SegDev *d_segs, uint32_t nseg, uint64_t rounds,
                uint64_t mtiles, uint64_t gtiles, uint32_t *d_fb, unsigned long long *d_mism,
                uint32_t *d_gctr, hipStream_t st, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr,
-               bool reset = true) {
+               bool reset = true, int ctype = 0) {
   if (mode == kModeVerify && reset) {
     HIPCHK(hipMemsetAsync(d_fb, 0xFF, sizeof(uint32_t) * (nseg ? nseg : 1), st));
     HIPCHK(hipMemsetAsync(d_mism, 0, sizeof(unsigned long long), st));
@@ -256,15 +265,15 @@ int launch_all(DevCtx &c, int mode, const SegDev *d_segs, uint32_t nseg, uint64_
     if (g_tile_order == 2) HIPCHK(hipMemsetAsync(d_gctr, 0, sizeof(uint32_t), st));
     if (ev0) HIPCHK(hipEventRecord(ev0, st));
     HIPCHK(launch_tiles(mode, g_tile_order, g_nt_loads, g_depth, grid, d_segs, nseg, rounds, mtiles,
-                        c.d_tab_main, d_fb, d_mism, g_diag, g_store_policy, d_gctr, st));
+                        c.d_tab_main_t[ctype], d_fb, d_mism, g_diag, g_store_policy, d_gctr, st));
     if (ev1) HIPCHK(hipEventRecord(ev1, st));
   }
-  if (gtiles) HIPCHK(launch_generic(mode, d_segs, nseg, gtiles, c.d_tab_main, d_fb, d_mism, st));
+  if (gtiles) HIPCHK(launch_generic(mode, d_segs, nseg, gtiles, c.d_tab_main_t[ctype], d_fb, d_mism, st));
   return HDFS_CRC32C_OK;
 }
 
 // CRC of one device buffer continuing from crc (caller holds c.mu).
-int stream_crc_locked(DevCtx &c, uint32_t crc, const void *dbuf, uint64_t len, uint32_t *out) {
+int stream_crc_locked(DevCtx &c, uint32_t crc, const void *dbuf, uint64_t len, uint32_t *out, int ctype = 0) {
   if (len == 0) {
     *out = crc;
     return HDFS_CRC32C_OK;
@@ -278,17 +287,19 @@ int stream_crc_locked(DevCtx &c, uint32_t crc, const void *dbuf, uint64_t len, u
     HIPCHK(hipMalloc(&c.d_raw, cap * 4));
     c.raw_cap = cap;
   }
-  hdfs_crc32c_segment in = {dbuf, len, kStreamPiece, HDFS_CRC32C_SEG_RAW, 0, 0, c.d_raw, nullptr};
+  hdfs_crc32c_segment in = {dbuf, len, kStreamPiece,
+                            HDFS_CRC32C_SEG_RAW | (ctype ? HDFS_CRC32C_SEG_CRC32 : 0u), 0, 0, c.d_raw, nullptr};
   SegDev s;
   int rc = fill_seg(in, HDFS_CRC32C_MODE_COMPUTE, s, 0);
   if (rc) return rc;
   uint64_t rounds = 0, gtiles = 0, mtiles = 0;
   classify(s, rounds, gtiles, mtiles);
   HIPCHK(hipMemcpyAsync(c.d_seg, &s, sizeof(s), hipMemcpyHostToDevice, c.stream));
-  rc = launch_all(c, kModeCompute, c.d_seg, 1, rounds, mtiles, gtiles, nullptr, nullptr, c.d_small + 8, c.stream);
+  rc = launch_all(c, kModeCompute, c.d_seg, 1, rounds, mtiles, gtiles, nullptr, nullptr, c.d_small + 8, c.stream,
+                  nullptr, nullptr, true, ctype);
   if (rc) return rc;
   HIPCHK(hipMemsetAsync(c.d_small, 0, 4, c.stream));
-  HIPCHK(launch_combine(c.d_raw, nraw, kStreamPiece, len, c.d_tab_pow2, ~crc, c.d_small, c.stream));
+  HIPCHK(launch_combine(c.d_raw, nraw, kStreamPiece, len, c.d_tab_pow2_t[ctype], ~crc, c.d_small, c.stream));
   uint32_t acc = 0;
   HIPCHK(hipMemcpyAsync(&acc, c.d_small, 4, hipMemcpyDeviceToHost, c.stream));
   HIPCHK(hipStreamSynchronize(c.stream));
@@ -296,7 +307,7 @@ int stream_crc_locked(DevCtx &c, uint32_t crc, const void *dbuf, uint64_t len, u
   return HDFS_CRC32C_OK;
 }
 
-int stream_crc_any(uint32_t crc, const void *buf, uint64_t len, uint32_t *out) {
+int stream_crc_any(uint32_t crc, const void *buf, uint64_t len, uint32_t *out, int ctype = 0) {
   DevCtx *c = nullptr;
   int rc = ctx_init(-1, &c);
   if (rc) return rc;
@@ -306,13 +317,13 @@ int stream_crc_any(uint32_t crc, const void *buf, uint64_t len, uint32_t *out) {
     *out = crc;
     return HDFS_CRC32C_OK;
   }
-  if (device_accessible(buf)) return stream_crc_locked(*c, crc, buf, len, out);
+  if (device_accessible(buf)) return stream_crc_locked(*c, crc, buf, len, out, ctype);
   const uint8_t *p = static_cast<const uint8_t *>(buf);
   while (len) {
     const size_t n = len < kStageCap ? size_t(len) : kStageCap;
     std::memcpy(c->h_stage, p, n);
     HIPCHK(hipMemcpyAsync(c->d_stage, c->h_stage, n, hipMemcpyHostToDevice, c->stream));
-    rc = stream_crc_locked(*c, crc, c->d_stage, n, &crc);
+    rc = stream_crc_locked(*c, crc, c->d_stage, n, &crc, ctype);
     if (rc) return rc;
     p += n;
     len -= n;
@@ -401,7 +412,8 @@ int host_pipeline(int mode, const uint8_t *data, uint64_t len, uint32_t cs, uint
   if (!cs) return fail(HDFS_CRC32C_EINVAL, "chunk_size 0");
   if (!len) return HDFS_CRC32C_OK;
   if (!data || !crcs) return fail(HDFS_CRC32C_EINVAL, "null host buffer");
-  if (flags & ~(HDFS_CRC32C_SEG_BE | HDFS_CRC32C_SEG_RAW)) return fail(HDFS_CRC32C_EINVAL, "bad flags");
+  if (flags & ~(HDFS_CRC32C_SEG_BE | HDFS_CRC32C_SEG_RAW | HDFS_CRC32C_SEG_CRC32))
+    return fail(HDFS_CRC32C_EINVAL, "bad flags");
   if (mode == kModeVerify && (flags & HDFS_CRC32C_SEG_RAW)) return fail(HDFS_CRC32C_EINVAL, "RAW is compute-only");
   const uint64_t unit = uint64_t(cs) * 8;  // pieces hold whole tiles: bitmap bytes never straddle
   uint64_t piece = piece_req ? piece_req : (uint64_t(64) << 20);
@@ -455,7 +467,7 @@ int host_pipeline(int mode, const uint8_t *data, uint64_t len, uint32_t cs, uint
     HIPCHK(hipEventRecord(c.ev_copy[b], c.copy_stream));
     HIPCHK(hipStreamWaitEvent(c.comp_stream, c.ev_copy[b], 0));
     rc = launch_all(c, mode, c.p_segs + i, 1, rounds[i], mt[i], gt[i], c.p_fb + i, c.p_mism, c.p_gctr + b,
-                    c.comp_stream, nullptr, nullptr, false);
+                    c.comp_stream, nullptr, nullptr, false, seg_ctype(flags));
     if (rc) return rc;
     if (mode == kModeCompute)
       HIPCHK(hipMemcpyAsync(hc + c0 * 4, c.p_crc[b], nc * 4, hipMemcpyDeviceToHost, c.comp_stream));
@@ -493,6 +505,7 @@ using namespace hdfs_crc32c;
 struct hdfs_crc32c_plan {
   int dev = -1;
   int mode = 0;
+  int ctype = 0;  // table set: 0 CRC32C, 1 CRC32 (zlib)
   uint32_t nseg = 0;
   SegDev *d_segs = nullptr;
   uint32_t *d_first_bad = nullptr;
@@ -549,6 +562,14 @@ int hdfs_crc32c_stream_dev(uint32_t crc, const void *dbuf, uint64_t len, uint32_
   return stream_crc_any(crc, dbuf, len, out);
 }
 
+int hdfs_crc32c_stream_ex(int ctype, uint32_t crc, const void *buf, uint64_t len, uint32_t *out) {
+  if (!out) return fail(HDFS_CRC32C_EINVAL, "null out");
+  if (len && !buf) return fail(HDFS_CRC32C_EINVAL, "null buffer");
+  if (ctype != HDFS_CRC32C_CSUM_CRC32C && ctype != HDFS_CRC32C_CSUM_CRC32)
+    return fail(HDFS_CRC32C_EINVAL, "bad checksum type %d", ctype);
+  return stream_crc_any(crc, buf, len, out, ctype == HDFS_CRC32C_CSUM_CRC32 ? 1 : 0);
+}
+
 int hdfs_crc32c_plan_create(hdfs_crc32c_plan **plan, int mode, const hdfs_crc32c_segment *segs,
                             size_t nseg) {
   if (!plan) return fail(HDFS_CRC32C_EINVAL, "null plan pointer");
@@ -563,9 +584,12 @@ int hdfs_crc32c_plan_create(hdfs_crc32c_plan **plan, int mode, const hdfs_crc32c
   DeviceGuard g(c->dev);
   std::vector<SegDev> host(nseg ? nseg : 1);
   uint64_t rounds = 0, gtiles = 0, mtiles = 0, main_bytes = 0, gen_bytes = 0, nch = 0;
+  const int ctype = nseg ? seg_ctype(segs[0].flags) : 0;
   for (size_t i = 0; i < nseg; i++) {
     rc = fill_seg(segs[i], mode, host[i], i);
     if (rc) return rc;
+    if (seg_ctype(segs[i].flags) != ctype)
+      return fail(HDFS_CRC32C_EINVAL, "segment %zu: CRC32/CRC32C mixed within one plan", i);
     if (!device_accessible(segs[i].data) || !device_accessible(segs[i].crcs) ||
         !device_accessible(segs[i].bitmap))
       return fail(HDFS_CRC32C_EINVAL, "segment %zu: pointer is not device-accessible memory", i);
@@ -579,6 +603,7 @@ int hdfs_crc32c_plan_create(hdfs_crc32c_plan **plan, int mode, const hdfs_crc32c
   auto *p = new hdfs_crc32c_plan;
   p->dev = c->dev;
   p->mode = mode;
+  p->ctype = ctype;
   p->nseg = static_cast<uint32_t>(nseg);
   p->rounds = rounds;
   p->mtiles = mtiles;
@@ -617,7 +642,7 @@ int hdfs_crc32c_plan_execute(hdfs_crc32c_plan *p, void *stream) {
     p->next_event++;
   }
   return launch_all(c, p->mode, p->d_segs, p->nseg, p->rounds, p->mtiles, p->gtiles, p->d_first_bad,
-                    p->d_mism, p->d_gctr, st, e0, e1);
+                    p->d_mism, p->d_gctr, st, e0, e1, true, p->ctype);
 }
 
 int hdfs_crc32c_plan_results(hdfs_crc32c_plan *p, void *stream, uint32_t *first_bad, size_t nseg,
@@ -723,9 +748,11 @@ int hdfs_crc32c_plan_time(hdfs_crc32c_plan *p, void *stream, int iters, double *
 int hdfs_crc32c_verify_crcdata(const void *crcdata, int32_t chunksize, int32_t crcdlen, int32_t dlen,
                                int ctype, int32_t *first_bad) {
   if (first_bad) *first_bad = -1;
-  if (ctype == HDFS_CRC32C_CSUM_CRC32)
-    return fail(HDFS_CRC32C_ERR_DATANODE_UNSUPPORTED_CHECKSUM, "CRC32 (zlib) not implemented yet");
-  if (ctype != HDFS_CRC32C_CSUM_CRC32C) return fail(HDFS_CRC32C_EINVAL, "bad checksum type %d", ctype);
+  // The reference ASSERTs ctype is CRC32 or CRC32C (src/datanode.c:2938);
+  // CSUM_NULL and unknown types are refused here.
+  if (ctype != HDFS_CRC32C_CSUM_CRC32C && ctype != HDFS_CRC32C_CSUM_CRC32)
+    return fail(HDFS_CRC32C_EINVAL, "bad checksum type %d", ctype);
+  const uint32_t pflag = ctype == HDFS_CRC32C_CSUM_CRC32 ? HDFS_CRC32C_SEG_CRC32 : 0u;
   if (chunksize <= 0 || dlen < 0 || crcdlen < 0)
     return fail(HDFS_CRC32C_ERR_DATANODE_PACKET_SIZE, "bad packet sizes");
   const int64_t nch = (int64_t(dlen) + chunksize - 1) / chunksize;
@@ -746,7 +773,7 @@ int hdfs_crc32c_verify_crcdata(const void *crcdata, int32_t chunksize, int32_t c
   std::memcpy(c->h_stage, region + crcdlen, size_t(dlen));  // data (16-B aligned on device)
   std::memcpy(c->h_stage + off_crc, region, size_t(crcdlen));
   HIPCHK(hipMemcpyAsync(c->d_stage, c->h_stage, off_bm, hipMemcpyHostToDevice, c->stream));
-  hdfs_crc32c_segment in = {c->d_stage, uint64_t(dlen), uint32_t(chunksize), HDFS_CRC32C_SEG_BE, 0, 0,
+  hdfs_crc32c_segment in = {c->d_stage, uint64_t(dlen), uint32_t(chunksize), HDFS_CRC32C_SEG_BE | pflag, 0, 0,
                             c->d_stage + off_crc, c->d_stage + off_bm};
   SegDev s;
   rc = fill_seg(in, HDFS_CRC32C_MODE_VERIFY, s, 0);
@@ -756,7 +783,8 @@ int hdfs_crc32c_verify_crcdata(const void *crcdata, int32_t chunksize, int32_t c
   HIPCHK(hipMemcpyAsync(c->d_seg, &s, sizeof(s), hipMemcpyHostToDevice, c->stream));
   uint32_t *d_fb = c->d_small + 1;
   auto *d_m = reinterpret_cast<unsigned long long *>(c->d_small + 2);
-  rc = launch_all(*c, kModeVerify, c->d_seg, 1, rounds, mtiles, gtiles, d_fb, d_m, c->d_small + 8, c->stream);
+  rc = launch_all(*c, kModeVerify, c->d_seg, 1, rounds, mtiles, gtiles, d_fb, d_m, c->d_small + 8, c->stream,
+                  nullptr, nullptr, true, seg_ctype(pflag));
   if (rc) return rc;
   uint32_t fb = 0;
   HIPCHK(hipMemcpyAsync(&fb, d_fb, 4, hipMemcpyDeviceToHost, c->stream));
@@ -769,8 +797,12 @@ int hdfs_crc32c_verify_crcdata(const void *crcdata, int32_t chunksize, int32_t c
 }
 
 int hdfs_crc32c_compose_crcs(const void *const *iov_base, const size_t *iov_len, int iovcnt, size_t total,
-                             uint32_t chunk, void *crc_be_out) {
+                             uint32_t chunk, int ctype, void *crc_be_out) {
   if (chunk == 0) return fail(HDFS_CRC32C_EINVAL, "chunk 0");
+  // src/datanode.c:2826 ASSERTs the send checksum is CRC32 or CRC32C.
+  if (ctype != HDFS_CRC32C_CSUM_CRC32C && ctype != HDFS_CRC32C_CSUM_CRC32)
+    return fail(HDFS_CRC32C_EINVAL, "bad checksum type %d", ctype);
+  const uint32_t pflag = ctype == HDFS_CRC32C_CSUM_CRC32 ? HDFS_CRC32C_SEG_CRC32 : 0u;
   if (total == 0) return HDFS_CRC32C_OK;
   if (!iov_base || !iov_len || iovcnt <= 0 || !crc_be_out) return fail(HDFS_CRC32C_EINVAL, "bad iovecs");
   const size_t nch = (total + chunk - 1) / chunk;
@@ -790,14 +822,16 @@ int hdfs_crc32c_compose_crcs(const void *const *iov_base, const size_t *iov_len,
   }
   if (have != total) return fail(HDFS_CRC32C_EINVAL, "iovecs hold %zu of %zu bytes", have, total);
   HIPCHK(hipMemcpyAsync(c->d_stage, c->h_stage, total, hipMemcpyHostToDevice, c->stream));
-  hdfs_crc32c_segment in = {c->d_stage, total, chunk, HDFS_CRC32C_SEG_BE, 0, 0, c->d_stage + off_crc, nullptr};
+  hdfs_crc32c_segment in = {c->d_stage, total, chunk, HDFS_CRC32C_SEG_BE | pflag, 0, 0, c->d_stage + off_crc,
+                            nullptr};
   SegDev s;
   rc = fill_seg(in, HDFS_CRC32C_MODE_COMPUTE, s, 0);
   if (rc) return rc;
   uint64_t rounds = 0, gtiles = 0, mtiles = 0;
   classify(s, rounds, gtiles, mtiles);
   HIPCHK(hipMemcpyAsync(c->d_seg, &s, sizeof(s), hipMemcpyHostToDevice, c->stream));
-  rc = launch_all(*c, kModeCompute, c->d_seg, 1, rounds, mtiles, gtiles, nullptr, nullptr, c->d_small + 8, c->stream);
+  rc = launch_all(*c, kModeCompute, c->d_seg, 1, rounds, mtiles, gtiles, nullptr, nullptr, c->d_small + 8, c->stream,
+                  nullptr, nullptr, true, seg_ctype(pflag));
   if (rc) return rc;
   HIPCHK(hipMemcpyAsync(crc_be_out, c->d_stage + off_crc, nch * 4, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));

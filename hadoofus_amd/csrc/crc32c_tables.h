@@ -13,14 +13,15 @@
 
 namespace hdfs_crc32c {
 
-constexpr uint32_t kPoly = 0x82f63b78u;
+constexpr uint32_t kPoly = 0x82f63b78u;      // CRC-32C (Castagnoli), src/crc32c_sw.c:63
+constexpr uint32_t kPolyZlib = 0xedb88320u;  // CRC-32 (IEEE, zlib crc32()), HDFS_CSUM_CRC32
 
 // t[k][e]: register contribution of byte e followed by k zero bytes,
 // i.e. the classic slicing table t_k.
-inline void make_slicing4(uint32_t t[4][256]) {
+inline void make_slicing4(uint32_t t[4][256], uint32_t poly = kPoly) {
   for (uint32_t e = 0; e < 256; e++) {
     uint32_t c = e;
-    for (int b = 0; b < 8; b++) c = (c >> 1) ^ (kPoly & (0u - (c & 1u)));
+    for (int b = 0; b < 8; b++) c = (c >> 1) ^ (poly & (0u - (c & 1u)));
     t[0][e] = c;
   }
   for (uint32_t e = 0; e < 256; e++) {
@@ -51,9 +52,9 @@ struct Gf2 {
     for (int i = 0; i < 32; i++) r.col[i] = 1u << i;
     return r;
   }
-  static Gf2 one_zero_byte() {
+  static Gf2 one_zero_byte(uint32_t poly = kPoly) {
     Gf2 bit;  // one zero bit: c -> (c >> 1) ^ (c & 1 ? poly : 0)
-    bit.col[0] = kPoly;
+    bit.col[0] = poly;
     for (int i = 1; i < 32; i++) bit.col[i] = 1u << (i - 1);
     Gf2 r = bit;
     for (int k = 0; k < 3; k++) r = r.compose(r);
@@ -62,8 +63,8 @@ struct Gf2 {
 };
 
 // Operator for n zero bytes (square-and-multiply).
-inline Gf2 zeros_op(uint64_t n) {
-  Gf2 acc = Gf2::identity(), p = Gf2::one_zero_byte();
+inline Gf2 zeros_op(uint64_t n, uint32_t poly = kPoly) {
+  Gf2 acc = Gf2::identity(), p = Gf2::one_zero_byte(poly);
   while (n) {
     if (n & 1) acc = p.compose(acc);
     n >>= 1;

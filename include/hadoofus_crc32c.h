@@ -66,6 +66,10 @@ int hdfs_crc32c_device_info(int device, char *arch, size_t arch_len, int *num_cu
 
 #define HDFS_CRC32C_SEG_BE 1u   /* crcs[] in wire (big-endian) order, src/util.h:68-92 */
 #define HDFS_CRC32C_SEG_RAW 2u  /* compute: raw register (init 0, no final inversion) */
+/* Chunks use zlib's CRC-32 polynomial 0xEDB88320 (HDFS_CSUM_CRC32, the
+ * crc32() calls of src/datanode.c:2832-2845,2940-2952) instead of CRC-32C.
+ * All segments of one plan must agree. */
+#define HDFS_CRC32C_SEG_CRC32 4u
 
 /* One chunk stream: chunk i = bytes [i*chunk_size, min((i+1)*chunk_size, len))
  * of `data`; the last chunk may be partial (src/datanode.c:2946). */
@@ -105,20 +109,26 @@ void hdfs_crc32c_plan_destroy(hdfs_crc32c_plan *plan);
 /* CRC of one arbitrary device buffer continuing from `crc` (the
  * _hdfs_crc32c contract on device memory); synchronous. */
 int hdfs_crc32c_stream_dev(uint32_t crc, const void *dbuf, uint64_t len, uint32_t *out);
+/* Same for host or device memory and either checksum type: ctype
+ * HDFS_CRC32C_CSUM_CRC32C is _hdfs_crc32c, HDFS_CRC32C_CSUM_CRC32 is zlib's
+ * crc32(crc, buf, len) (the CRC32 branch of src/datanode.c:2845,2952). */
+int hdfs_crc32c_stream_ex(int ctype, uint32_t crc, const void *buf, uint64_t len, uint32_t *out);
 
 /* ---- datanode mirrors on host memory (synchronous) ---------------------- */
 /* _verify_crcdata (src/datanode.c:2931-2963) plus the CRC-length framing
  * check of _process_recv_packet (src/datanode.c:2441-2442) on a packet region
  * [crcdlen bytes of BE CRCs | dlen bytes of data].  Returns 0, or
- * HDFS_CRC32C_ERR_DATANODE_{CRC_LEN,BAD_CHECKSUM,UNSUPPORTED_CHECKSUM}, or a
- * negative HDFS_CRC32C_E* status; *first_bad = first mismatching chunk or -1. */
+ * HDFS_CRC32C_ERR_DATANODE_{PACKET_SIZE,CRC_LEN,BAD_CHECKSUM}, or a negative
+ * HDFS_CRC32C_E* status (EINVAL for a ctype other than CRC32 / CRC32C, which
+ * the reference ASSERTs); *first_bad = first mismatching chunk or -1. */
 int hdfs_crc32c_verify_crcdata(const void *crcdata, int32_t chunksize, int32_t crcdlen,
     int32_t dlen, int ctype, int32_t *first_bad);
 /* CRC loop of _compose_data_packet_header (src/datanode.c:2814-2860):
  * ceil(total/chunk) big-endian CRCs of the concatenation of iovcnt
- * fragments (CRCs chain across fragment boundaries). */
+ * fragments (CRCs chain across fragment boundaries); ctype is the packet's
+ * sendcsum_type (HDFS_CRC32C_CSUM_CRC32 or _CRC32C). */
 int hdfs_crc32c_compose_crcs(const void *const *iov_base, const size_t *iov_len, int iovcnt,
-    size_t total, uint32_t chunk, void *crc_be_out);
+    size_t total, uint32_t chunk, int ctype, void *crc_be_out);
 
 /* ---- host-resident streaming (pipelined H2D / kernel / D2H) -------------- */
 /* Per-chunk CRCs of a HOST buffer: pieces of piece_bytes (0 = 64 MiB, rounded

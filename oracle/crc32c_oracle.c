@@ -21,11 +21,19 @@
  *   oracle_compose_crcs   <- src/datanode.c:2814-2860 (write-path CRC loop,
  *                            chained across iovec fragments)
  *   oracle_zeros/combine  <- src/crc32c_sse42.c:99-200 generalised to any n
+ *   oracle_crc32_zlib     <- zlib crc32() (third-party dependency of
+ *                            src/datanode.c:12,2832-2845,2940-2952, not in
+ *                            /root/reference; pinned version: the image's
+ *                            zlib 1.2.11).  Restates zlib's published
+ *                            algorithm: reflected CRC-32, poly 0xEDB88320,
+ *                            register pre/post inverted, crc32(0,..) start.
  *
  * Parity is PINNED: tests/test_oracle.py checks every function here against
  * the reference's own KATs (tests/t_unit.c:146-217) and against golden
  * vectors produced by the reference compiled unchanged from /root/reference
  * (oracle/_ref, recipe in oracle/Makefile, generator oracle/gen_golden.py).
+ * The CRC32 (zlib) leg is pinned against zlib 1.2.11 itself (Python's zlib
+ * module in this container; fixtures tests/golden/zlib_*.json).
  */
 #include <stddef.h>
 #include <stdint.h>
@@ -34,6 +42,9 @@
 #include <time.h>
 
 #define ORACLE_POLY 0x82f63b78u /* src/crc32c_sw.c:63 */
+#define ORACLE_POLY_ZLIB 0xedb88320u /* zlib crc32(), HDFS_CSUM_CRC32 */
+#define ORACLE_CSUM_CRC32 1  /* include/hadoofus/objects.h:173 */
+#define ORACLE_CSUM_CRC32C 2
 
 /* ------------------------------------------------------------------ */
 /* Software slicing-by-8 (src/crc32c_sw.c:72-127)                      */
@@ -59,7 +70,35 @@ static void sw_init(void)
 	sw_ready = 1;
 }
 
-__attribute__((constructor)) static void oracle_ctor(void) { sw_init(); }
+static uint32_t zlib_tab[256];
+
+static void zlib_init(void)
+{
+	for (uint32_t n = 0; n < 256; n++) {
+		uint32_t c = n;
+		for (int k = 0; k < 8; k++)
+			c = (c >> 1) ^ (ORACLE_POLY_ZLIB & (0u - (c & 1u)));
+		zlib_tab[n] = c;
+	}
+}
+
+__attribute__((constructor)) static void oracle_ctor(void)
+{
+	sw_init();
+	zlib_init();
+}
+
+/* zlib crc32(crc, buf, len): byte-at-a-time table form of the reflected
+ * CRC-32 (see header for the pinning). */
+uint32_t oracle_crc32_zlib(uint32_t crc, const void *buf, size_t len)
+{
+	const uint8_t *p = buf;
+	uint32_t c = ~crc;
+	while (len--)
+		c = zlib_tab[(c ^ *p++) & 0xff] ^ (c >> 8);
+	return ~c;
+}
+
 
 uint32_t oracle_crc32c_sw(uint32_t crc, const void *buf, size_t len)
 {
@@ -308,6 +347,12 @@ static inline void be32enc(uint8_t *p, uint32_t v) /* src/util.h:82-92 */
 	p[3] = v;
 }
 
+static uint32_t crc_of(int ctype, uint32_t crc, const void *buf, size_t len)
+{
+	return ctype == ORACLE_CSUM_CRC32 ? oracle_crc32_zlib(crc, buf, len)
+					  : oracle_crc32c_sw(crc, buf, len);
+}
+
 /* Reference error numbers (include/objects.h:21-113, values checked by
  * compiling the reference header in this container). */
 #define ORACLE_ERR_CRC_LEN 26
@@ -321,7 +366,7 @@ static inline void be32enc(uint8_t *p, uint32_t v) /* src/util.h:82-92 */
  * (-1 if none), which is where the reference's loop returns.
  */
 int oracle_verify_crcdata(const void *crcdata, int32_t chunksize, int32_t crcdlen,
-    int32_t dlen, int32_t *first_bad)
+    int32_t dlen, int ctype, int32_t *first_bad)
 {
 	const uint8_t *crcs = crcdata;
 	const uint8_t *data = crcs + crcdlen;
@@ -332,7 +377,9 @@ int oracle_verify_crcdata(const void *crcdata, int32_t chunksize, int32_t crcdle
 		int32_t clen = dlen - i * chunksize;
 		if (clen > chunksize)
 			clen = chunksize;
-		uint32_t crc = oracle_crc32c_sw(0, data + (size_t)i * chunksize, clen);
+		/* crcinit: crc32(0L, Z_NULL, 0) == 0 for CRC32, 0 for CRC32C
+		 * (src/datanode.c:2940-2943) */
+		uint32_t crc = crc_of(ctype, 0, data + (size_t)i * chunksize, clen);
 		if (crc != be32dec(crcs + 4 * (size_t)i)) {
 			*first_bad = i;
 			return ORACLE_ERR_BAD_CHECKSUM;
@@ -347,7 +394,7 @@ int oracle_verify_crcdata(const void *crcdata, int32_t chunksize, int32_t crcdle
  * (iov_base[k], iov_len[k]).  Writes ceil(total/chunk) * 4 bytes.
  */
 void oracle_compose_crcs(const void *const *iov_base, const size_t *iov_len, int iovcnt,
-    size_t total, uint32_t chunk, void *crc_be_out)
+    size_t total, uint32_t chunk, int ctype, void *crc_be_out)
 {
 	uint8_t *out = crc_be_out;
 	size_t nch = (total + chunk - 1) / chunk;
@@ -362,7 +409,7 @@ void oracle_compose_crcs(const void *const *iov_base, const size_t *iov_len, int
 			size_t t = iov_len[k] - off;
 			if (t > clen)
 				t = clen;
-			crc = oracle_crc32c_sw(crc, (const uint8_t *)iov_base[k] + off, t);
+			crc = crc_of(ctype, crc, (const uint8_t *)iov_base[k] + off, t);
 			clen -= t;
 			off += t;
 			if (off == iov_len[k]) {
@@ -374,7 +421,8 @@ void oracle_compose_crcs(const void *const *iov_base, const size_t *iov_len, int
 	}
 }
 
-/* Per-chunk CRCs (LE u32 out) of a buffer; the last chunk may be partial. */
+/* Per-chunk CRCs (LE u32 out) of a buffer; the last chunk may be partial.
+ * use_hw: 0 sw slicing, 1 SSE4.2, 2 zlib CRC32. */
 void oracle_chunk_crcs(const void *data, uint64_t len, uint32_t chunk, uint32_t *out, int use_hw)
 {
 	const uint8_t *p = data;
@@ -383,8 +431,9 @@ void oracle_chunk_crcs(const void *data, uint64_t len, uint32_t chunk, uint32_t 
 		uint64_t clen = len - i * chunk;
 		if (clen > chunk)
 			clen = chunk;
-		out[i] = use_hw ? oracle_crc32c_hw(0, p + i * chunk, clen)
-				: oracle_crc32c_sw(0, p + i * chunk, clen);
+		out[i] = use_hw == 2 ? oracle_crc32_zlib(0, p + i * chunk, clen)
+			 : use_hw ? oracle_crc32c_hw(0, p + i * chunk, clen)
+				  : oracle_crc32c_sw(0, p + i * chunk, clen);
 	}
 }
 

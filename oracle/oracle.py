@@ -37,6 +37,9 @@ def _bind(lib, name, restype, argtypes):
     return f
 
 
+CSUM_CRC32, CSUM_CRC32C = 1, 2  # include/hadoofus/objects.h:173-174
+
+
 class Oracle:
     def __init__(self, path=LIB):
         if not os.path.exists(path):
@@ -45,14 +48,15 @@ class Oracle:
         self._sw = _bind(lib, "oracle_crc32c_sw", _u32, [_u32, _vp, _sz])
         self._hw = _bind(lib, "oracle_crc32c_hw", _u32, [_u32, _vp, _sz])
         self._bit = _bind(lib, "oracle_crc32c_bitwise", _u32, [_u32, _vp, _sz])
+        self._zlib = _bind(lib, "oracle_crc32_zlib", _u32, [_u32, _vp, _sz])
         self._comb = _bind(lib, "oracle_crc32c_combine", _u32, [_u32, _u32, _u64])
         self._zap = _bind(lib, "oracle_zeros_apply", _u32, [_u32, _u64])
         self._ver = _bind(lib, "oracle_verify_crcdata", ctypes.c_int,
-                          [_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                          [_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int,
                            ctypes.POINTER(ctypes.c_int32)])
         self._compose = _bind(lib, "oracle_compose_crcs", None,
                               [ctypes.POINTER(_vp), ctypes.POINTER(_sz), ctypes.c_int,
-                               _sz, _u32, _vp])
+                               _sz, _u32, ctypes.c_int, _vp])
         self._chunks = _bind(lib, "oracle_chunk_crcs", None, [_vp, _u64, _u32, _vp, ctypes.c_int])
         self._fill = _bind(lib, "oracle_splitmix_fill", None, [_vp, _u64, _u64, _u64])
         self._bench = _bind(lib, "oracle_bench_chunks", ctypes.c_double,
@@ -69,7 +73,7 @@ class Oracle:
 
     def crc32c(self, crc, data, kind="sw"):
         p, n = self._buf(data)
-        f = {"sw": self._sw, "hw": self._hw, "bitwise": self._bit}[kind]
+        f = {"sw": self._sw, "hw": self._hw, "bitwise": self._bit, "zlib": self._zlib}[kind]
         return f(crc & 0xFFFFFFFF, p, n)
 
     def combine(self, crc_a, crc_b, len_b):
@@ -78,14 +82,14 @@ class Oracle:
     def zeros_apply(self, reg, nbytes):
         return self._zap(reg, nbytes)
 
-    def verify_crcdata(self, region, chunksize, crcdlen, dlen):
+    def verify_crcdata(self, region, chunksize, crcdlen, dlen, ctype=CSUM_CRC32C):
         """-> (err, first_bad) ; err 0 / 26 (CRC_LEN) / 29 (BAD_CHECKSUM)."""
         arr = np.frombuffer(bytes(region), dtype=np.uint8)
         fb = ctypes.c_int32(-1)
-        err = self._ver(arr.ctypes.data, chunksize, crcdlen, dlen, ctypes.byref(fb))
+        err = self._ver(arr.ctypes.data, chunksize, crcdlen, dlen, ctype, ctypes.byref(fb))
         return err, fb.value
 
-    def compose_crcs(self, iovecs, chunk=512):
+    def compose_crcs(self, iovecs, chunk=512, ctype=CSUM_CRC32C):
         """Write-path BE CRC bytes for a list of byte fragments (datanode.c:2814-2860)."""
         arrs = [np.frombuffer(bytes(v), dtype=np.uint8) for v in iovecs]
         total = sum(a.nbytes for a in arrs)
@@ -93,13 +97,14 @@ class Oracle:
         bases = (_vp * max(n, 1))(*[a.ctypes.data for a in arrs])
         lens = (_sz * max(n, 1))(*[a.nbytes for a in arrs])
         out = np.zeros(((total + chunk - 1) // chunk) * 4, dtype=np.uint8)
-        self._compose(bases, lens, n, total, chunk, out.ctypes.data)
+        self._compose(bases, lens, n, total, chunk, ctype, out.ctypes.data)
         return out.tobytes()
 
-    def chunk_crcs(self, data, chunk, hw=True):
+    def chunk_crcs(self, data, chunk, hw=True, ctype=CSUM_CRC32C):
         p, n = self._buf(data)
         out = np.zeros((n + chunk - 1) // chunk, dtype=np.uint32)
-        self._chunks(p, n, chunk, out.ctypes.data, 1 if (hw and self.have_hw) else 0)
+        code = 2 if ctype == CSUM_CRC32 else (1 if (hw and self.have_hw) else 0)
+        self._chunks(p, n, chunk, out.ctypes.data, code)
         return out
 
     def splitmix(self, nwords, seed=0, g0=0):

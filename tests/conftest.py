@@ -35,6 +35,11 @@ def golden():
         g["verify"] = json.load(f)["cases"]
     with open(os.path.join(GOLDEN, "block_digests.json")) as f:
         g["blocks"] = json.load(f)["blocks"]
+    # CRC32 (zlib 1.2.11) leg, oracle/gen_golden_zlib.py
+    with open(os.path.join(GOLDEN, "zlib_vectors.json")) as f:
+        g["zlib"] = json.load(f)
+    g["zlib_sweep"] = np.load(os.path.join(GOLDEN, "zlib_edge_sweep.npy"))
+    g["zlib_chunks"] = dict(np.load(os.path.join(GOLDEN, "zlib_chunk_crcs.npz")))
     return g
 
 

@@ -178,8 +178,9 @@ def test_verify_crcdata_golden(engine, golden):
         assert err == (engine.ERR_BAD_CHECKSUM if case["mismatch"] else 0)
         if nch:
             assert engine.verify_crcdata(region, cs, nch * 4 + 4, dlen)[0] == engine.ERR_CRC_LEN
-    assert engine.verify_crcdata(b"\0" * 8, 512, 4, 512, ctype=engine.CSUM_CRC32)[0] == \
-        engine.ERR_UNSUPPORTED_CHECKSUM
+    # CSUM_NULL is not a checksum the reference verifies (src/datanode.c:2938 ASSERT)
+    with pytest.raises(engine.CRC32CError):
+        engine.verify_crcdata(b"\0" * 8, 512, 4, 512, ctype=engine.CSUM_NULL)
 
 
 def test_compose_crcs_vs_oracle(engine, oracle):
@@ -188,6 +189,8 @@ def test_compose_crcs_vs_oracle(engine, oracle):
     for cuts in ([0, 65536 + 300], [0, 1, 100, 513, 40000, 65836], [0, 65536]):
         frags = [data[a:b] for a, b in zip(cuts[:-1], cuts[1:])]
         assert engine.compose_crcs(frags, 512) == oracle.compose_crcs(frags, 512)
+        assert engine.compose_crcs(frags, 512, ctype=engine.CSUM_CRC32) == \
+            oracle.compose_crcs(frags, 512, ctype=engine.CSUM_CRC32)
 
 
 # --- large inputs: stream CRC and the pinned full-block digests ---------------
