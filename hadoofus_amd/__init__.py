@@ -13,6 +13,13 @@ from .abi import (  # noqa: F401
     ERR_BAD_CHECKSUM,
     ERR_CRC_LEN,
     ERR_PACKET_SIZE,
+    ERR_INVALID_PACKETHEADERPROTO,
+    ERR_UNEXPECTED_CRC_LEN,
+    PROTO_V1,
+    PROTO_V2,
+    Packet,
+    parse_packets,
+    verify_packets,
     ERR_UNSUPPORTED_CHECKSUM,
     MODE_COMPUTE,
     MODE_VERIFY,

@@ -19,10 +19,13 @@ LIB_PATH = os.path.join(HERE, "lib", "libhadoofus_crc32c.so")
 CSUM_NULL, CSUM_CRC32, CSUM_CRC32C = 0, 1, 2
 # include/objects.h:21-113 (enum hdfs_error_numeric values)
 ERR_UNSUPPORTED_CHECKSUM = 8
+ERR_INVALID_PACKETHEADERPROTO = 18
 ERR_PACKET_SIZE = 25
 ERR_CRC_LEN = 26
+ERR_UNEXPECTED_CRC_LEN = 27
 ERR_BAD_CHECKSUM = 29
 MODE_COMPUTE, MODE_VERIFY = 0, 1
+PROTO_V1, PROTO_V2 = 1, 2
 SEG_BE, SEG_RAW, SEG_CRC32 = 1, 2, 4
 
 _u32, _u64, _vp, _sz, _int = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
@@ -46,6 +49,27 @@ class Segment(ctypes.Structure):
         ("crcs", _vp),
         ("bitmap", _vp),
     ]
+
+
+class Packet(ctypes.Structure):
+    """struct hdfs_crc32c_packet."""
+    _fields_ = [
+        ("stream_off", _u64),
+        ("offset_in_block", ctypes.c_int64),
+        ("seqno", ctypes.c_int64),
+        ("data_len", ctypes.c_int32),
+        ("crc_len", ctypes.c_int32),
+        ("header_len", _u32),
+        ("error", ctypes.c_int32),
+        ("first_bad", ctypes.c_int32),
+        ("bad_chunks", _u32),
+        ("last", ctypes.c_uint8),
+        ("sync", ctypes.c_uint8),
+        ("reserved", ctypes.c_uint8 * 6),
+    ]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_ if f != "reserved"}
 
 
 _lib = None
@@ -86,6 +110,9 @@ def load(path=LIB_PATH):
           [_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _int, ctypes.POINTER(ctypes.c_int32)])
     _bind(lib, "hdfs_crc32c_compose_crcs", _int,
           [ctypes.POINTER(_vp), ctypes.POINTER(_sz), _int, _sz, _u32, _int, _vp])
+    for name in ("hdfs_crc32c_parse_packets", "hdfs_crc32c_verify_packets"):
+        _bind(lib, name, _int, [_vp, _u64, _int, _u32, _int, ctypes.POINTER(Packet), _sz,
+                                ctypes.POINTER(_sz), ctypes.POINTER(_u64)])
     _bind(lib, "hdfs_crc32c_dev_alloc", _int, [ctypes.POINTER(_vp), _u64])
     _bind(lib, "hdfs_crc32c_dev_free", _int, [_vp])
     _bind(lib, "hdfs_crc32c_memcpy", _int, [_vp, _vp, _u64, _int])
@@ -163,6 +190,30 @@ def stream_ex(ctype, crc, buf):
     out = _u32(0)
     _check(load().hdfs_crc32c_stream_ex(ctype, crc & 0xFFFFFFFF, p if n else None, n, ctypes.byref(out)))
     return out.value
+
+
+def _packets(fn, stream, proto, chunk_size, ctype, max_pkts):
+    keep, p, n = _host(stream)
+    if max_pkts is None:
+        max_pkts = n // (25 if proto == PROTO_V1 else 6) + 1
+    arr = (Packet * max(1, max_pkts))()
+    npk, used = _sz(0), _u64(0)
+    rc = getattr(load(), fn)(p, n, proto, chunk_size, ctype, arr, max_pkts, ctypes.byref(npk), ctypes.byref(used))
+    if rc < 0:
+        _check(rc)
+    return rc, [arr[i].as_dict() for i in range(npk.value)], used.value
+
+
+def parse_packets(stream, proto=PROTO_V2, chunk_size=512, ctype=CSUM_CRC32C, max_pkts=None):
+    """Framing walk of a host packet stream (no device work).
+    -> (rc, [packet dicts], consumed)."""
+    return _packets("hdfs_crc32c_parse_packets", stream, proto, chunk_size, ctype, max_pkts)
+
+
+def verify_packets(stream, proto=PROTO_V2, chunk_size=512, ctype=CSUM_CRC32C, max_pkts=None):
+    """Framing + GPU verification of every packet's chunks.
+    -> (rc, [packet dicts], consumed); rc = first error in stream order."""
+    return _packets("hdfs_crc32c_verify_packets", stream, proto, chunk_size, ctype, max_pkts)
 
 
 def compose_crcs(iovecs, chunk=512, ctype=CSUM_CRC32C):

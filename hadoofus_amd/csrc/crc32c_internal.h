@@ -53,6 +53,21 @@ constexpr uint32_t kTabMainWords = kTabSliceWords + kTabZposWords;
 constexpr uint32_t kPow2Levels = 48;
 constexpr uint32_t kTabPow2Words = kPow2Levels * 1024;
 
+// One received packet inside a de-framing piece (packet-stream verifier).
+// The piece's raw bytes are the wire bytes; the gather kernel copies each
+// packet's CRCs to a 4-B aligned CRC arena and its data to a 16-B aligned
+// data arena so the verify kernels see ordinary segments.
+struct PktDesc {
+  uint64_t src_crc;   // piece-relative offset of the packet's CRC bytes (data follows)
+  uint64_t dst_data;  // data arena offset (16-B aligned)
+  uint64_t dst_crc;   // CRC arena offset (4-B aligned)
+  uint32_t dlen;      // data bytes
+  uint32_t ncrc;      // CRC words
+  uint32_t unit0;     // first gather unit of the packet (piece-relative)
+  uint32_t nunits;    // gather units: ceil(dlen / kGatherSlice)
+};
+constexpr uint32_t kGatherSlice = 65536;  // data bytes per gather workgroup
+
 constexpr uint32_t kRoundBytes = 512;  // sub-chunk handled by 8 lanes per round
 constexpr uint32_t kTileChunks = 8;
 

@@ -634,9 +634,69 @@ __global__ __launch_bounds__(256) void corrupt_kernel(uint8_t *__restrict__ data
   data[local * cs + bit / 8] ^= static_cast<uint8_t>(1u << (bit % 8));
 }
 
+// De-framing gather for the packet-stream verifier: one workgroup per
+// 64 KiB slice of one packet's data.  Packet payloads sit at arbitrary byte
+// offsets of the wire stream (header 25 or 6+hlen bytes, then 4 B per chunk),
+// so each lane reads the dword-aligned window around its 16 output bytes and
+// funnel-shifts it into place (v_alignbyte_b32); stores are 16-B aligned.
+// The slice also moves its share of the packet's BE CRC words.
+DEV uint32_t align_word(uint32_t hi, uint32_t lo, uint32_t sh) {
+  return __builtin_amdgcn_alignbyte(hi, lo, sh);
+}
+
+__global__ __launch_bounds__(256) void packet_gather_kernel(const uint8_t *__restrict__ raw,
+                                                             const PktDesc *__restrict__ descs, uint32_t npk,
+                                                             uint8_t *__restrict__ arena,
+                                                             uint8_t *__restrict__ crc_arena) {
+  const uint32_t u = blockIdx.x;
+  uint32_t lo = 0, hi = npk - 1;  // last packet with unit0 <= u
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi + 1) >> 1;
+    if (descs[mid].unit0 <= u) lo = mid; else hi = mid - 1;
+  }
+  const PktDesc d = descs[lo];
+  const uint32_t s = u - d.unit0;
+  const uint8_t *src = raw + d.src_crc + 4ull * d.ncrc;
+  uint8_t *dst = arena + d.dst_data;
+  const uint64_t b0 = uint64_t(s) * kGatherSlice;
+  const uint64_t b1 = min(uint64_t(d.dlen), b0 + kGatherSlice);
+  for (uint64_t o = b0 + 16ull * threadIdx.x; o < b1; o += 16ull * blockDim.x) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(src + o);
+    const uint32_t sh = uint32_t(a & 3);
+    const uint8_t *a0 = reinterpret_cast<const uint8_t *>(a - sh);
+    uint32_t w[5];
+#pragma unroll
+    for (int i = 0; i < 5; i++) w[i] = gload32(a0 + 4 * i);
+    u32x4 v;
+    v.x = align_word(w[1], w[0], sh);
+    v.y = align_word(w[2], w[1], sh);
+    v.z = align_word(w[3], w[2], sh);
+    v.w = align_word(w[4], w[3], sh);
+    *(GAS u32x4 *)(GAS uint8_t *)(dst + o) = v;
+  }
+  // CRC words [s*q, (s+1)*q) of this packet, q = ceil(ncrc / nunits)
+  const uint32_t q = (d.ncrc + d.nunits - 1) / d.nunits;
+  const uint32_t w1 = min(d.ncrc, (s + 1) * q);
+  const uint8_t *csrc = raw + d.src_crc;
+  uint8_t *cdst = crc_arena + d.dst_crc;
+  for (uint32_t w = s * q + threadIdx.x; w < w1; w += blockDim.x) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(csrc + 4ull * w);
+    const uint32_t sh = uint32_t(a & 3);
+    const uint8_t *a0 = reinterpret_cast<const uint8_t *>(a - sh);
+    gstore32(cdst + 4ull * w, align_word(gload32(a0 + 4), gload32(a0), sh));
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Host-side launchers (used by crc32c_engine.cpp).
 // ---------------------------------------------------------------------------
+hipError_t launch_gather(const uint8_t *raw, const PktDesc *descs, uint32_t npk, uint32_t units, uint8_t *arena,
+                         uint8_t *crc_arena, hipStream_t stream) {
+  if (!npk || !units) return hipSuccess;
+  hipLaunchKernelGGL(packet_gather_kernel, dim3(units), dim3(256), 0, stream, raw, descs, npk, arena, crc_arena);
+  return hipGetLastError();
+}
+
 hipError_t launch_tiles(int mode, int order, int nt, int depth, int grid, const SegDev *segs, uint32_t nseg,
                         uint64_t total_rounds, uint64_t total_tiles, const uint32_t *gtab,
                         uint32_t *first_bad, unsigned long long *mism, unsigned long long *diag,

@@ -44,8 +44,10 @@ uint32_t _hdfs_sw_crc32c(uint32_t crc, const void *buf, unsigned len);
 /* Datanode-level results reuse the reference's enum hdfs_error_numeric
  * values (include/objects.h:21-113; checked by compiling that header). */
 #define HDFS_CRC32C_ERR_DATANODE_UNSUPPORTED_CHECKSUM 8
+#define HDFS_CRC32C_ERR_INVALID_PACKETHEADERPROTO 18
 #define HDFS_CRC32C_ERR_DATANODE_PACKET_SIZE 25
 #define HDFS_CRC32C_ERR_DATANODE_CRC_LEN 26
+#define HDFS_CRC32C_ERR_DATANODE_UNEXPECTED_CRC_LEN 27
 #define HDFS_CRC32C_ERR_DATANODE_BAD_CHECKSUM 29
 
 /* enum hdfs_checksum_type (include/objects.h:169-175) */
@@ -129,6 +131,50 @@ int hdfs_crc32c_verify_crcdata(const void *crcdata, int32_t chunksize, int32_t c
  * sendcsum_type (HDFS_CRC32C_CSUM_CRC32 or _CRC32C). */
 int hdfs_crc32c_compose_crcs(const void *const *iov_base, const size_t *iov_len, int iovcnt,
     size_t total, uint32_t chunk, int ctype, void *crc_be_out);
+
+/* ---- datanode packet streams (src/datanode.c:2345-2494) ----------------- */
+/* Framing of a run of received packets, the sequential part of _recv_packet /
+ * _process_recv_packet:
+ *   PROTO_V1 (proto < HDFS_DATANODE_AP_2_0, include/hadoofus/lowlevel.h:429-433):
+ *     [plen s32][offsetInBlock s64][seqno s64][last s8][dataLen s32], 25 bytes
+ *   PROTO_V2: [plen s32][hlen u16][PacketHeaderProto (hlen bytes)]
+ *   followed by crcdlen = plen - dataLen - 4 bytes of BE CRCs and the data. */
+#define HDFS_CRC32C_PROTO_V1 1
+#define HDFS_CRC32C_PROTO_V2 2
+
+typedef struct hdfs_crc32c_packet {
+	uint64_t stream_off;      /* offset of the packet (its plen) in the stream */
+	int64_t offset_in_block;  /* header offsetInBlock */
+	int64_t seqno;            /* header seqno */
+	int32_t data_len;         /* dataLen */
+	int32_t crc_len;          /* crcdlen = plen - dataLen - 4; CRCs at stream_off + header_len */
+	uint32_t header_len;      /* 25 (v1) or 6 + hlen (v2) */
+	int32_t error;            /* 0 or the HDFS_CRC32C_ERR_* this packet raises */
+	int32_t first_bad;        /* first bad chunk of the packet, -1 if none */
+	uint32_t bad_chunks;      /* number of bad chunks in the packet */
+	uint8_t last;             /* lastPacketInBlock */
+	uint8_t sync;             /* syncBlock (v2) */
+	uint8_t reserved[6];
+} hdfs_crc32c_packet;
+
+/* Framing only, on the host (no device work): walks up to max_pkts packets
+ * of the HOST stream, applying the checks of src/datanode.c:2428-2456
+ * (PACKET_SIZE, CRC_LEN, UNEXPECTED_CRC_LEN, empty non-last packet) and the
+ * header decode (INVALID_PACKETHEADERPROTO).  The walk stops after a framing
+ * error (recorded in that packet's .error), after an empty last packet (end
+ * of block), or at an incomplete packet (not recorded).  *consumed = bytes of
+ * complete, framing-clean packets.  Returns the first packet error, 0, or a
+ * negative HDFS_CRC32C_E* status.  ctype: HDFS_CRC32C_CSUM_*. */
+int hdfs_crc32c_parse_packets(const void *stream, uint64_t len, int proto, uint32_t chunk_size,
+    int ctype, hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts, uint64_t *consumed);
+/* Framing as above, then every chunk of every framing-clean packet verified
+ * on the GPU (_verify_crcdata, src/datanode.c:2931-2963): the stream goes
+ * H2D once in pieces overlapped with a de-framing gather kernel and the
+ * verify kernels.  Per packet: .error = BAD_CHECKSUM, .first_bad,
+ * .bad_chunks.  Returns the first error in stream order (what the reference
+ * returns from its packet loop), 0, or a negative status. */
+int hdfs_crc32c_verify_packets(const void *stream, uint64_t len, int proto, uint32_t chunk_size,
+    int ctype, hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts, uint64_t *consumed);
 
 /* ---- host-resident streaming (pipelined H2D / kernel / D2H) -------------- */
 /* Per-chunk CRCs of a HOST buffer: pieces of piece_bytes (0 = 64 MiB, rounded

@@ -438,6 +438,214 @@ void oracle_chunk_crcs(const void *data, uint64_t len, uint32_t chunk, uint32_t 
 }
 
 /* ------------------------------------------------------------------ */
+/* Packet streams: _recv_packet -> _process_recv_packet -> _verify_crcdata */
+/* (src/datanode.c:2345-2494, 2931-2963)                                */
+/* ------------------------------------------------------------------ */
+#define ORACLE_ERR_INVALID_PACKETHEADERPROTO 18 /* include/hadoofus/objects.h:68 */
+#define ORACLE_ERR_PACKET_SIZE 25
+#define ORACLE_ERR_UNEXPECTED_CRC_LEN 27
+
+struct oracle_packet { /* same layout as hdfs_crc32c_packet */
+	uint64_t stream_off;
+	int64_t offset_in_block, seqno;
+	int32_t data_len, crc_len;
+	uint32_t header_len;
+	int32_t error, first_bad;
+	uint32_t bad_chunks;
+	uint8_t last, sync, reserved[6];
+};
+
+static int64_t rd_be(const uint8_t *p, int n) /* _hdfs_bslurp_s*, src/heapbuf.c:174-215 */
+{
+	uint64_t v = 0;
+	for (int i = 0; i < n; i++)
+		v = (v << 8) | p[i];
+	if (n == 4)
+		return (int32_t)(uint32_t)v;
+	if (n == 1)
+		return (int8_t)v;
+	return (int64_t)v;
+}
+
+/* protobuf-c unpack of PacketHeaderProto (src/proto/datatransfer.proto:228-235):
+ * field table {number, wire type}; returns 0 on success. */
+static int pb_header(const uint8_t *p, size_t n, int64_t *off, int64_t *seq,
+    uint8_t *last, int32_t *dlen, uint8_t *sync)
+{
+	static const int want_wt[6] = { -1, 1, 1, 0, 5, 0 };
+	int have = 0;
+	size_t i = 0;
+	while (i < n) {
+		uint64_t tag = 0;
+		int k;
+		if (!(p[i] & 0xf8))
+			return -1;
+		for (k = 0; k < 5 && i + k < n; k++) {
+			tag |= (uint64_t)(p[i + k] & 0x7f) << (7 * k);
+			if (!(p[i + k] & 0x80))
+				break;
+		}
+		if (k == 5 || i + k >= n)
+			return -1;
+		i += k + 1;
+		int wt = tag & 7;
+		uint64_t fn = tag >> 3;
+		const uint8_t *v = p + i;
+		size_t vlen;
+		if (wt == 0) {
+			for (k = 0; k < 10 && i + k < n; k++)
+				if (!(p[i + k] & 0x80))
+					break;
+			if (k == 10 || i + k >= n)
+				return -1;
+			vlen = k + 1;
+		} else if (wt == 1) {
+			vlen = 8;
+		} else if (wt == 5) {
+			vlen = 4;
+		} else if (wt == 2) {
+			uint64_t l = 0;
+			for (k = 0; k < 5 && i + k < n; k++) {
+				l |= (uint64_t)(p[i + k] & 0x7f) << (7 * k);
+				if (!(p[i + k] & 0x80))
+					break;
+			}
+			if (k == 5 || i + k >= n)
+				return -1;
+			vlen = k + 1 + l;
+		} else {
+			return -1;
+		}
+		if (vlen > n - i)
+			return -1;
+		if (fn >= 1 && fn <= 5) {
+			if (wt != want_wt[fn])
+				return -1;
+			uint64_t le = 0;
+			int any = 0;
+			for (size_t b = 0; b < vlen; b++) {
+				if (wt != 0)
+					le |= (uint64_t)v[b] << (8 * b);
+				else if (v[b] & 0x7f)
+					any = 1;
+			}
+			switch (fn) {
+			case 1: *off = (int64_t)le; break;
+			case 2: *seq = (int64_t)le; break;
+			case 3: *last = (uint8_t)any; break;
+			case 4: *dlen = (int32_t)(uint32_t)le; break;
+			case 5: *sync = (uint8_t)any; break;
+			}
+			if (fn <= 4)
+				have |= 1 << fn;
+		}
+		i += vlen;
+	}
+	return have == 0x1e ? 0 : -1;
+}
+
+/* Per-chunk verify of one packet: every chunk, not only up to the first
+ * mismatch (the build's per-packet report); the reference's verdict is the
+ * first mismatch (src/datanode.c:2945-2960). */
+static void verify_one(const uint8_t *crcs, const uint8_t *data, int32_t dlen, uint32_t cs,
+    int ctype, struct oracle_packet *k)
+{
+	for (int64_t i = 0; i < ((int64_t)dlen + cs - 1) / cs; i++) {
+		int64_t clen = dlen - i * (int64_t)cs;
+		if (clen > cs)
+			clen = cs;
+		if (crc_of(ctype, 0, data + i * cs, (size_t)clen) != be32dec(crcs + 4 * i)) {
+			if (k->first_bad < 0)
+				k->first_bad = (int32_t)i;
+			k->bad_chunks++;
+			k->error = ORACLE_ERR_BAD_CHECKSUM;
+		}
+	}
+}
+
+/* Returns the first packet error in stream order (0 if none); *npkts
+ * records and *consumed bytes as documented for hdfs_crc32c_verify_packets. */
+int oracle_verify_packets(const uint8_t *s, uint64_t len, int proto, uint32_t cs, int ctype,
+    int do_verify, struct oracle_packet *out, size_t max_pkts, size_t *npkts, uint64_t *consumed)
+{
+	size_t n = 0;
+	uint64_t pos = 0;
+	*consumed = 0;
+	while (n < max_pkts) {
+		struct oracle_packet k;
+		memset(&k, 0, sizeof(k));
+		k.stream_off = pos;
+		k.first_bad = -1;
+		const uint8_t *p = s + pos;
+		uint64_t rem = len - pos;
+		int64_t plen, dlen;
+		if (proto == 1) { /* v1: src/datanode.c:2363-2384 */
+			if (rem < 25)
+				break;
+			plen = rd_be(p, 4);
+			k.offset_in_block = rd_be(p + 4, 8);
+			k.seqno = rd_be(p + 12, 8);
+			k.last = rd_be(p + 20, 1) != 0;
+			dlen = rd_be(p + 21, 4);
+			k.header_len = 25;
+		} else { /* v2: src/datanode.c:2387-2418 */
+			if (rem < 6)
+				break;
+			plen = rd_be(p, 4);
+			uint16_t hlen = (uint16_t)rd_be(p + 4, 2);
+			if (rem < 6u + hlen)
+				break;
+			k.header_len = 6u + hlen;
+			int32_t d32 = 0;
+			if (pb_header(p + 6, hlen, &k.offset_in_block, &k.seqno, &k.last, &d32, &k.sync)) {
+				k.offset_in_block = k.seqno = 0;
+				k.last = k.sync = 0;
+				k.error = ORACLE_ERR_INVALID_PACKETHEADERPROTO;
+				out[n++] = k;
+				break;
+			}
+			dlen = d32;
+		}
+		/* _process_recv_packet: src/datanode.c:2428-2446 */
+		int64_t crcdlen = plen - dlen - 4;
+		const int64_t onegb = 1024 * 1024 * 1024;
+		k.data_len = (int32_t)dlen;
+		k.crc_len = (int32_t)crcdlen;
+		if (plen < 0 || dlen < 0 || dlen > onegb || plen > onegb || crcdlen < 0)
+			k.error = ORACLE_ERR_PACKET_SIZE;
+		else if (ctype != 0 && crcdlen != ((dlen + cs - 1) / cs) * 4)
+			k.error = ORACLE_ERR_CRC_LEN;
+		else if (ctype == 0 && crcdlen > 0)
+			k.error = ORACLE_ERR_UNEXPECTED_CRC_LEN;
+		if (k.error) {
+			out[n++] = k;
+			break;
+		}
+		if (dlen == 0) { /* src/datanode.c:2448-2456 */
+			if (!k.last)
+				k.error = ORACLE_ERR_PACKET_SIZE;
+			else
+				*consumed = pos + k.header_len;
+			out[n++] = k;
+			break;
+		}
+		uint64_t total = k.header_len + (uint64_t)crcdlen + (uint64_t)dlen;
+		if (rem < total)
+			break;
+		if (do_verify && crcdlen > 0)
+			verify_one(p + k.header_len, p + k.header_len + crcdlen, (int32_t)dlen, cs, ctype, &k);
+		out[n++] = k;
+		pos += total;
+		*consumed = pos;
+	}
+	*npkts = n;
+	for (size_t i = 0; i < n; i++)
+		if (out[i].error)
+			return out[i].error;
+	return 0;
+}
+
+/* ------------------------------------------------------------------ */
 /* Synthetic data: LE u64 words w[g] = splitmix64(seed,g) */
 /* ------------------------------------------------------------------ */
 static inline uint64_t splitmix64(uint64_t seed, uint64_t g)

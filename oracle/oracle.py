@@ -37,7 +37,15 @@ def _bind(lib, name, restype, argtypes):
     return f
 
 
-CSUM_CRC32, CSUM_CRC32C = 1, 2  # include/hadoofus/objects.h:173-174
+CSUM_NULL, CSUM_CRC32, CSUM_CRC32C = 0, 1, 2  # include/hadoofus/objects.h:172-174
+
+
+class OraclePacket(ctypes.Structure):
+    """struct oracle_packet (same layout as hdfs_crc32c_packet)."""
+    _fields_ = [("stream_off", _u64), ("offset_in_block", ctypes.c_int64), ("seqno", ctypes.c_int64),
+                ("data_len", ctypes.c_int32), ("crc_len", ctypes.c_int32), ("header_len", _u32),
+                ("error", ctypes.c_int32), ("first_bad", ctypes.c_int32), ("bad_chunks", _u32),
+                ("last", ctypes.c_uint8), ("sync", ctypes.c_uint8), ("reserved", ctypes.c_uint8 * 6)]
 
 
 class Oracle:
@@ -61,6 +69,9 @@ class Oracle:
         self._fill = _bind(lib, "oracle_splitmix_fill", None, [_vp, _u64, _u64, _u64])
         self._bench = _bind(lib, "oracle_bench_chunks", ctypes.c_double,
                             [_vp, _u64, _u32, ctypes.c_int, ctypes.c_int, _vp, _vp])
+        self._pk = _bind(lib, "oracle_verify_packets", ctypes.c_int,
+                         [_vp, _u64, ctypes.c_int, _u32, ctypes.c_int, ctypes.c_int,
+                          ctypes.POINTER(OraclePacket), _sz, ctypes.POINTER(_sz), ctypes.POINTER(_u64)])
         self.have_hw = bool(_bind(lib, "oracle_have_hw", ctypes.c_int, [])())
 
     @staticmethod
@@ -106,6 +117,20 @@ class Oracle:
         code = 2 if ctype == CSUM_CRC32 else (1 if (hw and self.have_hw) else 0)
         self._chunks(p, n, chunk, out.ctypes.data, code)
         return out
+
+    def verify_packets(self, stream, proto=2, chunk_size=512, ctype=CSUM_CRC32C, max_pkts=None, verify=True):
+        """Packet-stream framing + per-chunk verify (src/datanode.c:2345-2494).
+        -> (rc, [packet dicts], consumed)."""
+        p, n = self._buf(stream)
+        if max_pkts is None:
+            max_pkts = n // (25 if proto == 1 else 6) + 1
+        arr = (OraclePacket * max(1, max_pkts))()
+        npk, used = _sz(0), _u64(0)
+        rc = self._pk(p, n, proto, chunk_size, ctype, int(verify), arr, max_pkts, ctypes.byref(npk),
+                      ctypes.byref(used))
+        out = [{f: getattr(arr[i], f) for f, _ in OraclePacket._fields_ if f != "reserved"}
+               for i in range(npk.value)]
+        return rc, out, used.value
 
     def splitmix(self, nwords, seed=0, g0=0):
         out = np.empty(nwords, dtype=np.uint64)

@@ -1,0 +1,129 @@
+"""Packet-stream framing + verify (src/datanode.c:2345-2494, 2931-2963).
+
+CPU: the oracle against the constructed fixtures of
+oracle/gen_golden_packets.py, and the engine's host-side framing walk
+(hdfs_crc32c_parse_packets, no device work) against the same fixtures.
+GPU: hdfs_crc32c_verify_packets against the fixtures and, on large
+generated streams, against the oracle."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from packet_stream import CSUM_CRC32, CSUM_CRC32C, assemble, build_stream
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "packet_cases.json")
+BAD = 29
+
+
+def _cases():
+    with open(GOLDEN) as f:
+        return json.load(f)["cases"]
+
+
+CASES = _cases()
+
+
+def _stream(case):
+    s = assemble(case["parts"])
+    return s[:case["cut"]] if "cut" in case else s
+
+
+def _framing_only(pkts):
+    """Expected records of a framing-only walk: checksum verdicts cleared."""
+    out = []
+    for p in pkts:
+        p = dict(p)
+        if p["error"] == BAD:
+            p.update(error=0, first_bad=-1, bad_chunks=0)
+        out.append(p)
+    return out
+
+
+def _args(case):
+    return case["proto"], case["chunk_size"], case["ctype"], case["max_pkts"]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_oracle_packets_fixture(oracle, case):
+    rc, pkts, used = oracle.verify_packets(_stream(case), *_args(case))
+    assert (rc, used) == (case["expect"]["rc"], case["expect"]["consumed"])
+    assert pkts == case["expect"]["packets"]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_engine_parse_fixture(case):
+    import hadoofus_amd as h
+    want = _framing_only(case["expect"]["packets"])
+    rc, pkts, used = h.parse_packets(_stream(case), *_args(case))
+    assert pkts == want
+    assert used == case["expect"]["consumed"]
+    assert rc == next((p["error"] for p in want if p["error"]), 0)
+
+
+def test_engine_parse_rejects_bad_args():
+    import hadoofus_amd as h
+    for kw in (dict(proto=3), dict(ctype=5), dict(chunk_size=0)):
+        with pytest.raises(h.CRC32CError):
+            h.parse_packets(b"\0" * 64, **kw)
+
+
+def test_builder_streams_match_oracle(oracle):
+    """The generated streams used at GPU scale are what the oracle expects."""
+    s, bad = build_stream(oracle.crc32c, 2, 512, CSUM_CRC32C, [65536] * 5 + [777], corrupt=[(1, 3), (5, 1)])
+    rc, pkts, used = oracle.verify_packets(s)
+    assert rc == BAD and used == len(s) and len(pkts) == 7
+    assert [p["first_bad"] for p in pkts] == [-1, 3, -1, -1, -1, 1, -1]
+
+
+# --- GPU ---------------------------------------------------------------------
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_gpu_verify_packets_fixture(engine, case):
+    rc, pkts, used = engine.verify_packets(_stream(case), *_args(case))
+    assert pkts == case["expect"]["packets"]
+    assert (rc, used) == (case["expect"]["rc"], case["expect"]["consumed"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("proto,cs,ctype,dlen,npk", [
+    (2, 512, CSUM_CRC32C, 65536, 2100),    # ~131 MiB: three 64 MiB pieces, both slots
+    (1, 512, CSUM_CRC32C, 65536, 300),
+    (2, 512, CSUM_CRC32, 65536, 300),
+    (2, 4096, CSUM_CRC32C, 61440, 200),
+    (2, 512, CSUM_CRC32C, 40000, 500),     # partial last chunk in every packet
+])
+def test_gpu_verify_packets_large_vs_oracle(engine, oracle, proto, cs, ctype, dlen, npk):
+    rng = np.random.default_rng(npk + cs + proto)
+    nch = (dlen + cs - 1) // cs
+    corrupt = [(int(rng.integers(0, npk)), int(rng.integers(0, nch))) for _ in range(25)]
+    dl = [dlen] * (npk - 1) + [dlen // 3 + 1]
+    s, bad = build_stream(oracle.crc32c, proto, cs, ctype, dl, seed=npk, corrupt=corrupt)
+    want = oracle.verify_packets(s, proto, cs, ctype)
+    got = engine.verify_packets(s, proto, cs, ctype)
+    assert got[0] == want[0] == BAD
+    assert got[2] == want[2] == len(s)
+    assert got[1] == want[1]
+    assert {k: (p["first_bad"], p["bad_chunks"]) for k, p in enumerate(got[1]) if p["error"]} == \
+        {k: (v[0], len(v)) for k, v in bad.items()}
+
+
+@pytest.mark.gpu
+def test_gpu_verify_packets_huge_packet(engine, oracle):
+    """A packet larger than the 64 MiB piece gets a piece of its own."""
+    dl = [65536, (80 << 20) + 100, 65536]
+    s, bad = build_stream(oracle.crc32c, 2, 512, CSUM_CRC32C, dl, seed=5, corrupt=[(1, 0), (1, 163840), (2, 7)])
+    got = engine.verify_packets(s)
+    assert got == oracle.verify_packets(s)
+    assert got[1][1]["bad_chunks"] == 2 and got[1][1]["first_bad"] == 0
+
+
+@pytest.mark.gpu
+def test_gpu_verify_packets_pinned_stream(engine, oracle):
+    s, _ = build_stream(oracle.crc32c, 2, 512, CSUM_CRC32C, [65536] * 64, seed=9, corrupt=[(10, 10)])
+    pin = engine.PinnedBuffer(len(s))
+    pin.array[:] = np.frombuffer(s, np.uint8)
+    got = engine.verify_packets(pin.array)
+    assert got == oracle.verify_packets(s)
+    pin.free()
