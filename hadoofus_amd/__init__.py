@@ -32,6 +32,7 @@ from .abi import (  # noqa: F401
     Segment,
     crc32c,
     compose_crcs,
+    composite_crcs,
     compute_host,
     verify_host,
     PinnedBuffer,

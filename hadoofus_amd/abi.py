@@ -113,6 +113,7 @@ def load(path=LIB_PATH):
     for name in ("hdfs_crc32c_parse_packets", "hdfs_crc32c_verify_packets"):
         _bind(lib, name, _int, [_vp, _u64, _int, _u32, _int, ctypes.POINTER(Packet), _sz,
                                 ctypes.POINTER(_sz), ctypes.POINTER(_u64)])
+    _bind(lib, "hdfs_crc32c_composite_crcs", _int, [ctypes.POINTER(Segment), _sz, ctypes.POINTER(_u32)])
     _bind(lib, "hdfs_crc32c_dev_alloc", _int, [ctypes.POINTER(_vp), _u64])
     _bind(lib, "hdfs_crc32c_dev_free", _int, [_vp])
     _bind(lib, "hdfs_crc32c_memcpy", _int, [_vp, _vp, _u64, _int])
@@ -202,6 +203,15 @@ def _packets(fn, stream, proto, chunk_size, ctype, max_pkts):
     if rc < 0:
         _check(rc)
     return rc, [arr[i].as_dict() for i in range(npk.value)], used.value
+
+
+def composite_crcs(segments):
+    """Whole-segment CRCs from each segment's device chunk-CRC array."""
+    n = len(segments)
+    arr = (Segment * max(1, n))(*segments)
+    out = (_u32 * max(1, n))()
+    _check(load().hdfs_crc32c_composite_crcs(arr, n, out))
+    return [out[i] for i in range(n)]
 
 
 def parse_packets(stream, proto=PROTO_V2, chunk_size=512, ctype=CSUM_CRC32C, max_pkts=None):

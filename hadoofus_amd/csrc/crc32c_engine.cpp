@@ -38,6 +38,8 @@ hipError_t launch_combine(const uint32_t *raws, uint64_t nraw, uint32_t cs, uint
 hipError_t launch_fill(uint64_t *out, uint64_t nwords, uint64_t seed, uint64_t g0, hipStream_t stream);
 hipError_t launch_corrupt(uint8_t *data, uint64_t len, uint32_t cs, uint64_t chunk0, uint64_t modulus,
                           uint64_t bitmul, hipStream_t stream);
+hipError_t launch_composite(const SegDev *segs, uint32_t nseg, const uint64_t *run_prefix, uint64_t total_runs,
+                            const uint32_t *pow2, uint32_t *out, hipStream_t stream);
 hipError_t launch_gather(const uint8_t *raw, const PktDesc *descs, uint32_t npk, uint32_t units, uint8_t *arena,
                          uint8_t *crc_arena, hipStream_t stream);
 
@@ -1184,6 +1186,52 @@ int hdfs_crc32c_probe_read(const void *dptr, uint64_t bytes, void *stream, int i
   (void)hipEventDestroy(a);
   (void)hipEventDestroy(b);
   *gbps = double(bytes) * iters / (ms * 1e-3) / 1e9;
+  return HDFS_CRC32C_OK;
+}
+
+int hdfs_crc32c_composite_crcs(const hdfs_crc32c_segment *segs, size_t nseg, uint32_t *out) {
+  if (nseg && (!segs || !out)) return fail(HDFS_CRC32C_EINVAL, "null segments / out");
+  if (nseg > 0xFFFFFFF0u) return fail(HDFS_CRC32C_EINVAL, "too many segments");
+  if (!nseg) return HDFS_CRC32C_OK;
+  DevCtx *cp = nullptr;
+  int rc = ctx_init(-1, &cp);
+  if (rc) return rc;
+  DevCtx &c = *cp;
+  DeviceGuard g(c.dev);
+  const int ctype = seg_ctype(segs[0].flags);
+  std::vector<SegDev> host(nseg);
+  std::vector<uint64_t> prefix(nseg);
+  uint64_t runs = 0;
+  for (size_t i = 0; i < nseg; i++) {
+    rc = fill_seg(segs[i], HDFS_CRC32C_MODE_COMPUTE, host[i], i);
+    if (rc) return rc;
+    if (seg_ctype(segs[i].flags) != ctype)
+      return fail(HDFS_CRC32C_EINVAL, "segment %zu: CRC32/CRC32C mixed in one call", i);
+    if (segs[i].crc_init && !(segs[i].flags & HDFS_CRC32C_SEG_RAW))
+      return fail(HDFS_CRC32C_EINVAL, "segment %zu: composite needs chunk CRCs started from 0", i);
+    if (segs[i].len && !device_accessible(segs[i].crcs))
+      return fail(HDFS_CRC32C_EINVAL, "segment %zu: crcs is not device-accessible memory", i);
+    prefix[i] = runs;
+    runs += (uint64_t(host[i].nchunks) + 63) / 64;
+  }
+  std::lock_guard<std::mutex> lk(c.mu);
+  SegDev *d_segs = nullptr;
+  uint64_t *d_prefix = nullptr;
+  uint32_t *d_out = nullptr;
+  hipError_t e = hipMalloc(&d_segs, nseg * sizeof(SegDev));
+  if (e == hipSuccess) e = hipMalloc(&d_prefix, nseg * 8);
+  if (e == hipSuccess) e = hipMalloc(&d_out, nseg * 4);
+  if (e == hipSuccess) e = hipMemcpyAsync(d_segs, host.data(), nseg * sizeof(SegDev), hipMemcpyHostToDevice, c.stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(d_prefix, prefix.data(), nseg * 8, hipMemcpyHostToDevice, c.stream);
+  if (e == hipSuccess) e = hipMemsetAsync(d_out, 0, nseg * 4, c.stream);
+  if (e == hipSuccess)
+    e = launch_composite(d_segs, uint32_t(nseg), d_prefix, runs, c.d_tab_pow2_t[ctype], d_out, c.stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(out, d_out, nseg * 4, hipMemcpyDefault, c.stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c.stream);
+  if (d_segs) (void)hipFree(d_segs);
+  if (d_prefix) (void)hipFree(d_prefix);
+  if (d_out) (void)hipFree(d_out);
+  if (e != hipSuccess) return fail(HDFS_CRC32C_EHIP, "composite: %s", hipGetErrorString(e));
   return HDFS_CRC32C_OK;
 }
 

@@ -594,6 +594,51 @@ __global__ __launch_bounds__(256) void crc32c_combine_kernel(
   if ((threadIdx.x & 63u) == 0 && v) atomicXor(acc, v);
 }
 
+// Composite CRC of whole segments from their chunk CRCs (no data re-read):
+// c(A||B) = Z_|B|(c(A)) ^ c(B), so c(seg) = XOR_i Z_{bytes after chunk i}(c_i).
+// One thread folds a run of kCompRun chunks sequentially
+// (acc = Z_{len_i}(acc) ^ c_i, one table application per chunk for
+// power-of-two chunk sizes), then shifts its partial past the rest of the
+// segment; partials XOR-reduce per wave (or per lane when a wave straddles
+// two segments) into out[seg].
+constexpr uint32_t kCompRun = 64;
+
+__global__ __launch_bounds__(256) void composite_kernel(const SegDev *__restrict__ segs, uint32_t nseg,
+                                                         const uint64_t *__restrict__ run_prefix,
+                                                         uint64_t total_runs, const uint32_t *__restrict__ pow2,
+                                                         uint32_t *__restrict__ out) {
+  const uint64_t r = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  uint32_t s = 0, v = 0;
+  if (r < total_runs) {
+    uint32_t lo = 0, hi = nseg - 1;  // last segment with run_prefix <= r
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi + 1) >> 1;
+      if (run_prefix[mid] <= r) lo = mid; else hi = mid - 1;
+    }
+    s = lo;
+    const SegDev sg = segs[s];
+    const uint64_t j = r - run_prefix[s];
+    const uint64_t c0 = j * kCompRun, c1 = min(c0 + kCompRun, static_cast<uint64_t>(sg.nchunks));
+    uint32_t acc = 0;
+    for (uint64_t i = c0; i < c1; i++) {
+      const uint64_t l = min(static_cast<uint64_t>(sg.chunk_size), sg.len - i * sg.chunk_size);
+      uint32_t c = sg.crcs[i];
+      if (sg.flags & kSegBigEndian) c = __builtin_bswap32(c);
+      acc = zapply(pow2, acc, l) ^ c;
+    }
+    const uint64_t end = min(c1 * sg.chunk_size, sg.len);
+    v = zapply(pow2, acc, sg.len - end);
+  }
+  const uint32_t s0 = __builtin_amdgcn_readfirstlane(s);
+  if (__all(s == s0)) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v ^= __shfl_xor(v, off);
+    if ((threadIdx.x & 63u) == 0 && v) atomicXor(out + s0, v);
+  } else if (v) {
+    atomicXor(out + s, v);
+  }
+}
+
 // splitmix64 synthetic blocks: w[k] = splitmix64(seed, g0 + k).
 DEV uint64_t splitmix64(uint64_t seed, uint64_t g) {
   uint64_t z = seed + (g + 1) * 0x9E3779B97F4A7C15ull;
@@ -808,6 +853,15 @@ hipError_t launch_combine(const uint32_t *raws, uint64_t nraw, uint32_t cs, uint
   const uint32_t blocks = static_cast<uint32_t>((n + 255) / 256);
   hipLaunchKernelGGL(crc32c_combine_kernel, dim3(blocks), dim3(256), 0, stream, raws, nraw, cs, len,
                      pow2, reg0, acc);
+  return hipGetLastError();
+}
+
+hipError_t launch_composite(const SegDev *segs, uint32_t nseg, const uint64_t *run_prefix, uint64_t total_runs,
+                            const uint32_t *pow2, uint32_t *out, hipStream_t stream) {
+  if (!total_runs) return hipSuccess;
+  const uint32_t blocks = static_cast<uint32_t>((total_runs + 255) / 256);
+  hipLaunchKernelGGL(composite_kernel, dim3(blocks), dim3(256), 0, stream, segs, nseg, run_prefix, total_runs, pow2,
+                     out);
   return hipGetLastError();
 }
 

@@ -116,6 +116,17 @@ int hdfs_crc32c_stream_dev(uint32_t crc, const void *dbuf, uint64_t len, uint32_
  * crc32(crc, buf, len) (the CRC32 branch of src/datanode.c:2845,2952). */
 int hdfs_crc32c_stream_ex(int ctype, uint32_t crc, const void *buf, uint64_t len, uint32_t *out);
 
+/* Block composite CRC (the COMPOSITE_CRC block checksum of
+ * src/proto/datatransfer.proto:316-322, src/proto/hdfs.proto:483-497, which
+ * the reference declares but does not compute): for each segment, the CRC of
+ * its whole data, derived from the per-chunk CRCs in segs[i].crcs (device
+ * memory, as a compute plan wrote them: wire order if HDFS_CRC32C_SEG_BE,
+ * CRC32 tables if HDFS_CRC32C_SEG_CRC32) with the combine identity
+ * c(A||B) = Z_|B|(c(A)) ^ c(B) -- the data is not re-read.  crc_init must be
+ * 0 (or SEG_RAW: raw registers combine the same way).  out: host or device
+ * u32[nseg]; synchronous. */
+int hdfs_crc32c_composite_crcs(const hdfs_crc32c_segment *segs, size_t nseg, uint32_t *out);
+
 /* ---- datanode mirrors on host memory (synchronous) ---------------------- */
 /* _verify_crcdata (src/datanode.c:2931-2963) plus the CRC-length framing
  * check of _process_recv_packet (src/datanode.c:2441-2442) on a packet region
