@@ -40,6 +40,7 @@ hipError_t launch_corrupt(uint8_t *data, uint64_t len, uint32_t cs, uint64_t chu
                           uint64_t bitmul, hipStream_t stream);
 hipError_t launch_composite(const SegDev *segs, uint32_t nseg, const uint64_t *run_prefix, uint64_t total_runs,
                             const uint32_t *pow2, uint32_t *out, hipStream_t stream);
+hipError_t launch_prep(uint32_t *fb, uint32_t nfb, unsigned long long *mism, uint32_t *gctr, hipStream_t stream);
 hipError_t launch_gather(const uint8_t *raw, const PktDesc *descs, uint32_t npk, uint32_t units, uint8_t *arena,
                          uint8_t *crc_arena, hipStream_t stream);
 
@@ -267,16 +268,15 @@ int launch_all(DevCtx &c, int mode, const SegDev *d_segs, uint32_t nseg, uint64_
                uint64_t mtiles, uint64_t gtiles, uint32_t *d_fb, unsigned long long *d_mism,
                uint32_t *d_gctr, hipStream_t st, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr,
                bool reset = true, int ctype = 0) {
-  if (mode == kModeVerify && reset) {
-    HIPCHK(hipMemsetAsync(d_fb, 0xFF, sizeof(uint32_t) * (nseg ? nseg : 1), st));
-    HIPCHK(hipMemsetAsync(d_mism, 0, sizeof(unsigned long long), st));
-  }
+  const bool vreset = mode == kModeVerify && reset;
+  uint32_t *gz = (rounds && g_tile_order == 2) ? d_gctr : nullptr;
+  if (vreset || gz)
+    HIPCHK(launch_prep(vreset ? d_fb : nullptr, vreset ? (nseg ? nseg : 1u) : 0u, vreset ? d_mism : nullptr, gz, st));
   if (rounds) {
     // >= 4 rounds per wave (16 waves per block) before adding blocks: each
     // block pays a ~156 KiB LDS table fill.
     uint64_t want = (rounds + 63) / 64;
     int grid = static_cast<int>(want < 1 ? 1 : (want > uint64_t(c.num_cu) ? c.num_cu : want));
-    if (g_tile_order == 2) HIPCHK(hipMemsetAsync(d_gctr, 0, sizeof(uint32_t), st));
     if (ev0) HIPCHK(hipEventRecord(ev0, st));
     HIPCHK(launch_tiles(mode, g_tile_order, g_nt_loads, g_depth, grid, d_segs, nseg, rounds, mtiles,
                         c.d_tab_main_t[ctype], d_fb, d_mism, g_diag, g_store_policy, d_gctr, st));

@@ -139,8 +139,11 @@ struct Cursor {
 //    that workgroups claim with one global atomic each once their own slice
 //    is done (published to the workgroup's other waves through an LDS slot).
 //    The pool absorbs the cross-workgroup / cross-XCD speed spread; its
-//    atomics only happen at the end, off the hot loop.
-constexpr uint32_t kUnit = 256;       // tiles per global pool unit
+//    atomics only happen at the end, off the hot loop.  Unit size (runtime,
+//    a power of two in [16, 256]) targets >= 4 units per workgroup; launches
+//    with < 32 rounds per wave skip the pool (one unit per workgroup would
+//    make the tail, not shorten it).
+constexpr uint32_t kUnitMaxShift = 8, kUnitMinShift = 4;
 constexpr uint32_t kSlots = 8;        // LDS slots for published units
 constexpr uint64_t kPhase1Num = 23, kPhase1Den = 25;  // 92 % static
 
@@ -154,6 +157,7 @@ struct Sched {
   uint64_t ntiles;   // ORDER 2: total tiles
   uint32_t *gctr;    // ORDER 2: global unit counter (zeroed per launch)
   uint64_t *slots;   // ORDER 2: LDS [kSlots] of (unit + 1) << 32 | global unit
+  uint32_t ushift;   // ORDER 2: log2 tiles per pool unit
 };
 
 DEV uint32_t grab(const Sched &w) {
@@ -171,7 +175,7 @@ DEV bool ticket_tile(const Sched &w, uint32_t t, uint64_t &g) {
     return true;
   }
   if (ORDER != 2) return false;
-  const uint32_t j = t - w.nk, u = j / kUnit, o = j % kUnit, s = u % kSlots;
+  const uint32_t j = t - w.nk, u = j >> w.ushift, o = j & ((1u << w.ushift) - 1u), s = u % kSlots;
   if (o == 0) {  // first ticket of local unit u: claim a pool unit and publish it
     uint32_t gu = 0;
     if (w.lane == 0) gu = atomicAdd(w.gctr, 1u);
@@ -180,12 +184,12 @@ DEV bool ticket_tile(const Sched &w, uint32_t t, uint64_t &g) {
       __hip_atomic_store(&w.slots[s], (uint64_t(u + 1) << 32) | gu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
   uint64_t v;
-  for (;;) {  // the publisher is a running wave that already holds ticket u*kUnit
+  for (;;) {  // the publisher is a running wave that already holds ticket u << ushift
     v = __hip_atomic_load(&w.slots[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (rfl(static_cast<uint32_t>(v >> 32)) == u + 1) break;
     __builtin_amdgcn_s_sleep(2);
   }
-  g = w.p2first + uint64_t(rfl(static_cast<uint32_t>(v))) * kUnit + o;
+  g = w.p2first + (uint64_t(rfl(static_cast<uint32_t>(v))) << w.ushift) + o;
   return g < w.ntiles;
 }
 
@@ -350,12 +354,33 @@ __global__ __launch_bounds__(1024) void crc32c_tiles_kernel(
 
   if (threadIdx.x < 2 + 2 * kSlots) lds[kLdsWords + threadIdx.x] = 0u;
   // LDS image: word (P*16384 + e*64 + h*32 + l) = t_{3-(2P+h)}[e] for all 32 l.
-  for (uint32_t idx = threadIdx.x; idx < kLdsSliceBytes / 4; idx += blockDim.x) {
-    const uint32_t P = idx >> 14, e = (idx >> 6) & 255u, h = (idx >> 5) & 1u;
-    lds[idx] = gtab[(3u - (2u * P + h)) * 256u + e];
+  // Filled with 16-B stores, consecutive lanes on consecutive 16 B (no bank
+  // conflicts); the 8 source words a lane needs are loaded up front so the
+  // fill costs about one L2 round trip, not one per store.
+  {
+    constexpr uint32_t kQ = kLdsSliceBytes / 16 / 1024;  // 16-B stores per thread (blockDim 1024)
+    uint32_t v[kQ];
+#pragma unroll
+    for (uint32_t k = 0; k < kQ; k++) {
+      const uint32_t idx = 4u * (k * 1024u + threadIdx.x);
+      const uint32_t P = idx >> 14, e = (idx >> 6) & 255u, h = (idx >> 5) & 1u;
+      v[k] = gtab[(3u - (2u * P + h)) * 256u + e];
+    }
+    u32x4 z[2];
+#pragma unroll
+    for (uint32_t k = 0; k < 2; k++) {
+      const uint32_t q = k * 1024u + threadIdx.x;
+      z[k] = q < kTabZposWords / 4 ? gload16(gtab + kTabSliceWords + 4u * q) : u32x4{0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kQ; k++)
+      *reinterpret_cast<u32x4 *>(&lds[4u * (k * 1024u + threadIdx.x)]) = u32x4{v[k], v[k], v[k], v[k]};
+#pragma unroll
+    for (uint32_t k = 0; k < 2; k++) {
+      const uint32_t q = k * 1024u + threadIdx.x;
+      if (q < kTabZposWords / 4) *reinterpret_cast<u32x4 *>(&lds[kLdsSliceBytes / 4 + 4u * q]) = z[k];
+    }
   }
-  for (uint32_t w = threadIdx.x; w < kTabZposWords; w += blockDim.x)
-    lds[kLdsSliceBytes / 4 + w] = gtab[kTabSliceWords + w];
   __syncthreads();
 
   LaneConst L;
@@ -397,13 +422,20 @@ __global__ __launch_bounds__(1024) void crc32c_tiles_kernel(
       }
     }
   } else {
-    const uint64_t r_static = ORDER == 2 ? total_rounds * kPhase1Num / kPhase1Den : total_rounds;
+    const bool pool = ORDER == 2 && total_rounds >= 32ull * nwaves;
+    const uint64_t r_static = pool ? total_rounds * kPhase1Num / kPhase1Den : total_rounds;
     const uint64_t b0 = rfl64(r_static * blockIdx.x / gridDim.x);
     const uint64_t b1 = rfl64(r_static * (blockIdx.x + 1) / gridDim.x);
     w.gfirst = tile_at_round(sg, nseg, b0, total_tiles);
     w.nk = static_cast<uint32_t>(tile_at_round(sg, nseg, b1, total_tiles) - w.gfirst);
     w.p2first = tile_at_round(sg, nseg, r_static, total_tiles);
     w.ntiles = total_tiles;
+    {
+      const uint64_t per = (total_tiles - w.p2first) / (4ull * gridDim.x);
+      w.ushift = per >= (1ull << kUnitMaxShift) ? kUnitMaxShift
+               : per < (1ull << kUnitMinShift) ? kUnitMinShift
+                                               : 63u - static_cast<uint32_t>(__builtin_clzll(per));
+    }
     w.gctr = gctr;
     w.slots = reinterpret_cast<uint64_t *>(&lds[kLdsWords + 2]);
     uint64_t g;
@@ -639,6 +671,19 @@ __global__ __launch_bounds__(256) void composite_kernel(const SegDev *__restrict
   }
 }
 
+// Per-launch reset of the verify results and the pool counter in one launch
+// (instead of up to three hipMemsetAsync fills).
+__global__ __launch_bounds__(256) void prep_kernel(uint32_t *__restrict__ fb, uint32_t nfb,
+                                                    unsigned long long *__restrict__ mism,
+                                                    uint32_t *__restrict__ gctr) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (fb && i < nfb) fb[i] = 0xFFFFFFFFu;
+  if (i == 0) {
+    if (mism) *mism = 0ull;
+    if (gctr) *gctr = 0u;
+  }
+}
+
 // splitmix64 synthetic blocks: w[k] = splitmix64(seed, g0 + k).
 DEV uint64_t splitmix64(uint64_t seed, uint64_t g) {
   uint64_t z = seed + (g + 1) * 0x9E3779B97F4A7C15ull;
@@ -862,6 +907,12 @@ hipError_t launch_composite(const SegDev *segs, uint32_t nseg, const uint64_t *r
   const uint32_t blocks = static_cast<uint32_t>((total_runs + 255) / 256);
   hipLaunchKernelGGL(composite_kernel, dim3(blocks), dim3(256), 0, stream, segs, nseg, run_prefix, total_runs, pow2,
                      out);
+  return hipGetLastError();
+}
+
+hipError_t launch_prep(uint32_t *fb, uint32_t nfb, unsigned long long *mism, uint32_t *gctr, hipStream_t stream) {
+  const uint32_t n = nfb ? nfb : 1u;
+  hipLaunchKernelGGL(prep_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, fb, nfb, mism, gctr);
   return hipGetLastError();
 }
 

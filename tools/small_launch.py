@@ -1,0 +1,73 @@
+"""Small-launch costs (GPU box): per-execute device time of verify plans over
+small inputs and many-segment tables, and the host-side latency of the
+drop-in / datanode-mirror calls.  Prints one JSON object."""
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import hadoofus_amd as h  # noqa: E402
+
+h.load()
+cs = 512
+total = 256 << 20
+dbuf = h.DeviceBuffer(total)
+h.fill_splitmix64(dbuf.ptr, total // 8, 0, 0)
+crcs = h.DeviceBuffer(total // cs * 4)
+bms = h.DeviceBuffer(total // cs // 8 + 64)
+out = {}
+
+
+def segs_of(seg_bytes, n):
+    return [h.Segment(data=dbuf.ptr + i * seg_bytes, len=seg_bytes, chunk_size=cs, flags=h.SEG_BE, crc_init=0,
+                      crcs=crcs.ptr + i * (seg_bytes // cs) * 4, bitmap=bms.ptr + i * (seg_bytes // cs // 8))
+            for i in range(n)]
+
+
+def plan_us(segs, iters):
+    h.Plan(h.MODE_COMPUTE, segs).execute()
+    vp = h.Plan(h.MODE_VERIFY, segs)
+    vp.execute()
+    _, m = vp.results()
+    assert m == 0
+    lib = h.load()
+    ms = ctypes.c_double(0)
+    assert lib.hdfs_crc32c_plan_time(vp.ptr, None, iters, ctypes.byref(ms)) == 0
+    return ms.value * 1e3
+
+
+for name, seg_bytes, n in [("1x64KiB", 65536, 1), ("1x1MiB", 1 << 20, 1), ("1x16MiB", 16 << 20, 1),
+                           ("1x64MiB", 64 << 20, 1), ("1x256MiB", 256 << 20, 1),
+                           ("1024x64KiB", 65536, 1024), ("4096x16KiB", 16384, 4096),
+                           ("16x16MiB", 16 << 20, 16)]:
+    us = plan_us(segs_of(seg_bytes, n), 50 if seg_bytes * n <= (64 << 20) else 10)
+    out[f"verify_{name}_us"] = round(us, 2)
+    out[f"verify_{name}_GBps"] = round(seg_bytes * n * (1 + 4 / cs) / us / 1e3, 1)
+
+# host-side call latency
+x512 = np.frombuffer(os.urandom(512), np.uint8)
+x64k = np.frombuffer(os.urandom(65536), np.uint8)
+for name, buf in [("512B", x512), ("64KiB", x64k)]:
+    h.crc32c(0, buf)
+    t0 = time.perf_counter()
+    for _ in range(200):
+        h.crc32c(0, buf)
+    out[f"dropin_host_{name}_us"] = round((time.perf_counter() - t0) / 200 * 1e6, 1)
+t0 = time.perf_counter()
+for _ in range(200):
+    h.stream_crc_dev(0, dbuf.ptr, 65536)
+out["stream_dev_64KiB_us"] = round((time.perf_counter() - t0) / 200 * 1e6, 1)
+be = h.compose_crcs([x64k.tobytes()], 512)
+region = be + x64k.tobytes()
+h.verify_crcdata(region, 512, len(be), 65536)
+t0 = time.perf_counter()
+for _ in range(200):
+    rc, _ = h.verify_crcdata(region, 512, len(be), 65536)
+    assert rc == 0
+out["verify_crcdata_64KiB_us"] = round((time.perf_counter() - t0) / 200 * 1e6, 1)
+print(json.dumps(out))
