@@ -294,3 +294,35 @@ def test_dropin_consumer_runs(engine, tmp_path):
     p = subprocess.run([str(exe), str(txt)], capture_output=True, text=True, timeout=120)
     assert p.returncode == 0, p.stdout + p.stderr
     assert "0 failures" in p.stdout
+
+
+def test_segment_beyond_4gib(engine, oracle):
+    """One 5 GiB segment (10.5 M chunks): 64-bit byte offsets everywhere.
+    Sampled chunk CRCs against the oracle (data regenerated by formula),
+    the C3 corruption pattern across the 4 GiB boundary, and the composite
+    of the whole segment against its data-reading stream CRC."""
+    n, cs = 5 << 30, 512
+    dbuf = engine.DeviceBuffer(n)
+    engine.fill_splitmix64(dbuf.ptr, n // 8, 0, 0)
+    nch = n // cs
+    crcs = engine.DeviceBuffer(nch * 4)
+    bm = engine.DeviceBuffer(nch // 8)
+    seg = engine.Segment(data=dbuf.ptr, len=n, chunk_size=cs, flags=engine.SEG_BE, crc_init=0,
+                         crcs=crcs.ptr, bitmap=bm.ptr)
+    engine.Plan(engine.MODE_COMPUTE, [seg]).execute()
+    got = crcs.download(dtype=">u4").astype(np.uint32)
+    rng = np.random.default_rng(4)
+    picks = sorted(set([0, nch - 1, (4 << 30) // cs - 1, (4 << 30) // cs] +
+                       [int(x) for x in rng.integers(0, nch, 200)]))
+    for i in picks:
+        data = splitmix64_np(cs // 8, seed=0, g0=i * (cs // 8)).view(np.uint8)
+        assert got[i] == oracle.crc32c(0, data, "hw"), i
+    assert engine.composite_crcs([seg])[0] == engine.stream_crc_dev(0, dbuf.ptr, n)
+    engine.corrupt(dbuf.ptr, n, cs, 0, 65537, 7919)
+    vp = engine.Plan(engine.MODE_VERIFY, [seg])
+    vp.execute()
+    fb, m = vp.results()
+    expected = list(range(0, nch, 65537))
+    assert m == len(expected) and fb[0] == 0
+    bits = np.unpackbits(bm.download(), bitorder="little")
+    assert list(np.nonzero(bits)[0]) == expected
