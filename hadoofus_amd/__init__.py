@@ -30,6 +30,7 @@ from .abi import (  # noqa: F401
     DeviceBuffer,
     Plan,
     Segment,
+    Session,
     crc32c,
     compose_crcs,
     composite_crcs,

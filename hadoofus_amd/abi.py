@@ -113,6 +113,13 @@ def load(path=LIB_PATH):
     for name in ("hdfs_crc32c_parse_packets", "hdfs_crc32c_verify_packets"):
         _bind(lib, name, _int, [_vp, _u64, _int, _u32, _int, ctypes.POINTER(Packet), _sz,
                                 ctypes.POINTER(_sz), ctypes.POINTER(_u64)])
+    _bind(lib, "hdfs_crc32c_session_create", _int, [ctypes.POINTER(_vp), _int, _u32, _int, _u64, _sz])
+    _bind(lib, "hdfs_crc32c_session_buffer", _int, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_u64)])
+    _bind(lib, "hdfs_crc32c_session_commit", _int, [_vp, _u64])
+    _bind(lib, "hdfs_crc32c_session_flush", _int, [_vp])
+    _bind(lib, "hdfs_crc32c_session_poll", _int, [_vp, ctypes.POINTER(Packet), _sz, ctypes.POINTER(_sz), _int])
+    _bind(lib, "hdfs_crc32c_session_pending", _int, [_vp, ctypes.POINTER(_u64), ctypes.POINTER(_sz)])
+    _bind(lib, "hdfs_crc32c_session_destroy", None, [_vp])
     _bind(lib, "hdfs_crc32c_composite_crcs", _int, [ctypes.POINTER(Segment), _sz, ctypes.POINTER(_u32)])
     _bind(lib, "hdfs_crc32c_dev_alloc", _int, [ctypes.POINTER(_vp), _u64])
     _bind(lib, "hdfs_crc32c_dev_free", _int, [_vp])
@@ -203,6 +210,53 @@ def _packets(fn, stream, proto, chunk_size, ctype, max_pkts):
     if rc < 0:
         _check(rc)
     return rc, [arr[i].as_dict() for i in range(npk.value)], used.value
+
+
+class Session:
+    """Streaming packet-verify session (hdfs_crc32c_session_*)."""
+
+    def __init__(self, proto=PROTO_V2, chunk_size=512, ctype=CSUM_CRC32C, slot_bytes=0, nslots=0):
+        p = _vp()
+        _check(load().hdfs_crc32c_session_create(ctypes.byref(p), proto, chunk_size, ctype, slot_bytes, nslots))
+        self.ptr = p.value
+
+    def buffer(self):
+        w, room = _vp(), _u64(0)
+        _check(load().hdfs_crc32c_session_buffer(self.ptr, ctypes.byref(w), ctypes.byref(room)))
+        return w.value, room.value
+
+    def write(self, data):
+        """Copy bytes in (as a socket read into the slot would), committing
+        slot by slot."""
+        mv = memoryview(data).cast("B")
+        off = 0
+        while off < len(mv):
+            w, room = self.buffer()
+            n = min(room, len(mv) - off)
+            ctypes.memmove(w, (ctypes.c_char * n).from_buffer_copy(mv[off:off + n]), n)
+            _check(load().hdfs_crc32c_session_commit(self.ptr, n))
+            off += n
+
+    def flush(self):
+        _check(load().hdfs_crc32c_session_flush(self.ptr))
+
+    def poll(self, max_pkts=4096, wait=False):
+        arr = (Packet * max(1, max_pkts))()
+        n = _sz(0)
+        rc = load().hdfs_crc32c_session_poll(self.ptr, arr, max_pkts, ctypes.byref(n), 1 if wait else 0)
+        if rc < 0:
+            _check(rc)
+        return rc, [arr[i].as_dict() for i in range(n.value)]
+
+    def pending(self):
+        b, n = _u64(0), _sz(0)
+        _check(load().hdfs_crc32c_session_pending(self.ptr, ctypes.byref(b), ctypes.byref(n)))
+        return b.value, n.value
+
+    def close(self):
+        if self.ptr:
+            load().hdfs_crc32c_session_destroy(self.ptr)
+            self.ptr = None
 
 
 def composite_crcs(segments):

@@ -17,34 +17,10 @@
 #include <string>
 #include <vector>
 
-#include "crc32c_internal.h"
-#include "crc32c_packets.h"
+#include "crc32c_engine.h"
 #include "crc32c_tables.h"
-#include "hadoofus_crc32c.h"
 
 namespace hdfs_crc32c {
-
-hipError_t launch_tiles(int mode, int order, int nt, int depth, int grid, const SegDev *segs, uint32_t nseg,
-                        uint64_t total_rounds, uint64_t total_tiles, const uint32_t *gtab,
-                        uint32_t *first_bad, unsigned long long *mism, unsigned long long *diag,
-                        uint32_t store_policy, uint32_t *gctr, hipStream_t stream);
-hipError_t launch_probe_read(const uint8_t *p, uint64_t nbytes, uint32_t *out, int grid, int block, int variant,
-                             hipStream_t stream);
-hipError_t launch_generic(int mode, const SegDev *segs, uint32_t nseg, uint64_t total_gtiles,
-                          const uint32_t *gtab, uint32_t *first_bad, unsigned long long *mism,
-                          hipStream_t stream);
-hipError_t launch_combine(const uint32_t *raws, uint64_t nraw, uint32_t cs, uint64_t len,
-                          const uint32_t *pow2, uint32_t reg0, uint32_t *acc, hipStream_t stream);
-hipError_t launch_fill(uint64_t *out, uint64_t nwords, uint64_t seed, uint64_t g0, hipStream_t stream);
-hipError_t launch_corrupt(uint8_t *data, uint64_t len, uint32_t cs, uint64_t chunk0, uint64_t modulus,
-                          uint64_t bitmul, hipStream_t stream);
-hipError_t launch_composite(const SegDev *segs, uint32_t nseg, const uint64_t *run_prefix, uint64_t total_runs,
-                            const uint32_t *pow2, uint32_t *out, hipStream_t stream);
-hipError_t launch_prep(uint32_t *fb, uint32_t nfb, unsigned long long *mism, uint32_t *gctr, hipStream_t stream);
-hipError_t launch_gather(const uint8_t *raw, const PktDesc *descs, uint32_t npk, uint32_t units, uint8_t *arena,
-                         uint8_t *crc_arena, hipStream_t stream);
-
-namespace {
 
 thread_local char g_err[512] = "";
 
@@ -55,59 +31,6 @@ int fail(int code, const char *fmt, ...) {
   va_end(ap);
   return code;
 }
-
-#define HIPCHK(expr)                                                                   \
-  do {                                                                                 \
-    hipError_t e_ = (expr);                                                            \
-    if (e_ != hipSuccess)                                                              \
-      return fail(HDFS_CRC32C_EHIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_),    \
-                  __FILE__, __LINE__);                                                 \
-  } while (0)
-
-constexpr int kMaxDev = 64;
-constexpr uint32_t kStreamPiece = 4096;          // stream CRC: raw CRC per 4 KiB piece
-constexpr size_t kStageCap = size_t(64) << 20;   // host->device staging for one-shots
-
-struct DevCtx {
-  bool ready = false;
-  int dev = -1;
-  int num_cu = 0;
-  char arch[64] = "";
-  // table sets per checksum type: [0] CRC32C, [1] CRC32 (zlib polynomial)
-  uint32_t *d_tab_main_t[2] = {nullptr, nullptr};
-  uint32_t *d_tab_pow2_t[2] = {nullptr, nullptr};
-  hipStream_t stream = nullptr;
-  // one-shot scratch (guarded by mu)
-  uint8_t *h_stage = nullptr;
-  uint8_t *d_stage = nullptr;
-  uint32_t *d_raw = nullptr;
-  size_t raw_cap = 0;
-  SegDev *d_seg = nullptr;
-  uint32_t *d_small = nullptr;  // [0] acc, [1] first_bad, [2..3] mismatches
-  // host pipeline (guarded by mu): two staging slots on two streams
-  hipStream_t copy_stream = nullptr, comp_stream = nullptr;
-  hipEvent_t ev_copy[2] = {nullptr, nullptr}, ev_comp[2] = {nullptr, nullptr};
-  uint8_t *p_data[2] = {nullptr, nullptr};
-  uint32_t *p_crc[2] = {nullptr, nullptr};
-  uint8_t *p_bm[2] = {nullptr, nullptr};
-  size_t p_cap = 0;        // bytes per data slot
-  size_t p_chunk_cap = 0;  // chunks per CRC slot
-  SegDev *p_segs = nullptr;
-  uint32_t *p_fb = nullptr;
-  uint32_t *p_gctr = nullptr;  // [2], one per slot
-  unsigned long long *p_mism = nullptr;
-  size_t p_npieces_cap = 0;
-  // packet-stream verifier (guarded by mu): per-slot wire / data / CRC
-  // buffers, whole-call packet tables, pinned host staging for the tables
-  uint8_t *k_raw[2] = {nullptr, nullptr};
-  uint8_t *k_arena[2] = {nullptr, nullptr};
-  uint8_t *k_crc[2] = {nullptr, nullptr};
-  size_t k_raw_cap = 0, k_arena_cap = 0, k_crc_cap = 0;
-  uint8_t *k_meta = nullptr;    // device: descs | segs | fb | bitmaps
-  uint8_t *k_hmeta = nullptr;   // pinned host mirror
-  size_t k_meta_cap = 0;
-  std::mutex mu;
-};
 
 DevCtx g_ctx[kMaxDev];
 std::mutex g_init_mu;
@@ -127,18 +50,6 @@ uint32_t g_store_policy = uint32_t(env_int("HDFS_CRC32C_STORE", 0));
 // Diagnostic per-wave timestamps (device buffer, 3 x u64 per wave) or null.
 unsigned long long *g_diag = nullptr;
 
-struct DeviceGuard {
-  int prev = -1;
-  bool changed = false;
-  explicit DeviceGuard(int dev) {
-    if (hipGetDevice(&prev) == hipSuccess && prev != dev) {
-      changed = hipSetDevice(dev) == hipSuccess;
-    }
-  }
-  ~DeviceGuard() {
-    if (changed) (void)hipSetDevice(prev);
-  }
-};
 
 int ctx_init(int device, DevCtx **out) {
   int ndev = 0;
@@ -249,9 +160,6 @@ int fill_seg(const hdfs_crc32c_segment &in, int mode, SegDev &s, size_t idx) {
   return HDFS_CRC32C_OK;
 }
 
-// Table set of a segment: 0 = CRC32C, 1 = CRC32 (zlib polynomial).
-inline int seg_ctype(uint32_t flags) { return (flags & HDFS_CRC32C_SEG_CRC32) ? 1 : 0; }
-
 bool device_accessible(const void *p) {
   if (!p) return true;
   hipPointerAttribute_t a;
@@ -266,8 +174,7 @@ bool device_accessible(const void *p) {
 // ctype: 0 = CRC32C, 1 = CRC32 (zlib polynomial) -- selects the table set.
 int launch_all(DevCtx &c, int mode, const SegDev *d_segs, uint32_t nseg, uint64_t rounds,
                uint64_t mtiles, uint64_t gtiles, uint32_t *d_fb, unsigned long long *d_mism,
-               uint32_t *d_gctr, hipStream_t st, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr,
-               bool reset = true, int ctype = 0) {
+               uint32_t *d_gctr, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1, bool reset, int ctype) {
   const bool vreset = mode == kModeVerify && reset;
   uint32_t *gz = (rounds && g_tile_order == 2) ? d_gctr : nullptr;
   if (vreset || gz)
@@ -355,18 +262,6 @@ bool is_pinned_host(const void *p) {
   return a.type == hipMemoryTypeHost || a.devicePointer != nullptr;
 }
 
-struct HostRegistration {
-  const void *p = nullptr;
-  ~HostRegistration() {
-    if (p) (void)hipHostUnregister(const_cast<void *>(p));
-  }
-  int ensure(const void *ptr, size_t n) {
-    if (!ptr || !n || is_pinned_host(ptr)) return HDFS_CRC32C_OK;
-    HIPCHK(hipHostRegister(const_cast<void *>(ptr), n, hipHostRegisterDefault));
-    p = ptr;
-    return HDFS_CRC32C_OK;
-  }
-};
 
 int pipe_reserve(DevCtx &c, size_t piece, uint32_t cs, size_t npieces) {
   if (!c.copy_stream) {
@@ -506,196 +401,11 @@ int host_pipeline(int mode, const uint8_t *data, uint64_t len, uint32_t cs, uint
   return HDFS_CRC32C_OK;
 }
 
-// Grow-only device buffer pair.
-int grow2(uint8_t *(&buf)[2], size_t &cap, size_t need) {
-  if (need <= cap) return HDFS_CRC32C_OK;
-  for (int b = 0; b < 2; b++) {
-    if (buf[b]) HIPCHK(hipFree(buf[b]));
-    buf[b] = nullptr;
-  }
-  cap = 0;
-  for (int b = 0; b < 2; b++) HIPCHK(hipMalloc(&buf[b], need));
-  cap = need;
-  return HDFS_CRC32C_OK;
-}
-
-inline uint64_t align_up(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
-
-// Packet-stream verify: framing on the host, then the wire bytes of the
-// framing-clean packets go H2D in pieces (copy stream) while the previous
-// piece is de-framed by packet_gather_kernel and verified by the tiled /
-// generic kernels (compute stream), two slots deep.
-int verify_packets_impl(const uint8_t *stream, uint64_t len, int proto, uint32_t cs, int ctype,
-                        hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts, uint64_t *consumed,
-                        bool verify) {
-  if (npkts) *npkts = 0;
-  if (consumed) *consumed = 0;
-  if (max_pkts && !pkts) return fail(HDFS_CRC32C_EINVAL, "null packet array");
-  std::vector<hdfs_crc32c_packet> recs;
-  uint64_t used = 0;
-  int rc = parse_packet_stream(stream, len, proto, cs, ctype, max_pkts, recs, &used, g_err, sizeof(g_err));
-  if (rc) return rc;
-  std::vector<size_t> vidx;  // packets whose chunks go to the GPU
-  if (verify && ctype != HDFS_CRC32C_CSUM_NULL)
-    for (size_t i = 0; i < recs.size(); i++)
-      if (!recs[i].error && recs[i].crc_len > 0) vidx.push_back(i);
-  if (!vidx.empty()) {
-    DevCtx *cp = nullptr;
-    rc = ctx_init(-1, &cp);
-    if (rc) return rc;
-    DevCtx &c = *cp;
-    DeviceGuard g(c.dev);
-    std::lock_guard<std::mutex> lk(c.mu);
-    hipPointerAttribute_t pa;
-    if (hipPointerGetAttributes(&pa, stream) == hipSuccess && pa.type == hipMemoryTypeDevice)
-      return fail(HDFS_CRC32C_EINVAL, "packet stream must be host memory (the datanode's recvbuf)");
-    (void)hipGetLastError();
-    const size_t nv = vidx.size();
-    // Pieces: runs of consecutive verified packets whose wire span is <= 64 MiB
-    // (a larger packet gets a piece of its own).
-    constexpr uint64_t kPieceCap = uint64_t(64) << 20;
-    struct Piece {
-      size_t v0, v1;          // [v0, v1) into vidx
-      uint64_t src0, span;    // wire bytes [src0, src0 + span)
-      uint64_t arena, crcb;   // arena / CRC-arena bytes
-      uint32_t units;
-      uint64_t rounds, mtiles, gtiles;
-    };
-    std::vector<Piece> pieces;
-    auto wire_begin = [&](size_t v) { return recs[vidx[v]].stream_off + recs[vidx[v]].header_len; };
-    auto wire_end = [&](size_t v) {
-      const hdfs_crc32c_packet &k = recs[vidx[v]];
-      return k.stream_off + k.header_len + uint64_t(k.crc_len) + uint64_t(k.data_len);
-    };
-    for (size_t v = 0; v < nv; v++) {
-      if (pieces.empty() || wire_end(v) - pieces.back().src0 > kPieceCap) {
-        pieces.push_back(Piece{v, v, wire_begin(v), 0, 0, 0, 0, 0, 0, 0});
-      }
-      Piece &pc = pieces.back();
-      pc.v1 = v + 1;
-      pc.span = wire_end(v) - pc.src0;
-      pc.arena += align_up(uint64_t(recs[vidx[v]].data_len), 16);
-      pc.crcb += uint64_t(recs[vidx[v]].crc_len);
-      pc.units += uint32_t((uint64_t(recs[vidx[v]].data_len) + kGatherSlice - 1) / kGatherSlice);
-    }
-    uint64_t max_span = 0, max_arena = 0, max_crc = 0, bm_total = 0;
-    for (auto &pc : pieces) {
-      max_span = std::max(max_span, pc.span);
-      max_arena = std::max(max_arena, pc.arena);
-      max_crc = std::max(max_crc, pc.crcb);
-    }
-    std::vector<uint64_t> bm_off(nv);
-    for (size_t v = 0; v < nv; v++) {
-      bm_off[v] = bm_total;
-      bm_total += (uint64_t(recs[vidx[v]].crc_len) / 4 + 7) / 8;
-    }
-    // Device tables: descs | segs | fb | bitmaps (one allocation, pinned mirror).
-    const size_t off_segs = align_up(nv * sizeof(PktDesc), 256);
-    const size_t off_fb = off_segs + align_up(nv * sizeof(SegDev), 256);
-    const size_t off_bm = off_fb + align_up(nv * 4, 256);
-    const size_t meta = off_bm + align_up(bm_total, 256) + 256;
-    if (meta > c.k_meta_cap) {
-      if (c.k_meta) HIPCHK(hipFree(c.k_meta));
-      if (c.k_hmeta) HIPCHK(hipHostFree(c.k_hmeta));
-      c.k_meta = nullptr;
-      c.k_hmeta = nullptr;
-      c.k_meta_cap = 0;
-      HIPCHK(hipMalloc(&c.k_meta, meta));
-      HIPCHK(hipHostMalloc(&c.k_hmeta, meta, hipHostMallocDefault));
-      c.k_meta_cap = meta;
-    }
-    if ((rc = grow2(c.k_raw, c.k_raw_cap, max_span + 64)) || (rc = grow2(c.k_arena, c.k_arena_cap, max_arena + 64)) ||
-        (rc = grow2(c.k_crc, c.k_crc_cap, max_crc + 64)))
-      return rc;
-    rc = pipe_reserve(c, kGatherSlice, 512, 1);  // streams + events only
-    if (rc) return rc;
-    auto *hd = reinterpret_cast<PktDesc *>(c.k_hmeta);
-    auto *hs = reinterpret_cast<SegDev *>(c.k_hmeta + off_segs);
-    auto *d_descs = reinterpret_cast<PktDesc *>(c.k_meta);
-    auto *d_segs = reinterpret_cast<SegDev *>(c.k_meta + off_segs);
-    auto *d_fb = reinterpret_cast<uint32_t *>(c.k_meta + off_fb);
-    uint8_t *d_bm = c.k_meta + off_bm;
-    const uint32_t sflags = HDFS_CRC32C_SEG_BE | (ctype == HDFS_CRC32C_CSUM_CRC32 ? HDFS_CRC32C_SEG_CRC32 : 0u);
-    for (size_t pi = 0; pi < pieces.size(); pi++) {
-      Piece &pc = pieces[pi];
-      const int b = int(pi & 1);
-      uint64_t aoff = 0, coff = 0;
-      uint32_t unit = 0;
-      for (size_t v = pc.v0; v < pc.v1; v++) {
-        const hdfs_crc32c_packet &k = recs[vidx[v]];
-        PktDesc &d = hd[v];
-        d.src_crc = k.stream_off + k.header_len - pc.src0;
-        d.dst_data = aoff;
-        d.dst_crc = coff;
-        d.dlen = uint32_t(k.data_len);
-        d.ncrc = uint32_t(k.crc_len / 4);
-        d.unit0 = unit;
-        d.nunits = uint32_t((uint64_t(d.dlen) + kGatherSlice - 1) / kGatherSlice);
-        hdfs_crc32c_segment in = {c.k_arena[b] + aoff, uint64_t(d.dlen), cs, sflags, 0, 0,
-                                  c.k_crc[b] + coff, d_bm + bm_off[v]};
-        rc = fill_seg(in, HDFS_CRC32C_MODE_VERIFY, hs[v], v);
-        if (rc) return rc;
-        classify(hs[v], pc.rounds, pc.gtiles, pc.mtiles);
-        aoff += align_up(d.dlen, 16);
-        coff += 4ull * d.ncrc;
-        unit += d.nunits;
-      }
-    }
-    HostRegistration reg;
-    if ((rc = reg.ensure(stream, len))) return rc;
-    HIPCHK(hipMemcpyAsync(c.k_meta, c.k_hmeta, off_fb, hipMemcpyHostToDevice, c.comp_stream));
-    HIPCHK(hipEventRecord(c.ev_comp[0], c.comp_stream));
-    HIPCHK(hipEventRecord(c.ev_comp[1], c.comp_stream));
-    const int ct = seg_ctype(sflags);
-    for (size_t pi = 0; pi < pieces.size(); pi++) {
-      const Piece &pc = pieces[pi];
-      const int b = int(pi & 1);
-      const uint32_t npk = uint32_t(pc.v1 - pc.v0);
-      HIPCHK(hipStreamWaitEvent(c.copy_stream, c.ev_comp[b], 0));  // slot free
-      HIPCHK(hipMemcpyAsync(c.k_raw[b], stream + pc.src0, pc.span, hipMemcpyHostToDevice, c.copy_stream));
-      HIPCHK(hipEventRecord(c.ev_copy[b], c.copy_stream));
-      HIPCHK(hipStreamWaitEvent(c.comp_stream, c.ev_copy[b], 0));
-      HIPCHK(launch_gather(c.k_raw[b], d_descs + pc.v0, npk, pc.units, c.k_arena[b], c.k_crc[b], c.comp_stream));
-      rc = launch_all(c, kModeVerify, d_segs + pc.v0, npk, pc.rounds, pc.mtiles, pc.gtiles, d_fb + pc.v0,
-                      c.p_mism, c.p_gctr + b, c.comp_stream, nullptr, nullptr, true, ct);
-      if (rc) return rc;
-      HIPCHK(hipEventRecord(c.ev_comp[b], c.comp_stream));
-    }
-    HIPCHK(hipMemcpyAsync(c.k_hmeta + off_fb, c.k_meta + off_fb, meta - 256 - off_fb, hipMemcpyDeviceToHost,
-                          c.comp_stream));
-    HIPCHK(hipStreamSynchronize(c.comp_stream));
-    HIPCHK(hipStreamSynchronize(c.copy_stream));
-    const auto *hfb = reinterpret_cast<const uint32_t *>(c.k_hmeta + off_fb);
-    const uint8_t *hbm = c.k_hmeta + off_bm;
-    for (size_t v = 0; v < nv; v++) {
-      hdfs_crc32c_packet &k = recs[vidx[v]];
-      if (hfb[v] == 0xFFFFFFFFu) continue;
-      const uint32_t nch = uint32_t(k.crc_len / 4);
-      uint32_t bad = 0;
-      for (uint32_t j = 0; j < (nch + 7) / 8; j++) {
-        uint32_t byte = hbm[bm_off[v] + j];
-        if (j == nch / 8) byte &= (1u << (nch % 8)) - 1u;  // bits past the last chunk
-        bad += uint32_t(__builtin_popcount(byte));
-      }
-      k.error = HDFS_CRC32C_ERR_DATANODE_BAD_CHECKSUM;
-      k.first_bad = int32_t(hfb[v]);
-      k.bad_chunks = bad;
-    }
-  }
-  if (!recs.empty()) std::memcpy(pkts, recs.data(), recs.size() * sizeof(hdfs_crc32c_packet));
-  if (npkts) *npkts = recs.size();
-  if (consumed) *consumed = used;
-  for (auto &k : recs)
-    if (k.error) return k.error;
-  return HDFS_CRC32C_OK;
-}
-
 [[noreturn]] void die(const char *who) {
   std::fprintf(stderr, "%s: MI355X CRC32C engine unavailable: %s\n", who, g_err);
   std::abort();
 }
 
-}  // namespace
 }  // namespace hdfs_crc32c
 
 using namespace hdfs_crc32c;
@@ -1233,18 +943,6 @@ int hdfs_crc32c_composite_crcs(const hdfs_crc32c_segment *segs, size_t nseg, uin
   if (d_out) (void)hipFree(d_out);
   if (e != hipSuccess) return fail(HDFS_CRC32C_EHIP, "composite: %s", hipGetErrorString(e));
   return HDFS_CRC32C_OK;
-}
-
-int hdfs_crc32c_parse_packets(const void *stream, uint64_t len, int proto, uint32_t chunk_size, int ctype,
-                              hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts, uint64_t *consumed) {
-  return verify_packets_impl(static_cast<const uint8_t *>(stream), len, proto, chunk_size, ctype, pkts, max_pkts,
-                             npkts, consumed, false);
-}
-
-int hdfs_crc32c_verify_packets(const void *stream, uint64_t len, int proto, uint32_t chunk_size, int ctype,
-                               hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts, uint64_t *consumed) {
-  return verify_packets_impl(static_cast<const uint8_t *>(stream), len, proto, chunk_size, ctype, pkts, max_pkts,
-                             npkts, consumed, true);
 }
 
 }  // extern "C"

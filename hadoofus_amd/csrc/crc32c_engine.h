@@ -1,0 +1,149 @@
+// Engine internals shared by the host translation units of
+// libhadoofus_crc32c.so (not part of the public C ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstddef>
+#include <cstdint>
+#include <mutex>
+
+#include "crc32c_internal.h"
+#include "hadoofus_crc32c.h"
+
+namespace hdfs_crc32c {
+
+// ---- kernel launchers (crc32c_kernels.hip) ----
+hipError_t launch_tiles(int mode, int order, int nt, int depth, int grid, const SegDev *segs, uint32_t nseg,
+                        uint64_t total_rounds, uint64_t total_tiles, const uint32_t *gtab,
+                        uint32_t *first_bad, unsigned long long *mism, unsigned long long *diag,
+                        uint32_t store_policy, uint32_t *gctr, hipStream_t stream);
+hipError_t launch_probe_read(const uint8_t *p, uint64_t nbytes, uint32_t *out, int grid, int block, int variant,
+                             hipStream_t stream);
+hipError_t launch_generic(int mode, const SegDev *segs, uint32_t nseg, uint64_t total_gtiles,
+                          const uint32_t *gtab, uint32_t *first_bad, unsigned long long *mism,
+                          hipStream_t stream);
+hipError_t launch_combine(const uint32_t *raws, uint64_t nraw, uint32_t cs, uint64_t len,
+                          const uint32_t *pow2, uint32_t reg0, uint32_t *acc, hipStream_t stream);
+hipError_t launch_fill(uint64_t *out, uint64_t nwords, uint64_t seed, uint64_t g0, hipStream_t stream);
+hipError_t launch_corrupt(uint8_t *data, uint64_t len, uint32_t cs, uint64_t chunk0, uint64_t modulus,
+                          uint64_t bitmul, hipStream_t stream);
+hipError_t launch_composite(const SegDev *segs, uint32_t nseg, const uint64_t *run_prefix, uint64_t total_runs,
+                            const uint32_t *pow2, uint32_t *out, hipStream_t stream);
+hipError_t launch_prep(uint32_t *fb, uint32_t nfb, unsigned long long *mism, uint32_t *gctr, hipStream_t stream);
+hipError_t launch_gather(const uint8_t *raw, const PktDesc *descs, uint32_t npk, uint32_t units, uint8_t *arena,
+                         uint8_t *crc_arena, hipStream_t stream);
+
+// ---- errors ----
+extern thread_local char g_err[512];
+int fail(int code, const char *fmt, ...);
+
+#define HIPCHK(expr)                                                                   \
+  do {                                                                                 \
+    hipError_t e_ = (expr);                                                            \
+    if (e_ != hipSuccess)                                                              \
+      return ::hdfs_crc32c::fail(HDFS_CRC32C_EHIP, "%s: %s (%s:%d)", #expr,            \
+                                 hipGetErrorString(e_), __FILE__, __LINE__);           \
+  } while (0)
+
+// ---- per-device engine context ----
+constexpr int kMaxDev = 64;
+constexpr uint32_t kStreamPiece = 4096;          // stream CRC: raw CRC per 4 KiB piece
+constexpr size_t kStageCap = size_t(64) << 20;   // host->device staging for one-shots
+
+// Device buffers of one in-flight packet piece (packet-stream verifier):
+// wire bytes, de-framed data / CRC arenas, and the piece's tables
+// (descs | segs | first-bad | bitmaps).
+struct PieceSlot {
+  uint8_t *raw = nullptr, *arena = nullptr, *crc = nullptr, *meta = nullptr;
+  size_t raw_cap = 0, arena_cap = 0, crc_cap = 0, meta_cap = 0;
+  uint32_t *gctr = nullptr;            // tiled-kernel pool counter
+  unsigned long long *mism = nullptr;  // mismatch count
+  hipEvent_t copied = nullptr;         // copy stream: wire bytes and tables landed
+  hipEvent_t done = nullptr;           // compute stream: slot free again
+};
+
+struct DevCtx {
+  bool ready = false;
+  int dev = -1;
+  int num_cu = 0;
+  char arch[64] = "";
+  // table sets per checksum type: [0] CRC32C, [1] CRC32 (zlib polynomial)
+  uint32_t *d_tab_main_t[2] = {nullptr, nullptr};
+  uint32_t *d_tab_pow2_t[2] = {nullptr, nullptr};
+  hipStream_t stream = nullptr;
+  // one-shot scratch (guarded by mu)
+  uint8_t *h_stage = nullptr;
+  uint8_t *d_stage = nullptr;
+  uint32_t *d_raw = nullptr;
+  size_t raw_cap = 0;
+  SegDev *d_seg = nullptr;
+  uint32_t *d_small = nullptr;  // [0] acc, [1] first_bad, [2..3] mismatches
+  // host pipeline (guarded by mu): two staging slots on two streams
+  hipStream_t copy_stream = nullptr, comp_stream = nullptr;
+  hipEvent_t ev_copy[2] = {nullptr, nullptr}, ev_comp[2] = {nullptr, nullptr};
+  uint8_t *p_data[2] = {nullptr, nullptr};
+  uint32_t *p_crc[2] = {nullptr, nullptr};
+  uint8_t *p_bm[2] = {nullptr, nullptr};
+  size_t p_cap = 0;        // bytes per data slot
+  size_t p_chunk_cap = 0;  // chunks per CRC slot
+  SegDev *p_segs = nullptr;
+  uint32_t *p_fb = nullptr;
+  uint32_t *p_gctr = nullptr;  // [2], one per slot
+  unsigned long long *p_mism = nullptr;
+  size_t p_npieces_cap = 0;
+  // packet-stream verifier (guarded by mu): two device piece slots and the
+  // pinned host tables of one call
+  PieceSlot kslot[2];
+  uint8_t *k_hmeta = nullptr;
+  size_t k_hmeta_cap = 0;
+  std::mutex mu;
+};
+
+extern DevCtx g_ctx[kMaxDev];
+extern int g_tile_order;
+
+struct DeviceGuard {
+  int prev = -1;
+  bool changed = false;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) == hipSuccess && prev != dev) {
+      changed = hipSetDevice(dev) == hipSuccess;
+    }
+  }
+  ~DeviceGuard() {
+    if (changed) (void)hipSetDevice(prev);
+  }
+};
+
+int ctx_init(int device, DevCtx **out);
+// Split a segment between the tiled and the generic kernel (prefix indices).
+void classify(SegDev &s, uint64_t &rounds, uint64_t &gtiles, uint64_t &mtiles);
+int fill_seg(const hdfs_crc32c_segment &in, int mode, SegDev &s, size_t idx);
+// Table set of a segment: 0 = CRC32C, 1 = CRC32 (zlib polynomial).
+inline int seg_ctype(uint32_t flags) { return (flags & HDFS_CRC32C_SEG_CRC32) ? 1 : 0; }
+bool device_accessible(const void *p);
+bool is_pinned_host(const void *p);
+// Enqueue one compute / verify pass (prep + tiled + generic kernels) on st.
+int launch_all(DevCtx &c, int mode, const SegDev *d_segs, uint32_t nseg, uint64_t rounds, uint64_t mtiles,
+               uint64_t gtiles, uint32_t *d_fb, unsigned long long *d_mism, uint32_t *d_gctr, hipStream_t st,
+               hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, bool reset = true, int ctype = 0);
+// Copy / compute streams, events and the small pipeline buffers.
+int pipe_reserve(DevCtx &c, size_t piece, uint32_t cs, size_t npieces);
+
+struct HostRegistration {
+  const void *p = nullptr;
+  ~HostRegistration() {
+    if (p) (void)hipHostUnregister(const_cast<void *>(p));
+  }
+  int ensure(const void *ptr, size_t n) {
+    if (!ptr || !n || is_pinned_host(ptr)) return HDFS_CRC32C_OK;
+    HIPCHK(hipHostRegister(const_cast<void *>(ptr), n, hipHostRegisterDefault));
+    p = ptr;
+    return HDFS_CRC32C_OK;
+  }
+};
+
+inline uint64_t align_up(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
+
+}  // namespace hdfs_crc32c

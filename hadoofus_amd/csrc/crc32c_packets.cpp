@@ -21,8 +21,12 @@
 // nonzero varint payload bit.
 #include "crc32c_packets.h"
 
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <deque>
+
+#include "crc32c_engine.h"
 
 namespace hdfs_crc32c {
 namespace {
@@ -216,3 +220,508 @@ int parse_packet_stream(const uint8_t *s, uint64_t len, int proto, uint32_t chun
 }
 
 }  // namespace hdfs_crc32c
+
+// ===========================================================================
+// GPU side: pieces of framing-clean packets -> H2D, de-framing gather, verify
+// ===========================================================================
+namespace hdfs_crc32c {
+namespace {
+
+constexpr uint64_t kPieceCap = uint64_t(64) << 20;  // wire bytes per piece (sync verify)
+
+struct PieceLayout {
+  size_t n = 0;                 // packets in the piece
+  uint64_t src0 = 0, span = 0;  // wire bytes [src0, src0 + span) of the host buffer
+  uint64_t arena = 0, crcb = 0, bm = 0;
+  uint32_t units = 0;
+  uint64_t rounds = 0, mtiles = 0, gtiles = 0;
+  size_t off_segs = 0, off_fb = 0, off_bm = 0, meta = 0;  // table layout (device and pinned host)
+};
+
+uint64_t wire_begin(const hdfs_crc32c_packet &k) { return k.stream_off + k.header_len; }
+uint64_t wire_end(const hdfs_crc32c_packet &k) {
+  return k.stream_off + k.header_len + uint64_t(k.crc_len) + uint64_t(k.data_len);
+}
+
+void layout_piece(const hdfs_crc32c_packet *recs, const size_t *idx, size_t n, PieceLayout &L) {
+  L = PieceLayout{};
+  L.n = n;
+  L.src0 = wire_begin(recs[idx[0]]);
+  L.span = wire_end(recs[idx[n - 1]]) - L.src0;
+  for (size_t v = 0; v < n; v++) {
+    const hdfs_crc32c_packet &k = recs[idx[v]];
+    L.arena += align_up(uint64_t(k.data_len), 16);
+    L.crcb += uint64_t(k.crc_len);
+    L.bm += (uint64_t(k.crc_len) / 4 + 7) / 8;
+    L.units += uint32_t((uint64_t(k.data_len) + kGatherSlice - 1) / kGatherSlice);
+  }
+  L.off_segs = align_up(n * sizeof(PktDesc), 256);
+  L.off_fb = L.off_segs + align_up(n * sizeof(SegDev), 256);
+  L.off_bm = L.off_fb + align_up(n * 4, 256);
+  L.meta = L.off_bm + align_up(L.bm, 256);
+}
+
+int grow(uint8_t *&buf, size_t &cap, size_t need) {
+  if (need <= cap) return HDFS_CRC32C_OK;
+  if (buf) HIPCHK(hipFree(buf));
+  buf = nullptr;
+  cap = 0;
+  HIPCHK(hipMalloc(&buf, need));
+  cap = need;
+  return HDFS_CRC32C_OK;
+}
+
+// Make slot s large enough for L (waits for the slot's previous piece first
+// if a buffer has to be replaced).
+int reserve_slot(PieceSlot &s, const PieceLayout &L) {
+  if (!s.done) {
+    HIPCHK(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming));
+    HIPCHK(hipMalloc(&s.gctr, 64));
+    HIPCHK(hipMalloc(&s.mism, 64));
+  }
+  if (L.span + 64 > s.raw_cap || L.arena + 64 > s.arena_cap || L.crcb + 64 > s.crc_cap || L.meta > s.meta_cap) {
+    HIPCHK(hipEventSynchronize(s.done));
+    int rc;
+    if ((rc = grow(s.raw, s.raw_cap, L.span + 64)) || (rc = grow(s.arena, s.arena_cap, L.arena + 64)) ||
+        (rc = grow(s.crc, s.crc_cap, L.crcb + 64)) || (rc = grow(s.meta, s.meta_cap, L.meta)))
+      return rc;
+  }
+  return HDFS_CRC32C_OK;
+}
+
+void release_slot(PieceSlot &s) {
+  if (s.done) (void)hipEventSynchronize(s.done);
+  for (uint8_t *p : {s.raw, s.arena, s.crc, s.meta})
+    if (p) (void)hipFree(p);
+  if (s.gctr) (void)hipFree(s.gctr);
+  if (s.mism) (void)hipFree(s.mism);
+  if (s.done) (void)hipEventDestroy(s.done);
+  if (s.copied) (void)hipEventDestroy(s.copied);
+  s = PieceSlot{};
+}
+
+// Build the piece's gather descriptors and verify segments in hmeta
+// (pinned; device addresses of slot s) and finish L's tile counts.
+int build_piece(const hdfs_crc32c_packet *recs, const size_t *idx, PieceLayout &L, uint32_t cs, int ctype,
+                const PieceSlot &s, uint8_t *hmeta) {
+  auto *hd = reinterpret_cast<PktDesc *>(hmeta);
+  auto *hs = reinterpret_cast<SegDev *>(hmeta + L.off_segs);
+  const uint32_t sflags = HDFS_CRC32C_SEG_BE | (ctype == HDFS_CRC32C_CSUM_CRC32 ? HDFS_CRC32C_SEG_CRC32 : 0u);
+  uint64_t aoff = 0, coff = 0, boff = 0;
+  uint32_t unit = 0;
+  L.rounds = L.mtiles = L.gtiles = 0;
+  for (size_t v = 0; v < L.n; v++) {
+    const hdfs_crc32c_packet &k = recs[idx[v]];
+    PktDesc &d = hd[v];
+    d.src_crc = wire_begin(k) - L.src0;
+    d.dst_data = aoff;
+    d.dst_crc = coff;
+    d.dlen = uint32_t(k.data_len);
+    d.ncrc = uint32_t(k.crc_len / 4);
+    d.unit0 = unit;
+    d.nunits = uint32_t((uint64_t(d.dlen) + kGatherSlice - 1) / kGatherSlice);
+    hdfs_crc32c_segment in = {s.arena + aoff, uint64_t(d.dlen), cs, sflags, 0, 0, s.crc + coff,
+                              s.meta + L.off_bm + boff};
+    int rc = fill_seg(in, HDFS_CRC32C_MODE_VERIFY, hs[v], v);
+    if (rc) return rc;
+    classify(hs[v], L.rounds, L.gtiles, L.mtiles);
+    aoff += align_up(d.dlen, 16);
+    coff += 4ull * d.ncrc;
+    boff += (uint64_t(d.ncrc) + 7) / 8;
+    unit += d.nunits;
+  }
+  return HDFS_CRC32C_OK;
+}
+
+// Copy stream: tables + wire bytes H2D once slot s is free; compute stream:
+// gather, verify, results D2H into hmeta.  s.done marks completion.
+int enqueue_piece(DevCtx &c, const uint8_t *host, const PieceLayout &L, PieceSlot &s, uint8_t *hmeta, int ctype,
+                  hipStream_t copy, hipStream_t comp) {
+  HIPCHK(hipStreamWaitEvent(copy, s.done, 0));
+  HIPCHK(hipMemcpyAsync(s.meta, hmeta, L.off_fb, hipMemcpyHostToDevice, copy));
+  HIPCHK(hipMemcpyAsync(s.raw, host + L.src0, L.span, hipMemcpyHostToDevice, copy));
+  HIPCHK(hipEventRecord(s.copied, copy));
+  HIPCHK(hipStreamWaitEvent(comp, s.copied, 0));
+  HIPCHK(launch_gather(s.raw, reinterpret_cast<const PktDesc *>(s.meta), uint32_t(L.n), L.units, s.arena, s.crc,
+                       comp));
+  int rc = launch_all(c, kModeVerify, reinterpret_cast<const SegDev *>(s.meta + L.off_segs), uint32_t(L.n),
+                      L.rounds, L.mtiles, L.gtiles, reinterpret_cast<uint32_t *>(s.meta + L.off_fb), s.mism,
+                      s.gctr, comp, nullptr, nullptr, true, ctype == HDFS_CRC32C_CSUM_CRC32 ? 1 : 0);
+  if (rc) return rc;
+  HIPCHK(hipMemcpyAsync(hmeta + L.off_fb, s.meta + L.off_fb, L.meta - L.off_fb, hipMemcpyDeviceToHost, comp));
+  HIPCHK(hipEventRecord(s.done, comp));
+  return HDFS_CRC32C_OK;
+}
+
+// After the piece completed: per-packet verdicts from first-bad + bitmaps.
+void finish_piece(hdfs_crc32c_packet *recs, const size_t *idx, const PieceLayout &L, const uint8_t *hmeta) {
+  const auto *fb = reinterpret_cast<const uint32_t *>(hmeta + L.off_fb);
+  const uint8_t *bm = hmeta + L.off_bm;
+  for (size_t v = 0; v < L.n; v++) {
+    hdfs_crc32c_packet &k = recs[idx[v]];
+    const uint32_t nch = uint32_t(k.crc_len / 4), nb = (nch + 7) / 8;
+    if (fb[v] != 0xFFFFFFFFu) {
+      uint32_t bad = 0;
+      for (uint32_t j = 0; j < nb; j++) {
+        uint32_t byte = bm[j];
+        if (j == nch / 8) byte &= (1u << (nch % 8)) - 1u;  // bits past the last chunk
+        bad += uint32_t(__builtin_popcount(byte));
+      }
+      k.error = HDFS_CRC32C_ERR_DATANODE_BAD_CHECKSUM;
+      k.first_bad = int32_t(fb[v]);
+      k.bad_chunks = bad;
+    }
+    bm += nb;
+  }
+}
+
+int first_error(const hdfs_crc32c_packet *p, size_t n) {
+  for (size_t i = 0; i < n; i++)
+    if (p[i].error) return p[i].error;
+  return HDFS_CRC32C_OK;
+}
+
+int check_stream_memory(const void *stream) {
+  hipPointerAttribute_t pa;
+  if (hipPointerGetAttributes(&pa, stream) == hipSuccess && pa.type == hipMemoryTypeDevice)
+    return fail(HDFS_CRC32C_EINVAL, "packet stream must be host memory (the datanode's recvbuf)");
+  (void)hipGetLastError();
+  return HDFS_CRC32C_OK;
+}
+
+// Synchronous packet-run verify: framing, then pieces of <= 64 MiB of wire
+// bytes alternate between the context's two device slots (H2D of piece k+1
+// overlaps the kernels of piece k).
+int verify_packets_impl(const uint8_t *stream, uint64_t len, int proto, uint32_t cs, int ctype,
+                        hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts, uint64_t *consumed, bool verify) {
+  if (npkts) *npkts = 0;
+  if (consumed) *consumed = 0;
+  if (max_pkts && !pkts) return fail(HDFS_CRC32C_EINVAL, "null packet array");
+  std::vector<hdfs_crc32c_packet> recs;
+  uint64_t used = 0;
+  int rc = parse_packet_stream(stream, len, proto, cs, ctype, max_pkts, recs, &used, g_err, sizeof(g_err));
+  if (rc) return rc;
+  std::vector<size_t> vidx;  // packets whose chunks go to the GPU
+  if (verify && ctype != HDFS_CRC32C_CSUM_NULL)
+    for (size_t i = 0; i < recs.size(); i++)
+      if (!recs[i].error && recs[i].crc_len > 0) vidx.push_back(i);
+  if (!vidx.empty()) {
+    DevCtx *cp = nullptr;
+    if ((rc = ctx_init(-1, &cp))) return rc;
+    DevCtx &c = *cp;
+    DeviceGuard g(c.dev);
+    std::lock_guard<std::mutex> lk(c.mu);
+    if ((rc = check_stream_memory(stream))) return rc;
+    std::vector<std::pair<size_t, size_t>> pieces;  // [v0, v1) into vidx
+    for (size_t v = 0; v < vidx.size(); v++) {
+      if (pieces.empty() || wire_end(recs[vidx[v]]) - wire_begin(recs[vidx[pieces.back().first]]) > kPieceCap)
+        pieces.push_back({v, v});
+      pieces.back().second = v + 1;
+    }
+    std::vector<PieceLayout> lay(pieces.size());
+    std::vector<size_t> hoff(pieces.size());
+    size_t htotal = 0;
+    for (size_t i = 0; i < pieces.size(); i++) {
+      layout_piece(recs.data(), vidx.data() + pieces[i].first, pieces[i].second - pieces[i].first, lay[i]);
+      hoff[i] = htotal;
+      htotal += align_up(lay[i].meta, 256);
+    }
+    if (htotal > c.k_hmeta_cap) {
+      if (c.k_hmeta) HIPCHK(hipHostFree(c.k_hmeta));
+      c.k_hmeta = nullptr;
+      c.k_hmeta_cap = 0;
+      HIPCHK(hipHostMalloc(&c.k_hmeta, htotal, hipHostMallocDefault));
+      c.k_hmeta_cap = htotal;
+    }
+    if ((rc = pipe_reserve(c, kGatherSlice, 512, 1))) return rc;  // copy / compute streams
+    HostRegistration reg;
+    if ((rc = reg.ensure(stream, len))) return rc;
+    for (size_t i = 0; i < pieces.size(); i++) {
+      PieceSlot &s = c.kslot[i & 1];
+      if ((rc = reserve_slot(s, lay[i])) ||
+          (rc = build_piece(recs.data(), vidx.data() + pieces[i].first, lay[i], cs, ctype, s, c.k_hmeta + hoff[i])) ||
+          (rc = enqueue_piece(c, stream, lay[i], s, c.k_hmeta + hoff[i], ctype, c.copy_stream, c.comp_stream)))
+        return rc;
+    }
+    HIPCHK(hipStreamSynchronize(c.comp_stream));
+    HIPCHK(hipStreamSynchronize(c.copy_stream));
+    for (size_t i = 0; i < pieces.size(); i++)
+      finish_piece(recs.data(), vidx.data() + pieces[i].first, lay[i], c.k_hmeta + hoff[i]);
+  }
+  if (!recs.empty()) std::memcpy(pkts, recs.data(), recs.size() * sizeof(hdfs_crc32c_packet));
+  if (npkts) *npkts = recs.size();
+  if (consumed) *consumed = used;
+  return first_error(recs.data(), recs.size());
+}
+
+}  // namespace
+}  // namespace hdfs_crc32c
+
+using namespace hdfs_crc32c;
+
+// ===========================================================================
+// Streaming sessions: a pinned ring of host slots that socket reads land in
+// directly; full slots are framed and verified asynchronously while the
+// caller keeps receiving into the next slot.
+// ===========================================================================
+struct hdfs_crc32c_session {
+  int dev = -1, proto = 0, ctype = 0;
+  uint32_t cs = 0;
+  uint64_t slot_bytes = 0;
+  std::vector<uint8_t *> hslot;      // pinned wire-byte slots
+  std::vector<uint64_t> hfill;
+  std::vector<uint8_t *> hmeta;      // pinned tables per host slot
+  std::vector<size_t> hmeta_cap;
+  std::vector<hipEvent_t> hdone;     // last GPU work reading / writing host slot i
+  std::vector<bool> hbusy;
+  PieceSlot dslot[2];
+  hipStream_t copy = nullptr, comp = nullptr;
+  size_t cur = 0;
+  uint64_t base_off = 0;             // session stream offset of hslot[cur][0]
+  uint64_t nsub = 0;
+  int sticky = 0;                    // framing error / oversized packet: no more input
+  struct Sub {
+    size_t hs;
+    bool gpu;
+    std::vector<hdfs_crc32c_packet> recs;
+    std::vector<size_t> vidx;
+    PieceLayout L;
+  };
+  std::deque<Sub> inflight;
+  std::deque<hdfs_crc32c_packet> ready;
+};
+
+namespace {
+
+int session_finish_front(hdfs_crc32c_session *s, bool wait, bool *progressed) {
+  *progressed = false;
+  if (s->inflight.empty()) return HDFS_CRC32C_OK;
+  hdfs_crc32c_session::Sub &f = s->inflight.front();
+  if (f.gpu) {
+    if (wait) {
+      HIPCHK(hipEventSynchronize(s->hdone[f.hs]));
+    } else {
+      const hipError_t q = hipEventQuery(s->hdone[f.hs]);
+      if (q == hipErrorNotReady) return HDFS_CRC32C_OK;
+      HIPCHK(q);
+    }
+    finish_piece(f.recs.data(), f.vidx.data(), f.L, s->hmeta[f.hs]);
+  }
+  s->hbusy[f.hs] = false;
+  for (auto &k : f.recs) s->ready.push_back(k);
+  s->inflight.pop_front();
+  *progressed = true;
+  return HDFS_CRC32C_OK;
+}
+
+// Host slot i must be free (its submission finished) before reuse.
+int session_wait_slot(hdfs_crc32c_session *s, size_t i) {
+  while (s->hbusy[i]) {
+    bool p = false;
+    int rc = session_finish_front(s, true, &p);
+    if (rc) return rc;
+  }
+  return HDFS_CRC32C_OK;
+}
+
+int session_submit(hdfs_crc32c_session *s) {
+  const size_t hs = s->cur;
+  const uint64_t fill = s->hfill[hs];
+  if (!fill) return HDFS_CRC32C_OK;
+  const uint8_t *base = s->hslot[hs];
+  hdfs_crc32c_session::Sub sub;
+  sub.hs = hs;
+  sub.gpu = false;
+  uint64_t off = 0;
+  for (;;) {  // one parse per block: an empty last packet ends a block, the next may follow
+    std::vector<hdfs_crc32c_packet> part;
+    uint64_t used = 0;
+    int rc = parse_packet_stream(base + off, fill - off, s->proto, s->cs, s->ctype, SIZE_MAX, part, &used, g_err,
+                                 sizeof(g_err));
+    if (rc) return rc;
+    for (auto &k : part) {
+      k.stream_off += off;  // slot-relative here; made absolute below
+      sub.recs.push_back(k);
+    }
+    off += used;
+    if (!part.empty() && part.back().error) {
+      s->sticky = part.back().error;
+      break;
+    }
+    const bool end_of_block = !part.empty() && part.back().data_len == 0 && part.back().last;
+    if (!end_of_block || off >= fill) break;
+  }
+  if (!s->sticky && off == 0 && fill == s->slot_bytes) {
+    s->sticky = HDFS_CRC32C_EINVAL;
+    return fail(HDFS_CRC32C_EINVAL, "a packet is larger than the session slot (%llu bytes)",
+                (unsigned long long)s->slot_bytes);
+  }
+  if (s->ctype != HDFS_CRC32C_CSUM_NULL)
+    for (size_t i = 0; i < sub.recs.size(); i++)
+      if (!sub.recs[i].error && sub.recs[i].crc_len > 0) sub.vidx.push_back(i);
+  // the next slot receives the incomplete tail of this one
+  const size_t nx = (hs + 1) % s->hslot.size();
+  int rc = session_wait_slot(s, nx);
+  if (rc) return rc;
+  const uint64_t tail = s->sticky ? 0 : fill - off;
+  if (tail) std::memcpy(s->hslot[nx], base + off, tail);
+  s->hfill[nx] = tail;
+  if (!sub.vidx.empty()) {
+    DevCtx &c = g_ctx[s->dev];
+    layout_piece(sub.recs.data(), sub.vidx.data(), sub.vidx.size(), sub.L);
+    if (sub.L.meta > s->hmeta_cap[hs]) {
+      if (s->hmeta[hs]) HIPCHK(hipHostFree(s->hmeta[hs]));
+      s->hmeta[hs] = nullptr;
+      s->hmeta_cap[hs] = 0;
+      HIPCHK(hipHostMalloc(&s->hmeta[hs], sub.L.meta, hipHostMallocDefault));
+      s->hmeta_cap[hs] = sub.L.meta;
+    }
+    PieceSlot &d = s->dslot[s->nsub & 1];
+    if ((rc = reserve_slot(d, sub.L)) ||
+        (rc = build_piece(sub.recs.data(), sub.vidx.data(), sub.L, s->cs, s->ctype, d, s->hmeta[hs])) ||
+        (rc = enqueue_piece(c, base, sub.L, d, s->hmeta[hs], s->ctype, s->copy, s->comp)))
+      return rc;
+    HIPCHK(hipEventRecord(s->hdone[hs], s->comp));
+    sub.gpu = true;
+    s->nsub++;
+  }
+  for (auto &k : sub.recs) k.stream_off += s->base_off;
+  s->hbusy[hs] = true;
+  s->inflight.push_back(std::move(sub));
+  s->base_off += off;
+  s->cur = nx;
+  return HDFS_CRC32C_OK;
+}
+
+void session_free(hdfs_crc32c_session *s) {
+  if (s->comp) (void)hipStreamSynchronize(s->comp);
+  if (s->copy) (void)hipStreamSynchronize(s->copy);
+  for (auto &d : s->dslot) release_slot(d);
+  for (auto p : s->hslot)
+    if (p) (void)hipHostFree(p);
+  for (auto p : s->hmeta)
+    if (p) (void)hipHostFree(p);
+  for (auto e : s->hdone)
+    if (e) (void)hipEventDestroy(e);
+  if (s->copy) (void)hipStreamDestroy(s->copy);
+  if (s->comp) (void)hipStreamDestroy(s->comp);
+  delete s;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hdfs_crc32c_parse_packets(const void *stream, uint64_t len, int proto, uint32_t chunk_size, int ctype,
+                              hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts, uint64_t *consumed) {
+  return verify_packets_impl(static_cast<const uint8_t *>(stream), len, proto, chunk_size, ctype, pkts, max_pkts,
+                             npkts, consumed, false);
+}
+
+int hdfs_crc32c_verify_packets(const void *stream, uint64_t len, int proto, uint32_t chunk_size, int ctype,
+                               hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts, uint64_t *consumed) {
+  return verify_packets_impl(static_cast<const uint8_t *>(stream), len, proto, chunk_size, ctype, pkts, max_pkts,
+                             npkts, consumed, true);
+}
+
+int hdfs_crc32c_session_create(hdfs_crc32c_session **out, int proto, uint32_t chunk_size, int ctype,
+                               uint64_t slot_bytes, size_t nslots) {
+  if (!out) return fail(HDFS_CRC32C_EINVAL, "null session pointer");
+  *out = nullptr;
+  if (proto != HDFS_CRC32C_PROTO_V1 && proto != HDFS_CRC32C_PROTO_V2)
+    return fail(HDFS_CRC32C_EINVAL, "bad packet protocol %d", proto);
+  if (ctype != HDFS_CRC32C_CSUM_NULL && ctype != HDFS_CRC32C_CSUM_CRC32 && ctype != HDFS_CRC32C_CSUM_CRC32C)
+    return fail(HDFS_CRC32C_EINVAL, "bad checksum type %d", ctype);
+  if (ctype != HDFS_CRC32C_CSUM_NULL && chunk_size == 0) return fail(HDFS_CRC32C_EINVAL, "chunk_size 0");
+  if (!slot_bytes) slot_bytes = uint64_t(64) << 20;
+  if (slot_bytes < 4096) return fail(HDFS_CRC32C_EINVAL, "slot_bytes < 4096");
+  if (!nslots) nslots = 4;
+  if (nslots < 2) return fail(HDFS_CRC32C_EINVAL, "need at least 2 slots");
+  DevCtx *c = nullptr;
+  int rc = ctx_init(-1, &c);
+  if (rc) return rc;
+  DeviceGuard g(c->dev);
+  auto *s = new hdfs_crc32c_session;
+  s->dev = c->dev;
+  s->proto = proto;
+  s->cs = chunk_size;
+  s->ctype = ctype;
+  s->slot_bytes = slot_bytes;
+  s->hslot.assign(nslots, nullptr);
+  s->hfill.assign(nslots, 0);
+  s->hmeta.assign(nslots, nullptr);
+  s->hmeta_cap.assign(nslots, 0);
+  s->hdone.assign(nslots, nullptr);
+  s->hbusy.assign(nslots, false);
+  hipError_t e = hipStreamCreateWithFlags(&s->copy, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&s->comp, hipStreamNonBlocking);
+  for (size_t i = 0; i < nslots && e == hipSuccess; i++) {
+    e = hipHostMalloc(&s->hslot[i], slot_bytes, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&s->hdone[i], hipEventDisableTiming);
+  }
+  if (e != hipSuccess) {
+    session_free(s);
+    return fail(HDFS_CRC32C_ENOMEM, "session allocation: %s", hipGetErrorString(e));
+  }
+  *out = s;
+  return HDFS_CRC32C_OK;
+}
+
+int hdfs_crc32c_session_buffer(hdfs_crc32c_session *s, void **wptr, uint64_t *room) {
+  if (!s || !wptr || !room) return fail(HDFS_CRC32C_EINVAL, "null argument");
+  if (s->sticky) return fail(HDFS_CRC32C_EINVAL, "session stopped after error %d", s->sticky);
+  *wptr = s->hslot[s->cur] + s->hfill[s->cur];
+  *room = s->slot_bytes - s->hfill[s->cur];
+  return HDFS_CRC32C_OK;
+}
+
+int hdfs_crc32c_session_commit(hdfs_crc32c_session *s, uint64_t nbytes) {
+  if (!s) return fail(HDFS_CRC32C_EINVAL, "null session");
+  if (s->sticky) return fail(HDFS_CRC32C_EINVAL, "session stopped after error %d", s->sticky);
+  if (nbytes > s->slot_bytes - s->hfill[s->cur]) return fail(HDFS_CRC32C_EINVAL, "commit past the slot");
+  DeviceGuard g(s->dev);
+  s->hfill[s->cur] += nbytes;
+  return s->hfill[s->cur] == s->slot_bytes ? session_submit(s) : HDFS_CRC32C_OK;
+}
+
+int hdfs_crc32c_session_flush(hdfs_crc32c_session *s) {
+  if (!s) return fail(HDFS_CRC32C_EINVAL, "null session");
+  if (s->sticky) return HDFS_CRC32C_OK;
+  DeviceGuard g(s->dev);
+  return session_submit(s);
+}
+
+int hdfs_crc32c_session_poll(hdfs_crc32c_session *s, hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts,
+                             int wait) {
+  if (!s || !npkts || (max_pkts && !pkts)) return fail(HDFS_CRC32C_EINVAL, "null argument");
+  *npkts = 0;
+  DeviceGuard g(s->dev);
+  bool p = true;
+  while (p && s->ready.size() < max_pkts) {
+    int rc = session_finish_front(s, wait != 0, &p);
+    if (rc) return rc;
+  }
+  size_t n = 0;
+  while (n < max_pkts && !s->ready.empty()) {
+    pkts[n++] = s->ready.front();
+    s->ready.pop_front();
+  }
+  *npkts = n;
+  return first_error(pkts, n);
+}
+
+int hdfs_crc32c_session_pending(const hdfs_crc32c_session *s, uint64_t *buffered, size_t *inflight) {
+  if (!s) return fail(HDFS_CRC32C_EINVAL, "null session");
+  if (buffered) *buffered = s->hfill[s->cur];
+  if (inflight) *inflight = s->inflight.size() + s->ready.size();
+  return HDFS_CRC32C_OK;
+}
+
+void hdfs_crc32c_session_destroy(hdfs_crc32c_session *s) {
+  if (!s) return;
+  DeviceGuard g(s->dev);
+  session_free(s);
+}
+
+}  // extern "C"

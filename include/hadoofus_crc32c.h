@@ -187,6 +187,36 @@ int hdfs_crc32c_parse_packets(const void *stream, uint64_t len, int proto, uint3
 int hdfs_crc32c_verify_packets(const void *stream, uint64_t len, int proto, uint32_t chunk_size,
     int ctype, hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts, uint64_t *consumed);
 
+/* Streaming sessions for socket-fed packets (pinned ring
+ * buffers fed by socket reads, src/net.c:241-263 -> src/datanode.c:2345-2494):
+ * the session owns nslots pinned host slots of slot_bytes (defaults 4 x
+ * 64 MiB); the caller receives straight into the current slot
+ * (session_buffer -> recv() -> session_commit).  A full slot (or a flush) is
+ * framed on the host and its packets verified asynchronously on the GPU
+ * while the caller keeps receiving into the next slot; the incomplete tail
+ * packet moves to the next slot.  session_poll returns finished packet
+ * records in stream order (stream_off counts from the session start; an
+ * empty last packet ends a block and the next block may follow).  A framing
+ * error stops the session (its record is still returned).  A packet larger
+ * than slot_bytes is an error.  One thread per session. */
+typedef struct hdfs_crc32c_session hdfs_crc32c_session;
+int hdfs_crc32c_session_create(hdfs_crc32c_session **s, int proto, uint32_t chunk_size, int ctype,
+    uint64_t slot_bytes, size_t nslots);
+/* Write pointer and free bytes of the current slot. */
+int hdfs_crc32c_session_buffer(hdfs_crc32c_session *s, void **wptr, uint64_t *room);
+/* nbytes were written at the write pointer; a full slot is submitted. */
+int hdfs_crc32c_session_commit(hdfs_crc32c_session *s, uint64_t nbytes);
+/* Submit the current slot's complete packets now (end of input, or latency). */
+int hdfs_crc32c_session_flush(hdfs_crc32c_session *s);
+/* Up to max_pkts finished records; wait != 0 blocks until every submitted
+ * slot is done.  Returns the first packet error among the returned records,
+ * 0, or a negative status. */
+int hdfs_crc32c_session_poll(hdfs_crc32c_session *s, hdfs_crc32c_packet *pkts, size_t max_pkts,
+    size_t *npkts, int wait);
+/* Bytes waiting in the current slot; submitted-but-unreturned packet count. */
+int hdfs_crc32c_session_pending(const hdfs_crc32c_session *s, uint64_t *buffered, size_t *inflight);
+void hdfs_crc32c_session_destroy(hdfs_crc32c_session *s);
+
 /* ---- host-resident streaming (pipelined H2D / kernel / D2H) -------------- */
 /* Per-chunk CRCs of a HOST buffer: pieces of piece_bytes (0 = 64 MiB, rounded
  * to whole 8-chunk tiles) are copied H2D on a copy stream into one of two
