@@ -14,7 +14,7 @@ CSRC = os.path.join(HERE, "csrc")
 INCLUDE = os.path.join(ROOT, "include")
 LIBDIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIBDIR, "libhadoofus_crc32c.so")
-SOURCES = ["crc32c_kernels.hip", "crc32c_engine.cpp", "crc32c_packets.cpp"]
+SOURCES = ["crc32c_kernels.hip", "crc32c_probes.hip", "crc32c_engine.cpp", "crc32c_packets.cpp"]
 HEADERS = ["crc32c_internal.h", "crc32c_tables.h", "crc32c_packets.h"]
 ARCH = os.environ.get("HADOOFUS_OFFLOAD_ARCH", "gfx950")
 

@@ -39,7 +39,7 @@ int env_int(const char *name, int dflt) {
   const char *e = std::getenv(name);
   return e ? std::atoi(e) : dflt;
 }
-int g_tile_order = env_int("HDFS_CRC32C_TILE_ORDER", 2);
+int g_tile_order = env_int("HDFS_CRC32C_TILE_ORDER", 3);
 // Data-stream load policy of the tiled kernel: 0 default, 1 nontemporal.
 int g_nt_loads = env_int("HDFS_CRC32C_NT", 1);
 // Rounds in flight per wave + 1 (register buffers of the tiled kernel): 3 or 4.
@@ -176,7 +176,7 @@ int launch_all(DevCtx &c, int mode, const SegDev *d_segs, uint32_t nseg, uint64_
                uint64_t mtiles, uint64_t gtiles, uint32_t *d_fb, unsigned long long *d_mism,
                uint32_t *d_gctr, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1, bool reset, int ctype) {
   const bool vreset = mode == kModeVerify && reset;
-  uint32_t *gz = (rounds && g_tile_order == 2) ? d_gctr : nullptr;
+  uint32_t *gz = (rounds && g_tile_order >= 2) ? d_gctr : nullptr;
   if (vreset || gz)
     HIPCHK(launch_prep(vreset ? d_fb : nullptr, vreset ? (nseg ? nseg : 1u) : 0u, vreset ? d_mism : nullptr, gz, st));
   if (rounds) {
@@ -185,7 +185,12 @@ int launch_all(DevCtx &c, int mode, const SegDev *d_segs, uint32_t nseg, uint64_
     uint64_t want = (rounds + 63) / 64;
     int grid = static_cast<int>(want < 1 ? 1 : (want > uint64_t(c.num_cu) ? c.num_cu : want));
     if (ev0) HIPCHK(hipEventRecord(ev0, st));
-    HIPCHK(launch_tiles(mode, g_tile_order, g_nt_loads, g_depth, grid, d_segs, nseg, rounds, mtiles,
+    // The interleaved schedule (3) pays a segment look-up whenever a strided
+    // tile leaves the current segment: small launches (which also skip the
+    // pool) and tables of small segments keep the contiguous slices (2).
+    const bool small = rounds < 32ull * 16u * uint64_t(grid) || mtiles < 2ull * uint64_t(grid) * nseg;
+    const int order = (g_tile_order == 3 && small) ? 2 : g_tile_order;
+    HIPCHK(launch_tiles(mode, order, g_nt_loads, g_depth, grid, d_segs, nseg, rounds, mtiles,
                         c.d_tab_main_t[ctype], d_fb, d_mism, g_diag, g_store_policy, d_gctr, st));
     if (ev1) HIPCHK(hipEventRecord(ev1, st));
   }
@@ -859,7 +864,7 @@ int hdfs_crc32c_set_tuning(int nt_loads, void *diag) {
 }
 
 int hdfs_crc32c_set_tile_order(int order) {
-  if (order < 0 || order > 2) return fail(HDFS_CRC32C_EINVAL, "tile order must be 0, 1 or 2");
+  if (order < 0 || order > 3) return fail(HDFS_CRC32C_EINVAL, "tile order must be 0..3");
   g_tile_order = order;
   return HDFS_CRC32C_OK;
 }

@@ -139,7 +139,12 @@ struct Cursor {
 //    that workgroups claim with one global atomic each once their own slice
 //    is done (published to the workgroup's other waves through an LDS slot).
 //    The pool absorbs the cross-workgroup / cross-XCD speed spread; its
-//    atomics only happen at the end, off the hot loop.  Unit size (runtime,
+//    atomics only happen at the end, off the hot loop.
+//  ORDER 3 (interleaved two-phase): as ORDER 2, but the static phase deals
+//    tiles round-robin over the workgroups (workgroup b takes global tiles
+//    b, b+G, b+2G, ...), so at any moment the whole grid reads one contiguous
+//    window of memory instead of G separate streams; the read probes of
+//    crc32c_probes.hip measured this shape faster on MI355X HBM.  Unit size (runtime,
 //    a power of two in [16, 256]) targets >= 4 units per workgroup; launches
 //    with < 32 rounds per wave skip the pool (one unit per workgroup would
 //    make the tail, not shorten it).
@@ -149,7 +154,7 @@ constexpr uint64_t kPhase1Num = 23, kPhase1Den = 25;  // 92 % static
 
 struct Sched {
   uint64_t r1;       // ORDER 0: end of the wave's round slice
-  uint64_t gfirst;   // ORDER 1/2: first global tile of the workgroup's slice
+  uint64_t gfirst;   // ORDER 1/2: first global tile of the workgroup's slice (3: blockIdx)
   uint32_t nk;       // ORDER 1/2: tiles of the workgroup's slice
   uint32_t *ctr;     // ORDER 1/2: LDS ticket counter
   uint32_t lane;
@@ -157,7 +162,8 @@ struct Sched {
   uint64_t ntiles;   // ORDER 2: total tiles
   uint32_t *gctr;    // ORDER 2: global unit counter (zeroed per launch)
   uint64_t *slots;   // ORDER 2: LDS [kSlots] of (unit + 1) << 32 | global unit
-  uint32_t ushift;   // ORDER 2: log2 tiles per pool unit
+  uint32_t ushift;   // ORDER 2/3: log2 tiles per pool unit
+  uint32_t gstride;  // ORDER 3: tile stride of the static phase (gridDim)
 };
 
 DEV uint32_t grab(const Sched &w) {
@@ -171,10 +177,10 @@ DEV uint32_t grab(const Sched &w) {
 template <int ORDER>
 DEV bool ticket_tile(const Sched &w, uint32_t t, uint64_t &g) {
   if (t < w.nk) {
-    g = w.gfirst + t;
+    g = w.gfirst + (ORDER == 3 ? uint64_t(t) * w.gstride : uint64_t(t));
     return true;
   }
-  if (ORDER != 2) return false;
+  if (ORDER < 2) return false;
   const uint32_t j = t - w.nk, u = j >> w.ushift, o = j & ((1u << w.ushift) - 1u), s = u % kSlots;
   if (o == 0) {  // first ticket of local unit u: claim a pool unit and publish it
     uint32_t gu = 0;
@@ -214,7 +220,9 @@ DEV Cursor advance(Cursor c, SegP segs, uint32_t nseg, const Sched &w) {
       c.valid = false;
       return c;
     }
-    if (ORDER == 2 && g < segs[c.seg].mtile_start) {  // pool tiles may lie behind the slice
+    if ((ORDER == 2 && g < segs[c.seg].mtile_start) ||  // pool tiles may lie behind the slice
+        (ORDER == 3 && (g < segs[c.seg].mtile_start ||   // interleaved tiles jump G ahead
+                        g >= segs[c.seg].mtile_start + segs[c.seg].main_tiles))) {
       uint32_t lo = 0, hi = nseg;
       while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
@@ -422,13 +430,21 @@ __global__ __launch_bounds__(1024) void crc32c_tiles_kernel(
       }
     }
   } else {
-    const bool pool = ORDER == 2 && total_rounds >= 32ull * nwaves;
-    const uint64_t r_static = pool ? total_rounds * kPhase1Num / kPhase1Den : total_rounds;
-    const uint64_t b0 = rfl64(r_static * blockIdx.x / gridDim.x);
-    const uint64_t b1 = rfl64(r_static * (blockIdx.x + 1) / gridDim.x);
-    w.gfirst = tile_at_round(sg, nseg, b0, total_tiles);
-    w.nk = static_cast<uint32_t>(tile_at_round(sg, nseg, b1, total_tiles) - w.gfirst);
-    w.p2first = tile_at_round(sg, nseg, r_static, total_tiles);
+    const bool pool = ORDER >= 2 && total_rounds >= 32ull * nwaves;
+    if (ORDER == 3) {
+      const uint64_t p2 = pool ? total_tiles * kPhase1Num / kPhase1Den : total_tiles;
+      w.gfirst = blockIdx.x;
+      w.gstride = gridDim.x;
+      w.nk = p2 > blockIdx.x ? static_cast<uint32_t>((p2 - 1 - blockIdx.x) / gridDim.x + 1) : 0u;
+      w.p2first = p2;
+    } else {
+      const uint64_t r_static = pool ? total_rounds * kPhase1Num / kPhase1Den : total_rounds;
+      const uint64_t b0 = rfl64(r_static * blockIdx.x / gridDim.x);
+      const uint64_t b1 = rfl64(r_static * (blockIdx.x + 1) / gridDim.x);
+      w.gfirst = tile_at_round(sg, nseg, b0, total_tiles);
+      w.nk = static_cast<uint32_t>(tile_at_round(sg, nseg, b1, total_tiles) - w.gfirst);
+      w.p2first = tile_at_round(sg, nseg, r_static, total_tiles);
+    }
     w.ntiles = total_tiles;
     {
       const uint64_t per = (total_tiles - w.p2first) / (4ull * gridDim.x);
@@ -796,7 +812,10 @@ hipError_t launch_tiles(int mode, int order, int nt, int depth, int grid, const 
                      total_rounds, total_tiles, gtab, first_bad, mism, diag, store_policy, gctr)
 #define HDFS_LAUNCH_M(M)                                                   \
   do {                                                                     \
-    if (order == 2) HDFS_LAUNCH(M, 2, 1, 3);                               \
+    if (order == 3 && depth == 4) HDFS_LAUNCH(M, 3, 1, 4);                 \
+    else if (order == 3) HDFS_LAUNCH(M, 3, 1, 3);                          \
+    else if (order == 2 && depth == 4) HDFS_LAUNCH(M, 2, 1, 4);            \
+    else if (order == 2) HDFS_LAUNCH(M, 2, 1, 3);                          \
     else if (depth == 4) HDFS_LAUNCH(M, 1, 1, 4);                          \
     else if (order && nt) HDFS_LAUNCH(M, 1, 1, 3);                         \
     else if (order) HDFS_LAUNCH(M, 1, 0, 3);                               \
@@ -861,8 +880,12 @@ __global__ __launch_bounds__(1024) void probe_quad_kernel(const uint8_t *__restr
   if (v == 0x9E3779B9u) out[0] = v;
 }
 
+hipError_t launch_probe2(const uint8_t *p, uint64_t nbytes, uint32_t *out, int grid, int block, int variant,
+                         hipStream_t stream);
+
 hipError_t launch_probe_read(const uint8_t *p, uint64_t nbytes, uint32_t *out, int grid, int block, int variant,
                              hipStream_t stream) {
+  if (variant >= 10) return launch_probe2(p, nbytes, out, grid, block, variant, stream);
   switch (variant) {
     case 1: hipLaunchKernelGGL((probe_read_kernel<4, 1>), dim3(grid), dim3(block), 0, stream, p, nbytes, out); break;
     case 2: hipLaunchKernelGGL((probe_read_kernel<8, 0>), dim3(grid), dim3(block), 0, stream, p, nbytes, out); break;

@@ -254,8 +254,11 @@ int hdfs_crc32c_plan_time(hdfs_crc32c_plan *plan, void *stream, int iters, doubl
 /* hipDeviceSynchronize on the engine's device. */
 int hdfs_crc32c_device_sync(void);
 /* Tiled-kernel schedule: 0 static per-wave slices, 1 workgroup-dynamic,
- * 2 (default) workgroup-dynamic over 92 % + a global pool of 256-tile units
- * (waves of a workgroup take tiles from an LDS counter).  Env
+ * 2 workgroup-dynamic over contiguous slices of 92 % of the tiles + a global
+ * pool of 16-256-tile units, 3 (default) as 2 but the static 92 % dealt
+ * round-robin over the workgroups (the grid sweeps one contiguous window;
+ * launches that are small or made of small segments fall back to 2).
+ * Waves of a workgroup take tiles from an LDS counter.  Env
  * HDFS_CRC32C_TILE_ORDER. */
 int hdfs_crc32c_set_tile_order(int order);
 /* Tuning / diagnostics: nt_loads=1 (default) streams chunk data with nontemporal loads

@@ -29,7 +29,8 @@ comp = h.Plan(h.MODE_COMPUTE, segs)
 ver = h.Plan(h.MODE_VERIFY, segs)
 comp.execute()
 h.device_sync()
-VARIANTS = [(1, 1, 3), (2, 1, 3)]  # (order, nt, depth)
+VARIANTS = [tuple(int(x) for x in v.split(",")) for v in
+            os.environ.get("AB_VARIANTS", "1,1,3;2,1,3").split(";")]  # (order, nt, depth)
 res = {}
 for rnd in range(4):
     for order, nt, depth in VARIANTS:
@@ -77,6 +78,6 @@ for order, nt, depth in list(VARIANTS)[::-1] + list(VARIANTS):
     })
     np.save(os.path.join(ROOT, "gpurun_out", f"diag_o{order}_nt{nt}_d{depth}.npy"), d)
 h.set_tuning(1, None)
-h.set_tile_order(1)
+h.set_tile_order(3)
 h.set_depth(3)
 print(json.dumps(out))
