@@ -15,7 +15,7 @@ INCLUDE = os.path.join(ROOT, "include")
 LIBDIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIBDIR, "libhadoofus_crc32c.so")
 SOURCES = ["crc32c_kernels.hip", "crc32c_probes.hip", "crc32c_engine.cpp", "crc32c_packets.cpp"]
-HEADERS = ["crc32c_internal.h", "crc32c_tables.h", "crc32c_packets.h"]
+HEADERS = ["crc32c_internal.h", "crc32c_tables.h", "crc32c_packets.h", "crc32c_engine.h", "exports.map"]
 ARCH = os.environ.get("HADOOFUS_OFFLOAD_ARCH", "gfx950")
 
 
@@ -41,7 +41,7 @@ def build(force=False, verbose=False):
     os.makedirs(LIBDIR, exist_ok=True)
     tmp = LIB + ".tmp"
     cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-function", f"-I{INCLUDE}", f"-I{CSRC}",
+           "-Wall", "-Wno-unused-function", f"-Wl,--version-script={os.path.join(CSRC, 'exports.map')}", f"-I{INCLUDE}", f"-I{CSRC}",
            "-o", tmp] + [os.path.join(CSRC, f) for f in SOURCES]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)

@@ -45,6 +45,32 @@ def test_exports_every_declared_symbol(libpath):
         assert n in exported
 
 
+def test_exports_nothing_else(libpath):
+    """Built with -fvisibility=hidden: the only exported functions are the
+    declared C ABI (HIP kernel host stubs are exported by the toolchain)."""
+    out = subprocess.check_output(["nm", "-D", "--defined-only", libpath], text=True)
+    decl = set(_declared("crc32c.h")) | set(_declared("hadoofus_crc32c.h"))
+    extra = []
+    for line in out.splitlines():
+        parts = line.split()
+        if len(parts) < 3 or parts[1] not in "TW":
+            continue
+        name = parts[2]
+        if name in decl or name in ("_init", "_fini"):
+            continue
+        if name.startswith("_ZN11hdfs_crc32c") and "_kernel" in name:
+            continue
+        extra.append(name)
+    assert not extra, extra
+
+
+def test_packet_struct_layout():
+    import ctypes
+
+    from hadoofus_amd.abi import Packet
+    assert ctypes.sizeof(Packet) == 56
+
+
 def test_segment_struct_layout():
     import ctypes
 
