@@ -91,7 +91,7 @@ def load(path=LIB_PATH):
         raise ImportError(f"{path} not built; run `python -m hadoofus_amd.build` "
                           "(or __graft_entry__.build())")
     lib = ctypes.CDLL(path)
-    for n in ("_hdfs_crc32c", "_hdfs_sse42_crc32c", "_hdfs_sw_crc32c"):
+    for n in ("_hdfs_crc32c", "_hdfs_sse42_crc32c", "_hdfs_armv8_crc32c", "_hdfs_sw_crc32c"):
         _bind(lib, n, _u32, [_u32, _vp, ctypes.c_uint])
     _bind(lib, "hdfs_crc32c_last_error", ctypes.c_char_p, [])
     _bind(lib, "hdfs_crc32c_init", _int, [_int])

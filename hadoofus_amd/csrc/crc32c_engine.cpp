@@ -462,6 +462,13 @@ uint32_t _hdfs_sse42_crc32c(uint32_t crc, const void *buf, unsigned len) {
   return out;
 }
 
+uint32_t _hdfs_armv8_crc32c(uint32_t crc, const void *buf, unsigned len) {
+  uint32_t out = 0;
+  if (len == 0) return crc;
+  if (stream_crc_any(crc, buf, len, &out)) die("_hdfs_armv8_crc32c");
+  return out;
+}
+
 uint32_t _hdfs_sw_crc32c(uint32_t crc, const void *buf, unsigned len) {
   uint32_t out = 0;
   if (len == 0) return crc;

@@ -6,8 +6,9 @@
  * libhadoofus_crc32c.so.  Semantics are those of the reference: the CRC is
  * pre- and post-inverted inside the call; pass 0 to start and the previous
  * return value to continue.  Every backend symbol is served by the MI355X
- * engine (include/hadoofus_crc32c.h); _hdfs_armv8_crc32c is not provided
- * (aarch64 only in the reference).
+ * engine (include/hadoofus_crc32c.h), with the reference's per-architecture
+ * declarations (src/crc32c.h:15-22); the library defines all four, so
+ * either declaration set links.
  */
 #ifndef _HADOOFUS_CRC32C_H
 #define _HADOOFUS_CRC32C_H
@@ -19,7 +20,13 @@ extern "C" {
 #endif
 
 uint32_t _hdfs_crc32c(uint32_t crc, const void *buf, unsigned len);
+
+#if defined(__amd64__) || defined(__i386__)
 uint32_t _hdfs_sse42_crc32c(uint32_t crc, const void *buf, unsigned len);
+#elif defined(__aarch64__)
+uint32_t _hdfs_armv8_crc32c(uint32_t crc, const void *buf, unsigned len);
+#endif
+
 uint32_t _hdfs_sw_crc32c(uint32_t crc, const void *buf, unsigned len);
 
 #ifdef __cplusplus

@@ -33,6 +33,7 @@ extern "C" {
 /* ---- 1. drop-in (replaces src/crc32c.h:13, :17, :24) -------------------- */
 uint32_t _hdfs_crc32c(uint32_t crc, const void *buf, unsigned len);
 uint32_t _hdfs_sse42_crc32c(uint32_t crc, const void *buf, unsigned len);
+uint32_t _hdfs_armv8_crc32c(uint32_t crc, const void *buf, unsigned len);  /* aarch64 name, same engine */
 uint32_t _hdfs_sw_crc32c(uint32_t crc, const void *buf, unsigned len);
 
 /* ---- status codes ------------------------------------------------------- */
