@@ -1,0 +1,117 @@
+/*
+ * C consumer of the packet-stream API (include/hadoofus_crc32c.h), written
+ * the way a datanode receive loop would use it (src/datanode.c:2345-2494):
+ * builds a v2 packet stream in memory (PacketHeaderProto encoded by hand,
+ * CRCs from the engine's own write-path mirror hdfs_crc32c_compose_crcs),
+ * corrupts one chunk, then verifies it (1) in one hdfs_crc32c_verify_packets
+ * call and (2) through a streaming session fed in odd-sized "socket reads".
+ * Prints "0 failures" on success.  Test infrastructure (tests/test_abi.py
+ * links it on CPU, tests/test_packets.py runs it on the GPU).
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "hadoofus_crc32c.h"
+
+#define NPK 40
+#define DLEN 65536
+#define CS 512
+
+static int failures;
+
+static void check(int cond, const char *what)
+{
+	if (!cond) {
+		printf("FAIL: %s (%s)\n", what, hdfs_crc32c_last_error());
+		failures++;
+	}
+}
+
+static size_t put_be32(uint8_t *p, uint32_t v)
+{
+	p[0] = v >> 24; p[1] = v >> 16; p[2] = v >> 8; p[3] = v;
+	return 4;
+}
+
+/* [plen s32][hlen u16][PacketHeaderProto]: fields 1,2 sfixed64, 3 bool, 4 sfixed32 */
+static size_t put_header(uint8_t *p, int64_t off, int64_t seq, int last, int32_t dlen, int32_t crclen)
+{
+	size_t n = put_be32(p, (uint32_t)(4 + crclen + dlen));
+	p[n++] = 0;
+	p[n++] = 25;
+	p[n++] = 0x09; memcpy(p + n, &off, 8); n += 8;
+	p[n++] = 0x11; memcpy(p + n, &seq, 8); n += 8;
+	p[n++] = 0x18; p[n++] = (uint8_t)(last != 0);
+	p[n++] = 0x25; memcpy(p + n, &dlen, 4); n += 4;
+	return n;
+}
+
+int main(void)
+{
+	const size_t crclen = DLEN / CS * 4, pk = 31 + crclen + DLEN;
+	const size_t total = NPK * pk + 31;
+	uint8_t *s = malloc(total), *data = malloc(DLEN);
+	hdfs_crc32c_packet rec[NPK + 1];
+	size_t n = 0;
+	uint64_t used = 0;
+	uint32_t x = 12345;
+
+	for (int k = 0; k < NPK; k++) {
+		uint8_t *p = s + k * pk;
+		for (int i = 0; i < DLEN; i++) {
+			x = x * 1103515245u + 12345u;
+			data[i] = (uint8_t)(x >> 16);
+		}
+		size_t h = put_header(p, (int64_t)k * DLEN, k, 0, DLEN, (int32_t)crclen);
+		const void *base = data;
+		size_t len = DLEN;
+		check(hdfs_crc32c_compose_crcs(&base, &len, 1, DLEN, CS, HDFS_CRC32C_CSUM_CRC32C, p + h) == 0,
+		    "compose_crcs");
+		memcpy(p + h + crclen, data, DLEN);
+	}
+	put_header(s + NPK * pk, (int64_t)NPK * DLEN, NPK, 1, 0, 0);
+	s[7 * pk + 31 + crclen + 3 * CS + 17] ^= 0x40; /* packet 7, chunk 3 */
+
+	int rc = hdfs_crc32c_verify_packets(s, total, HDFS_CRC32C_PROTO_V2, CS, HDFS_CRC32C_CSUM_CRC32C,
+	    rec, NPK + 1, &n, &used);
+	check(rc == HDFS_CRC32C_ERR_DATANODE_BAD_CHECKSUM, "verify_packets rc");
+	check(n == NPK + 1 && used == total, "verify_packets count");
+	for (size_t i = 0; i < n; i++)
+		check(rec[i].error == (i == 7 ? HDFS_CRC32C_ERR_DATANODE_BAD_CHECKSUM : 0) &&
+		    rec[i].first_bad == (i == 7 ? 3 : -1), "per-packet verdict");
+
+	hdfs_crc32c_session *sess = NULL;
+	check(hdfs_crc32c_session_create(&sess, HDFS_CRC32C_PROTO_V2, CS, HDFS_CRC32C_CSUM_CRC32C,
+	    1 << 20, 3) == 0, "session_create");
+	size_t off = 0, got = 0, bad = 0;
+	while (off < total && !failures) {
+		void *w;
+		uint64_t room;
+		check(hdfs_crc32c_session_buffer(sess, &w, &room) == 0, "session_buffer");
+		size_t chunk = 70001 < room ? 70001 : (size_t)room;
+		if (chunk > total - off)
+			chunk = total - off;
+		memcpy(w, s + off, chunk); /* recv() would write here */
+		check(hdfs_crc32c_session_commit(sess, chunk) == 0, "session_commit");
+		off += chunk;
+	}
+	check(hdfs_crc32c_session_flush(sess) == 0, "session_flush");
+	for (;;) {
+		size_t k = 0;
+		rc = hdfs_crc32c_session_poll(sess, rec, NPK + 1, &k, 1);
+		check(rc >= 0, "session_poll");
+		if (!k)
+			break;
+		for (size_t i = 0; i < k; i++)
+			bad += rec[i].error != 0;
+		got += k;
+	}
+	hdfs_crc32c_session_destroy(sess);
+	check(got == NPK + 1 && bad == 1, "session records");
+	printf("%d failures\n", failures);
+	free(s);
+	free(data);
+	return failures != 0;
+}

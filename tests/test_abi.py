@@ -124,6 +124,20 @@ def build_consumer(tmp_path, libpath):
     return exe, txt
 
 
+def build_c(tmp_path, libpath, name):
+    """Compile + link tests/consumer/<name>.c against the engine."""
+    exe = tmp_path / name
+    libdir = os.path.dirname(libpath)
+    subprocess.check_call(["gcc", "-std=gnu99", "-O2", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+                           os.path.join(ROOT, "tests", "consumer", name + ".c"), "-o", str(exe),
+                           "-L", libdir, "-Wl,-rpath," + libdir, "-lhadoofus_crc32c"])
+    return exe
+
+
+def test_packet_consumer_links(tmp_path, libpath):
+    assert build_c(tmp_path, libpath, "packet_consumer").exists()
+
+
 def test_dropin_consumer_links(tmp_path, libpath):
     exe, txt = build_consumer(tmp_path, libpath)
     assert exe.exists() and txt.read_text().count("\n") >= 7

@@ -127,3 +127,17 @@ def test_gpu_verify_packets_pinned_stream(engine, oracle):
     got = engine.verify_packets(pin.array)
     assert got == oracle.verify_packets(s)
     pin.free()
+
+
+@pytest.mark.gpu
+def test_gpu_packet_consumer_runs(engine, tmp_path):
+    """The C consumer (tests/consumer/packet_consumer.c) verifies a packet
+    run in one call and through a session fed in odd-sized reads."""
+    import subprocess
+
+    from hadoofus_amd import build
+    from test_abi import build_c
+    exe = build_c(tmp_path, build.LIB, "packet_consumer")
+    p = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "0 failures" in p.stdout
