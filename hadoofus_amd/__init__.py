@@ -48,6 +48,7 @@ from .abi import (  # noqa: F401
     set_tuning,
     set_probe,
     set_depth,
+    set_group_shift,
     set_store_policy,
     load,
     stream_crc_dev,

@@ -132,6 +132,7 @@ def load(path=LIB_PATH):
     _bind(lib, "hdfs_crc32c_corrupt", _int, [_vp, _u64, _u32, _u64, _u64, _u64, _vp])
     _bind(lib, "hdfs_crc32c_device_sync", _int, [])
     _bind(lib, "hdfs_crc32c_set_tile_order", _int, [_int])
+    _bind(lib, "hdfs_crc32c_set_group_shift", _int, [_int])
     _bind(lib, "hdfs_crc32c_probe_read", _int, [_vp, _u64, _vp, _int, ctypes.POINTER(ctypes.c_double)])
     _bind(lib, "hdfs_crc32c_set_tuning", _int, [_int, _vp])
     _bind(lib, "hdfs_crc32c_set_probe", _int, [_int, _int, _int])
@@ -464,6 +465,10 @@ class PinnedBuffer:
 
 def set_probe(variant=0, grid_per_cu=2, block=1024):
     _check(load().hdfs_crc32c_set_probe(variant, grid_per_cu, block))
+
+
+def set_group_shift(shift):
+    _check(load().hdfs_crc32c_set_group_shift(shift))
 
 
 def set_depth(depth):

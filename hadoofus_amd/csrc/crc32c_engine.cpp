@@ -47,6 +47,8 @@ int g_depth = env_int("HDFS_CRC32C_DEPTH", 3);
 // Result-store policy of the tiled kernel: 0 default, 1 nontemporal,
 // 2 diagnostic only (drops the compute-mode CRC stores).
 uint32_t g_store_policy = uint32_t(env_int("HDFS_CRC32C_STORE", 0));
+// Schedule 3: log2 tiles per round-robin group (0..6).
+uint32_t g_group_shift = uint32_t(env_int("HDFS_CRC32C_GROUP", 2)) & 15u;
 // Diagnostic per-wave timestamps (device buffer, 3 x u64 per wave) or null.
 unsigned long long *g_diag = nullptr;
 
@@ -191,7 +193,8 @@ int launch_all(DevCtx &c, int mode, const SegDev *d_segs, uint32_t nseg, uint64_
     const bool small = rounds < 32ull * 16u * uint64_t(grid) || mtiles < 2ull * uint64_t(grid) * nseg;
     const int order = (g_tile_order == 3 && small) ? 2 : g_tile_order;
     HIPCHK(launch_tiles(mode, order, g_nt_loads, g_depth, grid, d_segs, nseg, rounds, mtiles,
-                        c.d_tab_main_t[ctype], d_fb, d_mism, g_diag, g_store_policy, d_gctr, st));
+                        c.d_tab_main_t[ctype], d_fb, d_mism, g_diag, g_store_policy | (g_group_shift << 8), d_gctr,
+                        st));
     if (ev1) HIPCHK(hipEventRecord(ev1, st));
   }
   if (gtiles) HIPCHK(launch_generic(mode, d_segs, nseg, gtiles, c.d_tab_main_t[ctype], d_fb, d_mism, st));
@@ -867,6 +870,12 @@ int hdfs_crc32c_set_depth(int depth) {
 int hdfs_crc32c_set_tuning(int nt_loads, void *diag) {
   g_nt_loads = nt_loads ? 1 : 0;
   g_diag = static_cast<unsigned long long *>(diag);
+  return HDFS_CRC32C_OK;
+}
+
+int hdfs_crc32c_set_group_shift(int shift) {
+  if (shift < 0 || shift > 6) return fail(HDFS_CRC32C_EINVAL, "group shift must be 0..6");
+  g_group_shift = uint32_t(shift);
   return HDFS_CRC32C_OK;
 }
 

@@ -141,10 +141,13 @@ struct Cursor {
 //    The pool absorbs the cross-workgroup / cross-XCD speed spread; its
 //    atomics only happen at the end, off the hot loop.
 //  ORDER 3 (interleaved two-phase): as ORDER 2, but the static phase deals
-//    tiles round-robin over the workgroups (workgroup b takes global tiles
-//    b, b+G, b+2G, ...), so at any moment the whole grid reads one contiguous
-//    window of memory instead of G separate streams; the read probes of
-//    crc32c_probes.hip measured this shape faster on MI355X HBM.  Unit size (runtime,
+//    groups of 2^gshift consecutive tiles round-robin over the workgroups
+//    (workgroup b takes groups b, b+G, b+2G, ...), so at any moment the
+//    whole grid reads one contiguous window of memory instead of G separate
+//    streams; the read probes of crc32c_probes.hip measured this shape
+//    faster on MI355X HBM.  Groups of 4 tiles own whole 128-B lines of
+//    expected CRCs (8 chunks x 4 B per tile), so no two XCDs' L2s fetch
+//    the same CRC line.  Unit size (runtime,
 //    a power of two in [16, 256]) targets >= 4 units per workgroup; launches
 //    with < 32 rounds per wave skip the pool (one unit per workgroup would
 //    make the tail, not shorten it).
@@ -163,7 +166,8 @@ struct Sched {
   uint32_t *gctr;    // ORDER 2: global unit counter (zeroed per launch)
   uint64_t *slots;   // ORDER 2: LDS [kSlots] of (unit + 1) << 32 | global unit
   uint32_t ushift;   // ORDER 2/3: log2 tiles per pool unit
-  uint32_t gstride;  // ORDER 3: tile stride of the static phase (gridDim)
+  uint32_t gstride;  // ORDER 3: group stride of the static phase (gridDim)
+  uint32_t gshift;   // ORDER 3: log2 tiles per group
 };
 
 DEV uint32_t grab(const Sched &w) {
@@ -177,7 +181,10 @@ DEV uint32_t grab(const Sched &w) {
 template <int ORDER>
 DEV bool ticket_tile(const Sched &w, uint32_t t, uint64_t &g) {
   if (t < w.nk) {
-    g = w.gfirst + (ORDER == 3 ? uint64_t(t) * w.gstride : uint64_t(t));
+    if (ORDER == 3)
+      g = ((w.gfirst + uint64_t(t >> w.gshift) * w.gstride) << w.gshift) + (t & ((1u << w.gshift) - 1u));
+    else
+      g = w.gfirst + t;
     return true;
   }
   if (ORDER < 2) return false;
@@ -355,7 +362,7 @@ template <int MODE, int ORDER, int NT, int DEPTH>
 __global__ __launch_bounds__(1024) void crc32c_tiles_kernel(
     const SegDev *__restrict__ segs, uint32_t nseg, uint64_t total_rounds, uint64_t total_tiles,
     const uint32_t *__restrict__ gtab, uint32_t *__restrict__ first_bad,
-    unsigned long long *__restrict__ mism, unsigned long long *__restrict__ diag, uint32_t store_policy,
+    unsigned long long *__restrict__ mism, unsigned long long *__restrict__ diag, uint32_t tune,
     uint32_t *__restrict__ gctr) {
   // + ticket counter, pad, kSlots 64-bit pool slots
   __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords + 2 + 2 * kSlots];
@@ -392,7 +399,7 @@ __global__ __launch_bounds__(1024) void crc32c_tiles_kernel(
   __syncthreads();
 
   LaneConst L;
-  L.store_policy = store_policy;
+  L.store_policy = tune & 0xffu;  // tune: [7:0] store policy, [11:8] ORDER-3 group shift
   L.lane = threadIdx.x & 63u;
   L.hsel = (L.lane >> 3) & 1u;                              // load: odd sub-chunk of each 1 KiB
   L.loff = 16u * (4u * (L.lane & 7u) + (L.lane >> 4));      // load: byte offset in the sub-chunk
@@ -432,11 +439,14 @@ __global__ __launch_bounds__(1024) void crc32c_tiles_kernel(
   } else {
     const bool pool = ORDER >= 2 && total_rounds >= 32ull * nwaves;
     if (ORDER == 3) {
-      const uint64_t p2 = pool ? total_tiles * kPhase1Num / kPhase1Den : total_tiles;
+      // static phase: whole groups only; the pool takes the rest
+      w.gshift = (tune >> 8) & 15u;
+      const uint64_t ngroups = (pool ? total_tiles * kPhase1Num / kPhase1Den : total_tiles) >> w.gshift;
       w.gfirst = blockIdx.x;
       w.gstride = gridDim.x;
-      w.nk = p2 > blockIdx.x ? static_cast<uint32_t>((p2 - 1 - blockIdx.x) / gridDim.x + 1) : 0u;
-      w.p2first = p2;
+      w.nk = ngroups > blockIdx.x ? static_cast<uint32_t>(((ngroups - 1 - blockIdx.x) / gridDim.x + 1) << w.gshift)
+                                  : 0u;
+      w.p2first = ngroups << w.gshift;
     } else {
       const uint64_t r_static = pool ? total_rounds * kPhase1Num / kPhase1Den : total_rounds;
       const uint64_t b0 = rfl64(r_static * blockIdx.x / gridDim.x);
@@ -806,10 +816,10 @@ hipError_t launch_gather(const uint8_t *raw, const PktDesc *descs, uint32_t npk,
 hipError_t launch_tiles(int mode, int order, int nt, int depth, int grid, const SegDev *segs, uint32_t nseg,
                         uint64_t total_rounds, uint64_t total_tiles, const uint32_t *gtab,
                         uint32_t *first_bad, unsigned long long *mism, unsigned long long *diag,
-                        uint32_t store_policy, uint32_t *gctr, hipStream_t stream) {
+                        uint32_t tune, uint32_t *gctr, hipStream_t stream) {
 #define HDFS_LAUNCH(M, O, N, D)                                                                        \
   hipLaunchKernelGGL((crc32c_tiles_kernel<M, O, N, D>), dim3(grid), dim3(1024), 0, stream, segs, nseg,  \
-                     total_rounds, total_tiles, gtab, first_bad, mism, diag, store_policy, gctr)
+                     total_rounds, total_tiles, gtab, first_bad, mism, diag, tune, gctr)
 #define HDFS_LAUNCH_M(M)                                                   \
   do {                                                                     \
     if (order == 3 && depth == 4) HDFS_LAUNCH(M, 3, 1, 4);                 \

@@ -30,16 +30,18 @@ ver = h.Plan(h.MODE_VERIFY, segs)
 comp.execute()
 h.device_sync()
 VARIANTS = [tuple(int(x) for x in v.split(",")) for v in
-            os.environ.get("AB_VARIANTS", "1,1,3;2,1,3").split(";")]  # (order, nt, depth)
+            os.environ.get("AB_VARIANTS", "1,1,3;2,1,3").split(";")]  # (order, nt, depth[, group shift])
+VARIANTS = [v if len(v) == 4 else v + (2,) for v in VARIANTS]
 res = {}
 for rnd in range(4):
-    for order, nt, depth in VARIANTS:
+    for order, nt, depth, gs in VARIANTS:
         h.set_tile_order(order)
         h.set_tuning(nt, None)
         h.set_depth(depth)
+        h.set_group_shift(gs)
         for name, p in (("compute", comp), ("verify", ver)):
             ms = p.time(3)
-            res.setdefault(f"{name}_o{order}_nt{nt}_d{depth}", []).append(B * BLOCK / (ms * 1e-3) / 1e9)
+            res.setdefault(f"{name}_o{order}_nt{nt}_d{depth}_g{gs}", []).append(B * BLOCK / (ms * 1e-3) / 1e9)
 fb, m = ver.results()
 out["verify_mismatches"] = m
 for k, v in res.items():
@@ -47,9 +49,10 @@ for k, v in res.items():
 # per-wave timestamps for the default variant
 nwaves = 256 * 16
 diag = h.DeviceBuffer(nwaves * 3 * 8)
-for order, nt, depth in list(VARIANTS)[::-1] + list(VARIANTS):
+for order, nt, depth, gs in list(VARIANTS)[::-1][:2]:
     h.set_tile_order(order)
     h.set_depth(depth)
+    h.set_group_shift(gs)
     h.set_tuning(nt, diag.ptr)
     diag.fill(0)
     ver.execute()
@@ -59,7 +62,7 @@ for order, nt, depth in list(VARIANTS)[::-1] + list(VARIANTS):
     ok = en > 0
     t0 = st[ok].min()
     span = (en[ok].max() - t0) / 100.0  # 100 MHz ticks -> us
-    out[f"diag_o{order}_nt{nt}_d{depth}"] = {
+    out[f"diag_o{order}_nt{nt}_d{depth}_g{gs}"] = {
         "span_us": round(span, 1),
         "wave_end_p50_us": round(float(np.percentile(en[ok] - t0, 50)) / 100, 1),
         "wave_end_p05_us": round(float(np.percentile(en[ok] - t0, 5)) / 100, 1),
@@ -70,14 +73,15 @@ for order, nt, depth in list(VARIANTS)[::-1] + list(VARIANTS):
     e = ((en - t0) / 100.0).reshape(-1, 16)  # [block][wave]
     blk_max, blk_min = e.max(1), e.min(1)
     xcd = np.arange(e.shape[0]) % 8
-    out[f"diag_o{order}_nt{nt}_d{depth}"].update({
+    out[f"diag_o{order}_nt{nt}_d{depth}_g{gs}"].update({
         "within_block_spread_us_median": round(float(np.median(blk_max - blk_min)), 1),
         "block_end_max_p05_p50_p95_us": [round(float(np.percentile(blk_max, q)), 1) for q in (5, 50, 95)],
         "xcd_mean_block_end_us": [round(float(blk_max[xcd == x].mean()), 1) for x in range(8)],
         "wave_in_block_mean_end_us": [round(float(v), 1) for v in e.mean(0)],
     })
-    np.save(os.path.join(ROOT, "gpurun_out", f"diag_o{order}_nt{nt}_d{depth}.npy"), d)
+    np.save(os.path.join(ROOT, "gpurun_out", f"diag_o{order}_nt{nt}_d{depth}_g{gs}.npy"), d)
 h.set_tuning(1, None)
 h.set_tile_order(3)
 h.set_depth(3)
+h.set_group_shift(2)
 print(json.dumps(out))
