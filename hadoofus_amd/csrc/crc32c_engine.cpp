@@ -48,7 +48,7 @@ int g_depth = env_int("HDFS_CRC32C_DEPTH", 3);
 // 2 diagnostic only (drops the compute-mode CRC stores).
 uint32_t g_store_policy = uint32_t(env_int("HDFS_CRC32C_STORE", 0));
 // Schedule 3: log2 tiles per round-robin group (0..6).
-uint32_t g_group_shift = uint32_t(env_int("HDFS_CRC32C_GROUP", 2)) & 15u;
+uint32_t g_group_shift = uint32_t(env_int("HDFS_CRC32C_GROUP", 3)) & 15u;
 // Diagnostic per-wave timestamps (device buffer, 3 x u64 per wave) or null.
 unsigned long long *g_diag = nullptr;
 

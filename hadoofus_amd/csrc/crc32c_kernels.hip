@@ -145,9 +145,9 @@ struct Cursor {
 //    (workgroup b takes groups b, b+G, b+2G, ...), so at any moment the
 //    whole grid reads one contiguous window of memory instead of G separate
 //    streams; the read probes of crc32c_probes.hip measured this shape
-//    faster on MI355X HBM.  Groups of 4 tiles own whole 128-B lines of
-//    expected CRCs (8 chunks x 4 B per tile), so no two XCDs' L2s fetch
-//    the same CRC line.  Unit size (runtime,
+//    faster on MI355X HBM.  Groups of >= 4 tiles own whole 128-B lines of
+//    expected / computed CRCs (8 chunks x 4 B per tile), so no two XCDs'
+//    L2s fetch or write the same CRC line (default 8 tiles per group).  Unit size (runtime,
 //    a power of two in [16, 256]) targets >= 4 units per workgroup; launches
 //    with < 32 rounds per wave skip the pool (one unit per workgroup would
 //    make the tail, not shorten it).

@@ -262,8 +262,9 @@ int hdfs_crc32c_device_sync(void);
  * Waves of a workgroup take tiles from an LDS counter.  Env
  * HDFS_CRC32C_TILE_ORDER. */
 int hdfs_crc32c_set_tile_order(int order);
-/* Schedule 3: 2^shift consecutive tiles per round-robin group (default 2:
- * one 128-B line of expected CRCs per group).  Env HDFS_CRC32C_GROUP. */
+/* Schedule 3: 2^shift consecutive tiles per round-robin group (default 3:
+ * 32 KiB of 512-B chunks, two whole 128-B lines of CRCs per group).  Env
+ * HDFS_CRC32C_GROUP. */
 int hdfs_crc32c_set_group_shift(int shift);
 /* Tuning / diagnostics: nt_loads=1 (default) streams chunk data with nontemporal loads
  * (env HDFS_CRC32C_NT); diag = device u64[3 * waves] receiving per-wave

@@ -31,7 +31,7 @@ comp.execute()
 h.device_sync()
 VARIANTS = [tuple(int(x) for x in v.split(",")) for v in
             os.environ.get("AB_VARIANTS", "1,1,3;2,1,3").split(";")]  # (order, nt, depth[, group shift])
-VARIANTS = [v if len(v) == 4 else v + (2,) for v in VARIANTS]
+VARIANTS = [v if len(v) == 4 else v + (3,) for v in VARIANTS]
 res = {}
 for rnd in range(4):
     for order, nt, depth, gs in VARIANTS:
@@ -83,5 +83,5 @@ for order, nt, depth, gs in list(VARIANTS)[::-1][:2]:
 h.set_tuning(1, None)
 h.set_tile_order(3)
 h.set_depth(3)
-h.set_group_shift(2)
+h.set_group_shift(3)
 print(json.dumps(out))
