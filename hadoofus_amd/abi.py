@@ -137,6 +137,7 @@ def load(path=LIB_PATH):
     _bind(lib, "hdfs_crc32c_set_tuning", _int, [_int, _vp])
     _bind(lib, "hdfs_crc32c_set_probe", _int, [_int, _int, _int])
     _bind(lib, "hdfs_crc32c_set_depth", _int, [_int])
+    _bind(lib, "hdfs_crc32c_set_shape", _int, [_int, _int])
     _bind(lib, "hdfs_crc32c_set_store_policy", _int, [_int])
     _bind(lib, "hdfs_crc32c_compute_host", _int, [_vp, _u64, _u32, _u32, _u32, _vp, _u64])
     _bind(lib, "hdfs_crc32c_verify_host", _int,
@@ -473,6 +474,11 @@ def set_group_shift(shift):
 
 def set_depth(depth):
     _check(load().hdfs_crc32c_set_depth(depth))
+
+
+def set_shape(streams, block):
+    """Tiled-kernel shape: tile streams per wave and threads per workgroup."""
+    _check(load().hdfs_crc32c_set_shape(streams, block))
 
 
 def set_store_policy(policy):

@@ -42,8 +42,12 @@ int env_int(const char *name, int dflt) {
 int g_tile_order = env_int("HDFS_CRC32C_TILE_ORDER", 3);
 // Data-stream load policy of the tiled kernel: 0 default, 1 nontemporal.
 int g_nt_loads = env_int("HDFS_CRC32C_NT", 1);
-// Rounds in flight per wave + 1 (register buffers of the tiled kernel): 3 or 4.
+// Rounds in flight per wave + 1 (register buffers of the tiled kernel): 2..4.
 int g_depth = env_int("HDFS_CRC32C_DEPTH", 3);
+// Tile streams per wave (1, 2, 4) and threads per workgroup (512, 768, 1024)
+// of the tiled kernel; non-default shapes exist for schedule 3 only.
+int g_streams = env_int("HDFS_CRC32C_STREAMS", 1);
+int g_block = env_int("HDFS_CRC32C_BLOCK", 1024);
 // Result-store policy of the tiled kernel: 0 default, 1 nontemporal,
 // 2 diagnostic only (drops the compute-mode CRC stores).
 uint32_t g_store_policy = uint32_t(env_int("HDFS_CRC32C_STORE", 0));
@@ -192,7 +196,9 @@ int launch_all(DevCtx &c, int mode, const SegDev *d_segs, uint32_t nseg, uint64_
     // pool) and tables of small segments keep the contiguous slices (2).
     const bool small = rounds < 32ull * 16u * uint64_t(grid) || mtiles < 2ull * uint64_t(grid) * nseg;
     const int order = (g_tile_order == 3 && small) ? 2 : g_tile_order;
-    HIPCHK(launch_tiles(mode, order, g_nt_loads, g_depth, grid, d_segs, nseg, rounds, mtiles,
+    // store policy 4 (diagnostic): verify plans run the load-only twin
+    const int kmode = (mode == kModeVerify && g_store_policy == 4) ? int(kModeLoadOnly) : mode;
+    HIPCHK(launch_tiles(kmode, order, g_nt_loads, g_depth, g_streams, g_block, grid, d_segs, nseg, rounds, mtiles,
                         c.d_tab_main_t[ctype], d_fb, d_mism, g_diag, g_store_policy | (g_group_shift << 8), d_gctr,
                         st));
     if (ev1) HIPCHK(hipEventRecord(ev1, st));
@@ -856,14 +862,22 @@ int hdfs_crc32c_device_sync(void) {
 }
 
 int hdfs_crc32c_set_store_policy(int policy) {
-  if (policy < 0 || policy > 3) return fail(HDFS_CRC32C_EINVAL, "store policy 0..3");
+  if (policy < 0 || policy > 4) return fail(HDFS_CRC32C_EINVAL, "store policy 0..4");
   g_store_policy = uint32_t(policy);
   return HDFS_CRC32C_OK;
 }
 
 int hdfs_crc32c_set_depth(int depth) {
-  if (depth != 3 && depth != 4) return fail(HDFS_CRC32C_EINVAL, "depth must be 3 or 4");
+  if (depth < 2 || depth > 4) return fail(HDFS_CRC32C_EINVAL, "depth must be 2..4");
   g_depth = depth;
+  return HDFS_CRC32C_OK;
+}
+
+int hdfs_crc32c_set_shape(int streams, int block) {
+  if (streams != 1 && streams != 2 && streams != 4) return fail(HDFS_CRC32C_EINVAL, "streams must be 1, 2 or 4");
+  if (block != 512 && block != 768 && block != 1024) return fail(HDFS_CRC32C_EINVAL, "block must be 512, 768 or 1024");
+  g_streams = streams;
+  g_block = block;
   return HDFS_CRC32C_OK;
 }
 

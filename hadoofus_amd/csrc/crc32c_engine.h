@@ -14,10 +14,10 @@
 namespace hdfs_crc32c {
 
 // ---- kernel launchers (crc32c_kernels.hip) ----
-hipError_t launch_tiles(int mode, int order, int nt, int depth, int grid, const SegDev *segs, uint32_t nseg,
-                        uint64_t total_rounds, uint64_t total_tiles, const uint32_t *gtab,
-                        uint32_t *first_bad, unsigned long long *mism, unsigned long long *diag,
-                        uint32_t tune, uint32_t *gctr, hipStream_t stream);
+hipError_t launch_tiles(int mode, int order, int nt, int depth, int streams, int block, int grid,
+                        const SegDev *segs, uint32_t nseg, uint64_t total_rounds, uint64_t total_tiles,
+                        const uint32_t *gtab, uint32_t *first_bad, unsigned long long *mism,
+                        unsigned long long *diag, uint32_t tune, uint32_t *gctr, hipStream_t stream);
 hipError_t launch_probe_read(const uint8_t *p, uint64_t nbytes, uint32_t *out, int grid, int block, int variant,
                              hipStream_t stream);
 hipError_t launch_generic(int mode, const SegDev *segs, uint32_t nseg, uint64_t total_gtiles,

@@ -11,7 +11,10 @@ enum : uint32_t {
   kSegRaw = 2u,        // write the raw register (init 0, no final inversion)
 };
 
-enum Mode : int { kModeCompute = 0, kModeVerify = 1 };
+// kModeLoadOnly: diagnostic twin of verify (same loads, same store ops with
+// their records dropped, no CRC arithmetic) -- the kernel's own memory
+// ceiling, for DESIGN.md; never used by the product path.
+enum Mode : int { kModeCompute = 0, kModeVerify = 1, kModeLoadOnly = 2 };
 
 // One entry of the device-resident segment table.  A segment is one chunk
 // stream with one bytesPerChecksum (src/datanode.c:2186); chunk i covers

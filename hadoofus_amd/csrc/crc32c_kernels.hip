@@ -285,7 +285,7 @@ DEV void issue(uint32_t (&d)[16], uint32_t &exp, const Cursor c, SegP segs, uint
     d[4 * k + 2] = v.z;
     d[4 * k + 3] = v.w;
   }
-  if (MODE == kModeVerify) exp = gload32(segs[c.seg].crcs + c.tile * kTileChunks + min(qg, last));
+  if (MODE != kModeCompute) exp = gload32(segs[c.seg].crcs + c.tile * kTileChunks + min(qg, last));
 }
 
 struct LaneConst {
@@ -293,25 +293,18 @@ struct LaneConst {
   uint32_t store_policy;  // 0 default, 1 nontemporal, 2 diagnostic: drop result stores
 };
 
-// Process one round held in d[] for cursor c; st is the lane's running
-// register across the rounds of a tile.
+// Finish one round of one stream after its 16 slicing steps: on a tile's
+// last round, combine the 8 lanes of each chunk and write / compare.  The
+// finalize issues no vector-memory op (LDS and swizzles only).  The result
+// store runs every round, by every lane, through a bounds-checked buffer
+// descriptor: its size is 0 unless this is a valid last round, and lanes
+// that must not write get an out-of-range offset, so the hardware drops
+// them.  Every round therefore issues exactly the same vector-memory ops
+// (4 loads, [1 expected-CRC load], 1 store) and the compiler's vmcnt waits
+// stay exact.
 template <int MODE>
-DEV void process(const uint32_t *lds, uint32_t (&d)[16], uint32_t exp, const Cursor c, SegP segs, uint32_t &st,
-                 const LaneConst &L, uint32_t *__restrict__ first_bad, unsigned long long *__restrict__ mism) {
-  transpose(d);
-  if (c.r == 0) st = (L.qi == 0) ? segs[c.seg].reg_init : 0u;
-  else st = zshift(lds, L.z448, st);
-  uint32_t x = st ^ d[0];
-#pragma unroll
-  for (int w = 0; w < 15; w++) x = slice4(lds, x, d[w + 1], L.lb0, L.lb1);
-  st = slice4(lds, x, 0u, L.lb0, L.lb1);
-  // Finalize only after a tile's last round; the finalize itself issues no
-  // vector-memory op (LDS and swizzles only).  The result store below runs
-  // every round, by every lane, through a bounds-checked buffer descriptor:
-  // its size is 0 unless this is a valid last round, and lanes that must not
-  // write get an out-of-range offset, so the hardware drops them.  Every
-  // round therefore issues exactly the same vector-memory ops (4 loads,
-  // [1 expected-CRC load], 1 store) and the compiler's vmcnt waits stay exact.
+DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, uint32_t st, const LaneConst &L,
+                uint32_t *__restrict__ first_bad, unsigned long long *__restrict__ mism) {
   const bool last = c.valid && (c.r + 1 == segs[c.seg].chunk_size / kRoundBytes);
   const uint32_t flags = segs[c.seg].flags;
   const uint32_t nch = min(kTileChunks, segs[c.seg].nchunks - c.tile * kTileChunks);
@@ -358,41 +351,95 @@ DEV void process(const uint32_t *lds, uint32_t (&d)[16], uint32_t exp, const Cur
   }
 }
 
-template <int MODE, int ORDER, int NT, int DEPTH>
-__global__ __launch_bounds__(1024) void crc32c_tiles_kernel(
+// Process one round of each of the wave's S streams (d[s] for cursor c[s]);
+// st[s] is stream s's running lane register across the rounds of a tile.
+// The S slicing chains are independent and interleaved step by step, so one
+// lane keeps S table lookups in flight (latency hiding by ILP, not waves).
+template <int MODE, int S>
+DEV void process(const uint32_t *lds, uint32_t (&d)[S][16], const uint32_t (&exp)[S], const Cursor (&c)[S],
+                 SegP segs, uint32_t (&st)[S], const LaneConst &L, uint32_t *__restrict__ first_bad,
+                 unsigned long long *__restrict__ mism) {
+  if constexpr (MODE == kModeLoadOnly) {
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+      uint32_t v = exp[s];
+#pragma unroll
+      for (int w = 0; w < 16; w++) v ^= d[s][w];
+      st[s] ^= v;
+      // the verify bitmap store with its record dropped keeps the op count
+      const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(segs[c[s].seg].bitmap + c[s].tile, 0, 0,
+                                                                          0x00020000);
+      __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(st[s]), rb, 0u, 0, 0);
+      if (st[s] == 0x9E3779B9u && c[s].r == 0xFFFFFFFFu) atomicAdd(mism, 1ull);  // keeps the loads live
+    }
+    return;
+  }
+  uint32_t x[S];
+#pragma unroll
+  for (int s = 0; s < S; s++) {
+    transpose(d[s]);
+    if (c[s].r == 0) st[s] = (L.qi == 0) ? segs[c[s].seg].reg_init : 0u;
+    else st[s] = zshift(lds, L.z448, st[s]);
+    x[s] = st[s] ^ d[s][0];
+  }
+#pragma unroll
+  for (int w = 0; w < 15; w++) {
+#pragma unroll
+    for (int s = 0; s < S; s++) x[s] = slice4(lds, x[s], d[s][w + 1], L.lb0, L.lb1);
+  }
+#pragma unroll
+  for (int s = 0; s < S; s++) st[s] = slice4(lds, x[s], 0u, L.lb0, L.lb1);
+#pragma unroll
+  for (int s = 0; s < S; s++) finish<MODE>(lds, exp[s], c[s], segs, st[s], L, first_bad, mism);
+}
+
+// Tiled kernel.  MODE compute / verify; ORDER schedule (above); NT
+// nontemporal data loads; DEPTH register round buffers per stream (DEPTH-1
+// rounds stay in flight while one is processed); S independent tile streams
+// per wave (S x 4 KiB per round, S chains of ILP); BLOCK threads per
+// workgroup (one workgroup per CU: the LDS image takes 156 KiB).
+template <int MODE, int ORDER, int NT, int DEPTH, int S, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
     const SegDev *__restrict__ segs, uint32_t nseg, uint64_t total_rounds, uint64_t total_tiles,
     const uint32_t *__restrict__ gtab, uint32_t *__restrict__ first_bad,
     unsigned long long *__restrict__ mism, unsigned long long *__restrict__ diag, uint32_t tune,
     uint32_t *__restrict__ gctr) {
+  static_assert(ORDER != 0 || S == 1, "static per-wave slices serve one stream");
+  static_assert(DEPTH >= 2 && DEPTH <= 4 && S >= 1 && S <= 4, "shape");
   // + ticket counter, pad, kSlots 64-bit pool slots
   __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords + 2 + 2 * kSlots];
 
   if (threadIdx.x < 2 + 2 * kSlots) lds[kLdsWords + threadIdx.x] = 0u;
   // LDS image: word (P*16384 + e*64 + h*32 + l) = t_{3-(2P+h)}[e] for all 32 l.
   // Filled with 16-B stores, consecutive lanes on consecutive 16 B (no bank
-  // conflicts); the 8 source words a lane needs are loaded up front so the
+  // conflicts); the source words a lane needs are loaded up front so the
   // fill costs about one L2 round trip, not one per store.
   {
-    constexpr uint32_t kQ = kLdsSliceBytes / 16 / 1024;  // 16-B stores per thread (blockDim 1024)
+    constexpr uint32_t kStores = kLdsSliceBytes / 16;
+    constexpr uint32_t kQ = (kStores + BLOCK - 1) / BLOCK;  // 16-B stores per thread
+    constexpr uint32_t kZ = (kTabZposWords / 4 + BLOCK - 1) / BLOCK;
     uint32_t v[kQ];
 #pragma unroll
     for (uint32_t k = 0; k < kQ; k++) {
-      const uint32_t idx = 4u * (k * 1024u + threadIdx.x);
+      const uint32_t idx = 4u * min(k * BLOCK + threadIdx.x, kStores - 1u);
       const uint32_t P = idx >> 14, e = (idx >> 6) & 255u, h = (idx >> 5) & 1u;
       v[k] = gtab[(3u - (2u * P + h)) * 256u + e];
     }
-    u32x4 z[2];
+    u32x4 z[kZ];
 #pragma unroll
-    for (uint32_t k = 0; k < 2; k++) {
-      const uint32_t q = k * 1024u + threadIdx.x;
+    for (uint32_t k = 0; k < kZ; k++) {
+      const uint32_t q = k * BLOCK + threadIdx.x;
       z[k] = q < kTabZposWords / 4 ? gload16(gtab + kTabSliceWords + 4u * q) : u32x4{0u, 0u, 0u, 0u};
     }
 #pragma unroll
-    for (uint32_t k = 0; k < kQ; k++)
-      *reinterpret_cast<u32x4 *>(&lds[4u * (k * 1024u + threadIdx.x)]) = u32x4{v[k], v[k], v[k], v[k]};
+    for (uint32_t k = 0; k < kQ; k++) {
+      const uint32_t q = k * BLOCK + threadIdx.x;
+      if (kStores % BLOCK == 0 || q < kStores)
+        *reinterpret_cast<u32x4 *>(&lds[4u * q]) = u32x4{v[k], v[k], v[k], v[k]};
+    }
 #pragma unroll
-    for (uint32_t k = 0; k < 2; k++) {
-      const uint32_t q = k * 1024u + threadIdx.x;
+    for (uint32_t k = 0; k < kZ; k++) {
+      const uint32_t q = k * BLOCK + threadIdx.x;
       if (q < kTabZposWords / 4) *reinterpret_cast<u32x4 *>(&lds[kLdsSliceBytes / 4 + 4u * q]) = z[k];
     }
   }
@@ -411,7 +458,7 @@ __global__ __launch_bounds__(1024) void crc32c_tiles_kernel(
   L.zbase = kLdsSliceBytes / 4 + (L.zk ? L.zk - 1u : 0u) * 1024u;
   L.z448 = kLdsSliceBytes / 4 + 6u * 1024u;
 
-  const uint32_t wpb = blockDim.x >> 6;
+  constexpr uint32_t wpb = BLOCK / 64;
   const uint32_t wave = rfl(blockIdx.x * wpb + (threadIdx.x >> 6));
   const uint32_t nwaves = gridDim.x * wpb;
   const SegP sg = (SegP)(segs);
@@ -420,8 +467,11 @@ __global__ __launch_bounds__(1024) void crc32c_tiles_kernel(
   if (diag && L.lane == 0) diag[3 * wave] = __builtin_amdgcn_s_memrealtime();
   uint64_t nrounds = 0;
   Sched w{0, 0, 0, &lds[kLdsWords], L.lane};
-  Cursor c0{0u, 0u, 0u, false};
+  Cursor cur[DEPTH][S];
+#pragma unroll
+  for (int s = 0; s < S; s++) cur[0][s] = Cursor{0u, 0u, 0u, false};
   if (ORDER == 0) {
+    Cursor &c0 = cur[0][0];
     const uint64_t r0 = rfl64(total_rounds * wave / nwaves);
     w.r1 = rfl64(total_rounds * (wave + 1) / nwaves);
     if (r0 < w.r1) {
@@ -437,7 +487,7 @@ __global__ __launch_bounds__(1024) void crc32c_tiles_kernel(
       }
     }
   } else {
-    const bool pool = ORDER >= 2 && total_rounds >= 32ull * nwaves;
+    const bool pool = ORDER >= 2 && total_rounds >= 32ull * nwaves * S;
     if (ORDER == 3) {
       // static phase: whole groups only; the pool takes the rest
       w.gshift = (tune >> 8) & 15u;
@@ -464,89 +514,81 @@ __global__ __launch_bounds__(1024) void crc32c_tiles_kernel(
     }
     w.gctr = gctr;
     w.slots = reinterpret_cast<uint64_t *>(&lds[kLdsWords + 2]);
-    uint64_t g;
-    if (ticket_tile<ORDER>(w, grab(w), g)) {
-      uint32_t lo = 0, hi = nseg;
-      while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (sg[mid].mtile_start <= g) lo = mid; else hi = mid;
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+      uint64_t g;
+      if (ticket_tile<ORDER>(w, grab(w), g)) {
+        uint32_t lo = 0, hi = nseg;
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (sg[mid].mtile_start <= g) lo = mid; else hi = mid;
+        }
+        cur[0][s] = locate(sg, lo, g);
       }
-      c0 = locate(sg, lo, g);
     }
   }
-  if (!c0.valid) {
+  bool any = false;
+#pragma unroll
+  for (int s = 0; s < S; s++) any |= cur[0][s].valid;
+  if (!any) {
     if (diag && L.lane == 0) diag[3 * wave + 1] = __builtin_amdgcn_s_memrealtime();
     return;
   }
+  // A stream that got no tile parks on stream 0's position (valid = false):
+  // its loads stay in bounds and its stores are dropped.
+#pragma unroll
+  for (int s = 1; s < S; s++)
+    if (!cur[0][s].valid) cur[0][s] = Cursor{cur[0][0].seg, cur[0][0].tile, cur[0][0].r, false};
 
-  // DEPTH round buffers in rotation: while one round is processed the next
-  // DEPTH-1 are in flight (DEPTH 4: 16 KiB per wave, 256 KiB per CU).
-  // One exit test per iteration (after all issues) and no memory op under a
-  // condition: every path issues the same vector-memory ops in the same
-  // order, so the vmcnt bookkeeping stays exact.  c0 is always valid at the
-  // top of an iteration; rounds of an exhausted cursor are processed with
-  // their stores dropped.
-  uint32_t st = 0;
-  if constexpr (DEPTH == 3) {
-    uint32_t A[16], B[16], C[16];
-    uint32_t eA = 0, eB = 0, eC = 0;
-    Cursor c1 = advance<ORDER>(c0, sg, nseg, w);
-    Cursor c2 = advance<ORDER>(c1, sg, nseg, w);
-    issue<MODE, NT>(A, eA, c0, sg, L.hsel, L.loff, L.qg);
-    issue<MODE, NT>(B, eB, c1, sg, L.hsel, L.loff, L.qg);
-    issue<MODE, NT>(C, eC, c2, sg, L.hsel, L.loff, L.qg);
-    for (;;) {
-      process<MODE>(lds, A, eA, c0, sg, st, L, first_bad, mism);
-      const Cursor c3 = advance<ORDER>(c2, sg, nseg, w);
-      issue<MODE, NT>(A, eA, c3, sg, L.hsel, L.loff, L.qg);
-      process<MODE>(lds, B, eB, c1, sg, st, L, first_bad, mism);  // no-op store if c1 is exhausted
-      const Cursor c4 = advance<ORDER>(c3, sg, nseg, w);
-      issue<MODE, NT>(B, eB, c4, sg, L.hsel, L.loff, L.qg);
-      process<MODE>(lds, C, eC, c2, sg, st, L, first_bad, mism);
-      const Cursor c5 = advance<ORDER>(c4, sg, nseg, w);
-      issue<MODE, NT>(C, eC, c5, sg, L.hsel, L.loff, L.qg);
-      nrounds += 1u + (c1.valid ? 1u : 0u) + (c2.valid ? 1u : 0u);
-      if (!c3.valid) break;
-      c0 = c3;
-      c1 = c4;
-      c2 = c5;
+  // DEPTH round buffers per stream in rotation: slot k is processed, then
+  // refilled with the round after the newest cursor (slot k-1).  Fully
+  // unrolled, so every buffer stays in fixed registers.  One exit test per
+  // iteration (after all issues) and no memory op under a condition: every
+  // path issues the same vector-memory ops in the same order, so the vmcnt
+  // bookkeeping stays exact.  Rounds of an exhausted cursor are processed
+  // with their stores dropped.
+  uint32_t buf[DEPTH][S][16];
+  uint32_t ex[DEPTH][S];
+  uint32_t st[S];
+#pragma unroll
+  for (int s = 0; s < S; s++) st[s] = 0u;
+#pragma unroll
+  for (int k = 1; k < DEPTH; k++) {
+#pragma unroll
+    for (int s = 0; s < S; s++) cur[k][s] = advance<ORDER>(cur[k - 1][s], sg, nseg, w);
+  }
+#pragma unroll
+  for (int k = 0; k < DEPTH; k++) {
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+      ex[k][s] = 0u;
+      issue<MODE, NT>(buf[k][s], ex[k][s], cur[k][s], sg, L.hsel, L.loff, L.qg);
     }
-  } else {
-    uint32_t A[16], B[16], C[16], D[16];
-    uint32_t eA = 0, eB = 0, eC = 0, eD = 0;
-    Cursor c1 = advance<ORDER>(c0, sg, nseg, w);
-    Cursor c2 = advance<ORDER>(c1, sg, nseg, w);
-    Cursor c3 = advance<ORDER>(c2, sg, nseg, w);
-    issue<MODE, NT>(A, eA, c0, sg, L.hsel, L.loff, L.qg);
-    issue<MODE, NT>(B, eB, c1, sg, L.hsel, L.loff, L.qg);
-    issue<MODE, NT>(C, eC, c2, sg, L.hsel, L.loff, L.qg);
-    issue<MODE, NT>(D, eD, c3, sg, L.hsel, L.loff, L.qg);
-    for (;;) {
-      process<MODE>(lds, A, eA, c0, sg, st, L, first_bad, mism);
-      const Cursor c4 = advance<ORDER>(c3, sg, nseg, w);
-      issue<MODE, NT>(A, eA, c4, sg, L.hsel, L.loff, L.qg);
-      process<MODE>(lds, B, eB, c1, sg, st, L, first_bad, mism);
-      const Cursor c5 = advance<ORDER>(c4, sg, nseg, w);
-      issue<MODE, NT>(B, eB, c5, sg, L.hsel, L.loff, L.qg);
-      process<MODE>(lds, C, eC, c2, sg, st, L, first_bad, mism);
-      const Cursor c6 = advance<ORDER>(c5, sg, nseg, w);
-      issue<MODE, NT>(C, eC, c6, sg, L.hsel, L.loff, L.qg);
-      process<MODE>(lds, D, eD, c3, sg, st, L, first_bad, mism);
-      const Cursor c7 = advance<ORDER>(c6, sg, nseg, w);
-      issue<MODE, NT>(D, eD, c7, sg, L.hsel, L.loff, L.qg);
-      nrounds += 1u + (c1.valid ? 1u : 0u) + (c2.valid ? 1u : 0u) + (c3.valid ? 1u : 0u);
-      if (!c4.valid) break;
-      c0 = c4;
-      c1 = c5;
-      c2 = c6;
-      c3 = c7;
+  }
+  for (;;) {
+#pragma unroll
+    for (int k = 0; k < DEPTH; k++) {
+      process<MODE, S>(lds, buf[k], ex[k], cur[k], sg, st, L, first_bad, mism);
+#pragma unroll
+      for (int s = 0; s < S; s++) nrounds += cur[k][s].valid ? 1u : 0u;
+      const int prev = (k + DEPTH - 1) % DEPTH;
+#pragma unroll
+      for (int s = 0; s < S; s++) {
+        cur[k][s] = advance<ORDER>(cur[prev][s], sg, nseg, w);
+        issue<MODE, NT>(buf[k][s], ex[k][s], cur[k][s], sg, L.hsel, L.loff, L.qg);
+      }
     }
+    bool more = false;
+#pragma unroll
+    for (int s = 0; s < S; s++) more |= cur[0][s].valid;
+    if (!more) break;
   }
   if (diag && L.lane == 0) {
     diag[3 * wave + 1] = __builtin_amdgcn_s_memrealtime();
     diag[3 * wave + 2] = nrounds;
   }
 }
+
 
 // Generic path: one lane per chunk, 8 lanes per tile.  Serves chunks the
 // tiled kernel cannot: partial last chunks, chunk sizes that are not a
@@ -813,26 +855,38 @@ hipError_t launch_gather(const uint8_t *raw, const PktDesc *descs, uint32_t npk,
   return hipGetLastError();
 }
 
-hipError_t launch_tiles(int mode, int order, int nt, int depth, int grid, const SegDev *segs, uint32_t nseg,
-                        uint64_t total_rounds, uint64_t total_tiles, const uint32_t *gtab,
-                        uint32_t *first_bad, unsigned long long *mism, unsigned long long *diag,
-                        uint32_t tune, uint32_t *gctr, hipStream_t stream) {
-#define HDFS_LAUNCH(M, O, N, D)                                                                        \
-  hipLaunchKernelGGL((crc32c_tiles_kernel<M, O, N, D>), dim3(grid), dim3(1024), 0, stream, segs, nseg,  \
+hipError_t launch_tiles(int mode, int order, int nt, int depth, int streams, int block, int grid,
+                        const SegDev *segs, uint32_t nseg, uint64_t total_rounds, uint64_t total_tiles,
+                        const uint32_t *gtab, uint32_t *first_bad, unsigned long long *mism,
+                        unsigned long long *diag, uint32_t tune, uint32_t *gctr, hipStream_t stream) {
+#define HDFS_LAUNCH(M, O, N, D, S, B)                                                                     \
+  hipLaunchKernelGGL((crc32c_tiles_kernel<M, O, N, D, S, B>), dim3(grid), dim3(B), 0, stream, segs, nseg, \
                      total_rounds, total_tiles, gtab, first_bad, mism, diag, tune, gctr)
-#define HDFS_LAUNCH_M(M)                                                   \
-  do {                                                                     \
-    if (order == 3 && depth == 4) HDFS_LAUNCH(M, 3, 1, 4);                 \
-    else if (order == 3) HDFS_LAUNCH(M, 3, 1, 3);                          \
-    else if (order == 2 && depth == 4) HDFS_LAUNCH(M, 2, 1, 4);            \
-    else if (order == 2) HDFS_LAUNCH(M, 2, 1, 3);                          \
-    else if (depth == 4) HDFS_LAUNCH(M, 1, 1, 4);                          \
-    else if (order && nt) HDFS_LAUNCH(M, 1, 1, 3);                         \
-    else if (order) HDFS_LAUNCH(M, 1, 0, 3);                               \
-    else if (nt) HDFS_LAUNCH(M, 0, 1, 3);                                  \
-    else HDFS_LAUNCH(M, 0, 0, 3);                                          \
+  // Shapes other than (depth 3, 1 stream, 1024 threads) exist for schedule 3
+  // only (tuning experiments, tools/exp_ab.py); anything else falls back to
+  // the default shape of the requested schedule.
+#define HDFS_LAUNCH_M(M)                                                                \
+  do {                                                                                  \
+    if (order == 3 && depth == 2 && streams == 2 && block == 1024) HDFS_LAUNCH(M, 3, 1, 2, 2, 1024); \
+    else if (order == 3 && depth == 3 && streams == 2 && block == 1024) HDFS_LAUNCH(M, 3, 1, 3, 2, 1024); \
+    else if (order == 3 && depth == 3 && streams == 2 && block == 768) HDFS_LAUNCH(M, 3, 1, 3, 2, 768); \
+    else if (order == 3 && depth == 2 && streams == 2 && block == 512) HDFS_LAUNCH(M, 3, 1, 2, 2, 512); \
+    else if (order == 3 && depth == 3 && streams == 2 && block == 512) HDFS_LAUNCH(M, 3, 1, 3, 2, 512); \
+    else if (order == 3 && depth == 2 && streams == 4 && block == 512) HDFS_LAUNCH(M, 3, 1, 2, 4, 512); \
+    else if (order == 3 && depth == 3 && streams == 1 && block == 768) HDFS_LAUNCH(M, 3, 1, 3, 1, 768); \
+    else if (order == 3 && depth == 3 && streams == 1 && block == 512) HDFS_LAUNCH(M, 3, 1, 3, 1, 512); \
+    else if (order == 3 && depth == 4) HDFS_LAUNCH(M, 3, 1, 4, 1, 1024);                \
+    else if (order == 3) HDFS_LAUNCH(M, 3, 1, 3, 1, 1024);                              \
+    else if (order == 2 && depth == 4) HDFS_LAUNCH(M, 2, 1, 4, 1, 1024);                \
+    else if (order == 2) HDFS_LAUNCH(M, 2, 1, 3, 1, 1024);                              \
+    else if (depth == 4) HDFS_LAUNCH(M, 1, 1, 4, 1, 1024);                              \
+    else if (order && nt) HDFS_LAUNCH(M, 1, 1, 3, 1, 1024);                             \
+    else if (order) HDFS_LAUNCH(M, 1, 0, 3, 1, 1024);                                   \
+    else if (nt) HDFS_LAUNCH(M, 0, 1, 3, 1, 1024);                                      \
+    else HDFS_LAUNCH(M, 0, 0, 3, 1, 1024);                                              \
   } while (0)
-  if (mode == kModeVerify) HDFS_LAUNCH_M(kModeVerify);
+  if (mode == kModeLoadOnly) HDFS_LAUNCH(kModeLoadOnly, 3, 1, 3, 1, 1024);
+  else if (mode == kModeVerify) HDFS_LAUNCH_M(kModeVerify);
   else HDFS_LAUNCH_M(kModeCompute);
 #undef HDFS_LAUNCH_M
 #undef HDFS_LAUNCH

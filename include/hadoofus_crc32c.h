@@ -270,11 +270,19 @@ int hdfs_crc32c_set_group_shift(int shift);
  * (env HDFS_CRC32C_NT); diag = device u64[3 * waves] receiving per-wave
  * start/end s_memrealtime stamps and rounds processed (NULL = off). */
 int hdfs_crc32c_set_tuning(int nt_loads, void *diag);
-/* Register round buffers per wave of the tiled kernel (3 or 4; depth-1
+/* Register round buffers per tile stream of the tiled kernel (2..4; depth-1
  * rounds stay in flight while one is processed).  Env HDFS_CRC32C_DEPTH. */
 int hdfs_crc32c_set_depth(int depth);
+/* Tiled-kernel shape: independent tile streams per wave (1, 2, 4) and
+ * threads per workgroup (512, 768, 1024).  Shapes other than (1, 1024) are
+ * built for schedule 3 only; other combinations run the default shape.
+ * Env HDFS_CRC32C_STREAMS / HDFS_CRC32C_BLOCK. */
+int hdfs_crc32c_set_shape(int streams, int block);
 /* Compute-mode result store policy: 0 default, 1 nontemporal, 2 diagnostic
- * (stores dropped; output undefined -- timing experiments only).
+ * (stores dropped; output undefined -- timing experiments only), 4
+ * diagnostic: verify plans run a load-only twin of the kernel (same loads and
+ * store ops, no CRC arithmetic, results undefined) -- the memory ceiling of
+ * the kernel's access pattern.
  * Env HDFS_CRC32C_STORE. */
 int hdfs_crc32c_set_store_policy(int policy);
 /* Empirical streaming-read bandwidth of `bytes` at dptr (GB/s, 1e9 B/s):

@@ -1,0 +1,70 @@
+"""Every tiled-kernel schedule and shape (tools/exp_ab.py's A/B variants)
+against the oracle on a C5-like table (mixed bytesPerChecksum 512..4096, so
+tiles span 1..8 rounds) large enough that schedule 3 and its global pool are
+engaged (>= 32 rounds per wave per stream).  Compute output bit-exact vs the
+oracle; verify finds exactly the corrupted chunks (bitmaps, first bad)."""
+import numpy as np
+import pytest
+
+from oracle import splitmix64_np
+
+pytestmark = pytest.mark.gpu
+
+SEG = 16 << 20
+NSEG = 64  # 1 GiB: >= 32 rounds per wave per stream at every shape, so schedule 3 + pool run
+# (order, depth, streams, block): the built shapes (crc32c_kernels.hip launch_tiles)
+SHAPES = [(3, 3, 1, 1024), (3, 4, 1, 1024), (3, 2, 2, 1024), (3, 3, 2, 1024), (3, 3, 2, 768),
+          (3, 2, 2, 512), (3, 3, 2, 512), (3, 2, 4, 512), (3, 3, 1, 768), (3, 3, 1, 512),
+          (2, 3, 1, 1024), (1, 3, 1, 1024), (0, 3, 1, 1024)]
+
+
+@pytest.fixture(scope="module")
+def table(engine, oracle):
+    host = splitmix64_np(NSEG * SEG // 8, seed=5).view(np.uint8).copy()
+    sizes = [512 << (i % 4) for i in range(NSEG)]
+    want = [oracle.chunk_crcs(host[i * SEG:(i + 1) * SEG], cs) for i, cs in enumerate(sizes)]
+    dbuf = engine.DeviceBuffer(host.nbytes)
+    dbuf.upload(host)
+    return host, sizes, want, dbuf
+
+
+def _set(engine, order, depth, streams, block):
+    engine.set_tile_order(order)
+    engine.set_depth(depth)
+    engine.set_shape(streams, block)
+
+
+@pytest.mark.parametrize("order,depth,streams,block", SHAPES)
+def test_shape_compute_verify(engine, table, order, depth, streams, block):
+    host, sizes, want, dbuf = table
+    nch = [SEG // cs for cs in sizes]
+    crcs = [engine.DeviceBuffer(n * 4) for n in nch]
+    bms = [engine.DeviceBuffer(n // 8) for n in nch]
+    segs = [engine.Segment(data=dbuf.ptr + i * SEG, len=SEG, chunk_size=cs, flags=engine.SEG_BE, crc_init=0,
+                           crcs=crcs[i].ptr, bitmap=bms[i].ptr) for i, cs in enumerate(sizes)]
+    try:
+        _set(engine, order, depth, streams, block)
+        engine.Plan(engine.MODE_COMPUTE, segs).execute()
+        for i, n in enumerate(nch):
+            np.testing.assert_array_equal(crcs[i].download(n * 4, dtype=">u4").astype(np.uint32), want[i],
+                                          err_msg=f"segment {i}")
+        # corrupt chunk k*997 + i of every third segment by flipping its expected CRC
+        bad = {}
+        for i, n in enumerate(nch):
+            if i % 3 == 0:
+                picks = sorted({(k * 997 + i) % n for k in range(5)})
+                bad[i] = picks
+                arr = want[i].astype(">u4")
+                for c in picks:
+                    arr[c] ^= np.uint32(1 << (c % 32))
+                crcs[i].upload(arr.view(np.uint8))
+        vp = engine.Plan(engine.MODE_VERIFY, segs)
+        vp.execute()
+        first_bad, mism = vp.results()
+        assert mism == sum(len(v) for v in bad.values())
+        for i, n in enumerate(nch):
+            bits = np.unpackbits(bms[i].download(n // 8), bitorder="little")
+            assert list(np.nonzero(bits)[0]) == bad.get(i, []), i
+            assert first_bad[i] == (bad[i][0] if i in bad else 0xFFFFFFFF)
+    finally:
+        _set(engine, 3, 3, 1, 1024)
