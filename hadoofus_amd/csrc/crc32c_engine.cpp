@@ -12,6 +12,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
+#include <chrono>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -115,6 +116,11 @@ int ctx_init(int device, DevCtx **out) {
   HIPCHK(hipMalloc(&c.d_stage, kStageCap));
   HIPCHK(hipMalloc(&c.d_seg, sizeof(SegDev)));
   HIPCHK(hipMalloc(&c.d_small, 64));  // [0] acc [1] first_bad [2..3] mism [8] pool counter
+  HIPCHK(hipHostMalloc(&c.h_small_in, kSmallIn, hipHostMallocCoherent | hipHostMallocMapped));
+  HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&c.h_small_out), kSmallOut, hipHostMallocCoherent | hipHostMallocMapped));
+  std::memset(c.h_small_out, 0, kSmallOut);
+  HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&c.dv_small_in), c.h_small_in, 0));
+  HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&c.dv_small_out), c.h_small_out, 0));
   c.ready = true;
   *out = &c;
   return HDFS_CRC32C_OK;
@@ -242,6 +248,48 @@ int stream_crc_locked(DevCtx &c, uint32_t crc, const void *dbuf, uint64_t len, u
   return HDFS_CRC32C_OK;
 }
 
+// Small synchronous call (small_chunks_kernel): the caller has written the
+// data to h_small_in[0, len) (and for verify the wire CRCs to
+// h_small_in[kSmallMax, +4*nch)).  One launch; the host polls the completion
+// sequence number the kernel stores to pinned memory after its results
+// (a fault is caught by the stream synchronisation the poll falls back to).
+bool small_ok(uint64_t len, uint64_t cs) {
+  if (!len || len > kSmallMax || !cs) return false;
+  const uint64_t nch = (len + cs - 1) / cs;
+  return nch <= kSmallMaxChunks && (cs % 4 == 0 || nch == 1);
+}
+
+static const bool g_small_trace = std::getenv("HDFS_CRC32C_SMALL_TRACE") != nullptr;
+
+int small_call(DevCtx &c, int mode, uint32_t len, uint32_t cs, uint32_t reg0, bool be, int ctype,
+               const uint8_t *dsrc = nullptr) {
+  const uint32_t seq = ++c.small_seq;
+  const auto tl = std::chrono::steady_clock::now();
+  HIPCHK(launch_small_chunks(mode, dsrc ? dsrc : c.dv_small_in, len, dsrc ? 1u : 0u, cs, reg0, be ? 1u : 0u,
+                             reinterpret_cast<const uint32_t *>(c.dv_small_in + kSmallMax), c.d_tab_main_t[ctype],
+                             c.d_tab_pow2_t[ctype], c.dv_small_out, c.dv_small_out + kSmallMeta, seq, c.stream));
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t spin = 1;; spin++) {
+    if (__atomic_load_n(&c.h_small_out[2], __ATOMIC_ACQUIRE) == seq) {
+      if (g_small_trace) {  // diagnostic: host launch / wait time, kernel phase stamps (10 ns ticks)
+        const auto t1 = std::chrono::steady_clock::now();
+        const uint32_t *m = c.h_small_out;
+        std::fprintf(stderr, "small len=%u cs=%u launch_us=%.2f wait_us=%.2f load_us=%.2f comp_us=%.2f out_us=%.2f\n",
+                     len, cs, std::chrono::duration<double, std::micro>(t0 - tl).count(),
+                     std::chrono::duration<double, std::micro>(t1 - t0).count(), (m[5] - m[4]) / 100.0,
+                     (m[6] - m[5]) / 100.0, (m[7] - m[6]) / 100.0);
+      }
+      return HDFS_CRC32C_OK;
+    }
+    if ((spin & 4095u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200)) {
+      HIPCHK(hipStreamSynchronize(c.stream));
+      if (__atomic_load_n(&c.h_small_out[2], __ATOMIC_ACQUIRE) == seq) return HDFS_CRC32C_OK;
+      return fail(HDFS_CRC32C_EHIP, "small kernel finished without publishing its result");
+    }
+    __builtin_ia32_pause();
+  }
+}
+
 int stream_crc_any(uint32_t crc, const void *buf, uint64_t len, uint32_t *out, int ctype = 0) {
   DevCtx *c = nullptr;
   int rc = ctx_init(-1, &c);
@@ -252,7 +300,24 @@ int stream_crc_any(uint32_t crc, const void *buf, uint64_t len, uint32_t *out, i
     *out = crc;
     return HDFS_CRC32C_OK;
   }
-  if (device_accessible(buf)) return stream_crc_locked(*c, crc, buf, len, out, ctype);
+  if (device_accessible(buf)) {
+    if (small_ok(len, len) && (reinterpret_cast<uintptr_t>(buf) & 15u) == 0) {
+      rc = small_call(*c, kModeCompute, uint32_t(len), uint32_t(len), ~crc, false, ctype,
+                      static_cast<const uint8_t *>(buf));
+      if (rc) return rc;
+      *out = c->h_small_out[kSmallMeta];
+      return HDFS_CRC32C_OK;
+    }
+    return stream_crc_locked(*c, crc, buf, len, out, ctype);
+  }
+  if (small_ok(len, len)) {
+    // one chunk of len bytes continuing from the caller's register
+    std::memcpy(c->h_small_in, buf, size_t(len));
+    rc = small_call(*c, kModeCompute, uint32_t(len), uint32_t(len), ~crc, false, ctype);
+    if (rc) return rc;
+    *out = c->h_small_out[kSmallMeta];
+    return HDFS_CRC32C_OK;
+  }
   const uint8_t *p = static_cast<const uint8_t *>(buf);
   while (len) {
     const size_t n = len < kStageCap ? size_t(len) : kStageCap;
@@ -694,6 +759,19 @@ int hdfs_crc32c_verify_crcdata(const void *crcdata, int32_t chunksize, int32_t c
   if (rc) return rc;
   DeviceGuard g(c->dev);
   std::lock_guard<std::mutex> lk(c->mu);
+  const uint8_t *reg = static_cast<const uint8_t *>(crcdata);
+  if (small_ok(uint64_t(dlen), uint64_t(chunksize))) {
+    std::memcpy(c->h_small_in, reg + crcdlen, size_t(dlen));
+    std::memcpy(c->h_small_in + kSmallMax, reg, size_t(crcdlen));
+    rc = small_call(*c, kModeVerify, uint32_t(dlen), uint32_t(chunksize), 0xFFFFFFFFu, true, seg_ctype(pflag));
+    if (rc) return rc;
+    const uint32_t fb = c->h_small_out[0];
+    if (fb != 0xFFFFFFFFu) {
+      if (first_bad) *first_bad = int32_t(fb);
+      return fail(HDFS_CRC32C_ERR_DATANODE_BAD_CHECKSUM, "chunk %u: bad checksum", fb);
+    }
+    return HDFS_CRC32C_OK;
+  }
   const size_t off_crc = (size_t(dlen) + 255) & ~size_t(255);
   const size_t off_bm = off_crc + ((size_t(crcdlen) + 255) & ~size_t(255));
   const size_t bm_len = size_t((nch + 7) / 8);
@@ -742,14 +820,22 @@ int hdfs_crc32c_compose_crcs(const void *const *iov_base, const size_t *iov_len,
   if (off_crc + nch * 4 > kStageCap) return fail(HDFS_CRC32C_EINVAL, "packet larger than staging");
   DeviceGuard g(c->dev);
   std::lock_guard<std::mutex> lk(c->mu);
+  const bool small = small_ok(total, chunk);
+  uint8_t *dst = small ? c->h_small_in : c->h_stage;
   size_t have = 0;
   for (int k = 0; k < iovcnt && have < total; k++) {
     const size_t n = iov_len[k] < total - have ? iov_len[k] : total - have;
     if (n && !iov_base[k]) return fail(HDFS_CRC32C_EINVAL, "null iovec %d", k);
-    std::memcpy(c->h_stage + have, iov_base[k], n);
+    std::memcpy(dst + have, iov_base[k], n);
     have += n;
   }
   if (have != total) return fail(HDFS_CRC32C_EINVAL, "iovecs hold %zu of %zu bytes", have, total);
+  if (small) {
+    rc = small_call(*c, kModeCompute, uint32_t(total), chunk, 0xFFFFFFFFu, true, seg_ctype(pflag));
+    if (rc) return rc;
+    std::memcpy(crc_be_out, c->h_small_out + kSmallMeta, nch * 4);
+    return HDFS_CRC32C_OK;
+  }
   HIPCHK(hipMemcpyAsync(c->d_stage, c->h_stage, total, hipMemcpyHostToDevice, c->stream));
   hdfs_crc32c_segment in = {c->d_stage, total, chunk, HDFS_CRC32C_SEG_BE | pflag, 0, 0, c->d_stage + off_crc,
                             nullptr};

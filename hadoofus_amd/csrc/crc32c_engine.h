@@ -30,6 +30,9 @@ hipError_t launch_corrupt(uint8_t *data, uint64_t len, uint32_t cs, uint64_t chu
                           uint64_t bitmul, hipStream_t stream);
 hipError_t launch_composite(const SegDev *segs, uint32_t nseg, const uint64_t *run_prefix, uint64_t total_runs,
                             const uint32_t *pow2, uint32_t *out, hipStream_t stream);
+hipError_t launch_small_chunks(int mode, const uint8_t *p, uint32_t len, uint32_t exact, uint32_t cs, uint32_t reg0,
+                               uint32_t be, const uint32_t *expect, const uint32_t *tab, const uint32_t *pow2,
+                               uint32_t *meta, uint32_t *crcs, uint32_t seq, hipStream_t stream);
 hipError_t launch_prep(uint32_t *fb, uint32_t nfb, unsigned long long *mism, uint32_t *gctr, hipStream_t stream);
 hipError_t launch_gather(const uint8_t *raw, const PktDesc *descs, uint32_t npk, uint32_t units, uint8_t *arena,
                          uint8_t *crc_arena, hipStream_t stream);
@@ -50,6 +53,11 @@ int fail(int code, const char *fmt, ...);
 constexpr int kMaxDev = 64;
 constexpr uint32_t kStreamPiece = 4096;          // stream CRC: raw CRC per 4 KiB piece
 constexpr size_t kStageCap = size_t(64) << 20;   // host->device staging for one-shots
+// small synchronous calls: input = data [0, kSmallMax) + wire CRCs; output =
+// kSmallMeta meta words + CRCs
+constexpr size_t kSmallIn = kSmallMax + size_t(kSmallMaxChunks) * 4 + 64;
+constexpr uint32_t kSmallMeta = 16;
+constexpr size_t kSmallOut = (kSmallMeta + size_t(kSmallMaxChunks)) * 4;
 
 // Device buffers of one in-flight packet piece (packet-stream verifier):
 // wire bytes, de-framed data / CRC arenas, and the piece's tables
@@ -79,6 +87,12 @@ struct DevCtx {
   size_t raw_cap = 0;
   SegDev *d_seg = nullptr;
   uint32_t *d_small = nullptr;  // [0] acc, [1] first_bad, [2..3] mismatches
+  // small synchronous calls: fine-grained pinned input stage (data, then
+  // expected CRCs) and output block (meta words, then CRCs), read / written
+  // by small_chunks_kernel directly (no DMA copies); seq = completion number
+  uint8_t *h_small_in = nullptr, *dv_small_in = nullptr;
+  uint32_t *h_small_out = nullptr, *dv_small_out = nullptr;
+  uint32_t small_seq = 0;
   // host pipeline (guarded by mu): two staging slots on two streams
   hipStream_t copy_stream = nullptr, comp_stream = nullptr;
   hipEvent_t ev_copy[2] = {nullptr, nullptr}, ev_comp[2] = {nullptr, nullptr};

@@ -71,6 +71,11 @@ struct PktDesc {
 };
 constexpr uint32_t kGatherSlice = 65536;  // data bytes per gather workgroup
 
+// Synchronous host-memory calls up to this size (and chunk count) run as one
+// small kernel reading pinned host memory (small_chunks_kernel).
+constexpr uint32_t kSmallMax = 65536;
+constexpr uint32_t kSmallMaxChunks = 2048;
+
 constexpr uint32_t kRoundBytes = 512;  // sub-chunk handled by 8 lanes per round
 constexpr uint32_t kTileChunks = 8;
 

@@ -694,6 +694,154 @@ __global__ __launch_bounds__(256) void crc32c_combine_kernel(
   if ((threadIdx.x & 63u) == 0 && v) atomicXor(acc, v);
 }
 
+// One-launch kernel for the synchronous host-memory calls on <= kSmallMax
+// bytes: the drop-in _hdfs_crc32c family (src/crc32c.h:13-24, one chunk of
+// `len` bytes continuing from the caller's register), the write loop mirror
+// (src/datanode.c:2814-2860, compute) and _verify_crcdata
+// (src/datanode.c:2931-2963, verify).  The caller's bytes are staged in
+// fine-grained pinned host memory and read by the kernel over PCIe
+// (coalesced 1 KiB per wave instruction, no DMA copy, no second launch);
+// results and a completion sequence number go straight back to pinned host
+// memory, which the host polls.
+//
+// Each chunk is split in 64-B pieces, one per thread: piece k of chunk j
+// yields the raw register r (the chunk's first piece starts from `reg0`),
+// shifted past the rest of its chunk with the power-of-two zeros operators
+// (the combine algebra of src/crc32c_sse42.c:99-200) and XOR-ed into the
+// chunk's accumulator in LDS.  Needs chunk_size % 4 == 0 and at most
+// kSmallMaxChunks chunks.
+// meta: [0] first bad chunk (verify, 0xFFFFFFFF none) [1] mismatches
+//       [2] completion sequence number; crcs: compute output (u32, BE if be)
+template <int MODE>
+__global__ __launch_bounds__(1024) void small_chunks_kernel(const uint8_t *__restrict__ p, uint32_t len,
+                                                             uint32_t exact, uint32_t cs, uint32_t reg0, uint32_t be,
+                                                             const uint32_t *__restrict__ expect,
+                                                             const uint32_t *__restrict__ tab,
+                                                             const uint32_t *__restrict__ pow2,
+                                                             uint32_t *__restrict__ meta,
+                                                             uint32_t *__restrict__ crcs, uint32_t seq) {
+  __shared__ uint32_t tt[1024];                                    // t0..t3
+  __shared__ __attribute__((aligned(16))) uint32_t zt[16 * 1024];  // Z_{2^b}, b < 16
+  __shared__ uint32_t dat[kSmallMax / 4 + kSmallMax / 64];         // one pad word per 16
+  __shared__ uint32_t acc[kSmallMaxChunks];
+  __shared__ uint32_t res[2];
+  const uint32_t tid = threadIdx.x;
+  // piece size: 16, 32 or 64 B, the smallest that keeps the pieces within
+  // one pass of the block (short chains for short inputs)
+  const uint32_t nch = (len + cs - 1) / cs;
+  uint32_t psz = 16u;
+  while (psz < 64u && nch * ((cs + psz - 1) / psz) > 1024u) psz *= 2u;
+  const uint32_t ppc = (cs + psz - 1) / psz;
+  // Every global / host load of the prologue is issued before any LDS
+  // store (one PCIe round trip for the data, one HBM/L2 trip for tables).
+  // Only the operator levels a shift (< len) can use are loaded.
+  static_assert(kSmallMax / 16 == 4 * 1024 && kSmallMaxChunks == 2 * 1024, "prologue shape");
+  const uint64_t ts0 = __builtin_amdgcn_s_memrealtime();  // phase stamps (100 MHz) -> meta[4..11]
+  const uint32_t nlev = len > 1u ? 32u - __builtin_clz(len - 1u) : 1u;
+  const uint32_t nvec = (len + 15u) / 16u;
+  const uint32_t tv = tab[tid];
+  u32x4 zv[4], dv[4];
+  uint32_t ev[2] = {0u, 0u};
+#pragma unroll
+  for (uint32_t k = 0; k < 4; k++) {
+    const uint32_t q = k * 1024u + tid;
+    zv[k] = q < nlev * 256u ? gload16(pow2 + 4u * q) : u32x4{0u, 0u, 0u, 0u};
+    dv[k] = u32x4{0u, 0u, 0u, 0u};
+    if (q < nvec) {
+      if (exact && 16u * q + 16u > len) {  // device source: never read past len
+        uint32_t wds[4] = {0u, 0u, 0u, 0u};
+        for (uint32_t b = 16u * q; b < len; b++) wds[(b >> 2) & 3u] |= uint32_t(gload8(p + b)) << (8u * (b & 3u));
+        dv[k] = u32x4{wds[0], wds[1], wds[2], wds[3]};
+      } else {
+        dv[k] = gload16(p + 16ull * q);
+      }
+    }
+  }
+  if (MODE == kModeVerify) {
+#pragma unroll
+    for (uint32_t k = 0; k < 2; k++)
+      if (k * 1024u + tid < nch) ev[k] = gload32(expect + k * 1024u + tid);
+  }
+  tt[tid] = tv;
+  for (uint32_t j = tid; j < nch; j += 1024u) acc[j] = 0u;
+  if (tid < 2) res[tid] = tid == 0 ? 0xFFFFFFFFu : 0u;
+#pragma unroll
+  for (uint32_t k = 0; k < 4; k++) {
+    const uint32_t q = k * 1024u + tid;
+    if (q < nlev * 256u) *reinterpret_cast<u32x4 *>(&zt[4u * q]) = zv[k];
+    if (q < nvec) {
+      const uint32_t w = 4u * q + (q >> 2);
+      dat[w] = dv[k].x;
+      dat[w + 1] = dv[k].y;
+      dat[w + 2] = dv[k].z;
+      dat[w + 3] = dv[k].w;
+    }
+  }
+  __syncthreads();
+  const uint64_t ts1 = __builtin_amdgcn_s_memrealtime();
+  for (uint32_t t = tid; t < nch * ppc; t += 1024u) {
+    const uint32_t j = t / ppc, k = t - j * ppc;
+    const uint32_t cend = min((j + 1u) * cs, len);
+    const uint32_t b0 = j * cs + psz * k;
+    if (b0 >= cend) continue;  // last chunk is short
+    const uint32_t e = min(b0 + psz, cend);
+    uint32_t c = k == 0 ? reg0 : 0u;
+    uint32_t b = b0;
+    for (; b + 4u <= e; b += 4u) {
+      const uint32_t w = b >> 2;
+      const uint32_t x = c ^ dat[w + (w >> 4)];
+      c = tt[768u + (x & 0xffu)] ^ tt[512u + ((x >> 8) & 0xffu)] ^ tt[256u + ((x >> 16) & 0xffu)] ^ tt[x >> 24];
+    }
+    for (; b < e; b++) {
+      const uint32_t w = b >> 2;
+      const uint32_t byte = (dat[w + (w >> 4)] >> (8u * (b & 3u))) & 0xffu;
+      c = tt[(c ^ byte) & 0xffu] ^ (c >> 8);
+    }
+    for (uint32_t d = cend - e, lvl = 0; d; lvl++, d >>= 1) {
+      if (d & 1u) {
+        const uint32_t *z = zt + lvl * 1024u;
+        c = z[c & 0xffu] ^ z[256u + ((c >> 8) & 0xffu)] ^ z[512u + ((c >> 16) & 0xffu)] ^ z[768u + (c >> 24)];
+      }
+    }
+    atomicXor(&acc[j], c);
+  }
+  __syncthreads();
+  const uint64_t ts2 = __builtin_amdgcn_s_memrealtime();
+  if (MODE == kModeVerify) {
+#pragma unroll
+    for (uint32_t k = 0; k < 2; k++) {
+      const uint32_t j = k * 1024u + tid;
+      if (j < nch && (be ? __builtin_bswap32(ev[k]) : ev[k]) != ~acc[j]) {
+        atomicMin(&res[0], j);
+        atomicAdd(&res[1], 1u);
+      }
+    }
+    __syncthreads();
+  }
+  // Wave 0 alone writes every result to host memory, so one system-scope
+  // fence (one PCIe write round trip) orders them all before the sequence
+  // number the host polls.
+  if (tid < 64u) {
+    if (MODE == kModeCompute) {
+      for (uint32_t j = tid; j < nch; j += 64u) {
+        const uint32_t v = ~acc[j];
+        crcs[j] = be ? __builtin_bswap32(v) : v;
+      }
+    }
+    if (tid == 0) {
+      const uint64_t ts3 = __builtin_amdgcn_s_memrealtime();
+      meta[0] = res[0];
+      meta[1] = res[1];
+      meta[4] = uint32_t(ts0);
+      meta[5] = uint32_t(ts1);
+      meta[6] = uint32_t(ts2);
+      meta[7] = uint32_t(ts3);
+    }
+    __threadfence_system();
+    if (tid == 0) __hip_atomic_store(&meta[2], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 // Composite CRC of whole segments from their chunk CRCs (no data re-read):
 // c(A||B) = Z_|B|(c(A)) ^ c(B), so c(seg) = XOR_i Z_{bytes after chunk i}(c_i).
 // One thread folds a run of kCompRun chunks sequentially
@@ -994,6 +1142,22 @@ hipError_t launch_composite(const SegDev *segs, uint32_t nseg, const uint64_t *r
   const uint32_t blocks = static_cast<uint32_t>((total_runs + 255) / 256);
   hipLaunchKernelGGL(composite_kernel, dim3(blocks), dim3(256), 0, stream, segs, nseg, run_prefix, total_runs, pow2,
                      out);
+  return hipGetLastError();
+}
+
+hipError_t launch_small_chunks(int mode, const uint8_t *p, uint32_t len, uint32_t exact, uint32_t cs, uint32_t reg0,
+                               uint32_t be, const uint32_t *expect, const uint32_t *tab, const uint32_t *pow2,
+                               uint32_t *meta, uint32_t *crcs, uint32_t seq, hipStream_t stream) {
+  const uint32_t nch = cs ? (len + cs - 1) / cs : 0u;
+  if (!len || len > kSmallMax || !cs || (cs % 4u && nch > 1) || nch > kSmallMaxChunks ||
+      (reinterpret_cast<uintptr_t>(p) & 15u))
+    return hipErrorInvalidValue;
+  if (mode == kModeVerify)
+    hipLaunchKernelGGL(small_chunks_kernel<kModeVerify>, dim3(1), dim3(1024), 0, stream, p, len, exact, cs, reg0, be,
+                       expect, tab, pow2, meta, crcs, seq);
+  else
+    hipLaunchKernelGGL(small_chunks_kernel<kModeCompute>, dim3(1), dim3(1024), 0, stream, p, len, exact, cs, reg0,
+                       be, expect, tab, pow2, meta, crcs, seq);
   return hipGetLastError();
 }
 

@@ -326,3 +326,46 @@ def test_segment_beyond_4gib(engine, oracle):
     assert m == len(expected) and fb[0] == 0
     bits = np.unpackbits(bm.download(), bitorder="little")
     assert list(np.nonzero(bits)[0]) == expected
+
+
+@pytest.mark.parametrize("n", [1, 3, 63, 64, 65, 255, 256, 257, 4095, 4096, 4097, 65535, 65536, 65537, 200001])
+def test_dropin_small_launch_sizes(engine, oracle, n):
+    """Host buffers up to 64 KiB take the one-launch small kernel (pinned
+    stage read over PCIe, zeros-operator combine of 64-B pieces); larger ones
+    the staged 4 KiB-piece path.  Both ends of the switch, every piece-count
+    remainder, chained from a non-zero CRC, all three drop-in symbols."""
+    data = np.random.default_rng(n).integers(0, 256, n, dtype=np.uint8)
+    for crc0 in (0, 0x9E3779B9):
+        want = oracle.crc32c(crc0, data)
+        for entry in ("_hdfs_crc32c", "_hdfs_sse42_crc32c", "_hdfs_sw_crc32c"):
+            assert engine.crc32c(crc0, data, entry) == want, (entry, crc0)
+    # and the CRC32 (zlib) table set through the same kernel
+    import zlib
+    assert engine.stream_ex(engine.CSUM_CRC32, 0, data) == zlib.crc32(data.tobytes())
+
+
+@pytest.mark.parametrize("cs", [4, 64, 100, 512, 777, 4096, 65536])
+@pytest.mark.parametrize("dlen", [1, 511, 512, 513, 8192, 65535, 65536, 65537])
+def test_packet_mirrors_small_and_large(engine, oracle, cs, dlen):
+    """_verify_crcdata / the write loop on one packet, through both engine
+    paths: the one-launch small kernel (dlen <= 64 KiB, <= 2048 chunks,
+    chunk % 4 == 0) and the staged plan path (everything else: cs 4 at 64 KiB
+    is 16384 chunks, cs 777, dlen > 64 KiB).  Every chunk CRC, then the
+    first-bad answer for a corrupted data byte and for a corrupted CRC word."""
+    rng = np.random.default_rng(cs * 100003 + dlen)
+    data = rng.integers(0, 256, dlen, dtype=np.uint8)
+    nch = (dlen + cs - 1) // cs
+    for ctype in (engine.CSUM_CRC32C, engine.CSUM_CRC32):
+        want = oracle.compose_crcs([data.tobytes()], cs, ctype=ctype)
+        got = engine.compose_crcs([data[: dlen // 3].tobytes(), data[dlen // 3:].tobytes()], cs, ctype=ctype)
+        assert got == want
+        region = bytearray(want + data.tobytes())
+        assert engine.verify_crcdata(bytes(region), cs, nch * 4, dlen, ctype=ctype) == (0, -1)
+        bad = int(rng.integers(0, nch))
+        pos = nch * 4 + bad * cs + int(rng.integers(0, min(cs, dlen - bad * cs)))
+        region[pos] ^= 0x40
+        assert engine.verify_crcdata(bytes(region), cs, nch * 4, dlen, ctype=ctype) == (engine.ERR_BAD_CHECKSUM, bad)
+        region[pos] ^= 0x40
+        region[4 * (nch - 1)] ^= 1  # the last chunk's wire CRC
+        assert engine.verify_crcdata(bytes(region), cs, nch * 4, dlen, ctype=ctype) == \
+            (engine.ERR_BAD_CHECKSUM, nch - 1)

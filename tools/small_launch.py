@@ -52,7 +52,9 @@ for name, seg_bytes, n in [("1x64KiB", 65536, 1), ("1x1MiB", 1 << 20, 1), ("1x16
 # host-side call latency
 x512 = np.frombuffer(os.urandom(512), np.uint8)
 x64k = np.frombuffer(os.urandom(65536), np.uint8)
-for name, buf in [("512B", x512), ("64KiB", x64k)]:
+x4k = x64k[:4096].copy()
+x64k1 = np.frombuffer(os.urandom(65537), np.uint8)
+for name, buf in [("512B", x512), ("4KiB", x4k), ("64KiB", x64k), ("64KiB+1", x64k1)]:
     h.crc32c(0, buf)
     t0 = time.perf_counter()
     for _ in range(200):
