@@ -41,8 +41,9 @@ int env_int(const char *name, int dflt) {
   return e ? std::atoi(e) : dflt;
 }
 int g_tile_order = env_int("HDFS_CRC32C_TILE_ORDER", 3);
-// Data-stream load policy of the tiled kernel: 0 default, 1 nontemporal.
-int g_nt_loads = env_int("HDFS_CRC32C_NT", 1);
+// Data-stream loads of the tiled kernel: 0 default policy, 1 nontemporal,
+// 2 nontemporal buffer loads (SGPR base + cached per-lane offsets).
+int g_nt_loads = env_int("HDFS_CRC32C_NT", 2);
 // Rounds in flight per wave + 1 (register buffers of the tiled kernel): 2..4.
 int g_depth = env_int("HDFS_CRC32C_DEPTH", 3);
 // Tile streams per wave (1, 2, 4) and threads per workgroup (512, 768, 1024)
@@ -968,7 +969,8 @@ int hdfs_crc32c_set_shape(int streams, int block) {
 }
 
 int hdfs_crc32c_set_tuning(int nt_loads, void *diag) {
-  g_nt_loads = nt_loads ? 1 : 0;
+  if (nt_loads < 0 || nt_loads > 2) return fail(HDFS_CRC32C_EINVAL, "nt_loads 0..2");
+  g_nt_loads = nt_loads;
   g_diag = static_cast<unsigned long long *>(diag);
   return HDFS_CRC32C_OK;
 }

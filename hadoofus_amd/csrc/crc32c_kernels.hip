@@ -269,23 +269,62 @@ DEV uint64_t tile_at_round(SegP segs, uint32_t nseg, uint64_t r, uint64_t total_
 // expected CRC of the lane's chunk.  Unconditional (addresses clamped into
 // the tile) so the vector-memory count is static and the compiler's
 // s_waitcnt vmcnt(N) for the round being processed stays counted.
-template <int MODE, int NT>
+// Per-lane load offsets for the buffer-load form of issue(): chunk g's
+// 16-B piece of the lane sits at (2k + hsel) * cs + loff from the round's
+// base; cached per chunk size (wave-uniform compare, no VALU in the common
+// case of one chunk size).
+struct LaneOff {
+  uint32_t cs;
+  uint32_t v[4];
+};
+
+template <int MODE, int NT, int BUF>
 DEV void issue(uint32_t (&d)[16], uint32_t &exp, const Cursor c, SegP segs, uint32_t hsel, uint32_t loff,
-               uint32_t qg) {
+               uint32_t qg, LaneOff &lo) {
   const uint32_t cs = segs[c.seg].chunk_size;
-  const uint32_t last = min(kTileChunks, segs[c.seg].nchunks - c.tile * kTileChunks) - 1u;
-  const uint8_t *p = segs[c.seg].data + static_cast<uint64_t>(c.tile) * kTileChunks * cs +
-                     static_cast<uint64_t>(c.r) * kRoundBytes + loff;
+  if constexpr (BUF) {
+    // Buffer loads: the round's base in SGPRs, per-lane offsets from the
+    // cache, and the descriptor's range (the valid bytes of this round's
+    // chunks) returns zeros for chunks past a partial tile's end instead of
+    // clamping addresses.
+    const uint32_t nch = min(kTileChunks, segs[c.seg].nchunks - c.tile * kTileChunks);
+    const uint8_t *base = segs[c.seg].data + static_cast<uint64_t>(c.tile) * kTileChunks * cs +
+                          static_cast<uint64_t>(c.r) * kRoundBytes;
+    if (lo.cs != cs) {
+      lo.cs = cs;
 #pragma unroll
-  for (int k = 0; k < 4; k++) {
-    const uint32_t g = min(2u * k + hsel, last);
-    const u32x4 v = NT ? gload16_nt(p + static_cast<uint64_t>(g) * cs) : gload16(p + static_cast<uint64_t>(g) * cs);
-    d[4 * k + 0] = v.x;
-    d[4 * k + 1] = v.y;
-    d[4 * k + 2] = v.z;
-    d[4 * k + 3] = v.w;
+      for (int k = 0; k < 4; k++) lo.v[k] = (2u * k + hsel) * cs + loff;
+    }
+    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t *>(base), 0, static_cast<int>((nch - 1u) * cs + kRoundBytes), 0x00020000);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const u32x4 v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rd, lo.v[k], 0, NT ? 2 : 0));
+      d[4 * k + 0] = v.x;
+      d[4 * k + 1] = v.y;
+      d[4 * k + 2] = v.z;
+      d[4 * k + 3] = v.w;
+    }
+    if (MODE != kModeCompute) {
+      const __amdgpu_buffer_rsrc_t re = __builtin_amdgcn_make_buffer_rsrc(
+          segs[c.seg].crcs + c.tile * kTileChunks, 0, static_cast<int>(nch * 4u), 0x00020000);
+      exp = __builtin_amdgcn_raw_buffer_load_b32(re, qg * 4u, 0, 0);
+    }
+  } else {
+    const uint32_t last = min(kTileChunks, segs[c.seg].nchunks - c.tile * kTileChunks) - 1u;
+    const uint8_t *p = segs[c.seg].data + static_cast<uint64_t>(c.tile) * kTileChunks * cs +
+                       static_cast<uint64_t>(c.r) * kRoundBytes + loff;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t g = min(2u * k + hsel, last);
+      const u32x4 v = NT ? gload16_nt(p + static_cast<uint64_t>(g) * cs) : gload16(p + static_cast<uint64_t>(g) * cs);
+      d[4 * k + 0] = v.x;
+      d[4 * k + 1] = v.y;
+      d[4 * k + 2] = v.z;
+      d[4 * k + 3] = v.w;
+    }
+    if (MODE != kModeCompute) exp = gload32(segs[c.seg].crcs + c.tile * kTileChunks + min(qg, last));
   }
-  if (MODE != kModeCompute) exp = gload32(segs[c.seg].crcs + c.tile * kTileChunks + min(qg, last));
 }
 
 struct LaneConst {
@@ -334,15 +373,20 @@ DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, ui
       u32x4 v4 = {val, val, val, val};
       __builtin_amdgcn_raw_buffer_store_b128(v4, r4, leader ? L.qg * 16u : 0x80000000u, 0, 0);
     } else {
+      // descriptor fields forced uniform (readfirstlane): otherwise the
+      // compiler may treat them as divergent and wrap the store in a
+      // waterfall loop
       const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-          segs[c.seg].crcs + c.tile * kTileChunks, 0, keep ? static_cast<int>(nch * 4u) : 0, 0x00020000);
+          reinterpret_cast<uint32_t *>(rfl64(reinterpret_cast<uint64_t>(segs[c.seg].crcs + c.tile * kTileChunks))), 0,
+          static_cast<int>(rfl(keep ? nch * 4u : 0u)), 0x00020000);
       const uint32_t off = leader ? L.qg * 4u : 0x80000000u;
       if (L.store_policy == 1) __builtin_amdgcn_raw_buffer_store_b32(val, rs, off, 0, 2);  // nt
       else __builtin_amdgcn_raw_buffer_store_b32(val, rs, off, 0, 0);
     }
   } else {
     const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
-        segs[c.seg].bitmap + c.tile, 0, (last && L.store_policy != 2) ? 1 : 0, 0x00020000);
+        reinterpret_cast<uint8_t *>(rfl64(reinterpret_cast<uint64_t>(segs[c.seg].bitmap + c.tile))), 0,
+        static_cast<int>(rfl((last && L.store_policy != 2) ? 1u : 0u)), 0x00020000);
     __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(byte), rb, L.lane == 0 ? 0u : 0x80000000u, 0, 0);
     if (byte && L.lane == 0) {  // rare: only tiles with a mismatch
       atomicMin(&first_bad[c.seg], c.tile * kTileChunks + __builtin_ctz(byte));
@@ -398,7 +442,7 @@ DEV void process(const uint32_t *lds, uint32_t (&d)[S][16], const uint32_t (&exp
 // rounds stay in flight while one is processed); S independent tile streams
 // per wave (S x 4 KiB per round, S chains of ILP); BLOCK threads per
 // workgroup (one workgroup per CU: the LDS image takes 156 KiB).
-template <int MODE, int ORDER, int NT, int DEPTH, int S, int BLOCK>
+template <int MODE, int ORDER, int NT, int DEPTH, int S, int BLOCK, int BUF = 0>
 __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
     const SegDev *__restrict__ segs, uint32_t nseg, uint64_t total_rounds, uint64_t total_tiles,
     const uint32_t *__restrict__ gtab, uint32_t *__restrict__ first_bad,
@@ -446,7 +490,7 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
   __syncthreads();
 
   LaneConst L;
-  L.store_policy = tune & 0xffu;  // tune: [7:0] store policy, [11:8] ORDER-3 group shift
+  L.store_policy = rfl(tune & 0xffu);  // tune: [7:0] store policy, [11:8] ORDER-3 group shift (uniform: SGPR)
   L.lane = threadIdx.x & 63u;
   L.hsel = (L.lane >> 3) & 1u;                              // load: odd sub-chunk of each 1 KiB
   L.loff = 16u * (4u * (L.lane & 7u) + (L.lane >> 4));      // load: byte offset in the sub-chunk
@@ -550,6 +594,7 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
   uint32_t buf[DEPTH][S][16];
   uint32_t ex[DEPTH][S];
   uint32_t st[S];
+  LaneOff lo{0u, {0u, 0u, 0u, 0u}};
 #pragma unroll
   for (int s = 0; s < S; s++) st[s] = 0u;
 #pragma unroll
@@ -562,7 +607,7 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
 #pragma unroll
     for (int s = 0; s < S; s++) {
       ex[k][s] = 0u;
-      issue<MODE, NT>(buf[k][s], ex[k][s], cur[k][s], sg, L.hsel, L.loff, L.qg);
+      issue<MODE, NT, BUF>(buf[k][s], ex[k][s], cur[k][s], sg, L.hsel, L.loff, L.qg, lo);
     }
   }
   for (;;) {
@@ -575,7 +620,7 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
 #pragma unroll
       for (int s = 0; s < S; s++) {
         cur[k][s] = advance<ORDER>(cur[prev][s], sg, nseg, w);
-        issue<MODE, NT>(buf[k][s], ex[k][s], cur[k][s], sg, L.hsel, L.loff, L.qg);
+        issue<MODE, NT, BUF>(buf[k][s], ex[k][s], cur[k][s], sg, L.hsel, L.loff, L.qg, lo);
       }
     }
     bool more = false;
@@ -1010,12 +1055,16 @@ hipError_t launch_tiles(int mode, int order, int nt, int depth, int streams, int
 #define HDFS_LAUNCH(M, O, N, D, S, B)                                                                     \
   hipLaunchKernelGGL((crc32c_tiles_kernel<M, O, N, D, S, B>), dim3(grid), dim3(B), 0, stream, segs, nseg, \
                      total_rounds, total_tiles, gtab, first_bad, mism, diag, tune, gctr)
+#define HDFS_LAUNCH_B(M, O, N, D, S, B)                                                                      \
+  hipLaunchKernelGGL((crc32c_tiles_kernel<M, O, N, D, S, B, 1>), dim3(grid), dim3(B), 0, stream, segs, nseg, \
+                     total_rounds, total_tiles, gtab, first_bad, mism, diag, tune, gctr)
   // Shapes other than (depth 3, 1 stream, 1024 threads) exist for schedule 3
   // only (tuning experiments, tools/exp_ab.py); anything else falls back to
   // the default shape of the requested schedule.
 #define HDFS_LAUNCH_M(M)                                                                \
   do {                                                                                  \
-    if (order == 3 && depth == 2 && streams == 2 && block == 1024) HDFS_LAUNCH(M, 3, 1, 2, 2, 1024); \
+    if (order == 3 && nt == 2 && depth == 3 && streams == 1 && block == 1024) HDFS_LAUNCH_B(M, 3, 1, 3, 1, 1024); \
+    else if (order == 3 && depth == 2 && streams == 2 && block == 1024) HDFS_LAUNCH(M, 3, 1, 2, 2, 1024); \
     else if (order == 3 && depth == 3 && streams == 2 && block == 1024) HDFS_LAUNCH(M, 3, 1, 3, 2, 1024); \
     else if (order == 3 && depth == 3 && streams == 2 && block == 768) HDFS_LAUNCH(M, 3, 1, 3, 2, 768); \
     else if (order == 3 && depth == 2 && streams == 2 && block == 512) HDFS_LAUNCH(M, 3, 1, 2, 2, 512); \
@@ -1037,6 +1086,7 @@ hipError_t launch_tiles(int mode, int order, int nt, int depth, int streams, int
   else if (mode == kModeVerify) HDFS_LAUNCH_M(kModeVerify);
   else HDFS_LAUNCH_M(kModeCompute);
 #undef HDFS_LAUNCH_M
+#undef HDFS_LAUNCH_B
 #undef HDFS_LAUNCH
   return hipGetLastError();
 }

@@ -266,8 +266,9 @@ int hdfs_crc32c_set_tile_order(int order);
  * 32 KiB of 512-B chunks, two whole 128-B lines of CRCs per group).  Env
  * HDFS_CRC32C_GROUP. */
 int hdfs_crc32c_set_group_shift(int shift);
-/* Tuning / diagnostics: nt_loads=1 (default) streams chunk data with nontemporal loads
- * (env HDFS_CRC32C_NT); diag = device u64[3 * waves] receiving per-wave
+/* Tuning / diagnostics: nt_loads=1 streams chunk data with nontemporal global loads,
+ * 2 (default) with nontemporal buffer loads (schedule 3 default shape; other
+ * schedules and shapes use 1), 0 default-policy loads (env HDFS_CRC32C_NT); diag = device u64[3 * waves] receiving per-wave
  * start/end s_memrealtime stamps and rounds processed (NULL = off). */
 int hdfs_crc32c_set_tuning(int nt_loads, void *diag);
 /* Register round buffers per tile stream of the tiled kernel (2..4; depth-1

@@ -1,8 +1,9 @@
 """Every tiled-kernel schedule and shape (tools/exp_ab.py's A/B variants)
 against the oracle on a C5-like table (mixed bytesPerChecksum 512..4096, so
 tiles span 1..8 rounds) large enough that schedule 3 and its global pool are
-engaged (>= 32 rounds per wave per stream).  Compute output bit-exact vs the
-oracle; verify finds exactly the corrupted chunks (bitmaps, first bad)."""
+engaged (>= 32 rounds per wave per stream), with segments ending 0..4 chunks
+short of a whole tile.  Compute output bit-exact vs the oracle; verify finds
+exactly the corrupted chunks (bitmaps, first bad)."""
 import numpy as np
 import pytest
 
@@ -12,38 +13,42 @@ pytestmark = pytest.mark.gpu
 
 SEG = 16 << 20
 NSEG = 64  # 1 GiB: >= 32 rounds per wave per stream at every shape, so schedule 3 + pool run
-# (order, depth, streams, block): the built shapes (crc32c_kernels.hip launch_tiles)
-SHAPES = [(3, 3, 1, 1024), (3, 4, 1, 1024), (3, 2, 2, 1024), (3, 3, 2, 1024), (3, 3, 2, 768),
-          (3, 2, 2, 512), (3, 3, 2, 512), (3, 2, 4, 512), (3, 3, 1, 768), (3, 3, 1, 512),
-          (2, 3, 1, 1024), (1, 3, 1, 1024), (0, 3, 1, 1024)]
+# (order, depth, streams, block, loads): the built shapes (crc32c_kernels.hip
+# launch_tiles); loads 1 = nontemporal global loads, 2 = nontemporal buffer loads
+SHAPES = [(3, 3, 1, 1024, 1), (3, 3, 1, 1024, 2), (3, 4, 1, 1024, 1), (3, 2, 2, 1024, 1), (3, 3, 2, 1024, 1),
+          (3, 3, 2, 768, 1), (3, 2, 2, 512, 1), (3, 3, 2, 512, 1), (3, 2, 4, 512, 1), (3, 3, 1, 768, 1),
+          (3, 3, 1, 512, 1), (2, 3, 1, 1024, 1), (1, 3, 1, 1024, 1), (0, 3, 1, 1024, 1), (1, 3, 1, 1024, 0)]
 
 
 @pytest.fixture(scope="module")
 def table(engine, oracle):
     host = splitmix64_np(NSEG * SEG // 8, seed=5).view(np.uint8).copy()
     sizes = [512 << (i % 4) for i in range(NSEG)]
-    want = [oracle.chunk_crcs(host[i * SEG:(i + 1) * SEG], cs) for i, cs in enumerate(sizes)]
+    # segments end 0..4 chunks short of 16 MiB: partial last tiles
+    lens = [SEG - (i % 5) * cs for i, cs in enumerate(sizes)]
+    want = [oracle.chunk_crcs(host[i * SEG:i * SEG + n], cs) for i, (cs, n) in enumerate(zip(sizes, lens))]
     dbuf = engine.DeviceBuffer(host.nbytes)
     dbuf.upload(host)
-    return host, sizes, want, dbuf
+    return host, sizes, lens, want, dbuf
 
 
-def _set(engine, order, depth, streams, block):
+def _set(engine, order, depth, streams, block, loads):
     engine.set_tile_order(order)
     engine.set_depth(depth)
     engine.set_shape(streams, block)
+    engine.set_tuning(loads, None)
 
 
-@pytest.mark.parametrize("order,depth,streams,block", SHAPES)
-def test_shape_compute_verify(engine, table, order, depth, streams, block):
-    host, sizes, want, dbuf = table
-    nch = [SEG // cs for cs in sizes]
+@pytest.mark.parametrize("order,depth,streams,block,loads", SHAPES)
+def test_shape_compute_verify(engine, table, order, depth, streams, block, loads):
+    host, sizes, lens, want, dbuf = table
+    nch = [n // cs for cs, n in zip(sizes, lens)]
     crcs = [engine.DeviceBuffer(n * 4) for n in nch]
-    bms = [engine.DeviceBuffer(n // 8) for n in nch]
-    segs = [engine.Segment(data=dbuf.ptr + i * SEG, len=SEG, chunk_size=cs, flags=engine.SEG_BE, crc_init=0,
+    bms = [engine.DeviceBuffer((n + 7) // 8) for n in nch]
+    segs = [engine.Segment(data=dbuf.ptr + i * SEG, len=lens[i], chunk_size=cs, flags=engine.SEG_BE, crc_init=0,
                            crcs=crcs[i].ptr, bitmap=bms[i].ptr) for i, cs in enumerate(sizes)]
     try:
-        _set(engine, order, depth, streams, block)
+        _set(engine, order, depth, streams, block, loads)
         engine.Plan(engine.MODE_COMPUTE, segs).execute()
         for i, n in enumerate(nch):
             np.testing.assert_array_equal(crcs[i].download(n * 4, dtype=">u4").astype(np.uint32), want[i],
@@ -63,8 +68,8 @@ def test_shape_compute_verify(engine, table, order, depth, streams, block):
         first_bad, mism = vp.results()
         assert mism == sum(len(v) for v in bad.values())
         for i, n in enumerate(nch):
-            bits = np.unpackbits(bms[i].download(n // 8), bitorder="little")
+            bits = np.unpackbits(bms[i].download((n + 7) // 8), bitorder="little")[:n]
             assert list(np.nonzero(bits)[0]) == bad.get(i, []), i
             assert first_bad[i] == (bad[i][0] if i in bad else 0xFFFFFFFF)
     finally:
-        _set(engine, 3, 3, 1, 1024)
+        _set(engine, 3, 3, 1, 1024, 1)
