@@ -357,9 +357,11 @@ DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, ui
     out = (flags & kSegRaw) ? v : ~v;
     if (MODE == kModeVerify) {
       const uint32_t e = (flags & kSegBigEndian) ? __builtin_bswap32(exp) : exp;
+      // leaders are lanes 8g, so the ballot has bits only at multiples of 8;
+      // one multiply gathers bit 8g into bit 56+g (no carries: each byte of
+      // the product collects at most one term per bit)
       const uint64_t m = __ballot(leader && e != out);
-#pragma unroll
-      for (int g = 0; g < 8; g++) byte |= static_cast<uint32_t>((m >> (8 * g)) & 1u) << g;
+      byte = static_cast<uint32_t>((m * 0x0102040810204080ull) >> 56);
     }
   }
   byte = rfl(byte);
