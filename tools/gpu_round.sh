@@ -6,7 +6,7 @@ cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-round}
-step() { local name=$1; shift; "$@"; local rc=$?; echo "[$name] rc=$rc"; case $rc in 0) ;; *) exit $rc;; esac; }
+step() { local name=$1; shift; "$@"; local rc=$?; echo "[$name] rc=$rc" >&2; case $rc in 0) ;; *) exit $rc;; esac; }
 step tests timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/${TAG}_tests.log 2>&1
 tail -2 gpurun_out/${TAG}_tests.log
 step smoke timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()"
