@@ -287,7 +287,9 @@ int small_call(DevCtx &c, int mode, uint32_t len, uint32_t cs, uint32_t reg0, bo
       if (__atomic_load_n(&c.h_small_out[2], __ATOMIC_ACQUIRE) == seq) return HDFS_CRC32C_OK;
       return fail(HDFS_CRC32C_EHIP, "small kernel finished without publishing its result");
     }
+#if defined(__x86_64__) || defined(__i386__)
     __builtin_ia32_pause();
+#endif
   }
 }
 
