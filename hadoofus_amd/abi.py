@@ -72,6 +72,24 @@ class Packet(ctypes.Structure):
         return {f: getattr(self, f) for f, _ in self._fields_ if f != "reserved"}
 
 
+class OutPacket(ctypes.Structure):
+    """struct hdfs_crc32c_out_packet (write path)."""
+    _fields_ = [
+        ("hdr_off", _u64),
+        ("data_off", _u64),
+        ("offset_in_block", ctypes.c_int64),
+        ("seqno", ctypes.c_int64),
+        ("data_len", ctypes.c_int32),
+        ("hdr_len", _u32),
+        ("crc_len", _u32),
+        ("last", ctypes.c_uint8),
+        ("reserved", ctypes.c_uint8 * 3),
+    ]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_ if f != "reserved"}
+
+
 _lib = None
 
 
@@ -137,6 +155,9 @@ def load(path=LIB_PATH):
     _bind(lib, "hdfs_crc32c_set_tuning", _int, [_int, _vp])
     _bind(lib, "hdfs_crc32c_set_probe", _int, [_int, _int, _int])
     _bind(lib, "hdfs_crc32c_set_depth", _int, [_int])
+    _bind(lib, "hdfs_crc32c_compose_packets", _int,
+          [_vp, _u64, ctypes.c_int64, ctypes.c_int64, _int, _int, _int, _vp, _u64, ctypes.POINTER(OutPacket), _sz,
+           ctypes.POINTER(_sz), ctypes.POINTER(_u64)])
     _bind(lib, "hdfs_crc32c_set_shape", _int, [_int, _int])
     _bind(lib, "hdfs_crc32c_set_store_policy", _int, [_int])
     _bind(lib, "hdfs_crc32c_compute_host", _int, [_vp, _u64, _u32, _u32, _u32, _vp, _u64])
@@ -280,6 +301,27 @@ def verify_packets(stream, proto=PROTO_V2, chunk_size=512, ctype=CSUM_CRC32C, ma
     """Framing + GPU verification of every packet's chunks.
     -> (rc, [packet dicts], consumed); rc = first error in stream order."""
     return _packets("hdfs_crc32c_verify_packets", stream, proto, chunk_size, ctype, max_pkts)
+
+
+def compose_packets(data, offset_in_block=0, seqno=0, proto=PROTO_V2, ctype=CSUM_CRC32C, finish=False,
+                    dptr=None, nbytes=None):
+    """Outgoing packets of one write (_send_packet + _compose_data_packet_header,
+    src/datanode.c:2583-2609, 2781-2868) of host bytes `data`, or of device
+    memory (dptr, nbytes).  -> (header bytes, [packet dicts])."""
+    lib = load()
+    if dptr is not None:
+        p, n, keep = dptr, nbytes, None
+    else:
+        keep, p, n = _host(data)
+    npk, used = _sz(0), _u64(0)
+    _check(lib.hdfs_crc32c_compose_packets(p if n else None, n, offset_in_block, seqno, proto, ctype, int(finish),
+                                           None, 0, None, 0, ctypes.byref(npk), ctypes.byref(used)))
+    hdr = np.zeros(max(1, used.value), dtype=np.uint8)
+    arr = (OutPacket * max(1, npk.value))()
+    _check(lib.hdfs_crc32c_compose_packets(p if n else None, n, offset_in_block, seqno, proto, ctype, int(finish),
+                                           hdr.ctypes.data, used.value, arr, npk.value, ctypes.byref(npk),
+                                           ctypes.byref(used)))
+    return hdr[: used.value].tobytes(), [arr[i].as_dict() for i in range(npk.value)]
 
 
 def compose_crcs(iovecs, chunk=512, ctype=CSUM_CRC32C):

@@ -483,6 +483,56 @@ int host_pipeline(int mode, const uint8_t *data, uint64_t len, uint32_t cs, uint
   return HDFS_CRC32C_OK;
 }
 
+// BE per-chunk CRCs of a host or device buffer into HOST memory (the write
+// path's packet composer): small host / aligned device buffers in one launch
+// of small_chunks_kernel, larger host buffers through the H2D pipeline,
+// larger device buffers as one compute pass.
+int chunk_crcs_to_host(const void *data, uint64_t len, uint32_t cs, int ctype, uint32_t *out_be) {
+  if (!len) return HDFS_CRC32C_OK;
+  if (!data || !out_be || !cs) return fail(HDFS_CRC32C_EINVAL, "bad chunk CRC request");
+  const uint32_t flags = HDFS_CRC32C_SEG_BE | (ctype == HDFS_CRC32C_CSUM_CRC32 ? HDFS_CRC32C_SEG_CRC32 : 0u);
+  const int tset = seg_ctype(flags);
+  const uint64_t nch = (len + cs - 1) / cs;
+  const bool dev = device_accessible(data);
+  if (!dev && !small_ok(len, cs))
+    return host_pipeline(kModeCompute, static_cast<const uint8_t *>(data), len, cs, flags, 0, out_be, nullptr, 0,
+                         nullptr, nullptr);
+  DevCtx *c = nullptr;
+  int rc = ctx_init(-1, &c);
+  if (rc) return rc;
+  DeviceGuard g(c->dev);
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (small_ok(len, cs) && (!dev || (reinterpret_cast<uintptr_t>(data) & 15u) == 0)) {
+    if (!dev) std::memcpy(c->h_small_in, data, size_t(len));
+    rc = small_call(*c, kModeCompute, uint32_t(len), cs, 0xFFFFFFFFu, true, tset,
+                    dev ? static_cast<const uint8_t *>(data) : nullptr);
+    if (rc) return rc;
+    std::memcpy(out_be, c->h_small_out + kSmallMeta, size_t(nch) * 4);
+    return HDFS_CRC32C_OK;
+  }
+  void *d_out = nullptr;
+  HIPCHK(hipMalloc(&d_out, size_t(nch) * 4));
+  hdfs_crc32c_segment in = {data, len, cs, flags, 0, 0, d_out, nullptr};
+  SegDev sd;
+  rc = fill_seg(in, HDFS_CRC32C_MODE_COMPUTE, sd, 0);
+  uint64_t rounds = 0, gtiles = 0, mtiles = 0;
+  if (!rc) {
+    classify(sd, rounds, gtiles, mtiles);
+    hipError_t e = hipMemcpyAsync(c->d_seg, &sd, sizeof(sd), hipMemcpyHostToDevice, c->stream);
+    if (e != hipSuccess) rc = fail(HDFS_CRC32C_EHIP, "segment upload: %s", hipGetErrorString(e));
+  }
+  if (!rc)
+    rc = launch_all(*c, kModeCompute, c->d_seg, 1, rounds, mtiles, gtiles, nullptr, nullptr, c->d_small + 8,
+                    c->stream, nullptr, nullptr, true, tset);
+  if (!rc) {
+    hipError_t e = hipMemcpyAsync(out_be, d_out, size_t(nch) * 4, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) rc = fail(HDFS_CRC32C_EHIP, "chunk CRCs: %s", hipGetErrorString(e));
+  }
+  (void)hipFree(d_out);
+  return rc;
+}
+
 [[noreturn]] void die(const char *who) {
   std::fprintf(stderr, "%s: MI355X CRC32C engine unavailable: %s\n", who, g_err);
   std::abort();

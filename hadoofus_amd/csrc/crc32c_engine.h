@@ -145,6 +145,12 @@ int launch_all(DevCtx &c, int mode, const SegDev *d_segs, uint32_t nseg, uint64_
 // Copy / compute streams, events and the small pipeline buffers.
 int pipe_reserve(DevCtx &c, size_t piece, uint32_t cs, size_t npieces);
 
+// BE per-chunk CRCs (chunk cs; ctype HDFS_CRC32C_CSUM_*) of a host or
+// device buffer into host memory.
+int chunk_crcs_to_host(const void *data, uint64_t len, uint32_t cs, int ctype, uint32_t *out_be);
+int host_pipeline(int mode, const uint8_t *data, uint64_t len, uint32_t cs, uint32_t flags, uint32_t crc_init,
+                  void *crcs, uint8_t *bitmap, uint64_t piece_req, uint64_t *first_bad, uint64_t *mismatches);
+
 struct HostRegistration {
   const void *p = nullptr;
   ~HostRegistration() {

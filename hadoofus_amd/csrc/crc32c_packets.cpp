@@ -25,6 +25,7 @@
 #include <cstdio>
 #include <cstring>
 #include <deque>
+#include <vector>
 
 #include "crc32c_engine.h"
 
@@ -609,6 +610,60 @@ void session_free(hdfs_crc32c_session *s) {
   delete s;
 }
 
+// ---- write path (_send_packet / _compose_data_packet_header) -------------
+constexpr int64_t kPacketSize = 64 * 1024;  // PACKET_SIZE, src/datanode.c:38
+constexpr uint32_t kWriteChunk = 512;       // CHUNK_SIZE, src/datanode.c:37
+
+struct OutPlan {
+  int64_t offset;
+  int64_t seqno;
+  uint64_t data_off;
+  int32_t dlen;
+  bool last;
+};
+
+// Packet sizing of one write: src/datanode.c:2590 (min(remains_tot,
+// PACKET_SIZE)) and :2592-2609 (an unaligned offset first completes its chunk).
+void plan_out_packets(uint64_t len, int64_t off, int64_t seq, bool finish, std::vector<OutPlan> &v) {
+  uint64_t pos = 0;
+  while (pos < len) {
+    int64_t n = int64_t(std::min<uint64_t>(len - pos, uint64_t(kPacketSize)));
+    if (off % kWriteChunk) n = std::min<int64_t>(n, kWriteChunk - off % kWriteChunk);
+    v.push_back(OutPlan{off, seq, pos, int32_t(n), false});
+    off += n;
+    pos += uint64_t(n);
+    seq++;
+  }
+  // hdfs_datanode_finish_block: an empty packet, lastPacketInBlock = (remains_pkt == 0)
+  if (finish) v.push_back(OutPlan{off, seq, pos, 0, true});
+}
+
+inline uint8_t *put_be(uint8_t *p, uint64_t v, int n) {
+  for (int i = n - 1; i >= 0; i--) *p++ = uint8_t(v >> (8 * i));
+  return p;
+}
+inline uint8_t *put_le(uint8_t *p, uint64_t v, int n) {
+  for (int i = 0; i < n; i++) *p++ = uint8_t(v >> (8 * i));
+  return p;
+}
+
+// protobuf-c packing of PacketHeaderProto as the reference fills it
+// (src/datanode.c:2795-2806): required fields in number order, sfixed64 /
+// sfixed32 little-endian, the bool as a one-byte varint, syncBlock unset.
+constexpr uint32_t kHdrProtoBytes = 25;
+uint8_t *put_header_proto(uint8_t *p, int64_t off, int64_t seq, bool last, int32_t dlen) {
+  *p++ = 0x09;  // field 1, wire type 1 (64-bit)
+  p = put_le(p, uint64_t(off), 8);
+  *p++ = 0x11;  // field 2, wire type 1
+  p = put_le(p, uint64_t(seq), 8);
+  *p++ = 0x18;  // field 3, wire type 0 (varint)
+  *p++ = last ? 1 : 0;
+  *p++ = 0x25;  // field 4, wire type 5 (32-bit)
+  return put_le(p, uint32_t(dlen), 4);
+}
+
+uint32_t out_header_bytes(int proto) { return proto == HDFS_CRC32C_PROTO_V1 ? 25u : 4u + 2u + kHdrProtoBytes; }
+
 }  // namespace
 
 extern "C" {
@@ -623,6 +678,84 @@ int hdfs_crc32c_verify_packets(const void *stream, uint64_t len, int proto, uint
                                hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts, uint64_t *consumed) {
   return verify_packets_impl(static_cast<const uint8_t *>(stream), len, proto, chunk_size, ctype, pkts, max_pkts,
                              npkts, consumed, true);
+}
+
+int hdfs_crc32c_compose_packets(const void *data, uint64_t len, int64_t offset_in_block, int64_t seqno, int proto,
+                                int ctype, int finish, void *hdr_out, uint64_t hdr_cap, hdfs_crc32c_out_packet *pkts,
+                                size_t max_pkts, size_t *npkts, uint64_t *hdr_used) {
+  if (npkts) *npkts = 0;
+  if (hdr_used) *hdr_used = 0;
+  if (proto != HDFS_CRC32C_PROTO_V1 && proto != HDFS_CRC32C_PROTO_V2)
+    return fail(HDFS_CRC32C_EINVAL, "proto must be 1 or 2");
+  if (ctype != HDFS_CRC32C_CSUM_NULL && ctype != HDFS_CRC32C_CSUM_CRC32 && ctype != HDFS_CRC32C_CSUM_CRC32C)
+    return fail(HDFS_CRC32C_EINVAL, "bad checksum type %d", ctype);
+  if (offset_in_block < 0) return fail(HDFS_CRC32C_EINVAL, "negative block offset");
+  if (len && !data) return fail(HDFS_CRC32C_EINVAL, "null data");
+  std::vector<OutPlan> plan;
+  plan_out_packets(len, offset_in_block, seqno, finish != 0, plan);
+  const bool csum = ctype != HDFS_CRC32C_CSUM_NULL;
+  const uint32_t hb = out_header_bytes(proto);
+  uint64_t need = 0;
+  for (const OutPlan &k : plan)
+    need += hb + (csum ? 4ull * ((uint64_t(k.dlen) + kWriteChunk - 1) / kWriteChunk) : 0ull);
+  if (npkts) *npkts = plan.size();
+  if (hdr_used) *hdr_used = need;
+  if (!hdr_out || !pkts) return HDFS_CRC32C_OK;  // size query
+  if (max_pkts < plan.size() || hdr_cap < need)
+    return fail(HDFS_CRC32C_EINVAL, "need %zu packets / %llu header bytes", plan.size(), (unsigned long long)need);
+  // Chunk CRCs of the whole write on the GPU: the chunk grid is uniform
+  // (512 B from the first chunk-aligned byte) except for the first packet of
+  // an unaligned write, which is a single short chunk of its own.
+  std::vector<uint32_t> head, body;
+  uint64_t n0 = 0;
+  if (csum && len) {
+    n0 = (offset_in_block % kWriteChunk) ? uint64_t(plan[0].dlen) : 0;
+    if (n0) {
+      head.resize(1);
+      int rc = chunk_crcs_to_host(data, n0, uint32_t(n0), ctype, head.data());
+      if (rc) return rc;
+    }
+    if (len > n0) {
+      body.resize((len - n0 + kWriteChunk - 1) / kWriteChunk);
+      int rc = chunk_crcs_to_host(static_cast<const uint8_t *>(data) + n0, len - n0, kWriteChunk, ctype,
+                                  body.data());
+      if (rc) return rc;
+    }
+  }
+  uint8_t *out = static_cast<uint8_t *>(hdr_out);
+  uint64_t pos = 0;
+  for (size_t i = 0; i < plan.size(); i++) {
+    const OutPlan &k = plan[i];
+    const uint64_t ncrc = csum ? (uint64_t(k.dlen) + kWriteChunk - 1) / kWriteChunk : 0;
+    uint8_t *p = out + pos;
+    p = put_be(p, uint64_t(uint32_t(int32_t(k.dlen + 4 * ncrc + 4))), 4);  // plen (src/datanode.c:2792)
+    if (proto == HDFS_CRC32C_PROTO_V2) {
+      p = put_be(p, kHdrProtoBytes, 2);  // hlen (s16)
+      p = put_header_proto(p, k.offset, k.seqno, k.last, k.dlen);
+    } else {  // src/datanode.c:2808-2812
+      p = put_be(p, uint64_t(k.offset), 8);
+      p = put_be(p, uint64_t(k.seqno), 8);
+      *p++ = k.last ? 1 : 0;
+      p = put_be(p, uint32_t(k.dlen), 4);
+    }
+    if (ncrc) {  // CRCs are already in wire (BE) byte order
+      const uint32_t *src = (n0 && i == 0) ? head.data() : body.data() + (k.data_off - n0) / kWriteChunk;
+      std::memcpy(p, src, size_t(ncrc) * 4);
+      p += ncrc * 4;
+    }
+    hdfs_crc32c_out_packet &o = pkts[i];
+    std::memset(&o, 0, sizeof(o));
+    o.hdr_off = pos;
+    o.data_off = k.data_off;
+    o.offset_in_block = k.offset;
+    o.seqno = k.seqno;
+    o.data_len = k.dlen;
+    o.hdr_len = uint32_t(p - (out + pos));
+    o.crc_len = uint32_t(ncrc * 4);
+    o.last = k.last ? 1 : 0;
+    pos += o.hdr_len;
+  }
+  return HDFS_CRC32C_OK;
 }
 
 int hdfs_crc32c_session_create(hdfs_crc32c_session **out, int proto, uint32_t chunk_size, int ctype,

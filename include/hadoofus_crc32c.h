@@ -188,6 +188,39 @@ int hdfs_crc32c_parse_packets(const void *stream, uint64_t len, int proto, uint3
 int hdfs_crc32c_verify_packets(const void *stream, uint64_t len, int proto, uint32_t chunk_size,
     int ctype, hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts, uint64_t *consumed);
 
+/* ---- write path: outgoing data packets ---------------------------------- */
+/* One outgoing data packet, as _send_packet sizes it and
+ * _compose_data_packet_header builds its header buffer
+ * (src/datanode.c:2583-2609, 2781-2868): hdr_out[hdr_off, +hdr_len) is the
+ * header buffer the reference would writev() before the packet's data
+ * ([plen s32][hlen u16][PacketHeaderProto] (v2) or the 25-byte v1 header,
+ * then 4 BE CRC bytes per 512-B chunk), data[data_off, +data_len) the data. */
+typedef struct hdfs_crc32c_out_packet {
+	uint64_t hdr_off;         /* header + CRC bytes in hdr_out */
+	uint64_t data_off;        /* data bytes in the caller's buffer */
+	int64_t offset_in_block;  /* header offsetInBlock */
+	int64_t seqno;            /* header seqno */
+	int32_t data_len;         /* dataLen */
+	uint32_t hdr_len;         /* header bytes incl. plen, hlen and CRCs */
+	uint32_t crc_len;         /* CRC bytes (4 per chunk; 0 for CSUM_NULL) */
+	uint8_t last;             /* lastPacketInBlock */
+	uint8_t reserved[3];
+} hdfs_crc32c_out_packet;
+
+/* Compose the outgoing packets of one write of len bytes (host or device
+ * memory) starting at block offset offset_in_block with sequence number
+ * seqno: packets of at most 64 KiB (PACKET_SIZE, src/datanode.c:38), the
+ * first one cut at the next 512-B chunk boundary when offset_in_block is
+ * unaligned (src/datanode.c:2590-2609); finish != 0 appends the empty
+ * lastPacketInBlock packet of hdfs_datanode_finish_block.  Every chunk CRC
+ * (CRC32C or zlib CRC32 by ctype; none for CSUM_NULL) is computed on the GPU
+ * in one pass over the data.  With hdr_out or pkts NULL (or too small) only
+ * the sizes are returned: *npkts packets, *hdr_used header bytes (an
+ * undersized call returns HDFS_CRC32C_EINVAL). */
+int hdfs_crc32c_compose_packets(const void *data, uint64_t len, int64_t offset_in_block, int64_t seqno,
+    int proto, int ctype, int finish, void *hdr_out, uint64_t hdr_cap, hdfs_crc32c_out_packet *pkts,
+    size_t max_pkts, size_t *npkts, uint64_t *hdr_used);
+
 /* Streaming sessions for socket-fed packets (pinned ring
  * buffers fed by socket reads, src/net.c:241-263 -> src/datanode.c:2345-2494):
  * the session owns nslots pinned host slots of slot_bytes (defaults 4 x

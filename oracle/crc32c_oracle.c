@@ -20,6 +20,8 @@
  *                            the framing check of src/datanode.c:2438-2446
  *   oracle_compose_crcs   <- src/datanode.c:2814-2860 (write-path CRC loop,
  *                            chained across iovec fragments)
+ *   oracle_compose_packets <- src/datanode.c:2583-2609 (_send_packet packet
+ *                            sizing) + :2781-2868 (_compose_data_packet_header)
  *   oracle_zeros/combine  <- src/crc32c_sse42.c:99-200 generalised to any n
  *   oracle_crc32_zlib     <- zlib crc32() (third-party dependency of
  *                            src/datanode.c:12,2832-2845,2940-2952, not in
@@ -43,6 +45,7 @@
 
 #define ORACLE_POLY 0x82f63b78u /* src/crc32c_sw.c:63 */
 #define ORACLE_POLY_ZLIB 0xedb88320u /* zlib crc32(), HDFS_CSUM_CRC32 */
+#define ORACLE_CSUM_NULL 0   /* include/hadoofus/objects.h:172 */
 #define ORACLE_CSUM_CRC32 1  /* include/hadoofus/objects.h:173 */
 #define ORACLE_CSUM_CRC32C 2
 
@@ -642,6 +645,108 @@ int oracle_verify_packets(const uint8_t *s, uint64_t len, int proto, uint32_t cs
 	for (size_t i = 0; i < n; i++)
 		if (out[i].error)
 			return out[i].error;
+	return 0;
+}
+
+/* ------------------------------------------------------------------ */
+/* Write path: outgoing data packets                                    */
+/* ------------------------------------------------------------------ */
+/* Same layout as hdfs_crc32c_out_packet. */
+struct oracle_out_packet {
+	uint64_t hdr_off, data_off;
+	int64_t offset_in_block, seqno;
+	int32_t data_len;
+	uint32_t hdr_len, crc_len;
+	uint8_t last, reserved[3];
+};
+
+static uint8_t *bput(uint8_t *p, uint64_t v, int n) /* _hdfs_bappend_s*, src/heapbuf.c */
+{
+	for (int i = n - 1; i >= 0; i--)
+		*p++ = (uint8_t)(v >> (8 * i));
+	return p;
+}
+
+/*
+ * One write of len bytes through the reference's packet loop: _send_packet
+ * sizes each new packet (src/datanode.c:2590: min(remains_tot, PACKET_SIZE =
+ * 64 KiB, :38); :2592-2609: an offset that is not a multiple of CHUNK_SIZE =
+ * 512 first completes its chunk) and _compose_data_packet_header
+ * (src/datanode.c:2781-2868) builds its header buffer: plen = dataLen +
+ * 4*crclen + 4, then the v2 [hlen s16][PacketHeaderProto] or the v1 25-byte
+ * header, then one BE CRC per 512-B chunk of the packet (crcinit 0 for
+ * CRC32C, crc32(0, NULL, 0) = 0 for CRC32).  finish appends
+ * hdfs_datanode_finish_block's empty packet (lastPacketInBlock =
+ * (remains_pkt == 0)).  The PacketHeaderProto bytes restate protobuf-c's
+ * packing of the fields the reference sets (:2799-2806): field 1 sfixed64,
+ * 2 sfixed64, 3 bool varint, 4 sfixed32, in field order.
+ * Returns 0, or -1 when hdr_cap / max_pkts are too small.
+ */
+int oracle_compose_packets(const uint8_t *data, uint64_t len, int64_t offset, int64_t seqno, int proto,
+    int ctype, int finish, uint8_t *hdr, uint64_t hdr_cap, struct oracle_out_packet *pk, size_t max_pkts,
+    size_t *npkts, uint64_t *hdr_used)
+{
+	const int64_t PACKET = 64 * 1024, CHUNK = 512;
+	uint64_t remains_tot = len, fed = 0, used = 0;
+	size_t n = 0;
+	int last_done = 0;
+	while (remains_tot > 0 || (finish && !last_done)) {
+		int64_t remains_pkt = remains_tot < (uint64_t)PACKET ? (int64_t)remains_tot : PACKET;
+		if (offset % CHUNK && remains_pkt > CHUNK - offset % CHUNK)
+			remains_pkt = CHUNK - offset % CHUNK;
+		int64_t crclen = ctype != ORACLE_CSUM_NULL ? (remains_pkt + CHUNK - 1) / CHUNK : 0;
+		uint64_t hlen = (proto == 1 ? 25 : 4 + 2 + 25) + 4 * (uint64_t)crclen;
+		if (n >= max_pkts || used + hlen > hdr_cap)
+			return -1;
+		uint8_t *h = hdr + used, *q = h;
+		q = bput(q, (uint64_t)(uint32_t)(remains_pkt + 4 * crclen + 4), 4);
+		if (proto == 1) {
+			q = bput(q, (uint64_t)offset, 8);
+			q = bput(q, (uint64_t)seqno, 8);
+			*q++ = remains_pkt == 0;
+			q = bput(q, (uint64_t)(uint32_t)remains_pkt, 4);
+		} else {
+			uint8_t pb[25];
+			pb[0] = (1 << 3) | 1;
+			for (int i = 0; i < 8; i++)
+				pb[1 + i] = (uint8_t)((uint64_t)offset >> (8 * i));
+			pb[9] = (2 << 3) | 1;
+			for (int i = 0; i < 8; i++)
+				pb[10 + i] = (uint8_t)((uint64_t)seqno >> (8 * i));
+			pb[18] = (3 << 3) | 0;
+			pb[19] = remains_pkt == 0;
+			pb[20] = (4 << 3) | 5;
+			for (int i = 0; i < 4; i++)
+				pb[21 + i] = (uint8_t)((uint32_t)remains_pkt >> (8 * i));
+			q = bput(q, sizeof(pb), 2);
+			memcpy(q, pb, sizeof(pb));
+			q += sizeof(pb);
+		}
+		for (int64_t i = 0; i < crclen; i++) {
+			int64_t clen = remains_pkt - i * CHUNK < CHUNK ? remains_pkt - i * CHUNK : CHUNK;
+			be32enc(q, crc_of(ctype, 0, data + fed + (uint64_t)(i * CHUNK), (size_t)clen));
+			q += 4;
+		}
+		memset(&pk[n], 0, sizeof(pk[n]));
+		pk[n].hdr_off = used;
+		pk[n].data_off = fed;
+		pk[n].offset_in_block = offset;
+		pk[n].seqno = seqno;
+		pk[n].data_len = (int32_t)remains_pkt;
+		pk[n].hdr_len = (uint32_t)(q - h);
+		pk[n].crc_len = (uint32_t)(4 * crclen);
+		pk[n].last = remains_pkt == 0;
+		if (remains_pkt == 0)
+			last_done = 1;
+		n++;
+		used += (uint64_t)(q - h);
+		fed += (uint64_t)remains_pkt;
+		remains_tot -= (uint64_t)remains_pkt;
+		offset += remains_pkt;
+		seqno++;
+	}
+	*npkts = n;
+	*hdr_used = used;
 	return 0;
 }
 

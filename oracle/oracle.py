@@ -48,6 +48,13 @@ class OraclePacket(ctypes.Structure):
                 ("last", ctypes.c_uint8), ("sync", ctypes.c_uint8), ("reserved", ctypes.c_uint8 * 6)]
 
 
+class OracleOutPacket(ctypes.Structure):
+    """struct oracle_out_packet (same layout as hdfs_crc32c_out_packet)."""
+    _fields_ = [("hdr_off", _u64), ("data_off", _u64), ("offset_in_block", ctypes.c_int64),
+                ("seqno", ctypes.c_int64), ("data_len", ctypes.c_int32), ("hdr_len", _u32), ("crc_len", _u32),
+                ("last", ctypes.c_uint8), ("reserved", ctypes.c_uint8 * 3)]
+
+
 class Oracle:
     def __init__(self, path=LIB):
         if not os.path.exists(path):
@@ -72,6 +79,10 @@ class Oracle:
         self._pk = _bind(lib, "oracle_verify_packets", ctypes.c_int,
                          [_vp, _u64, ctypes.c_int, _u32, ctypes.c_int, ctypes.c_int,
                           ctypes.POINTER(OraclePacket), _sz, ctypes.POINTER(_sz), ctypes.POINTER(_u64)])
+        self._opk = _bind(lib, "oracle_compose_packets", ctypes.c_int,
+                          [_vp, _u64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                           _vp, _u64, ctypes.POINTER(OracleOutPacket), _sz, ctypes.POINTER(_sz),
+                           ctypes.POINTER(_u64)])
         self.have_hw = bool(_bind(lib, "oracle_have_hw", ctypes.c_int, [])())
 
     @staticmethod
@@ -117,6 +128,20 @@ class Oracle:
         code = 2 if ctype == CSUM_CRC32 else (1 if (hw and self.have_hw) else 0)
         self._chunks(p, n, chunk, out.ctypes.data, code)
         return out
+
+    def compose_packets(self, data, offset_in_block=0, seqno=0, proto=2, ctype=CSUM_CRC32C, finish=False):
+        """Write-path packets of one write (src/datanode.c:2583-2609, 2781-2868).
+        -> (header bytes, [packet dicts])."""
+        p, n = self._buf(data)
+        maxp = n // 512 + 3
+        hdr = np.zeros(maxp * (31 + 4 * 129), dtype=np.uint8)
+        arr = (OracleOutPacket * maxp)()
+        npk, used = _sz(0), _u64(0)
+        rc = self._opk(p, n, offset_in_block, seqno, proto, ctype, int(finish), hdr.ctypes.data, hdr.nbytes, arr,
+                       maxp, ctypes.byref(npk), ctypes.byref(used))
+        assert rc == 0
+        return hdr[: used.value].tobytes(), [{f: getattr(arr[i], f) for f, _ in OracleOutPacket._fields_
+                                              if f != "reserved"} for i in range(npk.value)]
 
     def verify_packets(self, stream, proto=2, chunk_size=512, ctype=CSUM_CRC32C, max_pkts=None, verify=True):
         """Packet-stream framing + per-chunk verify (src/datanode.c:2345-2494).

@@ -141,3 +141,24 @@ def test_packet_consumer_links(tmp_path, libpath):
 def test_dropin_consumer_links(tmp_path, libpath):
     exe, txt = build_consumer(tmp_path, libpath)
     assert exe.exists() and txt.read_text().count("\n") >= 7
+
+
+def test_struct_layouts_match_c(tmp_path):
+    """ctypes mirrors of the public structs have the C layout (gcc, the
+    reference's compiler)."""
+    import ctypes
+
+    from hadoofus_amd.abi import OutPacket, Packet, Segment
+    src = tmp_path / "l.c"
+    src.write_text(
+        '#include <stddef.h>\n#include <stdio.h>\n#include "hadoofus_crc32c.h"\n'
+        "int main(void){ printf(\"%zu %zu %zu %zu %zu %zu\\n\", sizeof(hdfs_crc32c_out_packet),"
+        " offsetof(hdfs_crc32c_out_packet, data_len), offsetof(hdfs_crc32c_out_packet, crc_len),"
+        " offsetof(hdfs_crc32c_out_packet, last), sizeof(hdfs_crc32c_packet), sizeof(hdfs_crc32c_segment));"
+        " return 0; }\n")
+    exe = tmp_path / "l"
+    subprocess.check_call(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), str(src),
+                           "-o", str(exe)])
+    got = [int(x) for x in subprocess.check_output([str(exe)], text=True).split()]
+    assert got == [ctypes.sizeof(OutPacket), OutPacket.data_len.offset, OutPacket.crc_len.offset,
+                   OutPacket.last.offset, ctypes.sizeof(Packet), ctypes.sizeof(Segment)]
