@@ -494,9 +494,12 @@ int chunk_crcs_to_host(const void *data, uint64_t len, uint32_t cs, int ctype, u
   const int tset = seg_ctype(flags);
   const uint64_t nch = (len + cs - 1) / cs;
   const bool dev = device_accessible(data);
-  if (!dev && !small_ok(len, cs))
-    return host_pipeline(kModeCompute, static_cast<const uint8_t *>(data), len, cs, flags, 0, out_be, nullptr, 0,
+  if (!dev && !small_ok(len, cs)) {
+    // >= 8 pieces per call (4..64 MiB) so the H2D copies overlap the kernels
+    const uint64_t piece = std::min<uint64_t>(uint64_t(64) << 20, std::max<uint64_t>(uint64_t(4) << 20, len / 8));
+    return host_pipeline(kModeCompute, static_cast<const uint8_t *>(data), len, cs, flags, 0, out_be, nullptr, piece,
                          nullptr, nullptr);
+  }
   DevCtx *c = nullptr;
   int rc = ctx_init(-1, &c);
   if (rc) return rc;
@@ -510,8 +513,14 @@ int chunk_crcs_to_host(const void *data, uint64_t len, uint32_t cs, int ctype, u
     std::memcpy(out_be, c->h_small_out + kSmallMeta, size_t(nch) * 4);
     return HDFS_CRC32C_OK;
   }
-  void *d_out = nullptr;
-  HIPCHK(hipMalloc(&d_out, size_t(nch) * 4));
+  if (nch > c->crc_scratch_cap) {  // grown, never shrunk (guarded by mu)
+    if (c->d_crc_scratch) HIPCHK(hipFree(c->d_crc_scratch));
+    c->d_crc_scratch = nullptr;
+    c->crc_scratch_cap = 0;
+    HIPCHK(hipMalloc(&c->d_crc_scratch, size_t(nch) * 4));
+    c->crc_scratch_cap = nch;
+  }
+  void *d_out = c->d_crc_scratch;
   hdfs_crc32c_segment in = {data, len, cs, flags, 0, 0, d_out, nullptr};
   SegDev sd;
   rc = fill_seg(in, HDFS_CRC32C_MODE_COMPUTE, sd, 0);
@@ -529,7 +538,6 @@ int chunk_crcs_to_host(const void *data, uint64_t len, uint32_t cs, int ctype, u
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) rc = fail(HDFS_CRC32C_EHIP, "chunk CRCs: %s", hipGetErrorString(e));
   }
-  (void)hipFree(d_out);
   return rc;
 }
 

@@ -93,6 +93,9 @@ struct DevCtx {
   uint8_t *h_small_in = nullptr, *dv_small_in = nullptr;
   uint32_t *h_small_out = nullptr, *dv_small_out = nullptr;
   uint32_t small_seq = 0;
+  // device CRC scratch of chunk_crcs_to_host (guarded by mu)
+  void *d_crc_scratch = nullptr;
+  uint64_t crc_scratch_cap = 0;
   // host pipeline (guarded by mu): two staging slots on two streams
   hipStream_t copy_stream = nullptr, comp_stream = nullptr;
   hipEvent_t ev_copy[2] = {nullptr, nullptr}, ev_comp[2] = {nullptr, nullptr};
