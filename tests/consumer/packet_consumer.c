@@ -4,7 +4,9 @@
  * builds a v2 packet stream in memory (PacketHeaderProto encoded by hand,
  * CRCs from the engine's own write-path mirror hdfs_crc32c_compose_crcs),
  * corrupts one chunk, then verifies it (1) in one hdfs_crc32c_verify_packets
- * call and (2) through a streaming session fed in odd-sized "socket reads".
+ * call and (2) through a streaming session fed in odd-sized "socket reads";
+ * then (3) composes the packets of one write (hdfs_crc32c_compose_packets)
+ * and reads them back through the verifier.
  * Prints "0 failures" on success.  Test infrastructure (tests/test_abi.py
  * links it on CPU, tests/test_packets.py runs it on the GPU).
  */
@@ -110,6 +112,47 @@ int main(void)
 	}
 	hdfs_crc32c_session_destroy(sess);
 	check(got == NPK + 1 && bad == 1, "session records");
+
+	/* write path: one 1 MiB + 100 B write at an unaligned block offset,
+	 * composed by the engine (sizes first), sent as header buffer + data per
+	 * packet, read back by the packet verifier */
+	{
+		const size_t wlen = (1 << 20) + 100;
+		uint8_t *w = malloc(wlen), *hdr, *wire;
+		hdfs_crc32c_out_packet *opk;
+		size_t nopk = 0, wpos = 0;
+		uint64_t hlen = 0;
+		for (size_t i = 0; i < wlen; i++) {
+			x = x * 1103515245u + 12345u;
+			w[i] = (uint8_t)(x >> 16);
+		}
+		check(hdfs_crc32c_compose_packets(w, wlen, 1000, 5, HDFS_CRC32C_PROTO_V2, HDFS_CRC32C_CSUM_CRC32C, 1,
+		    NULL, 0, NULL, 0, &nopk, &hlen) == 0, "compose_packets sizes");
+		hdr = malloc(hlen);
+		opk = calloc(nopk, sizeof(*opk));
+		wire = malloc(hlen + wlen);
+		check(hdfs_crc32c_compose_packets(w, wlen, 1000, 5, HDFS_CRC32C_PROTO_V2, HDFS_CRC32C_CSUM_CRC32C, 1,
+		    hdr, hlen, opk, nopk, &nopk, &hlen) == 0, "compose_packets");
+		check(nopk == 19 && opk[0].data_len == 24 && opk[nopk - 1].last, "compose_packets layout");
+		for (size_t i = 0; i < nopk; i++) { /* writev(hdr part, data part) */
+			memcpy(wire + wpos, hdr + opk[i].hdr_off, opk[i].hdr_len);
+			wpos += opk[i].hdr_len;
+			memcpy(wire + wpos, w + opk[i].data_off, (size_t)opk[i].data_len);
+			wpos += (size_t)opk[i].data_len;
+		}
+		hdfs_crc32c_packet *rrec = calloc(nopk, sizeof(*rrec));
+		rc = hdfs_crc32c_verify_packets(wire, wpos, HDFS_CRC32C_PROTO_V2, CS, HDFS_CRC32C_CSUM_CRC32C, rrec,
+		    nopk, &n, &used);
+		check(rc == 0 && n == nopk && used == wpos, "write -> read round trip");
+		for (size_t i = 0; i < n; i++)
+			check(rrec[i].seqno == opk[i].seqno && rrec[i].offset_in_block == opk[i].offset_in_block &&
+			    rrec[i].data_len == opk[i].data_len && rrec[i].last == opk[i].last, "round-trip fields");
+		free(rrec);
+		free(wire);
+		free(opk);
+		free(hdr);
+		free(w);
+	}
 	printf("%d failures\n", failures);
 	free(s);
 	free(data);
