@@ -37,7 +37,7 @@ def _worker(rank, world, port, q):
     col.close()
 
 
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 8])
 def test_gloo_world2_sharding_and_aggregate(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
