@@ -369,3 +369,38 @@ def test_packet_mirrors_small_and_large(engine, oracle, cs, dlen):
         region[4 * (nch - 1)] ^= 1  # the last chunk's wire CRC
         assert engine.verify_crcdata(bytes(region), cs, nch * 4, dlen, ctype=ctype) == \
             (engine.ERR_BAD_CHECKSUM, nch - 1)
+
+
+def test_dropin_concurrent_threads(engine, oracle):
+    """The reference's CRC functions are reentrant and thread-safe after load
+    (src/crc32c.h): 8 host threads calling the drop-in symbols
+    and the per-packet mirror at once (ctypes drops the GIL) all get the
+    oracle's answers."""
+    import threading
+    rng = np.random.default_rng(5)
+    bufs = [rng.integers(0, 256, int(n), dtype=np.uint8) for n in rng.integers(1, 200000, 64)]
+    want = [oracle.crc32c(0, b) for b in bufs]
+    errors = []
+
+    def worker(t):
+        try:
+            for i in range(t, t + 160):
+                k = i % len(bufs)
+                got = engine.crc32c(0, bufs[k], ("_hdfs_crc32c", "_hdfs_sse42_crc32c", "_hdfs_sw_crc32c")[i % 3])
+                if got != want[k]:
+                    errors.append((t, k, got, want[k]))
+                if i % 7 == 0:
+                    be = oracle.compose_crcs([bufs[k].tobytes()], 512)
+                    rc, fb = engine.verify_crcdata(be + bufs[k].tobytes(), 512, len(be), bufs[k].nbytes)
+                    if (rc, fb) != (0, -1):
+                        errors.append((t, k, "verify", rc, fb))
+        except Exception as e:  # surfaced below
+            errors.append((t, repr(e)))
+
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join(timeout=120)
+    assert not any(th.is_alive() for th in ths)
+    assert not errors, errors[:5]
