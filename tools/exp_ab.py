@@ -45,20 +45,22 @@ digest0 = h.stream_crc_dev(0, crcs2.ptr, B * BLOCK // cs * 4)
 out["expect_bad"] = expect_bad
 VARIANTS = [tuple(int(x) for x in v.split(",")) for v in
             os.environ.get("AB_VARIANTS", "1,1,3;2,1,3").split(";")]
-# (order, nt, depth[, group shift[, streams, block]])
-VARIANTS = [(v + (3, 1, 1024)[len(v) - 3:]) if len(v) < 6 else v for v in VARIANTS]
+# (order, nt, depth[, group shift[, streams, block[, store policy]]])
+VARIANTS = [(v + (3, 1, 1024, 0)[len(v) - 3:]) if len(v) < 7 else v for v in VARIANTS]
 
 
-def apply(order, nt, depth, gs, S, blk, diag_ptr=None):
+def apply(order, nt, depth, gs, S, blk, pol, diag_ptr=None):
     h.set_tile_order(order)
     h.set_tuning(nt, diag_ptr)
     h.set_depth(depth)
     h.set_group_shift(gs)
     h.set_shape(S, blk)
+    h.set_store_policy(pol)
 
 
-def tag(order, nt, depth, gs, S, blk):
-    return f"o{order}_nt{nt}_d{depth}_g{gs}" + ("" if (S, blk) == (1, 1024) else f"_s{S}_b{blk}")
+def tag(order, nt, depth, gs, S, blk, pol=0):
+    return (f"o{order}_nt{nt}_d{depth}_g{gs}" + ("" if (S, blk) == (1, 1024) else f"_s{S}_b{blk}") +
+            ("" if pol == 0 else f"_p{pol}"))
 res = {}
 for rnd in range(4):
     for v in VARIANTS:
@@ -75,7 +77,7 @@ for k, v in res.items():
 nwaves = 256 * 16
 diag = h.DeviceBuffer(nwaves * 3 * 8)
 for v in list(VARIANTS)[::-1][:2]:
-    order, nt, depth, gs, S, blk = v
+    order, nt, depth, gs, S, blk, pol = v
     apply(*v, diag_ptr=diag.ptr)
     nwaves_v = 256 * (blk // 64)
     diag.fill(0)
@@ -104,5 +106,5 @@ for v in list(VARIANTS)[::-1][:2]:
         "wave_in_block_mean_end_us": [round(float(v), 1) for v in e.mean(0)],
     })
     np.save(os.path.join(ROOT, "gpurun_out", f"diag_{tag(*v)}.npy"), d)
-apply(3, 1, 3, 3, 1, 1024)
+apply(3, 2, 3, 3, 1, 1024, 0)
 print(json.dumps(out))
