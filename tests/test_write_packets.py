@@ -101,3 +101,50 @@ def test_engine_write_read_round_trip(engine, proto):
     rc, got, _ = engine.verify_packets(bytes(wire), proto=proto)
     assert rc == engine.ERR_BAD_CHECKSUM
     assert [(i, p["first_bad"]) for i, p in enumerate(got) if p["error"]] == [(3, 5), (7, 0)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ctype", [0, 1, 2], ids=["null", "crc32", "crc32c"])
+def test_datanode_basics_scenario(engine, ctype):
+    """The reference's end-to-end test without the cluster
+    (tests/t_datanode_basics.c:25-26,85-86,174-274): 70 MiB of '0'+(i%10)
+    written as 64 MiB blocks (hdfs_datanode_write + finish_block) with each
+    checksum type, the packets of every block read back through the packet
+    verifier (v2 stream; the 6 MiB tail block also through a streaming
+    session fed in odd-sized reads), payload reassembled and compared."""
+    towrite, blocksz = 70 << 20, 64 << 20
+    buf = (np.arange(towrite, dtype=np.int64) % 10 + ord("0")).astype(np.uint8)
+    rbuf = np.zeros(towrite, dtype=np.uint8)
+    wtot = 0
+    while wtot < towrite:
+        wblk = min(towrite - wtot, blocksz)
+        hdr, pkts = engine.compose_packets(buf[wtot:wtot + wblk], 0, 0, engine.PROTO_V2, ctype, True)
+        assert sum(p["data_len"] for p in pkts) == wblk and pkts[-1]["last"] == 1
+        wire = _wire(hdr, pkts, buf[wtot:wtot + wblk])
+        rc, got, used = engine.verify_packets(wire, proto=engine.PROTO_V2, ctype=ctype)
+        assert rc == 0 and used == len(wire) and len(got) == len(pkts)
+        w = np.frombuffer(wire, dtype=np.uint8)
+        for p in got:
+            a = p["stream_off"] + p["header_len"] + p["crc_len"]
+            rbuf[wtot + p["offset_in_block"]:wtot + p["offset_in_block"] + p["data_len"]] = w[a:a + p["data_len"]]
+        if wblk < blocksz:  # the tail block again, through a session
+            s = engine.Session(proto=engine.PROTO_V2, ctype=ctype, slot_bytes=1 << 20, nslots=3)
+            recs, pos, i = [], 0, 0
+            while pos < len(wire):  # odd-sized "socket reads"
+                n = min(65537 + 4099 * (i % 7), len(wire) - pos)
+                s.write(wire[pos:pos + n])
+                pos += n
+                i += 1
+                recs += s.poll()[1]
+            s.flush()
+            while True:
+                rc, more = s.poll(wait=True)
+                assert rc == 0
+                if not more:
+                    break
+                recs += more
+            s.close()
+            assert [(r["offset_in_block"], r["data_len"], r["error"]) for r in recs] == \
+                [(p["offset_in_block"], p["data_len"], 0) for p in got]
+        wtot += wblk
+    assert np.array_equal(buf, rbuf), "read differed from write"
