@@ -40,7 +40,13 @@ def build(force=False, verbose=False):
         return LIB
     os.makedirs(LIBDIR, exist_ok=True)
     tmp = LIB + ".tmp"
+    # -amdgpu-atomic-optimizer-strategy=None: the kernels' atomics are
+    # already single-lane (ticket counters, pool claims) or pre-reduced per
+    # wave; the optimizer's ballot/mbcnt scaffolding around each one cost
+    # VALU in the hot loop (verify +0.6-0.9 % in a binary A/B,
+    # tools/exp_ab_libs.py, profiles/r01/exp_ab_libs_atomic_optimizer.json).
     cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-mllvm", "-amdgpu-atomic-optimizer-strategy=None",
            "-Wall", "-Wno-unused-function", f"-Wl,--version-script={os.path.join(CSRC, 'exports.map')}", f"-I{INCLUDE}", f"-I{CSRC}",
            "-o", tmp] + [os.path.join(CSRC, f) for f in SOURCES]
     if verbose:
