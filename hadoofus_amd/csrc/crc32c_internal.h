@@ -20,21 +20,24 @@ enum Mode : int { kModeCompute = 0, kModeVerify = 1, kModeLoadOnly = 2 };
 // stream with one bytesPerChecksum (src/datanode.c:2186); chunk i covers
 // bytes [i*cs, min((i+1)*cs, len)).  Chunks are grouped in TILES of 8
 // (tile t = chunks 8t..8t+7), which is also the bitmap byte they own.
+// The fields the tiled kernel reads every round come first (bytes 0..51),
+// so the compiler can fetch them with few wide scalar loads.
 struct SegDev {
   const uint8_t *data;   // device pointer
-  uint64_t len;          // bytes
   uint32_t *crcs;        // compute: out; verify: expected in
   uint8_t *bitmap;       // verify: out, one bit per chunk, byte t per tile t
-  uint64_t round_start;  // global index of this segment's first main-path round
-  uint64_t gtile_start;  // global index of this segment's first generic tile
   uint64_t mtile_start;  // global index of this segment's first main-path tile
   uint32_t chunk_size;   // bytes per checksum
   uint32_t flags;        // kSeg*
   uint32_t nchunks;      // ceil(len / chunk_size)
   uint32_t main_tiles;   // tiles [0, main_tiles) run on the tiled kernel
-  uint32_t gen_tiles;    // tiles [main_tiles, main_tiles+gen_tiles) run generic
   uint32_t reg_init;     // register value each chunk starts from (~crc_init, or 0 if raw)
+  uint32_t gen_tiles;    // tiles [main_tiles, main_tiles+gen_tiles) run generic
+  uint64_t len;          // bytes
+  uint64_t round_start;  // global index of this segment's first main-path round
+  uint64_t gtile_start;  // global index of this segment's first generic tile
 };
+static_assert(sizeof(SegDev) == 80, "SegDev layout");
 
 // LDS image of the tiled kernel (bytes).
 //  [0, 128 KiB)          slicing-by-4 tables, each replicated 32x so that

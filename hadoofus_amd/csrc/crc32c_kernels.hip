@@ -117,6 +117,22 @@ DEV uint64_t rfl64(uint64_t x) {
 #define CAS __attribute__((address_space(4)))
 typedef const CAS SegDev *SegP;
 
+// The first 48 bytes of a SegDev (the fields read every round), fetched as
+// one aggregate so it lowers to two wide scalar loads instead of one load
+// per field.
+struct SegHot {
+  const uint8_t *data;
+  uint32_t *crcs;
+  uint8_t *bitmap;
+  uint64_t mtile_start;
+  uint32_t chunk_size, flags, nchunks, main_tiles;
+};
+static_assert(sizeof(SegHot) == 48, "SegHot is the head of SegDev");
+DEV SegHot seg_hot(SegP segs, uint32_t s) {
+  const CAS SegHot *p = reinterpret_cast<const CAS SegHot *>(&segs[s]);
+  return SegHot{p->data, p->crcs, p->bitmap, p->mtile_start, p->chunk_size, p->flags, p->nchunks, p->main_tiles};
+}
+
 // Wave-uniform position of one round: (segment, tile, round).
 struct Cursor {
   uint32_t seg, tile, r;
@@ -281,14 +297,15 @@ struct LaneOff {
 template <int MODE, int NT, int BUF>
 DEV void issue(uint32_t (&d)[16], uint32_t &exp, const Cursor c, SegP segs, uint32_t hsel, uint32_t loff,
                uint32_t qg, LaneOff &lo) {
-  const uint32_t cs = segs[c.seg].chunk_size;
+  const SegHot sh = seg_hot(segs, c.seg);
+  const uint32_t cs = sh.chunk_size;
   if constexpr (BUF) {
     // Buffer loads: the round's base in SGPRs, per-lane offsets from the
     // cache, and the descriptor's range (the valid bytes of this round's
     // chunks) returns zeros for chunks past a partial tile's end instead of
     // clamping addresses.
-    const uint32_t nch = min(kTileChunks, segs[c.seg].nchunks - c.tile * kTileChunks);
-    const uint8_t *base = segs[c.seg].data + static_cast<uint64_t>(c.tile) * kTileChunks * cs +
+    const uint32_t nch = min(kTileChunks, sh.nchunks - c.tile * kTileChunks);
+    const uint8_t *base = sh.data + static_cast<uint64_t>(c.tile) * kTileChunks * cs +
                           static_cast<uint64_t>(c.r) * kRoundBytes;
     if (lo.cs != cs) {
       lo.cs = cs;
@@ -307,7 +324,7 @@ DEV void issue(uint32_t (&d)[16], uint32_t &exp, const Cursor c, SegP segs, uint
     }
     if (MODE != kModeCompute) {
       const __amdgpu_buffer_rsrc_t re = __builtin_amdgcn_make_buffer_rsrc(
-          segs[c.seg].crcs + c.tile * kTileChunks, 0, static_cast<int>(nch * 4u), 0x00020000);
+          sh.crcs + c.tile * kTileChunks, 0, static_cast<int>(nch * 4u), 0x00020000);
       exp = __builtin_amdgcn_raw_buffer_load_b32(re, qg * 4u, 0, 0);
     }
   } else {
@@ -344,9 +361,10 @@ struct LaneConst {
 template <int MODE>
 DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, uint32_t st, const LaneConst &L,
                 uint32_t *__restrict__ first_bad, unsigned long long *__restrict__ mism) {
-  const bool last = c.valid && (c.r + 1 == segs[c.seg].chunk_size / kRoundBytes);
-  const uint32_t flags = segs[c.seg].flags;
-  const uint32_t nch = min(kTileChunks, segs[c.seg].nchunks - c.tile * kTileChunks);
+  const SegHot sh = seg_hot(segs, c.seg);
+  const bool last = c.valid && (c.r + 1 == sh.chunk_size / kRoundBytes);
+  const uint32_t flags = sh.flags;
+  const uint32_t nch = min(kTileChunks, sh.nchunks - c.tile * kTileChunks);
   const bool leader = last && (L.qi == 0) && (L.qg < nch);
   uint32_t out = 0, byte = 0;
   if (last) {
@@ -379,7 +397,7 @@ DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, ui
       // compiler may treat them as divergent and wrap the store in a
       // waterfall loop
       const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-          reinterpret_cast<uint32_t *>(rfl64(reinterpret_cast<uint64_t>(segs[c.seg].crcs + c.tile * kTileChunks))), 0,
+          reinterpret_cast<uint32_t *>(rfl64(reinterpret_cast<uint64_t>(sh.crcs + c.tile * kTileChunks))), 0,
           static_cast<int>(rfl(keep ? nch * 4u : 0u)), 0x00020000);
       const uint32_t off = leader ? L.qg * 4u : 0x80000000u;
       if (L.store_policy == 1) __builtin_amdgcn_raw_buffer_store_b32(val, rs, off, 0, 2);  // nt
@@ -387,7 +405,7 @@ DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, ui
     }
   } else {
     const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<uint8_t *>(rfl64(reinterpret_cast<uint64_t>(segs[c.seg].bitmap + c.tile))), 0,
+        reinterpret_cast<uint8_t *>(rfl64(reinterpret_cast<uint64_t>(sh.bitmap + c.tile))), 0,
         static_cast<int>(rfl((last && L.store_policy != 2) ? 1u : 0u)), 0x00020000);
     __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(byte), rb, L.lane == 0 ? 0u : 0x80000000u, 0, 0);
     if (byte && L.lane == 0) {  // rare: only tiles with a mismatch
