@@ -263,7 +263,7 @@ bool small_ok(uint64_t len, uint64_t cs) {
 static const bool g_small_trace = std::getenv("HDFS_CRC32C_SMALL_TRACE") != nullptr;
 
 int small_call(DevCtx &c, int mode, uint32_t len, uint32_t cs, uint32_t reg0, bool be, int ctype,
-               const uint8_t *dsrc = nullptr) {
+               const uint8_t *dsrc) {
   const uint32_t seq = ++c.small_seq;
   const auto tl = std::chrono::steady_clock::now();
   HIPCHK(launch_small_chunks(mode, dsrc ? dsrc : c.dv_small_in, len, dsrc ? 1u : 0u, cs, reg0, be ? 1u : 0u,

@@ -148,6 +148,15 @@ int launch_all(DevCtx &c, int mode, const SegDev *d_segs, uint32_t nseg, uint64_
 // Copy / compute streams, events and the small pipeline buffers.
 int pipe_reserve(DevCtx &c, size_t piece, uint32_t cs, size_t npieces);
 
+// One-launch path for synchronous calls on <= kSmallMax bytes
+// (small_chunks_kernel; caller holds c.mu and has staged the data in
+// c.h_small_in[0, len), wire CRCs at c.h_small_in + kSmallMax for verify,
+// unless dsrc names a 16-B aligned device source).  ctype: table set (0
+// CRC32C, 1 CRC32).  Results: c.h_small_out[0] first bad, [1] mismatches,
+// CRCs from c.h_small_out + kSmallMeta.
+bool small_ok(uint64_t len, uint64_t cs);
+int small_call(DevCtx &c, int mode, uint32_t len, uint32_t cs, uint32_t reg0, bool be, int ctype,
+               const uint8_t *dsrc = nullptr);
 // BE per-chunk CRCs (chunk cs; ctype HDFS_CRC32C_CSUM_*) of a host or
 // device buffer into host memory.
 int chunk_crcs_to_host(const void *data, uint64_t len, uint32_t cs, int ctype, uint32_t *out_be);

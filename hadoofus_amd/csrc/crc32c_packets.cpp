@@ -414,6 +414,30 @@ int verify_packets_impl(const uint8_t *stream, uint64_t len, int proto, uint32_t
     DeviceGuard g(c.dev);
     std::lock_guard<std::mutex> lk(c.mu);
     if ((rc = check_stream_memory(stream))) return rc;
+    // One packet of <= 64 KiB (the common per-read case): one launch of the
+    // small-call kernel instead of the H2D / gather / verify piece pipeline.
+    if (vidx.size() == 1 && small_ok(uint64_t(recs[vidx[0]].data_len), cs)) {
+      hdfs_crc32c_packet &k = recs[vidx[0]];
+      const uint8_t *crcp = stream + k.stream_off + k.header_len;
+      std::memcpy(c.h_small_in, crcp + k.crc_len, size_t(k.data_len));
+      std::memcpy(c.h_small_in + kSmallMax, crcp, size_t(k.crc_len));
+      rc = small_call(c, kModeVerify, uint32_t(k.data_len), cs, 0xFFFFFFFFu, true,
+                      ctype == HDFS_CRC32C_CSUM_CRC32 ? 1 : 0);
+      if (rc) return rc;
+      if (c.h_small_out[0] != 0xFFFFFFFFu) {
+        k.error = HDFS_CRC32C_ERR_DATANODE_BAD_CHECKSUM;
+        k.first_bad = int32_t(c.h_small_out[0]);
+        k.bad_chunks = c.h_small_out[1];
+      }
+      vidx.clear();
+    }
+  }
+  if (!vidx.empty()) {
+    DevCtx *cp = nullptr;
+    if ((rc = ctx_init(-1, &cp))) return rc;
+    DevCtx &c = *cp;
+    DeviceGuard g(c.dev);
+    std::lock_guard<std::mutex> lk(c.mu);
     std::vector<std::pair<size_t, size_t>> pieces;  // [v0, v1) into vidx
     for (size_t v = 0; v < vidx.size(); v++) {
       if (pieces.empty() || wire_end(recs[vidx[v]]) - wire_begin(recs[vidx[pieces.back().first]]) > kPieceCap)

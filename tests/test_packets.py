@@ -141,3 +141,29 @@ def test_gpu_packet_consumer_runs(engine, tmp_path):
     p = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert p.returncode == 0, p.stdout + p.stderr
     assert "0 failures" in p.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("proto,cs,ctype,dlen,last_empty", [
+    (2, 512, CSUM_CRC32C, 65536, True),   # one data packet + the empty last one
+    (2, 512, CSUM_CRC32C, 65536, False),
+    (1, 512, CSUM_CRC32C, 1000, True),
+    (2, 100, CSUM_CRC32C, 30000, True),   # chunk 100: still the one-launch path
+    (2, 777, CSUM_CRC32C, 30000, True),   # chunk 777 (not a multiple of 4): piece pipeline
+    (2, 512, CSUM_CRC32, 65536, True),
+    (2, 32, CSUM_CRC32C, 65536, True),    # 2048 chunks: the one-launch path's limit
+    (2, 16, CSUM_CRC32C, 65536, True),    # 4096 chunks: piece pipeline
+])
+def test_gpu_verify_single_packet(engine, oracle, proto, cs, ctype, dlen, last_empty):
+    """A run holding one data packet (the per-read case) takes the one-launch
+    small-call kernel when it fits; verdicts equal the oracle's, clean and
+    with one or two corrupted chunks."""
+    nch = (dlen + cs - 1) // cs
+    for corrupt in ((), ((0, nch - 1),), ((0, 0), (0, nch // 2))):
+        s, bad = build_stream(oracle.crc32c, proto, cs, ctype, [dlen], seed=dlen + cs, corrupt=corrupt,
+                              last_empty=last_empty)
+        want = oracle.verify_packets(s, proto, cs, ctype)
+        got = engine.verify_packets(s, proto, cs, ctype)
+        assert got == want
+        assert {k: (p["first_bad"], p["bad_chunks"]) for k, p in enumerate(got[1]) if p["error"]} == \
+            {k: (v[0], len(v)) for k, v in bad.items()}

@@ -72,4 +72,17 @@ for _ in range(200):
     rc, _ = h.verify_crcdata(region, 512, len(be), 65536)
     assert rc == 0
 out["verify_crcdata_64KiB_us"] = round((time.perf_counter() - t0) / 200 * 1e6, 1)
+# one received v2 packet of 64 KiB (+ the empty last packet) through the packet-run API
+hdr = (b"\x09" + (0).to_bytes(8, "little") + b"\x11" + (0).to_bytes(8, "little") + b"\x18\x00\x25" +
+       (65536).to_bytes(4, "little"))
+last = (b"\x09" + (65536).to_bytes(8, "little") + b"\x11" + (1).to_bytes(8, "little") + b"\x18\x01\x25" +
+        (0).to_bytes(4, "little"))
+pkt = ((4 + len(be) + 65536).to_bytes(4, "big") + len(hdr).to_bytes(2, "big") + hdr + be + x64k.tobytes() +
+       (4).to_bytes(4, "big") + len(last).to_bytes(2, "big") + last)
+rc, recs, used = h.verify_packets(pkt)
+assert rc == 0 and len(recs) == 2 and used == len(pkt), (rc, recs)
+t0 = time.perf_counter()
+for _ in range(200):
+    h.verify_packets(pkt)
+out["verify_packets_1x64KiB_us"] = round((time.perf_counter() - t0) / 200 * 1e6, 1)
 print(json.dumps(out))
