@@ -128,10 +128,19 @@ int ctx_init(int device, DevCtx **out) {
 }
 
 // Split a segment between the tiled kernel and the generic kernel.
-// Tiled: data 16-B aligned, chunk_size a multiple of 512, full chunks only.
+// Tiled: chunk_size a multiple of 512, full chunks only (any data alignment).
+// Data alignment the tiled kernel requires.  gfx950 under ROCm serves
+// dwordx4 buffer / global loads at any byte address (unaligned access mode),
+// so any segment start works: 4-B aligned data runs at the aligned rate,
+// byte-unaligned data at ~0.6 of it -- both ~2-3x the one-lane-per-chunk
+// generic kernel they used to take (tools/exp_unaligned.py,
+// profiles/r01/exp_unaligned.json).  HDFS_CRC32C_ALIGN=16 restores the old
+// rule.
+static const uintptr_t g_tile_align = uintptr_t(std::max(1, env_int("HDFS_CRC32C_ALIGN", 1)));
+
 void classify(SegDev &s, uint64_t &rounds, uint64_t &gtiles, uint64_t &mtiles) {
   const uint64_t ntiles = (uint64_t(s.nchunks) + kTileChunks - 1) / kTileChunks;
-  const bool eligible = s.nchunks > 0 && (reinterpret_cast<uintptr_t>(s.data) & 15u) == 0 &&
+  const bool eligible = s.nchunks > 0 && (reinterpret_cast<uintptr_t>(s.data) % g_tile_align) == 0 &&
                         s.chunk_size % kRoundBytes == 0;
   const bool partial = s.len % s.chunk_size != 0;
   if (eligible) {

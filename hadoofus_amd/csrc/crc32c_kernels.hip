@@ -657,7 +657,7 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
 
 // Generic path: one lane per chunk, 8 lanes per tile.  Serves chunks the
 // tiled kernel cannot: partial last chunks, chunk sizes that are not a
-// multiple of 512, and segments whose data pointer is not 16-B aligned.
+// multiple of 512 (and, with HDFS_CRC32C_ALIGN > 1, data below that alignment).
 template <int MODE>
 __global__ __launch_bounds__(256) void crc32c_generic_kernel(
     const SegDev *__restrict__ segs, uint32_t nseg, uint64_t total_gtiles,

@@ -73,3 +73,38 @@ def test_shape_compute_verify(engine, table, order, depth, streams, block, loads
             assert first_bad[i] == (bad[i][0] if i in bad else 0xFFFFFFFF)
     finally:
         _set(engine, 3, 3, 1, 1024, 1)
+
+
+def test_unaligned_segments_default_schedule(engine, oracle):
+    """Segments starting at every byte alignment run on the tiled kernel
+    (unaligned buffer loads; schedule 3 + pool engaged at this size) and stay
+    bit-exact; partial last chunks go to the generic kernel."""
+    nseg, seg = 48, 16 << 20
+    host = splitmix64_np((nseg * seg + 64) // 8, seed=11).view(np.uint8).copy()
+    dbuf = engine.DeviceBuffer(host.nbytes)
+    dbuf.upload(host)
+    offs = [i * seg + (i % 16) for i in range(nseg)]
+    lens = [seg - 16 - (i % 3) * 100 for i in range(nseg)]  # some partial last chunks
+    cs = 512
+    want = [oracle.chunk_crcs(host[o:o + n], cs) for o, n in zip(offs, lens)]
+    crcs = [engine.DeviceBuffer(w.nbytes) for w in want]
+    bms = [engine.DeviceBuffer((w.size + 7) // 8) for w in want]
+    segs = [engine.Segment(data=dbuf.ptr + o, len=n, chunk_size=cs, flags=engine.SEG_BE, crc_init=0,
+                           crcs=c.ptr, bitmap=b.ptr) for o, n, c, b in zip(offs, lens, crcs, bms)]
+    engine.Plan(engine.MODE_COMPUTE, segs).execute()
+    for i, w in enumerate(want):
+        np.testing.assert_array_equal(crcs[i].download(dtype=">u4").astype(np.uint32), w, err_msg=str(i))
+    # flip one expected CRC in every 5th segment; verify finds exactly those
+    bad = {}
+    for i in range(0, nseg, 5):
+        k = (i * 7919) % want[i].size
+        arr = want[i].astype(">u4")
+        arr[k] ^= np.uint32(0x100)
+        crcs[i].upload(arr.view(np.uint8))
+        bad[i] = k
+    vp = engine.Plan(engine.MODE_VERIFY, segs)
+    vp.execute()
+    first_bad, mism = vp.results()
+    assert mism == len(bad)
+    for i in range(nseg):
+        assert first_bad[i] == bad.get(i, 0xFFFFFFFF), i
