@@ -223,8 +223,11 @@ def stream_ex(ctype, crc, buf):
     return out.value
 
 
-def _packets(fn, stream, proto, chunk_size, ctype, max_pkts):
-    keep, p, n = _host(stream)
+def _packets(fn, stream, proto, chunk_size, ctype, max_pkts, dptr=None, nbytes=None):
+    if dptr is not None:  # device-resident stream
+        keep, p, n = None, dptr, nbytes
+    else:
+        keep, p, n = _host(stream)
     if max_pkts is None:
         max_pkts = n // (25 if proto == PROTO_V1 else 6) + 1
     arr = (Packet * max(1, max_pkts))()
@@ -291,16 +294,19 @@ def composite_crcs(segments):
     return [out[i] for i in range(n)]
 
 
-def parse_packets(stream, proto=PROTO_V2, chunk_size=512, ctype=CSUM_CRC32C, max_pkts=None):
-    """Framing walk of a host packet stream (no device work).
-    -> (rc, [packet dicts], consumed)."""
-    return _packets("hdfs_crc32c_parse_packets", stream, proto, chunk_size, ctype, max_pkts)
+def parse_packets(stream, proto=PROTO_V2, chunk_size=512, ctype=CSUM_CRC32C, max_pkts=None, dptr=None,
+                  nbytes=None):
+    """Framing walk of a packet stream: host bytes `stream` (no device work),
+    or device memory (dptr, nbytes).  -> (rc, [packet dicts], consumed)."""
+    return _packets("hdfs_crc32c_parse_packets", stream, proto, chunk_size, ctype, max_pkts, dptr, nbytes)
 
 
-def verify_packets(stream, proto=PROTO_V2, chunk_size=512, ctype=CSUM_CRC32C, max_pkts=None):
-    """Framing + GPU verification of every packet's chunks.
+def verify_packets(stream, proto=PROTO_V2, chunk_size=512, ctype=CSUM_CRC32C, max_pkts=None, dptr=None,
+                   nbytes=None):
+    """Framing + GPU verification of every packet's chunks, of host bytes
+    `stream` or of device memory (dptr, nbytes).
     -> (rc, [packet dicts], consumed); rc = first error in stream order."""
-    return _packets("hdfs_crc32c_verify_packets", stream, proto, chunk_size, ctype, max_pkts)
+    return _packets("hdfs_crc32c_verify_packets", stream, proto, chunk_size, ctype, max_pkts, dptr, nbytes)
 
 
 def compose_packets(data, offset_in_block=0, seqno=0, proto=PROTO_V2, ctype=CSUM_CRC32C, finish=False,

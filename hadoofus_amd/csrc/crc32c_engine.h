@@ -36,6 +36,8 @@ hipError_t launch_small_chunks(int mode, const uint8_t *p, uint32_t len, uint32_
 hipError_t launch_prep(uint32_t *fb, uint32_t nfb, unsigned long long *mism, uint32_t *gctr, hipStream_t stream);
 hipError_t launch_gather(const uint8_t *raw, const PktDesc *descs, uint32_t npk, uint32_t units, uint8_t *arena,
                          uint8_t *crc_arena, hipStream_t stream);
+hipError_t launch_header_window(const uint8_t *s, uint64_t len, uint64_t base, uint64_t stride, uint32_t count,
+                                uint8_t *out, hipStream_t stream);
 
 // ---- errors ----
 extern thread_local char g_err[512];
@@ -114,6 +116,12 @@ struct DevCtx {
   PieceSlot kslot[2];
   uint8_t *k_hmeta = nullptr;
   size_t k_hmeta_cap = 0;
+  // device-resident packet streams (guarded by mu): header windows (device
+  // rows + pinned host copy) and the verify tables (segs | first-bad | bitmaps)
+  uint8_t *w_dev = nullptr, *w_host = nullptr;
+  uint32_t w_cap = 0;  // rows
+  uint8_t *v_meta = nullptr;
+  size_t v_meta_cap = 0;
   std::mutex mu;
 };
 

@@ -73,6 +73,7 @@ struct PktDesc {
   uint32_t nunits;    // gather units: ceil(dlen / kGatherSlice)
 };
 constexpr uint32_t kGatherSlice = 65536;  // data bytes per gather workgroup
+constexpr uint32_t kHdrWin = 64;          // header-window row bytes (device packet streams)
 
 // Synchronous host-memory calls up to this size (and chunk count) run as one
 // small kernel reading pinned host memory (small_chunks_kernel).

@@ -1068,6 +1068,35 @@ hipError_t launch_gather(const uint8_t *raw, const PktDesc *descs, uint32_t npk,
   return hipGetLastError();
 }
 
+// Header windows of a device-resident packet stream: row k of out is the
+// kHdrWin bytes at base + k * stride (zero past len).  The host framing walk
+// (crc32c_packets.cpp) reads them after one D2H copy instead of fetching
+// each header with its own copy; for the fixed-size packets of a block
+// transfer one window covers the whole stream.  One thread per dword of a
+// row; byte loads because the rows sit at any byte offset.
+__global__ __launch_bounds__(256) void header_window_kernel(const uint8_t *__restrict__ s, uint64_t len,
+                                                            uint64_t base, uint64_t stride, uint32_t count,
+                                                            uint32_t *__restrict__ out) {
+  const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+  constexpr uint32_t kWords = kHdrWin / 4;
+  if (t >= count * kWords) return;
+  const uint64_t at = base + uint64_t(t / kWords) * stride + 4ull * (t % kWords);
+  uint32_t w = 0;
+#pragma unroll
+  for (int b = 0; b < 4; b++)
+    if (at + b < len) w |= uint32_t(s[at + b]) << (8 * b);
+  out[t] = w;
+}
+
+hipError_t launch_header_window(const uint8_t *s, uint64_t len, uint64_t base, uint64_t stride, uint32_t count,
+                                uint8_t *out, hipStream_t stream) {
+  if (!count) return hipSuccess;
+  const uint32_t threads = count * (kHdrWin / 4);
+  hipLaunchKernelGGL(header_window_kernel, dim3((threads + 255) / 256), dim3(256), 0, stream, s, len, base, stride,
+                     count, reinterpret_cast<uint32_t *>(out));
+  return hipGetLastError();
+}
+
 hipError_t launch_tiles(int mode, int order, int nt, int depth, int streams, int block, int grid,
                         const SegDev *segs, uint32_t nseg, uint64_t total_rounds, uint64_t total_tiles,
                         const uint32_t *gtab, uint32_t *first_bad, unsigned long long *mism,

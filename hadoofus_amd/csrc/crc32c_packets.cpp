@@ -135,11 +135,7 @@ bool decode_header(const uint8_t *p, size_t n, Header &h) {
 
 }  // namespace
 
-int parse_packet_stream(const uint8_t *s, uint64_t len, int proto, uint32_t chunk_size, int ctype,
-                        size_t max_pkts, std::vector<hdfs_crc32c_packet> &out, uint64_t *consumed,
-                        char *errbuf, size_t errlen) {
-  out.clear();
-  *consumed = 0;
+int check_framing_args(int proto, uint32_t chunk_size, int ctype, char *errbuf, size_t errlen) {
   if (proto != HDFS_CRC32C_PROTO_V1 && proto != HDFS_CRC32C_PROTO_V2) {
     std::snprintf(errbuf, errlen, "bad packet protocol %d", proto);
     return HDFS_CRC32C_EINVAL;
@@ -152,68 +148,87 @@ int parse_packet_stream(const uint8_t *s, uint64_t len, int proto, uint32_t chun
     std::snprintf(errbuf, errlen, "chunk_size 0");
     return HDFS_CRC32C_EINVAL;
   }
+  return HDFS_CRC32C_OK;
+}
+
+// Returns kStepNext (k is a complete packet of `total` wire bytes; the walk
+// goes on at pos + total), kStepStop (k is recorded and the walk ends:
+// framing error or the empty last packet) or kStepMore (the packet is
+// incomplete; nothing recorded).
+int frame_step(const uint8_t *p, uint64_t rem, uint64_t pos, int proto, uint32_t chunk_size, int ctype,
+               hdfs_crc32c_packet &k, uint64_t &total) {
+  std::memset(&k, 0, sizeof(k));
+  k.stream_off = pos;
+  k.first_bad = -1;
+  int64_t plen = 0, dlen = 0;
+  if (proto == HDFS_CRC32C_PROTO_V1) {  // src/datanode.c:2363-2384
+    if (rem < 25) return kStepMore;
+    plen = int32_t(be32(p));
+    k.offset_in_block = int64_t(be64(p + 4));
+    k.seqno = int64_t(be64(p + 12));
+    k.last = p[20] != 0;
+    dlen = int32_t(be32(p + 21));
+    k.header_len = 25;
+  } else {  // src/datanode.c:2387-2418
+    if (rem < 6) return kStepMore;
+    plen = int32_t(be32(p));
+    const uint32_t hlen = (uint32_t(p[4]) << 8) | p[5];
+    if (rem < 6 + uint64_t(hlen)) return kStepMore;
+    k.header_len = 6 + hlen;
+    Header h;
+    if (!decode_header(p + 6, hlen, h)) {
+      k.error = HDFS_CRC32C_ERR_INVALID_PACKETHEADERPROTO;
+      return kStepStop;
+    }
+    k.offset_in_block = h.offset;
+    k.seqno = h.seqno;
+    k.last = h.last;
+    k.sync = h.sync;
+    dlen = h.dlen;
+  }
+  // _process_recv_packet framing checks (src/datanode.c:2428-2446)
+  const int64_t crcdlen = plen - dlen - 4;
+  k.data_len = int32_t(dlen);
+  k.crc_len = int32_t(crcdlen);
+  if (plen < 0 || dlen < 0 || dlen > kOneGB || plen > kOneGB || crcdlen < 0)
+    k.error = HDFS_CRC32C_ERR_DATANODE_PACKET_SIZE;
+  else if (ctype != HDFS_CRC32C_CSUM_NULL && crcdlen != ((dlen + chunk_size - 1) / chunk_size) * 4)
+    k.error = HDFS_CRC32C_ERR_DATANODE_CRC_LEN;
+  else if (ctype == HDFS_CRC32C_CSUM_NULL && crcdlen > 0)
+    k.error = HDFS_CRC32C_ERR_DATANODE_UNEXPECTED_CRC_LEN;
+  if (k.error) return kStepStop;
+  if (dlen == 0) {  // src/datanode.c:2448-2456: v2's trailing empty packet
+    if (!k.last) k.error = HDFS_CRC32C_ERR_DATANODE_PACKET_SIZE;
+    total = k.header_len;
+    return kStepStop;
+  }
+  total = uint64_t(k.header_len) + uint64_t(crcdlen) + uint64_t(dlen);
+  if (rem < total) return kStepMore;  // incomplete: the reference reads more (src/datanode.c:2463-2467)
+  return kStepNext;
+}
+
+int parse_packet_stream(const uint8_t *s, uint64_t len, int proto, uint32_t chunk_size, int ctype,
+                        size_t max_pkts, std::vector<hdfs_crc32c_packet> &out, uint64_t *consumed,
+                        char *errbuf, size_t errlen) {
+  out.clear();
+  *consumed = 0;
+  int rc = check_framing_args(proto, chunk_size, ctype, errbuf, errlen);
+  if (rc) return rc;
   if (len && !s) {
     std::snprintf(errbuf, errlen, "null stream");
     return HDFS_CRC32C_EINVAL;
   }
   uint64_t pos = 0;
   while (out.size() < max_pkts) {
-    const uint8_t *p = s + pos;
-    const uint64_t rem = len - pos;
     hdfs_crc32c_packet k;
-    std::memset(&k, 0, sizeof(k));
-    k.stream_off = pos;
-    k.first_bad = -1;
-    int64_t plen = 0, dlen = 0;
-    if (proto == HDFS_CRC32C_PROTO_V1) {  // src/datanode.c:2363-2384
-      if (rem < 25) break;
-      plen = int32_t(be32(p));
-      k.offset_in_block = int64_t(be64(p + 4));
-      k.seqno = int64_t(be64(p + 12));
-      k.last = p[20] != 0;
-      dlen = int32_t(be32(p + 21));
-      k.header_len = 25;
-    } else {  // src/datanode.c:2387-2418
-      if (rem < 6) break;
-      plen = int32_t(be32(p));
-      const uint32_t hlen = (uint32_t(p[4]) << 8) | p[5];
-      if (rem < 6 + uint64_t(hlen)) break;
-      k.header_len = 6 + hlen;
-      Header h;
-      if (!decode_header(p + 6, hlen, h)) {
-        k.error = HDFS_CRC32C_ERR_INVALID_PACKETHEADERPROTO;
-        out.push_back(k);
-        break;
-      }
-      k.offset_in_block = h.offset;
-      k.seqno = h.seqno;
-      k.last = h.last;
-      k.sync = h.sync;
-      dlen = h.dlen;
-    }
-    // _process_recv_packet framing checks (src/datanode.c:2428-2446)
-    const int64_t crcdlen = plen - dlen - 4;
-    k.data_len = int32_t(dlen);
-    k.crc_len = int32_t(crcdlen);
-    if (plen < 0 || dlen < 0 || dlen > kOneGB || plen > kOneGB || crcdlen < 0)
-      k.error = HDFS_CRC32C_ERR_DATANODE_PACKET_SIZE;
-    else if (ctype != HDFS_CRC32C_CSUM_NULL && crcdlen != ((dlen + chunk_size - 1) / chunk_size) * 4)
-      k.error = HDFS_CRC32C_ERR_DATANODE_CRC_LEN;
-    else if (ctype == HDFS_CRC32C_CSUM_NULL && crcdlen > 0)
-      k.error = HDFS_CRC32C_ERR_DATANODE_UNEXPECTED_CRC_LEN;
-    if (k.error) {
-      out.push_back(k);
-      break;
-    }
-    if (dlen == 0) {  // src/datanode.c:2448-2456: v2's trailing empty packet
-      if (!k.last) k.error = HDFS_CRC32C_ERR_DATANODE_PACKET_SIZE;
-      out.push_back(k);
-      if (!k.error) *consumed = pos + k.header_len;
-      break;
-    }
-    const uint64_t total = uint64_t(k.header_len) + uint64_t(crcdlen) + uint64_t(dlen);
-    if (rem < total) break;  // incomplete: the reference reads more (src/datanode.c:2463-2467)
+    uint64_t total = 0;
+    const int st = frame_step(s + pos, len - pos, pos, proto, chunk_size, ctype, k, total);
+    if (st == kStepMore) break;
     out.push_back(k);
+    if (st == kStepStop) {
+      if (!k.error) *consumed = pos + total;
+      break;
+    }
     pos += total;
     *consumed = pos;
   }
@@ -383,12 +398,184 @@ int first_error(const hdfs_crc32c_packet *p, size_t n) {
   return HDFS_CRC32C_OK;
 }
 
-int check_stream_memory(const void *stream) {
-  hipPointerAttribute_t pa;
-  if (hipPointerGetAttributes(&pa, stream) == hipSuccess && pa.type == hipMemoryTypeDevice)
-    return fail(HDFS_CRC32C_EINVAL, "packet stream must be host memory (the datanode's recvbuf)");
-  (void)hipGetLastError();
+// ---- device-resident packet streams ----
+// The framing walk needs ~30 header bytes per packet from a stream the host
+// cannot read.  It asks header_window_kernel for rows of kHdrWin bytes at
+// base + k * stride, where stride is the size of the packet just framed:
+// the fixed-size packets of a block transfer all land on that grid, so a
+// regular stream costs two small D2H round trips (first header, then one
+// window over the rest).  A packet off the grid (a short tail, a trailing
+// empty packet, a stream of mixed sizes) starts a new window at its offset;
+// the window length grows while windows keep hitting and drops back after a
+// miss, so an irregular stream does not pay for rows it never reads.
+struct HeaderWindows {
+  DevCtx &c;
+  const uint8_t *d;
+  uint64_t len;
+  uint64_t base = 0, stride = 0;
+  uint32_t count = 0, used = 0, budget = 8192;
+
+  const uint8_t *lookup(uint64_t pos) {
+    if (!count || pos < base) return nullptr;
+    const uint64_t off = pos - base;
+    const uint64_t k = stride ? off / stride : 0;
+    if ((stride ? off % stride : off) != 0 || k >= count) return nullptr;
+    used = std::max(used, uint32_t(k) + 1);
+    return c.w_host + k * kHdrWin;
+  }
+
+  int fetch(uint64_t pos, uint64_t stride_guess, size_t rows_left) {
+    constexpr uint32_t kMaxRows = 1u << 16;  // 4 MiB of rows per window
+    if (count) budget = (used * 2 >= count) ? std::min(kMaxRows, budget * 8) : 64;
+    uint64_t n = stride_guess ? (len - pos) / stride_guess + 1 : 1;
+    n = std::min<uint64_t>({n, rows_left, budget});
+    if (n == 0) n = 1;
+    if (n > c.w_cap) {
+      uint32_t cap = 1024;
+      while (cap < n) cap *= 2;
+      if (c.w_dev) HIPCHK(hipFree(c.w_dev));
+      if (c.w_host) HIPCHK(hipHostFree(c.w_host));
+      c.w_dev = c.w_host = nullptr;
+      c.w_cap = 0;
+      HIPCHK(hipMalloc(&c.w_dev, size_t(cap) * kHdrWin));
+      HIPCHK(hipHostMalloc(&c.w_host, size_t(cap) * kHdrWin, hipHostMallocDefault));
+      c.w_cap = cap;
+    }
+    HIPCHK(launch_header_window(d, len, pos, stride_guess, uint32_t(n), c.w_dev, c.stream));
+    HIPCHK(hipMemcpyAsync(c.w_host, c.w_dev, size_t(n) * kHdrWin, hipMemcpyDeviceToHost, c.stream));
+    HIPCHK(hipStreamSynchronize(c.stream));
+    base = pos;
+    stride = stride_guess;
+    count = uint32_t(n);
+    used = 0;
+    return HDFS_CRC32C_OK;
+  }
+};
+
+// Framing walk over device memory (same records and stopping rules as
+// parse_packet_stream).  Caller holds c.mu.
+int parse_device_stream(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs, int ctype,
+                        size_t max_pkts, std::vector<hdfs_crc32c_packet> &out, uint64_t *consumed) {
+  out.clear();
+  *consumed = 0;
+  HeaderWindows w{c, d, len};
+  std::vector<uint8_t> big;  // v2 headers longer than a window row
+  uint64_t pos = 0, stride = 0;
+  while (out.size() < max_pkts && pos < len) {
+    const uint8_t *p = w.lookup(pos);
+    if (!p) {
+      int rc = w.fetch(pos, stride, max_pkts - out.size());
+      if (rc) return rc;
+      p = w.lookup(pos);
+    }
+    if (proto == HDFS_CRC32C_PROTO_V2 && len - pos >= 6) {
+      const uint64_t need = 6 + ((uint64_t(p[4]) << 8) | p[5]);
+      if (need > kHdrWin && len - pos >= need) {
+        big.resize(need);
+        HIPCHK(hipMemcpy(big.data(), d + pos, need, hipMemcpyDeviceToHost));
+        p = big.data();
+      }
+    }
+    hdfs_crc32c_packet k;
+    uint64_t total = 0;
+    const int st = frame_step(p, len - pos, pos, proto, cs, ctype, k, total);
+    if (st == kStepMore) break;
+    out.push_back(k);
+    if (st == kStepStop) {
+      if (!k.error) *consumed = pos + total;
+      break;
+    }
+    pos += total;
+    stride = total;
+    *consumed = pos;
+  }
   return HDFS_CRC32C_OK;
+}
+
+// Verify of a device-resident stream: no copies and no de-framing gather --
+// every framing-clean packet is one verify segment pointing into the stream
+// itself (CRCs at stream_off + header_len, data right after them; the tiled
+// kernel takes both at any byte offset), all of them in one launch.
+int verify_device_stream(DevCtx &c, const uint8_t *d, std::vector<hdfs_crc32c_packet> &recs,
+                         const std::vector<size_t> &vidx, uint32_t cs, int ctype) {
+  PieceLayout L;
+  L.n = vidx.size();
+  for (size_t i : vidx) L.bm += (uint64_t(recs[i].crc_len) / 4 + 7) / 8;
+  L.off_segs = 0;
+  L.off_fb = align_up(L.n * sizeof(SegDev), 256);
+  L.off_bm = L.off_fb + align_up(L.n * 4, 256);
+  L.meta = L.off_bm + align_up(L.bm, 256);
+  if (L.meta > c.k_hmeta_cap) {
+    if (c.k_hmeta) HIPCHK(hipHostFree(c.k_hmeta));
+    c.k_hmeta = nullptr;
+    c.k_hmeta_cap = 0;
+    HIPCHK(hipHostMalloc(&c.k_hmeta, L.meta, hipHostMallocDefault));
+    c.k_hmeta_cap = L.meta;
+  }
+  if (L.meta + 64 > c.v_meta_cap) {
+    if (c.v_meta) HIPCHK(hipFree(c.v_meta));
+    c.v_meta = nullptr;
+    c.v_meta_cap = 0;
+    HIPCHK(hipMalloc(&c.v_meta, L.meta + 64));
+    c.v_meta_cap = L.meta + 64;
+  }
+  uint8_t *hm = c.k_hmeta, *dm = c.v_meta;
+  auto *hs = reinterpret_cast<SegDev *>(hm);
+  const uint32_t sflags = HDFS_CRC32C_SEG_BE | (ctype == HDFS_CRC32C_CSUM_CRC32 ? HDFS_CRC32C_SEG_CRC32 : 0u);
+  uint64_t boff = 0;
+  for (size_t v = 0; v < L.n; v++) {
+    const hdfs_crc32c_packet &k = recs[vidx[v]];
+    const uint8_t *crcp = d + wire_begin(k);
+    hdfs_crc32c_segment in = {crcp + k.crc_len, uint64_t(k.data_len), cs, sflags, 0, 0,
+                              const_cast<uint8_t *>(crcp), dm + L.off_bm + boff};
+    int rc = fill_seg(in, HDFS_CRC32C_MODE_VERIFY, hs[v], v);
+    if (rc) return rc;
+    classify(hs[v], L.rounds, L.gtiles, L.mtiles);
+    boff += (uint64_t(k.crc_len) / 4 + 7) / 8;
+  }
+  // the pool counter and mismatch word live past the tables
+  auto *gctr = reinterpret_cast<uint32_t *>(dm + L.meta);
+  auto *mism = reinterpret_cast<unsigned long long *>(dm + L.meta + 8);
+  HIPCHK(hipMemcpyAsync(dm, hm, L.off_fb, hipMemcpyHostToDevice, c.stream));
+  int rc = launch_all(c, kModeVerify, reinterpret_cast<const SegDev *>(dm), uint32_t(L.n), L.rounds, L.mtiles,
+                      L.gtiles, reinterpret_cast<uint32_t *>(dm + L.off_fb), mism, gctr, c.stream, nullptr, nullptr,
+                      true, ctype == HDFS_CRC32C_CSUM_CRC32 ? 1 : 0);
+  if (rc) return rc;
+  HIPCHK(hipMemcpyAsync(hm + L.off_fb, dm + L.off_fb, L.meta - L.off_fb, hipMemcpyDeviceToHost, c.stream));
+  HIPCHK(hipStreamSynchronize(c.stream));
+  finish_piece(recs.data(), vidx.data(), L, hm);
+  return HDFS_CRC32C_OK;
+}
+
+// Device memory of which device (-1: host / unknown memory).
+int stream_device(const void *stream) {
+  hipPointerAttribute_t pa;
+  if (hipPointerGetAttributes(&pa, stream) == hipSuccess && pa.type == hipMemoryTypeDevice) return pa.device;
+  (void)hipGetLastError();
+  return -1;
+}
+
+int verify_packets_dev_impl(int dev, const uint8_t *stream, uint64_t len, int proto, uint32_t cs, int ctype,
+                            hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts, uint64_t *consumed,
+                            bool verify) {
+  DevCtx *cp = nullptr;
+  int rc;
+  if ((rc = ctx_init(dev, &cp))) return rc;
+  DevCtx &c = *cp;
+  DeviceGuard g(c.dev);
+  std::lock_guard<std::mutex> lk(c.mu);
+  std::vector<hdfs_crc32c_packet> recs;
+  uint64_t used = 0;
+  if ((rc = parse_device_stream(c, stream, len, proto, cs, ctype, max_pkts, recs, &used))) return rc;
+  std::vector<size_t> vidx;
+  if (verify && ctype != HDFS_CRC32C_CSUM_NULL)
+    for (size_t i = 0; i < recs.size(); i++)
+      if (!recs[i].error && recs[i].crc_len > 0) vidx.push_back(i);
+  if (!vidx.empty() && (rc = verify_device_stream(c, stream, recs, vidx, cs, ctype))) return rc;
+  if (!recs.empty()) std::memcpy(pkts, recs.data(), recs.size() * sizeof(hdfs_crc32c_packet));
+  if (npkts) *npkts = recs.size();
+  if (consumed) *consumed = used;
+  return first_error(recs.data(), recs.size());
 }
 
 // Synchronous packet-run verify: framing, then pieces of <= 64 MiB of wire
@@ -399,9 +586,16 @@ int verify_packets_impl(const uint8_t *stream, uint64_t len, int proto, uint32_t
   if (npkts) *npkts = 0;
   if (consumed) *consumed = 0;
   if (max_pkts && !pkts) return fail(HDFS_CRC32C_EINVAL, "null packet array");
+  int rc = check_framing_args(proto, cs, ctype, g_err, sizeof(g_err));
+  if (rc) return rc;
+  if (len && stream) {
+    const int dev = stream_device(stream);
+    if (dev >= 0) return verify_packets_dev_impl(dev, stream, len, proto, cs, ctype, pkts, max_pkts, npkts, consumed,
+                                                 verify);
+  }
   std::vector<hdfs_crc32c_packet> recs;
   uint64_t used = 0;
-  int rc = parse_packet_stream(stream, len, proto, cs, ctype, max_pkts, recs, &used, g_err, sizeof(g_err));
+  rc = parse_packet_stream(stream, len, proto, cs, ctype, max_pkts, recs, &used, g_err, sizeof(g_err));
   if (rc) return rc;
   std::vector<size_t> vidx;  // packets whose chunks go to the GPU
   if (verify && ctype != HDFS_CRC32C_CSUM_NULL)
@@ -413,7 +607,6 @@ int verify_packets_impl(const uint8_t *stream, uint64_t len, int proto, uint32_t
     DevCtx &c = *cp;
     DeviceGuard g(c.dev);
     std::lock_guard<std::mutex> lk(c.mu);
-    if ((rc = check_stream_memory(stream))) return rc;
     // One packet of <= 64 KiB (the common per-read case): one launch of the
     // small-call kernel instead of the H2D / gather / verify piece pipeline.
     if (vidx.size() == 1 && small_ok(uint64_t(recs[vidx[0]].data_len), cs)) {

@@ -24,4 +24,15 @@ int parse_packet_stream(const uint8_t *s, uint64_t len, int proto, uint32_t chun
                         size_t max_pkts, std::vector<hdfs_crc32c_packet> &out, uint64_t *consumed,
                         char *errbuf, size_t errlen);
 
+// Argument checks shared by every framing entry (EINVAL + message).
+int check_framing_args(int proto, uint32_t chunk_size, int ctype, char *errbuf, size_t errlen);
+
+// One step of the walk: the packet at stream offset `pos`, whose first bytes
+// are at p (rem = bytes of the stream from pos on; p must hold
+// min(rem, kHdrWin) bytes, enough for any v1 header and any v2 header of
+// up to kHdrWin - 6 bytes -- a longer v2 header needs 6 + hlen).
+enum { kStepNext = 0, kStepStop = 1, kStepMore = 2 };
+int frame_step(const uint8_t *p, uint64_t rem, uint64_t pos, int proto, uint32_t chunk_size, int ctype,
+               hdfs_crc32c_packet &k, uint64_t &total);
+
 }  // namespace hdfs_crc32c

@@ -167,3 +167,71 @@ def test_gpu_verify_single_packet(engine, oracle, proto, cs, ctype, dlen, last_e
         assert got == want
         assert {k: (p["first_bad"], p["bad_chunks"]) for k, p in enumerate(got[1]) if p["error"]} == \
             {k: (v[0], len(v)) for k, v in bad.items()}
+
+
+# --- GPU: device-resident streams (GPU-direct receive) -----------------------
+def _dev(engine, s, shift=0):
+    """Stream bytes in device memory at byte offset `shift` of a fresh buffer."""
+    buf = engine.DeviceBuffer(len(s) + shift + 64)
+    buf.fill(0)
+    buf.upload(np.frombuffer(s, np.uint8), offset=shift)
+    engine.device_sync()
+    return buf, buf.ptr + shift
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_gpu_device_stream_fixture(engine, case):
+    """The golden packet runs, uploaded to HBM: framing over header windows
+    and verify in place give the fixture's records."""
+    s = _stream(case)
+    if not s:
+        pytest.skip("empty stream")
+    proto, cs, ctype, max_pkts = _args(case)
+    for shift in (0, 3):
+        keep, p = _dev(engine, s, shift)
+        got = engine.verify_packets(None, proto, cs, ctype, max_pkts, dptr=p, nbytes=len(s))
+        assert got[1] == case["expect"]["packets"]
+        assert (got[0], got[2]) == (case["expect"]["rc"], case["expect"]["consumed"])
+        rc, pkts, used = engine.parse_packets(None, proto, cs, ctype, max_pkts, dptr=p, nbytes=len(s))
+        assert pkts == _framing_only(case["expect"]["packets"]) and used == case["expect"]["consumed"]
+        keep.free()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("proto,cs,ctype,sizes,shift", [
+    (2, 512, CSUM_CRC32C, "regular", 0),   # one window covers the run
+    (1, 512, CSUM_CRC32C, "regular", 1),   # v1: CRCs and data at odd offsets
+    (2, 512, CSUM_CRC32, "regular", 0),
+    (2, 4096, CSUM_CRC32C, "mixed", 0),    # window misses: sizes change every few packets
+    (2, 512, CSUM_CRC32C, "random", 2),    # every packet a different size
+])
+def test_gpu_device_stream_vs_oracle(engine, oracle, proto, cs, ctype, sizes, shift):
+    rng = np.random.default_rng(len(sizes) + cs + proto)
+    if sizes == "regular":
+        dl = [65536] * 700 + [12345]
+    elif sizes == "mixed":
+        dl = [int(x) for x in np.repeat(rng.choice([4096, 61440, 30000, 65536], 60), rng.integers(1, 8, 60))]
+    else:
+        dl = [int(x) for x in rng.integers(1, 70000, 300)]
+    corrupt = set()  # distinct chunks (two flips of one chunk would cancel)
+    for _ in range(20):
+        k = int(rng.integers(0, len(dl)))
+        corrupt.add((k, int(rng.integers(0, (dl[k] + cs - 1) // cs))))
+    s, bad = build_stream(oracle.crc32c, proto, cs, ctype, dl, seed=len(dl), corrupt=sorted(corrupt))
+    want = oracle.verify_packets(s, proto, cs, ctype)
+    keep, p = _dev(engine, s, shift)
+    got = engine.verify_packets(None, proto, cs, ctype, dptr=p, nbytes=len(s))
+    assert got == want
+    assert got[0] == BAD and got[2] == len(s)
+    assert {k: (q["first_bad"], q["bad_chunks"]) for k, q in enumerate(got[1]) if q["error"]} == \
+        {k: (v[0], len(v)) for k, v in bad.items()}
+    # the host path over the same bytes agrees, and so does a truncated view
+    assert engine.verify_packets(s, proto, cs, ctype) == got
+    cut = len(s) - 1000
+    assert engine.verify_packets(None, proto, cs, ctype, dptr=p, nbytes=cut) == \
+        oracle.verify_packets(s[:cut], proto, cs, ctype)
+    # max_pkts stops the walk early exactly like the host path
+    assert engine.verify_packets(None, proto, cs, ctype, max_pkts=37, dptr=p, nbytes=len(s)) == \
+        engine.verify_packets(s, proto, cs, ctype, max_pkts=37)
+    keep.free()
