@@ -193,6 +193,10 @@ bool device_accessible(const void *p) {
   return a.devicePointer != nullptr;
 }
 
+// HDFS_CRC32C_SMALL_RULE=0 (experiments): keep schedule 3 for small launches
+// and tables of small segments.
+static const int g_small_rule = env_int("HDFS_CRC32C_SMALL_RULE", 1);
+
 // ctype: 0 = CRC32C, 1 = CRC32 (zlib polynomial) -- selects the table set.
 int launch_all(DevCtx &c, int mode, const SegDev *d_segs, uint32_t nseg, uint64_t rounds,
                uint64_t mtiles, uint64_t gtiles, uint32_t *d_fb, unsigned long long *d_mism,
@@ -211,7 +215,7 @@ int launch_all(DevCtx &c, int mode, const SegDev *d_segs, uint32_t nseg, uint64_
     // tile leaves the current segment: small launches (which also skip the
     // pool) and tables of small segments keep the contiguous slices (2).
     const bool small = rounds < 32ull * 16u * uint64_t(grid) || mtiles < 2ull * uint64_t(grid) * nseg;
-    const int order = (g_tile_order == 3 && small) ? 2 : g_tile_order;
+    const int order = (g_tile_order == 3 && small && g_small_rule) ? 2 : g_tile_order;
     // store policy 4 (diagnostic): verify plans run the load-only twin
     const int kmode = (mode == kModeVerify && g_store_policy == 4) ? int(kModeLoadOnly) : mode;
     HIPCHK(launch_tiles(kmode, order, g_nt_loads, g_depth, g_streams, g_block, grid, d_segs, nseg, rounds, mtiles,

@@ -222,6 +222,8 @@ DEV bool ticket_tile(const Sched &w, uint32_t t, uint64_t &g) {
   return g < w.ntiles;
 }
 
+constexpr uint64_t kWalkTiles = 64;  // forward hops of up to this many tiles walk the table
+
 // Global tile g -> (segment, tile), walking forward from segment s.
 DEV Cursor locate(SegP segs, uint32_t s, uint64_t g) {
   while (g >= segs[s].mtile_start + segs[s].main_tiles) s++;
@@ -243,9 +245,12 @@ DEV Cursor advance(Cursor c, SegP segs, uint32_t nseg, const Sched &w) {
       c.valid = false;
       return c;
     }
-    if ((ORDER == 2 && g < segs[c.seg].mtile_start) ||  // pool tiles may lie behind the slice
-        (ORDER == 3 && (g < segs[c.seg].mtile_start ||   // interleaved tiles jump G ahead
-                        g >= segs[c.seg].mtile_start + segs[c.seg].main_tiles))) {
+    // Pool tiles may lie behind the slice or far ahead of it (a table of
+    // thousands of packet-sized segments: a forward walk from the slice to
+    // the pool cost 8x the whole kernel, tools/exp_packet_tables.py);
+    // interleaved tiles jump G ahead.  Short hops walk, long ones search.
+    const uint64_t end = segs[c.seg].mtile_start + segs[c.seg].main_tiles;
+    if (g < segs[c.seg].mtile_start || g >= end + (ORDER == 3 ? 0u : kWalkTiles)) {
       uint32_t lo = 0, hi = nseg;
       while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;

@@ -169,8 +169,9 @@ typedef struct hdfs_crc32c_packet {
 	uint8_t reserved[6];
 } hdfs_crc32c_packet;
 
-/* Framing only, on the host (no device work): walks up to max_pkts packets
- * of the HOST stream, applying the checks of src/datanode.c:2428-2456
+/* Framing only: walks up to max_pkts packets of the stream (host memory:
+ * no device work; device memory: the headers are read through
+ * header-window copies), applying the checks of src/datanode.c:2428-2456
  * (PACKET_SIZE, CRC_LEN, UNEXPECTED_CRC_LEN, empty non-last packet) and the
  * header decode (INVALID_PACKETHEADERPROTO).  The walk stops after a framing
  * error (recorded in that packet's .error), after an empty last packet (end
@@ -180,9 +181,9 @@ typedef struct hdfs_crc32c_packet {
 int hdfs_crc32c_parse_packets(const void *stream, uint64_t len, int proto, uint32_t chunk_size,
     int ctype, hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts, uint64_t *consumed);
 /* Framing as above, then every chunk of every framing-clean packet verified
- * on the GPU (_verify_crcdata, src/datanode.c:2931-2963): the stream goes
+ * on the GPU (_verify_crcdata, src/datanode.c:2931-2963): a host stream goes
  * H2D once in pieces overlapped with a de-framing gather kernel and the
- * verify kernels.  Per packet: .error = BAD_CHECKSUM, .first_bad,
+ * verify kernels; a device-resident stream is verified in place.  Per packet: .error = BAD_CHECKSUM, .first_bad,
  * .bad_chunks.  Returns the first error in stream order (what the reference
  * returns from its packet loop), 0, or a negative status. */
 int hdfs_crc32c_verify_packets(const void *stream, uint64_t len, int proto, uint32_t chunk_size,
