@@ -81,10 +81,13 @@ def cpu_baseline(sample_gib):
     data = o.splitmix(nbytes // 8, 0, 0).view("uint8")
     gen_s = time.time() - t0
     if have_reference():
-        ext = Reference().sse42_addr
+        ref = Reference()
+        ext = ref.sse42_addr
         kind, fn, label = "reference", "ext", "_hdfs_sse42_crc32c (src/crc32c_sse42.c built from /root/reference)"
+        sw_ext, sw_fn, sw_label = ctypes.cast(ref.sw_fn, ctypes.c_void_p).value, "ext", "_hdfs_sw_crc32c (reference)"
     else:
         ext, kind, fn, label = None, "port", "hw", "oracle SSE4.2 3-way restatement"
+        sw_ext, sw_fn, sw_label = None, "sw", "oracle slicing-by-8 restatement"
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
     s1, crc1 = o.bench_chunks(data, 512, 1, fn, ext)
     passes = 8
@@ -94,6 +97,9 @@ def cpu_baseline(sample_gib):
         tn += s
     # cross-check one block against the pinned digest
     dig = o.crc32c(0, crc1[: BLOCK // 512].view("uint8"), "hw")
+    # block 0 through the slicing-by-8 SW backend, one core
+    s_sw, crc_sw = o.bench_chunks(data[:BLOCK], 512, 1, sw_fn, sw_ext)
+    dig_sw = o.crc32c(0, crc_sw.view("uint8"), "hw")
     model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -114,6 +120,9 @@ def cpu_baseline(sample_gib):
         "cpu_model": model or platform.processor(),
         "nproc": os.cpu_count(),
         "digest_ok": dig == PINNED[(0, 512)],
+        "c1_sw_single_core": {"value": round(BLOCK / (1 << 30) / s_sw, 3), "unit": "GiB/s", "sample":
+                              f"{sw_label}; block 0 (128 MiB), 512 B chunks, 1 thread",
+                              "digest_ok": dig_sw == PINNED[(0, 512)]},
         "datagen_s": round(gen_s, 2),
     }
 
