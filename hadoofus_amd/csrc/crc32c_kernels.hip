@@ -133,6 +133,24 @@ DEV SegHot seg_hot(SegP segs, uint32_t s) {
   return SegHot{p->data, p->crcs, p->bitmap, p->mtile_start, p->chunk_size, p->flags, p->nchunks, p->main_tiles};
 }
 
+// Per-stream copy of the current segment's hot fields (and reg_init), kept
+// in SGPRs across rounds: issue / process / finish / advance of a round
+// re-read the table only when the cursor's segment changed (a wave-uniform
+// compare), instead of s_load + s_waitcnt lgkmcnt(0) several times a round.
+struct SegCache {
+  uint32_t seg;
+  uint32_t reg_init;
+  SegHot h;
+};
+DEV const SegCache &hot(SegCache &k, SegP segs, uint32_t s) {
+  if (s != k.seg) {
+    k.h = seg_hot(segs, s);
+    k.reg_init = segs[s].reg_init;
+    k.seg = s;
+  }
+  return k;
+}
+
 // Wave-uniform position of one round: (segment, tile, round).
 struct Cursor {
   uint32_t seg, tile, r;
@@ -233,9 +251,10 @@ DEV Cursor locate(SegP segs, uint32_t s, uint64_t g) {
 // Next round owned by this wave.  An exhausted cursor keeps its last
 // position (so speculative loads stay in bounds) with valid = false.
 template <int ORDER>
-DEV Cursor advance(Cursor c, SegP segs, uint32_t nseg, const Sched &w) {
+DEV Cursor advance(Cursor c, SegP segs, uint32_t nseg, const Sched &w, SegCache &kc) {
   if (!c.valid) return c;
-  if (c.r + 1 < segs[c.seg].chunk_size / kRoundBytes) {
+  const SegHot &sh = hot(kc, segs, c.seg).h;
+  if (c.r + 1 < sh.chunk_size / kRoundBytes) {
     c.r++;
     return c;
   }
@@ -249,8 +268,8 @@ DEV Cursor advance(Cursor c, SegP segs, uint32_t nseg, const Sched &w) {
     // thousands of packet-sized segments: a forward walk from the slice to
     // the pool cost 8x the whole kernel, tools/exp_packet_tables.py);
     // interleaved tiles jump G ahead.  Short hops walk, long ones search.
-    const uint64_t end = segs[c.seg].mtile_start + segs[c.seg].main_tiles;
-    if (g < segs[c.seg].mtile_start || g >= end + (ORDER == 3 ? 0u : kWalkTiles)) {
+    const uint64_t end = sh.mtile_start + sh.main_tiles;
+    if (g < sh.mtile_start || g >= end + (ORDER == 3 ? 0u : kWalkTiles)) {
       uint32_t lo = 0, hi = nseg;
       while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
@@ -258,6 +277,8 @@ DEV Cursor advance(Cursor c, SegP segs, uint32_t nseg, const Sched &w) {
       }
       return locate(segs, lo, g);
     }
+    if (g < end)  // same segment (the common case): from the cached fields, no table read
+      return Cursor{c.seg, rfl(static_cast<uint32_t>(g - sh.mtile_start)), 0u, true};
     return locate(segs, c.seg, g);
   }
   uint32_t s = c.seg, t = c.tile + 1;
@@ -301,8 +322,8 @@ struct LaneOff {
 
 template <int MODE, int NT, int BUF>
 DEV void issue(uint32_t (&d)[16], uint32_t &exp, const Cursor c, SegP segs, uint32_t hsel, uint32_t loff,
-               uint32_t qg, LaneOff &lo) {
-  const SegHot sh = seg_hot(segs, c.seg);
+               uint32_t qg, LaneOff &lo, SegCache &kc) {
+  const SegHot &sh = hot(kc, segs, c.seg).h;
   const uint32_t cs = sh.chunk_size;
   if constexpr (BUF) {
     // Buffer loads: the round's base in SGPRs, per-lane offsets from the
@@ -365,8 +386,8 @@ struct LaneConst {
 // stay exact.
 template <int MODE>
 DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, uint32_t st, const LaneConst &L,
-                uint32_t *__restrict__ first_bad, unsigned long long *__restrict__ mism) {
-  const SegHot sh = seg_hot(segs, c.seg);
+                uint32_t *__restrict__ first_bad, unsigned long long *__restrict__ mism, SegCache &kc) {
+  const SegHot &sh = hot(kc, segs, c.seg).h;
   const bool last = c.valid && (c.r + 1 == sh.chunk_size / kRoundBytes);
   const uint32_t flags = sh.flags;
   const uint32_t nch = min(kTileChunks, sh.nchunks - c.tile * kTileChunks);
@@ -427,7 +448,7 @@ DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, ui
 template <int MODE, int S>
 DEV void process(const uint32_t *lds, uint32_t (&d)[S][16], const uint32_t (&exp)[S], const Cursor (&c)[S],
                  SegP segs, uint32_t (&st)[S], const LaneConst &L, uint32_t *__restrict__ first_bad,
-                 unsigned long long *__restrict__ mism) {
+                 unsigned long long *__restrict__ mism, SegCache (&kc)[S]) {
   if constexpr (MODE == kModeLoadOnly) {
 #pragma unroll
     for (int s = 0; s < S; s++) {
@@ -447,7 +468,8 @@ DEV void process(const uint32_t *lds, uint32_t (&d)[S][16], const uint32_t (&exp
 #pragma unroll
   for (int s = 0; s < S; s++) {
     transpose(d[s]);
-    if (c[s].r == 0) st[s] = (L.qi == 0) ? segs[c[s].seg].reg_init : 0u;
+    const uint32_t ri = hot(kc[s], segs, c[s].seg).reg_init;  // uniform control flow: kc stays in SGPRs
+    if (c[s].r == 0) st[s] = (L.qi == 0) ? ri : 0u;
     else st[s] = zshift(lds, L.z448, st[s]);
     x[s] = st[s] ^ d[s][0];
   }
@@ -459,7 +481,7 @@ DEV void process(const uint32_t *lds, uint32_t (&d)[S][16], const uint32_t (&exp
 #pragma unroll
   for (int s = 0; s < S; s++) st[s] = slice4(lds, x[s], 0u, L.lb0, L.lb1);
 #pragma unroll
-  for (int s = 0; s < S; s++) finish<MODE>(lds, exp[s], c[s], segs, st[s], L, first_bad, mism);
+  for (int s = 0; s < S; s++) finish<MODE>(lds, exp[s], c[s], segs, st[s], L, first_bad, mism, kc[s]);
 }
 
 // Tiled kernel.  MODE compute / verify; ORDER schedule (above); NT
@@ -620,32 +642,36 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
   uint32_t ex[DEPTH][S];
   uint32_t st[S];
   LaneOff lo{0u, {0u, 0u, 0u, 0u}};
+  SegCache kc[S];
 #pragma unroll
-  for (int s = 0; s < S; s++) st[s] = 0u;
+  for (int s = 0; s < S; s++) {
+    st[s] = 0u;
+    kc[s].seg = 0xFFFFFFFFu;
+  }
 #pragma unroll
   for (int k = 1; k < DEPTH; k++) {
 #pragma unroll
-    for (int s = 0; s < S; s++) cur[k][s] = advance<ORDER>(cur[k - 1][s], sg, nseg, w);
+    for (int s = 0; s < S; s++) cur[k][s] = advance<ORDER>(cur[k - 1][s], sg, nseg, w, kc[s]);
   }
 #pragma unroll
   for (int k = 0; k < DEPTH; k++) {
 #pragma unroll
     for (int s = 0; s < S; s++) {
       ex[k][s] = 0u;
-      issue<MODE, NT, BUF>(buf[k][s], ex[k][s], cur[k][s], sg, L.hsel, L.loff, L.qg, lo);
+      issue<MODE, NT, BUF>(buf[k][s], ex[k][s], cur[k][s], sg, L.hsel, L.loff, L.qg, lo, kc[s]);
     }
   }
   for (;;) {
 #pragma unroll
     for (int k = 0; k < DEPTH; k++) {
-      process<MODE, S>(lds, buf[k], ex[k], cur[k], sg, st, L, first_bad, mism);
+      process<MODE, S>(lds, buf[k], ex[k], cur[k], sg, st, L, first_bad, mism, kc);
 #pragma unroll
       for (int s = 0; s < S; s++) nrounds += cur[k][s].valid ? 1u : 0u;
       const int prev = (k + DEPTH - 1) % DEPTH;
 #pragma unroll
       for (int s = 0; s < S; s++) {
-        cur[k][s] = advance<ORDER>(cur[prev][s], sg, nseg, w);
-        issue<MODE, NT, BUF>(buf[k][s], ex[k][s], cur[k][s], sg, L.hsel, L.loff, L.qg, lo);
+        cur[k][s] = advance<ORDER>(cur[prev][s], sg, nseg, w, kc[s]);
+        issue<MODE, NT, BUF>(buf[k][s], ex[k][s], cur[k][s], sg, L.hsel, L.loff, L.qg, lo, kc[s]);
       }
     }
     bool more = false;
