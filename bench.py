@@ -89,16 +89,25 @@ def cpu_baseline(sample_gib):
         ext, kind, fn, label = None, "port", "hw", "oracle SSE4.2 3-way restatement"
         sw_ext, sw_fn, sw_label = None, "sw", "oracle slicing-by-8 restatement"
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    s1, crc1 = o.bench_chunks(data, 512, 1, fn, ext)
-    passes = 8
-    tn = 0.0
-    for _ in range(passes):
-        s, _ = o.bench_chunks(data, 512, threads, fn, ext)
-        tn += s
+
+    def timed_passes(fn_, ext_, buf, nthreads, budget_s):
+        # whole passes over buf until budget_s of timed work (>= 1 pass)
+        tot, k, first = 0.0, 0, None
+        while k == 0 or tot < budget_s:
+            s, crcs = o.bench_chunks(buf, 512, nthreads, fn_, ext_)
+            first = crcs if first is None else first
+            tot += s
+            k += 1
+        return tot / k, k, first
+
+    # a bounded sample, ~10 s of wall time in all (task: 10-30 s of CPU work)
+    s1, passes1, crc1 = timed_passes(fn, ext, data, 1, 3.0)
+    sn, passes, _ = timed_passes(fn, ext, data, threads, 5.0)
+    tn = sn * passes
     # cross-check one block against the pinned digest
     dig = o.crc32c(0, crc1[: BLOCK // 512].view("uint8"), "hw")
     # block 0 through the slicing-by-8 SW backend, one core
-    s_sw, crc_sw = o.bench_chunks(data[:BLOCK], 512, 1, sw_fn, sw_ext)
+    s_sw, passes_sw, crc_sw = timed_passes(sw_fn, sw_ext, data[:BLOCK], 1, 1.0)
     dig_sw = o.crc32c(0, crc_sw.view("uint8"), "hw")
     model = ""
     try:
@@ -115,13 +124,13 @@ def cpu_baseline(sample_gib):
         "cores": threads,
         "kind": kind,
         "sample": f"{label}; per-512B-chunk CRCs over {gib:.0f} GiB splitmix64 (blocks 0..{nbytes // BLOCK - 1}), "
-                  f"{threads} threads x {passes} passes; single core {gib / s1:.2f} GiB/s",
+                  f"{threads} threads x {passes} passes; single core {gib / s1:.2f} GiB/s ({passes1} passes)",
         "single_core_value": round(gib / s1, 3),
         "cpu_model": model or platform.processor(),
         "nproc": os.cpu_count(),
         "digest_ok": dig == PINNED[(0, 512)],
         "c1_sw_single_core": {"value": round(BLOCK / (1 << 30) / s_sw, 3), "unit": "GiB/s", "sample":
-                              f"{sw_label}; block 0 (128 MiB), 512 B chunks, 1 thread",
+                              f"{sw_label}; block 0 (128 MiB), 512 B chunks, 1 thread, {passes_sw} passes",
                               "digest_ok": dig_sw == PINNED[(0, 512)]},
         "datagen_s": round(gen_s, 2),
     }

@@ -183,7 +183,8 @@ int hdfs_crc32c_parse_packets(const void *stream, uint64_t len, int proto, uint3
 /* Framing as above, then every chunk of every framing-clean packet verified
  * on the GPU (_verify_crcdata, src/datanode.c:2931-2963): a host stream goes
  * H2D once in pieces overlapped with a de-framing gather kernel and the
- * verify kernels; a device-resident stream is verified in place.  Per packet: .error = BAD_CHECKSUM, .first_bad,
+ * verify kernels; a device-resident stream is verified in place (its bytes
+ * must be complete: the caller synchronises whatever wrote them).  Per packet: .error = BAD_CHECKSUM, .first_bad,
  * .bad_chunks.  Returns the first error in stream order (what the reference
  * returns from its packet loop), 0, or a negative status. */
 int hdfs_crc32c_verify_packets(const void *stream, uint64_t len, int proto, uint32_t chunk_size,
