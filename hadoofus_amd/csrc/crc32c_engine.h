@@ -7,6 +7,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <mutex>
+#include <vector>
 
 #include "crc32c_internal.h"
 #include "hadoofus_crc32c.h"
@@ -120,8 +121,12 @@ struct DevCtx {
   // rows + pinned host copy) and the verify tables (segs | first-bad | bitmaps)
   uint8_t *w_dev = nullptr, *w_host = nullptr;
   uint32_t w_cap = 0;  // rows
-  uint8_t *v_meta = nullptr;
-  size_t v_meta_cap = 0;
+  struct VBatch {
+    uint8_t *h = nullptr, *d = nullptr;  // pinned / device tables of one verify batch
+    size_t hcap = 0, dcap = 0;
+  };
+  std::vector<VBatch> v_batch;
+  hipStream_t v_stream = nullptr;
   std::mutex mu;
 };
 

@@ -23,6 +23,8 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <vector>
@@ -408,12 +410,14 @@ int first_error(const hdfs_crc32c_packet *p, size_t n) {
 // empty packet, a stream of mixed sizes) starts a new window at its offset;
 // the window length grows while windows keep hitting and drops back after a
 // miss, so an irregular stream does not pay for rows it never reads.
+static const bool g_dstream_trace = std::getenv("HDFS_CRC32C_DSTREAM_TRACE") != nullptr;
+
 struct HeaderWindows {
   DevCtx &c;
   const uint8_t *d;
   uint64_t len;
   uint64_t base = 0, stride = 0;
-  uint32_t count = 0, used = 0, budget = 8192;
+  uint32_t count = 0, used = 0, budget = 8192, nfetch = 0;
 
   const uint8_t *lookup(uint64_t pos) {
     if (!count || pos < base) return nullptr;
@@ -447,84 +451,55 @@ struct HeaderWindows {
     base = pos;
     stride = stride_guess;
     count = uint32_t(n);
+    nfetch++;
     used = 0;
     return HDFS_CRC32C_OK;
   }
 };
 
-// Framing walk over device memory (same records and stopping rules as
-// parse_packet_stream).  Caller holds c.mu.
-int parse_device_stream(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs, int ctype,
-                        size_t max_pkts, std::vector<hdfs_crc32c_packet> &out, uint64_t *consumed) {
-  out.clear();
-  *consumed = 0;
-  HeaderWindows w{c, d, len};
-  std::vector<uint8_t> big;  // v2 headers longer than a window row
-  uint64_t pos = 0, stride = 0;
-  while (out.size() < max_pkts && pos < len) {
-    const uint8_t *p = w.lookup(pos);
-    if (!p) {
-      int rc = w.fetch(pos, stride, max_pkts - out.size());
-      if (rc) return rc;
-      p = w.lookup(pos);
-    }
-    if (proto == HDFS_CRC32C_PROTO_V2 && len - pos >= 6) {
-      const uint64_t need = 6 + ((uint64_t(p[4]) << 8) | p[5]);
-      if (need > kHdrWin && len - pos >= need) {
-        big.resize(need);
-        HIPCHK(hipMemcpy(big.data(), d + pos, need, hipMemcpyDeviceToHost));
-        p = big.data();
-      }
-    }
-    hdfs_crc32c_packet k;
-    uint64_t total = 0;
-    const int st = frame_step(p, len - pos, pos, proto, cs, ctype, k, total);
-    if (st == kStepMore) break;
-    out.push_back(k);
-    if (st == kStepStop) {
-      if (!k.error) *consumed = pos + total;
-      break;
-    }
-    pos += total;
-    stride = total;
-    *consumed = pos;
-  }
-  return HDFS_CRC32C_OK;
-}
-
-// Verify of a device-resident stream: no copies and no de-framing gather --
-// every framing-clean packet is one verify segment pointing into the stream
-// itself (CRCs at stream_off + header_len, data right after them; the tiled
-// kernel takes both at any byte offset), all of them in one launch.
-int verify_device_stream(DevCtx &c, const uint8_t *d, std::vector<hdfs_crc32c_packet> &recs,
-                         const std::vector<size_t> &vidx, uint32_t cs, int ctype) {
+// One verify launch over packets vidx[v0, v1) of a device-resident stream:
+// no copies and no de-framing gather -- every packet is one verify segment
+// pointing into the stream itself (CRCs at stream_off + header_len, data
+// right after them; the tiled kernel takes both at any byte offset).  Tables
+// go H2D, results D2H, all on c.v_stream, asynchronously: the framing walk
+// keeps reading header windows (on c.stream) while earlier batches verify.
+struct DevBatch {
+  size_t v0 = 0, v1 = 0;
   PieceLayout L;
-  L.n = vidx.size();
-  for (size_t i : vidx) L.bm += (uint64_t(recs[i].crc_len) / 4 + 7) / 8;
+};
+
+int submit_device_batch(DevCtx &c, const uint8_t *d, const std::vector<hdfs_crc32c_packet> &recs,
+                        const std::vector<size_t> &vidx, size_t bi, DevBatch &b, uint32_t cs, int ctype) {
+  PieceLayout &L = b.L;
+  L = PieceLayout{};
+  L.n = b.v1 - b.v0;
+  for (size_t v = b.v0; v < b.v1; v++) L.bm += (uint64_t(recs[vidx[v]].crc_len) / 4 + 7) / 8;
   L.off_segs = 0;
   L.off_fb = align_up(L.n * sizeof(SegDev), 256);
   L.off_bm = L.off_fb + align_up(L.n * 4, 256);
   L.meta = L.off_bm + align_up(L.bm, 256);
-  if (L.meta > c.k_hmeta_cap) {
-    if (c.k_hmeta) HIPCHK(hipHostFree(c.k_hmeta));
-    c.k_hmeta = nullptr;
-    c.k_hmeta_cap = 0;
-    HIPCHK(hipHostMalloc(&c.k_hmeta, L.meta, hipHostMallocDefault));
-    c.k_hmeta_cap = L.meta;
+  if (bi >= c.v_batch.size()) c.v_batch.resize(bi + 1);
+  DevCtx::VBatch &vb = c.v_batch[bi];  // previous user: an earlier call, synchronised at its end
+  if (L.meta > vb.hcap) {
+    if (vb.h) HIPCHK(hipHostFree(vb.h));
+    vb.h = nullptr;
+    vb.hcap = 0;
+    HIPCHK(hipHostMalloc(&vb.h, L.meta, hipHostMallocDefault));
+    vb.hcap = L.meta;
   }
-  if (L.meta + 64 > c.v_meta_cap) {
-    if (c.v_meta) HIPCHK(hipFree(c.v_meta));
-    c.v_meta = nullptr;
-    c.v_meta_cap = 0;
-    HIPCHK(hipMalloc(&c.v_meta, L.meta + 64));
-    c.v_meta_cap = L.meta + 64;
+  if (L.meta + 64 > vb.dcap) {
+    if (vb.d) HIPCHK(hipFree(vb.d));
+    vb.d = nullptr;
+    vb.dcap = 0;
+    HIPCHK(hipMalloc(&vb.d, L.meta + 64));
+    vb.dcap = L.meta + 64;
   }
-  uint8_t *hm = c.k_hmeta, *dm = c.v_meta;
+  uint8_t *hm = vb.h, *dm = vb.d;
   auto *hs = reinterpret_cast<SegDev *>(hm);
   const uint32_t sflags = HDFS_CRC32C_SEG_BE | (ctype == HDFS_CRC32C_CSUM_CRC32 ? HDFS_CRC32C_SEG_CRC32 : 0u);
   uint64_t boff = 0;
   for (size_t v = 0; v < L.n; v++) {
-    const hdfs_crc32c_packet &k = recs[vidx[v]];
+    const hdfs_crc32c_packet &k = recs[vidx[b.v0 + v]];
     const uint8_t *crcp = d + wire_begin(k);
     hdfs_crc32c_segment in = {crcp + k.crc_len, uint64_t(k.data_len), cs, sflags, 0, 0,
                               const_cast<uint8_t *>(crcp), dm + L.off_bm + boff};
@@ -536,14 +511,103 @@ int verify_device_stream(DevCtx &c, const uint8_t *d, std::vector<hdfs_crc32c_pa
   // the pool counter and mismatch word live past the tables
   auto *gctr = reinterpret_cast<uint32_t *>(dm + L.meta);
   auto *mism = reinterpret_cast<unsigned long long *>(dm + L.meta + 8);
-  HIPCHK(hipMemcpyAsync(dm, hm, L.off_fb, hipMemcpyHostToDevice, c.stream));
+  HIPCHK(hipMemcpyAsync(dm, hm, L.off_fb, hipMemcpyHostToDevice, c.v_stream));
   int rc = launch_all(c, kModeVerify, reinterpret_cast<const SegDev *>(dm), uint32_t(L.n), L.rounds, L.mtiles,
-                      L.gtiles, reinterpret_cast<uint32_t *>(dm + L.off_fb), mism, gctr, c.stream, nullptr, nullptr,
-                      true, ctype == HDFS_CRC32C_CSUM_CRC32 ? 1 : 0);
+                      L.gtiles, reinterpret_cast<uint32_t *>(dm + L.off_fb), mism, gctr, c.v_stream, nullptr,
+                      nullptr, true, ctype == HDFS_CRC32C_CSUM_CRC32 ? 1 : 0);
   if (rc) return rc;
-  HIPCHK(hipMemcpyAsync(hm + L.off_fb, dm + L.off_fb, L.meta - L.off_fb, hipMemcpyDeviceToHost, c.stream));
-  HIPCHK(hipStreamSynchronize(c.stream));
-  finish_piece(recs.data(), vidx.data(), L, hm);
+  HIPCHK(hipMemcpyAsync(hm + L.off_fb, dm + L.off_fb, L.meta - L.off_fb, hipMemcpyDeviceToHost, c.v_stream));
+  return HDFS_CRC32C_OK;
+}
+
+// Framing walk over device memory (same records and stopping rules as
+// parse_packet_stream), verifying as it goes when `verify`: framing-clean
+// packets with CRCs are submitted in batches of 1 024 growing to 4 096
+// packets (the first launch starts early; later ones amortise the launch),
+// overlapped with the rest of the walk.  Caller holds c.mu.
+int walk_device_stream(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs, int ctype,
+                       size_t max_pkts, bool verify, std::vector<hdfs_crc32c_packet> &out, uint64_t *consumed) {
+  out.clear();
+  *consumed = 0;
+  verify = verify && ctype != HDFS_CRC32C_CSUM_NULL;
+  if (verify && !c.v_stream) HIPCHK(hipStreamCreateWithFlags(&c.v_stream, hipStreamNonBlocking));
+  HeaderWindows w{c, d, len};
+  std::vector<uint8_t> big;  // v2 headers longer than a window row
+  std::vector<size_t> vidx;  // packets to verify
+  std::vector<DevBatch> batches;
+  size_t batch_cap = 1024, v_sub = 0;
+  auto submit = [&]() -> int {
+    DevBatch b;
+    b.v0 = v_sub;
+    b.v1 = vidx.size();
+    v_sub = b.v1;
+    batches.push_back(b);
+    return submit_device_batch(c, d, out, vidx, batches.size() - 1, batches.back(), cs, ctype);
+  };
+  uint64_t pos = 0, stride = 0;
+  int rc = HDFS_CRC32C_OK;
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
+  double t_submit = 0;
+  while (out.size() < max_pkts && pos < len) {
+    const uint8_t *p = w.lookup(pos);
+    if (!p) {
+      if ((rc = w.fetch(pos, stride, max_pkts - out.size()))) break;
+      p = w.lookup(pos);
+    }
+    if (proto == HDFS_CRC32C_PROTO_V2 && len - pos >= 6) {
+      const uint64_t need = 6 + ((uint64_t(p[4]) << 8) | p[5]);
+      if (need > kHdrWin && len - pos >= need) {
+        big.resize(need);
+        hipError_t e = hipMemcpy(big.data(), d + pos, need, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) {
+          rc = fail(HDFS_CRC32C_EHIP, "header copy: %s", hipGetErrorString(e));
+          break;
+        }
+        p = big.data();
+      }
+    }
+    hdfs_crc32c_packet k;
+    uint64_t total = 0;
+    const int st = frame_step(p, len - pos, pos, proto, cs, ctype, k, total);
+    if (st == kStepMore) break;
+    out.push_back(k);
+    if (verify && !k.error && k.crc_len > 0) {
+      vidx.push_back(out.size() - 1);
+      if (vidx.size() - v_sub >= batch_cap) {
+        const auto ts = clk::now();
+        rc = submit();
+        t_submit += std::chrono::duration<double, std::micro>(clk::now() - ts).count();
+        if (rc) break;
+        batch_cap = std::min<size_t>(batch_cap * 2, 4096);
+      }
+    }
+    if (st == kStepStop) {
+      if (!k.error) *consumed = pos + total;
+      break;
+    }
+    pos += total;
+    stride = total;
+    *consumed = pos;
+  }
+  const auto t1 = clk::now();
+  if (!rc && vidx.size() > v_sub) rc = submit();
+  const auto t2 = clk::now();
+  if (!batches.empty()) {
+    // drain the batches already queued even after an error (their tables
+    // and results live in this context's buffers)
+    hipError_t e = hipStreamSynchronize(c.v_stream);
+    if (!rc && e != hipSuccess) rc = fail(HDFS_CRC32C_EHIP, "verify: %s", hipGetErrorString(e));
+  }
+  if (g_dstream_trace) {  // diagnostic: where a device-stream call spends its time (us)
+    const auto t3 = clk::now();
+    auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+    std::fprintf(stderr, "dstream pkts=%zu batches=%zu windows=%u walk_us=%.1f (submit %.1f) last_submit_us=%.1f drain_us=%.1f\n",
+                 out.size(), batches.size(), w.nfetch, us(t0, t1), t_submit, us(t1, t2), us(t2, t3));
+  }
+  if (rc) return rc;
+  for (size_t bi = 0; bi < batches.size(); bi++)
+    finish_piece(out.data(), vidx.data() + batches[bi].v0, batches[bi].L, c.v_batch[bi].h);
   return HDFS_CRC32C_OK;
 }
 
@@ -566,12 +630,7 @@ int verify_packets_dev_impl(int dev, const uint8_t *stream, uint64_t len, int pr
   std::lock_guard<std::mutex> lk(c.mu);
   std::vector<hdfs_crc32c_packet> recs;
   uint64_t used = 0;
-  if ((rc = parse_device_stream(c, stream, len, proto, cs, ctype, max_pkts, recs, &used))) return rc;
-  std::vector<size_t> vidx;
-  if (verify && ctype != HDFS_CRC32C_CSUM_NULL)
-    for (size_t i = 0; i < recs.size(); i++)
-      if (!recs[i].error && recs[i].crc_len > 0) vidx.push_back(i);
-  if (!vidx.empty() && (rc = verify_device_stream(c, stream, recs, vidx, cs, ctype))) return rc;
+  if ((rc = walk_device_stream(c, stream, len, proto, cs, ctype, max_pkts, verify, recs, &used))) return rc;
   if (!recs.empty()) std::memcpy(pkts, recs.data(), recs.size() * sizeof(hdfs_crc32c_packet));
   if (npkts) *npkts = recs.size();
   if (consumed) *consumed = used;
