@@ -404,3 +404,23 @@ def test_dropin_concurrent_threads(engine, oracle):
         th.join(timeout=120)
     assert not any(th.is_alive() for th in ths)
     assert not errors, errors[:5]
+
+
+def test_dropin_max_len(engine, oracle):
+    """`unsigned len` at its maximum, 2^32 - 1 bytes (one call
+    caps at 4 GiB - 1; src/crc32c.h:13), through the three drop-in symbols on
+    device pointers (aligned, and odd with a chained non-zero crc) and on host
+    memory, against the oracle's SSE4.2 restatement on the same splitmix64 data."""
+    n = (1 << 32) - 1
+    host = oracle.splitmix(1 << 29, seed=3).view(np.uint8)
+    want0 = oracle.crc32c(0, host[:n], "hw")
+    want1 = oracle.crc32c(0xDEADBEEF, host[1:], "hw")
+    dbuf = engine.DeviceBuffer(1 << 32)
+    engine.fill_splitmix64(dbuf.ptr, 1 << 29, 3, 0)
+    lib = engine.load()
+    for entry in ("_hdfs_crc32c", "_hdfs_sse42_crc32c", "_hdfs_sw_crc32c"):
+        f = getattr(lib, entry)
+        assert f(0, dbuf.ptr, n) == want0, entry
+        assert f(0xDEADBEEF, dbuf.ptr + 1, n) == want1, entry
+    assert engine.crc32c(0, host[:n]) == want0
+    assert engine.crc32c(0xDEADBEEF, host[1:]) == want1
