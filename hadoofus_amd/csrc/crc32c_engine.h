@@ -37,8 +37,10 @@ hipError_t launch_small_chunks(int mode, const uint8_t *p, uint32_t len, uint32_
 hipError_t launch_prep(uint32_t *fb, uint32_t nfb, unsigned long long *mism, uint32_t *gctr, hipStream_t stream);
 hipError_t launch_gather(const uint8_t *raw, const PktDesc *descs, uint32_t npk, uint32_t units, uint8_t *arena,
                          uint8_t *crc_arena, hipStream_t stream);
+// proto 1 / 2: derive the stride from the packet at base (v1 / v2 header)
+// and store it in *stride_out; proto 0: rows at the given stride.
 hipError_t launch_header_window(const uint8_t *s, uint64_t len, uint64_t base, uint64_t stride, uint32_t count,
-                                uint8_t *out, hipStream_t stream);
+                                int proto, uint8_t *out, uint64_t *stride_out, hipStream_t stream);
 
 // ---- errors ----
 extern thread_local char g_err[512];

@@ -1105,11 +1105,26 @@ hipError_t launch_gather(const uint8_t *raw, const PktDesc *descs, uint32_t npk,
 // each header with its own copy; for the fixed-size packets of a block
 // transfer one window covers the whole stream.  One thread per dword of a
 // row; byte loads because the rows sit at any byte offset.
+// proto != 0 (first window of a walk, stride unknown to the host): the
+// stride is the wire size of the packet at base, header_len + plen - 4 as
+// frame_step computes it (v1 header 25 B, v2 6 + hlen), and thread 0 writes
+// it to *stride_out.  A wrong guess (a malformed first packet) costs nothing
+// but the window: every row holds the real bytes at its address, and the
+// host only reads a row whose address the walk reaches.
 __global__ __launch_bounds__(256) void header_window_kernel(const uint8_t *__restrict__ s, uint64_t len,
                                                             uint64_t base, uint64_t stride, uint32_t count,
-                                                            uint32_t *__restrict__ out) {
+                                                            int proto, uint32_t *__restrict__ out,
+                                                            uint64_t *__restrict__ stride_out) {
   const uint32_t t = blockIdx.x * 256u + threadIdx.x;
   constexpr uint32_t kWords = kHdrWin / 4;
+  if (proto) {
+    auto at0 = [&](uint64_t i) -> uint32_t { return base + i < len ? uint32_t(s[base + i]) : 0u; };
+    const int32_t plen = int32_t((at0(0) << 24) | (at0(1) << 16) | (at0(2) << 8) | at0(3));
+    const int64_t hl = proto == 2 ? 6 + int64_t((at0(4) << 8) | at0(5)) : 25;
+    const int64_t tot = hl + int64_t(plen) - 4;
+    stride = tot > 0 ? uint64_t(tot) : 0;
+    if (t == 0) *stride_out = stride;
+  }
   if (t >= count * kWords) return;
   const uint64_t at = base + uint64_t(t / kWords) * stride + 4ull * (t % kWords);
   uint32_t w = 0;
@@ -1120,11 +1135,12 @@ __global__ __launch_bounds__(256) void header_window_kernel(const uint8_t *__res
 }
 
 hipError_t launch_header_window(const uint8_t *s, uint64_t len, uint64_t base, uint64_t stride, uint32_t count,
-                                uint8_t *out, hipStream_t stream) {
+                                int proto, uint8_t *out, uint64_t *stride_out, hipStream_t stream) {
   if (!count) return hipSuccess;
+  if (proto && !stride_out) return hipErrorInvalidValue;
   const uint32_t threads = count * (kHdrWin / 4);
   hipLaunchKernelGGL(header_window_kernel, dim3((threads + 255) / 256), dim3(256), 0, stream, s, len, base, stride,
-                     count, reinterpret_cast<uint32_t *>(out));
+                     count, proto, reinterpret_cast<uint32_t *>(out), stride_out);
   return hipGetLastError();
 }
 

@@ -403,10 +403,10 @@ int first_error(const hdfs_crc32c_packet *p, size_t n) {
 // ---- device-resident packet streams ----
 // The framing walk needs ~30 header bytes per packet from a stream the host
 // cannot read.  It asks header_window_kernel for rows of kHdrWin bytes at
-// base + k * stride, where stride is the size of the packet just framed:
+// base + k * stride, where stride is the size of the packet just framed
+// (for a walk's first window the kernel reads it from the first header):
 // the fixed-size packets of a block transfer all land on that grid, so a
-// regular stream costs two small D2H round trips (first header, then one
-// window over the rest).  A packet off the grid (a short tail, a trailing
+// regular stream of up to 8 192 packets costs one small D2H round trip.  A packet off the grid (a short tail, a trailing
 // empty packet, a stream of mixed sizes) starts a new window at its offset;
 // the window length grows while windows keep hitting and drops back after a
 // miss, so an irregular stream does not pay for rows it never reads.
@@ -416,6 +416,7 @@ struct HeaderWindows {
   DevCtx &c;
   const uint8_t *d;
   uint64_t len;
+  int proto;
   uint64_t base = 0, stride = 0;
   uint32_t count = 0, used = 0, budget = 8192, nfetch = 0;
 
@@ -431,12 +432,15 @@ struct HeaderWindows {
   int fetch(uint64_t pos, uint64_t stride_guess, size_t rows_left) {
     constexpr uint32_t kMaxRows = 1u << 16;  // 4 MiB of rows per window
     if (count) budget = (used * 2 >= count) ? std::min(kMaxRows, budget * 8) : 64;
-    uint64_t n = stride_guess ? (len - pos) / stride_guess + 1 : 1;
+    // no stride yet: the kernel takes it from the header at pos; size the
+    // window for packets of >= 4 KiB (block transfers send 64 KiB ones)
+    const int sproto = stride_guess ? 0 : proto;
+    uint64_t n = (len - pos) / (stride_guess ? stride_guess : 4096) + 1;
     n = std::min<uint64_t>({n, rows_left, budget});
     if (n == 0) n = 1;
-    if (n > c.w_cap) {
+    if (n + 1 > c.w_cap) {  // + 1 row: the derived stride
       uint32_t cap = 1024;
-      while (cap < n) cap *= 2;
+      while (cap < n + 1) cap *= 2;
       if (c.w_dev) HIPCHK(hipFree(c.w_dev));
       if (c.w_host) HIPCHK(hipHostFree(c.w_host));
       c.w_dev = c.w_host = nullptr;
@@ -445,11 +449,14 @@ struct HeaderWindows {
       HIPCHK(hipHostMalloc(&c.w_host, size_t(cap) * kHdrWin, hipHostMallocDefault));
       c.w_cap = cap;
     }
-    HIPCHK(launch_header_window(d, len, pos, stride_guess, uint32_t(n), c.w_dev, c.stream));
-    HIPCHK(hipMemcpyAsync(c.w_host, c.w_dev, size_t(n) * kHdrWin, hipMemcpyDeviceToHost, c.stream));
+    auto *sdev = reinterpret_cast<uint64_t *>(c.w_dev + size_t(n) * kHdrWin);
+    HIPCHK(launch_header_window(d, len, pos, stride_guess, uint32_t(n), sproto, c.w_dev, sdev, c.stream));
+    HIPCHK(hipMemcpyAsync(c.w_host, c.w_dev, size_t(n) * kHdrWin + (sproto ? 8 : 0), hipMemcpyDeviceToHost,
+                          c.stream));
     HIPCHK(hipStreamSynchronize(c.stream));
     base = pos;
     stride = stride_guess;
+    if (sproto) std::memcpy(&stride, c.w_host + size_t(n) * kHdrWin, 8);
     count = uint32_t(n);
     nfetch++;
     used = 0;
@@ -531,7 +538,7 @@ int walk_device_stream(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uin
   *consumed = 0;
   verify = verify && ctype != HDFS_CRC32C_CSUM_NULL;
   if (verify && !c.v_stream) HIPCHK(hipStreamCreateWithFlags(&c.v_stream, hipStreamNonBlocking));
-  HeaderWindows w{c, d, len};
+  HeaderWindows w{c, d, len, proto};
   std::vector<uint8_t> big;  // v2 headers longer than a window row
   std::vector<size_t> vidx;  // packets to verify
   std::vector<DevBatch> batches;
