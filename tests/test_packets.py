@@ -235,3 +235,27 @@ def test_gpu_device_stream_vs_oracle(engine, oracle, proto, cs, ctype, sizes, sh
     assert engine.verify_packets(None, proto, cs, ctype, max_pkts=37, dptr=p, nbytes=len(s)) == \
         engine.verify_packets(s, proto, cs, ctype, max_pkts=37)
     keep.free()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("proto", [1, 2])
+def test_gpu_device_stream_first_window_guess(engine, oracle, proto):
+    """The first header window takes its stride from the first header on the
+    device (header_len + plen - 4).  Wrong guesses -- a first plen that is
+    negative, huge or too small, and streams shorter than a header -- must
+    give exactly the oracle's records (src/datanode.c:2428-2446)."""
+    cs = 512
+    s, _ = build_stream(oracle.crc32c, proto, cs, CSUM_CRC32C, [65536] * 5 + [777], seed=11)
+    cases = [s[:n] for n in range(0, 8)] + [s[:30], s]
+    for plen in (-5, 0, 1, 3, 0x7FFFFFF0, 200):
+        b = bytearray(s)
+        b[0:4] = (plen & 0xFFFFFFFF).to_bytes(4, "big")
+        cases.append(bytes(b))
+    for c in cases:
+        want = oracle.verify_packets(c, proto, cs, CSUM_CRC32C)
+        if not c:
+            continue
+        keep, p = _dev(engine, c, 1)
+        assert engine.verify_packets(None, proto, cs, CSUM_CRC32C, dptr=p, nbytes=len(c)) == want, len(c)
+        assert engine.verify_packets(c, proto, cs, CSUM_CRC32C) == want, len(c)
+        keep.free()
