@@ -1,18 +1,31 @@
 #!/usr/bin/env python3
 """Benchmark: CRC32C verify GiB/s (device-resident), 512 B chunks over 128 MiB
-HDFS blocks (BASELINE.json metric; SURVEY.md 8d config C3).
+HDFS blocks (BASELINE.json metric; SURVEY.md 8d).
 
-One STEP = one verify pass of the hot path over this rank's whole batch:
-1024 blocks x 128 MiB (128 GiB) of splitmix64 data generated on device,
-expected per-chunk CRCs in wire (big-endian) order, 1 in 65537 chunks
-corrupted; output = mismatch bitmap + first bad chunk per block.
+One STEP = one verify pass of the hot path over this rank's whole batch of
+128 MiB blocks of splitmix64 data generated on device: expected per-chunk
+CRCs in wire (big-endian) order, 1 in 65537 chunks corrupted; output = the
+mismatch bitmap + first bad chunk per block (_verify_crcdata,
+src/datanode.c:2931-2963, over every chunk of every block).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3|C4]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
 
-Ranks shard independent blocks (hadoofus_amd/shard.py: no data-path
-collective, scaling "weak"); one RCCL all-reduce aggregates {bytes,
+--config C3 (default, the headline): 1024 blocks (128 GiB) per GPU, weak
+scaling.  --config C4: 512 blocks (64 GiB) for the whole node split evenly
+over the ranks (BASELINE.json configs[3]), strong scaling.  Ranks shard
+independent blocks (hadoofus_amd/shard.py: no data-path collective); each
+rank binds its engine to LOCAL_RANK explicitly and the ranks' PCI bus ids
+are gathered and checked distinct; one all-reduce aggregates {bytes,
 mismatches, ok} (sum) and time (max).
+
+Around the timed C3 loop, outside it: C2 (compute-only) is timed and every
+block's CRC array is digest-checked against the reference-generated
+tests/golden/block_digests_all.npz; C5 (mixed 512/1024/2048/4096 in one
+launch) is computed on clean data, digest-checked per block, then verified
+after the corruption with its exact expected bitmap; the C3 bitmap is
+compared bit for bit with the corruption pattern; the verify kernel's
+load-only twin from the diagnostic build gives the empirical ceiling.
 Prints ONE JSON line on rank 0.
 """
 import argparse
@@ -22,13 +35,18 @@ import platform
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 BLOCK = 128 << 20
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+MOD, BITMUL = 65537, 7919  # SURVEY.md 8d corruption pattern
+SIZES = (512, 1024, 2048, 4096)
+DIGESTS = os.path.join(ROOT, "tests", "golden", "block_digests_all.npz")
 # SURVEY.md 8c pinned digests (reference-generated): _hdfs_crc32c(0, LE crc array)
-PINNED = {(0, 512): 0xF2590C08, (1, 512): 0xEB636035, (0, 4096): 0xB77BAB49, (1, 4096): 0xEF4F7B33}
+PINNED = {(0, 512): 0xF2590C08}
 
 
 def parse():
@@ -36,21 +54,21 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--blocks", type=int, default=1024, help="128 MiB blocks per GPU")
+    ap.add_argument("--config", choices=("C3", "C4"), default="C3")
+    ap.add_argument("--blocks", type=int, default=None,
+                    help="override the config's block count (per GPU for C3, total for C4)")
     ap.add_argument("--chunk", type=int, default=512)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
-    ap.add_argument("--no-extra", action="store_true", help="skip compute/mixed side measurements")
-    ap.add_argument("--cpu-gib", type=float, default=2.0, help="CPU baseline sample size")
-    ap.add_argument("--mixed", action="store_true",
-                    help="also time C5 (mixed 512/1024/2048/4096 bytesPerChecksum in one launch)")
+    ap.add_argument("--no-extra", action="store_true", help="skip C2/C5/ceiling side measurements")
+    ap.add_argument("--cpu-gib", type=float, default=4.0, help="CPU baseline sample size (GiB)")
     return ap.parse_args()
 
 
 def pmc_traffic(kernel, nbytes, chunk):
     """HBM traffic per launch from the committed rocprofv3 PMC passes
-    (tools/pmc_traffic.py -> profiles/<round>/pmc_traffic.json): the measured
-    bytes-per-payload-byte ratio of the same kernel and chunk size, scaled to
-    this launch.  None when no matching profile is committed."""
+    (tools/pmc_traffic.py -> profiles/<round>/pmc_traffic.json, newest round
+    last): the measured bytes-per-payload-byte ratio of the same kernel and
+    chunk size, scaled to this launch.  None when no profile is committed."""
     import glob
     best = None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json"))):
@@ -67,47 +85,74 @@ def pmc_traffic(kernel, nbytes, chunk):
     return int(k["traffic_bytes_per_payload_byte"] * nbytes), os.path.relpath(f, ROOT)
 
 
+def cgroup_cpu_limit():
+    """CPUs granted by the cgroup v2 quota (cpu.max), or None."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        return None if q == "max" else round(int(q) / int(p), 2)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(sample_gib):
-    """Reference CPU path timed on this host (rank 0, N=1): the reference's own
-    _hdfs_sse42_crc32c compiled from its sources (oracle/_ref) when present,
-    else the oracle's SSE4.2 restatement.  A reported baseline, not the target."""
+    """The reference's CPU path timed on this host (rank 0, N=1): its own
+    _hdfs_sse42_crc32c (src/crc32c_sse42.c:214-381) compiled from its sources
+    (oracle/_ref) when present, else the oracle's SSE4.2 restatement; one
+    call per 512 B chunk as _verify_crcdata makes them, one contiguous chunk
+    range per thread, on every core of this process's affinity set; the
+    single-core leg pinned to one core with sched_setaffinity.  A reported
+    baseline, not the target."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import ctypes
+    from concurrent.futures import ThreadPoolExecutor
 
     from oracle import Oracle, Reference, have_reference
     o = Oracle()
-    nbytes = int(sample_gib * (1 << 30)) // BLOCK * BLOCK
+    affinity = sorted(os.sched_getaffinity(0))
+    threads = min(len(affinity), 256)
+    nbytes = max(1, int(sample_gib * (1 << 30)) // BLOCK) * BLOCK
+    words = nbytes // 8
+    buf = np.empty(words, dtype=np.uint64)
     t0 = time.time()
-    data = o.splitmix(nbytes // 8, 0, 0).view("uint8")
+    parts = min(threads, 64)
+    step = (words + parts - 1) // parts
+    with ThreadPoolExecutor(parts) as ex:  # ctypes releases the GIL
+        list(ex.map(lambda i: o._fill(buf[i * step:].ctypes.data, max(0, min(step, words - i * step)), 0, i * step),
+                    range(parts)))
     gen_s = time.time() - t0
+    data = buf.view(np.uint8)
     if have_reference():
         ref = Reference()
-        ext = ref.sse42_addr
-        kind, fn, label = "reference", "ext", "_hdfs_sse42_crc32c (src/crc32c_sse42.c built from /root/reference)"
+        fn, ext, kind = "ext", ref.sse42_addr, "reference"
+        label = "_hdfs_sse42_crc32c (src/crc32c_sse42.c built from /root/reference)"
         sw_ext, sw_fn, sw_label = ctypes.cast(ref.sw_fn, ctypes.c_void_p).value, "ext", "_hdfs_sw_crc32c (reference)"
     else:
-        ext, kind, fn, label = None, "port", "hw", "oracle SSE4.2 3-way restatement"
+        fn, ext, kind, label = "hw", None, "port", "oracle SSE4.2 3-way restatement"
         sw_ext, sw_fn, sw_label = None, "sw", "oracle slicing-by-8 restatement"
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
 
-    def timed_passes(fn_, ext_, buf, nthreads, budget_s):
-        # whole passes over buf until budget_s of timed work (>= 1 pass)
+    def timed(fn_, ext_, view, nthreads, budget_s):
+        # whole passes over view until budget_s of timed work (>= 1 pass)
         tot, k, first = 0.0, 0, None
         while k == 0 or tot < budget_s:
-            s, crcs = o.bench_chunks(buf, 512, nthreads, fn_, ext_)
+            s, crcs = o.bench_chunks(view, 512, nthreads, fn_, ext_)
             first = crcs if first is None else first
             tot += s
             k += 1
-        return tot / k, k, first
+        return view.nbytes * k / tot / (1 << 30), k, first
 
-    # a bounded sample, ~10 s of wall time in all (task: 10-30 s of CPU work)
-    s1, passes1, crc1 = timed_passes(fn, ext, data, 1, 3.0)
-    sn, passes, _ = timed_passes(fn, ext, data, threads, 5.0)
-    tn = sn * passes
-    # cross-check one block against the pinned digest
+    gib = nbytes / (1 << 30)
+    # single core, pinned (the calling thread runs the work when nthreads == 1)
+    os.sched_setaffinity(0, {affinity[0]})
+    try:
+        v1, p1, crc1 = timed(fn, ext, data, 1, 3.0)
+        # SURVEY 8(d) C1: block 0 through the slicing-by-8 SW backend, one core
+        v_sw, p_sw, crc_sw = timed(sw_fn, sw_ext, data[:BLOCK], 1, 1.0)
+    finally:
+        os.sched_setaffinity(0, set(affinity))
+    # all cores: three repetitions, the median is the value
+    reps = [timed(fn, ext, data, threads, 2.0) for _ in range(3)]
+    vals = sorted(r[0] for r in reps)
     dig = o.crc32c(0, crc1[: BLOCK // 512].view("uint8"), "hw")
-    # SURVEY 8(d) C1: block 0 through the slicing-by-8 SW backend, one core
-    s_sw, passes_sw, crc_sw = timed_passes(sw_fn, sw_ext, data[:BLOCK], 1, 1.0)
     dig_sw = o.crc32c(0, crc_sw.view("uint8"), "hw")
     model = ""
     try:
@@ -117,86 +162,156 @@ def cpu_baseline(sample_gib):
                 break
     except OSError:
         pass
-    gib = nbytes / (1 << 30)
     return {
-        "value": round(gib * passes / tn, 2),
+        "value": round(vals[1], 2),
         "unit": "GiB/s",
         "cores": threads,
         "kind": kind,
-        "sample": f"{label}; per-512B-chunk CRCs over {gib:.0f} GiB splitmix64 (blocks 0..{nbytes // BLOCK - 1}), "
-                  f"{threads} threads x {passes} passes; single core {gib / s1:.2f} GiB/s ({passes1} passes)",
-        "single_core_value": round(gib / s1, 3),
+        "sample": f"{label}; one call per 512 B chunk over {gib:.0f} GiB of splitmix64 blocks "
+                  f"0..{nbytes // BLOCK - 1}, {threads} threads (the affinity set) on contiguous chunk ranges, "
+                  f"median of 3 repetitions x {min(r[1] for r in reps)}+ passes; single core pinned "
+                  f"(sched_setaffinity) {v1:.2f} GiB/s ({p1} passes)",
+        "repetitions": [round(v, 2) for v in vals],
+        "single_core_value": round(v1, 3),
         "cpu_model": model or platform.processor(),
+        "affinity_cpus": len(affinity),
         "nproc": os.cpu_count(),
+        "cgroup_cpu_limit": cgroup_cpu_limit(),
         "digest_ok": dig == PINNED[(0, 512)],
-        "c1_sw_single_core": {"value": round(BLOCK / (1 << 30) / s_sw, 3), "unit": "GiB/s", "sample":
-                              f"{sw_label}; block 0 (128 MiB), 512 B chunks, 1 thread, {passes_sw} passes",
+        "c1_sw_single_core": {"value": round(v_sw, 3), "unit": "GiB/s", "sample":
+                              f"{sw_label}; block 0 (128 MiB), 512 B chunks, 1 pinned core, {p_sw} passes",
                               "digest_ok": dig_sw == PINNED[(0, 512)]},
         "datagen_s": round(gen_s, 2),
     }
+
+
+class Golden:
+    """Reference-generated per-block digests (oracle/gen_block_digests.py)."""
+
+    def __init__(self):
+        z = np.load(DIGESTS)
+        self.be, self.le, self.n = z["be"], z["le"], z["be"].shape[0]
+
+    def check(self, h, crcs_ptr, offs, blocks, sizes):
+        """Digest (CRC of the BE CRC array) of each block's CRC array, all in
+        one compute launch over the arrays themselves; -> (ok, pinned)."""
+        digs = h.DeviceBuffer(4 * len(blocks))
+        segs = [h.Segment(data=crcs_ptr + off, len=BLOCK // cs * 4, chunk_size=BLOCK // cs * 4, flags=0, crc_init=0,
+                          crcs=digs.ptr + 4 * i) for i, (off, cs) in enumerate(zip(offs, sizes))]
+        p = h.Plan(h.MODE_COMPUTE, segs)
+        p.execute()
+        got = digs.download(dtype=np.uint32)
+        p.destroy()
+        digs.free()
+        ok = pinned = 0
+        for i, (g, cs) in enumerate(zip(blocks, sizes)):
+            if g < self.n:
+                pinned += 1
+                ok += int(got[i] == self.be[g, SIZES.index(cs)])
+        return ok, pinned
+
+
+def corrupted(g0, nblocks, per):
+    """Global 512-B chunk indices the corruption pattern flips in blocks
+    [g0, g0 + nblocks) (chunk i with i % MOD == 0)."""
+    start, end = g0 * per, (g0 + nblocks) * per
+    first = (start + MOD - 1) // MOD * MOD
+    return np.arange(first, end, MOD, dtype=np.int64)
+
+
+def bitmap_matches(bm_host, nbits_per_block, bad_local):
+    """bm_host: concatenated per-block bitmaps; bad_local: (block, chunk) pairs."""
+    bits = np.unpackbits(bm_host, bitorder="little")
+    want = np.zeros_like(bits)
+    for b, c in bad_local:
+        want[b * nbits_per_block + c] = 1
+    return bool(np.array_equal(bits, want))
 
 
 def main():
     args = parse()
     from hadoofus_amd import shard
     # torch (and with it the HIP runtime it ships) is imported before the
-    # engine library only when launched as ranks; both then share one runtime.
+    # engine library only when launched as ranks.
     d = shard.Collective("nccl") if shard.launched_by_torchrun() else shard.Local()
     import hadoofus_amd as h
 
     h.load()
+    h.init(d.local)  # explicit binding: this rank's GPU, whatever torch's current device is
+    dev, bus = h.bound_device()
+    infos = d.gather({"rank": d.rank, "local_rank": d.local, "device": dev, "pci_bus_id": bus})
+    ndev = shard.check_distinct_devices(infos)
     arch, ncu = h.device_info()
-    B, cs = args.blocks, args.chunk
+    cs = args.chunk
     per = BLOCK // cs
-    g_block0, B = shard.rank_blocks(d.rank, d.world, B)
+    scaling, g0, B = shard.workload_blocks(args.config, d.rank, d.world, args.blocks)
     stream = h.stream_create()
+    gblocks = list(range(g0, g0 + B))
 
     data = h.DeviceBuffer(B * BLOCK)
-    crcs = h.DeviceBuffer(B * (BLOCK // 512) * 4)
-    bms = h.DeviceBuffer(B * (BLOCK // 512) // 8)
-    h.fill_splitmix64(data.ptr, B * BLOCK // 8, 0, g_block0 << 24, None)
+    crcs = h.DeviceBuffer(B * per * 4)
+    bms = h.DeviceBuffer(B * per // 8)
+    h.fill_splitmix64(data.ptr, B * BLOCK // 8, 0, g0 << 24, None)
 
-    def segs(chunk_of, flags, with_bitmap):
-        out, off_c, off_b = [], 0, 0
-        for b in range(B):
-            c = chunk_of(b)
+    def segs(chunk_of, crc_ptr, bm_ptr):
+        out, off_c = [], 0
+        for b, g in enumerate(gblocks):
+            c = chunk_of(g)
             n = BLOCK // c
-            out.append(h.Segment(data=data.ptr + b * BLOCK, len=BLOCK, chunk_size=c, flags=flags, crc_init=0,
-                                 crcs=crcs.ptr + off_c * 4, bitmap=(bms.ptr + off_b // 8) if with_bitmap else None))
+            out.append(h.Segment(data=data.ptr + b * BLOCK, len=BLOCK, chunk_size=c, flags=h.SEG_BE, crc_init=0,
+                                 crcs=crc_ptr + off_c * 4, bitmap=(bm_ptr + off_c // 8) if bm_ptr else None))
             off_c += n
-            off_b += n
         return out
 
-    extra = {}
-    # Digest check of the hot kernel's output on the pinned blocks (rank 0 owns blocks 0 and 1).
-    digest_ok = None
-    if d.rank == 0 and B >= 2:
-        digest_ok = True
-        for c in (512, 4096):
-            p = h.Plan(h.MODE_COMPUTE, segs(lambda b: c, 0, False)[:2])
-            p.execute()
-            for blk in (0, 1):
-                got = h.stream_crc_dev(0, crcs.ptr + blk * (BLOCK // c) * 4, (BLOCK // c) * 4)
-                digest_ok &= got == PINNED[(blk, c)]
-            p.destroy()
+    extra, parity = {}, {}
+    golden = Golden()
 
-    # C2: compute-only (also produces the expected wire CRCs for C3).
-    comp = h.Plan(h.MODE_COMPUTE, segs(lambda b: cs, h.SEG_BE, False))
-    comp.execute()
-    h.device_sync()
+    # C2: compute-only, 512 B (also the expected wire CRCs of C3).
+    comp = h.Plan(h.MODE_COMPUTE, segs(lambda g: cs, crcs.ptr, None))
+    for _ in range(2):
+        comp.execute(stream)
+    h.stream_sync(stream)
     if not args.no_extra:
-        ms = comp.time(3, stream)
-        extra["compute_gibps"] = round(B * BLOCK / (ms * 1e-3) / (1 << 30), 1)
-        extra["probe_read_GBps"] = round(h.probe_read(data.ptr, B * BLOCK, 3, stream), 1)
-    h.device_sync()
+        comp.set_timing(max(2, args.steps))
+        for _ in range(args.steps):
+            comp.execute(stream)
+        kms_c, nl_c = comp.kernel_ms()
+        t_c = kms_c / nl_c * 1e-3
+        alg_c = B * BLOCK * (1 + 4 / cs)
+        extra["compute_gibps"] = round(B * BLOCK / t_c / (1 << 30), 1)
+        extra["compute_roofline"] = {"achieved": round(alg_c / t_c / 1e9, 1), "frac": round(alg_c / t_c / 1e9 /
+                                     HBM_PEAK_GBPS, 4), "kernel_avg_ms": round(t_c * 1e3, 3), "launches": nl_c}
+    ok, pinned = golden.check(h, crcs.ptr, [b * per * 4 for b in range(B)], gblocks, [cs] * B)
+    parity["c2_block_digests_ok"] = f"{ok}/{pinned}" + ("" if pinned == B else f" ({B - pinned} beyond the golden set)")
+    c2_ok = ok == pinned
 
-    # Corrupt 1 in 65537 chunks (global chunk index), then verify.
-    for b in range(B):
-        h.corrupt(data.ptr + b * BLOCK, BLOCK, cs, (g_block0 + b) * per, 65537, 7919, None)
-    h.device_sync()
-    expect_bad = shard.expected_bad(g_block0, B, per, 65537)
+    # C5: mixed bytesPerChecksum in one launch, computed on CLEAN data.
+    c5_of = lambda g: 512 << (g % 4)  # noqa: E731
+    c5_sizes = [c5_of(g) for g in gblocks]
+    c5_offs = np.concatenate([[0], np.cumsum([BLOCK // c for c in c5_sizes])])  # chunk offsets
+    crcs5 = bms5 = None
+    c5_ok = True
+    if not args.no_extra:
+        crcs5 = h.DeviceBuffer(int(c5_offs[-1]) * 4)
+        bms5 = h.DeviceBuffer(int(c5_offs[-1]) // 8)
+        mixc = h.Plan(h.MODE_COMPUTE, segs(c5_of, crcs5.ptr, None))
+        mixc.execute(stream)
+        h.stream_sync(stream)
+        mixc.destroy()
+        ok5, pinned5 = golden.check(h, crcs5.ptr, [int(o) * 4 for o in c5_offs[:-1]], gblocks, c5_sizes)
+        parity["c5_block_digests_ok"] = f"{ok5}/{pinned5}"
+        c5_ok = ok5 == pinned5
 
-    ver = h.Plan(h.MODE_VERIFY, segs(lambda b: cs, h.SEG_BE, True))
+    # Corrupt 1 in 65537 chunks (global 512-B chunk index), then verify.
+    for b, g in enumerate(gblocks):
+        h.corrupt(data.ptr + b * BLOCK, BLOCK, cs, g * per, MOD, BITMUL, None)
+    h.device_sync()
+    bad = corrupted(g0, B, per)
+    bad_local = [(int(i // per) - g0, int(i % per)) for i in bad]
+    expect_bad = len(bad)
+    expect_first = {b: c for b, c in reversed(bad_local)}
+
+    ver = h.Plan(h.MODE_VERIFY, segs(lambda g: cs, crcs.ptr, bms.ptr))
     for _ in range(args.warmup):
         ver.execute(stream)
     h.stream_sync(stream)
@@ -215,20 +330,61 @@ def main():
     kms, nlaunch = ver.kernel_ms()
     first_bad, m = ver.results(stream)
     parity_ok &= m == expect_bad
+    parity_ok &= all(first_bad[b] == expect_first.get(b, 0xFFFFFFFF) for b in range(B))
+    c3_bitmap_ok = bitmap_matches(bms.download(), per, bad_local)
+    parity_ok &= c3_bitmap_ok and c2_ok
     elapsed = t1 - t0
 
-    if args.mixed:
-        # C5: mixed bytesPerChecksum 512/1024/2048/4096 in one launch (compute + verify)
-        mixc = h.Plan(h.MODE_COMPUTE, segs(lambda b: 512 << (b % 4), h.SEG_BE, False))
-        mixc.execute(stream)
-        mixv = h.Plan(h.MODE_VERIFY, segs(lambda b: 512 << (b % 4), h.SEG_BE, True))
+    if not args.no_extra:
+        # C5 verify on the corrupted data against the clean mixed CRCs: every
+        # corrupted 512-B chunk lies in exactly one C5 chunk (32 MiB apart).
+        mixv = h.Plan(h.MODE_VERIFY, segs(c5_of, crcs5.ptr, bms5.ptr))
         mixv.execute(stream)
-        ms = mixv.time(3, stream)
-        _, mm = mixv.results(stream)
-        extra["mixed_verify_gibps"] = round(B * BLOCK / (ms * 1e-3) / (1 << 30), 1)
-        extra["mixed_mismatches"] = int(mm)
-        mixc.destroy()
+        mixv.set_timing(max(2, args.steps // 2))
+        for _ in range(max(2, args.steps // 2)):
+            mixv.execute(stream)
+        kms5, nl5 = mixv.kernel_ms()
+        fb5, mm = mixv.results(stream)
+        bad5 = [(b, c * 512 // c5_sizes[b]) for b, c in bad_local]
+        bits5 = np.unpackbits(bms5.download(), bitorder="little")
+        want5 = np.zeros_like(bits5)
+        for b, c in bad5:
+            want5[c5_offs[b] + c] = 1
+        first5 = {b: c for b, c in reversed(bad5)}
+        c5v_ok = (mm == len(bad5) and bool(np.array_equal(bits5, want5)) and
+                  all(fb5[b] == first5.get(b, 0xFFFFFFFF) for b in range(B)))
+        extra["mixed_verify_gibps"] = round(B * BLOCK / (kms5 / nl5 * 1e-3) / (1 << 30), 1)
+        parity["c5_mismatches"] = int(mm)
+        parity["c5_expected"] = len(bad5)
+        parity["c5_bitmap_ok"] = c5v_ok
+        parity_ok &= c5v_ok and c5_ok
         mixv.destroy()
+
+    # Empirical ceiling: the verify kernel's load-only twin (identical loads
+    # and store instructions, no CRC arithmetic) from the diagnostic build,
+    # same process, same data and segment table.
+    ceiling = None
+    if not args.no_extra:
+        try:
+            sys.path.insert(0, os.path.join(ROOT, "tools"))
+            import diaglib
+            dg = diaglib.Diag()
+            dg.init(d.local)
+            dg.set_store_policy(4)
+            twin = dg.plan(h.MODE_VERIFY, segs(lambda g: cs, crcs.ptr, bms.ptr))
+            twin.execute(stream)
+            twin.set_timing(max(2, args.steps // 2))
+            for _ in range(max(2, args.steps // 2)):
+                twin.execute(stream)
+            kt, nt = twin.kernel_ms()
+            twin.destroy()
+            dg.set_store_policy(0)
+            alg_t = B * BLOCK * (1 + 4 / cs + 1 / (8 * cs))
+            ceiling = alg_t / (kt / nt * 1e-3) / 1e9
+            extra["ceiling_GBps"] = round(ceiling, 1)
+            extra["ceiling_source"] = "load-only twin of crc32c_tiles_kernel<verify> (libhadoofus_crc32c_diag.so)"
+        except (ImportError, OSError) as e:
+            extra["ceiling_error"] = str(e)[:200]
 
     tot_bytes, tot_mism, ok, t_max = d.aggregate(B * BLOCK * args.steps, m, parity_ok, elapsed)
     n = d.world
@@ -240,6 +396,12 @@ def main():
         k_avg_s = kms / max(1, nlaunch) * 1e-3
         achieved = alg / k_avg_s / 1e9
         traffic, traffic_src = pmc_traffic("verify", nbytes, cs)
+        if args.config == "C3":
+            workload = ("C3 verify: 1024 x 128MiB HDFS blocks per GPU of splitmix64 data, 512B chunks, BE wire CRCs, "
+                        "1/65537 chunks corrupted, bitmap + first-bad out")
+        else:
+            workload = ("C4 verify: 64GiB (512 x 128MiB blocks) split evenly over the GPUs, 512B chunks, BE wire CRCs, "
+                        "1/65537 chunks corrupted, bitmap + first-bad out")
         line = {
             "metric": "CRC32C verify GiB/s (device-resident), 512B chunks over 128MiB HDFS blocks",
             "value": round(gib_s, 1),
@@ -249,26 +411,27 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(t_max / args.steps * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic",
             "config": {
-                "workload": "C3 verify: 128MiB HDFS blocks of splitmix64 data, 512B chunks, BE wire CRCs, "
-                            "1/65537 chunks corrupted, bitmap + first-bad out",
-                "blocks_per_gpu": B, "block_bytes": BLOCK, "chunk_size": cs,
+                "workload": workload, "blocks_per_gpu": B, "block_bytes": BLOCK, "chunk_size": cs,
                 "bytes_per_gpu_per_step": nbytes, "parallelism": f"shard{n}",
             },
             "roofline": {
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                 "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
+                "frac_of_measured_peak": round(achieved / ceiling, 4) if ceiling else None,
+                "measured_peak": round(ceiling, 1) if ceiling else None,
                 "kernel": "crc32c_tiles_kernel<verify>", "kernel_avg_ms": round(k_avg_s * 1e3, 3),
                 "alg_bytes_per_launch": int(alg),
             },
-            "parity": {"mismatches": int(tot_mism), "expected_per_gpu": int(expect_bad),
-                       "all_ranks_ok": ok == n, "pinned_digests_ok": digest_ok},
-            "device": {"arch": arch, "cus": ncu},
+            "parity": dict({"mismatches": int(tot_mism), "expected_per_gpu": int(expect_bad),
+                            "all_ranks_ok": ok == n, "c3_bitmap_ok": c3_bitmap_ok}, **parity),
+            "device": {"arch": arch, "cus": ncu, "ranks_on_distinct_gpus": ndev,
+                       "pci_bus_ids": [i["pci_bus_id"] for i in infos]},
             "extra": extra,
         }
         if n == 1 and not args.no_cpu:

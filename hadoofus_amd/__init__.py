@@ -4,9 +4,12 @@ The product is the C-ABI shared library ``hadoofus_amd/lib/libhadoofus_crc32c.so
 (include/hadoofus_crc32c.h, include/crc32c.h).  This package is a thin ctypes
 mirror of that ABI used by the tests and bench; it has no compute of its own
 and no fallback: if the library or a gfx950 device is missing, calls fail.
+Tuning knobs live only in the separate diagnostic build (tools/diaglib.py).
 """
 from .abi import (  # noqa: F401
     LIB_PATH,
+    bind_product,
+    bind_diag,
     CSUM_NULL,
     CSUM_CRC32,
     CSUM_CRC32C,
@@ -43,15 +46,9 @@ from .abi import (  # noqa: F401
     stream_create,
     stream_sync,
     device_info,
+    init,
+    bound_device,
     device_sync,
-    probe_read,
-    set_tile_order,
-    set_tuning,
-    set_probe,
-    set_depth,
-    set_shape,
-    set_group_shift,
-    set_store_policy,
     load,
     stream_crc_dev,
     stream_ex,

@@ -100,20 +100,14 @@ def _bind(lib, name, res, args):
     return f
 
 
-def load(path=LIB_PATH):
-    """Load the product library (raises if it was not built)."""
-    global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(path):
-        raise ImportError(f"{path} not built; run `python -m hadoofus_amd.build` "
-                          "(or __graft_entry__.build())")
-    lib = ctypes.CDLL(path)
+def bind_product(lib):
+    """Bind the C ABI of include/hadoofus_crc32c.h + include/crc32c.h on lib."""
     for n in ("_hdfs_crc32c", "_hdfs_sse42_crc32c", "_hdfs_armv8_crc32c", "_hdfs_sw_crc32c"):
         _bind(lib, n, _u32, [_u32, _vp, ctypes.c_uint])
     _bind(lib, "hdfs_crc32c_last_error", ctypes.c_char_p, [])
     _bind(lib, "hdfs_crc32c_init", _int, [_int])
     _bind(lib, "hdfs_crc32c_device_info", _int, [_int, ctypes.c_char_p, _sz, ctypes.POINTER(_int)])
+    _bind(lib, "hdfs_crc32c_bound_device", _int, [ctypes.POINTER(_int), ctypes.c_char_p, _sz])
     _bind(lib, "hdfs_crc32c_plan_create", _int, [ctypes.POINTER(_vp), _int, ctypes.POINTER(Segment), _sz])
     _bind(lib, "hdfs_crc32c_plan_execute", _int, [_vp, _vp])
     _bind(lib, "hdfs_crc32c_plan_results", _int, [_vp, _vp, ctypes.POINTER(_u32), _sz, ctypes.POINTER(_u64)])
@@ -149,29 +143,46 @@ def load(path=LIB_PATH):
     _bind(lib, "hdfs_crc32c_fill_splitmix64", _int, [_vp, _u64, _u64, _u64, _vp])
     _bind(lib, "hdfs_crc32c_corrupt", _int, [_vp, _u64, _u32, _u64, _u64, _u64, _vp])
     _bind(lib, "hdfs_crc32c_device_sync", _int, [])
-    _bind(lib, "hdfs_crc32c_set_tile_order", _int, [_int])
-    _bind(lib, "hdfs_crc32c_set_group_shift", _int, [_int])
-    _bind(lib, "hdfs_crc32c_probe_read", _int, [_vp, _u64, _vp, _int, ctypes.POINTER(ctypes.c_double)])
-    _bind(lib, "hdfs_crc32c_set_tuning", _int, [_int, _vp])
-    _bind(lib, "hdfs_crc32c_set_probe", _int, [_int, _int, _int])
-    _bind(lib, "hdfs_crc32c_set_depth", _int, [_int])
     _bind(lib, "hdfs_crc32c_compose_packets", _int,
           [_vp, _u64, ctypes.c_int64, ctypes.c_int64, _int, _int, _int, _vp, _u64, ctypes.POINTER(OutPacket), _sz,
            ctypes.POINTER(_sz), ctypes.POINTER(_u64)])
-    _bind(lib, "hdfs_crc32c_set_shape", _int, [_int, _int])
-    _bind(lib, "hdfs_crc32c_set_store_policy", _int, [_int])
     _bind(lib, "hdfs_crc32c_compute_host", _int, [_vp, _u64, _u32, _u32, _u32, _vp, _u64])
     _bind(lib, "hdfs_crc32c_verify_host", _int,
           [_vp, _u64, _u32, _u32, _u32, _vp, _vp, _u64, ctypes.POINTER(_u64), ctypes.POINTER(_u64)])
     _bind(lib, "hdfs_crc32c_host_alloc", _int, [ctypes.POINTER(_vp), _u64])
     _bind(lib, "hdfs_crc32c_host_free", _int, [_vp])
-    _lib = lib
     return lib
 
 
-def _check(rc):
+def bind_diag(lib):
+    """Bind the extra knobs of the diagnostic build (include/hadoofus_crc32c_diag.h)."""
+    _bind(lib, "hdfs_crc32c_set_tile_order", _int, [_int])
+    _bind(lib, "hdfs_crc32c_set_group_shift", _int, [_int])
+    _bind(lib, "hdfs_crc32c_set_xcd_major", _int, [_int])
+    _bind(lib, "hdfs_crc32c_probe_read", _int, [_vp, _u64, _vp, _int, ctypes.POINTER(ctypes.c_double)])
+    _bind(lib, "hdfs_crc32c_set_tuning", _int, [_int, _vp])
+    _bind(lib, "hdfs_crc32c_set_probe", _int, [_int, _int, _int])
+    _bind(lib, "hdfs_crc32c_set_depth", _int, [_int])
+    _bind(lib, "hdfs_crc32c_set_shape", _int, [_int, _int])
+    _bind(lib, "hdfs_crc32c_set_store_policy", _int, [_int])
+    return lib
+
+
+def load(path=LIB_PATH):
+    """Load the product library (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise ImportError(f"{path} not built; run `python -m hadoofus_amd.build` "
+                          "(or __graft_entry__.build())")
+    _lib = bind_product(ctypes.CDLL(path))
+    return _lib
+
+
+def _check(rc, lib=None):
     if rc != 0:
-        raise CRC32CError(rc, load().hdfs_crc32c_last_error().decode(errors="replace"))
+        raise CRC32CError(rc, (lib or load()).hdfs_crc32c_last_error().decode(errors="replace"))
 
 
 def _host(buf):
@@ -187,6 +198,19 @@ def device_info(device=-1):
     ncu = _int(0)
     _check(load().hdfs_crc32c_device_info(device, arch, 64, ctypes.byref(ncu)))
     return arch.value.decode(), ncu.value
+
+
+def init(device=-1):
+    """hdfs_crc32c_init: device >= 0 binds the engine to that device."""
+    _check(load().hdfs_crc32c_init(device))
+
+
+def bound_device():
+    """-> (device ordinal, PCI bus id) the engine runs on."""
+    d = _int(-1)
+    bus = ctypes.create_string_buffer(64)
+    _check(load().hdfs_crc32c_bound_device(ctypes.byref(d), bus, 64))
+    return d.value, bus.value.decode()
 
 
 def crc32c(crc, buf, entry="_hdfs_crc32c"):
@@ -386,48 +410,55 @@ class DeviceBuffer:
 
 
 class Plan:
-    """Batch compute/verify plan over a list of Segment descriptors."""
+    """Batch compute/verify plan over a list of Segment descriptors.  lib:
+    the library to run it on (default: the product library; tools pass the
+    diagnostic build loaded side by side)."""
 
-    def __init__(self, mode, segments):
+    def __init__(self, mode, segments, lib=None):
+        self.lib = lib or load()
         self.mode = mode
         self.nseg = len(segments)
         arr = (Segment * max(1, self.nseg))(*segments)
         self._segs = arr
         p = _vp()
-        _check(load().hdfs_crc32c_plan_create(ctypes.byref(p), mode, arr, self.nseg))
+        self._check(self.lib.hdfs_crc32c_plan_create(ctypes.byref(p), mode, arr, self.nseg))
         self.ptr = p.value
 
+    def _check(self, rc):
+        _check(rc, self.lib)
+
     def execute(self, stream=None):
-        _check(load().hdfs_crc32c_plan_execute(self.ptr, stream))
+        self._check(self.lib.hdfs_crc32c_plan_execute(self.ptr, stream))
 
     def results(self, stream=None):
         fb = (_u32 * max(1, self.nseg))()
         m = _u64(0)
-        _check(load().hdfs_crc32c_plan_results(self.ptr, stream, fb, self.nseg, ctypes.byref(m)))
+        self._check(self.lib.hdfs_crc32c_plan_results(self.ptr, stream, fb, self.nseg, ctypes.byref(m)))
         return list(fb)[: self.nseg], m.value
 
     def set_timing(self, on=True):
-        _check(load().hdfs_crc32c_plan_set_timing(self.ptr, 1 if on else 0))
+        """on: False/True, or an int > 1 = event pairs to pre-create."""
+        self._check(self.lib.hdfs_crc32c_plan_set_timing(self.ptr, int(on)))
 
     def kernel_ms(self):
         t = ctypes.c_double(0)
         n = _int(0)
-        _check(load().hdfs_crc32c_plan_kernel_ms(self.ptr, ctypes.byref(t), ctypes.byref(n)))
+        self._check(self.lib.hdfs_crc32c_plan_kernel_ms(self.ptr, ctypes.byref(t), ctypes.byref(n)))
         return t.value, n.value
 
     def stats(self):
         a, b, c = _u64(), _u64(), _u64()
-        _check(load().hdfs_crc32c_plan_stats(self.ptr, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
+        self._check(self.lib.hdfs_crc32c_plan_stats(self.ptr, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
         return {"main_bytes": a.value, "generic_bytes": b.value, "nchunks": c.value}
 
     def time(self, iters, stream=None):
         ms = ctypes.c_double(0)
-        _check(load().hdfs_crc32c_plan_time(self.ptr, stream, iters, ctypes.byref(ms)))
+        self._check(self.lib.hdfs_crc32c_plan_time(self.ptr, stream, iters, ctypes.byref(ms)))
         return ms.value
 
     def destroy(self):
         if self.ptr:
-            load().hdfs_crc32c_plan_destroy(self.ptr)
+            self.lib.hdfs_crc32c_plan_destroy(self.ptr)
             self.ptr = None
 
     def __del__(self):
@@ -457,21 +488,6 @@ def corrupt(dptr, nbytes, chunk, chunk0, modulus=65537, bitmul=7919, stream=None
 
 def device_sync():
     _check(load().hdfs_crc32c_device_sync())
-
-
-def set_tile_order(order):
-    _check(load().hdfs_crc32c_set_tile_order(order))
-
-
-def probe_read(dptr, nbytes, iters=3, stream=None):
-    """Measured streaming-read GB/s (the empirical roofline)."""
-    g = ctypes.c_double(0)
-    _check(load().hdfs_crc32c_probe_read(dptr, nbytes, stream, iters, ctypes.byref(g)))
-    return g.value
-
-
-def set_tuning(nt_loads=0, diag_ptr=None):
-    _check(load().hdfs_crc32c_set_tuning(nt_loads, diag_ptr))
 
 
 def compute_host(data, chunk_size, flags=0, crc_init=0, piece_bytes=0):
@@ -510,24 +526,3 @@ class PinnedBuffer:
         if self.ptr:
             load().hdfs_crc32c_host_free(self.ptr)
             self.ptr = None
-
-
-def set_probe(variant=0, grid_per_cu=2, block=1024):
-    _check(load().hdfs_crc32c_set_probe(variant, grid_per_cu, block))
-
-
-def set_group_shift(shift):
-    _check(load().hdfs_crc32c_set_group_shift(shift))
-
-
-def set_depth(depth):
-    _check(load().hdfs_crc32c_set_depth(depth))
-
-
-def set_shape(streams, block):
-    """Tiled-kernel shape: tile streams per wave and threads per workgroup."""
-    _check(load().hdfs_crc32c_set_shape(streams, block))
-
-
-def set_store_policy(policy):
-    _check(load().hdfs_crc32c_set_store_policy(policy))

@@ -20,6 +20,9 @@
 
 #include "crc32c_engine.h"
 #include "crc32c_tables.h"
+#ifdef HDFS_CRC32C_DIAG
+#include "hadoofus_crc32c_diag.h"
+#endif
 
 namespace hdfs_crc32c {
 
@@ -35,26 +38,46 @@ int fail(int code, const char *fmt, ...) {
 
 DevCtx g_ctx[kMaxDev];
 std::mutex g_init_mu;
-// Wave -> tile assignment of the tiled kernel: 0 contiguous slices, 1 interleaved.
+// Device the engine is bound to by hdfs_crc32c_init(device >= 0) (one
+// process per GPU: torchrun ranks bind LOCAL_RANK explicitly); -1 = the
+// calling thread's current HIP device.  Explicit, so the engine never
+// depends on sharing a HIP runtime (and its current-device state) with torch.
+std::atomic<int> g_bound_dev{-1};
+
+// Tiled-kernel launch configuration.  The release build runs the product
+// shapes only (schedule 3, nontemporal buffer loads, 3-deep pipeline, one
+// tile stream, 1024 threads, 8-tile groups; schedule 2 for small launches)
+// and reads nothing from the environment.  The diagnostic build
+// (-DHDFS_CRC32C_DIAG) starts from the same values, takes overrides from
+// HDFS_CRC32C_* variables and the setters of include/hadoofus_crc32c_diag.h.
+#ifdef HDFS_CRC32C_DIAG
 int env_int(const char *name, int dflt) {
   const char *e = std::getenv(name);
   return e ? std::atoi(e) : dflt;
 }
-int g_tile_order = env_int("HDFS_CRC32C_TILE_ORDER", 3);
+#define HDFS_KNOB(name, dflt) env_int(name, dflt)
+#else
+#define HDFS_KNOB(name, dflt) (dflt)
+#endif
+// Wave -> tile assignment of the tiled kernel (0 static, 1 workgroup-dynamic,
+// 2 two-phase contiguous, 3 two-phase interleaved).
+int g_tile_order = HDFS_KNOB("HDFS_CRC32C_TILE_ORDER", 3);
 // Data-stream loads of the tiled kernel: 0 default policy, 1 nontemporal,
 // 2 nontemporal buffer loads (SGPR base + cached per-lane offsets).
-int g_nt_loads = env_int("HDFS_CRC32C_NT", 2);
+int g_nt_loads = HDFS_KNOB("HDFS_CRC32C_NT", 2);
 // Rounds in flight per wave + 1 (register buffers of the tiled kernel): 2..4.
-int g_depth = env_int("HDFS_CRC32C_DEPTH", 3);
-// Tile streams per wave (1, 2, 4) and threads per workgroup (512, 768, 1024)
-// of the tiled kernel; non-default shapes exist for schedule 3 only.
-int g_streams = env_int("HDFS_CRC32C_STREAMS", 1);
-int g_block = env_int("HDFS_CRC32C_BLOCK", 1024);
-// Result-store policy of the tiled kernel: 0 default, 1 nontemporal,
-// 2 diagnostic only (drops the compute-mode CRC stores).
-uint32_t g_store_policy = uint32_t(env_int("HDFS_CRC32C_STORE", 0));
+int g_depth = HDFS_KNOB("HDFS_CRC32C_DEPTH", 3);
+// Tile streams per wave (1, 2, 4) and threads per workgroup (512, 768, 1024).
+int g_streams = HDFS_KNOB("HDFS_CRC32C_STREAMS", 1);
+int g_block = HDFS_KNOB("HDFS_CRC32C_BLOCK", 1024);
+// Result-store policy (diagnostic build only; the release kernel ignores it):
+// 0 default, 1 nontemporal, 2 drop compute-mode CRC stores, 3 full-line
+// writes, 4 verify plans run the load-only twin.
+uint32_t g_store_policy = uint32_t(HDFS_KNOB("HDFS_CRC32C_STORE", 0));
 // Schedule 3: log2 tiles per round-robin group (0..6).
-uint32_t g_group_shift = uint32_t(env_int("HDFS_CRC32C_GROUP", 3)) & 15u;
+uint32_t g_group_shift = uint32_t(HDFS_KNOB("HDFS_CRC32C_GROUP", 3)) & 15u;
+// Schedule 3: deal groups XCD-major (1) or by plain workgroup id (0).
+uint32_t g_xcd_major = uint32_t(HDFS_KNOB("HDFS_CRC32C_XCD", 0)) & 1u;
 // Diagnostic per-wave timestamps (device buffer, 3 x u64 per wave) or null.
 unsigned long long *g_diag = nullptr;
 
@@ -65,18 +88,19 @@ int ctx_init(int device, DevCtx **out) {
   if (e != hipSuccess || ndev <= 0)
     return fail(HDFS_CRC32C_ENODEV, "no HIP device visible (%s)",
                 e != hipSuccess ? hipGetErrorString(e) : "count 0");
+  if (device < 0) device = g_bound_dev.load(std::memory_order_acquire);
   if (device < 0) {
     if (hipGetDevice(&device) != hipSuccess) device = 0;
   }
   if (device >= ndev || device >= kMaxDev)
     return fail(HDFS_CRC32C_ENODEV, "device %d out of range (%d visible)", device, ndev);
   DevCtx &c = g_ctx[device];
-  if (c.ready) {
+  if (c.ready.load(std::memory_order_acquire)) {
     *out = &c;
     return HDFS_CRC32C_OK;
   }
   std::lock_guard<std::mutex> lk(g_init_mu);
-  if (c.ready) {
+  if (c.ready.load(std::memory_order_relaxed)) {
     *out = &c;
     return HDFS_CRC32C_OK;
   }
@@ -122,7 +146,7 @@ int ctx_init(int device, DevCtx **out) {
   std::memset(c.h_small_out, 0, kSmallOut);
   HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&c.dv_small_in), c.h_small_in, 0));
   HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&c.dv_small_out), c.h_small_out, 0));
-  c.ready = true;
+  c.ready.store(true, std::memory_order_release);
   *out = &c;
   return HDFS_CRC32C_OK;
 }
@@ -136,7 +160,7 @@ int ctx_init(int device, DevCtx **out) {
 // generic kernel they used to take (tools/exp_unaligned.py,
 // profiles/r01/exp_unaligned.json).  HDFS_CRC32C_ALIGN=16 restores the old
 // rule.
-static const uintptr_t g_tile_align = uintptr_t(std::max(1, env_int("HDFS_CRC32C_ALIGN", 1)));
+static const uintptr_t g_tile_align = uintptr_t(std::max(1, HDFS_KNOB("HDFS_CRC32C_ALIGN", 1)));
 
 void classify(SegDev &s, uint64_t &rounds, uint64_t &gtiles, uint64_t &mtiles) {
   const uint64_t ntiles = (uint64_t(s.nchunks) + kTileChunks - 1) / kTileChunks;
@@ -195,7 +219,7 @@ bool device_accessible(const void *p) {
 
 // HDFS_CRC32C_SMALL_RULE=0 (experiments): keep schedule 3 for small launches
 // and tables of small segments.
-static const int g_small_rule = env_int("HDFS_CRC32C_SMALL_RULE", 1);
+static const int g_small_rule = HDFS_KNOB("HDFS_CRC32C_SMALL_RULE", 1);
 
 // ctype: 0 = CRC32C, 1 = CRC32 (zlib polynomial) -- selects the table set.
 int launch_all(DevCtx &c, int mode, const SegDev *d_segs, uint32_t nseg, uint64_t rounds,
@@ -215,12 +239,22 @@ int launch_all(DevCtx &c, int mode, const SegDev *d_segs, uint32_t nseg, uint64_
     // tile leaves the current segment: small launches (which also skip the
     // pool) and tables of small segments keep the contiguous slices (2).
     const bool small = rounds < 32ull * 16u * uint64_t(grid) || mtiles < 2ull * uint64_t(grid) * nseg;
-    const int order = (g_tile_order == 3 && small && g_small_rule) ? 2 : g_tile_order;
-    // store policy 4 (diagnostic): verify plans run the load-only twin
-    const int kmode = (mode == kModeVerify && g_store_policy == 4) ? int(kModeLoadOnly) : mode;
-    HIPCHK(launch_tiles(kmode, order, g_nt_loads, g_depth, g_streams, g_block, grid, d_segs, nseg, rounds, mtiles,
-                        c.d_tab_main_t[ctype], d_fb, d_mism, g_diag, g_store_policy | (g_group_shift << 8), d_gctr,
-                        st));
+    const bool to_small = g_tile_order == 3 && small && g_small_rule;
+    const int order = to_small ? 2 : g_tile_order;
+    // buffer loads (nt 2) exist for schedule 3 only; the others use nontemporal global loads
+    const int nt = order == 3 ? g_nt_loads : std::min(g_nt_loads, 1);
+    // the small-launch fallback always runs the product's schedule-2 shape
+    const int depth = to_small ? 3 : g_depth, streams = to_small ? 1 : g_streams, block = to_small ? 1024 : g_block;
+    // store policy 4 (diagnostic build): verify plans run the load-only twin
+    const int kmode = (kDiag && mode == kModeVerify && g_store_policy == 4) ? int(kModeLoadOnly) : mode;
+    const hipError_t le = launch_tiles(kmode, order, nt, depth, streams, block, grid, d_segs, nseg, rounds,
+                                       mtiles, c.d_tab_main_t[ctype], d_fb, d_mism, kDiag ? g_diag : nullptr,
+                                       (kDiag ? g_store_policy : 0u) | (g_group_shift << 8) | (g_xcd_major << 12),
+                                       d_gctr, st);
+    if (le == hipErrorInvalidValue)
+      return fail(HDFS_CRC32C_EINVAL, "tiled kernel shape (order %d, nt %d, depth %d, streams %d, block %d) is not built",
+                  order, nt, depth, streams, block);
+    HIPCHK(le);
     if (ev1) HIPCHK(hipEventRecord(ev1, st));
   }
   if (gtiles) HIPCHK(launch_generic(mode, d_segs, nseg, gtiles, c.d_tab_main_t[ctype], d_fb, d_mism, st));
@@ -584,7 +618,22 @@ const char *hdfs_crc32c_last_error(void) { return g_err; }
 
 int hdfs_crc32c_init(int device) {
   DevCtx *c = nullptr;
-  return ctx_init(device, &c);
+  const int rc = ctx_init(device, &c);
+  if (rc == HDFS_CRC32C_OK && device >= 0) g_bound_dev.store(device, std::memory_order_release);
+  return rc;
+}
+
+int hdfs_crc32c_bound_device(int *device, char *pci_bus_id, size_t len) {
+  DevCtx *c = nullptr;
+  int rc = ctx_init(-1, &c);
+  if (rc) return rc;
+  if (device) *device = c->dev;
+  if (pci_bus_id && len) {
+    char buf[64] = "";
+    HIPCHK(hipDeviceGetPCIBusId(buf, int(sizeof(buf)), c->dev));
+    std::snprintf(pci_bus_id, len, "%s", buf);
+  }
+  return HDFS_CRC32C_OK;
 }
 
 int hdfs_crc32c_device_info(int device, char *arch, size_t arch_len, int *num_cu) {
@@ -828,12 +877,34 @@ int hdfs_crc32c_verify_crcdata(const void *crcdata, int32_t chunksize, int32_t c
     return fail(HDFS_CRC32C_ERR_DATANODE_CRC_LEN, "crcdlen %d != %lld", crcdlen, (long long)(nch * 4));
   if (dlen == 0) return HDFS_CRC32C_OK;
   if (!crcdata) return fail(HDFS_CRC32C_EINVAL, "null packet region");
+  const uint8_t *reg = static_cast<const uint8_t *>(crcdata);
+  {
+    // A packet beyond the one-shot staging (the reference's framing accepts
+    // up to 1 GiB, src/datanode.c:2433-2441) goes through the pipelined
+    // host path; the region is registered once so its CRC and data parts,
+    // which may share a page, are never registered separately.
+    const size_t off_crc = (size_t(dlen) + 255) & ~size_t(255);
+    const size_t off_bm = off_crc + ((size_t(crcdlen) + 255) & ~size_t(255));
+    if (off_bm + size_t((nch + 7) / 8) > kStageCap) {
+      HostRegistration whole;
+      int rc = whole.ensure(reg, size_t(crcdlen) + size_t(dlen));
+      if (rc) return rc;
+      uint64_t fb64 = UINT64_MAX, m = 0;
+      rc = host_pipeline(kModeVerify, reg + crcdlen, uint64_t(dlen), uint32_t(chunksize), HDFS_CRC32C_SEG_BE | pflag, 0,
+                         const_cast<uint8_t *>(reg), nullptr, 0, &fb64, &m);
+      if (rc) return rc;
+      if (fb64 != UINT64_MAX) {
+        if (first_bad) *first_bad = int32_t(fb64);
+        return fail(HDFS_CRC32C_ERR_DATANODE_BAD_CHECKSUM, "chunk %llu: bad checksum", (unsigned long long)fb64);
+      }
+      return HDFS_CRC32C_OK;
+    }
+  }
   DevCtx *c = nullptr;
   int rc = ctx_init(-1, &c);
   if (rc) return rc;
   DeviceGuard g(c->dev);
   std::lock_guard<std::mutex> lk(c->mu);
-  const uint8_t *reg = static_cast<const uint8_t *>(crcdata);
   if (small_ok(uint64_t(dlen), uint64_t(chunksize))) {
     std::memcpy(c->h_small_in, reg + crcdlen, size_t(dlen));
     std::memcpy(c->h_small_in + kSmallMax, reg, size_t(crcdlen));
@@ -848,8 +919,6 @@ int hdfs_crc32c_verify_crcdata(const void *crcdata, int32_t chunksize, int32_t c
   }
   const size_t off_crc = (size_t(dlen) + 255) & ~size_t(255);
   const size_t off_bm = off_crc + ((size_t(crcdlen) + 255) & ~size_t(255));
-  const size_t bm_len = size_t((nch + 7) / 8);
-  if (off_bm + bm_len > kStageCap) return fail(HDFS_CRC32C_EINVAL, "packet larger than staging");
   const uint8_t *region = static_cast<const uint8_t *>(crcdata);
   std::memcpy(c->h_stage, region + crcdlen, size_t(dlen));  // data (16-B aligned on device)
   std::memcpy(c->h_stage + off_crc, region, size_t(crcdlen));
@@ -938,18 +1007,28 @@ int hdfs_crc32c_dev_alloc(void **dptr, uint64_t bytes) {
   return HDFS_CRC32C_OK;
 }
 
+// Helpers below run on the engine's device (DeviceGuard), not on whatever
+// device the calling thread's HIP runtime has current.
+#define HDFS_ON_ENGINE_DEVICE()         \
+  DevCtx *ec_ = nullptr;                \
+  if (int rc_ = ctx_init(-1, &ec_)) return rc_; \
+  DeviceGuard eg_(ec_->dev)
+
 int hdfs_crc32c_dev_free(void *dptr) {
+  HDFS_ON_ENGINE_DEVICE();
   HIPCHK(hipFree(dptr));
   return HDFS_CRC32C_OK;
 }
 
 int hdfs_crc32c_memcpy(void *dst, const void *src, uint64_t bytes, int kind) {
   hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice : kind == 1 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
+  HDFS_ON_ENGINE_DEVICE();
   HIPCHK(hipMemcpy(dst, src, bytes, k));
   return HDFS_CRC32C_OK;
 }
 
 int hdfs_crc32c_memset(void *dptr, int value, uint64_t bytes) {
+  HDFS_ON_ENGINE_DEVICE();
   HIPCHK(hipMemset(dptr, value, bytes));
   return HDFS_CRC32C_OK;
 }
@@ -958,6 +1037,7 @@ int hdfs_crc32c_stream_create(void **stream) {
   DevCtx *c = nullptr;
   int rc = ctx_init(-1, &c);
   if (rc) return rc;
+  DeviceGuard g(c->dev);
   hipStream_t s;
   HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   *stream = s;
@@ -965,16 +1045,19 @@ int hdfs_crc32c_stream_create(void **stream) {
 }
 
 int hdfs_crc32c_stream_destroy(void *stream) {
+  HDFS_ON_ENGINE_DEVICE();
   HIPCHK(hipStreamDestroy(static_cast<hipStream_t>(stream)));
   return HDFS_CRC32C_OK;
 }
 
 int hdfs_crc32c_stream_sync(void *stream) {
+  HDFS_ON_ENGINE_DEVICE();
   HIPCHK(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
   return HDFS_CRC32C_OK;
 }
 
 int hdfs_crc32c_fill_splitmix64(void *dptr, uint64_t nwords, uint64_t seed, uint64_t g0, void *stream) {
+  HDFS_ON_ENGINE_DEVICE();
   HIPCHK(launch_fill(static_cast<uint64_t *>(dptr), nwords, seed, g0, static_cast<hipStream_t>(stream)));
   return HDFS_CRC32C_OK;
 }
@@ -983,6 +1066,7 @@ int hdfs_crc32c_corrupt(void *dptr, uint64_t len, uint32_t chunk, uint64_t chunk
                         uint64_t bitmul, void *stream) {
   if (!chunk || !modulus) return fail(HDFS_CRC32C_EINVAL, "chunk/modulus 0");
   if (!len) return HDFS_CRC32C_OK;
+  HDFS_ON_ENGINE_DEVICE();
   HIPCHK(launch_corrupt(static_cast<uint8_t *>(dptr), len, chunk, chunk0, modulus, bitmul,
                         static_cast<hipStream_t>(stream)));
   return HDFS_CRC32C_OK;
@@ -1005,6 +1089,7 @@ int hdfs_crc32c_host_alloc(void **p, uint64_t bytes) {
   DevCtx *c = nullptr;
   int rc = ctx_init(-1, &c);
   if (rc) return rc;
+  DeviceGuard g(c->dev);
   hipError_t e = hipHostMalloc(p, bytes ? bytes : 1, hipHostMallocDefault);
   if (e != hipSuccess) return fail(HDFS_CRC32C_ENOMEM, "hipHostMalloc(%llu): %s", (unsigned long long)bytes,
                                    hipGetErrorString(e));
@@ -1012,15 +1097,19 @@ int hdfs_crc32c_host_alloc(void **p, uint64_t bytes) {
 }
 
 int hdfs_crc32c_host_free(void *p) {
+  HDFS_ON_ENGINE_DEVICE();
   HIPCHK(hipHostFree(p));
   return HDFS_CRC32C_OK;
 }
 
 int hdfs_crc32c_device_sync(void) {
+  HDFS_ON_ENGINE_DEVICE();
   HIPCHK(hipDeviceSynchronize());
   return HDFS_CRC32C_OK;
 }
 
+#ifdef HDFS_CRC32C_DIAG
+// ---- diagnostic build only (include/hadoofus_crc32c_diag.h) ----
 int hdfs_crc32c_set_store_policy(int policy) {
   if (policy < 0 || policy > 4) return fail(HDFS_CRC32C_EINVAL, "store policy 0..4");
   g_store_policy = uint32_t(policy);
@@ -1051,6 +1140,12 @@ int hdfs_crc32c_set_tuning(int nt_loads, void *diag) {
 int hdfs_crc32c_set_group_shift(int shift) {
   if (shift < 0 || shift > 6) return fail(HDFS_CRC32C_EINVAL, "group shift must be 0..6");
   g_group_shift = uint32_t(shift);
+  return HDFS_CRC32C_OK;
+}
+
+int hdfs_crc32c_set_xcd_major(int on) {
+  if (on != 0 && on != 1) return fail(HDFS_CRC32C_EINVAL, "xcd_major must be 0 or 1");
+  g_xcd_major = uint32_t(on);
   return HDFS_CRC32C_OK;
 }
 
@@ -1094,6 +1189,7 @@ int hdfs_crc32c_probe_read(const void *dptr, uint64_t bytes, void *stream, int i
   *gbps = double(bytes) * iters / (ms * 1e-3) / 1e9;
   return HDFS_CRC32C_OK;
 }
+#endif  // HDFS_CRC32C_DIAG
 
 int hdfs_crc32c_composite_crcs(const hdfs_crc32c_segment *segs, size_t nseg, uint32_t *out) {
   if (nseg && (!segs || !out)) return fail(HDFS_CRC32C_EINVAL, "null segments / out");

@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdarg>
 #include <cstddef>
 #include <cstdint>
@@ -77,7 +78,9 @@ struct PieceSlot {
 };
 
 struct DevCtx {
-  bool ready = false;
+  // published with release after every field below is set up; the unlocked
+  // fast path of ctx_init reads it with acquire
+  std::atomic<bool> ready{false};
   int dev = -1;
   int num_cu = 0;
   char arch[64] = "";
@@ -133,7 +136,6 @@ struct DevCtx {
 };
 
 extern DevCtx g_ctx[kMaxDev];
-extern int g_tile_order;
 
 struct DeviceGuard {
   int prev = -1;

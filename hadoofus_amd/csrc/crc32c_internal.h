@@ -5,6 +5,17 @@
 
 namespace hdfs_crc32c {
 
+// Diagnostic build (libhadoofus_crc32c_diag.so, -DHDFS_CRC32C_DIAG, for
+// tools/ and the bench's ceiling measurement): tuning shapes, the load-only
+// twin, store-policy experiments, per-wave clock stamps and read probes.
+// The release library compiles none of them and reads no tuning knob from
+// the environment: nothing outside the code can change what it computes.
+#ifdef HDFS_CRC32C_DIAG
+constexpr bool kDiag = true;
+#else
+constexpr bool kDiag = false;
+#endif
+
 // Segment flags (also mirrored as HDFS_CRC32C_SEG_* in the public header).
 enum : uint32_t {
   kSegBigEndian = 1u,  // crcs[] are in wire byte order (src/util.h:68-92)
@@ -13,7 +24,7 @@ enum : uint32_t {
 
 // kModeLoadOnly: diagnostic twin of verify (same loads, same store ops with
 // their records dropped, no CRC arithmetic) -- the kernel's own memory
-// ceiling, for DESIGN.md; never used by the product path.
+// ceiling, for DESIGN.md; instantiated only in the diagnostic build.
 enum Mode : int { kModeCompute = 0, kModeVerify = 1, kModeLoadOnly = 2 };
 
 // One entry of the device-resident segment table.  A segment is one chunk

@@ -372,7 +372,9 @@ DEV void issue(uint32_t (&d)[16], uint32_t &exp, const Cursor c, SegP segs, uint
 
 struct LaneConst {
   uint32_t lane, hsel, loff, lb0, lb1, qi, qg, zk, zbase, z448;
-  uint32_t store_policy;  // 0 default, 1 nontemporal, 2 diagnostic: drop result stores
+  // 0 default; diagnostic build only: 1 nontemporal, 2 drop result stores,
+  // 3 full-line CRC writes (always 0 in the release build)
+  uint32_t store_policy;
 };
 
 // Finish one round of one stream after its 16 slicing steps: on a tile's
@@ -410,9 +412,9 @@ DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, ui
   }
   byte = rfl(byte);
   if (MODE == kModeCompute) {
-    const bool keep = last && L.store_policy != 2;
+    const bool keep = last && !(kDiag && L.store_policy == 2);
     const uint32_t val = (flags & kSegBigEndian) ? __builtin_bswap32(out) : out;
-    if (L.store_policy == 3) {
+    if (kDiag && L.store_policy == 3) {
       // diagnostic: 128-B full-line write per tile (crcs must hold 16 B per chunk)
       const __amdgpu_buffer_rsrc_t r4 = __builtin_amdgcn_make_buffer_rsrc(
           segs[c.seg].crcs + c.tile * kTileChunks * 4, 0, last ? static_cast<int>(nch * 16u) : 0, 0x00020000);
@@ -426,13 +428,13 @@ DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, ui
           reinterpret_cast<uint32_t *>(rfl64(reinterpret_cast<uint64_t>(sh.crcs + c.tile * kTileChunks))), 0,
           static_cast<int>(rfl(keep ? nch * 4u : 0u)), 0x00020000);
       const uint32_t off = leader ? L.qg * 4u : 0x80000000u;
-      if (L.store_policy == 1) __builtin_amdgcn_raw_buffer_store_b32(val, rs, off, 0, 2);  // nt
+      if (kDiag && L.store_policy == 1) __builtin_amdgcn_raw_buffer_store_b32(val, rs, off, 0, 2);  // nt
       else __builtin_amdgcn_raw_buffer_store_b32(val, rs, off, 0, 0);
     }
   } else {
     const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
         reinterpret_cast<uint8_t *>(rfl64(reinterpret_cast<uint64_t>(sh.bitmap + c.tile))), 0,
-        static_cast<int>(rfl((last && L.store_policy != 2) ? 1u : 0u)), 0x00020000);
+        static_cast<int>(rfl((last && !(kDiag && L.store_policy == 2)) ? 1u : 0u)), 0x00020000);
     __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(byte), rb, L.lane == 0 ? 0u : 0x80000000u, 0, 0);
     if (byte && L.lane == 0) {  // rare: only tiles with a mismatch
       atomicMin(&first_bad[c.seg], c.tile * kTileChunks + __builtin_ctz(byte));
@@ -449,7 +451,7 @@ template <int MODE, int S>
 DEV void process(const uint32_t *lds, uint32_t (&d)[S][16], const uint32_t (&exp)[S], const Cursor (&c)[S],
                  SegP segs, uint32_t (&st)[S], const LaneConst &L, uint32_t *__restrict__ first_bad,
                  unsigned long long *__restrict__ mism, SegCache (&kc)[S]) {
-  if constexpr (MODE == kModeLoadOnly) {
+  if constexpr (kDiag && MODE == kModeLoadOnly) {
 #pragma unroll
     for (int s = 0; s < S; s++) {
       uint32_t v = exp[s];
@@ -537,7 +539,9 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
   __syncthreads();
 
   LaneConst L;
-  L.store_policy = rfl(tune & 0xffu);  // tune: [7:0] store policy, [11:8] ORDER-3 group shift (uniform: SGPR)
+  // tune: [7:0] store policy (diagnostic build), [11:8] ORDER-3 group shift,
+  // [12] ORDER-3 XCD-major dealing (uniform: SGPR)
+  L.store_policy = kDiag ? rfl(tune & 0xffu) : 0u;
   L.lane = threadIdx.x & 63u;
   L.hsel = (L.lane >> 3) & 1u;                              // load: odd sub-chunk of each 1 KiB
   L.loff = 16u * (4u * (L.lane & 7u) + (L.lane >> 4));      // load: byte offset in the sub-chunk
@@ -555,7 +559,7 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
   const SegP sg = (SegP)(segs);
   // Diagnostic build path (diag != nullptr): per-wave start / end wall clock
   // (s_memrealtime, 100 MHz) and rounds processed; nothing is computed from it.
-  if (diag && L.lane == 0) diag[3 * wave] = __builtin_amdgcn_s_memrealtime();
+  if (kDiag && diag && L.lane == 0) diag[3 * wave] = __builtin_amdgcn_s_memrealtime();
   uint64_t nrounds = 0;
   Sched w{0, 0, 0, &lds[kLdsWords], L.lane};
   Cursor cur[DEPTH][S];
@@ -583,10 +587,16 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
       // static phase: whole groups only; the pool takes the rest
       w.gshift = (tune >> 8) & 15u;
       const uint64_t ngroups = (pool ? total_tiles * kPhase1Num / kPhase1Den : total_tiles) >> w.gshift;
-      w.gfirst = blockIdx.x;
+      // tune bit 12: XCD-major dealing.  Workgroups are dispatched to the 8
+      // XCDs round-robin (XCD = blockIdx % 8), so with the plain dealing the
+      // groups an XCD works on at one time are 8 apart; dealing by the
+      // virtual id (blockIdx % 8) * (G / 8) + blockIdx / 8 gives each XCD
+      // (and its L2) a contiguous run of G / 8 groups per sweep step.
+      const uint32_t b = blockIdx.x, G = gridDim.x;
+      w.gfirst = ((tune >> 12) & 1u) && (G % 8u) == 0 ? (b % 8u) * (G / 8u) + b / 8u : b;
       w.gstride = gridDim.x;
-      w.nk = ngroups > blockIdx.x ? static_cast<uint32_t>(((ngroups - 1 - blockIdx.x) / gridDim.x + 1) << w.gshift)
-                                  : 0u;
+      w.nk = ngroups > w.gfirst ? static_cast<uint32_t>(((ngroups - 1 - w.gfirst) / gridDim.x + 1) << w.gshift)
+                                : 0u;
       w.p2first = ngroups << w.gshift;
     } else {
       const uint64_t r_static = pool ? total_rounds * kPhase1Num / kPhase1Den : total_rounds;
@@ -622,7 +632,7 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
 #pragma unroll
   for (int s = 0; s < S; s++) any |= cur[0][s].valid;
   if (!any) {
-    if (diag && L.lane == 0) diag[3 * wave + 1] = __builtin_amdgcn_s_memrealtime();
+    if (kDiag && diag && L.lane == 0) diag[3 * wave + 1] = __builtin_amdgcn_s_memrealtime();
     return;
   }
   // A stream that got no tile parks on stream 0's position (valid = false):
@@ -679,7 +689,7 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
     for (int s = 0; s < S; s++) more |= cur[0][s].valid;
     if (!more) break;
   }
-  if (diag && L.lane == 0) {
+  if (kDiag && diag && L.lane == 0) {
     diag[3 * wave + 1] = __builtin_amdgcn_s_memrealtime();
     diag[3 * wave + 2] = nrounds;
   }
@@ -1148,45 +1158,66 @@ hipError_t launch_tiles(int mode, int order, int nt, int depth, int streams, int
                         const SegDev *segs, uint32_t nseg, uint64_t total_rounds, uint64_t total_tiles,
                         const uint32_t *gtab, uint32_t *first_bad, unsigned long long *mism,
                         unsigned long long *diag, uint32_t tune, uint32_t *gctr, hipStream_t stream) {
-#define HDFS_LAUNCH(M, O, N, D, S, B)                                                                     \
-  hipLaunchKernelGGL((crc32c_tiles_kernel<M, O, N, D, S, B>), dim3(grid), dim3(B), 0, stream, segs, nseg, \
+#define HDFS_LAUNCH(M, O, N, D, S, B, BUF)                                                                      \
+  hipLaunchKernelGGL((crc32c_tiles_kernel<M, O, N, D, S, B, BUF>), dim3(grid), dim3(B), 0, stream, segs, nseg, \
                      total_rounds, total_tiles, gtab, first_bad, mism, diag, tune, gctr)
-#define HDFS_LAUNCH_B(M, O, N, D, S, B)                                                                      \
-  hipLaunchKernelGGL((crc32c_tiles_kernel<M, O, N, D, S, B, 1>), dim3(grid), dim3(B), 0, stream, segs, nseg, \
-                     total_rounds, total_tiles, gtab, first_bad, mism, diag, tune, gctr)
-  // Shapes other than (depth 3, 1 stream, 1024 threads) exist for schedule 3
-  // only (tuning experiments, tools/exp_ab.py); anything else falls back to
-  // the default shape of the requested schedule.
-#define HDFS_LAUNCH_M(M)                                                                \
-  do {                                                                                  \
-    if (order == 3 && nt == 2 && depth == 3 && streams == 1 && block == 1024) HDFS_LAUNCH_B(M, 3, 1, 3, 1, 1024); \
-    else if (order == 3 && depth == 2 && streams == 2 && block == 1024) HDFS_LAUNCH(M, 3, 1, 2, 2, 1024); \
-    else if (order == 3 && depth == 3 && streams == 2 && block == 1024) HDFS_LAUNCH(M, 3, 1, 3, 2, 1024); \
-    else if (order == 3 && depth == 3 && streams == 2 && block == 768) HDFS_LAUNCH(M, 3, 1, 3, 2, 768); \
-    else if (order == 3 && depth == 2 && streams == 2 && block == 512) HDFS_LAUNCH(M, 3, 1, 2, 2, 512); \
-    else if (order == 3 && depth == 3 && streams == 2 && block == 512) HDFS_LAUNCH(M, 3, 1, 3, 2, 512); \
-    else if (order == 3 && depth == 2 && streams == 4 && block == 512) HDFS_LAUNCH(M, 3, 1, 2, 4, 512); \
-    else if (order == 3 && depth == 3 && streams == 1 && block == 768) HDFS_LAUNCH(M, 3, 1, 3, 1, 768); \
-    else if (order == 3 && depth == 3 && streams == 1 && block == 512) HDFS_LAUNCH(M, 3, 1, 3, 1, 512); \
-    else if (order == 3 && depth == 4) HDFS_LAUNCH(M, 3, 1, 4, 1, 1024);                \
-    else if (order == 3) HDFS_LAUNCH(M, 3, 1, 3, 1, 1024);                              \
-    else if (order == 2 && depth == 4) HDFS_LAUNCH(M, 2, 1, 4, 1, 1024);                \
-    else if (order == 2) HDFS_LAUNCH(M, 2, 1, 3, 1, 1024);                              \
-    else if (depth == 4) HDFS_LAUNCH(M, 1, 1, 4, 1, 1024);                              \
-    else if (order && nt) HDFS_LAUNCH(M, 1, 1, 3, 1, 1024);                             \
-    else if (order) HDFS_LAUNCH(M, 1, 0, 3, 1, 1024);                                   \
-    else if (nt) HDFS_LAUNCH(M, 0, 1, 3, 1, 1024);                                      \
-    else HDFS_LAUNCH(M, 0, 0, 3, 1, 1024);                                              \
-  } while (0)
-  if (mode == kModeLoadOnly) HDFS_LAUNCH(kModeLoadOnly, 3, 1, 3, 1, 1024);
-  else if (mode == kModeVerify) HDFS_LAUNCH_M(kModeVerify);
-  else HDFS_LAUNCH_M(kModeCompute);
-#undef HDFS_LAUNCH_M
-#undef HDFS_LAUNCH_B
+#define HDFS_SHAPE(O, N, D, S, B) (order == (O) && nt == (N) && depth == (D) && streams == (S) && block == (B))
+  if (mode != kModeCompute && mode != kModeVerify && !(kDiag && mode == kModeLoadOnly)) return hipErrorInvalidValue;
+  // Release build: the two product shapes only -- schedule 3 with nontemporal
+  // buffer loads (nt 2), and schedule 2 (small launches / tables of small
+  // segments) with nontemporal global loads; depth 3, one tile stream, 1024
+  // threads.  Anything else is refused, never silently replaced.
+#define HDFS_LAUNCH_PRODUCT(M)                                                                  \
+  if (HDFS_SHAPE(3, 2, 3, 1, 1024)) HDFS_LAUNCH(M, 3, 1, 3, 1, 1024, 1);                        \
+  else if (HDFS_SHAPE(2, 1, 3, 1, 1024)) HDFS_LAUNCH(M, 2, 1, 3, 1, 1024, 0);
+#ifndef HDFS_CRC32C_DIAG
+  if (mode == kModeVerify) {
+    HDFS_LAUNCH_PRODUCT(kModeVerify)
+    else return hipErrorInvalidValue;
+  } else {
+    HDFS_LAUNCH_PRODUCT(kModeCompute)
+    else return hipErrorInvalidValue;
+  }
+#else
+  // Diagnostic build: the tuning shapes of tools/exp_ab.py and
+  // tests/test_gpu_shapes.py, each launched only when requested exactly.
+#define HDFS_LAUNCH_ALL(M)                                                                      \
+  HDFS_LAUNCH_PRODUCT(M)                                                                        \
+  else if (HDFS_SHAPE(3, 1, 3, 1, 1024)) HDFS_LAUNCH(M, 3, 1, 3, 1, 1024, 0);                   \
+  else if (HDFS_SHAPE(3, 1, 4, 1, 1024)) HDFS_LAUNCH(M, 3, 1, 4, 1, 1024, 0);                   \
+  else if (HDFS_SHAPE(3, 1, 2, 2, 1024)) HDFS_LAUNCH(M, 3, 1, 2, 2, 1024, 0);                   \
+  else if (HDFS_SHAPE(3, 1, 3, 2, 1024)) HDFS_LAUNCH(M, 3, 1, 3, 2, 1024, 0);                   \
+  else if (HDFS_SHAPE(3, 1, 3, 2, 768)) HDFS_LAUNCH(M, 3, 1, 3, 2, 768, 0);                     \
+  else if (HDFS_SHAPE(3, 1, 2, 2, 512)) HDFS_LAUNCH(M, 3, 1, 2, 2, 512, 0);                     \
+  else if (HDFS_SHAPE(3, 1, 3, 2, 512)) HDFS_LAUNCH(M, 3, 1, 3, 2, 512, 0);                     \
+  else if (HDFS_SHAPE(3, 1, 2, 4, 512)) HDFS_LAUNCH(M, 3, 1, 2, 4, 512, 0);                     \
+  else if (HDFS_SHAPE(3, 1, 3, 1, 768)) HDFS_LAUNCH(M, 3, 1, 3, 1, 768, 0);                     \
+  else if (HDFS_SHAPE(3, 1, 3, 1, 512)) HDFS_LAUNCH(M, 3, 1, 3, 1, 512, 0);                     \
+  else if (HDFS_SHAPE(2, 1, 4, 1, 1024)) HDFS_LAUNCH(M, 2, 1, 4, 1, 1024, 0);                   \
+  else if (HDFS_SHAPE(1, 1, 3, 1, 1024)) HDFS_LAUNCH(M, 1, 1, 3, 1, 1024, 0);                   \
+  else if (HDFS_SHAPE(1, 1, 4, 1, 1024)) HDFS_LAUNCH(M, 1, 1, 4, 1, 1024, 0);                   \
+  else if (HDFS_SHAPE(1, 0, 3, 1, 1024)) HDFS_LAUNCH(M, 1, 0, 3, 1, 1024, 0);                   \
+  else if (HDFS_SHAPE(0, 1, 3, 1, 1024)) HDFS_LAUNCH(M, 0, 1, 3, 1, 1024, 0);                   \
+  else if (HDFS_SHAPE(0, 0, 3, 1, 1024)) HDFS_LAUNCH(M, 0, 0, 3, 1, 1024, 0);
+  if (mode == kModeLoadOnly) {
+    if (HDFS_SHAPE(3, 2, 3, 1, 1024)) HDFS_LAUNCH(kModeLoadOnly, 3, 1, 3, 1, 1024, 1);
+    else return hipErrorInvalidValue;
+  } else if (mode == kModeVerify) {
+    HDFS_LAUNCH_ALL(kModeVerify)
+    else return hipErrorInvalidValue;
+  } else {
+    HDFS_LAUNCH_ALL(kModeCompute)
+    else return hipErrorInvalidValue;
+  }
+#undef HDFS_LAUNCH_ALL
+#endif
+#undef HDFS_LAUNCH_PRODUCT
+#undef HDFS_SHAPE
 #undef HDFS_LAUNCH
   return hipGetLastError();
 }
 
+#ifdef HDFS_CRC32C_DIAG
 // Streaming-read probe: the empirical HBM read roofline for 16-B-per-lane
 // fully coalesced loads, no compute.  NLOAD loads in flight per lane, NT =
 // nontemporal policy.
@@ -1258,6 +1289,8 @@ hipError_t launch_probe_read(const uint8_t *p, uint64_t nbytes, uint32_t *out, i
   }
   return hipGetLastError();
 }
+
+#endif  // HDFS_CRC32C_DIAG
 
 hipError_t launch_generic(int mode, const SegDev *segs, uint32_t nseg, uint64_t total_gtiles,
                           const uint32_t *gtab, uint32_t *first_bad, unsigned long long *mism,

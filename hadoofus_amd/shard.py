@@ -33,6 +33,40 @@ def expected_bad(first_block, nblocks, chunks_per_block, modulus=65537):
     return 0 if first >= end else (end - 1 - first) // modulus + 1
 
 
+# BASELINE.json configs: C3 = 1024 x 128 MiB blocks per GPU (weak scaling,
+# the headline), C4 = 64 GiB = 512 blocks for the whole node, split evenly
+# (strong scaling).
+WORKLOADS = {"C3": ("weak", 1024), "C4": ("strong", 512)}
+
+
+def workload_blocks(config, rank, world, blocks=None):
+    """-> (scaling, first global block, blocks of this rank) for a bench
+    config; blocks overrides the config's block count (per rank for weak,
+    total for strong)."""
+    scaling, n = WORKLOADS[config]
+    n = n if blocks is None else blocks
+    if scaling == "weak":
+        b0, nb = rank_blocks(rank, world, n)
+    else:
+        b0, nb = split_blocks(n, rank, world)
+    return scaling, b0, nb
+
+
+def check_distinct_devices(infos):
+    """infos: one dict per rank with 'rank' and 'pci_bus_id' (the GPU the
+    rank's engine is bound to).  Raises if two ranks share a GPU -- e.g. every
+    rank silently landing on device 0."""
+    seen = {}
+    for inf in infos:
+        bus = inf["pci_bus_id"]
+        if not bus:
+            raise RuntimeError(f"rank {inf['rank']} reported no PCI bus id")
+        if bus in seen:
+            raise RuntimeError(f"ranks {seen[bus]} and {inf['rank']} share GPU {bus}")
+        seen[bus] = inf["rank"]
+    return len(seen)
+
+
 def launched_by_torchrun():
     return "TORCHELASTIC_RUN_ID" in os.environ or int(os.environ.get("WORLD_SIZE", "1")) > 1
 
@@ -68,6 +102,12 @@ class Collective:
         self.dist.all_reduce(t, op=getattr(self.dist.ReduceOp, op))
         return t.tolist()
 
+    def gather(self, obj):
+        """All ranks' picklable obj, in rank order (all_gather_object)."""
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
+
     def aggregate(self, nbytes, mismatches, ok, elapsed):
         """-> (total bytes, total mismatches, ranks ok, max elapsed)."""
         s = self.allreduce([float(nbytes), float(mismatches), float(bool(ok))], "SUM")
@@ -86,6 +126,9 @@ class Local:
 
     def barrier(self):
         pass
+
+    def gather(self, obj):
+        return [obj]
 
     def aggregate(self, nbytes, mismatches, ok, elapsed):
         return float(nbytes), float(mismatches), int(bool(ok)), float(elapsed)

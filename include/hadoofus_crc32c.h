@@ -12,6 +12,10 @@
  *    function.  All three run on the GPU engine; with no usable GPU they
  *    abort() with a message (there is no CPU fallback).
  *
+ * The release library has no tuning or diagnostic knobs: it reads nothing
+ * from the environment that changes what it computes.  Those live in the
+ * separate diagnostic build, include/hadoofus_crc32c_diag.h.
+ *
  * 2. BATCH (additive): per-chunk compute / verify over a table of chunk
  *    streams in device memory, the shape of the two datanode loops
  *    (src/datanode.c:2814-2860 write compute, src/datanode.c:2931-2963 read
@@ -57,9 +61,17 @@ uint32_t _hdfs_sw_crc32c(uint32_t crc, const void *buf, unsigned len);
 #define HDFS_CRC32C_CSUM_CRC32C 2
 
 const char *hdfs_crc32c_last_error(void);
-/* Initialise the engine on `device` (-1: the calling thread's current HIP
- * device).  Called implicitly by every entry point. */
+/* Initialise the engine on `device`.  device >= 0 also BINDS the engine to
+ * it: every later call that names no device (all of them) runs there, with
+ * no reliance on the caller's current-device state (one process per GPU:
+ * a rank calls hdfs_crc32c_init(LOCAL_RANK) first).  -1: the bound device,
+ * else the calling thread's current HIP device.  Called implicitly (with -1)
+ * by every entry point. */
 int hdfs_crc32c_init(int device);
+/* The device the engine runs on (ordinal in this process) and its PCI bus
+ * id ("0000:xx:00.0", hipDeviceGetPCIBusId), so launchers can check that
+ * ranks landed on distinct GPUs. */
+int hdfs_crc32c_bound_device(int *device, char *pci_bus_id, size_t len);
 /* gfx arch string of the engine's device, e.g. "gfx950". */
 int hdfs_crc32c_device_info(int device, char *arch, size_t arch_len, int *num_cu);
 
@@ -289,44 +301,6 @@ int hdfs_crc32c_corrupt(void *dptr, uint64_t len, uint32_t chunk, uint64_t chunk
 int hdfs_crc32c_plan_time(hdfs_crc32c_plan *plan, void *stream, int iters, double *ms_per_iter);
 /* hipDeviceSynchronize on the engine's device. */
 int hdfs_crc32c_device_sync(void);
-/* Tiled-kernel schedule: 0 static per-wave slices, 1 workgroup-dynamic,
- * 2 workgroup-dynamic over contiguous slices of 92 % of the tiles + a global
- * pool of 16-256-tile units, 3 (default) as 2 but the static 92 % dealt
- * round-robin over the workgroups (the grid sweeps one contiguous window;
- * launches that are small or made of small segments fall back to 2).
- * Waves of a workgroup take tiles from an LDS counter.  Env
- * HDFS_CRC32C_TILE_ORDER. */
-int hdfs_crc32c_set_tile_order(int order);
-/* Schedule 3: 2^shift consecutive tiles per round-robin group (default 3:
- * 32 KiB of 512-B chunks, two whole 128-B lines of CRCs per group).  Env
- * HDFS_CRC32C_GROUP. */
-int hdfs_crc32c_set_group_shift(int shift);
-/* Tuning / diagnostics: nt_loads=1 streams chunk data with nontemporal global loads,
- * 2 (default) with nontemporal buffer loads (schedule 3 default shape; other
- * schedules and shapes use 1), 0 default-policy loads (env HDFS_CRC32C_NT); diag = device u64[3 * waves] receiving per-wave
- * start/end s_memrealtime stamps and rounds processed (NULL = off). */
-int hdfs_crc32c_set_tuning(int nt_loads, void *diag);
-/* Register round buffers per tile stream of the tiled kernel (2..4; depth-1
- * rounds stay in flight while one is processed).  Env HDFS_CRC32C_DEPTH. */
-int hdfs_crc32c_set_depth(int depth);
-/* Tiled-kernel shape: independent tile streams per wave (1, 2, 4) and
- * threads per workgroup (512, 768, 1024).  Shapes other than (1, 1024) are
- * built for schedule 3 only; other combinations run the default shape.
- * Env HDFS_CRC32C_STREAMS / HDFS_CRC32C_BLOCK. */
-int hdfs_crc32c_set_shape(int streams, int block);
-/* Compute-mode result store policy: 0 default, 1 nontemporal, 2 diagnostic
- * (stores dropped; output undefined -- timing experiments only), 4
- * diagnostic: verify plans run a load-only twin of the kernel (same loads and
- * store ops, no CRC arithmetic, results undefined) -- the memory ceiling of
- * the kernel's access pattern.
- * Env HDFS_CRC32C_STORE. */
-int hdfs_crc32c_set_store_policy(int policy);
-/* Empirical streaming-read bandwidth of `bytes` at dptr (GB/s, 1e9 B/s):
- * fully coalesced 16-B-per-lane loads, no compute; the measured roofline. */
-int hdfs_crc32c_probe_read(const void *dptr, uint64_t bytes, void *stream, int iters, double *gbps);
-/* Probe shape (diagnostics): variant 0..4 = {4 loads, 4 nt, 8, 8 nt, 16 nt}
- * in flight per lane; grid = grid_per_cu x CUs blocks of `block` threads. */
-int hdfs_crc32c_set_probe(int variant, int grid_per_cu, int block);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,70 @@
+/*
+ * hadoofus_crc32c_diag.h -- DIAGNOSTIC build of the CRC32C engine
+ * (libhadoofus_crc32c_diag.so, compiled with -DHDFS_CRC32C_DIAG).
+ *
+ * The diagnostic library exports everything in hadoofus_crc32c.h plus the
+ * tuning and measurement knobs below, which the release library
+ * (libhadoofus_crc32c.so) does not contain: alternative tiled-kernel
+ * schedules and shapes, per-wave clock stamps, streaming-read probes, and
+ * store policies that DROP results (a load-only twin of the verify kernel
+ * that does no CRC arithmetic).  Used by tools/ experiments and by
+ * bench.py's empirical-ceiling measurement; never by a datanode.
+ * Environment overrides (HDFS_CRC32C_TILE_ORDER, _NT, _DEPTH, _STREAMS,
+ * _BLOCK, _STORE, _GROUP, _ALIGN, _SMALL_RULE) are read by this build only.
+ */
+#ifndef HADOOFUS_CRC32C_DIAG_H
+#define HADOOFUS_CRC32C_DIAG_H
+
+#include "hadoofus_crc32c.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+/* Tiled-kernel schedule: 0 static per-wave slices, 1 workgroup-dynamic,
+ * 2 workgroup-dynamic over contiguous slices of 92 % of the tiles + a global
+ * pool of 16-256-tile units, 3 (default) as 2 but the static 92 % dealt
+ * round-robin over the workgroups (the grid sweeps one contiguous window;
+ * launches that are small or made of small segments fall back to 2).
+ * Waves of a workgroup take tiles from an LDS counter.  Env
+ * HDFS_CRC32C_TILE_ORDER. */
+int hdfs_crc32c_set_tile_order(int order);
+/* Schedule 3: 2^shift consecutive tiles per round-robin group (default 3:
+ * 32 KiB of 512-B chunks, two whole 128-B lines of CRCs per group).  Env
+ * HDFS_CRC32C_GROUP. */
+int hdfs_crc32c_set_group_shift(int shift);
+/* Schedule 3: deal the static groups XCD-major (workgroup b takes virtual
+ * slot (b % 8) * (G / 8) + b / 8, so each XCD sweeps a contiguous run of
+ * groups) instead of by workgroup id.  Env HDFS_CRC32C_XCD. */
+int hdfs_crc32c_set_xcd_major(int on);
+/* Tuning / diagnostics: nt_loads=1 streams chunk data with nontemporal global loads,
+ * 2 (default) with nontemporal buffer loads (schedule 3 default shape; other
+ * schedules and shapes use 1), 0 default-policy loads (env HDFS_CRC32C_NT); diag = device u64[3 * waves] receiving per-wave
+ * start/end s_memrealtime stamps and rounds processed (NULL = off). */
+int hdfs_crc32c_set_tuning(int nt_loads, void *diag);
+/* Register round buffers per tile stream of the tiled kernel (2..4; depth-1
+ * rounds stay in flight while one is processed).  Env HDFS_CRC32C_DEPTH. */
+int hdfs_crc32c_set_depth(int depth);
+/* Tiled-kernel shape: independent tile streams per wave (1, 2, 4) and
+ * threads per workgroup (512, 768, 1024).  Only the shapes built into
+ * launch_tiles run; any other combination fails (EINVAL) at launch.
+ * Env HDFS_CRC32C_STREAMS / HDFS_CRC32C_BLOCK. */
+int hdfs_crc32c_set_shape(int streams, int block);
+/* Compute-mode result store policy: 0 default, 1 nontemporal, 2 diagnostic
+ * (stores dropped; output undefined -- timing experiments only), 4
+ * diagnostic: verify plans run a load-only twin of the kernel (same loads and
+ * store ops, no CRC arithmetic, results undefined) -- the memory ceiling of
+ * the kernel's access pattern.
+ * Env HDFS_CRC32C_STORE. */
+int hdfs_crc32c_set_store_policy(int policy);
+/* Empirical streaming-read bandwidth of `bytes` at dptr (GB/s, 1e9 B/s):
+ * fully coalesced 16-B-per-lane loads, no compute; the measured roofline. */
+int hdfs_crc32c_probe_read(const void *dptr, uint64_t bytes, void *stream, int iters, double *gbps);
+/* Probe shape (diagnostics): variant 0..4 = {4 loads, 4 nt, 8, 8 nt, 16 nt}
+ * in flight per lane; grid = grid_per_cu x CUs blocks of `block` threads. */
+int hdfs_crc32c_set_probe(int variant, int grid_per_cu, int block);
+
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HADOOFUS_CRC32C_DIAG_H */

@@ -32,6 +32,51 @@ def test_headers_compile_as_c(tmp_path):
                            "-c", str(src), "-o", str(tmp_path / "t.o")])
 
 
+@pytest.fixture(scope="module")
+def diagpath(libpath):
+    from hadoofus_amd import build
+    return build.DIAG_LIB
+
+
+def _exported(path):
+    out = subprocess.check_output(["nm", "-D", "--defined-only", path], text=True)
+    return set(l.split()[-1] for l in out.splitlines() if l.strip())
+
+
+def test_release_has_no_diagnostic_knobs(libpath, diagpath):
+    """The release library exports none of include/hadoofus_crc32c_diag.h and
+    reads none of the tuning variables (the strings are not even in it); the
+    diagnostic build exports and reads them all."""
+    diag_decl = set(_declared("hadoofus_crc32c_diag.h"))
+    assert {"hdfs_crc32c_set_store_policy", "hdfs_crc32c_probe_read", "hdfs_crc32c_set_tile_order"} <= diag_decl
+    assert not diag_decl & _exported(libpath)
+    assert diag_decl <= _exported(diagpath)
+    rel = open(libpath, "rb").read()
+    dia = open(diagpath, "rb").read()
+    for var in (b"HDFS_CRC32C_STORE", b"HDFS_CRC32C_TILE_ORDER", b"HDFS_CRC32C_NT", b"HDFS_CRC32C_DEPTH",
+                b"HDFS_CRC32C_STREAMS", b"HDFS_CRC32C_BLOCK", b"HDFS_CRC32C_GROUP", b"HDFS_CRC32C_ALIGN",
+                b"HDFS_CRC32C_SMALL_RULE", b"HDFS_CRC32C_XCD"):
+        assert var not in rel, var
+        assert var in dia, var
+
+
+def test_release_kernels_are_the_product_shapes(libpath, diagpath):
+    """Four tiled-kernel instantiations in the release build (compute /
+    verify x schedule 3 buffer loads / schedule 2), no load-only twin
+    (mode 2) and no read probes; the diagnostic build has them."""
+    import re as _re
+    rel = open(libpath, "rb").read()
+    dia = open(diagpath, "rb").read()
+    pat = rb"_ZN11hdfs_crc32c19crc32c_tiles_kernelILi(\d)ELi(\d)ELi(\d)ELi(\d)ELi(\d)ELi(\d+)ELi(\d)EEE"
+    shapes = set(_re.findall(pat, rel))
+    assert shapes == {(m, o, b"1", b"3", b"1", b"1024", buf) for m in (b"0", b"1")
+                      for o, buf in ((b"3", b"1"), (b"2", b"0"))}, shapes
+    assert b"probe_read_kernel" not in rel and b"probe2_kernel" not in rel
+    dshapes = set(_re.findall(pat, dia))
+    assert any(s[0] == b"2" for s in dshapes) and len(dshapes) > 20
+    assert b"probe_read_kernel" in dia
+
+
 def test_exports_every_declared_symbol(libpath):
     out = subprocess.check_output(["nm", "-D", "--defined-only", libpath], text=True)
     exported = set(l.split()[-1] for l in out.splitlines() if l.strip())

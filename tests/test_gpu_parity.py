@@ -222,6 +222,38 @@ def test_block_digests_on_device(engine, oracle, golden):
             assert engine.stream_crc_dev(0, out.ptr, out.nbytes) == want["digest"]
 
 
+def test_all_block_digests_on_device(engine):
+    """A spread of the bench's 8192 x 128 MiB blocks (C3 / C5 data of every
+    rank of an 8-GPU run) generated on device, per-chunk CRCs at all four
+    chunk sizes in ONE mixed compute plan, then each CRC array's digest in one
+    launch over the arrays -- the bench's own full-scale parity check --
+    against the reference-generated tests/golden/block_digests_all.npz."""
+    import os
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "block_digests_all.npz"))
+    blocks = [0, 1, 2, 3, 511, 1022, 1023, 1024, 2049, 4095, 6146, 8191]
+    blk = 128 << 20
+    data = engine.DeviceBuffer(len(blocks) * blk)
+    for i, g in enumerate(blocks):
+        engine.fill_splitmix64(data.ptr + i * blk, blk // 8, 0, g << 24)
+    for shift in range(4):  # every block at every chunk size across the four plans
+        sizes = [512 << ((i + shift) % 4) for i in range(len(blocks))]
+        offs = np.concatenate([[0], np.cumsum([blk // c for c in sizes])])
+        crcs = engine.DeviceBuffer(int(offs[-1]) * 4)
+        segs = [engine.Segment(data=data.ptr + i * blk, len=blk, chunk_size=c, flags=engine.SEG_BE, crc_init=0,
+                               crcs=crcs.ptr + int(offs[i]) * 4) for i, c in enumerate(sizes)]
+        engine.Plan(engine.MODE_COMPUTE, segs).execute()
+        digs = engine.DeviceBuffer(4 * len(blocks))
+        dsegs = [engine.Segment(data=crcs.ptr + int(offs[i]) * 4, len=blk // c * 4, chunk_size=blk // c * 4,
+                                flags=0, crc_init=0, crcs=digs.ptr + 4 * i) for i, c in enumerate(sizes)]
+        engine.Plan(engine.MODE_COMPUTE, dsegs).execute()
+        got = digs.download(dtype=np.uint32)
+        for i, (g, c) in enumerate(zip(blocks, sizes)):
+            j = (512, 1024, 2048, 4096).index(c)
+            assert got[i] == z["be"][g, j], (g, c)
+            first = crcs.download(4, offset=int(offs[i]) * 4, dtype=">u4")[0]
+            assert first == z["crc0"][g, j], (g, c)
+
+
 def test_verify_roundtrip_corruption_pattern(engine):
     """Size-independent property used at full bench scale: compute -> corrupt
     (i % 65537 == 0) -> verify finds exactly the corrupted chunks."""
@@ -424,3 +456,29 @@ def test_dropin_max_len(engine, oracle):
         assert f(0xDEADBEEF, dbuf.ptr + 1, n) == want1, entry
     assert engine.crc32c(0, host[:n]) == want0
     assert engine.crc32c(0xDEADBEEF, host[1:]) == want1
+
+
+def test_verify_crcdata_packet_beyond_staging(engine, oracle):
+    """A packet larger than the 64 MiB one-shot staging (the reference's
+    framing admits up to 1 GiB, src/datanode.c:2433-2441) is verified through
+    the pipelined host path with the reference's result, not refused
+    (ADVICE r1): clean -> 0; one corrupted chunk -> BAD_CHECKSUM + its index."""
+    cs = 512
+    dlen = (80 << 20) + 300  # partial last chunk
+    rng = np.random.default_rng(80)
+    data = rng.integers(0, 256, dlen, dtype=np.uint8)
+    crcs = oracle.chunk_crcs(data, cs).astype(">u4").view(np.uint8)
+    region = np.concatenate([crcs, data])
+    assert engine.verify_crcdata(region, cs, crcs.nbytes, dlen) == (0, -1)
+    k = 150_001
+    region[crcs.nbytes + k * cs + 9] ^= 0x40
+    assert oracle.verify_crcdata(region, cs, crcs.nbytes, dlen) == (engine.ERR_BAD_CHECKSUM, k)
+    assert engine.verify_crcdata(region, cs, crcs.nbytes, dlen) == (engine.ERR_BAD_CHECKSUM, k)
+
+
+def test_bound_device_explicit(engine):
+    """hdfs_crc32c_init(0) binds the engine; bound_device reports it with a
+    PCI bus id (what bench.py gathers per rank)."""
+    engine.init(0)
+    dev, bus = engine.bound_device()
+    assert dev == 0 and bus.count(":") == 2 and bus.endswith(".0"), bus

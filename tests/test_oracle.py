@@ -106,3 +106,25 @@ def test_oracle_vs_reference_random():
         assert r.crc32c(cin, buf, "sw") == want
         assert o.crc32c(cin, buf, "sw") == want
         assert o.crc32c(cin, buf, "hw") == want
+
+
+def test_all_block_digests_sampled(oracle):
+    """The oracle restatement against the reference-generated per-block
+    digests of the full bench workloads (oracle/gen_block_digests.py,
+    tests/golden/block_digests_all.npz): a spread of blocks at every chunk
+    size, LE and wire-order digests and crc[0]."""
+    import os
+
+    import numpy as np
+    from oracle import splitmix64_np  # noqa: F401
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "block_digests_all.npz"))
+    assert z["be"].shape == (8192, 4) and list(z["chunk_sizes"]) == [512, 1024, 2048, 4096]
+    assert z["le"][0, 0] == 0xF2590C08 and z["le"][1, 0] == 0xEB636035  # SURVEY.md 8c
+    buf = np.empty(1 << 24, dtype=np.uint64)
+    for b in (2, 1023, 4097, 8191):
+        oracle._fill(buf.ctypes.data, 1 << 24, 0, b << 24)
+        for j, cs in enumerate((512, 1024, 2048, 4096)):
+            crcs = oracle.chunk_crcs(buf.view(np.uint8), cs)
+            assert int(crcs[0]) == z["crc0"][b, j]
+            assert oracle.crc32c(0, crcs.astype("<u4").view(np.uint8), "hw") == z["le"][b, j], (b, cs)
+            assert oracle.crc32c(0, crcs.astype(">u4").view(np.uint8), "hw") == z["be"][b, j], (b, cs)

@@ -11,11 +11,13 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import hadoofus_amd as h  # noqa: E402
+import diaglib  # noqa: E402
 
 BLOCK = 128 << 20
 B = int(os.environ.get("BLOCKS", "1024"))
 cs = 512
-h.load()
+h.load(diaglib.DIAG_LIB_PATH)  # tuning knobs: diagnostic build only
+D = diaglib.Diag(lib=h.load())
 data = h.DeviceBuffer(B * BLOCK)
 crcs = h.DeviceBuffer(B * BLOCK // cs * 4)   # expected CRCs (default shape, clean data)
 crcs2 = h.DeviceBuffer(B * BLOCK // cs * 4)  # compute-mode output of the variant under test
@@ -23,7 +25,7 @@ bms = h.DeviceBuffer(B * BLOCK // cs // 8)
 h.fill_splitmix64(data.ptr, B * BLOCK // 8, 0, 0)
 h.device_sync()
 out = {"blocks": B}
-out["probe_read_GBps"] = [round(h.probe_read(data.ptr, B * BLOCK, 3), 1) for _ in range(3)]
+out["probe_read_GBps"] = [round(D.probe_read(data.ptr, B * BLOCK, 3), 1) for _ in range(3)]
 segs = [h.Segment(data=data.ptr + b * BLOCK, len=BLOCK, chunk_size=cs, flags=h.SEG_BE, crc_init=0,
                   crcs=crcs.ptr + b * (BLOCK // cs) * 4, bitmap=bms.ptr + b * (BLOCK // cs) // 8) for b in range(B)]
 segs2 = [h.Segment(data=data.ptr + b * BLOCK, len=BLOCK, chunk_size=cs, flags=h.SEG_BE, crc_init=0,
@@ -50,12 +52,12 @@ VARIANTS = [(v + (3, 1, 1024, 0)[len(v) - 3:]) if len(v) < 7 else v for v in VAR
 
 
 def apply(order, nt, depth, gs, S, blk, pol, diag_ptr=None):
-    h.set_tile_order(order)
-    h.set_tuning(nt, diag_ptr)
-    h.set_depth(depth)
-    h.set_group_shift(gs)
-    h.set_shape(S, blk)
-    h.set_store_policy(pol)
+    D.set_tile_order(order)
+    D.set_tuning(nt, diag_ptr)
+    D.set_depth(depth)
+    D.set_group_shift(gs)
+    D.set_shape(S, blk)
+    D.set_store_policy(pol)
 
 
 def tag(order, nt, depth, gs, S, blk, pol=0):

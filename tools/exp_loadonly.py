@@ -9,11 +9,13 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import hadoofus_amd as h  # noqa: E402
+import diaglib  # noqa: E402
 
 BLOCK = 128 << 20
 B = int(os.environ.get("BLOCKS", "1024"))
 cs = 512
-h.load()
+h.load(diaglib.DIAG_LIB_PATH)  # tuning knobs: diagnostic build only
+D = diaglib.Diag(lib=h.load())
 data = h.DeviceBuffer(B * BLOCK)
 crcs = h.DeviceBuffer(B * BLOCK // cs * 4)
 bms = h.DeviceBuffer(B * BLOCK // cs // 8)
@@ -28,15 +30,15 @@ res = {}
 PROBES = [int(x) for x in os.environ.get("PROBES", "14,11").split(",")]
 for rnd in range(int(os.environ.get("ROUNDS", "4"))):
     for pol in (0, 4):
-        h.set_store_policy(pol)
+        D.set_store_policy(pol)
         ms = ver.time(3)
         res.setdefault(f"verify_policy{pol}_alg_GBps", []).append(alg / (ms * 1e-3) / 1e9)
-    h.set_store_policy(0)
+    D.set_store_policy(0)
     for v in PROBES:
-        h.set_probe(v, 2, 512)
-        res.setdefault(f"probe{v}_g2_b512_GBps", []).append(h.probe_read(data.ptr, B * BLOCK, 3))
-    h.set_probe(0, 2, 1024)
-h.set_store_policy(0)
+        D.set_probe(v, 2, 512)
+        res.setdefault(f"probe{v}_g2_b512_GBps", []).append(D.probe_read(data.ptr, B * BLOCK, 3))
+    D.set_probe(0, 2, 1024)
+D.set_store_policy(0)
 ver.execute()
 _, m = ver.results()
 out = {"blocks": B, "mismatches_policy0": m}

@@ -9,9 +9,11 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import hadoofus_amd as h  # noqa: E402
+import diaglib  # noqa: E402
 
 n = int(os.environ.get("PROBE_GIB", "64")) << 30
-h.load()
+h.load(diaglib.DIAG_LIB_PATH)  # tuning knobs: diagnostic build only
+D = diaglib.Diag(lib=h.load())
 buf = h.DeviceBuffer(n)
 h.fill_splitmix64(buf.ptr, n // 8, 0, 0)
 h.device_sync()
@@ -21,11 +23,11 @@ for variant in [4, 8] + list(range(10, 24)):
     for gpc, blk in shapes:
         if variant < 10 and (gpc, blk) != (1, 1024):
             continue
-        h.set_probe(variant, gpc, blk)
-        vals = [h.probe_read(buf.ptr, n, 2) for _ in range(2)]
+        D.set_probe(variant, gpc, blk)
+        vals = [D.probe_read(buf.ptr, n, 2) for _ in range(2)]
         out[f"v{variant}_g{gpc}_b{blk}"] = round(max(vals), 1)
         print(f"v{variant}_g{gpc}_b{blk}", out[f"v{variant}_g{gpc}_b{blk}"], file=sys.stderr, flush=True)
-h.set_probe()
+D.set_probe()
 best = sorted(out.items(), key=lambda kv: -kv[1])[:6]
 out["best"] = best
 print(json.dumps(out))
