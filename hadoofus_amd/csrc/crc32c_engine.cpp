@@ -77,7 +77,7 @@ uint32_t g_store_policy = uint32_t(HDFS_KNOB("HDFS_CRC32C_STORE", 0));
 // Schedule 3: log2 tiles per round-robin group (0..6).
 uint32_t g_group_shift = uint32_t(HDFS_KNOB("HDFS_CRC32C_GROUP", 3)) & 15u;
 // Schedule 3: deal groups XCD-major (1) or by plain workgroup id (0).
-uint32_t g_xcd_major = uint32_t(HDFS_KNOB("HDFS_CRC32C_XCD", 0)) & 1u;
+uint32_t g_xcd_major = uint32_t(HDFS_KNOB("HDFS_CRC32C_XCD", 1)) & 1u;
 // Diagnostic per-wave timestamps (device buffer, 3 x u64 per wave) or null.
 unsigned long long *g_diag = nullptr;
 
@@ -1111,7 +1111,7 @@ int hdfs_crc32c_device_sync(void) {
 #ifdef HDFS_CRC32C_DIAG
 // ---- diagnostic build only (include/hadoofus_crc32c_diag.h) ----
 int hdfs_crc32c_set_store_policy(int policy) {
-  if (policy < 0 || policy > 4) return fail(HDFS_CRC32C_EINVAL, "store policy 0..4");
+  if (policy < 0 || policy > 8) return fail(HDFS_CRC32C_EINVAL, "store policy 0..8");
   g_store_policy = uint32_t(policy);
   return HDFS_CRC32C_OK;
 }

@@ -428,7 +428,12 @@ DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, ui
           reinterpret_cast<uint32_t *>(rfl64(reinterpret_cast<uint64_t>(sh.crcs + c.tile * kTileChunks))), 0,
           static_cast<int>(rfl(keep ? nch * 4u : 0u)), 0x00020000);
       const uint32_t off = leader ? L.qg * 4u : 0x80000000u;
+      // diagnostic cache policies of the CRC store (gfx940+ CPol: 1 sc0, 2 nt, 16 sc1)
       if (kDiag && L.store_policy == 1) __builtin_amdgcn_raw_buffer_store_b32(val, rs, off, 0, 2);  // nt
+      else if (kDiag && L.store_policy == 5) __builtin_amdgcn_raw_buffer_store_b32(val, rs, off, 0, 16);  // sc1
+      else if (kDiag && L.store_policy == 6) __builtin_amdgcn_raw_buffer_store_b32(val, rs, off, 0, 17);  // sc0 sc1
+      else if (kDiag && L.store_policy == 7) __builtin_amdgcn_raw_buffer_store_b32(val, rs, off, 0, 18);  // nt sc1
+      else if (kDiag && L.store_policy == 8) __builtin_amdgcn_raw_buffer_store_b32(val, rs, off, 0, 1);   // sc0
       else __builtin_amdgcn_raw_buffer_store_b32(val, rs, off, 0, 0);
     }
   } else {

@@ -53,7 +53,8 @@ int hdfs_crc32c_set_shape(int streams, int block);
  * (stores dropped; output undefined -- timing experiments only), 4
  * diagnostic: verify plans run a load-only twin of the kernel (same loads and
  * store ops, no CRC arithmetic, results undefined) -- the memory ceiling of
- * the kernel's access pattern.
+ * the kernel's access pattern; 5 / 6 / 7 / 8: compute-mode CRC stores with
+ * cache policy sc1 / sc0 sc1 / nt sc1 / sc0.
  * Env HDFS_CRC32C_STORE. */
 int hdfs_crc32c_set_store_policy(int policy);
 /* Empirical streaming-read bandwidth of `bytes` at dptr (GB/s, 1e9 B/s):

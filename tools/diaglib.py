@@ -76,4 +76,4 @@ class Diag:
         self.set_tuning(2, None)
         self.set_group_shift(3)
         self.set_store_policy(0)
-        self.set_xcd_major(0)
+        self.set_xcd_major(1)
