@@ -427,14 +427,29 @@ DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, ui
       const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
           reinterpret_cast<uint32_t *>(rfl64(reinterpret_cast<uint64_t>(sh.crcs + c.tile * kTileChunks))), 0,
           static_cast<int>(rfl(keep ? nch * 4u : 0u)), 0x00020000);
-      const uint32_t off = leader ? L.qg * 4u : 0x80000000u;
+      uint32_t off = leader ? L.qg * 4u : 0x80000000u;
+      if (kDiag && L.store_policy == 9) {
+        // diagnostic: every tile's 32 B lands in a 256 KiB window (L2-resident writes)
+        const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+            reinterpret_cast<uint32_t *>(rfl64(reinterpret_cast<uint64_t>(sh.crcs))), 0,
+            static_cast<int>(rfl(keep ? 262144u : 0u)), 0x00020000);
+        const uint32_t wo = ((c.tile * 32u) & 262143u) + L.qg * 4u;
+        __builtin_amdgcn_raw_buffer_store_b32(val, rw, leader ? wo : 0x80000000u, 0, 0);
+        return;
+      }
+      if (kDiag && L.store_policy == 10 && L.qg != 0) off = 0x80000000u;  // diagnostic: 4 B per tile
       // diagnostic cache policies of the CRC store (gfx940+ CPol: 1 sc0, 2 nt, 16 sc1)
       if (kDiag && L.store_policy == 1) __builtin_amdgcn_raw_buffer_store_b32(val, rs, off, 0, 2);  // nt
       else if (kDiag && L.store_policy == 5) __builtin_amdgcn_raw_buffer_store_b32(val, rs, off, 0, 16);  // sc1
       else if (kDiag && L.store_policy == 6) __builtin_amdgcn_raw_buffer_store_b32(val, rs, off, 0, 17);  // sc0 sc1
       else if (kDiag && L.store_policy == 7) __builtin_amdgcn_raw_buffer_store_b32(val, rs, off, 0, 18);  // nt sc1
       else if (kDiag && L.store_policy == 8) __builtin_amdgcn_raw_buffer_store_b32(val, rs, off, 0, 1);   // sc0
-      else __builtin_amdgcn_raw_buffer_store_b32(val, rs, off, 0, 0);
+      else if (kDiag && L.store_policy == 11) __builtin_amdgcn_raw_buffer_store_b32(val, rs, off, 0, 0);  // default
+      // product: sc1.  Compute mode loses ~13 % to its CRC stores, per
+      // written-back line rather than per byte (4 B per tile costs as much as
+      // 32 B; an L2-resident window recovers half); sc1 stores measured +1.7 %
+      // compute, verify unchanged (tools/exp_knobs.py, profiles/r02/).
+      else __builtin_amdgcn_raw_buffer_store_b32(val, rs, off, 0, 16);
     }
   } else {
     const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(

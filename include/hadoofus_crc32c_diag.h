@@ -49,12 +49,15 @@ int hdfs_crc32c_set_depth(int depth);
  * launch_tiles run; any other combination fails (EINVAL) at launch.
  * Env HDFS_CRC32C_STREAMS / HDFS_CRC32C_BLOCK. */
 int hdfs_crc32c_set_shape(int streams, int block);
-/* Compute-mode result store policy: 0 default, 1 nontemporal, 2 diagnostic
+/* Compute-mode result store policy: 0 default (the product's sc1 store), 1 nontemporal, 2 diagnostic
  * (stores dropped; output undefined -- timing experiments only), 4
  * diagnostic: verify plans run a load-only twin of the kernel (same loads and
  * store ops, no CRC arithmetic, results undefined) -- the memory ceiling of
  * the kernel's access pattern; 5 / 6 / 7 / 8: compute-mode CRC stores with
- * cache policy sc1 / sc0 sc1 / nt sc1 / sc0.
+ * cache policy sc1 / sc0 sc1 / nt sc1 / sc0; 9: every tile's CRCs written into
+ * one 256 KiB window (L2-resident writes); 10: only chunk 0 of each tile
+ * stored (4 B per tile) -- timing experiments only, output undefined; 11:
+ * default-policy (no cache bits) CRC stores.
  * Env HDFS_CRC32C_STORE. */
 int hdfs_crc32c_set_store_policy(int policy);
 /* Empirical streaming-read bandwidth of `bytes` at dptr (GB/s, 1e9 B/s):
