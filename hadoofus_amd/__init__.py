@@ -23,6 +23,7 @@ from .abi import (  # noqa: F401
     Packet,
     parse_packets,
     verify_packets,
+    verify_packets_copy,
     ERR_UNSUPPORTED_CHECKSUM,
     MODE_COMPUTE,
     MODE_VERIFY,

@@ -125,6 +125,9 @@ def bind_product(lib):
     for name in ("hdfs_crc32c_parse_packets", "hdfs_crc32c_verify_packets"):
         _bind(lib, name, _int, [_vp, _u64, _int, _u32, _int, ctypes.POINTER(Packet), _sz,
                                 ctypes.POINTER(_sz), ctypes.POINTER(_u64)])
+    _bind(lib, "hdfs_crc32c_verify_packets_copy", _int,
+          [_vp, _u64, _int, _u32, _int, ctypes.POINTER(Packet), _sz, ctypes.POINTER(_sz), ctypes.POINTER(_u64), _vp,
+           _u64, ctypes.POINTER(_u64)])
     _bind(lib, "hdfs_crc32c_session_create", _int, [ctypes.POINTER(_vp), _int, _u32, _int, _u64, _sz])
     _bind(lib, "hdfs_crc32c_session_buffer", _int, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_u64)])
     _bind(lib, "hdfs_crc32c_session_commit", _int, [_vp, _u64])
@@ -331,6 +334,23 @@ def verify_packets(stream, proto=PROTO_V2, chunk_size=512, ctype=CSUM_CRC32C, ma
     `stream` or of device memory (dptr, nbytes).
     -> (rc, [packet dicts], consumed); rc = first error in stream order."""
     return _packets("hdfs_crc32c_verify_packets", stream, proto, chunk_size, ctype, max_pkts, dptr, nbytes)
+
+
+def verify_packets_copy(dptr, nbytes, dst, dst_cap, proto=PROTO_V2, chunk_size=512, ctype=CSUM_CRC32C,
+                        max_pkts=None):
+    """Verify + copy-out of a device-resident stream (dptr, nbytes) into the
+    device buffer dst (dst_cap bytes): the payloads de-framed in stream order.
+    -> (rc, [packet dicts], consumed, delivered)."""
+    if max_pkts is None:
+        max_pkts = nbytes // (25 if proto == PROTO_V1 else 6) + 1
+    arr = (Packet * max(1, max_pkts))()
+    npk, used, got = _sz(0), _u64(0), _u64(0)
+    rc = load().hdfs_crc32c_verify_packets_copy(dptr, nbytes, proto, chunk_size, ctype, arr, max_pkts,
+                                                ctypes.byref(npk), ctypes.byref(used), dst, dst_cap,
+                                                ctypes.byref(got))
+    if rc < 0:
+        _check(rc)
+    return rc, [arr[i].as_dict() for i in range(npk.value)], used.value, got.value
 
 
 def compose_packets(data, offset_in_block=0, seqno=0, proto=PROTO_V2, ctype=CSUM_CRC32C, finish=False,

@@ -24,7 +24,8 @@ LIB = os.path.join(LIBDIR, "libhadoofus_crc32c.so")
 DIAG_LIB = os.path.join(LIBDIR, "libhadoofus_crc32c_diag.so")
 SOURCES = ["crc32c_kernels.hip", "crc32c_engine.cpp", "crc32c_packets.cpp"]
 DIAG_SOURCES = SOURCES + ["crc32c_probes.hip"]
-HEADERS = ["crc32c_internal.h", "crc32c_tables.h", "crc32c_packets.h", "crc32c_engine.h", "exports.map"]
+HEADERS = ["crc32c_internal.h", "crc32c_tables.h", "crc32c_packets.h", "crc32c_engine.h", "crc32c_frame.h",
+           "exports.map"]
 PUBLIC = ["hadoofus_crc32c.h", "crc32c.h", "hadoofus_crc32c_diag.h"]
 ARCH = os.environ.get("HADOOFUS_OFFLOAD_ARCH", "gfx950")
 

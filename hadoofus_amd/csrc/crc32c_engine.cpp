@@ -224,7 +224,7 @@ static const int g_small_rule = HDFS_KNOB("HDFS_CRC32C_SMALL_RULE", 1);
 // ctype: 0 = CRC32C, 1 = CRC32 (zlib polynomial) -- selects the table set.
 int launch_all(DevCtx &c, int mode, const SegDev *d_segs, uint32_t nseg, uint64_t rounds,
                uint64_t mtiles, uint64_t gtiles, uint32_t *d_fb, unsigned long long *d_mism,
-               uint32_t *d_gctr, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1, bool reset, int ctype) {
+               uint32_t *d_gctr, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1, bool reset, int ctype, bool copy) {
   const bool vreset = mode == kModeVerify && reset;
   uint32_t *gz = (rounds && g_tile_order >= 2) ? d_gctr : nullptr;
   if (vreset || gz)
@@ -250,7 +250,7 @@ int launch_all(DevCtx &c, int mode, const SegDev *d_segs, uint32_t nseg, uint64_
     const hipError_t le = launch_tiles(kmode, order, nt, depth, streams, block, grid, d_segs, nseg, rounds,
                                        mtiles, c.d_tab_main_t[ctype], d_fb, d_mism, kDiag ? g_diag : nullptr,
                                        (kDiag ? g_store_policy : 0u) | (g_group_shift << 8) | (g_xcd_major << 12),
-                                       d_gctr, st);
+                                       d_gctr, st, copy ? 1 : 0);
     if (le == hipErrorInvalidValue)
       return fail(HDFS_CRC32C_EINVAL, "tiled kernel shape (order %d, nt %d, depth %d, streams %d, block %d) is not built",
                   order, nt, depth, streams, block);

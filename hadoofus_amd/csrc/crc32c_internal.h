@@ -47,8 +47,41 @@ struct SegDev {
   uint64_t len;          // bytes
   uint64_t round_start;  // global index of this segment's first main-path round
   uint64_t gtile_start;  // global index of this segment's first generic tile
+  uint8_t *copy_dst;     // verify + copy-out: the segment's data is also written here (or null)
+  uint64_t reserved;
 };
-static_assert(sizeof(SegDev) == 80, "SegDev layout");
+static_assert(sizeof(SegDev) == 96, "SegDev layout");
+
+// Device framing of a device-resident packet stream (frame_grid_kernel ->
+// grid_scan_kernel): packets at base + k * stride, stride = the wire size of
+// the packet at base.  Status per grid point k:
+enum : uint32_t {
+  kGridOn = 0,    // complete, framing-clean, wire size == stride: the walk goes on at k + 1
+  kGridOff = 1,   // complete, framing-clean, other size: recorded, the walk goes on off the grid
+  kGridStop = 2,  // recorded and the walk ends (framing error, empty last packet)
+  kGridMore = 3,  // incomplete / past the stream: not recorded, the walk ends
+};
+struct GridSummary {
+  uint32_t first_break;  // first grid point whose status is not kGridOn (count if none)
+  uint32_t recorded;     // packets of the walk framed by this pass
+  uint32_t last_status;  // status of first_break (kGridOn if none)
+  uint32_t nseg;         // verify segments built
+  uint64_t stride;
+  uint64_t rounds, mtiles, gtiles;  // tiled / generic work of the segment table
+  uint64_t payload;      // data bytes of the recorded framing-clean packets
+  uint64_t consumed;     // stream offset after the last complete framing-clean packet
+  uint64_t next_pos;     // where the walk continues (kGridOn / kGridOff)
+  uint64_t bm_bytes;     // bitmap bytes of the segment table
+  uint32_t nbad;         // verify: packets with bad chunks (grid_finalize_kernel)
+  uint32_t pad;
+};
+// Compact verify verdict of one packet (grid_finalize_kernel).
+struct GridBad {
+  uint32_t pkt;
+  int32_t first_bad;
+  uint32_t bad_chunks;
+  uint32_t pad;
+};
 
 // LDS image of the tiled kernel (bytes).
 //  [0, 128 KiB)          slicing-by-4 tables, each replicated 32x so that
@@ -85,6 +118,8 @@ struct PktDesc {
 };
 constexpr uint32_t kGatherSlice = 65536;  // data bytes per gather workgroup
 constexpr uint32_t kHdrWin = 64;          // header-window row bytes (device packet streams)
+
+constexpr uint32_t kGridMaxCount = 65536;  // grid points per device framing pass
 
 // Synchronous host-memory calls up to this size (and chunk count) run as one
 // small kernel reading pinned host memory (small_chunks_kernel).

@@ -21,6 +21,7 @@
 //      (CRC linearity, src/crc32c_sse42.c:270-319 uses the same algebra).
 #include <hip/hip_runtime.h>
 
+#include "crc32c_frame.h"
 #include "crc32c_internal.h"
 
 namespace hdfs_crc32c {
@@ -463,14 +464,41 @@ DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, ui
   }
 }
 
+// Verify + copy-out (COPY kernels): the round's data, still in the loaded
+// lane order, is stored to the segment's copy_dst at the same offsets it was
+// loaded from (fully coalesced 1 KiB per instruction, the mirror of issue()).
+// The descriptor's range is the valid bytes of the round (0 for a parked
+// cursor or a segment without copy_dst), so out-of-range lanes are dropped.
+DEV void copy_round(const uint32_t (&d)[16], const Cursor c, SegP segs, const LaneConst &L, SegCache &kc) {
+  const SegHot &sh = hot(kc, segs, c.seg).h;
+  const uint32_t cs = sh.chunk_size;
+  uint8_t *dst = segs[c.seg].copy_dst;
+  const uint32_t nch = min(kTileChunks, sh.nchunks - c.tile * kTileChunks);
+  const bool ok = c.valid && dst != nullptr;
+  uint8_t *base = ok ? dst + static_cast<uint64_t>(c.tile) * kTileChunks * cs + static_cast<uint64_t>(c.r) * kRoundBytes
+                     : dst;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<uint8_t *>(rfl64(reinterpret_cast<uint64_t>(base))), 0,
+      static_cast<int>(rfl(ok ? (nch - 1u) * cs + kRoundBytes : 0u)), 0x00020000);
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const u32x4 v = {d[4 * k + 0], d[4 * k + 1], d[4 * k + 2], d[4 * k + 3]};
+    __builtin_amdgcn_raw_buffer_store_b128(v, rs, (2u * k + L.hsel) * cs + L.loff, 0, 0);
+  }
+}
+
 // Process one round of each of the wave's S streams (d[s] for cursor c[s]);
 // st[s] is stream s's running lane register across the rounds of a tile.
 // The S slicing chains are independent and interleaved step by step, so one
 // lane keeps S table lookups in flight (latency hiding by ILP, not waves).
-template <int MODE, int S>
+template <int MODE, int S, int COPY>
 DEV void process(const uint32_t *lds, uint32_t (&d)[S][16], const uint32_t (&exp)[S], const Cursor (&c)[S],
                  SegP segs, uint32_t (&st)[S], const LaneConst &L, uint32_t *__restrict__ first_bad,
                  unsigned long long *__restrict__ mism, SegCache (&kc)[S]) {
+  if constexpr (COPY) {
+#pragma unroll
+    for (int s = 0; s < S; s++) copy_round(d[s], c[s], segs, L, kc[s]);
+  }
   if constexpr (kDiag && MODE == kModeLoadOnly) {
 #pragma unroll
     for (int s = 0; s < S; s++) {
@@ -511,7 +539,7 @@ DEV void process(const uint32_t *lds, uint32_t (&d)[S][16], const uint32_t (&exp
 // rounds stay in flight while one is processed); S independent tile streams
 // per wave (S x 4 KiB per round, S chains of ILP); BLOCK threads per
 // workgroup (one workgroup per CU: the LDS image takes 156 KiB).
-template <int MODE, int ORDER, int NT, int DEPTH, int S, int BLOCK, int BUF = 0>
+template <int MODE, int ORDER, int NT, int DEPTH, int S, int BLOCK, int BUF = 0, int COPY = 0>
 __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
     const SegDev *__restrict__ segs, uint32_t nseg, uint64_t total_rounds, uint64_t total_tiles,
     const uint32_t *__restrict__ gtab, uint32_t *__restrict__ first_bad,
@@ -694,7 +722,7 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
   for (;;) {
 #pragma unroll
     for (int k = 0; k < DEPTH; k++) {
-      process<MODE, S>(lds, buf[k], ex[k], cur[k], sg, st, L, first_bad, mism, kc);
+      process<MODE, S, COPY>(lds, buf[k], ex[k], cur[k], sg, st, L, first_bad, mism, kc);
 #pragma unroll
       for (int s = 0; s < S; s++) nrounds += cur[k][s].valid ? 1u : 0u;
       const int prev = (k + DEPTH - 1) % DEPTH;
@@ -753,6 +781,10 @@ __global__ __launch_bounds__(256) void crc32c_generic_kernel(
       const uint64_t off = static_cast<uint64_t>(chunk) * sg.chunk_size;
       const uint8_t *p = sg.data + off;
       uint64_t n = min(static_cast<uint64_t>(sg.chunk_size), sg.len - off);
+      if (sg.copy_dst) {  // verify + copy-out: this lane's chunk (tails and odd chunk sizes only)
+        uint8_t *q = sg.copy_dst + off;
+        for (uint64_t i = 0; i < n; i++) gstore8(q + i, gload8(p + i));
+      }
       uint32_t c = sg.reg_init;
       while (n && (reinterpret_cast<uintptr_t>(p) & 3u)) {
         c = t0[(c ^ gload8(p++)) & 0xffu] ^ (c >> 8);
@@ -1120,6 +1152,208 @@ __global__ __launch_bounds__(256) void packet_gather_kernel(const uint8_t *__res
 }
 
 // ---------------------------------------------------------------------------
+// Device framing of device-resident packet streams.  The reference's walk is
+// sequential (packet k+1 starts where packet k's plen puts it,
+// src/datanode.c:2345-2446), but the packets of a block transfer all have
+// the same wire size, so thread k frames the packet at base + k * stride
+// (stride = the wire size of the packet at base) with the host walk's own
+// frame_step (crc32c_frame.h) and the first grid point that is not a
+// complete, framing-clean packet of exactly that size ends the run.  The
+// scan kernel turns the run into a verify segment table in HBM (the host
+// never sees the headers), and the host continues from where the run left
+// the grid.
+__global__ __launch_bounds__(256) void frame_grid_kernel(const uint8_t *__restrict__ s, uint64_t len, uint64_t base,
+                                                         uint32_t count, int proto, uint32_t cs, int ctype,
+                                                         hdfs_crc32c_packet *__restrict__ recs,
+                                                         uint32_t *__restrict__ status, GridSummary *__restrict__ sum) {
+  const uint32_t k = blockIdx.x * 256u + threadIdx.x;
+  if (k >= count) return;
+  // the stride: the wire size of the packet at base (every thread reads the
+  // same header; cache-resident)
+  hdfs_crc32c_packet r;
+  uint64_t total = 0;
+  const int st0 = frame::frame_step(s + base, len - base, base, proto, cs, ctype, r, total);
+  const uint64_t stride = st0 == frame::kStepNext ? total : 0;
+  if (k == 0) sum->stride = stride;
+  if (k > 0 && stride == 0) return;  // packet 0 ends the walk: no other grid point is reached
+  const uint64_t pos = base + uint64_t(k) * stride;
+  uint32_t code = kGridMore;
+  if (pos < len) {
+    const int st = k == 0 ? st0 : frame::frame_step(s + pos, len - pos, pos, proto, cs, ctype, r, total);
+    code = st == frame::kStepMore ? kGridMore
+         : st == frame::kStepStop ? kGridStop
+         : total == stride        ? kGridOn
+                                  : kGridOff;
+    if (code != kGridMore) recs[k] = r;
+  }
+  status[k] = code;
+  if (code != kGridOn) atomicMin(&sum->first_break, k);
+}
+
+// One workgroup: the run's records -> verify segments (exclusive scans of
+// segments, rounds, main / generic tiles, bitmap bytes and payload bytes, in
+// the classify() rules of crc32c_engine.cpp), plus the run's summary.
+struct GridAcc {
+  uint64_t v[6];  // nseg, rounds, mtiles, gtiles, bitmap bytes, payload bytes
+};
+
+DEV void grid_contrib(const hdfs_crc32c_packet &r, uint32_t cs, int verify, GridAcc &a) {
+  if (r.error) return;
+  a.v[5] += uint64_t(r.data_len);
+  if (!verify || r.crc_len <= 0) return;
+  const uint32_t nch = uint32_t(r.crc_len) / 4u, ntiles = (nch + 7u) / 8u;
+  const bool eligible = cs % kRoundBytes == 0;
+  const bool partial = uint32_t(r.data_len) % cs != 0;
+  const uint32_t main = eligible ? (partial ? ntiles - 1u : ntiles) : 0u;
+  a.v[0] += 1;
+  a.v[1] += uint64_t(main) * (cs / kRoundBytes);
+  a.v[2] += main;
+  a.v[3] += ntiles - main;
+  a.v[4] += ntiles;
+}
+
+__global__ __launch_bounds__(1024) void grid_scan_kernel(
+    const uint8_t *__restrict__ s, uint64_t base, uint32_t count, const hdfs_crc32c_packet *__restrict__ recs,
+    const uint32_t *__restrict__ status, uint32_t cs, uint32_t sflags, int verify, uint8_t *__restrict__ bm_base,
+    uint8_t *__restrict__ copy_base, SegDev *__restrict__ segs, uint32_t *__restrict__ seg2pkt,
+    uint32_t *__restrict__ fb, GridSummary *__restrict__ sum) {
+  __shared__ uint64_t wsum[6][16];
+  const uint32_t fbk = min(sum->first_break, count);
+  const uint32_t st_fb = fbk < count ? status[fbk] : uint32_t(kGridOn);
+  const uint32_t recorded = fbk + (fbk < count && st_fb != kGridMore ? 1u : 0u);
+  const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+  const uint32_t per = (recorded + 1023u) / 1024u;
+  const uint32_t i0 = min(t * per, recorded), i1 = min(i0 + per, recorded);
+  GridAcc a{};
+  for (uint32_t i = i0; i < i1; i++) grid_contrib(recs[i], cs, verify, a);
+  // exclusive prefix: inclusive scan inside the wave, then across waves
+  GridAcc incl = a;
+#pragma unroll
+  for (int q = 0; q < 6; q++) {
+#pragma unroll
+    for (uint32_t off = 1; off < 64; off <<= 1) {
+      const uint64_t o = __shfl_up(incl.v[q], off);
+      if (lane >= off) incl.v[q] += o;
+    }
+    if (lane == 63) wsum[q][w] = incl.v[q];
+  }
+  __syncthreads();
+  GridAcc pre{}, tot{};
+#pragma unroll
+  for (int q = 0; q < 6; q++) {
+    for (uint32_t j = 0; j < 16; j++) {
+      if (j < w) pre.v[q] += wsum[q][j];
+      tot.v[q] += wsum[q][j];
+    }
+    pre.v[q] += incl.v[q] - a.v[q];
+  }
+  // second pass: the segment entries
+  for (uint32_t i = i0; i < i1; i++) {
+    const hdfs_crc32c_packet r = recs[i];
+    if (verify && !r.error && r.crc_len > 0) {
+      const uint32_t nch = uint32_t(r.crc_len) / 4u, ntiles = (nch + 7u) / 8u;
+      const bool eligible = cs % kRoundBytes == 0;
+      const bool partial = uint32_t(r.data_len) % cs != 0;
+      const uint32_t main = eligible ? (partial ? ntiles - 1u : ntiles) : 0u;
+      const uint32_t sg = static_cast<uint32_t>(pre.v[0]);
+      SegDev d;
+      const uint8_t *crcp = s + r.stream_off + r.header_len;
+      d.data = crcp + r.crc_len;
+      d.crcs = reinterpret_cast<uint32_t *>(const_cast<uint8_t *>(crcp));
+      d.bitmap = bm_base + pre.v[4];
+      d.mtile_start = pre.v[2];
+      d.chunk_size = cs;
+      d.flags = sflags;
+      d.nchunks = nch;
+      d.main_tiles = main;
+      d.reg_init = 0xFFFFFFFFu;
+      d.gen_tiles = ntiles - main;
+      d.len = uint64_t(r.data_len);
+      d.round_start = pre.v[1];
+      d.gtile_start = pre.v[3];
+      d.copy_dst = copy_base ? copy_base + pre.v[5] : nullptr;
+      d.reserved = 0;
+      segs[sg] = d;
+      seg2pkt[sg] = i;
+      fb[sg] = 0xFFFFFFFFu;
+    }
+    grid_contrib(r, cs, verify, pre);
+  }
+  if (t == 0) {
+    const uint64_t stride = sum->stride;
+    uint64_t consumed, next;
+    if (fbk == count) {
+      consumed = next = base + uint64_t(count) * stride;
+    } else if (st_fb == kGridMore) {
+      consumed = next = base + uint64_t(fbk) * stride;
+    } else {
+      const hdfs_crc32c_packet &r = recs[fbk];
+      next = r.stream_off + r.header_len + uint64_t(r.crc_len) + uint64_t(r.data_len);
+      consumed = r.error ? base + uint64_t(fbk) * stride : next;
+    }
+    sum->first_break = fbk;
+    sum->recorded = recorded;
+    sum->last_status = st_fb;
+    sum->nseg = static_cast<uint32_t>(tot.v[0]);
+    sum->rounds = tot.v[1];
+    sum->mtiles = tot.v[2];
+    sum->gtiles = tot.v[3];
+    sum->bm_bytes = tot.v[4];
+    sum->payload = tot.v[5];
+    sum->consumed = consumed;
+    sum->next_pos = next;
+    sum->nbad = 0;
+  }
+}
+
+// After verify: every segment with a bad chunk -> one compact GridBad entry
+// (packet index, first bad chunk, number of bad chunks from its bitmap).
+__global__ __launch_bounds__(256) void grid_finalize_kernel(const SegDev *__restrict__ segs, uint32_t nseg,
+                                                            const uint32_t *__restrict__ seg2pkt,
+                                                            const uint32_t *__restrict__ fb,
+                                                            GridBad *__restrict__ bad, uint32_t bad_cap,
+                                                            GridSummary *__restrict__ sum) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= nseg || fb[i] == 0xFFFFFFFFu) return;
+  const SegDev d = segs[i];
+  const uint32_t nb = (d.nchunks + 7u) / 8u;
+  uint32_t n = 0;
+  for (uint32_t j = 0; j < nb; j++) {
+    uint32_t byte = d.bitmap[j];
+    if (j == d.nchunks / 8u) byte &= (1u << (d.nchunks % 8u)) - 1u;  // bits past the last chunk
+    n += __builtin_popcount(byte);
+  }
+  const uint32_t slot = atomicAdd(&sum->nbad, 1u);
+  if (slot < bad_cap) bad[slot] = GridBad{seg2pkt[i], int32_t(fb[i]), n, 0u};
+}
+
+hipError_t launch_frame_grid(const uint8_t *s, uint64_t len, uint64_t base, uint32_t count, int proto, uint32_t cs,
+                             int ctype, hdfs_crc32c_packet *recs, uint32_t *status, GridSummary *sum,
+                             hipStream_t stream) {
+  if (!count || base >= len) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(frame_grid_kernel, dim3((count + 255) / 256), dim3(256), 0, stream, s, len, base, count, proto,
+                     cs, ctype, recs, status, sum);
+  return hipGetLastError();
+}
+
+hipError_t launch_grid_scan(const uint8_t *s, uint64_t base, uint32_t count, const hdfs_crc32c_packet *recs,
+                            const uint32_t *status, uint32_t cs, uint32_t sflags, int verify, uint8_t *bm_base,
+                            uint8_t *copy_base, SegDev *segs, uint32_t *seg2pkt, uint32_t *fb, GridSummary *sum,
+                            hipStream_t stream) {
+  hipLaunchKernelGGL(grid_scan_kernel, dim3(1), dim3(1024), 0, stream, s, base, count, recs, status, cs, sflags,
+                     verify, bm_base, copy_base, segs, seg2pkt, fb, sum);
+  return hipGetLastError();
+}
+
+hipError_t launch_grid_finalize(const SegDev *segs, uint32_t nseg, const uint32_t *seg2pkt, const uint32_t *fb,
+                                GridBad *bad, uint32_t bad_cap, GridSummary *sum, hipStream_t stream) {
+  if (!nseg) return hipSuccess;
+  hipLaunchKernelGGL(grid_finalize_kernel, dim3((nseg + 255) / 256), dim3(256), 0, stream, segs, nseg, seg2pkt, fb,
+                     bad, bad_cap, sum);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // Host-side launchers (used by crc32c_engine.cpp).
 // ---------------------------------------------------------------------------
 hipError_t launch_gather(const uint8_t *raw, const PktDesc *descs, uint32_t npk, uint32_t units, uint8_t *arena,
@@ -1177,12 +1411,21 @@ hipError_t launch_header_window(const uint8_t *s, uint64_t len, uint64_t base, u
 hipError_t launch_tiles(int mode, int order, int nt, int depth, int streams, int block, int grid,
                         const SegDev *segs, uint32_t nseg, uint64_t total_rounds, uint64_t total_tiles,
                         const uint32_t *gtab, uint32_t *first_bad, unsigned long long *mism,
-                        unsigned long long *diag, uint32_t tune, uint32_t *gctr, hipStream_t stream) {
-#define HDFS_LAUNCH(M, O, N, D, S, B, BUF)                                                                      \
-  hipLaunchKernelGGL((crc32c_tiles_kernel<M, O, N, D, S, B, BUF>), dim3(grid), dim3(B), 0, stream, segs, nseg, \
-                     total_rounds, total_tiles, gtab, first_bad, mism, diag, tune, gctr)
+                        unsigned long long *diag, uint32_t tune, uint32_t *gctr, hipStream_t stream, int copy) {
+#define HDFS_LAUNCH_C(M, O, N, D, S, B, BUF, C)                                                            \
+  hipLaunchKernelGGL((crc32c_tiles_kernel<M, O, N, D, S, B, BUF, C>), dim3(grid), dim3(B), 0, stream, segs, \
+                     nseg, total_rounds, total_tiles, gtab, first_bad, mism, diag, tune, gctr)
+#define HDFS_LAUNCH(M, O, N, D, S, B, BUF) HDFS_LAUNCH_C(M, O, N, D, S, B, BUF, 0)
 #define HDFS_SHAPE(O, N, D, S, B) (order == (O) && nt == (N) && depth == (D) && streams == (S) && block == (B))
   if (mode != kModeCompute && mode != kModeVerify && !(kDiag && mode == kModeLoadOnly)) return hipErrorInvalidValue;
+  if (copy) {
+    // verify + copy-out (device packet streams): the two product shapes only
+    if (mode != kModeVerify) return hipErrorInvalidValue;
+    if (HDFS_SHAPE(3, 2, 3, 1, 1024)) HDFS_LAUNCH_C(kModeVerify, 3, 1, 3, 1, 1024, 1, 1);
+    else if (HDFS_SHAPE(2, 1, 3, 1, 1024)) HDFS_LAUNCH_C(kModeVerify, 2, 1, 3, 1, 1024, 0, 1);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+  }
   // Release build: the two product shapes only -- schedule 3 with nontemporal
   // buffer loads (nt 2), and schedule 2 (small launches / tables of small
   // segments) with nontemporal global loads; depth 3, one tile stream, 1024
@@ -1234,6 +1477,7 @@ hipError_t launch_tiles(int mode, int order, int nt, int depth, int streams, int
 #undef HDFS_LAUNCH_PRODUCT
 #undef HDFS_SHAPE
 #undef HDFS_LAUNCH
+#undef HDFS_LAUNCH_C
   return hipGetLastError();
 }
 

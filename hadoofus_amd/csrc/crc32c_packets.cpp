@@ -2,23 +2,8 @@
 // _recv_packet / _process_recv_packet (src/datanode.c:2345-2446), so that the
 // CRC work of a whole run of packets can go to the GPU in one launch.
 //
-// Wire formats (big-endian integers, src/heapbuf.c:174-215):
-//   v1 (proto < HDFS_DATANODE_AP_2_0, include/hadoofus/lowlevel.h:429-433):
-//     [plen s32][offsetInBlock s64][seqno s64][lastPacketInBlock s8][dataLen s32]
-//     = 25 header bytes                                  (src/datanode.c:2363-2384)
-//   v2: [plen s32][hlen u16][PacketHeaderProto, hlen bytes] (src/datanode.c:2387-2418)
-//     message PacketHeaderProto { required sfixed64 offsetInBlock = 1;
-//       required sfixed64 seqno = 2; required bool lastPacketInBlock = 3;
-//       required sfixed32 dataLen = 4; optional bool syncBlock = 5; }
-//                                                   (src/proto/datatransfer.proto:228-235)
-//   then crcdlen = plen - dataLen - 4 bytes of BE CRCs and dataLen data bytes.
-//
-// The reference unpacks the header with protobuf-c; decode_header() below
-// restates the parts of protobuf-c's unpack that decide success for this
-// message: tag/wire-type scan, wire type must match each known field's type,
-// unknown fields skipped, groups and wire types 6/7 rejected, truncation
-// rejected, every required field present, last occurrence wins, bool = any
-// nonzero varint payload bit.
+// Framing rules and the PacketHeaderProto decode live in crc32c_frame.h,
+// shared with the device framing kernel.
 #include "crc32c_packets.h"
 
 #include <algorithm>
@@ -32,110 +17,6 @@
 #include "crc32c_engine.h"
 
 namespace hdfs_crc32c {
-namespace {
-
-constexpr int64_t kOneGB = 1024 * 1024 * 1024;  // src/datanode.c:2430
-
-inline uint32_t be32(const uint8_t *p) {
-  return (uint32_t(p[0]) << 24) | (uint32_t(p[1]) << 16) | (uint32_t(p[2]) << 8) | p[3];
-}
-inline uint64_t be64(const uint8_t *p) { return (uint64_t(be32(p)) << 32) | be32(p + 4); }
-inline uint32_t le32(const uint8_t *p) { uint32_t v; std::memcpy(&v, p, 4); return v; }
-inline uint64_t le64(const uint8_t *p) { uint64_t v; std::memcpy(&v, p, 8); return v; }
-
-struct Header {
-  int64_t offset = 0, seqno = 0;
-  int32_t dlen = 0;
-  bool last = false, sync = false;
-};
-
-// Varint of at most maxb bytes; returns its length or 0 if unterminated.
-size_t varint_len(const uint8_t *p, size_t rem, size_t maxb) {
-  const size_t n = rem < maxb ? rem : maxb;
-  for (size_t i = 0; i < n; i++)
-    if (!(p[i] & 0x80)) return i + 1;
-  return 0;
-}
-
-uint64_t varint_val(const uint8_t *p, size_t n) {
-  uint64_t v = 0;
-  for (size_t i = 0; i < n; i++) v |= uint64_t(p[i] & 0x7f) << (7 * i);
-  return v;
-}
-
-bool decode_header(const uint8_t *p, size_t n, Header &h) {
-  unsigned seen = 0;
-  size_t pos = 0;
-  while (pos < n) {
-    const uint8_t *q = p + pos;
-    const size_t rem = n - pos;
-    if ((q[0] & 0xf8) == 0) return false;  // field number 0
-    const size_t tl = varint_len(q, rem, 5);
-    if (!tl) return false;
-    const uint64_t tag = varint_val(q, tl);
-    const unsigned wt = unsigned(tag & 7);
-    const uint64_t field = tag >> 3;
-    const uint8_t *v = q + tl;
-    const size_t vrem = rem - tl;
-    size_t vl = 0;
-    switch (wt) {
-      case 0:
-        vl = varint_len(v, vrem, 10);
-        if (!vl) return false;
-        break;
-      case 1:
-        if (vrem < 8) return false;
-        vl = 8;
-        break;
-      case 2: {
-        const size_t ll = varint_len(v, vrem, 5);
-        if (!ll) return false;
-        const uint64_t l = varint_val(v, ll);
-        if (l > vrem - ll) return false;
-        vl = ll + size_t(l);
-        break;
-      }
-      case 5:
-        if (vrem < 4) return false;
-        vl = 4;
-        break;
-      default:
-        return false;  // groups (3, 4) and 6, 7
-    }
-    switch (field) {
-      case 1:
-        if (wt != 1) return false;
-        h.offset = int64_t(le64(v));
-        seen |= 1;
-        break;
-      case 2:
-        if (wt != 1) return false;
-        h.seqno = int64_t(le64(v));
-        seen |= 2;
-        break;
-      case 3:
-      case 5: {
-        if (wt != 0) return false;
-        bool b = false;
-        for (size_t i = 0; i < vl; i++) b |= (v[i] & 0x7f) != 0;
-        (field == 3 ? h.last : h.sync) = b;
-        if (field == 3) seen |= 4;
-        break;
-      }
-      case 4:
-        if (wt != 5) return false;
-        h.dlen = int32_t(le32(v));
-        seen |= 8;
-        break;
-      default:
-        break;  // unknown field: skipped
-    }
-    pos += tl + vl;
-  }
-  return seen == 15;
-}
-
-}  // namespace
 
 int check_framing_args(int proto, uint32_t chunk_size, int ctype, char *errbuf, size_t errlen) {
   if (proto != HDFS_CRC32C_PROTO_V1 && proto != HDFS_CRC32C_PROTO_V2) {
@@ -151,62 +32,6 @@ int check_framing_args(int proto, uint32_t chunk_size, int ctype, char *errbuf, 
     return HDFS_CRC32C_EINVAL;
   }
   return HDFS_CRC32C_OK;
-}
-
-// Returns kStepNext (k is a complete packet of `total` wire bytes; the walk
-// goes on at pos + total), kStepStop (k is recorded and the walk ends:
-// framing error or the empty last packet) or kStepMore (the packet is
-// incomplete; nothing recorded).
-int frame_step(const uint8_t *p, uint64_t rem, uint64_t pos, int proto, uint32_t chunk_size, int ctype,
-               hdfs_crc32c_packet &k, uint64_t &total) {
-  std::memset(&k, 0, sizeof(k));
-  k.stream_off = pos;
-  k.first_bad = -1;
-  int64_t plen = 0, dlen = 0;
-  if (proto == HDFS_CRC32C_PROTO_V1) {  // src/datanode.c:2363-2384
-    if (rem < 25) return kStepMore;
-    plen = int32_t(be32(p));
-    k.offset_in_block = int64_t(be64(p + 4));
-    k.seqno = int64_t(be64(p + 12));
-    k.last = p[20] != 0;
-    dlen = int32_t(be32(p + 21));
-    k.header_len = 25;
-  } else {  // src/datanode.c:2387-2418
-    if (rem < 6) return kStepMore;
-    plen = int32_t(be32(p));
-    const uint32_t hlen = (uint32_t(p[4]) << 8) | p[5];
-    if (rem < 6 + uint64_t(hlen)) return kStepMore;
-    k.header_len = 6 + hlen;
-    Header h;
-    if (!decode_header(p + 6, hlen, h)) {
-      k.error = HDFS_CRC32C_ERR_INVALID_PACKETHEADERPROTO;
-      return kStepStop;
-    }
-    k.offset_in_block = h.offset;
-    k.seqno = h.seqno;
-    k.last = h.last;
-    k.sync = h.sync;
-    dlen = h.dlen;
-  }
-  // _process_recv_packet framing checks (src/datanode.c:2428-2446)
-  const int64_t crcdlen = plen - dlen - 4;
-  k.data_len = int32_t(dlen);
-  k.crc_len = int32_t(crcdlen);
-  if (plen < 0 || dlen < 0 || dlen > kOneGB || plen > kOneGB || crcdlen < 0)
-    k.error = HDFS_CRC32C_ERR_DATANODE_PACKET_SIZE;
-  else if (ctype != HDFS_CRC32C_CSUM_NULL && crcdlen != ((dlen + chunk_size - 1) / chunk_size) * 4)
-    k.error = HDFS_CRC32C_ERR_DATANODE_CRC_LEN;
-  else if (ctype == HDFS_CRC32C_CSUM_NULL && crcdlen > 0)
-    k.error = HDFS_CRC32C_ERR_DATANODE_UNEXPECTED_CRC_LEN;
-  if (k.error) return kStepStop;
-  if (dlen == 0) {  // src/datanode.c:2448-2456: v2's trailing empty packet
-    if (!k.last) k.error = HDFS_CRC32C_ERR_DATANODE_PACKET_SIZE;
-    total = k.header_len;
-    return kStepStop;
-  }
-  total = uint64_t(k.header_len) + uint64_t(crcdlen) + uint64_t(dlen);
-  if (rem < total) return kStepMore;  // incomplete: the reference reads more (src/datanode.c:2463-2467)
-  return kStepNext;
 }
 
 int parse_packet_stream(const uint8_t *s, uint64_t len, int proto, uint32_t chunk_size, int ctype,
@@ -476,7 +301,8 @@ struct DevBatch {
 };
 
 int submit_device_batch(DevCtx &c, const uint8_t *d, const std::vector<hdfs_crc32c_packet> &recs,
-                        const std::vector<size_t> &vidx, size_t bi, DevBatch &b, uint32_t cs, int ctype) {
+                        const std::vector<size_t> &vidx, size_t bi, DevBatch &b, uint32_t cs, int ctype,
+                        uint8_t *copy_dst, const std::vector<uint64_t> &vpay) {
   PieceLayout &L = b.L;
   L = PieceLayout{};
   L.n = b.v1 - b.v0;
@@ -512,6 +338,7 @@ int submit_device_batch(DevCtx &c, const uint8_t *d, const std::vector<hdfs_crc3
                               const_cast<uint8_t *>(crcp), dm + L.off_bm + boff};
     int rc = fill_seg(in, HDFS_CRC32C_MODE_VERIFY, hs[v], v);
     if (rc) return rc;
+    if (copy_dst) hs[v].copy_dst = copy_dst + vpay[b.v0 + v];
     classify(hs[v], L.rounds, L.gtiles, L.mtiles);
     boff += (uint64_t(k.crc_len) / 4 + 7) / 8;
   }
@@ -521,26 +348,30 @@ int submit_device_batch(DevCtx &c, const uint8_t *d, const std::vector<hdfs_crc3
   HIPCHK(hipMemcpyAsync(dm, hm, L.off_fb, hipMemcpyHostToDevice, c.v_stream));
   int rc = launch_all(c, kModeVerify, reinterpret_cast<const SegDev *>(dm), uint32_t(L.n), L.rounds, L.mtiles,
                       L.gtiles, reinterpret_cast<uint32_t *>(dm + L.off_fb), mism, gctr, c.v_stream, nullptr,
-                      nullptr, true, ctype == HDFS_CRC32C_CSUM_CRC32 ? 1 : 0);
+                      nullptr, true, ctype == HDFS_CRC32C_CSUM_CRC32 ? 1 : 0, copy_dst != nullptr);
   if (rc) return rc;
   HIPCHK(hipMemcpyAsync(hm + L.off_fb, dm + L.off_fb, L.meta - L.off_fb, hipMemcpyDeviceToHost, c.v_stream));
   return HDFS_CRC32C_OK;
 }
 
-// Framing walk over device memory (same records and stopping rules as
-// parse_packet_stream), verifying as it goes when `verify`: framing-clean
-// packets with CRCs are submitted in batches of 1 024 growing to 4 096
-// packets (the first launch starts early; later ones amortise the launch),
-// overlapped with the rest of the walk.  Caller holds c.mu.
+// Host framing walk over device memory through header windows (same
+// records and stopping rules as parse_packet_stream), from stream offset
+// `pos`, appending to `out`: the fallback of grid_walk for the part of a
+// stream whose packets are not all one size.  Verifies as it goes when
+// `verify`: framing-clean packets with CRCs are submitted in batches of
+// 1 024 growing to 4 096 packets (the first launch starts early; later ones
+// amortise the launch), overlapped with the rest of the walk.  copy_dst:
+// verify + copy-out, each packet's data at copy_dst + *payload (advanced
+// by every framing-clean packet).  Caller holds c.mu.
 int walk_device_stream(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs, int ctype,
-                       size_t max_pkts, bool verify, std::vector<hdfs_crc32c_packet> &out, uint64_t *consumed) {
-  out.clear();
-  *consumed = 0;
+                       size_t max_pkts, bool verify, std::vector<hdfs_crc32c_packet> &out, uint64_t *consumed,
+                       uint64_t pos, uint8_t *copy_dst, uint64_t *payload) {
   verify = verify && ctype != HDFS_CRC32C_CSUM_NULL;
   if (verify && !c.v_stream) HIPCHK(hipStreamCreateWithFlags(&c.v_stream, hipStreamNonBlocking));
   HeaderWindows w{c, d, len, proto};
   std::vector<uint8_t> big;  // v2 headers longer than a window row
-  std::vector<size_t> vidx;  // packets to verify
+  std::vector<size_t> vidx;     // packets to verify
+  std::vector<uint64_t> vpay;   // their copy-out offsets
   std::vector<DevBatch> batches;
   size_t batch_cap = 1024, v_sub = 0;
   auto submit = [&]() -> int {
@@ -549,9 +380,9 @@ int walk_device_stream(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uin
     b.v1 = vidx.size();
     v_sub = b.v1;
     batches.push_back(b);
-    return submit_device_batch(c, d, out, vidx, batches.size() - 1, batches.back(), cs, ctype);
+    return submit_device_batch(c, d, out, vidx, batches.size() - 1, batches.back(), cs, ctype, copy_dst, vpay);
   };
-  uint64_t pos = 0, stride = 0;
+  uint64_t stride = 0;
   int rc = HDFS_CRC32C_OK;
   using clk = std::chrono::steady_clock;
   const auto t0 = clk::now();
@@ -581,6 +412,7 @@ int walk_device_stream(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uin
     out.push_back(k);
     if (verify && !k.error && k.crc_len > 0) {
       vidx.push_back(out.size() - 1);
+      vpay.push_back(*payload);
       if (vidx.size() - v_sub >= batch_cap) {
         const auto ts = clk::now();
         rc = submit();
@@ -589,6 +421,7 @@ int walk_device_stream(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uin
         batch_cap = std::min<size_t>(batch_cap * 2, 4096);
       }
     }
+    if (!k.error) *payload += uint64_t(k.data_len);
     if (st == kStepStop) {
       if (!k.error) *consumed = pos + total;
       break;
@@ -626,9 +459,191 @@ int stream_device(const void *stream) {
   return -1;
 }
 
+// ---- device framing (frame_grid_kernel / grid_scan_kernel) ----
+// Layout of one pass's device tables and pinned landing area.
+constexpr uint32_t kBadFirst = 1024;  // bad-packet entries copied back with the verify summary
+struct GridLayout {
+  size_t recs, status, segs, seg2pkt, fb, sum, bad, ctr, bm, dtotal;  // device offsets
+  size_t h_recs, h_sum, h_sum2, h_bad, htotal;                         // pinned offsets
+  GridLayout(uint32_t count, uint64_t bm_cap) {
+    size_t o = 0;
+    auto take = [&](size_t n) { const size_t at = o; o += align_up(n, 256); return at; };
+    recs = take(size_t(count) * sizeof(hdfs_crc32c_packet));
+    status = take(size_t(count) * 4);
+    segs = take(size_t(count) * sizeof(SegDev));
+    seg2pkt = take(size_t(count) * 4);
+    fb = take(size_t(count) * 4);
+    sum = take(sizeof(GridSummary));
+    bad = take(size_t(count) * sizeof(GridBad));
+    ctr = take(128);  // pool counter, mismatch count
+    bm = take(size_t(bm_cap));
+    dtotal = o;
+    o = 0;
+    h_recs = take(size_t(count) * sizeof(hdfs_crc32c_packet));
+    h_sum = take(sizeof(GridSummary));
+    h_sum2 = take(sizeof(GridSummary));
+    h_bad = take(size_t(kBadFirst) * sizeof(GridBad));
+    htotal = o;
+  }
+};
+
+int reserve_grid(DevCtx &c, size_t si, const GridLayout &L) {
+  if (si >= c.grid.size()) c.grid.resize(si + 1);
+  DevCtx::GridSlot &g = c.grid[si];  // previous user: an earlier call, synchronised at its end
+  if (L.dtotal > g.dcap) {
+    if (g.d) HIPCHK(hipFree(g.d));
+    g.d = nullptr;
+    g.dcap = 0;
+    HIPCHK(hipMalloc(&g.d, L.dtotal));
+    g.dcap = L.dtotal;
+  }
+  if (L.htotal > g.hcap) {
+    if (g.h) HIPCHK(hipHostFree(g.h));
+    g.h = nullptr;
+    g.hcap = 0;
+    HIPCHK(hipHostMalloc(&g.h, L.htotal, hipHostMallocDefault));
+    g.hcap = L.htotal;
+  }
+  return HDFS_CRC32C_OK;
+}
+
+// Framing + verify of a device-resident stream, run by run on the device:
+// each pass frames up to kGridMaxCount packets on the grid of the first
+// packet's size (frame_grid_kernel), builds their verify segment table in
+// HBM (grid_scan_kernel) and returns only a summary; the verify launch
+// (plus the optional fused copy-out) is enqueued on c.v_stream straight
+// from that summary while the records come back on c.stream.  A pass that
+// leaves the grid after at most two packets (a stream of mixed sizes) hands
+// the rest to the host window walk (walk_device_stream).  Same records,
+// stopping rules and consumed offset as parse_packet_stream.
+int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs, int ctype, size_t max_pkts,
+              bool verify, uint8_t *copy_dst, uint64_t copy_cap, std::vector<hdfs_crc32c_packet> &out,
+              uint64_t *consumed, uint64_t *payload_out) {
+  out.clear();
+  *consumed = 0;
+  verify = verify && ctype != HDFS_CRC32C_CSUM_NULL;
+  if (!c.v_stream) HIPCHK(hipStreamCreateWithFlags(&c.v_stream, hipStreamNonBlocking));
+  const uint32_t sflags = HDFS_CRC32C_SEG_BE | (ctype == HDFS_CRC32C_CSUM_CRC32 ? HDFS_CRC32C_SEG_CRC32 : 0u);
+  const int tset = ctype == HDFS_CRC32C_CSUM_CRC32 ? 1 : 0;
+  struct Pass {
+    size_t slot, off, n;
+    uint32_t nseg, count;
+    uint64_t bm_cap;
+  };
+  std::vector<Pass> passes;
+  uint64_t pos = 0, payload = 0;
+  int rc = HDFS_CRC32C_OK;
+  bool fallback = false;
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
+  while (out.size() < max_pkts && pos < len) {
+    const uint64_t left = len - pos;
+    const uint32_t count = uint32_t(std::min<uint64_t>({uint64_t(max_pkts - out.size()), kGridMaxCount, left / 6 + 1}));
+    const uint64_t bm_cap = left / 32 + count + 64;  // >= sum of ceil(chunks / 8) over the run
+    const GridLayout L(count, bm_cap);
+    const size_t si = passes.size();
+    if ((rc = reserve_grid(c, si, L))) break;
+    uint8_t *dg = c.grid[si].d, *hg = c.grid[si].h;
+    auto *recs = reinterpret_cast<hdfs_crc32c_packet *>(dg + L.recs);
+    auto *sum = reinterpret_cast<GridSummary *>(dg + L.sum);
+    hipError_t e = hipMemsetAsync(&sum->first_break, 0xFF, 4, c.stream);
+    if (e == hipSuccess) e = launch_frame_grid(d, len, pos, count, proto, cs, ctype, recs,
+                                               reinterpret_cast<uint32_t *>(dg + L.status), sum, c.stream);
+    if (e == hipSuccess)
+      e = launch_grid_scan(d, pos, count, recs, reinterpret_cast<const uint32_t *>(dg + L.status), cs, sflags,
+                           verify ? 1 : 0, dg + L.bm, copy_dst ? copy_dst + payload : nullptr,
+                           reinterpret_cast<SegDev *>(dg + L.segs), reinterpret_cast<uint32_t *>(dg + L.seg2pkt),
+                           reinterpret_cast<uint32_t *>(dg + L.fb), sum, c.stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(hg + L.h_sum, sum, sizeof(GridSummary), hipMemcpyDeviceToHost, c.stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c.stream);
+    if (e != hipSuccess) {
+      rc = fail(HDFS_CRC32C_EHIP, "device framing: %s", hipGetErrorString(e));
+      break;
+    }
+    const GridSummary S = *reinterpret_cast<const GridSummary *>(hg + L.h_sum);
+    if (S.recorded)
+      HIPCHK(hipMemcpyAsync(hg + L.h_recs, recs, size_t(S.recorded) * sizeof(hdfs_crc32c_packet),
+                            hipMemcpyDeviceToHost, c.stream));
+    if (copy_dst && payload + S.payload > copy_cap) {
+      rc = fail(HDFS_CRC32C_EINVAL, "copy-out buffer of %llu bytes is too small (%llu needed so far)",
+                (unsigned long long)copy_cap, (unsigned long long)(payload + S.payload));
+      break;
+    }
+    if (verify && S.nseg) {
+      auto *ctr = reinterpret_cast<uint32_t *>(dg + L.ctr);
+      rc = launch_all(c, kModeVerify, reinterpret_cast<const SegDev *>(dg + L.segs), S.nseg, S.rounds, S.mtiles,
+                      S.gtiles, reinterpret_cast<uint32_t *>(dg + L.fb), reinterpret_cast<unsigned long long *>(ctr + 16),
+                      ctr, c.v_stream, nullptr, nullptr, false, tset, copy_dst != nullptr);
+      if (rc) break;
+      auto *bad = reinterpret_cast<GridBad *>(dg + L.bad);
+      HIPCHK(launch_grid_finalize(reinterpret_cast<const SegDev *>(dg + L.segs), S.nseg,
+                                  reinterpret_cast<const uint32_t *>(dg + L.seg2pkt),
+                                  reinterpret_cast<const uint32_t *>(dg + L.fb), bad, count, sum, c.v_stream));
+      HIPCHK(hipMemcpyAsync(hg + L.h_sum2, sum, sizeof(GridSummary), hipMemcpyDeviceToHost, c.v_stream));
+      HIPCHK(hipMemcpyAsync(hg + L.h_bad, bad, size_t(std::min(kBadFirst, S.nseg)) * sizeof(GridBad),
+                            hipMemcpyDeviceToHost, c.v_stream));
+    }
+    passes.push_back({si, out.size(), S.recorded, verify ? S.nseg : 0u, count, bm_cap});
+    out.resize(out.size() + S.recorded);
+    payload += S.payload;
+    *consumed = S.consumed;
+    if (S.last_status == kGridStop || S.last_status == kGridMore) break;
+    pos = S.next_pos;
+    if (S.last_status == kGridOff && S.recorded <= 2) {
+      fallback = true;
+      break;
+    }
+  }
+  const auto t1 = clk::now();
+  // records of every pass (their copies overlapped the verify launches)
+  hipError_t e = hipStreamSynchronize(c.stream);
+  if (!rc && e != hipSuccess) rc = fail(HDFS_CRC32C_EHIP, "framing records: %s", hipGetErrorString(e));
+  if (!rc)
+    for (const Pass &p : passes)
+      if (p.n) std::memcpy(out.data() + p.off, c.grid[p.slot].h + GridLayout(p.count, p.bm_cap).h_recs,
+                           p.n * sizeof(hdfs_crc32c_packet));
+  if (!rc && fallback && out.size() < max_pkts)
+    rc = walk_device_stream(c, d, len, proto, cs, ctype, max_pkts, verify, out, consumed, pos, copy_dst, &payload);
+  e = hipStreamSynchronize(c.v_stream);  // drained even after an error: its tables live in this context
+  if (!rc && e != hipSuccess) rc = fail(HDFS_CRC32C_EHIP, "verify: %s", hipGetErrorString(e));
+  if (!rc && copy_dst && payload > copy_cap)
+    rc = fail(HDFS_CRC32C_EINVAL, "copy-out buffer of %llu bytes is too small (%llu needed)",
+              (unsigned long long)copy_cap, (unsigned long long)payload);
+  if (rc) return rc;
+  // verify verdicts: the compact list of packets with bad chunks
+  for (const Pass &p : passes) {
+    if (!p.nseg) continue;
+    const GridLayout L(p.count, p.bm_cap);
+    const uint8_t *hg = c.grid[p.slot].h;
+    const uint32_t nbad = reinterpret_cast<const GridSummary *>(hg + L.h_sum2)->nbad;
+    std::vector<GridBad> more;
+    const GridBad *bad = reinterpret_cast<const GridBad *>(hg + L.h_bad);
+    if (nbad > kBadFirst) {
+      more.resize(nbad);
+      HIPCHK(hipMemcpy(more.data(), c.grid[p.slot].d + L.bad, nbad * sizeof(GridBad), hipMemcpyDeviceToHost));
+      bad = more.data();
+    }
+    for (uint32_t i = 0; i < nbad; i++) {
+      hdfs_crc32c_packet &k = out[p.off + bad[i].pkt];
+      k.error = HDFS_CRC32C_ERR_DATANODE_BAD_CHECKSUM;
+      k.first_bad = bad[i].first_bad;
+      k.bad_chunks = bad[i].bad_chunks;
+    }
+  }
+  if (g_dstream_trace) {  // diagnostic: where a device-stream call spends its time (us)
+    const auto t2 = clk::now();
+    auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+    std::fprintf(stderr, "dstream grid pkts=%zu passes=%zu fallback=%d frame_us=%.1f total_us=%.1f\n", out.size(),
+                 passes.size(), int(fallback), us(t0, t1), us(t0, t2));
+  }
+  if (payload_out) *payload_out = payload;
+  return HDFS_CRC32C_OK;
+}
+
 int verify_packets_dev_impl(int dev, const uint8_t *stream, uint64_t len, int proto, uint32_t cs, int ctype,
                             hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts, uint64_t *consumed,
-                            bool verify) {
+                            bool verify, uint8_t *copy_dst = nullptr, uint64_t copy_cap = 0,
+                            uint64_t *delivered = nullptr) {
   DevCtx *cp = nullptr;
   int rc;
   if ((rc = ctx_init(dev, &cp))) return rc;
@@ -637,10 +652,19 @@ int verify_packets_dev_impl(int dev, const uint8_t *stream, uint64_t len, int pr
   std::lock_guard<std::mutex> lk(c.mu);
   std::vector<hdfs_crc32c_packet> recs;
   uint64_t used = 0;
-  if ((rc = walk_device_stream(c, stream, len, proto, cs, ctype, max_pkts, verify, recs, &used))) return rc;
+  if ((rc = grid_walk(c, stream, len, proto, cs, ctype, max_pkts, verify, copy_dst, copy_cap, recs, &used, nullptr)))
+    return rc;
   if (!recs.empty()) std::memcpy(pkts, recs.data(), recs.size() * sizeof(hdfs_crc32c_packet));
   if (npkts) *npkts = recs.size();
   if (consumed) *consumed = used;
+  if (delivered) {  // what the reference copies out before its loop returns an error (src/datanode.c:2470-2486)
+    uint64_t n = 0;
+    for (const auto &k : recs) {
+      if (k.error) break;
+      n += uint64_t(k.data_len);
+    }
+    *delivered = n;
+  }
   return first_error(recs.data(), recs.size());
 }
 
@@ -961,6 +985,27 @@ int hdfs_crc32c_verify_packets(const void *stream, uint64_t len, int proto, uint
                                hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts, uint64_t *consumed) {
   return verify_packets_impl(static_cast<const uint8_t *>(stream), len, proto, chunk_size, ctype, pkts, max_pkts,
                              npkts, consumed, true);
+}
+
+int hdfs_crc32c_verify_packets_copy(const void *stream, uint64_t len, int proto, uint32_t chunk_size, int ctype,
+                                    hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts, uint64_t *consumed,
+                                    void *dst, uint64_t dst_cap, uint64_t *delivered) {
+  if (npkts) *npkts = 0;
+  if (consumed) *consumed = 0;
+  if (delivered) *delivered = 0;
+  if (max_pkts && !pkts) return fail(HDFS_CRC32C_EINVAL, "null packet array");
+  int rc = check_framing_args(proto, chunk_size, ctype, g_err, sizeof(g_err));
+  if (rc) return rc;
+  if (ctype == HDFS_CRC32C_CSUM_NULL)
+    return fail(HDFS_CRC32C_EINVAL, "verify + copy-out needs CRC32 or CRC32C (src/datanode.c:2470-2486)");
+  if (!len) return HDFS_CRC32C_OK;
+  if (!stream) return fail(HDFS_CRC32C_EINVAL, "null stream");
+  const int dev = stream_device(stream);
+  if (dev < 0) return fail(HDFS_CRC32C_EINVAL, "verify + copy-out takes device-resident streams only");
+  if (!dst || stream_device(dst) != dev)
+    return fail(HDFS_CRC32C_EINVAL, "copy-out destination must be device memory of the stream's device");
+  return verify_packets_dev_impl(dev, static_cast<const uint8_t *>(stream), len, proto, chunk_size, ctype, pkts,
+                                 max_pkts, npkts, consumed, true, static_cast<uint8_t *>(dst), dst_cap, delivered);
 }
 
 int hdfs_crc32c_compose_packets(const void *data, uint64_t len, int64_t offset_in_block, int64_t seqno, int proto,

@@ -8,6 +8,7 @@
 #include <cstdint>
 #include <vector>
 
+#include "crc32c_frame.h"
 #include "hadoofus_crc32c.h"
 
 namespace hdfs_crc32c {
@@ -27,12 +28,11 @@ int parse_packet_stream(const uint8_t *s, uint64_t len, int proto, uint32_t chun
 // Argument checks shared by every framing entry (EINVAL + message).
 int check_framing_args(int proto, uint32_t chunk_size, int ctype, char *errbuf, size_t errlen);
 
-// One step of the walk: the packet at stream offset `pos`, whose first bytes
-// are at p (rem = bytes of the stream from pos on; p must hold
-// min(rem, kHdrWin) bytes, enough for any v1 header and any v2 header of
-// up to kHdrWin - 6 bytes -- a longer v2 header needs 6 + hlen).
-enum { kStepNext = 0, kStepStop = 1, kStepMore = 2 };
-int frame_step(const uint8_t *p, uint64_t rem, uint64_t pos, int proto, uint32_t chunk_size, int ctype,
-               hdfs_crc32c_packet &k, uint64_t &total);
+// One step of the walk (crc32c_frame.h, shared with the device framing
+// kernel): the packet at stream offset `pos`, whose first bytes are at p.
+using frame::frame_step;
+using frame::kStepMore;
+using frame::kStepNext;
+using frame::kStepStop;
 
 }  // namespace hdfs_crc32c

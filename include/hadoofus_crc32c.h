@@ -183,7 +183,8 @@ typedef struct hdfs_crc32c_packet {
 
 /* Framing only: walks up to max_pkts packets of the stream (host memory:
  * no device work; device memory: the headers are read through
- * header-window copies), applying the checks of src/datanode.c:2428-2456
+ * device framing kernels, with a host walk over header windows for streams
+ * of mixed packet sizes), applying the checks of src/datanode.c:2428-2456
  * (PACKET_SIZE, CRC_LEN, UNEXPECTED_CRC_LEN, empty non-last packet) and the
  * header decode (INVALID_PACKETHEADERPROTO).  The walk stops after a framing
  * error (recorded in that packet's .error), after an empty last packet (end
@@ -201,6 +202,21 @@ int hdfs_crc32c_parse_packets(const void *stream, uint64_t len, int proto, uint3
  * returns from its packet loop), 0, or a negative status. */
 int hdfs_crc32c_verify_packets(const void *stream, uint64_t len, int proto, uint32_t chunk_size,
     int ctype, hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts, uint64_t *consumed);
+
+/* Verify + copy-out of a DEVICE-resident packet stream (GPU-direct
+ * receive): hdfs_crc32c_verify_packets, and in the same pass over HBM the
+ * data of every framing-clean packet is written, de-framed and in stream
+ * order, to the device buffer dst (dst_cap bytes) -- the read path's
+ * _recv_packet_copy_data (src/datanode.c:2496-2553) fused into the verify
+ * kernel: each payload byte is read once and written once.  *delivered =
+ * payload bytes of the packets before the first packet with an error, i.e.
+ * what the reference copies to the caller before its packet loop returns
+ * that error (src/datanode.c:2470-2486); bytes of dst past *delivered are
+ * unspecified.  ctype must be CRC32 or CRC32C.  Returns as verify_packets;
+ * EINVAL if dst is too small for the framed payload. */
+int hdfs_crc32c_verify_packets_copy(const void *stream, uint64_t len, int proto, uint32_t chunk_size,
+    int ctype, hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts, uint64_t *consumed,
+    void *dst, uint64_t dst_cap, uint64_t *delivered);
 
 /* ---- write path: outgoing data packets ---------------------------------- */
 /* One outgoing data packet, as _send_packet sizes it and

@@ -61,15 +61,16 @@ def test_release_has_no_diagnostic_knobs(libpath, diagpath):
 
 
 def test_release_kernels_are_the_product_shapes(libpath, diagpath):
-    """Four tiled-kernel instantiations in the release build (compute /
-    verify x schedule 3 buffer loads / schedule 2), no load-only twin
-    (mode 2) and no read probes; the diagnostic build has them."""
+    """Six tiled-kernel instantiations in the release build (compute /
+    verify / verify + copy-out x schedule 3 buffer loads / schedule 2), no
+    load-only twin (mode 2) and no read probes; the diagnostic build has them."""
     import re as _re
     rel = open(libpath, "rb").read()
     dia = open(diagpath, "rb").read()
-    pat = rb"_ZN11hdfs_crc32c19crc32c_tiles_kernelILi(\d)ELi(\d)ELi(\d)ELi(\d)ELi(\d)ELi(\d+)ELi(\d)EEE"
+    pat = (rb"_ZN11hdfs_crc32c19crc32c_tiles_kernelILi(\d)ELi(\d)ELi(\d)ELi(\d)ELi(\d)ELi(\d+)ELi(\d)ELi(\d)"
+           rb"EEE")
     shapes = set(_re.findall(pat, rel))
-    assert shapes == {(m, o, b"1", b"3", b"1", b"1024", buf) for m in (b"0", b"1")
+    assert shapes == {(m, o, b"1", b"3", b"1", b"1024", buf, cp) for m, cp in ((b"0", b"0"), (b"1", b"0"), (b"1", b"1"))
                       for o, buf in ((b"3", b"1"), (b"2", b"0"))}, shapes
     assert b"probe_read_kernel" not in rel and b"probe2_kernel" not in rel
     dshapes = set(_re.findall(pat, dia))

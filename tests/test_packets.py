@@ -259,3 +259,105 @@ def test_gpu_device_stream_first_window_guess(engine, oracle, proto):
         assert engine.verify_packets(None, proto, cs, CSUM_CRC32C, dptr=p, nbytes=len(c)) == want, len(c)
         assert engine.verify_packets(c, proto, cs, CSUM_CRC32C) == want, len(c)
         keep.free()
+
+
+# --- GPU: device-resident streams, verify + copy-out -------------------------
+def _payloads(s, pkts):
+    """Data bytes of every packet before the first error (what the reference
+    copies out, src/datanode.c:2470-2553), concatenated in stream order."""
+    out = bytearray()
+    for p in pkts:
+        if p["error"]:
+            break
+        a = p["stream_off"] + p["header_len"] + p["crc_len"]
+        out += s[a:a + p["data_len"]]
+    return bytes(out)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("proto,cs,ctype,sizes,shift,corrupt_at", [
+    (2, 512, CSUM_CRC32C, "regular", 0, None),   # device framing in one pass, tiled kernel copies
+    (2, 512, CSUM_CRC32C, "regular", 3, 400),    # odd offsets; copy stops counting at the bad packet
+    (1, 512, CSUM_CRC32C, "regular", 1, None),
+    (2, 512, CSUM_CRC32, "partial", 0, None),    # 40000-B packets: partial chunks copied by the generic kernel
+    (2, 100, CSUM_CRC32C, "partial", 2, 7),      # chunk 100: every chunk on the generic kernel
+    (2, 4096, CSUM_CRC32C, "mixed", 0, None),    # sizes change: grid passes + window-walk fallback
+    (2, 512, CSUM_CRC32C, "random", 1, 150),
+])
+def test_gpu_device_stream_copy_out(engine, oracle, proto, cs, ctype, sizes, shift, corrupt_at):
+    """Verify + fused copy-out (hdfs_crc32c_verify_packets_copy): records equal
+    the oracle's, and the destination holds exactly the de-framed payload of
+    every packet before the first error, byte for byte."""
+    rng = np.random.default_rng(cs + proto + shift)
+    if sizes == "regular":
+        dl = [65536] * 600 + [12345]
+    elif sizes == "partial":
+        dl = [40000] * 200
+    elif sizes == "mixed":
+        dl = [int(x) for x in np.repeat(rng.choice([4096, 61440, 30000, 65536], 40), rng.integers(1, 8, 40))]
+    else:
+        dl = [int(x) for x in rng.integers(1, 70000, 250)]
+    corrupt = [] if corrupt_at is None else [(corrupt_at, 1)]
+    s, bad = build_stream(oracle.crc32c, proto, cs, ctype, dl, seed=len(dl) + cs, corrupt=corrupt)
+    mp = len(dl) + 2
+    want = oracle.verify_packets(s, proto, cs, ctype, max_pkts=mp)
+    keep, p = _dev(engine, s, shift)
+    total = sum(dl)
+    dst = engine.DeviceBuffer(total + 64)
+    dst.fill(0xA5)
+    rc, pkts, used, delivered = engine.verify_packets_copy(p, len(s), dst.ptr, total, proto, cs, ctype, max_pkts=mp)
+    assert (rc, pkts, used) == want
+    expect = _payloads(s, want[1])
+    assert delivered == len(expect)
+    assert dst.download(delivered).tobytes() == expect
+    if corrupt_at is None:
+        assert delivered == total
+    # the plain verify of the same bytes agrees
+    assert engine.verify_packets(None, proto, cs, ctype, max_pkts=mp, dptr=p, nbytes=len(s)) == want
+    keep.free()
+    dst.free()
+
+
+@pytest.mark.gpu
+def test_gpu_device_stream_copy_out_errors(engine, oracle):
+    """Refused: a destination smaller than the payload, a host stream, a
+    host destination and CSUM_NULL (no verify to fuse the copy into)."""
+    s, _ = build_stream(oracle.crc32c, 2, 512, CSUM_CRC32C, [65536] * 8, seed=3)
+    keep, p = _dev(engine, s)
+    dst = engine.DeviceBuffer(8 * 65536)
+    with pytest.raises(engine.CRC32CError):
+        engine.verify_packets_copy(p, len(s), dst.ptr, 8 * 65536 - 1)
+    host = np.zeros(8 * 65536, np.uint8)
+    with pytest.raises(engine.CRC32CError):
+        engine.verify_packets_copy(p, len(s), host.ctypes.data, host.nbytes)
+    with pytest.raises(engine.CRC32CError):
+        engine.verify_packets_copy(p, len(s), dst.ptr, dst.nbytes, ctype=0)
+    src = np.frombuffer(s, np.uint8).copy()
+    with pytest.raises(engine.CRC32CError):
+        engine.verify_packets_copy(src.ctypes.data, len(s), dst.ptr, dst.nbytes)
+    rc, pkts, used, delivered = engine.verify_packets_copy(p, len(s), dst.ptr, dst.nbytes)
+    assert rc == 0 and delivered == 8 * 65536 and used == len(s)
+    keep.free()
+    dst.free()
+
+
+@pytest.mark.gpu
+def test_gpu_device_stream_many_passes(engine, oracle):
+    """More packets than one device framing pass holds (65 536 grid points):
+    2 KiB packets, ~200 MiB of stream, two passes plus the tail; records,
+    verdicts and the copied payload are exact."""
+    n = 70000
+    dl = [2048] * n + [1000]
+    s, bad = build_stream(oracle.crc32c, 2, 512, CSUM_CRC32C, dl, seed=77, corrupt=[(5, 0), (65535, 3), (65536, 2),
+                                                                                     (69999, 1)])
+    mp = len(dl) + 2
+    want = oracle.verify_packets(s, max_pkts=mp)
+    keep, p = _dev(engine, s)
+    got = engine.verify_packets(None, max_pkts=mp, dptr=p, nbytes=len(s))
+    assert got == want
+    dst = engine.DeviceBuffer(sum(dl))
+    rc, pkts, used, delivered = engine.verify_packets_copy(p, len(s), dst.ptr, dst.nbytes, max_pkts=mp)
+    assert (rc, pkts, used) == want and delivered == 5 * 2048
+    assert dst.download(delivered).tobytes() == _payloads(s, want[1])
+    keep.free()
+    dst.free()

@@ -34,14 +34,19 @@ def wire_image(nbytes, seed):
     return out, len(pk)
 
 
-def timed(ptr, n, npk, reps=5, fn="hdfs_crc32c_verify_packets"):
+def timed(ptr, n, npk, reps=5, fn="hdfs_crc32c_verify_packets", dst=None):
     arr = (h.abi.Packet * (npk + 8))()
-    cnt, used = ctypes.c_size_t(0), ctypes.c_uint64(0)
+    cnt, used, got = ctypes.c_size_t(0), ctypes.c_uint64(0), ctypes.c_uint64(0)
     best, rc = 1e9, None
     for _ in range(reps):
         t0 = time.perf_counter()
-        rc = getattr(lib, fn)(ptr, n, h.PROTO_V2, 512, h.CSUM_CRC32C, arr, npk + 8, ctypes.byref(cnt),
-                              ctypes.byref(used))
+        if dst is not None:  # verify + fused copy-out
+            rc = lib.hdfs_crc32c_verify_packets_copy(ptr, n, h.PROTO_V2, 512, h.CSUM_CRC32C, arr, npk + 8,
+                                                     ctypes.byref(cnt), ctypes.byref(used), dst.ptr, dst.nbytes,
+                                                     ctypes.byref(got))
+        else:
+            rc = getattr(lib, fn)(ptr, n, h.PROTO_V2, 512, h.CSUM_CRC32C, arr, npk + 8, ctypes.byref(cnt),
+                                  ctypes.byref(used))
         best = min(best, time.perf_counter() - t0)
     assert rc >= 0 and cnt.value == npk and used.value == n, (rc, cnt.value, used.value)
     return best, rc, arr
@@ -58,6 +63,13 @@ pin.array[:] = img
 h.device_sync()
 t_dev, rc, _ = timed(dev.ptr, img.nbytes, npk)
 assert rc == 0
+dst = h.DeviceBuffer(payload)
+t_copy, rc, _ = timed(dev.ptr, img.nbytes, npk, dst=dst)
+assert rc == 0
+# the copied-out payload is the de-framed data, byte for byte
+H0 = img.nbytes // npk - 65536
+want = img.reshape(npk, H0 + 65536)[:, H0:].reshape(-1)
+copy_ok = bool(np.array_equal(dst.download(), want))
 t_parse, rc, _ = timed(dev.ptr, img.nbytes, npk, fn="hdfs_crc32c_parse_packets")
 assert rc == 0
 t_hparse, rc, _ = timed(pin.ptr, img.nbytes, npk, fn="hdfs_crc32c_parse_packets")
@@ -66,7 +78,9 @@ t_pin, rc, _ = timed(pin.ptr, img.nbytes, npk, reps=3)
 assert rc == 0
 out.update(packets=npk, wire_bytes=int(img.nbytes), device_GiBps=round(payload / t_dev / 2**30, 1),
            device_ms=round(t_dev * 1e3, 3), device_parse_ms=round(t_parse * 1e3, 3),
-           host_parse_ms=round(t_hparse * 1e3, 3), pinned_GiBps=round(payload / t_pin / 2**30, 1))
+           host_parse_ms=round(t_hparse * 1e3, 3), pinned_GiBps=round(payload / t_pin / 2**30, 1),
+           device_copy_GiBps=round(payload / t_copy / 2**30, 1), device_copy_ms=round(t_copy * 1e3, 3),
+           copy_bytes_exact=copy_ok)
 # one flipped bit per 1000th packet: verdicts come back for exactly those
 flips = list(range(5, npk, 1000))
 H = img.nbytes // npk - 65536
@@ -83,6 +97,9 @@ for npk_s in (1, 64):
     n = npk_s * (H + 65536)
     t, rc, _ = timed(dev.ptr, n, npk_s, reps=20)
     out[f"device_{npk_s}pkt_us"] = round(t * 1e6, 1)
+    t, rc, _ = timed(dev.ptr, n, npk_s, reps=20, dst=dst)
+    out[f"device_copy_{npk_s}pkt_us"] = round(t * 1e6, 1)
+dst.free()
 dev.free()
 pin.free()
 print(json.dumps(out))
