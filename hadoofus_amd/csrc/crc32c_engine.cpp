@@ -217,6 +217,12 @@ bool device_accessible(const void *p) {
   return a.devicePointer != nullptr;
 }
 
+bool any_unaligned(const SegDev *segs, size_t n) {
+  for (size_t i = 0; i < n; i++)
+    if (segs[i].main_tiles && (reinterpret_cast<uintptr_t>(segs[i].data) & 3u)) return true;
+  return false;
+}
+
 // HDFS_CRC32C_SMALL_RULE=0 (experiments): keep schedule 3 for small launches
 // and tables of small segments.
 static const int g_small_rule = HDFS_KNOB("HDFS_CRC32C_SMALL_RULE", 1);
@@ -224,9 +230,10 @@ static const int g_small_rule = HDFS_KNOB("HDFS_CRC32C_SMALL_RULE", 1);
 // ctype: 0 = CRC32C, 1 = CRC32 (zlib polynomial) -- selects the table set.
 int launch_all(DevCtx &c, int mode, const SegDev *d_segs, uint32_t nseg, uint64_t rounds,
                uint64_t mtiles, uint64_t gtiles, uint32_t *d_fb, unsigned long long *d_mism,
-               uint32_t *d_gctr, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1, bool reset, int ctype, bool copy) {
+               uint32_t *d_gctr, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1, bool reset, int ctype, bool copy,
+               bool gctr_zeroed, bool una) {
   const bool vreset = mode == kModeVerify && reset;
-  uint32_t *gz = (rounds && g_tile_order >= 2) ? d_gctr : nullptr;
+  uint32_t *gz = (rounds && g_tile_order >= 2 && !gctr_zeroed) ? d_gctr : nullptr;
   if (vreset || gz)
     HIPCHK(launch_prep(vreset ? d_fb : nullptr, vreset ? (nseg ? nseg : 1u) : 0u, vreset ? d_mism : nullptr, gz, st));
   if (rounds) {
@@ -250,7 +257,7 @@ int launch_all(DevCtx &c, int mode, const SegDev *d_segs, uint32_t nseg, uint64_
     const hipError_t le = launch_tiles(kmode, order, nt, depth, streams, block, grid, d_segs, nseg, rounds,
                                        mtiles, c.d_tab_main_t[ctype], d_fb, d_mism, kDiag ? g_diag : nullptr,
                                        (kDiag ? g_store_policy : 0u) | (g_group_shift << 8) | (g_xcd_major << 12),
-                                       d_gctr, st, copy ? 1 : 0);
+                                       d_gctr, st, copy ? 1 : 0, una ? 1 : 0);
     if (le == hipErrorInvalidValue)
       return fail(HDFS_CRC32C_EINVAL, "tiled kernel shape (order %d, nt %d, depth %d, streams %d, block %d) is not built",
                   order, nt, depth, streams, block);
@@ -285,7 +292,7 @@ int stream_crc_locked(DevCtx &c, uint32_t crc, const void *dbuf, uint64_t len, u
   classify(s, rounds, gtiles, mtiles);
   HIPCHK(hipMemcpyAsync(c.d_seg, &s, sizeof(s), hipMemcpyHostToDevice, c.stream));
   rc = launch_all(c, kModeCompute, c.d_seg, 1, rounds, mtiles, gtiles, nullptr, nullptr, c.d_small + 8, c.stream,
-                  nullptr, nullptr, true, ctype);
+                  nullptr, nullptr, true, ctype, false, false, any_unaligned(&s, 1));
   if (rc) return rc;
   HIPCHK(hipMemsetAsync(c.d_small, 0, 4, c.stream));
   HIPCHK(launch_combine(c.d_raw, nraw, kStreamPiece, len, c.d_tab_pow2_t[ctype], ~crc, c.d_small, c.stream));
@@ -579,7 +586,7 @@ int chunk_crcs_to_host(const void *data, uint64_t len, uint32_t cs, int ctype, u
   }
   if (!rc)
     rc = launch_all(*c, kModeCompute, c->d_seg, 1, rounds, mtiles, gtiles, nullptr, nullptr, c->d_small + 8,
-                    c->stream, nullptr, nullptr, true, tset);
+                    c->stream, nullptr, nullptr, true, tset, false, false, any_unaligned(&sd, 1));
   if (!rc) {
     hipError_t e = hipMemcpyAsync(out_be, d_out, size_t(nch) * 4, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
@@ -608,6 +615,7 @@ struct hdfs_crc32c_plan {
   uint32_t *d_gctr = nullptr;  // tiled-kernel pool counter (schedule 2)
   uint64_t rounds = 0, mtiles = 0, gtiles = 0, main_bytes = 0, gen_bytes = 0, nchunks = 0;
   bool timing = false;
+  bool una = false;  // some tiled segment's data is not 4-B aligned
   std::vector<std::pair<hipEvent_t, hipEvent_t>> events;  // pre-created pool
   size_t next_event = 0;
 };
@@ -728,6 +736,7 @@ int hdfs_crc32c_plan_create(hdfs_crc32c_plan **plan, int mode, const hdfs_crc32c
   p->main_bytes = main_bytes;
   p->gen_bytes = gen_bytes;
   p->nchunks = nch;
+  p->una = any_unaligned(host.data(), nseg);
   hipError_t e = hipMalloc(&p->d_segs, sizeof(SegDev) * host.size());
   if (e == hipSuccess) e = hipMemcpy(p->d_segs, host.data(), sizeof(SegDev) * host.size(), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMalloc(&p->d_first_bad, sizeof(uint32_t) * host.size());
@@ -759,7 +768,7 @@ int hdfs_crc32c_plan_execute(hdfs_crc32c_plan *p, void *stream) {
     p->next_event++;
   }
   return launch_all(c, p->mode, p->d_segs, p->nseg, p->rounds, p->mtiles, p->gtiles, p->d_first_bad,
-                    p->d_mism, p->d_gctr, st, e0, e1, true, p->ctype);
+                    p->d_mism, p->d_gctr, st, e0, e1, true, p->ctype, false, false, p->una);
 }
 
 int hdfs_crc32c_plan_results(hdfs_crc32c_plan *p, void *stream, uint32_t *first_bad, size_t nseg,

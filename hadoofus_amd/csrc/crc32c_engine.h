@@ -20,7 +20,7 @@ hipError_t launch_tiles(int mode, int order, int nt, int depth, int streams, int
                         const SegDev *segs, uint32_t nseg, uint64_t total_rounds, uint64_t total_tiles,
                         const uint32_t *gtab, uint32_t *first_bad, unsigned long long *mism,
                         unsigned long long *diag, uint32_t tune, uint32_t *gctr, hipStream_t stream,
-                        int copy = 0);
+                        int copy = 0, int una = 0);
 hipError_t launch_probe_read(const uint8_t *p, uint64_t nbytes, uint32_t *out, int grid, int block, int variant,
                              hipStream_t stream);
 hipError_t launch_generic(int mode, const SegDev *segs, uint32_t nseg, uint64_t total_gtiles,
@@ -45,13 +45,10 @@ hipError_t launch_header_window(const uint8_t *s, uint64_t len, uint64_t base, u
                                 int proto, uint8_t *out, uint64_t *stride_out, hipStream_t stream);
 
 // device framing of device-resident packet streams (crc32c_kernels.hip)
+// frame_grid_kernel + grid_build_kernel: one device framing pass.
 hipError_t launch_frame_grid(const uint8_t *s, uint64_t len, uint64_t base, uint32_t count, int proto, uint32_t cs,
-                             int ctype, hdfs_crc32c_packet *recs, uint32_t *status, GridSummary *sum,
-                             hipStream_t stream);
-hipError_t launch_grid_scan(const uint8_t *s, uint64_t base, uint32_t count, const hdfs_crc32c_packet *recs,
-                            const uint32_t *status, uint32_t cs, uint32_t sflags, int verify, uint8_t *bm_base,
-                            uint8_t *copy_base, SegDev *segs, uint32_t *seg2pkt, uint32_t *fb, GridSummary *sum,
-                            hipStream_t stream);
+                             int ctype, int verify, uint32_t sflags, uint8_t *bm_base, uint8_t *copy_base,
+                             GridBufs g, hipStream_t stream);
 hipError_t launch_grid_finalize(const SegDev *segs, uint32_t nseg, const uint32_t *seg2pkt, const uint32_t *fb,
                                 GridBad *bad, uint32_t bad_cap, GridSummary *sum, hipStream_t stream);
 
@@ -183,7 +180,9 @@ bool is_pinned_host(const void *p);
 int launch_all(DevCtx &c, int mode, const SegDev *d_segs, uint32_t nseg, uint64_t rounds, uint64_t mtiles,
                uint64_t gtiles, uint32_t *d_fb, unsigned long long *d_mism, uint32_t *d_gctr, hipStream_t st,
                hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, bool reset = true, int ctype = 0,
-               bool copy = false);
+               bool copy = false, bool gctr_zeroed = false, bool una = false);
+// Any segment whose data is not 4-B aligned (selects the realigning kernel).
+bool any_unaligned(const SegDev *segs, size_t n);
 // Copy / compute streams, events and the small pipeline buffers.
 int pipe_reserve(DevCtx &c, size_t piece, uint32_t cs, size_t npieces);
 

@@ -3,6 +3,8 @@
 #pragma once
 #include <cstdint>
 
+struct hdfs_crc32c_packet;  // include/hadoofus_crc32c.h
+
 namespace hdfs_crc32c {
 
 // Diagnostic build (libhadoofus_crc32c_diag.so, -DHDFS_CRC32C_DIAG, for
@@ -73,8 +75,22 @@ struct GridSummary {
   uint64_t next_pos;     // where the walk continues (kGridOn / kGridOff)
   uint64_t bm_bytes;     // bitmap bytes of the segment table
   uint32_t nbad;         // verify: packets with bad chunks (grid_finalize_kernel)
-  uint32_t pad;
+  uint32_t unaligned;    // some tiled segment's data is not 4-B aligned (realigning kernel)
 };
+// Device tables of one framing pass (count grid points).
+struct GridBufs {
+  ::hdfs_crc32c_packet *recs;  // [count] records
+  uint32_t *status;            // [count] kGrid*
+  void *contrib;               // [count] per-packet shares of the segment table (24 B each)
+  uint64_t *blk_sum;           // [blocks][6] block sums of the shares
+  uint32_t *blk_min;           // [blocks] first grid point of the block that is not kGridOn
+  SegDev *segs;                // [count] verify segments
+  uint32_t *seg2pkt;           // [count] segment -> grid point
+  uint32_t *fb;                // [count] first bad chunk per segment
+  uint32_t *gctr;              // tiled-kernel pool counter (zeroed by grid_build_kernel)
+  GridSummary *sum;
+};
+
 // Compact verify verdict of one packet (grid_finalize_kernel).
 struct GridBad {
   uint32_t pkt;

@@ -321,11 +321,21 @@ struct LaneOff {
   uint32_t v[4];
 };
 
-template <int MODE, int NT, int BUF>
-DEV void issue(uint32_t (&d)[16], uint32_t &exp, const Cursor c, SegP segs, uint32_t hsel, uint32_t loff,
-               uint32_t qg, LaneOff &lo, SegCache &kc) {
+// UNA (byte-unaligned segment data, e.g. packet payloads in a wire image):
+// with a = data & 3, every load is made from a - bytes earlier (4-B
+// aligned, the fast path of the memory pipeline) plus one extra dword
+// after the 16 B, and v_alignbyte_b32 funnels the 5 dwords into the lane's
+// 16 bytes.  The extra bytes read lie in the dwords that hold the segment's
+// first and last data bytes, so they never leave the pages the data is on.
+// The shift stays in a register across rounds (loads of rounds in flight use
+// the shift of their own segment).
+template <int MODE, int NT, int BUF, int UNA>
+DEV void issue(uint32_t (&d)[16], uint32_t &exp, uint32_t (&xw)[4], uint32_t &sh_a, const Cursor c, SegP segs,
+               uint32_t hsel, uint32_t loff, uint32_t qg, LaneOff &lo, SegCache &kc) {
   const SegHot &sh = hot(kc, segs, c.seg).h;
   const uint32_t cs = sh.chunk_size;
+  const uint32_t a = UNA ? static_cast<uint32_t>(reinterpret_cast<uintptr_t>(sh.data)) & 3u : 0u;
+  if (UNA) sh_a = a;
   if constexpr (BUF) {
     // Buffer loads: the round's base in SGPRs, per-lane offsets from the
     // cache, and the descriptor's range (the valid bytes of this round's
@@ -333,14 +343,14 @@ DEV void issue(uint32_t (&d)[16], uint32_t &exp, const Cursor c, SegP segs, uint
     // clamping addresses.
     const uint32_t nch = min(kTileChunks, sh.nchunks - c.tile * kTileChunks);
     const uint8_t *base = sh.data + static_cast<uint64_t>(c.tile) * kTileChunks * cs +
-                          static_cast<uint64_t>(c.r) * kRoundBytes;
+                          static_cast<uint64_t>(c.r) * kRoundBytes - a;
     if (lo.cs != cs) {
       lo.cs = cs;
 #pragma unroll
       for (int k = 0; k < 4; k++) lo.v[k] = (2u * k + hsel) * cs + loff;
     }
     const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t *>(base), 0, static_cast<int>((nch - 1u) * cs + kRoundBytes), 0x00020000);
+        const_cast<uint8_t *>(base), 0, static_cast<int>((nch - 1u) * cs + kRoundBytes + (a ? 4u : 0u)), 0x00020000);
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       const u32x4 v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rd, lo.v[k], 0, NT ? 2 : 0));
@@ -348,6 +358,7 @@ DEV void issue(uint32_t (&d)[16], uint32_t &exp, const Cursor c, SegP segs, uint
       d[4 * k + 1] = v.y;
       d[4 * k + 2] = v.z;
       d[4 * k + 3] = v.w;
+      if (UNA) xw[k] = __builtin_amdgcn_raw_buffer_load_b32(rd, lo.v[k] + 16u, 0, NT ? 2 : 0);
     }
     if (MODE != kModeCompute) {
       const __amdgpu_buffer_rsrc_t re = __builtin_amdgcn_make_buffer_rsrc(
@@ -357,7 +368,7 @@ DEV void issue(uint32_t (&d)[16], uint32_t &exp, const Cursor c, SegP segs, uint
   } else {
     const uint32_t last = min(kTileChunks, segs[c.seg].nchunks - c.tile * kTileChunks) - 1u;
     const uint8_t *p = segs[c.seg].data + static_cast<uint64_t>(c.tile) * kTileChunks * cs +
-                       static_cast<uint64_t>(c.r) * kRoundBytes + loff;
+                       static_cast<uint64_t>(c.r) * kRoundBytes + loff - a;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       const uint32_t g = min(2u * k + hsel, last);
@@ -366,6 +377,8 @@ DEV void issue(uint32_t (&d)[16], uint32_t &exp, const Cursor c, SegP segs, uint
       d[4 * k + 1] = v.y;
       d[4 * k + 2] = v.z;
       d[4 * k + 3] = v.w;
+      // a == 0: an in-bounds dummy (the dword after the data end may lie past its page)
+      if (UNA) xw[k] = gload32(p + static_cast<uint64_t>(g) * cs + (a ? 16u : 12u));
     }
     if (MODE != kModeCompute) exp = gload32(segs[c.seg].crcs + c.tile * kTileChunks + min(qg, last));
   }
@@ -491,10 +504,24 @@ DEV void copy_round(const uint32_t (&d)[16], const Cursor c, SegP segs, const La
 // st[s] is stream s's running lane register across the rounds of a tile.
 // The S slicing chains are independent and interleaved step by step, so one
 // lane keeps S table lookups in flight (latency hiding by ILP, not waves).
-template <int MODE, int S, int COPY>
-DEV void process(const uint32_t *lds, uint32_t (&d)[S][16], const uint32_t (&exp)[S], const Cursor (&c)[S],
-                 SegP segs, uint32_t (&st)[S], const LaneConst &L, uint32_t *__restrict__ first_bad,
-                 unsigned long long *__restrict__ mism, SegCache (&kc)[S]) {
+template <int MODE, int S, int COPY, int UNA>
+DEV void process(const uint32_t *lds, uint32_t (&d)[S][16], const uint32_t (&exp)[S], const uint32_t (&xw)[S][4],
+                 const uint32_t (&sh_a)[S], const Cursor (&c)[S], SegP segs, uint32_t (&st)[S], const LaneConst &L,
+                 uint32_t *__restrict__ first_bad, unsigned long long *__restrict__ mism, SegCache (&kc)[S]) {
+  if constexpr (UNA) {
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+      const uint32_t a = sh_a[s];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint32_t w0 = d[s][4 * k], w1 = d[s][4 * k + 1], w2 = d[s][4 * k + 2], w3 = d[s][4 * k + 3];
+        d[s][4 * k + 0] = __builtin_amdgcn_alignbyte(w1, w0, a);
+        d[s][4 * k + 1] = __builtin_amdgcn_alignbyte(w2, w1, a);
+        d[s][4 * k + 2] = __builtin_amdgcn_alignbyte(w3, w2, a);
+        d[s][4 * k + 3] = __builtin_amdgcn_alignbyte(xw[s][k], w3, a);
+      }
+    }
+  }
   if constexpr (COPY) {
 #pragma unroll
     for (int s = 0; s < S; s++) copy_round(d[s], c[s], segs, L, kc[s]);
@@ -539,7 +566,7 @@ DEV void process(const uint32_t *lds, uint32_t (&d)[S][16], const uint32_t (&exp
 // rounds stay in flight while one is processed); S independent tile streams
 // per wave (S x 4 KiB per round, S chains of ILP); BLOCK threads per
 // workgroup (one workgroup per CU: the LDS image takes 156 KiB).
-template <int MODE, int ORDER, int NT, int DEPTH, int S, int BLOCK, int BUF = 0, int COPY = 0>
+template <int MODE, int ORDER, int NT, int DEPTH, int S, int BLOCK, int BUF = 0, int COPY = 0, int UNA = 0>
 __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
     const SegDev *__restrict__ segs, uint32_t nseg, uint64_t total_rounds, uint64_t total_tiles,
     const uint32_t *__restrict__ gtab, uint32_t *__restrict__ first_bad,
@@ -698,6 +725,8 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
   // with their stores dropped.
   uint32_t buf[DEPTH][S][16];
   uint32_t ex[DEPTH][S];
+  uint32_t xw[DEPTH][S][4];  // UNA: the dword after each 16-B piece
+  uint32_t sha[DEPTH][S];    // UNA: byte shift of the round's segment
   uint32_t st[S];
   LaneOff lo{0u, {0u, 0u, 0u, 0u}};
   SegCache kc[S];
@@ -716,20 +745,22 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
 #pragma unroll
     for (int s = 0; s < S; s++) {
       ex[k][s] = 0u;
-      issue<MODE, NT, BUF>(buf[k][s], ex[k][s], cur[k][s], sg, L.hsel, L.loff, L.qg, lo, kc[s]);
+      issue<MODE, NT, BUF, UNA>(buf[k][s], ex[k][s], xw[k][s], sha[k][s], cur[k][s], sg, L.hsel, L.loff, L.qg, lo,
+                                kc[s]);
     }
   }
   for (;;) {
 #pragma unroll
     for (int k = 0; k < DEPTH; k++) {
-      process<MODE, S, COPY>(lds, buf[k], ex[k], cur[k], sg, st, L, first_bad, mism, kc);
+      process<MODE, S, COPY, UNA>(lds, buf[k], ex[k], xw[k], sha[k], cur[k], sg, st, L, first_bad, mism, kc);
 #pragma unroll
       for (int s = 0; s < S; s++) nrounds += cur[k][s].valid ? 1u : 0u;
       const int prev = (k + DEPTH - 1) % DEPTH;
 #pragma unroll
       for (int s = 0; s < S; s++) {
         cur[k][s] = advance<ORDER>(cur[prev][s], sg, nseg, w, kc[s]);
-        issue<MODE, NT, BUF>(buf[k][s], ex[k][s], cur[k][s], sg, L.hsel, L.loff, L.qg, lo, kc[s]);
+        issue<MODE, NT, BUF, UNA>(buf[k][s], ex[k][s], xw[k][s], sha[k][s], cur[k][s], sg, L.hsel, L.loff, L.qg,
+                                  lo, kc[s]);
       }
     }
     bool more = false;
@@ -1162,124 +1193,228 @@ __global__ __launch_bounds__(256) void packet_gather_kernel(const uint8_t *__res
 // scan kernel turns the run into a verify segment table in HBM (the host
 // never sees the headers), and the host continues from where the run left
 // the grid.
-__global__ __launch_bounds__(256) void frame_grid_kernel(const uint8_t *__restrict__ s, uint64_t len, uint64_t base,
-                                                         uint32_t count, int proto, uint32_t cs, int ctype,
-                                                         hdfs_crc32c_packet *__restrict__ recs,
-                                                         uint32_t *__restrict__ status, GridSummary *__restrict__ sum) {
-  const uint32_t k = blockIdx.x * 256u + threadIdx.x;
-  if (k >= count) return;
-  // the stride: the wire size of the packet at base (every thread reads the
-  // same header; cache-resident)
-  hdfs_crc32c_packet r;
-  uint64_t total = 0;
-  const int st0 = frame::frame_step(s + base, len - base, base, proto, cs, ctype, r, total);
-  const uint64_t stride = st0 == frame::kStepNext ? total : 0;
-  if (k == 0) sum->stride = stride;
-  if (k > 0 && stride == 0) return;  // packet 0 ends the walk: no other grid point is reached
-  const uint64_t pos = base + uint64_t(k) * stride;
-  uint32_t code = kGridMore;
-  if (pos < len) {
-    const int st = k == 0 ? st0 : frame::frame_step(s + pos, len - pos, pos, proto, cs, ctype, r, total);
-    code = st == frame::kStepMore ? kGridMore
-         : st == frame::kStepStop ? kGridStop
-         : total == stride        ? kGridOn
-                                  : kGridOff;
-    if (code != kGridMore) recs[k] = r;
-  }
-  status[k] = code;
-  if (code != kGridOn) atomicMin(&sum->first_break, k);
-}
-
-// One workgroup: the run's records -> verify segments (exclusive scans of
-// segments, rounds, main / generic tiles, bitmap bytes and payload bytes, in
-// the classify() rules of crc32c_engine.cpp), plus the run's summary.
-struct GridAcc {
-  uint64_t v[6];  // nseg, rounds, mtiles, gtiles, bitmap bytes, payload bytes
+// Per-packet share of the run's segment table (classify() rules of
+// crc32c_engine.cpp: tiled kernel for chunk sizes that are multiples of 512,
+// a partial last chunk moves the last tile to the generic kernel).
+struct GridContrib {
+  uint32_t nseg, rounds, mtiles, gtiles, bm, payload;
 };
 
-DEV void grid_contrib(const hdfs_crc32c_packet &r, uint32_t cs, int verify, GridAcc &a) {
-  if (r.error) return;
-  a.v[5] += uint64_t(r.data_len);
-  if (!verify || r.crc_len <= 0) return;
+DEV GridContrib grid_contrib(const hdfs_crc32c_packet &r, uint32_t cs, int verify) {
+  GridContrib a{0u, 0u, 0u, 0u, 0u, 0u};
+  if (r.error) return a;
+  a.payload = uint32_t(r.data_len);
+  if (!verify || r.crc_len <= 0) return a;
   const uint32_t nch = uint32_t(r.crc_len) / 4u, ntiles = (nch + 7u) / 8u;
   const bool eligible = cs % kRoundBytes == 0;
   const bool partial = uint32_t(r.data_len) % cs != 0;
   const uint32_t main = eligible ? (partial ? ntiles - 1u : ntiles) : 0u;
-  a.v[0] += 1;
-  a.v[1] += uint64_t(main) * (cs / kRoundBytes);
-  a.v[2] += main;
-  a.v[3] += ntiles - main;
-  a.v[4] += ntiles;
+  a.nseg = 1u;
+  a.rounds = main * (cs / kRoundBytes);
+  a.mtiles = main;
+  a.gtiles = ntiles - main;
+  a.bm = ntiles;
+  return a;
 }
 
-__global__ __launch_bounds__(1024) void grid_scan_kernel(
-    const uint8_t *__restrict__ s, uint64_t base, uint32_t count, const hdfs_crc32c_packet *__restrict__ recs,
-    const uint32_t *__restrict__ status, uint32_t cs, uint32_t sflags, int verify, uint8_t *__restrict__ bm_base,
+// A packet's first kHdrWin bytes, staged in LDS with four 16-B buffer loads
+// (zeros past the stream end), so frame_step's byte reads hit LDS instead of
+// making ~30 dependent trips to memory.
+DEV const uint8_t *stage_header(const uint8_t *s, uint64_t len, uint64_t pos, uint8_t *win) {
+  const uint64_t rem = len - pos;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t *>(s + pos), 0, static_cast<int>(rem < kHdrWin ? rem : kHdrWin), 0x00020000);
+#pragma unroll
+  for (int k = 0; k < int(kHdrWin / 16); k++)
+    *reinterpret_cast<u32x4 *>(win + 16 * k) =
+        __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * k, 0, 0));
+  return win;
+}
+
+// frame_step on the staged header when it fits, on the stream itself when a
+// v2 header is longer than the window.
+DEV int grid_frame(const uint8_t *s, uint64_t len, uint64_t pos, const uint8_t *win, int proto, uint32_t cs,
+                   int ctype, hdfs_crc32c_packet &r, uint64_t &total) {
+  const uint64_t rem = len - pos;
+  const bool fits = proto == HDFS_CRC32C_PROTO_V1 || rem < 6 ||
+                    6u + ((uint32_t(win[4]) << 8) | win[5]) <= kHdrWin;
+  return frame::frame_step(fits ? win : s + pos, rem, pos, proto, cs, ctype, r, total);
+}
+
+constexpr uint32_t kGridBlock = 256;
+
+__global__ __launch_bounds__(kGridBlock) void frame_grid_kernel(
+    const uint8_t *__restrict__ s, uint64_t len, uint64_t base, uint32_t count, int proto, uint32_t cs, int ctype,
+    int verify, hdfs_crc32c_packet *__restrict__ recs, uint32_t *__restrict__ status,
+    GridContrib *__restrict__ contrib, uint64_t *__restrict__ blk_sum, uint32_t *__restrict__ blk_min,
+    GridSummary *__restrict__ sum) {
+  __shared__ __attribute__((aligned(16))) uint8_t win[kGridBlock + 1][kHdrWin];
+  __shared__ uint64_t red[6][kGridBlock / 64];
+  __shared__ uint32_t redm[kGridBlock / 64];
+  const uint32_t t = threadIdx.x, k = blockIdx.x * kGridBlock + t, lane = t & 63u, w = t >> 6;
+  // the stride: the wire size of the packet at base (every block stages it)
+  if (t == 0) stage_header(s, len, base, win[kGridBlock]);
+  __syncthreads();
+  hdfs_crc32c_packet r;
+  uint64_t total = 0;
+  const int st0 = grid_frame(s, len, base, win[kGridBlock], proto, cs, ctype, r, total);
+  const uint64_t stride = st0 == frame::kStepNext ? total : 0;
+  if (k == 0) {
+    sum->stride = stride;
+    sum->unaligned = 0u;  // OR-ed by grid_build_kernel
+  }
+  uint32_t code = kGridMore;
+  GridContrib a{0u, 0u, 0u, 0u, 0u, 0u};
+  // grid point k is reachable only if packet 0 did not end the walk
+  if (k < count && (k == 0 || stride)) {
+    const uint64_t pos = base + uint64_t(k) * stride;
+    if (pos < len) {
+      int st = st0;
+      if (k) {
+        stage_header(s, len, pos, win[t]);
+        st = grid_frame(s, len, pos, win[t], proto, cs, ctype, r, total);
+      }
+      code = st == frame::kStepMore ? kGridMore
+           : st == frame::kStepStop ? kGridStop
+           : total == stride        ? kGridOn
+                                    : kGridOff;
+      if (code != kGridMore) {
+        recs[k] = r;
+        a = grid_contrib(r, cs, verify);
+      }
+    }
+  }
+  if (k < count) {
+    status[k] = code;
+    contrib[k] = a;
+  }
+  // block sums of the shares and the block's first grid point that is not On
+  uint64_t v[6] = {a.nseg, a.rounds, a.mtiles, a.gtiles, a.bm, a.payload};
+  uint32_t m = (k < count && code != kGridOn) ? k : 0xFFFFFFFFu;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+#pragma unroll
+    for (int q = 0; q < 6; q++) v[q] += __shfl_xor(v[q], off);
+    m = min(m, static_cast<uint32_t>(__shfl_xor(static_cast<int>(m), off)));
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int q = 0; q < 6; q++) red[q][w] = v[q];
+    redm[w] = m;
+  }
+  __syncthreads();
+  if (t < 6) {
+    uint64_t x = 0;
+    for (uint32_t j = 0; j < kGridBlock / 64; j++) x += red[t][j];
+    blk_sum[6 * blockIdx.x + t] = x;
+  }
+  if (t == 6) {
+    uint32_t x = 0xFFFFFFFFu;
+    for (uint32_t j = 0; j < kGridBlock / 64; j++) x = min(x, redm[j]);
+    blk_min[blockIdx.x] = x;
+  }
+}
+
+// Exclusive prefix of the shares, then the verify segment entries of the
+// run's packets and (one thread) the run's summary.  Same grid as
+// frame_grid_kernel; each block first reduces the other blocks' results.
+__global__ __launch_bounds__(kGridBlock) void grid_build_kernel(
+    const uint8_t *__restrict__ s, uint64_t base, uint32_t count, uint32_t nblk,
+    const hdfs_crc32c_packet *__restrict__ recs, const uint32_t *__restrict__ status,
+    const GridContrib *__restrict__ contrib, const uint64_t *__restrict__ blk_sum,
+    const uint32_t *__restrict__ blk_min, uint32_t cs, uint32_t sflags, uint8_t *__restrict__ bm_base,
     uint8_t *__restrict__ copy_base, SegDev *__restrict__ segs, uint32_t *__restrict__ seg2pkt,
-    uint32_t *__restrict__ fb, GridSummary *__restrict__ sum) {
-  __shared__ uint64_t wsum[6][16];
-  const uint32_t fbk = min(sum->first_break, count);
+    uint32_t *__restrict__ fb, uint32_t *__restrict__ gctr, GridSummary *__restrict__ sum) {
+  __shared__ uint64_t red[6][kGridBlock / 64];
+  __shared__ uint32_t redm[kGridBlock / 64];
+  __shared__ uint64_t pre[6];
+  const uint32_t t = threadIdx.x, b = blockIdx.x, k = b * kGridBlock + t, lane = t & 63u, w = t >> 6;
+  // 1. the run's end: the first grid point that is not On, over all blocks
+  uint32_t m = 0xFFFFFFFFu;
+  for (uint32_t j = t; j < nblk; j += kGridBlock) m = min(m, blk_min[j]);
+  // 2. shares of the blocks before this one
+  uint64_t v[6] = {0, 0, 0, 0, 0, 0};
+  for (uint32_t j = t; j < b; j += kGridBlock)
+#pragma unroll
+    for (int q = 0; q < 6; q++) v[q] += blk_sum[6 * j + q];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+#pragma unroll
+    for (int q = 0; q < 6; q++) v[q] += __shfl_xor(v[q], off);
+    m = min(m, static_cast<uint32_t>(__shfl_xor(static_cast<int>(m), off)));
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int q = 0; q < 6; q++) red[q][w] = v[q];
+    redm[w] = m;
+  }
+  __syncthreads();
+  uint32_t fbk = 0xFFFFFFFFu;
+  for (uint32_t j = 0; j < kGridBlock / 64; j++) fbk = min(fbk, redm[j]);
+  fbk = min(fbk, count);
+  if (t < 6) {
+    uint64_t x = 0;
+    for (uint32_t j = 0; j < kGridBlock / 64; j++) x += red[t][j];
+    pre[t] = x;
+  }
   const uint32_t st_fb = fbk < count ? status[fbk] : uint32_t(kGridOn);
   const uint32_t recorded = fbk + (fbk < count && st_fb != kGridMore ? 1u : 0u);
-  const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
-  const uint32_t per = (recorded + 1023u) / 1024u;
-  const uint32_t i0 = min(t * per, recorded), i1 = min(i0 + per, recorded);
-  GridAcc a{};
-  for (uint32_t i = i0; i < i1; i++) grid_contrib(recs[i], cs, verify, a);
-  // exclusive prefix: inclusive scan inside the wave, then across waves
-  GridAcc incl = a;
+  const uint32_t last = recorded ? recorded - 1u : 0u;  // the packet whose block writes the summary
+  if (b * kGridBlock > last) return;  // uniform per block: nothing of this run here
+  __syncthreads();
+  // 3. in-block exclusive scan of the shares of recorded packets
+  const GridContrib a = k < recorded ? contrib[k] : GridContrib{0u, 0u, 0u, 0u, 0u, 0u};
+  uint64_t incl[6] = {a.nseg, a.rounds, a.mtiles, a.gtiles, a.bm, a.payload};
+  const uint64_t own[6] = {a.nseg, a.rounds, a.mtiles, a.gtiles, a.bm, a.payload};
 #pragma unroll
   for (int q = 0; q < 6; q++) {
 #pragma unroll
     for (uint32_t off = 1; off < 64; off <<= 1) {
-      const uint64_t o = __shfl_up(incl.v[q], off);
-      if (lane >= off) incl.v[q] += o;
+      const uint64_t o = __shfl_up(incl[q], off);
+      if (lane >= off) incl[q] += o;
     }
-    if (lane == 63) wsum[q][w] = incl.v[q];
   }
   __syncthreads();
-  GridAcc pre{}, tot{};
+  if (lane == 63) {
+#pragma unroll
+    for (int q = 0; q < 6; q++) red[q][w] = incl[q];
+  }
+  __syncthreads();
+  uint64_t ex[6];
 #pragma unroll
   for (int q = 0; q < 6; q++) {
-    for (uint32_t j = 0; j < 16; j++) {
-      if (j < w) pre.v[q] += wsum[q][j];
-      tot.v[q] += wsum[q][j];
-    }
-    pre.v[q] += incl.v[q] - a.v[q];
+    ex[q] = pre[q] + incl[q] - own[q];
+    for (uint32_t j = 0; j < w; j++) ex[q] += red[q][j];
   }
-  // second pass: the segment entries
-  for (uint32_t i = i0; i < i1; i++) {
-    const hdfs_crc32c_packet r = recs[i];
-    if (verify && !r.error && r.crc_len > 0) {
-      const uint32_t nch = uint32_t(r.crc_len) / 4u, ntiles = (nch + 7u) / 8u;
-      const bool eligible = cs % kRoundBytes == 0;
-      const bool partial = uint32_t(r.data_len) % cs != 0;
-      const uint32_t main = eligible ? (partial ? ntiles - 1u : ntiles) : 0u;
-      const uint32_t sg = static_cast<uint32_t>(pre.v[0]);
-      SegDev d;
-      const uint8_t *crcp = s + r.stream_off + r.header_len;
-      d.data = crcp + r.crc_len;
-      d.crcs = reinterpret_cast<uint32_t *>(const_cast<uint8_t *>(crcp));
-      d.bitmap = bm_base + pre.v[4];
-      d.mtile_start = pre.v[2];
-      d.chunk_size = cs;
-      d.flags = sflags;
-      d.nchunks = nch;
-      d.main_tiles = main;
-      d.reg_init = 0xFFFFFFFFu;
-      d.gen_tiles = ntiles - main;
-      d.len = uint64_t(r.data_len);
-      d.round_start = pre.v[1];
-      d.gtile_start = pre.v[3];
-      d.copy_dst = copy_base ? copy_base + pre.v[5] : nullptr;
-      d.reserved = 0;
-      segs[sg] = d;
-      seg2pkt[sg] = i;
-      fb[sg] = 0xFFFFFFFFu;
-    }
-    grid_contrib(r, cs, verify, pre);
+  // 4. the segment entry of a recorded packet with CRCs
+  if (k < recorded && a.nseg) {
+    const hdfs_crc32c_packet r = recs[k];
+    const uint32_t nch = uint32_t(r.crc_len) / 4u, ntiles = (nch + 7u) / 8u;
+    const uint32_t sg = static_cast<uint32_t>(ex[0]);
+    const uint8_t *crcp = s + r.stream_off + r.header_len;
+    SegDev d;
+    d.data = crcp + r.crc_len;
+    d.crcs = reinterpret_cast<uint32_t *>(const_cast<uint8_t *>(crcp));
+    d.bitmap = bm_base + ex[4];
+    d.mtile_start = ex[2];
+    d.chunk_size = cs;
+    d.flags = sflags;
+    d.nchunks = nch;
+    d.main_tiles = a.mtiles;
+    d.reg_init = 0xFFFFFFFFu;
+    d.gen_tiles = ntiles - a.mtiles;
+    d.len = uint64_t(r.data_len);
+    d.round_start = ex[1];
+    d.gtile_start = ex[3];
+    d.copy_dst = copy_base ? copy_base + ex[5] : nullptr;
+    d.reserved = 0;
+    segs[sg] = d;
+    seg2pkt[sg] = k;
+    fb[sg] = 0xFFFFFFFFu;
+    if (a.mtiles && (reinterpret_cast<uintptr_t>(d.data) & 3u)) atomicOr(&sum->unaligned, 1u);
   }
-  if (t == 0) {
+  // 5. the summary, from the thread of the run's last packet
+  if (k == last) {
     const uint64_t stride = sum->stride;
     uint64_t consumed, next;
     if (fbk == count) {
@@ -1291,18 +1426,20 @@ __global__ __launch_bounds__(1024) void grid_scan_kernel(
       next = r.stream_off + r.header_len + uint64_t(r.crc_len) + uint64_t(r.data_len);
       consumed = r.error ? base + uint64_t(fbk) * stride : next;
     }
+    const bool any = recorded > 0;
     sum->first_break = fbk;
     sum->recorded = recorded;
     sum->last_status = st_fb;
-    sum->nseg = static_cast<uint32_t>(tot.v[0]);
-    sum->rounds = tot.v[1];
-    sum->mtiles = tot.v[2];
-    sum->gtiles = tot.v[3];
-    sum->bm_bytes = tot.v[4];
-    sum->payload = tot.v[5];
+    sum->nseg = any ? static_cast<uint32_t>(ex[0] + own[0]) : 0u;
+    sum->rounds = any ? ex[1] + own[1] : 0u;
+    sum->mtiles = any ? ex[2] + own[2] : 0u;
+    sum->gtiles = any ? ex[3] + own[3] : 0u;
+    sum->bm_bytes = any ? ex[4] + own[4] : 0u;
+    sum->payload = any ? ex[5] + own[5] : 0u;
     sum->consumed = consumed;
     sum->next_pos = next;
     sum->nbad = 0;
+    *gctr = 0u;  // the verify launch's pool counter (no separate reset launch)
   }
 }
 
@@ -1328,20 +1465,18 @@ __global__ __launch_bounds__(256) void grid_finalize_kernel(const SegDev *__rest
 }
 
 hipError_t launch_frame_grid(const uint8_t *s, uint64_t len, uint64_t base, uint32_t count, int proto, uint32_t cs,
-                             int ctype, hdfs_crc32c_packet *recs, uint32_t *status, GridSummary *sum,
-                             hipStream_t stream) {
+                             int ctype, int verify, uint32_t sflags, uint8_t *bm_base, uint8_t *copy_base,
+                             GridBufs g, hipStream_t stream) {
   if (!count || base >= len) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(frame_grid_kernel, dim3((count + 255) / 256), dim3(256), 0, stream, s, len, base, count, proto,
-                     cs, ctype, recs, status, sum);
-  return hipGetLastError();
-}
-
-hipError_t launch_grid_scan(const uint8_t *s, uint64_t base, uint32_t count, const hdfs_crc32c_packet *recs,
-                            const uint32_t *status, uint32_t cs, uint32_t sflags, int verify, uint8_t *bm_base,
-                            uint8_t *copy_base, SegDev *segs, uint32_t *seg2pkt, uint32_t *fb, GridSummary *sum,
-                            hipStream_t stream) {
-  hipLaunchKernelGGL(grid_scan_kernel, dim3(1), dim3(1024), 0, stream, s, base, count, recs, status, cs, sflags,
-                     verify, bm_base, copy_base, segs, seg2pkt, fb, sum);
+  const uint32_t nblk = (count + kGridBlock - 1) / kGridBlock;
+  auto *contrib = reinterpret_cast<GridContrib *>(g.contrib);
+  hipLaunchKernelGGL(frame_grid_kernel, dim3(nblk), dim3(kGridBlock), 0, stream, s, len, base, count, proto, cs,
+                     ctype, verify, g.recs, g.status, contrib, g.blk_sum, g.blk_min, g.sum);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(grid_build_kernel, dim3(nblk), dim3(kGridBlock), 0, stream, s, base, count, nblk, g.recs,
+                     g.status, contrib, g.blk_sum, g.blk_min, cs, sflags, bm_base, copy_base, g.segs, g.seg2pkt, g.fb,
+                     g.gctr, g.sum);
   return hipGetLastError();
 }
 
@@ -1411,19 +1546,33 @@ hipError_t launch_header_window(const uint8_t *s, uint64_t len, uint64_t base, u
 hipError_t launch_tiles(int mode, int order, int nt, int depth, int streams, int block, int grid,
                         const SegDev *segs, uint32_t nseg, uint64_t total_rounds, uint64_t total_tiles,
                         const uint32_t *gtab, uint32_t *first_bad, unsigned long long *mism,
-                        unsigned long long *diag, uint32_t tune, uint32_t *gctr, hipStream_t stream, int copy) {
-#define HDFS_LAUNCH_C(M, O, N, D, S, B, BUF, C)                                                            \
-  hipLaunchKernelGGL((crc32c_tiles_kernel<M, O, N, D, S, B, BUF, C>), dim3(grid), dim3(B), 0, stream, segs, \
+                        unsigned long long *diag, uint32_t tune, uint32_t *gctr, hipStream_t stream, int copy,
+                        int una) {
+#define HDFS_LAUNCH_CU(M, O, N, D, S, B, BUF, C, U)                                                            \
+  hipLaunchKernelGGL((crc32c_tiles_kernel<M, O, N, D, S, B, BUF, C, U>), dim3(grid), dim3(B), 0, stream, segs, \
                      nseg, total_rounds, total_tiles, gtab, first_bad, mism, diag, tune, gctr)
+#define HDFS_LAUNCH_C(M, O, N, D, S, B, BUF, C) HDFS_LAUNCH_CU(M, O, N, D, S, B, BUF, C, 0)
 #define HDFS_LAUNCH(M, O, N, D, S, B, BUF) HDFS_LAUNCH_C(M, O, N, D, S, B, BUF, 0)
 #define HDFS_SHAPE(O, N, D, S, B) (order == (O) && nt == (N) && depth == (D) && streams == (S) && block == (B))
   if (mode != kModeCompute && mode != kModeVerify && !(kDiag && mode == kModeLoadOnly)) return hipErrorInvalidValue;
-  if (copy) {
-    // verify + copy-out (device packet streams): the two product shapes only
-    if (mode != kModeVerify) return hipErrorInvalidValue;
-    if (HDFS_SHAPE(3, 2, 3, 1, 1024)) HDFS_LAUNCH_C(kModeVerify, 3, 1, 3, 1, 1024, 1, 1);
-    else if (HDFS_SHAPE(2, 1, 3, 1, 1024)) HDFS_LAUNCH_C(kModeVerify, 2, 1, 3, 1, 1024, 0, 1);
+  if (copy || una) {
+    // verify + copy-out (device packet streams) and byte-unaligned data: the
+    // two product shapes only
+    if (copy && mode != kModeVerify) return hipErrorInvalidValue;
+#define HDFS_LAUNCH_PRODUCT_CU(M, C, U)                                                           \
+    if (HDFS_SHAPE(3, 2, 3, 1, 1024)) HDFS_LAUNCH_CU(M, 3, 1, 3, 1, 1024, 1, C, U);               \
+    else if (HDFS_SHAPE(2, 1, 3, 1, 1024)) HDFS_LAUNCH_CU(M, 2, 1, 3, 1, 1024, 0, C, U);          \
     else return hipErrorInvalidValue;
+    if (mode == kModeCompute) {
+      HDFS_LAUNCH_PRODUCT_CU(kModeCompute, 0, 1)
+    } else if (copy && una) {
+      HDFS_LAUNCH_PRODUCT_CU(kModeVerify, 1, 1)
+    } else if (copy) {
+      HDFS_LAUNCH_PRODUCT_CU(kModeVerify, 1, 0)
+    } else {
+      HDFS_LAUNCH_PRODUCT_CU(kModeVerify, 0, 1)
+    }
+#undef HDFS_LAUNCH_PRODUCT_CU
     return hipGetLastError();
   }
   // Release build: the two product shapes only -- schedule 3 with nontemporal
@@ -1478,6 +1627,7 @@ hipError_t launch_tiles(int mode, int order, int nt, int depth, int streams, int
 #undef HDFS_SHAPE
 #undef HDFS_LAUNCH
 #undef HDFS_LAUNCH_C
+#undef HDFS_LAUNCH_CU
   return hipGetLastError();
 }
 

@@ -348,7 +348,8 @@ int submit_device_batch(DevCtx &c, const uint8_t *d, const std::vector<hdfs_crc3
   HIPCHK(hipMemcpyAsync(dm, hm, L.off_fb, hipMemcpyHostToDevice, c.v_stream));
   int rc = launch_all(c, kModeVerify, reinterpret_cast<const SegDev *>(dm), uint32_t(L.n), L.rounds, L.mtiles,
                       L.gtiles, reinterpret_cast<uint32_t *>(dm + L.off_fb), mism, gctr, c.v_stream, nullptr,
-                      nullptr, true, ctype == HDFS_CRC32C_CSUM_CRC32 ? 1 : 0, copy_dst != nullptr);
+                      nullptr, true, ctype == HDFS_CRC32C_CSUM_CRC32 ? 1 : 0, copy_dst != nullptr, false,
+                      any_unaligned(hs, L.n));
   if (rc) return rc;
   HIPCHK(hipMemcpyAsync(hm + L.off_fb, dm + L.off_fb, L.meta - L.off_fb, hipMemcpyDeviceToHost, c.v_stream));
   return HDFS_CRC32C_OK;
@@ -463,26 +464,29 @@ int stream_device(const void *stream) {
 // Layout of one pass's device tables and pinned landing area.
 constexpr uint32_t kBadFirst = 1024;  // bad-packet entries copied back with the verify summary
 struct GridLayout {
-  size_t recs, status, segs, seg2pkt, fb, sum, bad, ctr, bm, dtotal;  // device offsets
-  size_t h_recs, h_sum, h_sum2, h_bad, htotal;                         // pinned offsets
+  size_t recs, status, contrib, blk_sum, blk_min, segs, seg2pkt, fb, sum, bad, ctr, bm, dtotal;  // device offsets
+  size_t h_recs, h_sum, h_sum2, htotal;  // pinned offsets (h_sum2: summary after verify, then the bad list)
   GridLayout(uint32_t count, uint64_t bm_cap) {
+    const size_t nblk = (count + 255) / 256;
     size_t o = 0;
     auto take = [&](size_t n) { const size_t at = o; o += align_up(n, 256); return at; };
     recs = take(size_t(count) * sizeof(hdfs_crc32c_packet));
     status = take(size_t(count) * 4);
+    contrib = take(size_t(count) * 24);
+    blk_sum = take(nblk * 48);
+    blk_min = take(nblk * 4);
     segs = take(size_t(count) * sizeof(SegDev));
     seg2pkt = take(size_t(count) * 4);
     fb = take(size_t(count) * 4);
-    sum = take(sizeof(GridSummary));
+    sum = take(256);  // the bad list follows the summary: one copy back
     bad = take(size_t(count) * sizeof(GridBad));
     ctr = take(128);  // pool counter, mismatch count
     bm = take(size_t(bm_cap));
     dtotal = o;
     o = 0;
     h_recs = take(size_t(count) * sizeof(hdfs_crc32c_packet));
-    h_sum = take(sizeof(GridSummary));
-    h_sum2 = take(sizeof(GridSummary));
-    h_bad = take(size_t(kBadFirst) * sizeof(GridBad));
+    h_sum = take(256);
+    h_sum2 = take(256 + size_t(kBadFirst) * sizeof(GridBad));
     htotal = o;
   }
 };
@@ -536,26 +540,39 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
   bool fallback = false;
   using clk = std::chrono::steady_clock;
   const auto t0 = clk::now();
+  double t_enq = 0, t_sync = 0, t_venq = 0;
+  auto us_since = [](clk::time_point a, clk::time_point b) {
+    return std::chrono::duration<double, std::micro>(b - a).count();
+  };
   while (out.size() < max_pkts && pos < len) {
     const uint64_t left = len - pos;
     const uint32_t count = uint32_t(std::min<uint64_t>({uint64_t(max_pkts - out.size()), kGridMaxCount, left / 6 + 1}));
     const uint64_t bm_cap = left / 32 + count + 64;  // >= sum of ceil(chunks / 8) over the run
+    const auto tq0 = clk::now();
     const GridLayout L(count, bm_cap);
     const size_t si = passes.size();
     if ((rc = reserve_grid(c, si, L))) break;
     uint8_t *dg = c.grid[si].d, *hg = c.grid[si].h;
     auto *recs = reinterpret_cast<hdfs_crc32c_packet *>(dg + L.recs);
     auto *sum = reinterpret_cast<GridSummary *>(dg + L.sum);
-    hipError_t e = hipMemsetAsync(&sum->first_break, 0xFF, 4, c.stream);
-    if (e == hipSuccess) e = launch_frame_grid(d, len, pos, count, proto, cs, ctype, recs,
-                                               reinterpret_cast<uint32_t *>(dg + L.status), sum, c.stream);
-    if (e == hipSuccess)
-      e = launch_grid_scan(d, pos, count, recs, reinterpret_cast<const uint32_t *>(dg + L.status), cs, sflags,
-                           verify ? 1 : 0, dg + L.bm, copy_dst ? copy_dst + payload : nullptr,
-                           reinterpret_cast<SegDev *>(dg + L.segs), reinterpret_cast<uint32_t *>(dg + L.seg2pkt),
-                           reinterpret_cast<uint32_t *>(dg + L.fb), sum, c.stream);
+    auto *ctr = reinterpret_cast<uint32_t *>(dg + L.ctr);
+    const GridBufs gb{recs,
+                      reinterpret_cast<uint32_t *>(dg + L.status),
+                      dg + L.contrib,
+                      reinterpret_cast<uint64_t *>(dg + L.blk_sum),
+                      reinterpret_cast<uint32_t *>(dg + L.blk_min),
+                      reinterpret_cast<SegDev *>(dg + L.segs),
+                      reinterpret_cast<uint32_t *>(dg + L.seg2pkt),
+                      reinterpret_cast<uint32_t *>(dg + L.fb),
+                      ctr,
+                      sum};
+    hipError_t e = launch_frame_grid(d, len, pos, count, proto, cs, ctype, verify ? 1 : 0, sflags, dg + L.bm,
+                                     copy_dst ? copy_dst + payload : nullptr, gb, c.stream);
     if (e == hipSuccess) e = hipMemcpyAsync(hg + L.h_sum, sum, sizeof(GridSummary), hipMemcpyDeviceToHost, c.stream);
+    const auto tq = clk::now();
     if (e == hipSuccess) e = hipStreamSynchronize(c.stream);
+    t_enq += us_since(tq0, tq);
+    t_sync += us_since(tq, clk::now());
     if (e != hipSuccess) {
       rc = fail(HDFS_CRC32C_EHIP, "device framing: %s", hipGetErrorString(e));
       break;
@@ -570,19 +587,19 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
       break;
     }
     if (verify && S.nseg) {
-      auto *ctr = reinterpret_cast<uint32_t *>(dg + L.ctr);
+      // the pool counter was zeroed by grid_build_kernel: no reset launch
       rc = launch_all(c, kModeVerify, reinterpret_cast<const SegDev *>(dg + L.segs), S.nseg, S.rounds, S.mtiles,
                       S.gtiles, reinterpret_cast<uint32_t *>(dg + L.fb), reinterpret_cast<unsigned long long *>(ctr + 16),
-                      ctr, c.v_stream, nullptr, nullptr, false, tset, copy_dst != nullptr);
+                      ctr, c.v_stream, nullptr, nullptr, false, tset, copy_dst != nullptr, true, S.unaligned != 0);
       if (rc) break;
       auto *bad = reinterpret_cast<GridBad *>(dg + L.bad);
       HIPCHK(launch_grid_finalize(reinterpret_cast<const SegDev *>(dg + L.segs), S.nseg,
                                   reinterpret_cast<const uint32_t *>(dg + L.seg2pkt),
                                   reinterpret_cast<const uint32_t *>(dg + L.fb), bad, count, sum, c.v_stream));
-      HIPCHK(hipMemcpyAsync(hg + L.h_sum2, sum, sizeof(GridSummary), hipMemcpyDeviceToHost, c.v_stream));
-      HIPCHK(hipMemcpyAsync(hg + L.h_bad, bad, size_t(std::min(kBadFirst, S.nseg)) * sizeof(GridBad),
+      HIPCHK(hipMemcpyAsync(hg + L.h_sum2, sum, 256 + size_t(std::min(kBadFirst, S.nseg)) * sizeof(GridBad),
                             hipMemcpyDeviceToHost, c.v_stream));
     }
+    t_venq += us_since(tq, clk::now());
     passes.push_back({si, out.size(), S.recorded, verify ? S.nseg : 0u, count, bm_cap});
     out.resize(out.size() + S.recorded);
     payload += S.payload;
@@ -597,14 +614,18 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
   const auto t1 = clk::now();
   // records of every pass (their copies overlapped the verify launches)
   hipError_t e = hipStreamSynchronize(c.stream);
+  const auto t1b = clk::now();
   if (!rc && e != hipSuccess) rc = fail(HDFS_CRC32C_EHIP, "framing records: %s", hipGetErrorString(e));
   if (!rc)
     for (const Pass &p : passes)
       if (p.n) std::memcpy(out.data() + p.off, c.grid[p.slot].h + GridLayout(p.count, p.bm_cap).h_recs,
                            p.n * sizeof(hdfs_crc32c_packet));
+  const auto t1c = clk::now();
   if (!rc && fallback && out.size() < max_pkts)
     rc = walk_device_stream(c, d, len, proto, cs, ctype, max_pkts, verify, out, consumed, pos, copy_dst, &payload);
+  const auto t1d = clk::now();
   e = hipStreamSynchronize(c.v_stream);  // drained even after an error: its tables live in this context
+  const auto t1e = clk::now();
   if (!rc && e != hipSuccess) rc = fail(HDFS_CRC32C_EHIP, "verify: %s", hipGetErrorString(e));
   if (!rc && copy_dst && payload > copy_cap)
     rc = fail(HDFS_CRC32C_EINVAL, "copy-out buffer of %llu bytes is too small (%llu needed)",
@@ -617,7 +638,7 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
     const uint8_t *hg = c.grid[p.slot].h;
     const uint32_t nbad = reinterpret_cast<const GridSummary *>(hg + L.h_sum2)->nbad;
     std::vector<GridBad> more;
-    const GridBad *bad = reinterpret_cast<const GridBad *>(hg + L.h_bad);
+    const GridBad *bad = reinterpret_cast<const GridBad *>(hg + L.h_sum2 + 256);
     if (nbad > kBadFirst) {
       more.resize(nbad);
       HIPCHK(hipMemcpy(more.data(), c.grid[p.slot].d + L.bad, nbad * sizeof(GridBad), hipMemcpyDeviceToHost));
@@ -633,8 +654,11 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
   if (g_dstream_trace) {  // diagnostic: where a device-stream call spends its time (us)
     const auto t2 = clk::now();
     auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
-    std::fprintf(stderr, "dstream grid pkts=%zu passes=%zu fallback=%d frame_us=%.1f total_us=%.1f\n", out.size(),
-                 passes.size(), int(fallback), us(t0, t1), us(t0, t2));
+    std::fprintf(stderr,
+                 "dstream grid pkts=%zu passes=%zu fallback=%d enq_us=%.1f sum_sync_us=%.1f verify_enq_us=%.1f "
+                 "loop_us=%.1f recs_sync_us=%.1f memcpy_us=%.1f fallback_us=%.1f verify_sync_us=%.1f total_us=%.1f\n",
+                 out.size(), passes.size(), int(fallback), t_enq, t_sync, t_venq, us(t0, t1), us(t1, t1b), us(t1b, t1c),
+                 us(t1c, t1d), us(t1d, t1e), us(t0, t2));
   }
   if (payload_out) *payload_out = payload;
   return HDFS_CRC32C_OK;

@@ -61,17 +61,21 @@ def test_release_has_no_diagnostic_knobs(libpath, diagpath):
 
 
 def test_release_kernels_are_the_product_shapes(libpath, diagpath):
-    """Six tiled-kernel instantiations in the release build (compute /
-    verify / verify + copy-out x schedule 3 buffer loads / schedule 2), no
-    load-only twin (mode 2) and no read probes; the diagnostic build has them."""
+    """The release build's tiled kernels are the two product shapes (schedule
+    3 with buffer loads, schedule 2) in their product variants only: compute
+    and verify, each with and without the realigning path for byte-unaligned
+    data, verify also with the fused copy-out -- twelve in all; no load-only
+    twin (mode 2) and no read probes.  The diagnostic build has them."""
     import re as _re
     rel = open(libpath, "rb").read()
     dia = open(diagpath, "rb").read()
     pat = (rb"_ZN11hdfs_crc32c19crc32c_tiles_kernelILi(\d)ELi(\d)ELi(\d)ELi(\d)ELi(\d)ELi(\d+)ELi(\d)ELi(\d)"
-           rb"EEE")
+           rb"ELi(\d)EEE")
     shapes = set(_re.findall(pat, rel))
-    assert shapes == {(m, o, b"1", b"3", b"1", b"1024", buf, cp) for m, cp in ((b"0", b"0"), (b"1", b"0"), (b"1", b"1"))
-                      for o, buf in ((b"3", b"1"), (b"2", b"0"))}, shapes
+    variants = [(b"0", b"0", b"0"), (b"0", b"0", b"1")] + [(b"1", cp, un) for cp in (b"0", b"1") for un in (b"0", b"1")]
+    want = {(m, o, b"1", b"3", b"1", b"1024", buf, cp, un) for m, cp, un in variants
+            for o, buf in ((b"3", b"1"), (b"2", b"0"))}
+    assert shapes == want, shapes ^ want
     assert b"probe_read_kernel" not in rel and b"probe2_kernel" not in rel
     dshapes = set(_re.findall(pat, dia))
     assert any(s[0] == b"2" for s in dshapes) and len(dshapes) > 20

@@ -126,3 +126,38 @@ def test_unaligned_segments_default_schedule(engine, oracle):
     assert mism == len(bad)
     for i in range(nseg):
         assert first_bad[i] == bad.get(i, 0xFFFFFFFF), i
+
+
+@pytest.mark.parametrize("shift", [1, 2, 3])
+@pytest.mark.parametrize("cs,nch", [(512, 8 * 40), (1024, 64), (4096, 8 * 9 + 3), (512, 2_000_000 // 512)])
+def test_unaligned_realign_small_and_large(engine, oracle, shift, cs, nch):
+    """Byte-unaligned segments take the realigning kernel (aligned loads + one
+    dword, v_alignbyte): small launches (schedule 2, global loads) and large
+    ones (schedule 3, buffer loads); the data ends exactly at the end of its
+    allocation, so the realigning loads must stay inside the data's dwords.
+    Compute bit-exact vs the oracle, verify finds exactly the flipped CRCs."""
+    n = cs * nch
+    rng = np.random.default_rng(shift * 7 + cs)
+    host = rng.integers(0, 256, n, dtype=np.uint8)
+    buf = engine.DeviceBuffer(n + shift)
+    buf.upload(host, offset=shift)  # data = [ptr + shift, ptr + shift + n) == the buffer's end
+    want = oracle.chunk_crcs(host, cs)
+    crcs = engine.DeviceBuffer(want.nbytes)
+    bm = engine.DeviceBuffer((nch + 7) // 8)
+    seg = engine.Segment(data=buf.ptr + shift, len=n, chunk_size=cs, flags=engine.SEG_BE, crc_init=0, crcs=crcs.ptr,
+                         bitmap=bm.ptr)
+    engine.Plan(engine.MODE_COMPUTE, [seg]).execute()
+    np.testing.assert_array_equal(crcs.download(dtype=">u4").astype(np.uint32), want)
+    picks = sorted({(k * 7919 + shift) % nch for k in range(6)})
+    arr = want.astype(">u4")
+    for c in picks:
+        arr[c] ^= np.uint32(0x80)
+    crcs.upload(arr.view(np.uint8))
+    vp = engine.Plan(engine.MODE_VERIFY, [seg])
+    vp.execute()
+    first_bad, mism = vp.results()
+    assert mism == len(picks) and first_bad[0] == picks[0]
+    bits = np.unpackbits(bm.download(), bitorder="little")[:nch]
+    assert list(np.nonzero(bits)[0]) == picks
+    # the drop-in stream CRC over the same unaligned device bytes
+    assert engine.stream_crc_dev(0x5A5A5A5A, buf.ptr + shift, n) == oracle.crc32c(0x5A5A5A5A, host)
