@@ -380,7 +380,12 @@ DEV void issue(uint32_t (&d)[16], uint32_t &exp, uint32_t (&xw)[4], uint32_t &sh
       // a == 0: an in-bounds dummy (the dword after the data end may lie past its page)
       if (UNA) xw[k] = gload32(p + static_cast<uint64_t>(g) * cs + (a ? 16u : 12u));
     }
-    if (MODE != kModeCompute) exp = gload32(segs[c.seg].crcs + c.tile * kTileChunks + min(qg, last));
+    if (MODE != kModeCompute) {
+      // buffer load: expected CRCs of a packet sit at any byte offset of the wire image
+      const __amdgpu_buffer_rsrc_t re = __builtin_amdgcn_make_buffer_rsrc(
+          segs[c.seg].crcs + c.tile * kTileChunks, 0, static_cast<int>((last + 1u) * 4u), 0x00020000);
+      exp = __builtin_amdgcn_raw_buffer_load_b32(re, qg * 4u, 0, 0);
+    }
   }
 }
 
@@ -1217,27 +1222,30 @@ DEV GridContrib grid_contrib(const hdfs_crc32c_packet &r, uint32_t cs, int verif
   return a;
 }
 
-// A packet's first kHdrWin bytes, staged in LDS with four 16-B buffer loads
-// (zeros past the stream end), so frame_step's byte reads hit LDS instead of
-// making ~30 dependent trips to memory.
-DEV const uint8_t *stage_header(const uint8_t *s, uint64_t len, uint64_t pos, uint8_t *win) {
-  const uint64_t rem = len - pos;
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint8_t *>(s + pos), 0, static_cast<int>(rem < kHdrWin ? rem : kHdrWin), 0x00020000);
+// A packet's first kHdrWin bytes, staged in LDS with four 16-B loads, so
+// frame_step's byte reads hit LDS instead of making ~30 dependent trips to
+// memory.  Only when the whole window lies inside the stream (a packet
+// within kHdrWin bytes of the stream end is framed from memory directly).
+// (Buffer loads: they serve any byte address; a global_load_dwordx4 at an
+// address that is not 4-B aligned returns the aligned-down bytes.)
+DEV void stage_header(const uint8_t *s, uint64_t len, uint64_t pos, uint8_t *win) {
+  if (len - pos < kHdrWin) return;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(s + pos), 0, static_cast<int>(kHdrWin), 0x00020000);
 #pragma unroll
   for (int k = 0; k < int(kHdrWin / 16); k++)
     *reinterpret_cast<u32x4 *>(win + 16 * k) =
         __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * k, 0, 0));
-  return win;
 }
 
-// frame_step on the staged header when it fits, on the stream itself when a
-// v2 header is longer than the window.
+// frame_step on the staged header when it holds the whole header, on the
+// stream itself near the stream end or when a v2 header is longer than the
+// window.
 DEV int grid_frame(const uint8_t *s, uint64_t len, uint64_t pos, const uint8_t *win, int proto, uint32_t cs,
                    int ctype, hdfs_crc32c_packet &r, uint64_t &total) {
   const uint64_t rem = len - pos;
-  const bool fits = proto == HDFS_CRC32C_PROTO_V1 || rem < 6 ||
-                    6u + ((uint32_t(win[4]) << 8) | win[5]) <= kHdrWin;
+  const bool fits = rem >= kHdrWin && (proto == HDFS_CRC32C_PROTO_V1 ||
+                                       6u + ((uint32_t(win[4]) << 8) | win[5]) <= kHdrWin);
   return frame::frame_step(fits ? win : s + pos, rem, pos, proto, cs, ctype, r, total);
 }
 
@@ -1411,7 +1419,13 @@ __global__ __launch_bounds__(kGridBlock) void grid_build_kernel(
     segs[sg] = d;
     seg2pkt[sg] = k;
     fb[sg] = 0xFFFFFFFFu;
-    if (a.mtiles && (reinterpret_cast<uintptr_t>(d.data) & 3u)) atomicOr(&sum->unaligned, 1u);
+  }
+  // one atomic per wave that has a byte-unaligned tiled segment (per-thread
+  // atomics on one word serialise: 16 K of them cost ~150 us)
+  {
+    const bool una = k < recorded && a.nseg && a.mtiles &&
+                     ((reinterpret_cast<uintptr_t>(s) + recs[k].stream_off + recs[k].header_len + uint32_t(recs[k].crc_len)) & 3u);
+    if (__ballot(una) && lane == 0) atomicOr(&sum->unaligned, 1u);
   }
   // 5. the summary, from the thread of the run's last packet
   if (k == last) {

@@ -17,20 +17,21 @@ import hadoofus_amd as h  # noqa: E402
 h.load()
 D, CS = 65536, 512
 NCH = D // CS
-LAYOUTS = {"arena": None, "wire_h28": 28, "wire_h25": 25, "wire_h34": 34, "wire_h32": 32}
+LAYOUTS = {"arena": None, "arena_crc_odd": -1, "wire_h28": 28, "wire_h25": 25, "wire_h34": 34, "wire_h32": 32}
 out = {"env": {k: v for k, v in os.environ.items() if k.startswith("HDFS_CRC32C")}}
 
 
 def run(NPK, name, H):
-    stride = D if H is None else H + 4 * NCH + D
+    arena = H is None or H < 0  # H = -1: aligned data, CRC array at an odd address
+    stride = D if arena else H + 4 * NCH + D
     buf = h.DeviceBuffer(NPK * stride + 4096)
     h.fill_splitmix64(buf.ptr, buf.nbytes // 8, 11, 0)
-    crcbuf = h.DeviceBuffer(NPK * NCH * 4) if H is None else None
+    crcbuf = h.DeviceBuffer(NPK * NCH * 4 + 64) if arena else None
     bms = h.DeviceBuffer(NPK * NCH // 8)
     segs = []
     for k in range(NPK):
-        if H is None:
-            data, crcs = buf.ptr + k * D, crcbuf.ptr + k * NCH * 4
+        if arena:
+            data, crcs = buf.ptr + k * D, crcbuf.ptr + k * NCH * 4 + (1 if H else 0)
         else:
             crcs = buf.ptr + k * stride + H
             data = crcs + 4 * NCH
