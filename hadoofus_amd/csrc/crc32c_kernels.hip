@@ -319,19 +319,24 @@ DEV uint64_t tile_at_round(SegP segs, uint32_t nseg, uint64_t r, uint64_t total_
 struct LaneOff {
   uint32_t cs;
   uint32_t v[4];
+  uint32_t t;  // UNA: lanes 0..7 -> offset of the dword after chunk lane's 512-B round part
 };
 
-// UNA (byte-unaligned segment data, e.g. packet payloads in a wire image):
-// with a = data & 3, every load is made from a - bytes earlier (4-B
-// aligned, the fast path of the memory pipeline) plus one extra dword
-// after the 16 B, and v_alignbyte_b32 funnels the 5 dwords into the lane's
-// 16 bytes.  The extra bytes read lie in the dwords that hold the segment's
-// first and last data bytes, so they never leave the pages the data is on.
-// The shift stays in a register across rounds (loads of rounds in flight use
-// the shift of their own segment).
+// UNA (byte-unaligned segment data, e.g. packet payloads inside a wire
+// image): with a = data & 3 the four 1 KiB loads start a bytes early (4-B
+// aligned: the fast path of the memory pipeline).  After the transpose lane
+// L holds the 64 bytes of its quad starting a bytes early; the a bytes it
+// lacks at the end are the first dword of the next quad's window (lane L+1,
+// one DPP row shift) -- or, for the last quad of a chunk's round, the dword
+// just after the round part, which ONE extra load per round fetches for
+// all 8 chunks (lanes 0..7; ds_bpermute hands it to lanes 8j+7); 16
+// v_alignbyte_b32 then shift the lane's 17 dwords into place.  Every extra
+// byte read lies in a dword that also holds data of the segment, so no read
+// leaves the data's pages.  The shift rides with the round (rounds in
+// flight may belong to different segments).
 template <int MODE, int NT, int BUF, int UNA>
-DEV void issue(uint32_t (&d)[16], uint32_t &exp, uint32_t (&xw)[4], uint32_t &sh_a, const Cursor c, SegP segs,
-               uint32_t hsel, uint32_t loff, uint32_t qg, LaneOff &lo, SegCache &kc) {
+DEV void issue(uint32_t (&d)[16], uint32_t &exp, uint32_t &tl, uint32_t &sh_a, const Cursor c, SegP segs,
+               uint32_t hsel, uint32_t loff, uint32_t qg, uint32_t lane, LaneOff &lo, SegCache &kc) {
   const SegHot &sh = hot(kc, segs, c.seg).h;
   const uint32_t cs = sh.chunk_size;
   const uint32_t a = UNA ? static_cast<uint32_t>(reinterpret_cast<uintptr_t>(sh.data)) & 3u : 0u;
@@ -348,7 +353,9 @@ DEV void issue(uint32_t (&d)[16], uint32_t &exp, uint32_t (&xw)[4], uint32_t &sh
       lo.cs = cs;
 #pragma unroll
       for (int k = 0; k < 4; k++) lo.v[k] = (2u * k + hsel) * cs + loff;
+      if (UNA) lo.t = lane < kTileChunks ? lane * cs + kRoundBytes : 0x80000000u;
     }
+    // UNA: the range ends with the dword holding the last data byte
     const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t *>(base), 0, static_cast<int>((nch - 1u) * cs + kRoundBytes + (a ? 4u : 0u)), 0x00020000);
 #pragma unroll
@@ -358,8 +365,8 @@ DEV void issue(uint32_t (&d)[16], uint32_t &exp, uint32_t (&xw)[4], uint32_t &sh
       d[4 * k + 1] = v.y;
       d[4 * k + 2] = v.z;
       d[4 * k + 3] = v.w;
-      if (UNA) xw[k] = __builtin_amdgcn_raw_buffer_load_b32(rd, lo.v[k] + 16u, 0, NT ? 2 : 0);
     }
+    if (UNA) tl = __builtin_amdgcn_raw_buffer_load_b32(rd, lo.t, 0, NT ? 2 : 0);
     if (MODE != kModeCompute) {
       const __amdgpu_buffer_rsrc_t re = __builtin_amdgcn_make_buffer_rsrc(
           sh.crcs + c.tile * kTileChunks, 0, static_cast<int>(nch * 4u), 0x00020000);
@@ -367,8 +374,9 @@ DEV void issue(uint32_t (&d)[16], uint32_t &exp, uint32_t (&xw)[4], uint32_t &sh
     }
   } else {
     const uint32_t last = min(kTileChunks, segs[c.seg].nchunks - c.tile * kTileChunks) - 1u;
-    const uint8_t *p = segs[c.seg].data + static_cast<uint64_t>(c.tile) * kTileChunks * cs +
-                       static_cast<uint64_t>(c.r) * kRoundBytes + loff - a;
+    const uint8_t *rb = segs[c.seg].data + static_cast<uint64_t>(c.tile) * kTileChunks * cs +
+                        static_cast<uint64_t>(c.r) * kRoundBytes - a;
+    const uint8_t *p = rb + loff;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       const uint32_t g = min(2u * k + hsel, last);
@@ -377,9 +385,9 @@ DEV void issue(uint32_t (&d)[16], uint32_t &exp, uint32_t (&xw)[4], uint32_t &sh
       d[4 * k + 1] = v.y;
       d[4 * k + 2] = v.z;
       d[4 * k + 3] = v.w;
-      // a == 0: an in-bounds dummy (the dword after the data end may lie past its page)
-      if (UNA) xw[k] = gload32(p + static_cast<uint64_t>(g) * cs + (a ? 16u : 12u));
     }
+    // a == 0: an in-bounds dummy (the dword after the data end may lie past its page)
+    if (UNA) tl = gload32(rb + static_cast<uint64_t>(min(lane, last)) * cs + (a ? kRoundBytes : kRoundBytes - 4u));
     if (MODE != kModeCompute) {
       // buffer load: expected CRCs of a packet sit at any byte offset of the wire image
       const __amdgpu_buffer_rsrc_t re = __builtin_amdgcn_make_buffer_rsrc(
@@ -505,51 +513,57 @@ DEV void copy_round(const uint32_t (&d)[16], const Cursor c, SegP segs, const La
   }
 }
 
+DEV void copy_quads(const uint32_t (&d)[16], const Cursor c, SegP segs, const LaneConst &L, SegCache &kc) {
+  const SegHot &sh = hot(kc, segs, c.seg).h;
+  const uint32_t cs = sh.chunk_size;
+  uint8_t *dst = segs[c.seg].copy_dst;
+  const uint32_t nch = min(kTileChunks, sh.nchunks - c.tile * kTileChunks);
+  const bool ok = c.valid && dst != nullptr;
+  uint8_t *base = ok ? dst + static_cast<uint64_t>(c.tile) * kTileChunks * cs + static_cast<uint64_t>(c.r) * kRoundBytes
+                     : dst;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<uint8_t *>(rfl64(reinterpret_cast<uint64_t>(base))), 0,
+      static_cast<int>(rfl(ok ? (nch - 1u) * cs + kRoundBytes : 0u)), 0x00020000);
+  const uint32_t off = L.qg * cs + 64u * L.qi;
+#pragma unroll
+  for (int m = 0; m < 4; m++) {
+    const u32x4 v = {d[4 * m + 0], d[4 * m + 1], d[4 * m + 2], d[4 * m + 3]};
+    __builtin_amdgcn_raw_buffer_store_b128(v, rs, off + 16u * m, 0, 0);
+  }
+}
+
 // Process one round of each of the wave's S streams (d[s] for cursor c[s]);
 // st[s] is stream s's running lane register across the rounds of a tile.
 // The S slicing chains are independent and interleaved step by step, so one
 // lane keeps S table lookups in flight (latency hiding by ILP, not waves).
+// Verify + copy-out of realigned (UNA) rounds: after the transpose lane L
+// holds the 64 bytes of quad L (chunk L >> 3, position L & 7), written with
+// four 16-B stores.
+DEV void copy_quads(const uint32_t (&d)[16], const Cursor c, SegP segs, const LaneConst &L, SegCache &kc);
+
 template <int MODE, int S, int COPY, int UNA>
-DEV void process(const uint32_t *lds, uint32_t (&d)[S][16], const uint32_t (&exp)[S], const uint32_t (&xw)[S][4],
+DEV void process(const uint32_t *lds, uint32_t (&d)[S][16], const uint32_t (&exp)[S], const uint32_t (&tl)[S],
                  const uint32_t (&sh_a)[S], const Cursor (&c)[S], SegP segs, uint32_t (&st)[S], const LaneConst &L,
                  uint32_t *__restrict__ first_bad, unsigned long long *__restrict__ mism, SegCache (&kc)[S]) {
-  if constexpr (UNA) {
-#pragma unroll
-    for (int s = 0; s < S; s++) {
-      const uint32_t a = sh_a[s];
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const uint32_t w0 = d[s][4 * k], w1 = d[s][4 * k + 1], w2 = d[s][4 * k + 2], w3 = d[s][4 * k + 3];
-        d[s][4 * k + 0] = __builtin_amdgcn_alignbyte(w1, w0, a);
-        d[s][4 * k + 1] = __builtin_amdgcn_alignbyte(w2, w1, a);
-        d[s][4 * k + 2] = __builtin_amdgcn_alignbyte(w3, w2, a);
-        d[s][4 * k + 3] = __builtin_amdgcn_alignbyte(xw[s][k], w3, a);
-      }
-    }
-  }
-  if constexpr (COPY) {
+  if constexpr (COPY && !UNA) {
 #pragma unroll
     for (int s = 0; s < S; s++) copy_round(d[s], c[s], segs, L, kc[s]);
-  }
-  if constexpr (kDiag && MODE == kModeLoadOnly) {
-#pragma unroll
-    for (int s = 0; s < S; s++) {
-      uint32_t v = exp[s];
-#pragma unroll
-      for (int w = 0; w < 16; w++) v ^= d[s][w];
-      st[s] ^= v;
-      // the verify bitmap store with its record dropped keeps the op count
-      const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(segs[c[s].seg].bitmap + c[s].tile, 0, 0,
-                                                                          0x00020000);
-      __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(st[s]), rb, 0u, 0, 0);
-      if (st[s] == 0x9E3779B9u && c[s].r == 0xFFFFFFFFu) atomicAdd(mism, 1ull);  // keeps the loads live
-    }
-    return;
   }
   uint32_t x[S];
 #pragma unroll
   for (int s = 0; s < S; s++) {
     transpose(d[s]);
+    if constexpr (UNA) {
+      const uint32_t a = sh_a[s];
+      const uint32_t nxt = dpp<0x101>(d[s][0]);  // row_shl:1 -- lane L + 1's first dword
+      const uint32_t tv = static_cast<uint32_t>(
+          __builtin_amdgcn_ds_bpermute(static_cast<int>((L.lane >> 3) * 4u), static_cast<int>(tl[s])));
+      const uint32_t w16 = (L.lane & 7u) == 7u ? tv : nxt;
+#pragma unroll
+      for (int j = 0; j < 15; j++) d[s][j] = __builtin_amdgcn_alignbyte(d[s][j + 1], d[s][j], a);
+      d[s][15] = __builtin_amdgcn_alignbyte(w16, d[s][15], a);
+      if constexpr (COPY) copy_quads(d[s], c[s], segs, L, kc[s]);
+    }
     const uint32_t ri = hot(kc[s], segs, c[s].seg).reg_init;  // uniform control flow: kc stays in SGPRs
     if (c[s].r == 0) st[s] = (L.qi == 0) ? ri : 0u;
     else st[s] = zshift(lds, L.z448, st[s]);
@@ -730,10 +744,10 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
   // with their stores dropped.
   uint32_t buf[DEPTH][S][16];
   uint32_t ex[DEPTH][S];
-  uint32_t xw[DEPTH][S][4];  // UNA: the dword after each 16-B piece
-  uint32_t sha[DEPTH][S];    // UNA: byte shift of the round's segment
+  uint32_t tl[DEPTH][S];   // UNA: lanes 0..7, the dword after chunk lane's round part
+  uint32_t sha[DEPTH][S];  // UNA: byte shift of the round's segment
   uint32_t st[S];
-  LaneOff lo{0u, {0u, 0u, 0u, 0u}};
+  LaneOff lo{0u, {0u, 0u, 0u, 0u}, 0u};
   SegCache kc[S];
 #pragma unroll
   for (int s = 0; s < S; s++) {
@@ -750,22 +764,24 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
 #pragma unroll
     for (int s = 0; s < S; s++) {
       ex[k][s] = 0u;
-      issue<MODE, NT, BUF, UNA>(buf[k][s], ex[k][s], xw[k][s], sha[k][s], cur[k][s], sg, L.hsel, L.loff, L.qg, lo,
-                                kc[s]);
+      tl[k][s] = 0u;
+      sha[k][s] = 0u;
+      issue<MODE, NT, BUF, UNA>(buf[k][s], ex[k][s], tl[k][s], sha[k][s], cur[k][s], sg, L.hsel, L.loff, L.qg, L.lane,
+                                lo, kc[s]);
     }
   }
   for (;;) {
 #pragma unroll
     for (int k = 0; k < DEPTH; k++) {
-      process<MODE, S, COPY, UNA>(lds, buf[k], ex[k], xw[k], sha[k], cur[k], sg, st, L, first_bad, mism, kc);
+      process<MODE, S, COPY, UNA>(lds, buf[k], ex[k], tl[k], sha[k], cur[k], sg, st, L, first_bad, mism, kc);
 #pragma unroll
       for (int s = 0; s < S; s++) nrounds += cur[k][s].valid ? 1u : 0u;
       const int prev = (k + DEPTH - 1) % DEPTH;
 #pragma unroll
       for (int s = 0; s < S; s++) {
         cur[k][s] = advance<ORDER>(cur[prev][s], sg, nseg, w, kc[s]);
-        issue<MODE, NT, BUF, UNA>(buf[k][s], ex[k][s], xw[k][s], sha[k][s], cur[k][s], sg, L.hsel, L.loff, L.qg,
-                                  lo, kc[s]);
+        issue<MODE, NT, BUF, UNA>(buf[k][s], ex[k][s], tl[k][s], sha[k][s], cur[k][s], sg, L.hsel, L.loff, L.qg,
+                                  L.lane, lo, kc[s]);
       }
     }
     bool more = false;
