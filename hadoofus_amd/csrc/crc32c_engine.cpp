@@ -217,6 +217,18 @@ bool device_accessible(const void *p) {
   return a.devicePointer != nullptr;
 }
 
+int launch_verify_dyn(DevCtx &c, const SegDev *d_segs, const GridSummary *dyn, uint64_t gtiles_ub, uint32_t *d_fb,
+                      unsigned long long *d_mism, uint32_t *d_gctr, hipStream_t st, int ctype, bool copy) {
+  (void)d_gctr;  // zeroed by grid_build_kernel
+  const hipError_t le = launch_tiles(kModeVerify, 2, std::min(g_nt_loads, 1), 3, 1, 1024, c.num_cu, d_segs, 0, 0, 0,
+                                     c.d_tab_main_t[ctype], d_fb, d_mism, nullptr, g_group_shift << 8, d_gctr, st,
+                                     copy ? 1 : 0, 1, dyn);
+  if (le == hipErrorInvalidValue) return fail(HDFS_CRC32C_EINVAL, "verify kernel shape not built");
+  HIPCHK(le);
+  HIPCHK(launch_generic(kModeVerify, d_segs, 0, gtiles_ub, c.d_tab_main_t[ctype], d_fb, d_mism, st, dyn));
+  return HDFS_CRC32C_OK;
+}
+
 bool any_unaligned(const SegDev *segs, size_t n) {
   for (size_t i = 0; i < n; i++)
     if (segs[i].main_tiles && (reinterpret_cast<uintptr_t>(segs[i].data) & 3u)) return true;

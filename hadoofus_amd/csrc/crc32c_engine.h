@@ -20,12 +20,12 @@ hipError_t launch_tiles(int mode, int order, int nt, int depth, int streams, int
                         const SegDev *segs, uint32_t nseg, uint64_t total_rounds, uint64_t total_tiles,
                         const uint32_t *gtab, uint32_t *first_bad, unsigned long long *mism,
                         unsigned long long *diag, uint32_t tune, uint32_t *gctr, hipStream_t stream,
-                        int copy = 0, int una = 0);
+                        int copy = 0, int una = 0, const GridSummary *dyn = nullptr);
 hipError_t launch_probe_read(const uint8_t *p, uint64_t nbytes, uint32_t *out, int grid, int block, int variant,
                              hipStream_t stream);
 hipError_t launch_generic(int mode, const SegDev *segs, uint32_t nseg, uint64_t total_gtiles,
                           const uint32_t *gtab, uint32_t *first_bad, unsigned long long *mism,
-                          hipStream_t stream);
+                          hipStream_t stream, const GridSummary *dyn = nullptr);
 hipError_t launch_combine(const uint32_t *raws, uint64_t nraw, uint32_t cs, uint64_t len,
                           const uint32_t *pow2, uint32_t reg0, uint32_t *acc, hipStream_t stream);
 hipError_t launch_fill(uint64_t *out, uint64_t nwords, uint64_t seed, uint64_t g0, hipStream_t stream);
@@ -48,7 +48,7 @@ hipError_t launch_header_window(const uint8_t *s, uint64_t len, uint64_t base, u
 // frame_grid_kernel + grid_build_kernel: one device framing pass.
 hipError_t launch_frame_grid(const uint8_t *s, uint64_t len, uint64_t base, uint32_t count, int proto, uint32_t cs,
                              int ctype, int verify, uint32_t sflags, uint8_t *bm_base, uint8_t *copy_base,
-                             GridBufs g, hipStream_t stream);
+                             uint64_t copy_cap, GridBufs g, hipStream_t stream);
 hipError_t launch_grid_finalize(const SegDev *segs, uint32_t nseg, const uint32_t *seg2pkt, const uint32_t *fb,
                                 GridBad *bad, uint32_t bad_cap, GridSummary *sum, hipStream_t stream);
 
@@ -148,6 +148,7 @@ struct DevCtx {
   struct GridSlot {
     uint8_t *d = nullptr, *h = nullptr;
     size_t dcap = 0, hcap = 0;
+    hipEvent_t framed = nullptr;  // the pass's segment table is built (c.stream -> c.v_stream)
   };
   std::vector<GridSlot> grid;
   std::mutex mu;
@@ -181,6 +182,11 @@ int launch_all(DevCtx &c, int mode, const SegDev *d_segs, uint32_t nseg, uint64_
                uint64_t gtiles, uint32_t *d_fb, unsigned long long *d_mism, uint32_t *d_gctr, hipStream_t st,
                hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, bool reset = true, int ctype = 0,
                bool copy = false, bool gctr_zeroed = false, bool una = false);
+// Verify pass over a segment table built on the device (grid_build_kernel):
+// sizes read by the kernels from *dyn; grid sized for rounds_ub / gtiles_ub
+// (upper bounds).  Schedule 2 (packet tables), realigning kernel.
+int launch_verify_dyn(DevCtx &c, const SegDev *d_segs, const GridSummary *dyn, uint64_t gtiles_ub, uint32_t *d_fb,
+                      unsigned long long *d_mism, uint32_t *d_gctr, hipStream_t st, int ctype, bool copy);
 // Any segment whose data is not 4-B aligned (selects the realigning kernel).
 bool any_unaligned(const SegDev *segs, size_t n);
 // Copy / compute streams, events and the small pipeline buffers.

@@ -590,9 +590,17 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
     const SegDev *__restrict__ segs, uint32_t nseg, uint64_t total_rounds, uint64_t total_tiles,
     const uint32_t *__restrict__ gtab, uint32_t *__restrict__ first_bad,
     unsigned long long *__restrict__ mism, unsigned long long *__restrict__ diag, uint32_t tune,
-    uint32_t *__restrict__ gctr) {
+    uint32_t *__restrict__ gctr, const GridSummary *__restrict__ dyn) {
   static_assert(ORDER != 0 || S == 1, "static per-wave slices serve one stream");
   static_assert(DEPTH >= 2 && DEPTH <= 4 && S >= 1 && S <= 4, "shape");
+  // dyn: sizes of a segment table built on the device (grid_build_kernel),
+  // read here instead of passed by the host -- no host round trip between
+  // framing and verify
+  if (dyn) {
+    nseg = dyn->nseg;
+    total_rounds = dyn->rounds;
+    total_tiles = dyn->mtiles;
+  }
   // + ticket counter, pad, kSlots 64-bit pool slots
   __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords + 2 + 2 * kSlots];
 
@@ -803,7 +811,11 @@ template <int MODE>
 __global__ __launch_bounds__(256) void crc32c_generic_kernel(
     const SegDev *__restrict__ segs, uint32_t nseg, uint64_t total_gtiles,
     const uint32_t *__restrict__ gtab, uint32_t *__restrict__ first_bad,
-    unsigned long long *__restrict__ mism) {
+    unsigned long long *__restrict__ mism, const GridSummary *__restrict__ dyn) {
+  if (dyn) {  // sizes from a device-built table (the launch's grid is an upper bound)
+    nseg = dyn->nseg;
+    total_gtiles = dyn->gtiles;
+  }
   __shared__ uint32_t tt[1024];
   for (uint32_t i = threadIdx.x; i < 1024u; i += blockDim.x) tt[i] = gtab[i];
   __syncthreads();
@@ -1347,7 +1359,7 @@ __global__ __launch_bounds__(kGridBlock) void grid_build_kernel(
     const hdfs_crc32c_packet *__restrict__ recs, const uint32_t *__restrict__ status,
     const GridContrib *__restrict__ contrib, const uint64_t *__restrict__ blk_sum,
     const uint32_t *__restrict__ blk_min, uint32_t cs, uint32_t sflags, uint8_t *__restrict__ bm_base,
-    uint8_t *__restrict__ copy_base, SegDev *__restrict__ segs, uint32_t *__restrict__ seg2pkt,
+    uint8_t *__restrict__ copy_base, uint64_t copy_cap, SegDev *__restrict__ segs, uint32_t *__restrict__ seg2pkt,
     uint32_t *__restrict__ fb, uint32_t *__restrict__ gctr, GridSummary *__restrict__ sum) {
   __shared__ uint64_t red[6][kGridBlock / 64];
   __shared__ uint32_t redm[kGridBlock / 64];
@@ -1430,7 +1442,9 @@ __global__ __launch_bounds__(kGridBlock) void grid_build_kernel(
     d.len = uint64_t(r.data_len);
     d.round_start = ex[1];
     d.gtile_start = ex[3];
-    d.copy_dst = copy_base ? copy_base + ex[5] : nullptr;
+    // never past the caller's buffer: a packet that does not fit is not copied
+    // (the host sees the run's payload exceed the capacity and fails the call)
+    d.copy_dst = copy_base && ex[5] + own[5] <= copy_cap ? copy_base + ex[5] : nullptr;
     d.reserved = 0;
     segs[sg] = d;
     seg2pkt[sg] = k;
@@ -1481,6 +1495,7 @@ __global__ __launch_bounds__(256) void grid_finalize_kernel(const SegDev *__rest
                                                             GridBad *__restrict__ bad, uint32_t bad_cap,
                                                             GridSummary *__restrict__ sum) {
   const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (nseg == 0xFFFFFFFFu) nseg = sum->nseg;  // launched before the host knows the run's size
   if (i >= nseg || fb[i] == 0xFFFFFFFFu) return;
   const SegDev d = segs[i];
   const uint32_t nb = (d.nchunks + 7u) / 8u;
@@ -1496,7 +1511,7 @@ __global__ __launch_bounds__(256) void grid_finalize_kernel(const SegDev *__rest
 
 hipError_t launch_frame_grid(const uint8_t *s, uint64_t len, uint64_t base, uint32_t count, int proto, uint32_t cs,
                              int ctype, int verify, uint32_t sflags, uint8_t *bm_base, uint8_t *copy_base,
-                             GridBufs g, hipStream_t stream) {
+                             uint64_t copy_cap, GridBufs g, hipStream_t stream) {
   if (!count || base >= len) return hipErrorInvalidValue;
   const uint32_t nblk = (count + kGridBlock - 1) / kGridBlock;
   auto *contrib = reinterpret_cast<GridContrib *>(g.contrib);
@@ -1505,15 +1520,17 @@ hipError_t launch_frame_grid(const uint8_t *s, uint64_t len, uint64_t base, uint
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(grid_build_kernel, dim3(nblk), dim3(kGridBlock), 0, stream, s, base, count, nblk, g.recs,
-                     g.status, contrib, g.blk_sum, g.blk_min, cs, sflags, bm_base, copy_base, g.segs, g.seg2pkt, g.fb,
-                     g.gctr, g.sum);
+                     g.status, contrib, g.blk_sum, g.blk_min, cs, sflags, bm_base, copy_base, copy_cap, g.segs,
+                     g.seg2pkt, g.fb, g.gctr, g.sum);
   return hipGetLastError();
 }
 
 hipError_t launch_grid_finalize(const SegDev *segs, uint32_t nseg, const uint32_t *seg2pkt, const uint32_t *fb,
                                 GridBad *bad, uint32_t bad_cap, GridSummary *sum, hipStream_t stream) {
-  if (!nseg) return hipSuccess;
-  hipLaunchKernelGGL(grid_finalize_kernel, dim3((nseg + 255) / 256), dim3(256), 0, stream, segs, nseg, seg2pkt, fb,
+  // nseg 0xFFFFFFFF: the run's size is read from *sum; the grid covers bad_cap segments
+  const uint32_t n = nseg == 0xFFFFFFFFu ? bad_cap : nseg;
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(grid_finalize_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, segs, nseg, seg2pkt, fb,
                      bad, bad_cap, sum);
   return hipGetLastError();
 }
@@ -1577,10 +1594,10 @@ hipError_t launch_tiles(int mode, int order, int nt, int depth, int streams, int
                         const SegDev *segs, uint32_t nseg, uint64_t total_rounds, uint64_t total_tiles,
                         const uint32_t *gtab, uint32_t *first_bad, unsigned long long *mism,
                         unsigned long long *diag, uint32_t tune, uint32_t *gctr, hipStream_t stream, int copy,
-                        int una) {
+                        int una, const GridSummary *dyn) {
 #define HDFS_LAUNCH_CU(M, O, N, D, S, B, BUF, C, U)                                                            \
   hipLaunchKernelGGL((crc32c_tiles_kernel<M, O, N, D, S, B, BUF, C, U>), dim3(grid), dim3(B), 0, stream, segs, \
-                     nseg, total_rounds, total_tiles, gtab, first_bad, mism, diag, tune, gctr)
+                     nseg, total_rounds, total_tiles, gtab, first_bad, mism, diag, tune, gctr, dyn)
 #define HDFS_LAUNCH_C(M, O, N, D, S, B, BUF, C) HDFS_LAUNCH_CU(M, O, N, D, S, B, BUF, C, 0)
 #define HDFS_LAUNCH(M, O, N, D, S, B, BUF) HDFS_LAUNCH_C(M, O, N, D, S, B, BUF, 0)
 #define HDFS_SHAPE(O, N, D, S, B) (order == (O) && nt == (N) && depth == (D) && streams == (S) && block == (B))
@@ -1738,15 +1755,16 @@ hipError_t launch_probe_read(const uint8_t *p, uint64_t nbytes, uint32_t *out, i
 
 hipError_t launch_generic(int mode, const SegDev *segs, uint32_t nseg, uint64_t total_gtiles,
                           const uint32_t *gtab, uint32_t *first_bad, unsigned long long *mism,
-                          hipStream_t stream) {
+                          hipStream_t stream, const GridSummary *dyn) {
   const uint64_t threads = total_gtiles * kTileChunks;
   const uint32_t blocks = static_cast<uint32_t>((threads + 255) / 256);
+  if (!blocks) return hipSuccess;
   if (mode == kModeVerify)
     hipLaunchKernelGGL(crc32c_generic_kernel<kModeVerify>, dim3(blocks), dim3(256), 0, stream, segs,
-                       nseg, total_gtiles, gtab, first_bad, mism);
+                       nseg, total_gtiles, gtab, first_bad, mism, dyn);
   else
     hipLaunchKernelGGL(crc32c_generic_kernel<kModeCompute>, dim3(blocks), dim3(256), 0, stream,
-                       segs, nseg, total_gtiles, gtab, first_bad, mism);
+                       segs, nseg, total_gtiles, gtab, first_bad, mism, dyn);
   return hipGetLastError();
 }
 

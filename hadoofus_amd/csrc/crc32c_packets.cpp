@@ -566,9 +566,37 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
                       reinterpret_cast<uint32_t *>(dg + L.fb),
                       ctr,
                       sum};
+    // framing and the segment table on c.stream; the verify of the run is
+    // queued behind it on c.v_stream right away, sized by the device-built
+    // summary (no host round trip before the GPU starts verifying)
     hipError_t e = launch_frame_grid(d, len, pos, count, proto, cs, ctype, verify ? 1 : 0, sflags, dg + L.bm,
-                                     copy_dst ? copy_dst + payload : nullptr, gb, c.stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(hg + L.h_sum, sum, sizeof(GridSummary), hipMemcpyDeviceToHost, c.stream);
+                                     copy_dst ? copy_dst + payload : nullptr, copy_dst ? copy_cap - payload : 0, gb,
+                                     c.stream);
+    if (e == hipSuccess && verify) {
+      if (!c.grid[si].framed) e = hipEventCreateWithFlags(&c.grid[si].framed, hipEventDisableTiming);
+      if (e == hipSuccess) e = hipEventRecord(c.grid[si].framed, c.stream);
+      if (e == hipSuccess) e = hipStreamWaitEvent(c.v_stream, c.grid[si].framed, 0);
+    }
+    if (e != hipSuccess) {
+      rc = fail(HDFS_CRC32C_EHIP, "device framing: %s", hipGetErrorString(e));
+      break;
+    }
+    if (verify) {
+      // generic tiles: at most one per packet for chunk sizes the tiled
+      // kernel takes, else every tile of every packet
+      const uint64_t gtiles_ub = cs % kRoundBytes == 0 ? count : left / (uint64_t(cs) * kTileChunks) + 2ull * count;
+      rc = launch_verify_dyn(c, reinterpret_cast<const SegDev *>(dg + L.segs), sum, gtiles_ub,
+                             reinterpret_cast<uint32_t *>(dg + L.fb), reinterpret_cast<unsigned long long *>(ctr + 16),
+                             ctr, c.v_stream, tset, copy_dst != nullptr);
+      if (rc) break;
+      auto *bad = reinterpret_cast<GridBad *>(dg + L.bad);
+      HIPCHK(launch_grid_finalize(reinterpret_cast<const SegDev *>(dg + L.segs), 0xFFFFFFFFu,
+                                  reinterpret_cast<const uint32_t *>(dg + L.seg2pkt),
+                                  reinterpret_cast<const uint32_t *>(dg + L.fb), bad, count, sum, c.v_stream));
+      HIPCHK(hipMemcpyAsync(hg + L.h_sum2, sum, 256 + size_t(std::min(kBadFirst, count)) * sizeof(GridBad),
+                            hipMemcpyDeviceToHost, c.v_stream));
+    }
+    e = hipMemcpyAsync(hg + L.h_sum, sum, sizeof(GridSummary), hipMemcpyDeviceToHost, c.stream);
     const auto tq = clk::now();
     if (e == hipSuccess) e = hipStreamSynchronize(c.stream);
     t_enq += us_since(tq0, tq);
@@ -585,19 +613,6 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
       rc = fail(HDFS_CRC32C_EINVAL, "copy-out buffer of %llu bytes is too small (%llu needed so far)",
                 (unsigned long long)copy_cap, (unsigned long long)(payload + S.payload));
       break;
-    }
-    if (verify && S.nseg) {
-      // the pool counter was zeroed by grid_build_kernel: no reset launch
-      rc = launch_all(c, kModeVerify, reinterpret_cast<const SegDev *>(dg + L.segs), S.nseg, S.rounds, S.mtiles,
-                      S.gtiles, reinterpret_cast<uint32_t *>(dg + L.fb), reinterpret_cast<unsigned long long *>(ctr + 16),
-                      ctr, c.v_stream, nullptr, nullptr, false, tset, copy_dst != nullptr, true, S.unaligned != 0);
-      if (rc) break;
-      auto *bad = reinterpret_cast<GridBad *>(dg + L.bad);
-      HIPCHK(launch_grid_finalize(reinterpret_cast<const SegDev *>(dg + L.segs), S.nseg,
-                                  reinterpret_cast<const uint32_t *>(dg + L.seg2pkt),
-                                  reinterpret_cast<const uint32_t *>(dg + L.fb), bad, count, sum, c.v_stream));
-      HIPCHK(hipMemcpyAsync(hg + L.h_sum2, sum, 256 + size_t(std::min(kBadFirst, S.nseg)) * sizeof(GridBad),
-                            hipMemcpyDeviceToHost, c.v_stream));
     }
     t_venq += us_since(tq, clk::now());
     passes.push_back({si, out.size(), S.recorded, verify ? S.nseg : 0u, count, bm_cap});
