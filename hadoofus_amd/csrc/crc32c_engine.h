@@ -149,7 +149,9 @@ struct DevCtx {
     uint8_t *d = nullptr, *h = nullptr;
     size_t dcap = 0, hcap = 0;
     hipEvent_t framed = nullptr;  // the pass's segment table is built (c.stream -> c.v_stream)
+    uint8_t *hd = nullptr;        // device address of h (coherent, mapped)
   };
+  uint32_t grid_seq = 0;
   std::vector<GridSlot> grid;
   std::mutex mu;
 };

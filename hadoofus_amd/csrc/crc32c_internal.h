@@ -76,6 +76,8 @@ struct GridSummary {
   uint64_t bm_bytes;     // bitmap bytes of the segment table
   uint32_t nbad;         // verify: packets with bad chunks (grid_finalize_kernel)
   uint32_t unaligned;    // some tiled segment's data is not 4-B aligned (realigning kernel)
+  uint32_t seq;          // host copy only: written last (after a system fence) by grid_build_kernel
+  uint32_t pad;
 };
 // Device tables of one framing pass (count grid points).
 struct GridBufs {
@@ -89,6 +91,12 @@ struct GridBufs {
   uint32_t *fb;                // [count] first bad chunk per segment
   uint32_t *gctr;              // tiled-kernel pool counter (zeroed by grid_build_kernel)
   GridSummary *sum;
+  // pinned host memory mapped into the device: the records and the summary
+  // are written there by the kernels themselves (no copy launches, which
+  // would queue behind the verify kernel for CUs)
+  ::hdfs_crc32c_packet *hrecs;
+  GridSummary *hsum;
+  uint32_t seq;                // written to hsum->seq once hsum is complete
 };
 
 // Compact verify verdict of one packet (grid_finalize_kernel).

@@ -1283,7 +1283,7 @@ __global__ __launch_bounds__(kGridBlock) void frame_grid_kernel(
     const uint8_t *__restrict__ s, uint64_t len, uint64_t base, uint32_t count, int proto, uint32_t cs, int ctype,
     int verify, hdfs_crc32c_packet *__restrict__ recs, uint32_t *__restrict__ status,
     GridContrib *__restrict__ contrib, uint64_t *__restrict__ blk_sum, uint32_t *__restrict__ blk_min,
-    GridSummary *__restrict__ sum) {
+    GridSummary *__restrict__ sum, hdfs_crc32c_packet *__restrict__ hrecs) {
   __shared__ __attribute__((aligned(16))) uint8_t win[kGridBlock + 1][kHdrWin];
   __shared__ uint64_t red[6][kGridBlock / 64];
   __shared__ uint32_t redm[kGridBlock / 64];
@@ -1316,6 +1316,7 @@ __global__ __launch_bounds__(kGridBlock) void frame_grid_kernel(
                                     : kGridOff;
       if (code != kGridMore) {
         recs[k] = r;
+        hrecs[k] = r;  // the caller's copy, straight to pinned host memory
         a = grid_contrib(r, cs, verify);
       }
     }
@@ -1360,7 +1361,8 @@ __global__ __launch_bounds__(kGridBlock) void grid_build_kernel(
     const GridContrib *__restrict__ contrib, const uint64_t *__restrict__ blk_sum,
     const uint32_t *__restrict__ blk_min, uint32_t cs, uint32_t sflags, uint8_t *__restrict__ bm_base,
     uint8_t *__restrict__ copy_base, uint64_t copy_cap, SegDev *__restrict__ segs, uint32_t *__restrict__ seg2pkt,
-    uint32_t *__restrict__ fb, uint32_t *__restrict__ gctr, GridSummary *__restrict__ sum) {
+    uint32_t *__restrict__ fb, uint32_t *__restrict__ gctr, GridSummary *__restrict__ sum,
+    GridSummary *__restrict__ hsum, uint32_t seq) {
   __shared__ uint64_t red[6][kGridBlock / 64];
   __shared__ uint32_t redm[kGridBlock / 64];
   __shared__ uint64_t pre[6];
@@ -1484,6 +1486,13 @@ __global__ __launch_bounds__(kGridBlock) void grid_build_kernel(
     sum->next_pos = next;
     sum->nbad = 0;
     *gctr = 0u;  // the verify launch's pool counter (no separate reset launch)
+    // the host's copy: every field, one system-scope fence, then the sequence
+    // number the host polls
+    GridSummary h = *sum;
+    h.seq = 0u;
+    *hsum = h;
+    __threadfence_system();
+    __hip_atomic_store(&hsum->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -1516,12 +1525,12 @@ hipError_t launch_frame_grid(const uint8_t *s, uint64_t len, uint64_t base, uint
   const uint32_t nblk = (count + kGridBlock - 1) / kGridBlock;
   auto *contrib = reinterpret_cast<GridContrib *>(g.contrib);
   hipLaunchKernelGGL(frame_grid_kernel, dim3(nblk), dim3(kGridBlock), 0, stream, s, len, base, count, proto, cs,
-                     ctype, verify, g.recs, g.status, contrib, g.blk_sum, g.blk_min, g.sum);
+                     ctype, verify, g.recs, g.status, contrib, g.blk_sum, g.blk_min, g.sum, g.hrecs);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(grid_build_kernel, dim3(nblk), dim3(kGridBlock), 0, stream, s, base, count, nblk, g.recs,
                      g.status, contrib, g.blk_sum, g.blk_min, cs, sflags, bm_base, copy_base, copy_cap, g.segs,
-                     g.seg2pkt, g.fb, g.gctr, g.sum);
+                     g.seg2pkt, g.fb, g.gctr, g.sum, g.hsum, g.seq);
   return hipGetLastError();
 }
 

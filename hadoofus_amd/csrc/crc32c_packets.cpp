@@ -503,9 +503,12 @@ int reserve_grid(DevCtx &c, size_t si, const GridLayout &L) {
   }
   if (L.htotal > g.hcap) {
     if (g.h) HIPCHK(hipHostFree(g.h));
-    g.h = nullptr;
+    g.h = g.hd = nullptr;
     g.hcap = 0;
-    HIPCHK(hipHostMalloc(&g.h, L.htotal, hipHostMallocDefault));
+    // fine-grained (coherent) and mapped: the framing kernels write the
+    // records and the summary here directly
+    HIPCHK(hipHostMalloc(&g.h, L.htotal, hipHostMallocCoherent | hipHostMallocMapped));
+    HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&g.hd), g.h, 0));
     g.hcap = L.htotal;
   }
   return HDFS_CRC32C_OK;
@@ -565,7 +568,12 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
                       reinterpret_cast<uint32_t *>(dg + L.seg2pkt),
                       reinterpret_cast<uint32_t *>(dg + L.fb),
                       ctr,
-                      sum};
+                      sum,
+                      reinterpret_cast<hdfs_crc32c_packet *>(c.grid[si].hd + L.h_recs),
+                      reinterpret_cast<GridSummary *>(c.grid[si].hd + L.h_sum),
+                      ++c.grid_seq};
+    auto *hsum = reinterpret_cast<volatile GridSummary *>(hg + L.h_sum);
+    hsum->seq = 0;
     // framing and the segment table on c.stream; the verify of the run is
     // queued behind it on c.v_stream right away, sized by the device-built
     // summary (no host round trip before the GPU starts verifying)
@@ -596,19 +604,30 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
       HIPCHK(hipMemcpyAsync(hg + L.h_sum2, sum, 256 + size_t(std::min(kBadFirst, count)) * sizeof(GridBad),
                             hipMemcpyDeviceToHost, c.v_stream));
     }
-    e = hipMemcpyAsync(hg + L.h_sum, sum, sizeof(GridSummary), hipMemcpyDeviceToHost, c.stream);
+    // the summary lands in pinned memory with its sequence number last: poll
+    // it (a fault is caught by the stream synchronisation after 200 ms)
     const auto tq = clk::now();
-    if (e == hipSuccess) e = hipStreamSynchronize(c.stream);
+    for (uint32_t spin = 1;; spin++) {
+      if (__atomic_load_n(&reinterpret_cast<GridSummary *>(hg + L.h_sum)->seq, __ATOMIC_ACQUIRE) == gb.seq) break;
+      if ((spin & 4095u) == 0 && clk::now() - tq > std::chrono::milliseconds(200)) {
+        e = hipStreamSynchronize(c.stream);
+        if (e == hipSuccess &&
+            __atomic_load_n(&reinterpret_cast<GridSummary *>(hg + L.h_sum)->seq, __ATOMIC_ACQUIRE) != gb.seq)
+          e = hipErrorUnknown;
+        break;
+      }
+#if defined(__x86_64__) || defined(__i386__)
+      __builtin_ia32_pause();
+#endif
+    }
     t_enq += us_since(tq0, tq);
     t_sync += us_since(tq, clk::now());
     if (e != hipSuccess) {
       rc = fail(HDFS_CRC32C_EHIP, "device framing: %s", hipGetErrorString(e));
       break;
     }
-    const GridSummary S = *reinterpret_cast<const GridSummary *>(hg + L.h_sum);
-    if (S.recorded)
-      HIPCHK(hipMemcpyAsync(hg + L.h_recs, recs, size_t(S.recorded) * sizeof(hdfs_crc32c_packet),
-                            hipMemcpyDeviceToHost, c.stream));
+    GridSummary S;
+    std::memcpy(&S, hg + L.h_sum, sizeof(S));
     if (copy_dst && payload + S.payload > copy_cap) {
       rc = fail(HDFS_CRC32C_EINVAL, "copy-out buffer of %llu bytes is too small (%llu needed so far)",
                 (unsigned long long)copy_cap, (unsigned long long)(payload + S.payload));
