@@ -580,11 +580,7 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
     hipError_t e = launch_frame_grid(d, len, pos, count, proto, cs, ctype, verify ? 1 : 0, sflags, dg + L.bm,
                                      copy_dst ? copy_dst + payload : nullptr, copy_dst ? copy_cap - payload : 0, gb,
                                      c.stream);
-    if (e == hipSuccess && verify) {
-      if (!c.grid[si].framed) e = hipEventCreateWithFlags(&c.grid[si].framed, hipEventDisableTiming);
-      if (e == hipSuccess) e = hipEventRecord(c.grid[si].framed, c.stream);
-      if (e == hipSuccess) e = hipStreamWaitEvent(c.v_stream, c.grid[si].framed, 0);
-    }
+
     if (e != hipSuccess) {
       rc = fail(HDFS_CRC32C_EHIP, "device framing: %s", hipGetErrorString(e));
       break;
@@ -593,16 +589,18 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
       // generic tiles: at most one per packet for chunk sizes the tiled
       // kernel takes, else every tile of every packet
       const uint64_t gtiles_ub = cs % kRoundBytes == 0 ? count : left / (uint64_t(cs) * kTileChunks) + 2ull * count;
+      // same stream as the framing kernels (stream order, no event); the host
+      // polls the framing summary instead of synchronising the stream
       rc = launch_verify_dyn(c, reinterpret_cast<const SegDev *>(dg + L.segs), sum, gtiles_ub,
                              reinterpret_cast<uint32_t *>(dg + L.fb), reinterpret_cast<unsigned long long *>(ctr + 16),
-                             ctr, c.v_stream, tset, copy_dst != nullptr);
+                             ctr, c.stream, tset, copy_dst != nullptr);
       if (rc) break;
       auto *bad = reinterpret_cast<GridBad *>(dg + L.bad);
       HIPCHK(launch_grid_finalize(reinterpret_cast<const SegDev *>(dg + L.segs), 0xFFFFFFFFu,
                                   reinterpret_cast<const uint32_t *>(dg + L.seg2pkt),
-                                  reinterpret_cast<const uint32_t *>(dg + L.fb), bad, count, sum, c.v_stream));
+                                  reinterpret_cast<const uint32_t *>(dg + L.fb), bad, count, sum, c.stream));
       HIPCHK(hipMemcpyAsync(hg + L.h_sum2, sum, 256 + size_t(std::min(kBadFirst, count)) * sizeof(GridBad),
-                            hipMemcpyDeviceToHost, c.v_stream));
+                            hipMemcpyDeviceToHost, c.stream));
     }
     // the summary lands in pinned memory with its sequence number last: poll
     // it (a fault is caught by the stream synchronisation after 200 ms)
@@ -646,10 +644,10 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
     }
   }
   const auto t1 = clk::now();
-  // records of every pass (their copies overlapped the verify launches)
-  hipError_t e = hipStreamSynchronize(c.stream);
+  // records of every pass: written to pinned memory by frame_grid_kernel,
+  // complete once the pass's summary was seen; copied out while the verify
+  // kernels still run
   const auto t1b = clk::now();
-  if (!rc && e != hipSuccess) rc = fail(HDFS_CRC32C_EHIP, "framing records: %s", hipGetErrorString(e));
   if (!rc)
     for (const Pass &p : passes)
       if (p.n) std::memcpy(out.data() + p.off, c.grid[p.slot].h + GridLayout(p.count, p.bm_cap).h_recs,
@@ -658,9 +656,12 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
   if (!rc && fallback && out.size() < max_pkts)
     rc = walk_device_stream(c, d, len, proto, cs, ctype, max_pkts, verify, out, consumed, pos, copy_dst, &payload);
   const auto t1d = clk::now();
-  e = hipStreamSynchronize(c.v_stream);  // drained even after an error: its tables live in this context
+  // drained even after an error: the tables of queued work live in this context
+  hipError_t e = hipStreamSynchronize(c.stream);
+  const hipError_t e2 = hipStreamSynchronize(c.v_stream);
   const auto t1e = clk::now();
   if (!rc && e != hipSuccess) rc = fail(HDFS_CRC32C_EHIP, "verify: %s", hipGetErrorString(e));
+  if (!rc && e2 != hipSuccess) rc = fail(HDFS_CRC32C_EHIP, "verify: %s", hipGetErrorString(e2));
   if (!rc && copy_dst && payload > copy_cap)
     rc = fail(HDFS_CRC32C_EINVAL, "copy-out buffer of %llu bytes is too small (%llu needed)",
               (unsigned long long)copy_cap, (unsigned long long)payload);
