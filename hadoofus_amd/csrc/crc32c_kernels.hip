@@ -1285,6 +1285,9 @@ __global__ __launch_bounds__(kGridBlock) void frame_grid_kernel(
     GridContrib *__restrict__ contrib, uint64_t *__restrict__ blk_sum, uint32_t *__restrict__ blk_min,
     GridSummary *__restrict__ sum, hdfs_crc32c_packet *__restrict__ hrecs) {
   __shared__ __attribute__((aligned(16))) uint8_t win[kGridBlock + 1][kHdrWin];
+  // the block's records, staged so the host copy goes out as contiguous
+  // 16-B stores (whole lines over PCIe) instead of one 56-B record per lane
+  __shared__ __attribute__((aligned(16))) hdfs_crc32c_packet srec[kGridBlock];
   __shared__ uint64_t red[6][kGridBlock / 64];
   __shared__ uint32_t redm[kGridBlock / 64];
   const uint32_t t = threadIdx.x, k = blockIdx.x * kGridBlock + t, lane = t & 63u, w = t >> 6;
@@ -1316,7 +1319,6 @@ __global__ __launch_bounds__(kGridBlock) void frame_grid_kernel(
                                     : kGridOff;
       if (code != kGridMore) {
         recs[k] = r;
-        hrecs[k] = r;  // the caller's copy, straight to pinned host memory
         a = grid_contrib(r, cs, verify);
       }
     }
@@ -1324,6 +1326,18 @@ __global__ __launch_bounds__(kGridBlock) void frame_grid_kernel(
   if (k < count) {
     status[k] = code;
     contrib[k] = a;
+  }
+  srec[t] = r;  // (garbage past the run's end: the host reads only recorded packets)
+  __syncthreads();
+  {
+    static_assert((kGridBlock * sizeof(hdfs_crc32c_packet)) % 16 == 0, "16-B record copy");
+    // rounded up: the last store may run 8 B past the block's last record
+    // (still inside the host area, whose record array is padded to 256 B)
+    const uint32_t nrec = min(kGridBlock, count - blockIdx.x * kGridBlock);
+    const uint32_t nvec = (nrec * uint32_t(sizeof(hdfs_crc32c_packet)) + 15u) / 16u;
+    const u32x4 *src = reinterpret_cast<const u32x4 *>(srec);
+    auto *dst = reinterpret_cast<u32x4 *>(hrecs + size_t(blockIdx.x) * kGridBlock);
+    for (uint32_t i = t; i < nvec; i += kGridBlock) dst[i] = src[i];
   }
   // block sums of the shares and the block's first grid point that is not On
   uint64_t v[6] = {a.nseg, a.rounds, a.mtiles, a.gtiles, a.bm, a.payload};
