@@ -1284,35 +1284,39 @@ __global__ __launch_bounds__(kGridBlock) void frame_grid_kernel(
     int verify, hdfs_crc32c_packet *__restrict__ recs, uint32_t *__restrict__ status,
     GridContrib *__restrict__ contrib, uint64_t *__restrict__ blk_sum, uint32_t *__restrict__ blk_min,
     GridSummary *__restrict__ sum, hdfs_crc32c_packet *__restrict__ hrecs) {
-  __shared__ __attribute__((aligned(16))) uint8_t win[kGridBlock + 1][kHdrWin];
+  __shared__ __attribute__((aligned(16))) uint8_t win[kGridBlock][kHdrWin];
   // the block's records, staged so the host copy goes out as contiguous
   // 16-B stores (whole lines over PCIe) instead of one 56-B record per lane
   __shared__ __attribute__((aligned(16))) hdfs_crc32c_packet srec[kGridBlock];
   __shared__ uint64_t red[6][kGridBlock / 64];
   __shared__ uint32_t redm[kGridBlock / 64];
   const uint32_t t = threadIdx.x, k = blockIdx.x * kGridBlock + t, lane = t & 63u, w = t >> 6;
-  // the stride: the wire size of the packet at base (every block stages it)
-  if (t == 0) stage_header(s, len, base, win[kGridBlock]);
-  __syncthreads();
-  hdfs_crc32c_packet r;
-  uint64_t total = 0;
-  const int st0 = grid_frame(s, len, base, win[kGridBlock], proto, cs, ctype, r, total);
-  const uint64_t stride = st0 == frame::kStepNext ? total : 0;
+  // The stride from the first 6 bytes of the packet at base: header_len +
+  // plen - 4 is exactly the wire size frame_step gives a complete, clean
+  // packet, so no thread decodes packet 0's PacketHeaderProto just to find
+  // the grid.  If packet 0 is not such a packet its status ends the run
+  // (first_break = 0) and the other grid points are never read.
+  uint64_t stride = 0;
+  {
+    auto at0 = [&](uint64_t i) -> uint32_t { return base + i < len ? uint32_t(s[base + i]) : 0u; };
+    const int32_t plen = int32_t((at0(0) << 24) | (at0(1) << 16) | (at0(2) << 8) | at0(3));
+    const int64_t hl = proto == HDFS_CRC32C_PROTO_V2 ? 6 + int64_t((at0(4) << 8) | at0(5)) : 25;
+    const int64_t tot = hl + int64_t(plen) - 4;
+    stride = tot > 0 ? uint64_t(tot) : 0;
+  }
   if (k == 0) {
     sum->stride = stride;
     sum->unaligned = 0u;  // OR-ed by grid_build_kernel
   }
+  hdfs_crc32c_packet r{};
+  uint64_t total = 0;
   uint32_t code = kGridMore;
   GridContrib a{0u, 0u, 0u, 0u, 0u, 0u};
-  // grid point k is reachable only if packet 0 did not end the walk
   if (k < count && (k == 0 || stride)) {
     const uint64_t pos = base + uint64_t(k) * stride;
     if (pos < len) {
-      int st = st0;
-      if (k) {
-        stage_header(s, len, pos, win[t]);
-        st = grid_frame(s, len, pos, win[t], proto, cs, ctype, r, total);
-      }
+      stage_header(s, len, pos, win[t]);
+      const int st = grid_frame(s, len, pos, win[t], proto, cs, ctype, r, total);
       code = st == frame::kStepMore ? kGridMore
            : st == frame::kStepStop ? kGridStop
            : total == stride        ? kGridOn
