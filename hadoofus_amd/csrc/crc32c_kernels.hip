@@ -1331,9 +1331,12 @@ __global__ __launch_bounds__(kGridBlock) void frame_grid_kernel(
     status[k] = code;
     contrib[k] = a;
   }
-  srec[t] = r;  // (garbage past the run's end: the host reads only recorded packets)
-  __syncthreads();
-  {
+  if (hrecs) {
+    // the caller's copy straight to pinned host memory, through LDS as
+    // contiguous 16-B stores (null: the host copies the records with a
+    // copy engine instead, off the CUs)
+    srec[t] = r;  // (garbage past the run's end: the host reads only recorded packets)
+    __syncthreads();
     static_assert((kGridBlock * sizeof(hdfs_crc32c_packet)) % 16 == 0, "16-B record copy");
     // rounded up: the last store may run 8 B past the block's last record
     // (still inside the host area, whose record array is padded to 256 B)

@@ -569,7 +569,7 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
                       reinterpret_cast<uint32_t *>(dg + L.fb),
                       ctr,
                       sum,
-                      reinterpret_cast<hdfs_crc32c_packet *>(c.grid[si].hd + L.h_recs),
+                      c.grid_nocu ? nullptr : reinterpret_cast<hdfs_crc32c_packet *>(c.grid[si].hd + L.h_recs),
                       reinterpret_cast<GridSummary *>(c.grid[si].hd + L.h_sum),
                       ++c.grid_seq};
     auto *hsum = reinterpret_cast<volatile GridSummary *>(hg + L.h_sum);
@@ -584,6 +584,21 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
     if (e != hipSuccess) {
       rc = fail(HDFS_CRC32C_EHIP, "device framing: %s", hipGetErrorString(e));
       break;
+    }
+    if (c.grid_nocu) {
+      // the run's records to pinned memory on a copy engine, concurrent with
+      // the verify kernel (a blit kernel would wait for it: it holds every CU)
+      if (!c.r_stream) e = hipStreamCreateWithFlags(&c.r_stream, hipStreamNonBlocking);
+      if (e == hipSuccess && !c.grid[si].framed) e = hipEventCreateWithFlags(&c.grid[si].framed, hipEventDisableTiming);
+      if (e == hipSuccess) e = hipEventRecord(c.grid[si].framed, c.stream);
+      if (e == hipSuccess) e = hipStreamWaitEvent(c.r_stream, c.grid[si].framed, 0);
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(c.grid[si].hd + L.h_recs, recs, size_t(count) * sizeof(hdfs_crc32c_packet),
+                           hipMemcpyDeviceToDeviceNoCU, c.r_stream);
+      if (e != hipSuccess) {
+        rc = fail(HDFS_CRC32C_EHIP, "record copy: %s", hipGetErrorString(e));
+        break;
+      }
     }
     if (verify) {
       // generic tiles: at most one per packet for chunk sizes the tiled
@@ -647,6 +662,10 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
   // records of every pass: written to pinned memory by frame_grid_kernel,
   // complete once the pass's summary was seen; copied out while the verify
   // kernels still run
+  if (c.grid_nocu && c.r_stream) {
+    hipError_t er = hipStreamSynchronize(c.r_stream);
+    if (!rc && er != hipSuccess) rc = fail(HDFS_CRC32C_EHIP, "record copy: %s", hipGetErrorString(er));
+  }
   const auto t1b = clk::now();
   if (!rc)
     for (const Pass &p : passes)
