@@ -1277,7 +1277,10 @@ DEV int grid_frame(const uint8_t *s, uint64_t len, uint64_t pos, const uint8_t *
   return frame::frame_step(fits ? win : s + pos, rem, pos, proto, cs, ctype, r, total);
 }
 
-constexpr uint32_t kGridBlock = 256;
+// 64 threads (one wave) per block: a pass of 16 K packets spreads over all
+// 256 CUs (the per-thread decode is a latency chain, so occupancy per CU
+// matters less than CUs engaged)
+constexpr uint32_t kGridBlock = 64;
 
 __global__ __launch_bounds__(kGridBlock) void frame_grid_kernel(
     const uint8_t *__restrict__ s, uint64_t len, uint64_t base, uint32_t count, int proto, uint32_t cs, int ctype,

@@ -467,7 +467,7 @@ struct GridLayout {
   size_t recs, status, contrib, blk_sum, blk_min, segs, seg2pkt, fb, sum, bad, ctr, bm, dtotal;  // device offsets
   size_t h_recs, h_sum, h_sum2, htotal;  // pinned offsets (h_sum2: summary after verify, then the bad list)
   GridLayout(uint32_t count, uint64_t bm_cap) {
-    const size_t nblk = (count + 255) / 256;
+    const size_t nblk = (count + 63) / 64;  // frame_grid_kernel blocks (kGridBlock)
     size_t o = 0;
     auto take = [&](size_t n) { const size_t at = o; o += align_up(n, 256); return at; };
     recs = take(size_t(count) * sizeof(hdfs_crc32c_packet));
@@ -581,24 +581,14 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
                                      copy_dst ? copy_dst + payload : nullptr, copy_dst ? copy_cap - payload : 0, gb,
                                      c.stream);
 
-    if (e != hipSuccess) {
-      rc = fail(HDFS_CRC32C_EHIP, "device framing: %s", hipGetErrorString(e));
-      break;
-    }
-    if (c.grid_nocu) {
-      // the run's records to pinned memory on a copy engine, concurrent with
-      // the verify kernel (a blit kernel would wait for it: it holds every CU)
+    if (e == hipSuccess && c.grid_nocu) {  // the tables are built: the record copy may start from here
       if (!c.r_stream) e = hipStreamCreateWithFlags(&c.r_stream, hipStreamNonBlocking);
       if (e == hipSuccess && !c.grid[si].framed) e = hipEventCreateWithFlags(&c.grid[si].framed, hipEventDisableTiming);
       if (e == hipSuccess) e = hipEventRecord(c.grid[si].framed, c.stream);
-      if (e == hipSuccess) e = hipStreamWaitEvent(c.r_stream, c.grid[si].framed, 0);
-      if (e == hipSuccess)
-        e = hipMemcpyAsync(c.grid[si].hd + L.h_recs, recs, size_t(count) * sizeof(hdfs_crc32c_packet),
-                           hipMemcpyDeviceToDeviceNoCU, c.r_stream);
-      if (e != hipSuccess) {
-        rc = fail(HDFS_CRC32C_EHIP, "record copy: %s", hipGetErrorString(e));
-        break;
-      }
+    }
+    if (e != hipSuccess) {
+      rc = fail(HDFS_CRC32C_EHIP, "device framing: %s", hipGetErrorString(e));
+      break;
     }
     if (verify) {
       // generic tiles: at most one per packet for chunk sizes the tiled
@@ -616,6 +606,19 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
                                   reinterpret_cast<const uint32_t *>(dg + L.fb), bad, count, sum, c.stream));
       HIPCHK(hipMemcpyAsync(hg + L.h_sum2, sum, 256 + size_t(std::min(kBadFirst, count)) * sizeof(GridBad),
                             hipMemcpyDeviceToHost, c.stream));
+    }
+    if (c.grid_nocu) {
+      // the run's records to pinned memory on a copy engine, concurrent with
+      // the verify kernel (a blit kernel would wait for it: it holds every
+      // CU); enqueued after the verify so the GPU gets that first
+      if (e == hipSuccess) e = hipStreamWaitEvent(c.r_stream, c.grid[si].framed, 0);
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(c.grid[si].hd + L.h_recs, recs, size_t(count) * sizeof(hdfs_crc32c_packet),
+                           hipMemcpyDeviceToDeviceNoCU, c.r_stream);
+      if (e != hipSuccess) {
+        rc = fail(HDFS_CRC32C_EHIP, "record copy: %s", hipGetErrorString(e));
+        break;
+      }
     }
     // the summary lands in pinned memory with its sequence number last: poll
     // it (a fault is caught by the stream synchronisation after 200 ms)
