@@ -153,7 +153,7 @@ struct DevCtx {
   };
   uint32_t grid_seq = 0;
   hipStream_t r_stream = nullptr;  // device framing: record copies on a copy engine
-  int grid_nocu = 1;               // 1: records by hipMemcpyDeviceToDeviceNoCU, 0: written by the kernel
+  int grid_nocu = 0;               // 1: records by hipMemcpyDeviceToDeviceNoCU, 0: written by the kernel
   std::vector<GridSlot> grid;
   std::mutex mu;
 };
