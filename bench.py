@@ -400,11 +400,18 @@ def main():
                     g = max(dg.probe_read(data.ptr, B * BLOCK, 2, stream) for _ in range(2))
                     cands[f"read probe {var} ({gpc}x{blk} per CU)"] = g
             dg.set_probe()
-            best = max(cands, key=cands.get)
-            ceiling = cands[best]
-            extra["ceiling_GBps"] = round(ceiling, 1)
-            extra["ceiling_source"] = best + " (libhadoofus_crc32c_diag.so, same process)"
             extra["ceiling_candidates_GBps"] = {k: round(v, 1) for k, v in cands.items()}
+            # a "ceiling" above the HBM spec means the diagnostic kernel skipped
+            # work (e.g. the compiler deleted unused loads): never report it
+            bad = {k for k, v in cands.items() if v > HBM_PEAK_GBPS}
+            if bad:
+                extra["ceiling_rejected_above_spec"] = sorted(bad)
+            cands = {k: v for k, v in cands.items() if k not in bad}
+            if cands:
+                best = max(cands, key=cands.get)
+                ceiling = cands[best]
+                extra["ceiling_GBps"] = round(ceiling, 1)
+                extra["ceiling_source"] = best + " (libhadoofus_crc32c_diag.so, same process)"
         except (ImportError, OSError) as e:
             extra["ceiling_error"] = str(e)[:200]
 

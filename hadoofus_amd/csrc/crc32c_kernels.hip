@@ -545,6 +545,25 @@ template <int MODE, int S, int COPY, int UNA>
 DEV void process(const uint32_t *lds, uint32_t (&d)[S][16], const uint32_t (&exp)[S], const uint32_t (&tl)[S],
                  const uint32_t (&sh_a)[S], const Cursor (&c)[S], SegP segs, uint32_t (&st)[S], const LaneConst &L,
                  uint32_t *__restrict__ first_bad, unsigned long long *__restrict__ mism, SegCache (&kc)[S]) {
+  if constexpr (kDiag && MODE == kModeLoadOnly) {
+    // Diagnostic twin of verify (diagnostic build only): the same loads and
+    // the same bitmap store op with its record dropped, no CRC arithmetic.
+    // The loaded words fold into st, and an impossible condition on st keeps
+    // them live (without it the compiler deletes the unused loads).
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+      uint32_t v = exp[s];
+#pragma unroll
+      for (int w = 0; w < 16; w++) v ^= d[s][w];
+      st[s] ^= v;
+      const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+          reinterpret_cast<uint8_t *>(rfl64(reinterpret_cast<uint64_t>(segs[c[s].seg].bitmap + c[s].tile))), 0, 0,
+          0x00020000);
+      __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(st[s]), rb, 0u, 0, 0);
+      if (st[s] == 0x9E3779B9u && c[s].r == 0xFFFFFFFFu) atomicAdd(mism, 1ull);
+    }
+    return;
+  }
   if constexpr (COPY && !UNA) {
 #pragma unroll
     for (int s = 0; s < S; s++) copy_round(d[s], c[s], segs, L, kc[s]);
