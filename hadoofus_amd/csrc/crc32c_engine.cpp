@@ -220,13 +220,24 @@ bool device_accessible(const void *p) {
 int launch_verify_dyn(DevCtx &c, const SegDev *d_segs, const GridSummary *dyn, uint64_t gtiles_ub, uint32_t *d_fb,
                       unsigned long long *d_mism, uint32_t *d_gctr, hipStream_t st, int ctype, bool copy) {
   (void)d_gctr;  // zeroed by grid_build_kernel
-  const hipError_t le = launch_tiles(kModeVerify, 2, std::min(g_nt_loads, 1), 3, 1, 1024, c.num_cu, d_segs, 0, 0, 0,
-                                     c.d_tab_main_t[ctype], d_fb, d_mism, nullptr, g_group_shift << 8, d_gctr, st,
-                                     copy ? 1 : 0, 1, dyn);
+  // schedule 3: a device-framed run is packets of one wire size, so its table
+  // is uniform (dyn->utiles, no segment search per tile); the kernel falls
+  // back to searching the table when it is not
+  const hipError_t le = launch_tiles(kModeVerify, 3, g_nt_loads, 3, 1, 1024, c.num_cu, d_segs, 0, 0, 0,
+                                     c.d_tab_main_t[ctype], d_fb, d_mism, nullptr,
+                                     (g_group_shift << 8) | (g_xcd_major << 12), d_gctr, st, copy ? 1 : 0, 1, dyn);
   if (le == hipErrorInvalidValue) return fail(HDFS_CRC32C_EINVAL, "verify kernel shape not built");
   HIPCHK(le);
   HIPCHK(launch_generic(kModeVerify, d_segs, 0, gtiles_ub, c.d_tab_main_t[ctype], d_fb, d_mism, st, dyn));
   return HDFS_CRC32C_OK;
+}
+
+uint32_t uniform_tiles(const SegDev *segs, size_t n) {
+  if (!n || !segs[0].main_tiles) return 0;
+  const uint32_t T = segs[0].main_tiles;
+  for (size_t i = 1; i < n; i++)
+    if (i + 1 < n ? segs[i].main_tiles != T : segs[i].main_tiles > T) return 0;
+  return T;
 }
 
 bool any_unaligned(const SegDev *segs, size_t n) {
@@ -243,7 +254,7 @@ static const int g_small_rule = HDFS_KNOB("HDFS_CRC32C_SMALL_RULE", 1);
 int launch_all(DevCtx &c, int mode, const SegDev *d_segs, uint32_t nseg, uint64_t rounds,
                uint64_t mtiles, uint64_t gtiles, uint32_t *d_fb, unsigned long long *d_mism,
                uint32_t *d_gctr, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1, bool reset, int ctype, bool copy,
-               bool gctr_zeroed, bool una) {
+               bool gctr_zeroed, bool una, uint32_t utiles) {
   const bool vreset = mode == kModeVerify && reset;
   uint32_t *gz = (rounds && g_tile_order >= 2 && !gctr_zeroed) ? d_gctr : nullptr;
   if (vreset || gz)
@@ -256,8 +267,9 @@ int launch_all(DevCtx &c, int mode, const SegDev *d_segs, uint32_t nseg, uint64_
     if (ev0) HIPCHK(hipEventRecord(ev0, st));
     // The interleaved schedule (3) pays a segment look-up whenever a strided
     // tile leaves the current segment: small launches (which also skip the
-    // pool) and tables of small segments keep the contiguous slices (2).
-    const bool small = rounds < 32ull * 16u * uint64_t(grid) || mtiles < 2ull * uint64_t(grid) * nseg;
+    // pool) and tables of small segments keep the contiguous slices (2) --
+    // unless the table is uniform, where the look-up is a division.
+    const bool small = rounds < 32ull * 16u * uint64_t(grid) || (!utiles && mtiles < 2ull * uint64_t(grid) * nseg);
     const bool to_small = g_tile_order == 3 && small && g_small_rule;
     const int order = to_small ? 2 : g_tile_order;
     // buffer loads (nt 2) exist for schedule 3 only; the others use nontemporal global loads
@@ -269,7 +281,7 @@ int launch_all(DevCtx &c, int mode, const SegDev *d_segs, uint32_t nseg, uint64_
     const hipError_t le = launch_tiles(kmode, order, nt, depth, streams, block, grid, d_segs, nseg, rounds,
                                        mtiles, c.d_tab_main_t[ctype], d_fb, d_mism, kDiag ? g_diag : nullptr,
                                        (kDiag ? g_store_policy : 0u) | (g_group_shift << 8) | (g_xcd_major << 12),
-                                       d_gctr, st, copy ? 1 : 0, una ? 1 : 0);
+                                       d_gctr, st, copy ? 1 : 0, una ? 1 : 0, nullptr, order == 3 ? utiles : 0u);
     if (le == hipErrorInvalidValue)
       return fail(HDFS_CRC32C_EINVAL, "tiled kernel shape (order %d, nt %d, depth %d, streams %d, block %d) is not built",
                   order, nt, depth, streams, block);
@@ -628,6 +640,7 @@ struct hdfs_crc32c_plan {
   uint64_t rounds = 0, mtiles = 0, gtiles = 0, main_bytes = 0, gen_bytes = 0, nchunks = 0;
   bool timing = false;
   bool una = false;  // some tiled segment's data is not 4-B aligned
+  uint32_t utiles = 0;  // uniform table: main tiles per segment
   std::vector<std::pair<hipEvent_t, hipEvent_t>> events;  // pre-created pool
   size_t next_event = 0;
 };
@@ -749,6 +762,7 @@ int hdfs_crc32c_plan_create(hdfs_crc32c_plan **plan, int mode, const hdfs_crc32c
   p->gen_bytes = gen_bytes;
   p->nchunks = nch;
   p->una = any_unaligned(host.data(), nseg);
+  p->utiles = uniform_tiles(host.data(), nseg);
   hipError_t e = hipMalloc(&p->d_segs, sizeof(SegDev) * host.size());
   if (e == hipSuccess) e = hipMemcpy(p->d_segs, host.data(), sizeof(SegDev) * host.size(), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMalloc(&p->d_first_bad, sizeof(uint32_t) * host.size());
@@ -780,7 +794,7 @@ int hdfs_crc32c_plan_execute(hdfs_crc32c_plan *p, void *stream) {
     p->next_event++;
   }
   return launch_all(c, p->mode, p->d_segs, p->nseg, p->rounds, p->mtiles, p->gtiles, p->d_first_bad,
-                    p->d_mism, p->d_gctr, st, e0, e1, true, p->ctype, false, false, p->una);
+                    p->d_mism, p->d_gctr, st, e0, e1, true, p->ctype, false, false, p->una, p->utiles);
 }
 
 int hdfs_crc32c_plan_results(hdfs_crc32c_plan *p, void *stream, uint32_t *first_bad, size_t nseg,

@@ -20,7 +20,7 @@ hipError_t launch_tiles(int mode, int order, int nt, int depth, int streams, int
                         const SegDev *segs, uint32_t nseg, uint64_t total_rounds, uint64_t total_tiles,
                         const uint32_t *gtab, uint32_t *first_bad, unsigned long long *mism,
                         unsigned long long *diag, uint32_t tune, uint32_t *gctr, hipStream_t stream,
-                        int copy = 0, int una = 0, const GridSummary *dyn = nullptr);
+                        int copy = 0, int una = 0, const GridSummary *dyn = nullptr, uint32_t utiles = 0);
 hipError_t launch_probe_read(const uint8_t *p, uint64_t nbytes, uint32_t *out, int grid, int block, int variant,
                              hipStream_t stream);
 hipError_t launch_generic(int mode, const SegDev *segs, uint32_t nseg, uint64_t total_gtiles,
@@ -143,17 +143,16 @@ struct DevCtx {
   hipStream_t v_stream = nullptr;
   // device framing passes (guarded by mu): device tables of one pass
   // (records | status | segments | seg2pkt | first-bad | summary | bad list |
-  // counters | bitmaps) and its pinned host landing area (records | summary
-  // after framing | summary after verify | bad list)
+  // counters | exceptions | bitmaps) and its pinned host landing area
+  // (summary + packet 0 + exceptions after framing | summary after verify |
+  // bad list)
   struct GridSlot {
     uint8_t *d = nullptr, *h = nullptr;
     size_t dcap = 0, hcap = 0;
-    hipEvent_t framed = nullptr;  // the pass's segment table is built (c.stream -> c.v_stream)
-    uint8_t *hd = nullptr;        // device address of h (coherent, mapped)
+    uint8_t *hd = nullptr;  // device address of h (coherent, mapped)
   };
   uint32_t grid_seq = 0;
-  hipStream_t r_stream = nullptr;  // device framing: record copies on a copy engine
-  int grid_nocu = 0;               // 1: records by hipMemcpyDeviceToDeviceNoCU, 0: written by the kernel
+  hipStream_t r_stream = nullptr;  // device framing: record copies of runs with many exceptions
   std::vector<GridSlot> grid;
   std::mutex mu;
 };
@@ -185,10 +184,14 @@ bool is_pinned_host(const void *p);
 int launch_all(DevCtx &c, int mode, const SegDev *d_segs, uint32_t nseg, uint64_t rounds, uint64_t mtiles,
                uint64_t gtiles, uint32_t *d_fb, unsigned long long *d_mism, uint32_t *d_gctr, hipStream_t st,
                hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, bool reset = true, int ctype = 0,
-               bool copy = false, bool gctr_zeroed = false, bool una = false);
+               bool copy = false, bool gctr_zeroed = false, bool una = false, uint32_t utiles = 0);
+// Main tiles per segment when the table is uniform (every segment but the
+// last has the same main_tiles T, the last at most T), else 0.
+uint32_t uniform_tiles(const SegDev *segs, size_t n);
 // Verify pass over a segment table built on the device (grid_build_kernel):
 // sizes read by the kernels from *dyn; grid sized for rounds_ub / gtiles_ub
-// (upper bounds).  Schedule 2 (packet tables), realigning kernel.
+// (upper bounds).  Schedule 3 with the uniform-table look-up the summary
+// enables for runs of equal packets, realigning kernel.
 int launch_verify_dyn(DevCtx &c, const SegDev *d_segs, const GridSummary *dyn, uint64_t gtiles_ub, uint32_t *d_fb,
                       unsigned long long *d_mism, uint32_t *d_gctr, hipStream_t st, int ctype, bool copy);
 // Any segment whose data is not 4-B aligned (selects the realigning kernel).

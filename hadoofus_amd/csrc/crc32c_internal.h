@@ -77,8 +77,24 @@ struct GridSummary {
   uint32_t nbad;         // verify: packets with bad chunks (grid_finalize_kernel)
   uint32_t unaligned;    // some tiled segment's data is not 4-B aligned (realigning kernel)
   uint32_t seq;          // host copy only: written last (after a system fence) by grid_build_kernel
-  uint32_t pad;
+  uint32_t nonuni;       // some segment breaks the uniform layout (OR-ed by grid_build_kernel)
+  uint32_t utiles;       // main tiles per segment of a uniform table (0: not uniform), for the verify kernel
+  uint32_t nexc;         // recorded packets whose record differs from the prediction from packet 0
 };
+// Records of a device-framed run reach the host as packet 0's record plus
+// the packets that differ from the prediction from it (stream_off + k *
+// stride, offsetInBlock + k * dataLen, seqno + k, every other field equal):
+// up to kExcMax of them land in pinned memory with the summary, the host
+// synthesises the rest.  Host area after the 256-B summary:
+//   [kGridHostRec0]  packet 0's record
+//   [kGridHostIdx]   kExcMax u32 grid indices of the exceptions
+//   [kGridHostExc]   kExcMax records of the exceptions
+constexpr uint32_t kExcMax = 64;
+constexpr uint32_t kGridRecBytes = 56;  // sizeof(hdfs_crc32c_packet), checked where it is complete
+constexpr uint32_t kGridHostRec0 = 256;
+constexpr uint32_t kGridHostIdx = kGridHostRec0 + 64;
+constexpr uint32_t kGridHostExc = kGridHostIdx + kExcMax * 4;
+constexpr uint32_t kGridHostBytes = kGridHostExc + kExcMax * kGridRecBytes;
 // Device tables of one framing pass (count grid points).
 struct GridBufs {
   ::hdfs_crc32c_packet *recs;  // [count] records
@@ -90,13 +106,15 @@ struct GridBufs {
   uint32_t *seg2pkt;           // [count] segment -> grid point
   uint32_t *fb;                // [count] first bad chunk per segment
   uint32_t *gctr;              // tiled-kernel pool counter (zeroed by grid_build_kernel)
+  uint32_t *done;              // [2]: grid_build blocks finished, exceptions found (zeroed by frame_grid_kernel)
+  uint32_t *exc;               // [count] grid indices of the exceptions
   GridSummary *sum;
-  // pinned host memory mapped into the device: the records and the summary
-  // are written there by the kernels themselves (no copy launches, which
-  // would queue behind the verify kernel for CUs)
-  ::hdfs_crc32c_packet *hrecs;
-  GridSummary *hsum;
-  uint32_t seq;                // written to hsum->seq once hsum is complete
+  // pinned host memory mapped into the device: the summary, packet 0's
+  // record and the exceptions (kGridHost*) are written there by the last
+  // grid_build block (no copy launch, which would queue behind the verify
+  // kernel for CUs)
+  uint8_t *hsum;
+  uint32_t seq;                // written to the host summary's seq once the area is complete
 };
 
 // Compact verify verdict of one packet (grid_finalize_kernel).

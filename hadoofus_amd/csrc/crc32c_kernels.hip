@@ -203,7 +203,19 @@ struct Sched {
   uint32_t ushift;   // ORDER 2/3: log2 tiles per pool unit
   uint32_t gstride;  // ORDER 3: group stride of the static phase (gridDim)
   uint32_t gshift;   // ORDER 3: log2 tiles per group
+  // Uniform tables (ut != 0): segment s holds global main tiles [s*ut, s*ut +
+  // main_tiles_s) with main_tiles_s == ut for every segment but the last (the
+  // packets of a block transfer).  A tile's segment is then g / ut -- a shift
+  // (ush) or a multiply-high by um = floor(2^64 / ut) + 1, exact for g < 2^32
+  // -- instead of a binary search of the table.
+  uint32_t ut, ush;
+  uint64_t um;
 };
+
+DEV Cursor ulocate(const Sched &w, uint64_t g) {
+  const uint32_t s = w.ush != 0xFFFFFFFFu ? static_cast<uint32_t>(g >> w.ush) : static_cast<uint32_t>(__umul64hi(g, w.um));
+  return Cursor{rfl(s), rfl(static_cast<uint32_t>(g - uint64_t(s) * w.ut)), 0u, true};
+}
 
 DEV uint32_t grab(const Sched &w) {
   uint32_t k = 0;
@@ -270,6 +282,7 @@ DEV Cursor advance(Cursor c, SegP segs, uint32_t nseg, const Sched &w, SegCache 
     // the pool cost 8x the whole kernel, tools/exp_packet_tables.py);
     // interleaved tiles jump G ahead.  Short hops walk, long ones search.
     const uint64_t end = sh.mtile_start + sh.main_tiles;
+    if (w.ut && (g < sh.mtile_start || g >= end)) return ulocate(w, g);
     if (g < sh.mtile_start || g >= end + (ORDER == 3 ? 0u : kWalkTiles)) {
       uint32_t lo = 0, hi = nseg;
       while (hi - lo > 1) {
@@ -513,33 +526,10 @@ DEV void copy_round(const uint32_t (&d)[16], const Cursor c, SegP segs, const La
   }
 }
 
-DEV void copy_quads(const uint32_t (&d)[16], const Cursor c, SegP segs, const LaneConst &L, SegCache &kc) {
-  const SegHot &sh = hot(kc, segs, c.seg).h;
-  const uint32_t cs = sh.chunk_size;
-  uint8_t *dst = segs[c.seg].copy_dst;
-  const uint32_t nch = min(kTileChunks, sh.nchunks - c.tile * kTileChunks);
-  const bool ok = c.valid && dst != nullptr;
-  uint8_t *base = ok ? dst + static_cast<uint64_t>(c.tile) * kTileChunks * cs + static_cast<uint64_t>(c.r) * kRoundBytes
-                     : dst;
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-      reinterpret_cast<uint8_t *>(rfl64(reinterpret_cast<uint64_t>(base))), 0,
-      static_cast<int>(rfl(ok ? (nch - 1u) * cs + kRoundBytes : 0u)), 0x00020000);
-  const uint32_t off = L.qg * cs + 64u * L.qi;
-#pragma unroll
-  for (int m = 0; m < 4; m++) {
-    const u32x4 v = {d[4 * m + 0], d[4 * m + 1], d[4 * m + 2], d[4 * m + 3]};
-    __builtin_amdgcn_raw_buffer_store_b128(v, rs, off + 16u * m, 0, 0);
-  }
-}
-
 // Process one round of each of the wave's S streams (d[s] for cursor c[s]);
 // st[s] is stream s's running lane register across the rounds of a tile.
 // The S slicing chains are independent and interleaved step by step, so one
 // lane keeps S table lookups in flight (latency hiding by ILP, not waves).
-// Verify + copy-out of realigned (UNA) rounds: after the transpose lane L
-// holds the 64 bytes of quad L (chunk L >> 3, position L & 7), written with
-// four 16-B stores.
-DEV void copy_quads(const uint32_t (&d)[16], const Cursor c, SegP segs, const LaneConst &L, SegCache &kc);
 
 template <int MODE, int S, int COPY, int UNA>
 DEV void process(const uint32_t *lds, uint32_t (&d)[S][16], const uint32_t (&exp)[S], const uint32_t (&tl)[S],
@@ -581,7 +571,16 @@ DEV void process(const uint32_t *lds, uint32_t (&d)[S][16], const uint32_t (&exp
 #pragma unroll
       for (int j = 0; j < 15; j++) d[s][j] = __builtin_amdgcn_alignbyte(d[s][j + 1], d[s][j], a);
       d[s][15] = __builtin_amdgcn_alignbyte(w16, d[s][15], a);
-      if constexpr (COPY) copy_quads(d[s], c[s], segs, L, kc[s]);
+      if constexpr (COPY) {
+        // the transpose is an involution: applied to the realigned quads it
+        // gives back the loaded lane order, so the copy goes out as four fully
+        // coalesced 1 KiB stores (quad-order stores touch 4x the lines each)
+        uint32_t e[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) e[j] = d[s][j];
+        transpose(e);
+        copy_round(e, c[s], segs, L, kc[s]);
+      }
     }
     const uint32_t ri = hot(kc[s], segs, c[s].seg).reg_init;  // uniform control flow: kc stays in SGPRs
     if (c[s].r == 0) st[s] = (L.qi == 0) ? ri : 0u;
@@ -609,7 +608,7 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
     const SegDev *__restrict__ segs, uint32_t nseg, uint64_t total_rounds, uint64_t total_tiles,
     const uint32_t *__restrict__ gtab, uint32_t *__restrict__ first_bad,
     unsigned long long *__restrict__ mism, unsigned long long *__restrict__ diag, uint32_t tune,
-    uint32_t *__restrict__ gctr, const GridSummary *__restrict__ dyn) {
+    uint32_t *__restrict__ gctr, const GridSummary *__restrict__ dyn, uint32_t utiles) {
   static_assert(ORDER != 0 || S == 1, "static per-wave slices serve one stream");
   static_assert(DEPTH >= 2 && DEPTH <= 4 && S >= 1 && S <= 4, "shape");
   // dyn: sizes of a segment table built on the device (grid_build_kernel),
@@ -619,6 +618,7 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
     nseg = dyn->nseg;
     total_rounds = dyn->rounds;
     total_tiles = dyn->mtiles;
+    utiles = dyn->utiles;
   }
   // + ticket counter, pad, kSlots 64-bit pool slots
   __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords + 2 + 2 * kSlots];
@@ -683,6 +683,10 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
   if (kDiag && diag && L.lane == 0) diag[3 * wave] = __builtin_amdgcn_s_memrealtime();
   uint64_t nrounds = 0;
   Sched w{0, 0, 0, &lds[kLdsWords], L.lane};
+  w.ut = utiles;
+  w.ush = (utiles & (utiles - 1u)) == 0u ? static_cast<uint32_t>(__builtin_ctz(utiles | (utiles == 0u ? 1u : 0u)))
+                                         : 0xFFFFFFFFu;
+  w.um = (utiles && w.ush == 0xFFFFFFFFu) ? ~0ull / utiles + 1ull : 0ull;
   Cursor cur[DEPTH][S];
 #pragma unroll
   for (int s = 0; s < S; s++) cur[0][s] = Cursor{0u, 0u, 0u, false};
@@ -740,12 +744,16 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
     for (int s = 0; s < S; s++) {
       uint64_t g;
       if (ticket_tile<ORDER>(w, grab(w), g)) {
-        uint32_t lo = 0, hi = nseg;
-        while (hi - lo > 1) {
-          const uint32_t mid = (lo + hi) >> 1;
-          if (sg[mid].mtile_start <= g) lo = mid; else hi = mid;
+        if (w.ut) {
+          cur[0][s] = ulocate(w, g);
+        } else {
+          uint32_t lo = 0, hi = nseg;
+          while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (sg[mid].mtile_start <= g) lo = mid; else hi = mid;
+          }
+          cur[0][s] = locate(sg, lo, g);
         }
-        cur[0][s] = locate(sg, lo, g);
       }
     }
   }
@@ -1305,11 +1313,8 @@ __global__ __launch_bounds__(kGridBlock) void frame_grid_kernel(
     const uint8_t *__restrict__ s, uint64_t len, uint64_t base, uint32_t count, int proto, uint32_t cs, int ctype,
     int verify, hdfs_crc32c_packet *__restrict__ recs, uint32_t *__restrict__ status,
     GridContrib *__restrict__ contrib, uint64_t *__restrict__ blk_sum, uint32_t *__restrict__ blk_min,
-    GridSummary *__restrict__ sum, hdfs_crc32c_packet *__restrict__ hrecs) {
+    GridSummary *__restrict__ sum, uint32_t *__restrict__ done) {
   __shared__ __attribute__((aligned(16))) uint8_t win[kGridBlock][kHdrWin];
-  // the block's records, staged so the host copy goes out as contiguous
-  // 16-B stores (whole lines over PCIe) instead of one 56-B record per lane
-  __shared__ __attribute__((aligned(16))) hdfs_crc32c_packet srec[kGridBlock];
   __shared__ uint64_t red[6][kGridBlock / 64];
   __shared__ uint32_t redm[kGridBlock / 64];
   const uint32_t t = threadIdx.x, k = blockIdx.x * kGridBlock + t, lane = t & 63u, w = t >> 6;
@@ -1329,6 +1334,9 @@ __global__ __launch_bounds__(kGridBlock) void frame_grid_kernel(
   if (k == 0) {
     sum->stride = stride;
     sum->unaligned = 0u;  // OR-ed by grid_build_kernel
+    sum->nonuni = 0u;     // OR-ed by grid_build_kernel
+    done[0] = 0u;         // grid_build_kernel: blocks finished
+    done[1] = 0u;         // grid_build_kernel: exceptions found
   }
   hdfs_crc32c_packet r{};
   uint64_t total = 0;
@@ -1352,21 +1360,6 @@ __global__ __launch_bounds__(kGridBlock) void frame_grid_kernel(
   if (k < count) {
     status[k] = code;
     contrib[k] = a;
-  }
-  if (hrecs) {
-    // the caller's copy straight to pinned host memory, through LDS as
-    // contiguous 16-B stores (null: the host copies the records with a
-    // copy engine instead, off the CUs)
-    srec[t] = r;  // (garbage past the run's end: the host reads only recorded packets)
-    __syncthreads();
-    static_assert((kGridBlock * sizeof(hdfs_crc32c_packet)) % 16 == 0, "16-B record copy");
-    // rounded up: the last store may run 8 B past the block's last record
-    // (still inside the host area, whose record array is padded to 256 B)
-    const uint32_t nrec = min(kGridBlock, count - blockIdx.x * kGridBlock);
-    const uint32_t nvec = (nrec * uint32_t(sizeof(hdfs_crc32c_packet)) + 15u) / 16u;
-    const u32x4 *src = reinterpret_cast<const u32x4 *>(srec);
-    auto *dst = reinterpret_cast<u32x4 *>(hrecs + size_t(blockIdx.x) * kGridBlock);
-    for (uint32_t i = t; i < nvec; i += kGridBlock) dst[i] = src[i];
   }
   // block sums of the shares and the block's first grid point that is not On
   uint64_t v[6] = {a.nseg, a.rounds, a.mtiles, a.gtiles, a.bm, a.payload};
@@ -1404,11 +1397,13 @@ __global__ __launch_bounds__(kGridBlock) void grid_build_kernel(
     const GridContrib *__restrict__ contrib, const uint64_t *__restrict__ blk_sum,
     const uint32_t *__restrict__ blk_min, uint32_t cs, uint32_t sflags, uint8_t *__restrict__ bm_base,
     uint8_t *__restrict__ copy_base, uint64_t copy_cap, SegDev *__restrict__ segs, uint32_t *__restrict__ seg2pkt,
-    uint32_t *__restrict__ fb, uint32_t *__restrict__ gctr, GridSummary *__restrict__ sum,
-    GridSummary *__restrict__ hsum, uint32_t seq) {
+    uint32_t *__restrict__ fb, uint32_t *__restrict__ gctr, uint32_t *__restrict__ done, uint32_t *__restrict__ exc,
+    GridSummary *__restrict__ sum, uint8_t *__restrict__ hsum, uint32_t seq) {
+  static_assert(sizeof(hdfs_crc32c_packet) == kGridRecBytes, "host record layout");
   __shared__ uint64_t red[6][kGridBlock / 64];
   __shared__ uint32_t redm[kGridBlock / 64];
   __shared__ uint64_t pre[6];
+  __shared__ uint32_t islast;
   const uint32_t t = threadIdx.x, b = blockIdx.x, k = b * kGridBlock + t, lane = t & 63u, w = t >> 6;
   // 1. the run's end: the first grid point that is not On, over all blocks
   uint32_t m = 0xFFFFFFFFu;
@@ -1441,102 +1436,154 @@ __global__ __launch_bounds__(kGridBlock) void grid_build_kernel(
   const uint32_t st_fb = fbk < count ? status[fbk] : uint32_t(kGridOn);
   const uint32_t recorded = fbk + (fbk < count && st_fb != kGridMore ? 1u : 0u);
   const uint32_t last = recorded ? recorded - 1u : 0u;  // the packet whose block writes the summary
-  if (b * kGridBlock > last) return;  // uniform per block: nothing of this run here
-  __syncthreads();
-  // 3. in-block exclusive scan of the shares of recorded packets
-  const GridContrib a = k < recorded ? contrib[k] : GridContrib{0u, 0u, 0u, 0u, 0u, 0u};
-  uint64_t incl[6] = {a.nseg, a.rounds, a.mtiles, a.gtiles, a.bm, a.payload};
-  const uint64_t own[6] = {a.nseg, a.rounds, a.mtiles, a.gtiles, a.bm, a.payload};
+  // the first segment's main tiles: the uniform layout's tiles per segment
+  // (a run with any segment has one at packet 0: a packet without CRCs ends it)
+  const GridContrib c0 = contrib[0];
+  const uint32_t T = c0.nseg ? c0.mtiles : 0u;
+  if (b * kGridBlock <= last) {  // uniform per block: blocks past the run only count themselves done
+    __syncthreads();
+    // 3. in-block exclusive scan of the shares of recorded packets
+    const GridContrib a = k < recorded ? contrib[k] : GridContrib{0u, 0u, 0u, 0u, 0u, 0u};
+    uint64_t incl[6] = {a.nseg, a.rounds, a.mtiles, a.gtiles, a.bm, a.payload};
+    const uint64_t own[6] = {a.nseg, a.rounds, a.mtiles, a.gtiles, a.bm, a.payload};
 #pragma unroll
-  for (int q = 0; q < 6; q++) {
+    for (int q = 0; q < 6; q++) {
 #pragma unroll
-    for (uint32_t off = 1; off < 64; off <<= 1) {
-      const uint64_t o = __shfl_up(incl[q], off);
-      if (lane >= off) incl[q] += o;
+      for (uint32_t off = 1; off < 64; off <<= 1) {
+        const uint64_t o = __shfl_up(incl[q], off);
+        if (lane >= off) incl[q] += o;
+      }
+    }
+    __syncthreads();
+    if (lane == 63) {
+#pragma unroll
+      for (int q = 0; q < 6; q++) red[q][w] = incl[q];
+    }
+    __syncthreads();
+    uint64_t ex[6];
+#pragma unroll
+    for (int q = 0; q < 6; q++) {
+      ex[q] = pre[q] + incl[q] - own[q];
+      for (uint32_t j = 0; j < w; j++) ex[q] += red[q][j];
+    }
+    const hdfs_crc32c_packet r = k < recorded ? recs[k] : hdfs_crc32c_packet{};
+    // 4. the segment entry of a recorded packet with CRCs
+    if (k < recorded && a.nseg) {
+      const uint32_t nch = uint32_t(r.crc_len) / 4u, ntiles = (nch + 7u) / 8u;
+      const uint32_t sg = static_cast<uint32_t>(ex[0]);
+      const uint8_t *crcp = s + r.stream_off + r.header_len;
+      SegDev d;
+      d.data = crcp + r.crc_len;
+      d.crcs = reinterpret_cast<uint32_t *>(const_cast<uint8_t *>(crcp));
+      d.bitmap = bm_base + ex[4];
+      d.mtile_start = ex[2];
+      d.chunk_size = cs;
+      d.flags = sflags;
+      d.nchunks = nch;
+      d.main_tiles = a.mtiles;
+      d.reg_init = 0xFFFFFFFFu;
+      d.gen_tiles = ntiles - a.mtiles;
+      d.len = uint64_t(r.data_len);
+      d.round_start = ex[1];
+      d.gtile_start = ex[3];
+      // never past the caller's buffer: a packet that does not fit is not copied
+      // (the host sees the run's payload exceed the capacity and fails the call)
+      d.copy_dst = copy_base && ex[5] + own[5] <= copy_cap ? copy_base + ex[5] : nullptr;
+      d.reserved = 0;
+      segs[sg] = d;
+      seg2pkt[sg] = k;
+      fb[sg] = 0xFFFFFFFFu;
+    }
+    // one atomic per wave that has a byte-unaligned tiled segment / a segment
+    // off the uniform layout (per-thread atomics on one word serialise: 16 K of
+    // them cost ~150 us)
+    {
+      const bool una = k < recorded && a.nseg && a.mtiles &&
+                       ((reinterpret_cast<uintptr_t>(s) + r.stream_off + r.header_len + uint32_t(r.crc_len)) & 3u);
+      if (__ballot(una) && lane == 0) atomicOr(&sum->unaligned, 1u);
+      const bool off_layout = k < recorded && a.nseg && (ex[2] != ex[0] * T || a.mtiles > T);
+      if (__ballot(off_layout) && lane == 0) atomicOr(&sum->nonuni, 1u);
+    }
+    // 5. records that differ from the prediction from packet 0 (wave-aggregated slots)
+    {
+      const uint64_t stride = sum->stride;
+      bool diff = false;
+      if (k >= 1 && k < recorded) {
+        hdfs_crc32c_packet p = recs[0];
+        p.stream_off = base + uint64_t(k) * stride;
+        p.offset_in_block += int64_t(k) * p.data_len;
+        p.seqno += int64_t(k);
+        const uint64_t *x = reinterpret_cast<const uint64_t *>(&p), *y = reinterpret_cast<const uint64_t *>(&r);
+#pragma unroll
+        for (int q = 0; q < int(kGridRecBytes / 8); q++) diff |= x[q] != y[q];
+      }
+      const uint64_t bal = __ballot(diff);
+      uint32_t at = 0;
+      if (lane == 0 && bal) at = atomicAdd(&done[1], static_cast<uint32_t>(__builtin_popcountll(bal)));
+      at = static_cast<uint32_t>(__shfl(static_cast<int>(at), 0));
+      if (diff) exc[at + static_cast<uint32_t>(__builtin_popcountll(bal & ((1ull << lane) - 1ull)))] = k;
+    }
+    // 6. the summary, from the thread of the run's last packet
+    if (k == last) {
+      const uint64_t stride = sum->stride;
+      uint64_t consumed, next;
+      if (fbk == count) {
+        consumed = next = base + uint64_t(count) * stride;
+      } else if (st_fb == kGridMore) {
+        consumed = next = base + uint64_t(fbk) * stride;
+      } else {
+        const hdfs_crc32c_packet &rf = recs[fbk];
+        next = rf.stream_off + rf.header_len + uint64_t(rf.crc_len) + uint64_t(rf.data_len);
+        consumed = rf.error ? base + uint64_t(fbk) * stride : next;
+      }
+      const bool any = recorded > 0;
+      sum->first_break = fbk;
+      sum->recorded = recorded;
+      sum->last_status = st_fb;
+      sum->nseg = any ? static_cast<uint32_t>(ex[0] + own[0]) : 0u;
+      sum->rounds = any ? ex[1] + own[1] : 0u;
+      sum->mtiles = any ? ex[2] + own[2] : 0u;
+      sum->gtiles = any ? ex[3] + own[3] : 0u;
+      sum->bm_bytes = any ? ex[4] + own[4] : 0u;
+      sum->payload = any ? ex[5] + own[5] : 0u;
+      sum->consumed = consumed;
+      sum->next_pos = next;
+      sum->nbad = 0;
+      *gctr = 0u;  // the verify launch's pool counter (no separate reset launch)
     }
   }
+  // 7. the last block to finish publishes the summary, packet 0's record and
+  // the exceptions to pinned host memory, then (one system-scope fence later)
+  // the sequence number the host polls.  Every thread fences its own stores
+  // before the block counts itself done.
+  __threadfence();
   __syncthreads();
-  if (lane == 63) {
-#pragma unroll
-    for (int q = 0; q < 6; q++) red[q][w] = incl[q];
-  }
+  if (t == 0) islast = atomicAdd(&done[0], 1u) == nblk - 1u ? 1u : 0u;
   __syncthreads();
-  uint64_t ex[6];
-#pragma unroll
-  for (int q = 0; q < 6; q++) {
-    ex[q] = pre[q] + incl[q] - own[q];
-    for (uint32_t j = 0; j < w; j++) ex[q] += red[q][j];
-  }
-  // 4. the segment entry of a recorded packet with CRCs
-  if (k < recorded && a.nseg) {
-    const hdfs_crc32c_packet r = recs[k];
-    const uint32_t nch = uint32_t(r.crc_len) / 4u, ntiles = (nch + 7u) / 8u;
-    const uint32_t sg = static_cast<uint32_t>(ex[0]);
-    const uint8_t *crcp = s + r.stream_off + r.header_len;
-    SegDev d;
-    d.data = crcp + r.crc_len;
-    d.crcs = reinterpret_cast<uint32_t *>(const_cast<uint8_t *>(crcp));
-    d.bitmap = bm_base + ex[4];
-    d.mtile_start = ex[2];
-    d.chunk_size = cs;
-    d.flags = sflags;
-    d.nchunks = nch;
-    d.main_tiles = a.mtiles;
-    d.reg_init = 0xFFFFFFFFu;
-    d.gen_tiles = ntiles - a.mtiles;
-    d.len = uint64_t(r.data_len);
-    d.round_start = ex[1];
-    d.gtile_start = ex[3];
-    // never past the caller's buffer: a packet that does not fit is not copied
-    // (the host sees the run's payload exceed the capacity and fails the call)
-    d.copy_dst = copy_base && ex[5] + own[5] <= copy_cap ? copy_base + ex[5] : nullptr;
-    d.reserved = 0;
-    segs[sg] = d;
-    seg2pkt[sg] = k;
-    fb[sg] = 0xFFFFFFFFu;
-  }
-  // one atomic per wave that has a byte-unaligned tiled segment (per-thread
-  // atomics on one word serialise: 16 K of them cost ~150 us)
-  {
-    const bool una = k < recorded && a.nseg && a.mtiles &&
-                     ((reinterpret_cast<uintptr_t>(s) + recs[k].stream_off + recs[k].header_len + uint32_t(recs[k].crc_len)) & 3u);
-    if (__ballot(una) && lane == 0) atomicOr(&sum->unaligned, 1u);
-  }
-  // 5. the summary, from the thread of the run's last packet
-  if (k == last) {
-    const uint64_t stride = sum->stride;
-    uint64_t consumed, next;
-    if (fbk == count) {
-      consumed = next = base + uint64_t(count) * stride;
-    } else if (st_fb == kGridMore) {
-      consumed = next = base + uint64_t(fbk) * stride;
-    } else {
-      const hdfs_crc32c_packet &r = recs[fbk];
-      next = r.stream_off + r.header_len + uint64_t(r.crc_len) + uint64_t(r.data_len);
-      consumed = r.error ? base + uint64_t(fbk) * stride : next;
-    }
-    const bool any = recorded > 0;
-    sum->first_break = fbk;
-    sum->recorded = recorded;
-    sum->last_status = st_fb;
-    sum->nseg = any ? static_cast<uint32_t>(ex[0] + own[0]) : 0u;
-    sum->rounds = any ? ex[1] + own[1] : 0u;
-    sum->mtiles = any ? ex[2] + own[2] : 0u;
-    sum->gtiles = any ? ex[3] + own[3] : 0u;
-    sum->bm_bytes = any ? ex[4] + own[4] : 0u;
-    sum->payload = any ? ex[5] + own[5] : 0u;
-    sum->consumed = consumed;
-    sum->next_pos = next;
-    sum->nbad = 0;
-    *gctr = 0u;  // the verify launch's pool counter (no separate reset launch)
-    // the host's copy: every field, one system-scope fence, then the sequence
-    // number the host polls
+  if (!islast) return;
+  __threadfence();  // acquire: the other blocks' summary fields, flags and exception slots
+  const uint32_t nexc = done[1];
+  if (t == 0) {
+    sum->nexc = nexc;
+    sum->utiles = (sum->nonuni || (sum->mtiles >> 32)) ? 0u : T;  // read by the verify kernel
     GridSummary h = *sum;
     h.seq = 0u;
-    *hsum = h;
-    __threadfence_system();
-    __hip_atomic_store(&hsum->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    *reinterpret_cast<GridSummary *>(hsum) = h;
+    const uint64_t *x = reinterpret_cast<const uint64_t *>(&recs[0]);
+    uint64_t *y = reinterpret_cast<uint64_t *>(hsum + kGridHostRec0);
+    for (int q = 0; q < int(kGridRecBytes / 8); q++) y[q] = x[q];
   }
+  for (uint32_t j = t; j < min(nexc, kExcMax); j += kGridBlock) {
+    const uint32_t i = exc[j];
+    reinterpret_cast<uint32_t *>(hsum + kGridHostIdx)[j] = i;
+    const uint64_t *x = reinterpret_cast<const uint64_t *>(&recs[i]);
+    uint64_t *y = reinterpret_cast<uint64_t *>(hsum + kGridHostExc + size_t(j) * kGridRecBytes);
+    for (int q = 0; q < int(kGridRecBytes / 8); q++) y[q] = x[q];
+  }
+  __threadfence_system();
+  __syncthreads();
+  if (t == 0)
+    __hip_atomic_store(&reinterpret_cast<GridSummary *>(hsum)->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // After verify: every segment with a bad chunk -> one compact GridBad entry
@@ -1568,12 +1615,12 @@ hipError_t launch_frame_grid(const uint8_t *s, uint64_t len, uint64_t base, uint
   const uint32_t nblk = (count + kGridBlock - 1) / kGridBlock;
   auto *contrib = reinterpret_cast<GridContrib *>(g.contrib);
   hipLaunchKernelGGL(frame_grid_kernel, dim3(nblk), dim3(kGridBlock), 0, stream, s, len, base, count, proto, cs,
-                     ctype, verify, g.recs, g.status, contrib, g.blk_sum, g.blk_min, g.sum, g.hrecs);
+                     ctype, verify, g.recs, g.status, contrib, g.blk_sum, g.blk_min, g.sum, g.done);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(grid_build_kernel, dim3(nblk), dim3(kGridBlock), 0, stream, s, base, count, nblk, g.recs,
                      g.status, contrib, g.blk_sum, g.blk_min, cs, sflags, bm_base, copy_base, copy_cap, g.segs,
-                     g.seg2pkt, g.fb, g.gctr, g.sum, g.hsum, g.seq);
+                     g.seg2pkt, g.fb, g.gctr, g.done, g.exc, g.sum, g.hsum, g.seq);
   return hipGetLastError();
 }
 
@@ -1646,10 +1693,12 @@ hipError_t launch_tiles(int mode, int order, int nt, int depth, int streams, int
                         const SegDev *segs, uint32_t nseg, uint64_t total_rounds, uint64_t total_tiles,
                         const uint32_t *gtab, uint32_t *first_bad, unsigned long long *mism,
                         unsigned long long *diag, uint32_t tune, uint32_t *gctr, hipStream_t stream, int copy,
-                        int una, const GridSummary *dyn) {
+                        int una, const GridSummary *dyn, uint32_t utiles) {
+  // uniform-table look-up: tile indices must fit 32 bits (multiply-high form)
+  if (utiles && !dyn && (total_tiles >> 32)) utiles = 0;
 #define HDFS_LAUNCH_CU(M, O, N, D, S, B, BUF, C, U)                                                            \
   hipLaunchKernelGGL((crc32c_tiles_kernel<M, O, N, D, S, B, BUF, C, U>), dim3(grid), dim3(B), 0, stream, segs, \
-                     nseg, total_rounds, total_tiles, gtab, first_bad, mism, diag, tune, gctr, dyn)
+                     nseg, total_rounds, total_tiles, gtab, first_bad, mism, diag, tune, gctr, dyn, utiles)
 #define HDFS_LAUNCH_C(M, O, N, D, S, B, BUF, C) HDFS_LAUNCH_CU(M, O, N, D, S, B, BUF, C, 0)
 #define HDFS_LAUNCH(M, O, N, D, S, B, BUF) HDFS_LAUNCH_C(M, O, N, D, S, B, BUF, 0)
 #define HDFS_SHAPE(O, N, D, S, B) (order == (O) && nt == (N) && depth == (D) && streams == (S) && block == (B))

@@ -78,6 +78,7 @@ struct PieceLayout {
   uint64_t arena = 0, crcb = 0, bm = 0;
   uint32_t units = 0;
   uint64_t rounds = 0, mtiles = 0, gtiles = 0;
+  uint32_t utiles = 0;          // uniform table: main tiles per segment (0: not uniform)
   size_t off_segs = 0, off_fb = 0, off_bm = 0, meta = 0;  // table layout (device and pinned host)
 };
 
@@ -174,6 +175,7 @@ int build_piece(const hdfs_crc32c_packet *recs, const size_t *idx, PieceLayout &
     boff += (uint64_t(d.ncrc) + 7) / 8;
     unit += d.nunits;
   }
+  L.utiles = uniform_tiles(hs, L.n);
   return HDFS_CRC32C_OK;
 }
 
@@ -190,7 +192,8 @@ int enqueue_piece(DevCtx &c, const uint8_t *host, const PieceLayout &L, PieceSlo
                        comp));
   int rc = launch_all(c, kModeVerify, reinterpret_cast<const SegDev *>(s.meta + L.off_segs), uint32_t(L.n),
                       L.rounds, L.mtiles, L.gtiles, reinterpret_cast<uint32_t *>(s.meta + L.off_fb), s.mism,
-                      s.gctr, comp, nullptr, nullptr, true, ctype == HDFS_CRC32C_CSUM_CRC32 ? 1 : 0);
+                      s.gctr, comp, nullptr, nullptr, true, ctype == HDFS_CRC32C_CSUM_CRC32 ? 1 : 0, false, false,
+                      false, L.utiles);
   if (rc) return rc;
   HIPCHK(hipMemcpyAsync(hmeta + L.off_fb, s.meta + L.off_fb, L.meta - L.off_fb, hipMemcpyDeviceToHost, comp));
   HIPCHK(hipEventRecord(s.done, comp));
@@ -349,7 +352,7 @@ int submit_device_batch(DevCtx &c, const uint8_t *d, const std::vector<hdfs_crc3
   int rc = launch_all(c, kModeVerify, reinterpret_cast<const SegDev *>(dm), uint32_t(L.n), L.rounds, L.mtiles,
                       L.gtiles, reinterpret_cast<uint32_t *>(dm + L.off_fb), mism, gctr, c.v_stream, nullptr,
                       nullptr, true, ctype == HDFS_CRC32C_CSUM_CRC32 ? 1 : 0, copy_dst != nullptr, false,
-                      any_unaligned(hs, L.n));
+                      any_unaligned(hs, L.n), uniform_tiles(hs, L.n));
   if (rc) return rc;
   HIPCHK(hipMemcpyAsync(hm + L.off_fb, dm + L.off_fb, L.meta - L.off_fb, hipMemcpyDeviceToHost, c.v_stream));
   return HDFS_CRC32C_OK;
@@ -464,8 +467,9 @@ int stream_device(const void *stream) {
 // Layout of one pass's device tables and pinned landing area.
 constexpr uint32_t kBadFirst = 1024;  // bad-packet entries copied back with the verify summary
 struct GridLayout {
-  size_t recs, status, contrib, blk_sum, blk_min, segs, seg2pkt, fb, sum, bad, ctr, bm, dtotal;  // device offsets
-  size_t h_recs, h_sum, h_sum2, htotal;  // pinned offsets (h_sum2: summary after verify, then the bad list)
+  size_t recs, status, contrib, blk_sum, blk_min, segs, seg2pkt, fb, sum, bad, ctr, done, exc, bm, dtotal;  // device
+  size_t h_sum, h_sum2, htotal;  // pinned offsets (h_sum: summary + packet 0 + exceptions, kGridHost*;
+                                 // h_sum2: summary after verify, then the bad list)
   GridLayout(uint32_t count, uint64_t bm_cap) {
     const size_t nblk = (count + 63) / 64;  // frame_grid_kernel blocks (kGridBlock)
     size_t o = 0;
@@ -481,15 +485,18 @@ struct GridLayout {
     sum = take(256);  // the bad list follows the summary: one copy back
     bad = take(size_t(count) * sizeof(GridBad));
     ctr = take(128);  // pool counter, mismatch count
+    done = take(64);  // grid_build_kernel: blocks finished, exceptions found
+    exc = take(size_t(count) * 4);
     bm = take(size_t(bm_cap));
     dtotal = o;
     o = 0;
-    h_recs = take(size_t(count) * sizeof(hdfs_crc32c_packet));
-    h_sum = take(256);
+    h_sum = take(kGridHostBytes);
     h_sum2 = take(256 + size_t(kBadFirst) * sizeof(GridBad));
     htotal = o;
   }
 };
+static_assert(sizeof(hdfs_crc32c_packet) == kGridRecBytes, "host record layout");
+static_assert(sizeof(GridSummary) <= kGridHostRec0, "summary area");
 
 int reserve_grid(DevCtx &c, size_t si, const GridLayout &L) {
   if (si >= c.grid.size()) c.grid.resize(si + 1);
@@ -505,8 +512,8 @@ int reserve_grid(DevCtx &c, size_t si, const GridLayout &L) {
     if (g.h) HIPCHK(hipHostFree(g.h));
     g.h = g.hd = nullptr;
     g.hcap = 0;
-    // fine-grained (coherent) and mapped: the framing kernels write the
-    // records and the summary here directly
+    // fine-grained (coherent) and mapped: grid_build_kernel writes the
+    // summary, packet 0's record and the exceptions here directly
     HIPCHK(hipHostMalloc(&g.h, L.htotal, hipHostMallocCoherent | hipHostMallocMapped));
     HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&g.hd), g.h, 0));
     g.hcap = L.htotal;
@@ -517,16 +524,18 @@ int reserve_grid(DevCtx &c, size_t si, const GridLayout &L) {
 // Framing + verify of a device-resident stream, run by run on the device:
 // each pass frames up to kGridMaxCount packets on the grid of the first
 // packet's size (frame_grid_kernel), builds their verify segment table in
-// HBM (grid_scan_kernel) and returns only a summary; the verify launch
-// (plus the optional fused copy-out) is enqueued on c.v_stream straight
-// from that summary while the records come back on c.stream.  A pass that
-// leaves the grid after at most two packets (a stream of mixed sizes) hands
-// the rest to the host window walk (walk_device_stream).  Same records,
-// stopping rules and consumed offset as parse_packet_stream.
+// HBM (grid_build_kernel) and returns only a summary, packet 0's record and
+// the records that differ from the prediction from it; the verify launch
+// (plus the optional fused copy-out) is queued behind them straight from the
+// device-built summary.  The host writes the pass's records into the
+// caller's array while the verify kernel runs.  A pass that leaves the grid
+// after at most two packets (a stream of mixed sizes) hands the rest to the
+// host window walk (walk_device_stream).  Same records, stopping rules and
+// consumed offset as parse_packet_stream.
 int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs, int ctype, size_t max_pkts,
-              bool verify, uint8_t *copy_dst, uint64_t copy_cap, std::vector<hdfs_crc32c_packet> &out,
+              bool verify, uint8_t *copy_dst, uint64_t copy_cap, hdfs_crc32c_packet *dst, size_t *nout,
               uint64_t *consumed, uint64_t *payload_out) {
-  out.clear();
+  *nout = 0;
   *consumed = 0;
   verify = verify && ctype != HDFS_CRC32C_CSUM_NULL;
   if (!c.v_stream) HIPCHK(hipStreamCreateWithFlags(&c.v_stream, hipStreamNonBlocking));
@@ -539,17 +548,18 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
   };
   std::vector<Pass> passes;
   uint64_t pos = 0, payload = 0;
+  size_t n = 0;  // records in dst
   int rc = HDFS_CRC32C_OK;
   bool fallback = false;
   using clk = std::chrono::steady_clock;
   const auto t0 = clk::now();
-  double t_enq = 0, t_sync = 0, t_venq = 0;
+  double t_enq = 0, t_sync = 0, t_fill = 0;
   auto us_since = [](clk::time_point a, clk::time_point b) {
     return std::chrono::duration<double, std::micro>(b - a).count();
   };
-  while (out.size() < max_pkts && pos < len) {
+  while (n < max_pkts && pos < len) {
     const uint64_t left = len - pos;
-    const uint32_t count = uint32_t(std::min<uint64_t>({uint64_t(max_pkts - out.size()), kGridMaxCount, left / 6 + 1}));
+    const uint32_t count = uint32_t(std::min<uint64_t>({uint64_t(max_pkts - n), kGridMaxCount, left / 6 + 1}));
     const uint64_t bm_cap = left / 32 + count + 64;  // >= sum of ceil(chunks / 8) over the run
     const auto tq0 = clk::now();
     const GridLayout L(count, bm_cap);
@@ -568,24 +578,19 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
                       reinterpret_cast<uint32_t *>(dg + L.seg2pkt),
                       reinterpret_cast<uint32_t *>(dg + L.fb),
                       ctr,
+                      reinterpret_cast<uint32_t *>(dg + L.done),
+                      reinterpret_cast<uint32_t *>(dg + L.exc),
                       sum,
-                      c.grid_nocu ? nullptr : reinterpret_cast<hdfs_crc32c_packet *>(c.grid[si].hd + L.h_recs),
-                      reinterpret_cast<GridSummary *>(c.grid[si].hd + L.h_sum),
+                      c.grid[si].hd + L.h_sum,
                       ++c.grid_seq};
-    auto *hsum = reinterpret_cast<volatile GridSummary *>(hg + L.h_sum);
-    hsum->seq = 0;
+    auto *hsum = reinterpret_cast<GridSummary *>(hg + L.h_sum);
+    __atomic_store_n(&hsum->seq, 0u, __ATOMIC_RELEASE);
     // framing and the segment table on c.stream; the verify of the run is
-    // queued behind it on c.v_stream right away, sized by the device-built
-    // summary (no host round trip before the GPU starts verifying)
+    // queued behind it right away, sized by the device-built summary (no host
+    // round trip before the GPU starts verifying)
     hipError_t e = launch_frame_grid(d, len, pos, count, proto, cs, ctype, verify ? 1 : 0, sflags, dg + L.bm,
                                      copy_dst ? copy_dst + payload : nullptr, copy_dst ? copy_cap - payload : 0, gb,
                                      c.stream);
-
-    if (e == hipSuccess && c.grid_nocu) {  // the tables are built: the record copy may start from here
-      if (!c.r_stream) e = hipStreamCreateWithFlags(&c.r_stream, hipStreamNonBlocking);
-      if (e == hipSuccess && !c.grid[si].framed) e = hipEventCreateWithFlags(&c.grid[si].framed, hipEventDisableTiming);
-      if (e == hipSuccess) e = hipEventRecord(c.grid[si].framed, c.stream);
-    }
     if (e != hipSuccess) {
       rc = fail(HDFS_CRC32C_EHIP, "device framing: %s", hipGetErrorString(e));
       break;
@@ -594,8 +599,6 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
       // generic tiles: at most one per packet for chunk sizes the tiled
       // kernel takes, else every tile of every packet
       const uint64_t gtiles_ub = cs % kRoundBytes == 0 ? count : left / (uint64_t(cs) * kTileChunks) + 2ull * count;
-      // same stream as the framing kernels (stream order, no event); the host
-      // polls the framing summary instead of synchronising the stream
       rc = launch_verify_dyn(c, reinterpret_cast<const SegDev *>(dg + L.segs), sum, gtiles_ub,
                              reinterpret_cast<uint32_t *>(dg + L.fb), reinterpret_cast<unsigned long long *>(ctr + 16),
                              ctr, c.stream, tset, copy_dst != nullptr);
@@ -607,29 +610,14 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
       HIPCHK(hipMemcpyAsync(hg + L.h_sum2, sum, 256 + size_t(std::min(kBadFirst, count)) * sizeof(GridBad),
                             hipMemcpyDeviceToHost, c.stream));
     }
-    if (c.grid_nocu) {
-      // the run's records to pinned memory on a copy engine, concurrent with
-      // the verify kernel (a blit kernel would wait for it: it holds every
-      // CU); enqueued after the verify so the GPU gets that first
-      if (e == hipSuccess) e = hipStreamWaitEvent(c.r_stream, c.grid[si].framed, 0);
-      if (e == hipSuccess)
-        e = hipMemcpyAsync(c.grid[si].hd + L.h_recs, recs, size_t(count) * sizeof(hdfs_crc32c_packet),
-                           hipMemcpyDeviceToDeviceNoCU, c.r_stream);
-      if (e != hipSuccess) {
-        rc = fail(HDFS_CRC32C_EHIP, "record copy: %s", hipGetErrorString(e));
-        break;
-      }
-    }
     // the summary lands in pinned memory with its sequence number last: poll
     // it (a fault is caught by the stream synchronisation after 200 ms)
     const auto tq = clk::now();
     for (uint32_t spin = 1;; spin++) {
-      if (__atomic_load_n(&reinterpret_cast<GridSummary *>(hg + L.h_sum)->seq, __ATOMIC_ACQUIRE) == gb.seq) break;
+      if (__atomic_load_n(&hsum->seq, __ATOMIC_ACQUIRE) == gb.seq) break;
       if ((spin & 4095u) == 0 && clk::now() - tq > std::chrono::milliseconds(200)) {
         e = hipStreamSynchronize(c.stream);
-        if (e == hipSuccess &&
-            __atomic_load_n(&reinterpret_cast<GridSummary *>(hg + L.h_sum)->seq, __ATOMIC_ACQUIRE) != gb.seq)
-          e = hipErrorUnknown;
+        if (e == hipSuccess && __atomic_load_n(&hsum->seq, __ATOMIC_ACQUIRE) != gb.seq) e = hipErrorUnknown;
         break;
       }
 #if defined(__x86_64__) || defined(__i386__)
@@ -637,21 +625,47 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
 #endif
     }
     t_enq += us_since(tq0, tq);
-    t_sync += us_since(tq, clk::now());
+    const auto tf = clk::now();
+    t_sync += us_since(tq, tf);
     if (e != hipSuccess) {
       rc = fail(HDFS_CRC32C_EHIP, "device framing: %s", hipGetErrorString(e));
       break;
     }
     GridSummary S;
-    std::memcpy(&S, hg + L.h_sum, sizeof(S));
+    std::memcpy(&S, hsum, sizeof(S));
     if (copy_dst && payload + S.payload > copy_cap) {
       rc = fail(HDFS_CRC32C_EINVAL, "copy-out buffer of %llu bytes is too small (%llu needed so far)",
                 (unsigned long long)copy_cap, (unsigned long long)(payload + S.payload));
       break;
     }
-    t_venq += us_since(tq, clk::now());
-    passes.push_back({si, out.size(), S.recorded, verify ? S.nseg : 0u, count, bm_cap});
-    out.resize(out.size() + S.recorded);
+    // the pass's records, written while the verify kernel runs: predicted
+    // from packet 0, then the exceptions (all of them from HBM if the host
+    // area could not hold them)
+    if (S.recorded) {
+      hdfs_crc32c_packet r0;
+      std::memcpy(&r0, hg + L.h_sum + kGridHostRec0, sizeof(r0));
+      hdfs_crc32c_packet *out = dst + n;
+      for (uint32_t k = 0; k < S.recorded; k++) {
+        hdfs_crc32c_packet &r = out[k];
+        r = r0;
+        r.stream_off = pos + uint64_t(k) * S.stride;
+        r.offset_in_block = r0.offset_in_block + int64_t(k) * r0.data_len;
+        r.seqno = r0.seqno + int64_t(k);
+      }
+      if (S.nexc <= kExcMax) {
+        const auto *idx = reinterpret_cast<const uint32_t *>(hg + L.h_sum + kGridHostIdx);
+        const uint8_t *er = hg + L.h_sum + kGridHostExc;
+        for (uint32_t j = 0; j < S.nexc; j++) std::memcpy(&out[idx[j]], er + size_t(j) * kGridRecBytes, kGridRecBytes);
+      } else {
+        if (!c.r_stream) HIPCHK(hipStreamCreateWithFlags(&c.r_stream, hipStreamNonBlocking));
+        HIPCHK(hipMemcpyAsync(out, recs, size_t(S.recorded) * sizeof(hdfs_crc32c_packet), hipMemcpyDeviceToHost,
+                              c.r_stream));
+        HIPCHK(hipStreamSynchronize(c.r_stream));
+      }
+    }
+    t_fill += us_since(tf, clk::now());
+    passes.push_back({si, n, S.recorded, verify ? S.nseg : 0u, count, bm_cap});
+    n += S.recorded;
     payload += S.payload;
     *consumed = S.consumed;
     if (S.last_status == kGridStop || S.last_status == kGridMore) break;
@@ -662,21 +676,15 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
     }
   }
   const auto t1 = clk::now();
-  // records of every pass: written to pinned memory by frame_grid_kernel,
-  // complete once the pass's summary was seen; copied out while the verify
-  // kernels still run
-  if (c.grid_nocu && c.r_stream) {
-    hipError_t er = hipStreamSynchronize(c.r_stream);
-    if (!rc && er != hipSuccess) rc = fail(HDFS_CRC32C_EHIP, "record copy: %s", hipGetErrorString(er));
+  if (!rc && fallback && n < max_pkts) {
+    std::vector<hdfs_crc32c_packet> more;
+    rc = walk_device_stream(c, d, len, proto, cs, ctype, max_pkts - n, verify, more, consumed, pos, copy_dst,
+                            &payload);
+    if (!rc && !more.empty()) {
+      std::memcpy(dst + n, more.data(), more.size() * sizeof(hdfs_crc32c_packet));
+      n += more.size();
+    }
   }
-  const auto t1b = clk::now();
-  if (!rc)
-    for (const Pass &p : passes)
-      if (p.n) std::memcpy(out.data() + p.off, c.grid[p.slot].h + GridLayout(p.count, p.bm_cap).h_recs,
-                           p.n * sizeof(hdfs_crc32c_packet));
-  const auto t1c = clk::now();
-  if (!rc && fallback && out.size() < max_pkts)
-    rc = walk_device_stream(c, d, len, proto, cs, ctype, max_pkts, verify, out, consumed, pos, copy_dst, &payload);
   const auto t1d = clk::now();
   // drained even after an error: the tables of queued work live in this context
   hipError_t e = hipStreamSynchronize(c.stream);
@@ -702,7 +710,7 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
       bad = more.data();
     }
     for (uint32_t i = 0; i < nbad; i++) {
-      hdfs_crc32c_packet &k = out[p.off + bad[i].pkt];
+      hdfs_crc32c_packet &k = dst[p.off + bad[i].pkt];
       k.error = HDFS_CRC32C_ERR_DATANODE_BAD_CHECKSUM;
       k.first_bad = bad[i].first_bad;
       k.bad_chunks = bad[i].bad_chunks;
@@ -712,11 +720,12 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
     const auto t2 = clk::now();
     auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
     std::fprintf(stderr,
-                 "dstream grid pkts=%zu passes=%zu fallback=%d enq_us=%.1f sum_sync_us=%.1f verify_enq_us=%.1f "
-                 "loop_us=%.1f recs_sync_us=%.1f memcpy_us=%.1f fallback_us=%.1f verify_sync_us=%.1f total_us=%.1f\n",
-                 out.size(), passes.size(), int(fallback), t_enq, t_sync, t_venq, us(t0, t1), us(t1, t1b), us(t1b, t1c),
-                 us(t1c, t1d), us(t1d, t1e), us(t0, t2));
+                 "dstream grid pkts=%zu passes=%zu fallback=%d enq_us=%.1f sum_sync_us=%.1f fill_us=%.1f "
+                 "loop_us=%.1f fallback_us=%.1f verify_sync_us=%.1f total_us=%.1f\n",
+                 n, passes.size(), int(fallback), t_enq, t_sync, t_fill, us(t0, t1), us(t1, t1d), us(t1d, t1e),
+                 us(t0, t2));
   }
+  *nout = n;
   if (payload_out) *payload_out = payload;
   return HDFS_CRC32C_OK;
 }
@@ -731,22 +740,22 @@ int verify_packets_dev_impl(int dev, const uint8_t *stream, uint64_t len, int pr
   DevCtx &c = *cp;
   DeviceGuard g(c.dev);
   std::lock_guard<std::mutex> lk(c.mu);
-  std::vector<hdfs_crc32c_packet> recs;
   uint64_t used = 0;
-  if ((rc = grid_walk(c, stream, len, proto, cs, ctype, max_pkts, verify, copy_dst, copy_cap, recs, &used, nullptr)))
+  size_t n = 0;
+  if ((rc = grid_walk(c, stream, len, proto, cs, ctype, max_pkts, verify, copy_dst, copy_cap, pkts, &n, &used,
+                      nullptr)))
     return rc;
-  if (!recs.empty()) std::memcpy(pkts, recs.data(), recs.size() * sizeof(hdfs_crc32c_packet));
-  if (npkts) *npkts = recs.size();
+  if (npkts) *npkts = n;
   if (consumed) *consumed = used;
   if (delivered) {  // what the reference copies out before its loop returns an error (src/datanode.c:2470-2486)
-    uint64_t n = 0;
-    for (const auto &k : recs) {
-      if (k.error) break;
-      n += uint64_t(k.data_len);
+    uint64_t b = 0;
+    for (size_t i = 0; i < n; i++) {
+      if (pkts[i].error) break;
+      b += uint64_t(pkts[i].data_len);
     }
-    *delivered = n;
+    *delivered = b;
   }
-  return first_error(recs.data(), recs.size());
+  return first_error(pkts, n);
 }
 
 // Synchronous packet-run verify: framing, then pieces of <= 64 MiB of wire
