@@ -1146,7 +1146,7 @@ int hdfs_crc32c_device_sync(void) {
 #ifdef HDFS_CRC32C_DIAG
 // ---- diagnostic build only (include/hadoofus_crc32c_diag.h) ----
 int hdfs_crc32c_set_store_policy(int policy) {
-  if (policy < 0 || policy > 11) return fail(HDFS_CRC32C_EINVAL, "store policy 0..11");
+  if (policy < 0 || policy > 13) return fail(HDFS_CRC32C_EINVAL, "store policy 0..13");
   g_store_policy = uint32_t(policy);
   return HDFS_CRC32C_OK;
 }

@@ -468,6 +468,19 @@ DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, ui
           reinterpret_cast<uint32_t *>(rfl64(reinterpret_cast<uint64_t>(sh.crcs + c.tile * kTileChunks))), 0,
           static_cast<int>(rfl(keep ? nch * 4u : 0u)), 0x00020000);
       uint32_t off = leader ? L.qg * 4u : 0x80000000u;
+      if (kDiag && (L.store_policy == 12 || L.store_policy == 13)) {
+        // diagnostic: only the last tile of each 8-tile group stores -- 12: one
+        // 256-B store over the whole group's CRCs (64 lanes x 4 B, sc1; the
+        // values are not the group's CRCs), 13: its own 32 B as usual
+        const bool grp = keep && (c.tile & 7u) == 7u;
+        const bool full = L.store_policy == 12;
+        const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(
+            reinterpret_cast<uint32_t *>(rfl64(reinterpret_cast<uint64_t>(sh.crcs + (full ? (c.tile & ~7u) : c.tile) *
+                                                                                             kTileChunks))),
+            0, static_cast<int>(rfl(grp ? (full ? 256u : nch * 4u) : 0u)), 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b32(val, rg, full ? L.lane * 4u : off, 0, 16);
+        return;
+      }
       if (kDiag && L.store_policy == 9) {
         // diagnostic: every tile's 32 B lands in a 256 KiB window (L2-resident writes)
         const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(

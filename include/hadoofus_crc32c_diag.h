@@ -57,7 +57,10 @@ int hdfs_crc32c_set_shape(int streams, int block);
  * cache policy sc1 / sc0 sc1 / nt sc1 / sc0; 9: every tile's CRCs written into
  * one 256 KiB window (L2-resident writes); 10: only chunk 0 of each tile
  * stored (4 B per tile) -- timing experiments only, output undefined; 11:
- * default-policy (no cache bits) CRC stores.
+ * default-policy (no cache bits) CRC stores; 12: only the last tile of each
+ * 8-tile group stores, one 256-B store over the group's CRC area; 13: only
+ * that tile stores its own 32 B -- 12 / 13 timing experiments only, output
+ * undefined.
  * Env HDFS_CRC32C_STORE. */
 int hdfs_crc32c_set_store_policy(int policy);
 /* Empirical streaming-read bandwidth of `bytes` at dptr (GB/s, 1e9 B/s):

@@ -75,12 +75,15 @@ def assemble(parts):
     return b"".join(out)
 
 
-def build_stream(crc32c, proto, cs, ctype, dlens, seed=0, corrupt=(), last_empty=True, sync_every=0):
+def build_stream(crc32c, proto, cs, ctype, dlens, seed=0, corrupt=(), last_empty=True, sync_every=0,
+                 seqnos=None, offset_skew=None):
     """A clean stream of packets with the given data lengths (the last one
     flagged lastPacketInBlock unless last_empty adds the v2-style trailing
     empty packet).  corrupt: iterable of (packet, chunk) -> flip one bit of
-    that chunk after its CRC is computed.  Returns (stream bytes, expected
-    per-packet bad chunk lists)."""
+    that chunk after its CRC is computed.  seqnos: header seqno per packet
+    (default k); offset_skew: {packet: bytes added to its offsetInBlock} --
+    header fields off the regular progression, same wire sizes.  Returns
+    (stream bytes, expected per-packet bad chunk lists)."""
     out = []
     bad = {}
     for pk, ch in corrupt:
@@ -93,11 +96,13 @@ def build_stream(crc32c, proto, cs, ctype, dlens, seed=0, corrupt=(), last_empty
             clen = min(cs, dl - ch * cs)
             d[ch * cs + (k * 7919 + ch) % clen] ^= np.uint8(1 << (ch % 8))
         last = (k == len(dlens) - 1) and not last_empty
+        seq = k if seqnos is None else seqnos[k]
+        ho = off + (offset_skew or {}).get(k, 0)
         if proto == 1:
-            out.append(frame_v1(off, k, last, crcs, d.tobytes()))
+            out.append(frame_v1(ho, seq, last, crcs, d.tobytes()))
         else:
             sync = (k % sync_every == 0) if sync_every else None
-            out.append(frame_v2(header_v2(off, k, last, dl, sync), crcs, d.tobytes()))
+            out.append(frame_v2(header_v2(ho, seq, last, dl, sync), crcs, d.tobytes()))
         off += dl
     if last_empty:
         k = len(dlens)

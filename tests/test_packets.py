@@ -361,3 +361,40 @@ def test_gpu_device_stream_many_passes(engine, oracle):
     assert dst.download(delivered).tobytes() == _payloads(s, want[1])
     keep.free()
     dst.free()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("proto,pattern", [(2, "few"), (1, "few"), (2, "all"), (2, "last")])
+def test_gpu_device_stream_irregular_headers(engine, oracle, proto, pattern):
+    """Runs of equal-size packets whose headers leave the regular progression
+    (seqno + 1, offsetInBlock + dataLen): the device framing reports those
+    packets as exceptions to the prediction from packet 0 -- a few (they ride
+    with the summary), more than its host area holds (every seqno shuffled:
+    the records come back from HBM), or only the final packet."""
+    npk = 300
+    rng = np.random.default_rng(npk + proto + len(pattern))
+    seqnos, skew = list(range(npk)), {}
+    if pattern == "few":
+        for k in (1, 10, 77, 200, 299):
+            seqnos[k] += 5
+        skew = {150: 512, 151: -3}
+    elif pattern == "all":
+        seqnos = [int(x) for x in rng.permutation(npk)]
+    else:
+        seqnos[-1] = 10 ** 12
+    dl = [65536] * npk
+    s, bad = build_stream(oracle.crc32c, proto, 512, CSUM_CRC32C, dl, seed=npk, corrupt=[(3, 9), (150, 0)],
+                          seqnos=seqnos, offset_skew=skew)
+    want = oracle.verify_packets(s, proto, 512, CSUM_CRC32C)
+    assert [q["seqno"] for q in want[1][:npk]] == seqnos
+    for shift in (0, 1):
+        keep, p = _dev(engine, s, shift)
+        got = engine.verify_packets(None, proto, 512, CSUM_CRC32C, dptr=p, nbytes=len(s))
+        assert got == want
+        assert engine.parse_packets(None, proto, 512, CSUM_CRC32C, dptr=p, nbytes=len(s))[1] == \
+            _framing_only(want[1])
+        dst = engine.DeviceBuffer(sum(dl))
+        rc, pkts, used, delivered = engine.verify_packets_copy(p, len(s), dst.ptr, dst.nbytes, proto)
+        assert (rc, pkts, used) == want and dst.download(delivered).tobytes() == _payloads(s, want[1])
+        keep.free()
+        dst.free()
