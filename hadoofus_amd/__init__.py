@@ -32,6 +32,7 @@ from .abi import (  # noqa: F401
     SEG_CRC32,
     CRC32CError,
     DeviceBuffer,
+    Mailbox,
     Plan,
     Segment,
     Session,

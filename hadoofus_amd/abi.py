@@ -146,6 +146,9 @@ def bind_product(lib):
     _bind(lib, "hdfs_crc32c_fill_splitmix64", _int, [_vp, _u64, _u64, _u64, _vp])
     _bind(lib, "hdfs_crc32c_corrupt", _int, [_vp, _u64, _u32, _u64, _u64, _u64, _vp])
     _bind(lib, "hdfs_crc32c_device_sync", _int, [])
+    _bind(lib, "hdfs_crc32c_mailbox_create", _int, [ctypes.POINTER(_vp), _u32])
+    _bind(lib, "hdfs_crc32c_mailbox_stats", _int, [_vp, ctypes.POINTER(_u64), ctypes.POINTER(_u64)])
+    _bind(lib, "hdfs_crc32c_mailbox_destroy", _int, [_vp])
     _bind(lib, "hdfs_crc32c_compose_packets", _int,
           [_vp, _u64, ctypes.c_int64, ctypes.c_int64, _int, _int, _int, _vp, _u64, ctypes.POINTER(OutPacket), _sz,
            ctypes.POINTER(_sz), ctypes.POINTER(_u64)])
@@ -168,6 +171,7 @@ def bind_diag(lib):
     _bind(lib, "hdfs_crc32c_set_depth", _int, [_int])
     _bind(lib, "hdfs_crc32c_set_shape", _int, [_int, _int])
     _bind(lib, "hdfs_crc32c_set_store_policy", _int, [_int])
+    _bind(lib, "hdfs_crc32c_set_runs", _int, [_int])
     return lib
 
 
@@ -263,6 +267,31 @@ def _packets(fn, stream, proto, chunk_size, ctype, max_pkts, dptr=None, nbytes=N
     if rc < 0:
         _check(rc)
     return rc, [arr[i].as_dict() for i in range(npk.value)], used.value
+
+
+class Mailbox:
+    """Opt-in resident kernel for the synchronous small calls
+    (hdfs_crc32c_mailbox_create); a context manager."""
+
+    def __init__(self, idle_ms=0):
+        self.ptr = _vp()
+        _check(load().hdfs_crc32c_mailbox_create(ctypes.byref(self.ptr), idle_ms))
+
+    def stats(self):
+        calls, launches = _u64(0), _u64(0)
+        _check(load().hdfs_crc32c_mailbox_stats(self.ptr, ctypes.byref(calls), ctypes.byref(launches)))
+        return calls.value, launches.value
+
+    def close(self):
+        if self.ptr:
+            _check(load().hdfs_crc32c_mailbox_destroy(self.ptr))
+            self.ptr = _vp()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
 
 class Session:

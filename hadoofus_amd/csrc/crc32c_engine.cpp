@@ -78,6 +78,8 @@ uint32_t g_store_policy = uint32_t(HDFS_KNOB("HDFS_CRC32C_STORE", 0));
 uint32_t g_group_shift = uint32_t(HDFS_KNOB("HDFS_CRC32C_GROUP", 3)) & 15u;
 // Schedule 3: deal groups XCD-major (1) or by plain workgroup id (0).
 uint32_t g_xcd_major = uint32_t(HDFS_KNOB("HDFS_CRC32C_XCD", 1)) & 1u;
+// Compute mode on tables of whole 8-tile groups: schedule 4 (runs).
+int g_runs = HDFS_KNOB("HDFS_CRC32C_RUNS", 1);
 // Diagnostic per-wave timestamps (device buffer, 3 x u64 per wave) or null.
 unsigned long long *g_diag = nullptr;
 
@@ -223,7 +225,7 @@ int launch_verify_dyn(DevCtx &c, const SegDev *d_segs, const GridSummary *dyn, u
   // schedule 3: a device-framed run is packets of one wire size, so its table
   // is uniform (dyn->utiles, no segment search per tile); the kernel falls
   // back to searching the table when it is not
-  const hipError_t le = launch_tiles(kModeVerify, 3, g_nt_loads, 3, 1, 1024, c.num_cu, d_segs, 0, 0, 0,
+  const hipError_t le = launch_tiles(kModeVerify, 3, g_nt_loads, 3, 1, 1024, c.bulk_cus(), d_segs, 0, 0, 0,
                                      c.d_tab_main_t[ctype], d_fb, d_mism, nullptr,
                                      (g_group_shift << 8) | (g_xcd_major << 12), d_gctr, st, copy ? 1 : 0, 1, dyn);
   if (le == hipErrorInvalidValue) return fail(HDFS_CRC32C_EINVAL, "verify kernel shape not built");
@@ -240,6 +242,15 @@ uint32_t uniform_tiles(const SegDev *segs, size_t n) {
   return T;
 }
 
+bool whole_groups(const SegDev *segs, size_t n) {
+  uint64_t m = 0;
+  for (size_t i = 0; i < n; i++) {
+    if (segs[i].main_tiles % kTileChunks) return false;
+    m += segs[i].main_tiles;
+  }
+  return m > 0;
+}
+
 bool any_unaligned(const SegDev *segs, size_t n) {
   for (size_t i = 0; i < n; i++)
     if (segs[i].main_tiles && (reinterpret_cast<uintptr_t>(segs[i].data) & 3u)) return true;
@@ -254,7 +265,7 @@ static const int g_small_rule = HDFS_KNOB("HDFS_CRC32C_SMALL_RULE", 1);
 int launch_all(DevCtx &c, int mode, const SegDev *d_segs, uint32_t nseg, uint64_t rounds,
                uint64_t mtiles, uint64_t gtiles, uint32_t *d_fb, unsigned long long *d_mism,
                uint32_t *d_gctr, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1, bool reset, int ctype, bool copy,
-               bool gctr_zeroed, bool una, uint32_t utiles) {
+               bool gctr_zeroed, bool una, uint32_t utiles, bool runs) {
   const bool vreset = mode == kModeVerify && reset;
   uint32_t *gz = (rounds && g_tile_order >= 2 && !gctr_zeroed) ? d_gctr : nullptr;
   if (vreset || gz)
@@ -263,7 +274,7 @@ int launch_all(DevCtx &c, int mode, const SegDev *d_segs, uint32_t nseg, uint64_
     // >= 4 rounds per wave (16 waves per block) before adding blocks: each
     // block pays a ~156 KiB LDS table fill.
     uint64_t want = (rounds + 63) / 64;
-    int grid = static_cast<int>(want < 1 ? 1 : (want > uint64_t(c.num_cu) ? c.num_cu : want));
+    int grid = static_cast<int>(want < 1 ? 1 : (want > uint64_t(c.bulk_cus()) ? c.bulk_cus() : want));
     if (ev0) HIPCHK(hipEventRecord(ev0, st));
     // The interleaved schedule (3) pays a segment look-up whenever a strided
     // tile leaves the current segment: small launches (which also skip the
@@ -271,17 +282,21 @@ int launch_all(DevCtx &c, int mode, const SegDev *d_segs, uint32_t nseg, uint64_
     // unless the table is uniform, where the look-up is a division.
     const bool small = rounds < 32ull * 16u * uint64_t(grid) || (!utiles && mtiles < 2ull * uint64_t(grid) * nseg);
     const bool to_small = g_tile_order == 3 && small && g_small_rule;
-    const int order = to_small ? 2 : g_tile_order;
-    // buffer loads (nt 2) exist for schedule 3 only; the others use nontemporal global loads
-    const int nt = order == 3 ? g_nt_loads : std::min(g_nt_loads, 1);
+    int order = to_small ? 2 : g_tile_order;
+    // buffer loads (nt 2) exist for schedules 3 / 4 only; the others use nontemporal global loads
+    const int nt = order >= 3 ? g_nt_loads : std::min(g_nt_loads, 1);
     // the small-launch fallback always runs the product's schedule-2 shape
     const int depth = to_small ? 3 : g_depth, streams = to_small ? 1 : g_streams, block = to_small ? 1024 : g_block;
+    // compute over whole 8-tile groups: schedule 4 (runs), product shape only
+    if (order == 3 && runs && g_runs && mode == kModeCompute && !una && !copy && nt == 2 && depth == 3 &&
+        streams == 1 && block == 1024)
+      order = 4;
     // store policy 4 (diagnostic build): verify plans run the load-only twin
     const int kmode = (kDiag && mode == kModeVerify && g_store_policy == 4) ? int(kModeLoadOnly) : mode;
     const hipError_t le = launch_tiles(kmode, order, nt, depth, streams, block, grid, d_segs, nseg, rounds,
                                        mtiles, c.d_tab_main_t[ctype], d_fb, d_mism, kDiag ? g_diag : nullptr,
                                        (kDiag ? g_store_policy : 0u) | (g_group_shift << 8) | (g_xcd_major << 12),
-                                       d_gctr, st, copy ? 1 : 0, una ? 1 : 0, nullptr, order == 3 ? utiles : 0u);
+                                       d_gctr, st, copy ? 1 : 0, una ? 1 : 0, nullptr, order >= 3 ? utiles : 0u);
     if (le == hipErrorInvalidValue)
       return fail(HDFS_CRC32C_EINVAL, "tiled kernel shape (order %d, nt %d, depth %d, streams %d, block %d) is not built",
                   order, nt, depth, streams, block);
@@ -340,8 +355,66 @@ bool small_ok(uint64_t len, uint64_t cs) {
 
 static const bool g_small_trace = std::getenv("HDFS_CRC32C_SMALL_TRACE") != nullptr;
 
+// Mailbox path of small_call: the resident kernel (re)launched if it is not
+// running, then one request line; same pinned result block and sequence
+// number as the launch path.
+int mb_launch(DevCtx &c, uint32_t seq0) {
+  c.mb_epoch++;
+  __atomic_store_n(&c.h_mb[16], (c.mb_epoch << 1) | 1u, __ATOMIC_RELEASE);
+  HIPCHK(launch_mailbox(c.dv_mb, c.dv_small_in, c.dv_small_out, c.dv_small_out + kSmallMeta, c.d_tab_main_t[0],
+                        c.d_tab_main_t[1], c.d_tab_pow2_t[0], c.d_tab_pow2_t[1], c.dv_mb + 16, c.mb_epoch, seq0,
+                        c.mb_idle_ticks, c.mb_stream));
+  c.mb_alive = true;
+  c.mb_launches++;
+  return HDFS_CRC32C_OK;
+}
+
+bool mb_exited(const DevCtx &c) { return __atomic_load_n(&c.h_mb[16], __ATOMIC_ACQUIRE) == (c.mb_epoch << 1); }
+
+int mailbox_call(DevCtx &c, int mode, uint32_t len, uint32_t cs, uint32_t reg0, bool be, int ctype) {
+  const uint32_t seq = ++c.small_seq;
+  if (c.mb_alive && mb_exited(c)) c.mb_alive = false;  // idled out since the last call
+  if (!c.mb_alive) {
+    const int rc = mb_launch(c, __atomic_load_n(&c.h_mb[0], __ATOMIC_ACQUIRE));
+    if (rc) return rc;
+  }
+  c.h_mb[1] = len;
+  c.h_mb[2] = cs | (mode == kModeVerify ? kMbVerifyFlag : 0u) | (be ? kMbBeFlag : 0u) | (ctype ? kMbCrc32Flag : 0u);
+  c.h_mb[3] = reg0;
+  __atomic_store_n(&c.h_mb[0], seq, __ATOMIC_RELEASE);  // data and fields first (x86-TSO / release)
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t spin = 1;; spin++) {
+    if (__atomic_load_n(&c.h_small_out[2], __ATOMIC_ACQUIRE) == seq) {
+      c.mb_calls++;
+      // a single chunk's CRC came with the completion word (one store)
+      if (mode != kModeVerify && len <= cs) c.h_small_out[kSmallMeta] = c.h_small_out[3];
+      return HDFS_CRC32C_OK;
+    }
+    if ((spin & 255u) == 0 && mb_exited(c)) {
+      // it idled out before it saw the request: a new one serves it
+      if (__atomic_load_n(&c.h_small_out[2], __ATOMIC_ACQUIRE) == seq) continue;
+      const int rc = mb_launch(c, seq - 1u);
+      if (rc) return rc;
+    }
+    if ((spin & 4095u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200)) {
+      const hipError_t e = hipStreamQuery(c.mb_stream);
+      if (e != hipSuccess && e != hipErrorNotReady) {
+        c.mb_alive = false;
+        return fail(HDFS_CRC32C_EHIP, "mailbox kernel: %s", hipGetErrorString(e));
+      }
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2))
+        return fail(HDFS_CRC32C_EHIP, "mailbox kernel did not answer request %u", seq);
+    }
+#if defined(__x86_64__) || defined(__i386__)
+    __builtin_ia32_pause();
+#endif
+  }
+}
+
 int small_call(DevCtx &c, int mode, uint32_t len, uint32_t cs, uint32_t reg0, bool be, int ctype,
                const uint8_t *dsrc) {
+  if (c.mb_on && !dsrc && (cs % 64u == 0 || len <= cs))  // one chunk: chunk size = len (fits the request line)
+    return mailbox_call(c, mode, len, len <= cs ? len : cs, reg0, be, ctype);
   const uint32_t seq = ++c.small_seq;
   const auto tl = std::chrono::steady_clock::now();
   HIPCHK(launch_small_chunks(mode, dsrc ? dsrc : c.dv_small_in, len, dsrc ? 1u : 0u, cs, reg0, be ? 1u : 0u,
@@ -641,6 +714,7 @@ struct hdfs_crc32c_plan {
   bool timing = false;
   bool una = false;  // some tiled segment's data is not 4-B aligned
   uint32_t utiles = 0;  // uniform table: main tiles per segment
+  bool runs = false;    // compute plan over whole 8-tile groups (schedule 4)
   std::vector<std::pair<hipEvent_t, hipEvent_t>> events;  // pre-created pool
   size_t next_event = 0;
 };
@@ -763,6 +837,7 @@ int hdfs_crc32c_plan_create(hdfs_crc32c_plan **plan, int mode, const hdfs_crc32c
   p->nchunks = nch;
   p->una = any_unaligned(host.data(), nseg);
   p->utiles = uniform_tiles(host.data(), nseg);
+  p->runs = mode == HDFS_CRC32C_MODE_COMPUTE && whole_groups(host.data(), nseg);
   hipError_t e = hipMalloc(&p->d_segs, sizeof(SegDev) * host.size());
   if (e == hipSuccess) e = hipMemcpy(p->d_segs, host.data(), sizeof(SegDev) * host.size(), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMalloc(&p->d_first_bad, sizeof(uint32_t) * host.size());
@@ -794,7 +869,7 @@ int hdfs_crc32c_plan_execute(hdfs_crc32c_plan *p, void *stream) {
     p->next_event++;
   }
   return launch_all(c, p->mode, p->d_segs, p->nseg, p->rounds, p->mtiles, p->gtiles, p->d_first_bad,
-                    p->d_mism, p->d_gctr, st, e0, e1, true, p->ctype, false, false, p->una, p->utiles);
+                    p->d_mism, p->d_gctr, st, e0, e1, true, p->ctype, false, false, p->una, p->utiles, p->runs);
 }
 
 int hdfs_crc32c_plan_results(hdfs_crc32c_plan *p, void *stream, uint32_t *first_bad, size_t nseg,
@@ -1139,7 +1214,76 @@ int hdfs_crc32c_host_free(void *p) {
 
 int hdfs_crc32c_device_sync(void) {
   HDFS_ON_ENGINE_DEVICE();
-  HIPCHK(hipDeviceSynchronize());
+  if (!ec_->mb_on) {
+    HIPCHK(hipDeviceSynchronize());
+    return HDFS_CRC32C_OK;
+  }
+  // a resident mailbox kernel never finishes while it is in use: every
+  // stream but its own
+  std::lock_guard<std::mutex> lk(ec_->mu);
+  HIPCHK(hipStreamSynchronize(nullptr));
+  for (hipStream_t s : {ec_->stream, ec_->v_stream, ec_->r_stream, ec_->copy_stream, ec_->comp_stream})
+    if (s) HIPCHK(hipStreamSynchronize(s));
+  return HDFS_CRC32C_OK;
+}
+
+struct hdfs_crc32c_mailbox {
+  int dev;
+};
+
+int hdfs_crc32c_mailbox_create(hdfs_crc32c_mailbox **mb, uint32_t idle_ms) {
+  if (!mb) return fail(HDFS_CRC32C_EINVAL, "null mailbox pointer");
+  *mb = nullptr;
+  DevCtx *c = nullptr;
+  int rc = ctx_init(-1, &c);
+  if (rc) return rc;
+  DeviceGuard g(c->dev);
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (c->mb_on) return fail(HDFS_CRC32C_EINVAL, "a mailbox is already open on device %d", c->dev);
+  if (!c->h_mb) {
+    HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&c->h_mb), 256, hipHostMallocCoherent | hipHostMallocMapped));
+    std::memset(c->h_mb, 0, 256);
+    HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&c->dv_mb), c->h_mb, 0));
+  }
+  if (!c->mb_stream) HIPCHK(hipStreamCreateWithFlags(&c->mb_stream, hipStreamNonBlocking));
+  const uint64_t ms = idle_ms ? idle_ms : 50u;
+  c->mb_idle_ticks = uint32_t(std::min<uint64_t>(ms * 100000u, 0xFFFFFFFFu));  // s_memrealtime: 100 MHz
+  c->mb_calls = c->mb_launches = 0;
+  // the bulk kernels' next launches leave the mailbox its CU
+  HIPCHK(hipStreamSynchronize(c->stream));
+  c->mb_on = true;
+  rc = mb_launch(*c, __atomic_load_n(&c->h_mb[0], __ATOMIC_ACQUIRE));
+  if (rc) {
+    c->mb_on = false;
+    return rc;
+  }
+  *mb = new hdfs_crc32c_mailbox{c->dev};
+  return HDFS_CRC32C_OK;
+}
+
+int hdfs_crc32c_mailbox_stats(const hdfs_crc32c_mailbox *mb, uint64_t *calls, uint64_t *launches) {
+  if (!mb) return fail(HDFS_CRC32C_EINVAL, "null mailbox");
+  DevCtx &c = g_ctx[mb->dev];
+  std::lock_guard<std::mutex> lk(c.mu);
+  if (calls) *calls = c.mb_calls;
+  if (launches) *launches = c.mb_launches;
+  return HDFS_CRC32C_OK;
+}
+
+int hdfs_crc32c_mailbox_destroy(hdfs_crc32c_mailbox *mb) {
+  if (!mb) return HDFS_CRC32C_OK;
+  DevCtx &c = g_ctx[mb->dev];
+  DeviceGuard g(mb->dev);
+  delete mb;
+  std::lock_guard<std::mutex> lk(c.mu);
+  if (!c.mb_on) return HDFS_CRC32C_OK;
+  c.mb_on = false;
+  if (c.mb_alive && !mb_exited(c)) {  // a quit request; the kernel acknowledges through its status word
+    c.h_mb[2] = kMbQuitFlag;
+    __atomic_store_n(&c.h_mb[0], ++c.small_seq, __ATOMIC_RELEASE);
+  }
+  c.mb_alive = false;
+  HIPCHK(hipStreamSynchronize(c.mb_stream));
   return HDFS_CRC32C_OK;
 }
 
@@ -1148,6 +1292,11 @@ int hdfs_crc32c_device_sync(void) {
 int hdfs_crc32c_set_store_policy(int policy) {
   if (policy < 0 || policy > 13) return fail(HDFS_CRC32C_EINVAL, "store policy 0..13");
   g_store_policy = uint32_t(policy);
+  return HDFS_CRC32C_OK;
+}
+
+int hdfs_crc32c_set_runs(int on) {
+  g_runs = on ? 1 : 0;
   return HDFS_CRC32C_OK;
 }
 

@@ -37,6 +37,11 @@ hipError_t launch_small_chunks(int mode, const uint8_t *p, uint32_t len, uint32_
                                uint32_t be, const uint32_t *expect, const uint32_t *tab, const uint32_t *pow2,
                                uint32_t *meta, uint32_t *crcs, uint32_t seq, hipStream_t stream);
 hipError_t launch_prep(uint32_t *fb, uint32_t nfb, unsigned long long *mism, uint32_t *gctr, hipStream_t stream);
+// Resident mailbox kernel (one workgroup; exits on a quit request or after
+// idle_ticks of 10 ns without one; status[0] = (epoch << 1) | alive).
+hipError_t launch_mailbox(const uint32_t *req, const uint8_t *in, uint32_t *meta, uint32_t *crcs, const uint32_t *tab0,
+                          const uint32_t *tab1, const uint32_t *pow0, const uint32_t *pow1, uint32_t *status,
+                          uint32_t epoch, uint32_t seq0, uint32_t idle_ticks, hipStream_t stream);
 hipError_t launch_gather(const uint8_t *raw, const PktDesc *descs, uint32_t npk, uint32_t units, uint8_t *arena,
                          uint8_t *crc_arena, hipStream_t stream);
 // proto 1 / 2: derive the stride from the packet at base (v1 / v2 header)
@@ -154,6 +159,15 @@ struct DevCtx {
   uint32_t grid_seq = 0;
   hipStream_t r_stream = nullptr;  // device framing: record copies of runs with many exceptions
   std::vector<GridSlot> grid;
+  // opt-in resident mailbox (guarded by mu): pinned request line ([0..3]
+  // seq, len, chunk_size | flags, register) and status word ([16])
+  bool mb_on = false, mb_alive = false;
+  uint32_t *h_mb = nullptr, *dv_mb = nullptr;
+  hipStream_t mb_stream = nullptr;
+  uint32_t mb_epoch = 0, mb_idle_ticks = 0;
+  uint64_t mb_calls = 0, mb_launches = 0;
+  // CUs the bulk (one-workgroup-per-CU) kernels may use
+  int bulk_cus() const { return num_cu - (mb_on ? 1 : 0); }
   std::mutex mu;
 };
 
@@ -184,7 +198,11 @@ bool is_pinned_host(const void *p);
 int launch_all(DevCtx &c, int mode, const SegDev *d_segs, uint32_t nseg, uint64_t rounds, uint64_t mtiles,
                uint64_t gtiles, uint32_t *d_fb, unsigned long long *d_mism, uint32_t *d_gctr, hipStream_t st,
                hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, bool reset = true, int ctype = 0,
-               bool copy = false, bool gctr_zeroed = false, bool una = false, uint32_t utiles = 0);
+               bool copy = false, bool gctr_zeroed = false, bool una = false, uint32_t utiles = 0,
+               bool runs = false);
+// Every segment's main tiles come in whole 8-tile groups (compute mode can
+// then run schedule 4: one wave per group, one 256-B CRC store per group).
+bool whole_groups(const SegDev *segs, size_t n);
 // Main tiles per segment when the table is uniform (every segment but the
 // last has the same main_tiles T, the last at most T), else 0.
 uint32_t uniform_tiles(const SegDev *segs, size_t n);

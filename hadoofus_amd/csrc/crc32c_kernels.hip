@@ -182,7 +182,14 @@ struct Cursor {
 //    streams; the read probes of crc32c_probes.hip measured this shape
 //    faster on MI355X HBM.  Groups of >= 4 tiles own whole 128-B lines of
 //    expected / computed CRCs (8 chunks x 4 B per tile), so no two XCDs'
-//    L2s fetch or write the same CRC line (default 8 tiles per group).  Unit size (runtime,
+//    L2s fetch or write the same CRC line (default 8 tiles per group).
+//  ORDER 4 (runs, compute mode): as ORDER 3 with 8-tile groups, but a ticket
+//    is a whole group and ONE wave processes its 8 tiles in a row, collecting
+//    the 64 CRCs in one register (lane 8j + q = tile j, chunk q) and writing
+//    them as one 256-B store (two whole lines) instead of eight 32-B stores
+//    from eight waves: each store that leaves the CU costs, per instruction
+//    as well as per byte (tools/exp_knobs.py, profiles/r02/).  Needs every
+//    segment's main tiles to be a multiple of 8 (the host checks).  Unit size (runtime,
 //    a power of two in [16, 256]) targets >= 4 units per workgroup; launches
 //    with < 32 rounds per wave skip the pool (one unit per workgroup would
 //    make the tail, not shorten it).
@@ -228,14 +235,19 @@ DEV uint32_t grab(const Sched &w) {
 template <int ORDER>
 DEV bool ticket_tile(const Sched &w, uint32_t t, uint64_t &g) {
   if (t < w.nk) {
-    if (ORDER == 3)
+    if (ORDER == 4)
+      g = (w.gfirst + uint64_t(t) * w.gstride) << 3;
+    else if (ORDER == 3)
       g = ((w.gfirst + uint64_t(t >> w.gshift) * w.gstride) << w.gshift) + (t & ((1u << w.gshift) - 1u));
     else
       g = w.gfirst + t;
     return true;
   }
   if (ORDER < 2) return false;
-  const uint32_t j = t - w.nk, u = j >> w.ushift, o = j & ((1u << w.ushift) - 1u), s = u % kSlots;
+  // ORDER 4: a ticket is 8 tiles, a pool unit 2^(ushift - 3) tickets
+  constexpr uint32_t tsh = ORDER == 4 ? 3u : 0u;
+  const uint32_t j = t - w.nk, u = j >> (w.ushift - tsh), o = (j & ((1u << (w.ushift - tsh)) - 1u)) << tsh,
+                 s = u % kSlots;
   if (o == 0) {  // first ticket of local unit u: claim a pool unit and publish it
     uint32_t gu = 0;
     if (w.lane == 0) gu = atomicAdd(w.gctr, 1u);
@@ -271,6 +283,11 @@ DEV Cursor advance(Cursor c, SegP segs, uint32_t nseg, const Sched &w, SegCache 
     c.r++;
     return c;
   }
+  if (ORDER == 4 && ((c.tile + 1u) & 7u) != 0u) {  // the run's next tile (main tiles come in whole groups)
+    c.tile++;
+    c.r = 0;
+    return c;
+  }
   if (ORDER != 0) {
     uint64_t g;
     if (!ticket_tile<ORDER>(w, grab(w), g)) {
@@ -283,7 +300,7 @@ DEV Cursor advance(Cursor c, SegP segs, uint32_t nseg, const Sched &w, SegCache 
     // interleaved tiles jump G ahead.  Short hops walk, long ones search.
     const uint64_t end = sh.mtile_start + sh.main_tiles;
     if (w.ut && (g < sh.mtile_start || g >= end)) return ulocate(w, g);
-    if (g < sh.mtile_start || g >= end + (ORDER == 3 ? 0u : kWalkTiles)) {
+    if (g < sh.mtile_start || g >= end + (ORDER >= 3 ? 0u : kWalkTiles)) {
       uint32_t lo = 0, hi = nseg;
       while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
@@ -426,9 +443,10 @@ struct LaneConst {
 // them.  Every round therefore issues exactly the same vector-memory ops
 // (4 loads, [1 expected-CRC load], 1 store) and the compiler's vmcnt waits
 // stay exact.
-template <int MODE>
+template <int MODE, int RUN>
 DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, uint32_t st, const LaneConst &L,
-                uint32_t *__restrict__ first_bad, unsigned long long *__restrict__ mism, SegCache &kc) {
+                uint32_t *__restrict__ first_bad, unsigned long long *__restrict__ mism, SegCache &kc,
+                uint32_t &acc) {
   const SegHot &sh = hot(kc, segs, c.seg).h;
   const bool last = c.valid && (c.r + 1 == sh.chunk_size / kRoundBytes);
   const uint32_t flags = sh.flags;
@@ -454,6 +472,20 @@ DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, ui
   if (MODE == kModeCompute) {
     const bool keep = last && !(kDiag && L.store_policy == 2);
     const uint32_t val = (flags & kSegBigEndian) ? __builtin_bswap32(out) : out;
+    if constexpr (RUN) {
+      // ORDER 4: lane 8j + q collects chunk q of the run's tile j from that
+      // chunk's leader lane 8q; the run's last tile writes the 64 CRCs of
+      // its 8 tiles (256 B, whole lines) with one sc1 store
+      const uint32_t j = c.tile & 7u;
+      const uint32_t v =
+          static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(static_cast<int>((L.lane & 7u) * 32u), static_cast<int>(val)));
+      acc = (last && (L.lane >> 3) == j) ? v : acc;
+      const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+          reinterpret_cast<uint32_t *>(rfl64(reinterpret_cast<uint64_t>(sh.crcs + (c.tile & ~7u) * kTileChunks))), 0,
+          static_cast<int>(rfl(last && j == 7u ? (56u + nch) * 4u : 0u)), 0x00020000);
+      __builtin_amdgcn_raw_buffer_store_b32(acc, rr, L.lane * 4u, 0, 16);
+      return;
+    }
     if (kDiag && L.store_policy == 3) {
       // diagnostic: 128-B full-line write per tile (crcs must hold 16 B per chunk)
       const __amdgpu_buffer_rsrc_t r4 = __builtin_amdgcn_make_buffer_rsrc(
@@ -544,10 +576,11 @@ DEV void copy_round(const uint32_t (&d)[16], const Cursor c, SegP segs, const La
 // The S slicing chains are independent and interleaved step by step, so one
 // lane keeps S table lookups in flight (latency hiding by ILP, not waves).
 
-template <int MODE, int S, int COPY, int UNA>
+template <int MODE, int S, int COPY, int UNA, int RUN>
 DEV void process(const uint32_t *lds, uint32_t (&d)[S][16], const uint32_t (&exp)[S], const uint32_t (&tl)[S],
                  const uint32_t (&sh_a)[S], const Cursor (&c)[S], SegP segs, uint32_t (&st)[S], const LaneConst &L,
-                 uint32_t *__restrict__ first_bad, unsigned long long *__restrict__ mism, SegCache (&kc)[S]) {
+                 uint32_t *__restrict__ first_bad, unsigned long long *__restrict__ mism, SegCache (&kc)[S],
+                 uint32_t (&acc)[S]) {
   if constexpr (kDiag && MODE == kModeLoadOnly) {
     // Diagnostic twin of verify (diagnostic build only): the same loads and
     // the same bitmap store op with its record dropped, no CRC arithmetic.
@@ -608,7 +641,7 @@ DEV void process(const uint32_t *lds, uint32_t (&d)[S][16], const uint32_t (&exp
 #pragma unroll
   for (int s = 0; s < S; s++) st[s] = slice4(lds, x[s], 0u, L.lb0, L.lb1);
 #pragma unroll
-  for (int s = 0; s < S; s++) finish<MODE>(lds, exp[s], c[s], segs, st[s], L, first_bad, mism, kc[s]);
+  for (int s = 0; s < S; s++) finish<MODE, RUN>(lds, exp[s], c[s], segs, st[s], L, first_bad, mism, kc[s], acc[s]);
 }
 
 // Tiled kernel.  MODE compute / verify; ORDER schedule (above); NT
@@ -721,9 +754,9 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
     }
   } else {
     const bool pool = ORDER >= 2 && total_rounds >= 32ull * nwaves * S;
-    if (ORDER == 3) {
+    if (ORDER >= 3) {
       // static phase: whole groups only; the pool takes the rest
-      w.gshift = (tune >> 8) & 15u;
+      w.gshift = ORDER == 4 ? 3u : (tune >> 8) & 15u;
       const uint64_t ngroups = (pool ? total_tiles * kPhase1Num / kPhase1Den : total_tiles) >> w.gshift;
       // tune bit 12: XCD-major dealing.  Workgroups are dispatched to the 8
       // XCDs round-robin (XCD = blockIdx % 8), so with the plain dealing the
@@ -733,8 +766,10 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
       const uint32_t b = blockIdx.x, G = gridDim.x;
       w.gfirst = ((tune >> 12) & 1u) && (G % 8u) == 0 ? (b % 8u) * (G / 8u) + b / 8u : b;
       w.gstride = gridDim.x;
-      w.nk = ngroups > w.gfirst ? static_cast<uint32_t>(((ngroups - 1 - w.gfirst) / gridDim.x + 1) << w.gshift)
-                                : 0u;
+      // tickets of the static phase: tiles (ORDER 3) or whole groups (ORDER 4)
+      w.nk = ngroups > w.gfirst
+                 ? static_cast<uint32_t>(((ngroups - 1 - w.gfirst) / gridDim.x + 1) << (ORDER == 4 ? 0u : w.gshift))
+                 : 0u;
       w.p2first = ngroups << w.gshift;
     } else {
       const uint64_t r_static = pool ? total_rounds * kPhase1Num / kPhase1Den : total_rounds;
@@ -795,11 +830,13 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
   uint32_t tl[DEPTH][S];   // UNA: lanes 0..7, the dword after chunk lane's round part
   uint32_t sha[DEPTH][S];  // UNA: byte shift of the round's segment
   uint32_t st[S];
+  uint32_t acc[S];  // ORDER 4 compute: the current run's CRCs, lane 8j + q = tile j, chunk q
   LaneOff lo{0u, {0u, 0u, 0u, 0u}, 0u};
   SegCache kc[S];
 #pragma unroll
   for (int s = 0; s < S; s++) {
     st[s] = 0u;
+    acc[s] = 0u;
     kc[s].seg = 0xFFFFFFFFu;
   }
 #pragma unroll
@@ -821,7 +858,9 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
   for (;;) {
 #pragma unroll
     for (int k = 0; k < DEPTH; k++) {
-      process<MODE, S, COPY, UNA>(lds, buf[k], ex[k], tl[k], sha[k], cur[k], sg, st, L, first_bad, mism, kc);
+      process<MODE, S, COPY, UNA, (ORDER == 4 && MODE == kModeCompute) ? 1 : 0>(lds, buf[k], ex[k], tl[k], sha[k],
+                                                                                cur[k], sg, st, L, first_bad, mism,
+                                                                                kc, acc);
 #pragma unroll
       for (int s = 0; s < S; s++) nrounds += cur[k][s].valid ? 1u : 0u;
       const int prev = (k + DEPTH - 1) % DEPTH;
@@ -1102,6 +1141,183 @@ __global__ __launch_bounds__(1024) void small_chunks_kernel(const uint8_t *__res
     __threadfence_system();
     if (tid == 0) __hip_atomic_store(&meta[2], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
+}
+
+// Resident "mailbox" variant of small_chunks_kernel (opt-in,
+// hdfs_crc32c_mailbox_create): ONE workgroup stays on one CU with both
+// table sets in LDS and serves the synchronous small calls (_hdfs_crc32c and
+// aliases, verify_crcdata, compose_crcs on <= 64 KiB of host memory,
+// src/datanode.c:2470-2476 is the per-packet call pattern) without a kernel
+// launch per call.  The host writes the caller's bytes to the pinned input
+// stage and then a 16-B request {seq, len, cs | flags, reg0}; wave 0 polls
+// that line over PCIe (system-coherent loads), the block reads the data with
+// coalesced system-coherent 1 KiB loads, and lane L of wave w ends up with
+// bytes [4096 w + 64 L, +64) (the tiled kernel's load order + permlane
+// transpose).  Results go to the same pinned output block as
+// small_chunks_kernel, its completion sequence number last.  Requests must
+// have chunk_size % 64 == 0 or a single chunk (else the host launches
+// small_chunks_kernel).  Exit: a quit request, or idle_ticks (100 MHz
+// s_memrealtime) without a request -- every wave leaves through the same
+// barrier-synchronised test; status[0] = (epoch << 1) | alive.
+
+DEV u32x4 sysload16(const __amdgpu_buffer_rsrc_t r, uint32_t off) {
+  // sc0 sc1: system-coherent, never served from a stale cache line
+  return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 17));
+}
+
+__global__ __launch_bounds__(1024) void mailbox_kernel(const uint32_t *__restrict__ req, const uint8_t *__restrict__ in,
+                                                       uint32_t *__restrict__ meta, uint32_t *__restrict__ crcs,
+                                                       const uint32_t *__restrict__ tab0, const uint32_t *__restrict__ tab1,
+                                                       const uint32_t *__restrict__ pow0, const uint32_t *__restrict__ pow1,
+                                                       uint32_t *__restrict__ status, uint32_t epoch, uint32_t seq0,
+                                                       uint32_t idle_ticks) {
+  __shared__ uint32_t tt[2][1024];                                    // t0..t3 per checksum type
+  __shared__ __attribute__((aligned(16))) uint32_t zt[2][16 * 1024];  // Z_{2^b}, b < 16, per type
+  __shared__ uint32_t acc[kSmallMaxChunks];
+  __shared__ uint32_t res[2];
+  __shared__ uint32_t ctl[4];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+  // tables once for the kernel's lifetime
+  tt[0][tid] = tab0[tid];
+  tt[1][tid] = tab1[tid];
+#pragma unroll
+  for (uint32_t k = 0; k < 4; k++) {
+    const uint32_t q = k * 1024u + tid;
+    *reinterpret_cast<u32x4 *>(&zt[0][4u * q]) = gload16(pow0 + 4u * q);
+    *reinterpret_cast<u32x4 *>(&zt[1][4u * q]) = gload16(pow1 + 4u * q);
+  }
+  const __amdgpu_buffer_rsrc_t rin =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(in), 0, static_cast<int>(kSmallMax + 4u * kSmallMaxChunks),
+                                        0x00020000);
+  // tiled-kernel load order for one 4 KiB round of 8 x 512 B (see issue())
+  const uint32_t hsel = (lane >> 3) & 1u, loff = 16u * (4u * (lane & 7u) + (lane >> 4));
+  uint32_t last = seq0;
+  uint64_t t_idle = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    if (tid == 0) {
+      u32x4 v;
+      for (;;) {
+        // volatile: a plain (or buffer-intrinsic) load is hoisted out of the
+        // loop by the compiler, which then spins on a stale value; volatile
+        // global loads are also system-coherent (sc0 sc1) on gfx950
+        v = *(const volatile GAS u32x4 *)(const GAS uint8_t *)req;
+        if (v.x != last) break;
+        if (__builtin_amdgcn_s_memrealtime() - t_idle > idle_ticks) {
+          v = u32x4{last, 0u, kMbQuitFlag, 0u};
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      ctl[0] = v.x;
+      ctl[1] = v.y;
+      ctl[2] = v.z;
+      ctl[3] = v.w;
+      res[0] = 0xFFFFFFFFu;
+      res[1] = 0u;
+    }
+    __syncthreads();
+    const uint32_t seq = ctl[0], len = ctl[1], csf = ctl[2], reg0 = ctl[3];
+    if (csf & kMbQuitFlag) break;  // uniform: every wave leaves here
+    const uint32_t cs = csf & 0x1FFFFu, ct = (csf & kMbCrc32Flag) ? 1u : 0u;
+    const bool verify = (csf & kMbVerifyFlag) != 0u, be = (csf & kMbBeFlag) != 0u;
+    const uint32_t nch = (len + cs - 1u) / cs;
+    for (uint32_t j = tid; j < nch; j += 1024u) acc[j] = 0u;
+    // every load before any compute: one PCIe round trip
+    uint32_t d[16] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    const uint32_t base = 4096u * w;
+    if (base < len) {
+#pragma unroll
+      for (uint32_t k = 0; k < 4; k++) {
+        const u32x4 x = sysload16(rin, base + (2u * k + hsel) * 512u + loff);
+        d[4 * k + 0] = x.x;
+        d[4 * k + 1] = x.y;
+        d[4 * k + 2] = x.z;
+        d[4 * k + 3] = x.w;
+      }
+    }
+    uint32_t ev[2] = {0u, 0u};
+    if (verify) {
+#pragma unroll
+      for (uint32_t k = 0; k < 2; k++)
+        if (k * 1024u + tid < nch)
+          ev[k] = __builtin_amdgcn_raw_buffer_load_b32(rin, kSmallMax + 4u * (k * 1024u + tid), 0, 17);
+    }
+    __syncthreads();  // acc cleared
+    if (base < len) {
+      transpose(d);
+      const uint32_t b0 = 64u * (64u * w + lane);  // this lane's piece
+      if (b0 < len) {
+        const uint32_t j = b0 / cs, ce = min((j + 1u) * cs, len), n = min(64u, ce - b0);
+        const uint32_t *t = tt[ct];
+        uint32_t c = (b0 == j * cs) ? reg0 : 0u;
+#pragma unroll
+        for (uint32_t q = 0; q < 16; q++) {
+          if (4u * q + 4u <= n) {
+            const uint32_t x = c ^ d[q];
+            c = t[768u + (x & 0xffu)] ^ t[512u + ((x >> 8) & 0xffu)] ^ t[256u + ((x >> 16) & 0xffu)] ^ t[x >> 24];
+          }
+        }
+        if (n & 3u) {
+          uint32_t tw = 0u;
+#pragma unroll
+          for (uint32_t q = 0; q < 16; q++) tw = (q == (n >> 2)) ? d[q] : tw;
+          for (uint32_t b = 0; b < (n & 3u); b++) c = t[(c ^ (tw >> (8u * b))) & 0xffu] ^ (c >> 8);
+        }
+        const uint32_t *z0 = zt[ct];
+        for (uint32_t dd = ce - b0 - n, lvl = 0; dd; lvl++, dd >>= 1) {
+          if (dd & 1u) {
+            const uint32_t *z = z0 + lvl * 1024u;
+            c = z[c & 0xffu] ^ z[256u + ((c >> 8) & 0xffu)] ^ z[512u + ((c >> 16) & 0xffu)] ^ z[768u + (c >> 24)];
+          }
+        }
+        atomicXor(&acc[j], c);
+      }
+    }
+    __syncthreads();
+    if (verify) {
+#pragma unroll
+      for (uint32_t k = 0; k < 2; k++) {
+        const uint32_t j = k * 1024u + tid;
+        if (j < nch && (be ? __builtin_bswap32(ev[k]) : ev[k]) != ~acc[j]) {
+          atomicMin(&res[0], j);
+          atomicAdd(&res[1], 1u);
+        }
+      }
+      __syncthreads();
+    }
+    // Completion: {first bad, mismatches, seq, CRC of a single chunk} as ONE
+    // 16-B system-scope store, so verify and single-chunk calls need no
+    // fence round trip; multi-chunk CRC arrays go first, then one fence.
+    if (w == 0) {
+      const bool one = verify || nch == 1u;
+      if (!one) {
+        for (uint32_t j = lane; j < nch; j += 64u) {
+          const uint32_t v = ~acc[j];
+          crcs[j] = be ? __builtin_bswap32(v) : v;
+        }
+        __threadfence_system();
+      }
+      if (lane == 0) {
+        const uint32_t v0 = ~acc[0];
+        *(volatile GAS u32x4 *)(GAS uint8_t *)meta = u32x4{res[0], res[1], seq, be ? __builtin_bswap32(v0) : v0};
+      }
+    }
+    last = seq;
+    t_idle = __builtin_amdgcn_s_memrealtime();
+    __syncthreads();  // ctl / res / acc are rewritten by the next request
+  }
+  if (tid == 0) {
+    __threadfence_system();
+    __hip_atomic_store(&status[0], epoch << 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+hipError_t launch_mailbox(const uint32_t *req, const uint8_t *in, uint32_t *meta, uint32_t *crcs, const uint32_t *tab0,
+                          const uint32_t *tab1, const uint32_t *pow0, const uint32_t *pow1, uint32_t *status,
+                          uint32_t epoch, uint32_t seq0, uint32_t idle_ticks, hipStream_t stream) {
+  hipLaunchKernelGGL(mailbox_kernel, dim3(1), dim3(1024), 0, stream, req, in, meta, crcs, tab0, tab1, pow0, pow1, status,
+                     epoch, seq0, idle_ticks);
+  return hipGetLastError();
 }
 
 // Composite CRC of whole segments from their chunk CRCs (no data re-read):
@@ -1749,6 +1965,7 @@ hipError_t launch_tiles(int mode, int order, int nt, int depth, int streams, int
     else return hipErrorInvalidValue;
   } else {
     HDFS_LAUNCH_PRODUCT(kModeCompute)
+    else if (HDFS_SHAPE(4, 2, 3, 1, 1024)) HDFS_LAUNCH(kModeCompute, 4, 1, 3, 1, 1024, 1);
     else return hipErrorInvalidValue;
   }
 #else
@@ -1780,6 +1997,7 @@ hipError_t launch_tiles(int mode, int order, int nt, int depth, int streams, int
     else return hipErrorInvalidValue;
   } else {
     HDFS_LAUNCH_ALL(kModeCompute)
+    else if (HDFS_SHAPE(4, 2, 3, 1, 1024)) HDFS_LAUNCH(kModeCompute, 4, 1, 3, 1, 1024, 1);
     else return hipErrorInvalidValue;
   }
 #undef HDFS_LAUNCH_ALL

@@ -298,6 +298,26 @@ int hdfs_crc32c_verify_host(const void *data, uint64_t len, uint32_t chunk_size,
 int hdfs_crc32c_host_alloc(void **p, uint64_t bytes);
 int hdfs_crc32c_host_free(void *p);
 
+/* ---- resident mailbox for the synchronous small calls ------------------- */
+/* Opt-in latency mode for the reference's per-packet call pattern
+ * (_verify_crcdata per received packet, src/datanode.c:2470-2476; the
+ * drop-in _hdfs_crc32c family; compose_crcs): while a mailbox is open on the
+ * engine's device, ONE workgroup of the engine stays resident on one CU with
+ * its tables in LDS and serves the synchronous calls on <= 64 KiB of host
+ * memory (chunk size a multiple of 64, or a single chunk) from a request
+ * line in pinned memory -- no kernel launch per call.  Other calls keep
+ * their one-launch path.  The resident kernel exits on its own after idle_ms
+ * without a request (0: 50 ms; the next call relaunches it) and on destroy.
+ * While a mailbox is open the engine's bulk kernels use one CU fewer, and a
+ * device-wide synchronisation (hipDeviceSynchronize, torch.cuda.synchronize)
+ * waits for the resident kernel's idle exit: synchronise streams instead.
+ * One mailbox per device (EBUSY-style HDFS_CRC32C_EINVAL for a second). */
+typedef struct hdfs_crc32c_mailbox hdfs_crc32c_mailbox;
+int hdfs_crc32c_mailbox_create(hdfs_crc32c_mailbox **mb, uint32_t idle_ms);
+/* Calls served by the resident kernel and kernel launches (first + relaunches after idle exits). */
+int hdfs_crc32c_mailbox_stats(const hdfs_crc32c_mailbox *mb, uint64_t *calls, uint64_t *launches);
+int hdfs_crc32c_mailbox_destroy(hdfs_crc32c_mailbox *mb);
+
 /* ---- device memory + synthetic data helpers (bench / tests) ------------- */
 int hdfs_crc32c_dev_alloc(void **dptr, uint64_t bytes);
 int hdfs_crc32c_dev_free(void *dptr);
@@ -315,7 +335,8 @@ int hdfs_crc32c_corrupt(void *dptr, uint64_t len, uint32_t chunk, uint64_t chunk
 /* Elapsed device time of `iters` back-to-back plan executions on `stream`
  * measured with HIP events (ms per execution). */
 int hdfs_crc32c_plan_time(hdfs_crc32c_plan *plan, void *stream, int iters, double *ms_per_iter);
-/* hipDeviceSynchronize on the engine's device. */
+/* hipDeviceSynchronize on the engine's device (with a mailbox open: the
+ * engine's streams and the NULL stream, not the resident kernel). */
 int hdfs_crc32c_device_sync(void);
 
 #ifdef __cplusplus

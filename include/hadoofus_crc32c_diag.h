@@ -63,6 +63,10 @@ int hdfs_crc32c_set_shape(int streams, int block);
  * undefined.
  * Env HDFS_CRC32C_STORE. */
 int hdfs_crc32c_set_store_policy(int policy);
+/* Compute plans over whole 8-tile groups run schedule 4 (one wave per group,
+ * one 256-B CRC store per group): 1 (default) or 0 (schedule 3).
+ * Env HDFS_CRC32C_RUNS. */
+int hdfs_crc32c_set_runs(int on);
 /* Empirical streaming-read bandwidth of `bytes` at dptr (GB/s, 1e9 B/s):
  * fully coalesced 16-B-per-lane loads, no compute; the measured roofline. */
 int hdfs_crc32c_probe_read(const void *dptr, uint64_t bytes, void *stream, int iters, double *gbps);

@@ -55,7 +55,7 @@ def test_release_has_no_diagnostic_knobs(libpath, diagpath):
     dia = open(diagpath, "rb").read()
     for var in (b"HDFS_CRC32C_STORE", b"HDFS_CRC32C_TILE_ORDER", b"HDFS_CRC32C_NT", b"HDFS_CRC32C_DEPTH",
                 b"HDFS_CRC32C_STREAMS", b"HDFS_CRC32C_BLOCK", b"HDFS_CRC32C_GROUP", b"HDFS_CRC32C_ALIGN",
-                b"HDFS_CRC32C_SMALL_RULE", b"HDFS_CRC32C_XCD"):
+                b"HDFS_CRC32C_SMALL_RULE", b"HDFS_CRC32C_XCD", b"HDFS_CRC32C_RUNS"):
         assert var not in rel, var
         assert var in dia, var
 
@@ -64,8 +64,9 @@ def test_release_kernels_are_the_product_shapes(libpath, diagpath):
     """The release build's tiled kernels are the two product shapes (schedule
     3 with buffer loads, schedule 2) in their product variants only: compute
     and verify, each with and without the realigning path for byte-unaligned
-    data, verify also with the fused copy-out -- twelve in all; no load-only
-    twin (mode 2) and no read probes.  The diagnostic build has them."""
+    data, verify also with the fused copy-out -- twelve in all -- plus
+    compute on schedule 4 (runs of whole 8-tile groups); no load-only twin
+    (mode 2) and no read probes.  The diagnostic build has them."""
     import re as _re
     rel = open(libpath, "rb").read()
     dia = open(diagpath, "rb").read()
@@ -75,6 +76,7 @@ def test_release_kernels_are_the_product_shapes(libpath, diagpath):
     variants = [(b"0", b"0", b"0"), (b"0", b"0", b"1")] + [(b"1", cp, un) for cp in (b"0", b"1") for un in (b"0", b"1")]
     want = {(m, o, b"1", b"3", b"1", b"1024", buf, cp, un) for m, cp, un in variants
             for o, buf in ((b"3", b"1"), (b"2", b"0"))}
+    want.add((b"0", b"4", b"1", b"3", b"1", b"1024", b"1", b"0", b"0"))
     assert shapes == want, shapes ^ want
     assert b"probe_read_kernel" not in rel and b"probe2_kernel" not in rel
     dshapes = set(_re.findall(pat, dia))

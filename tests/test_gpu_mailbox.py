@@ -1,0 +1,117 @@
+"""Resident mailbox kernel for the synchronous small calls
+(hdfs_crc32c_mailbox_create): the reference's per-packet call pattern
+(_verify_crcdata per received packet, src/datanode.c:2470-2476; the drop-in
+_hdfs_crc32c, src/crc32c.h:13; the write loop, src/datanode.c:2814-2860)
+served by one resident workgroup.  Every result equals the oracle's, calls
+outside the mailbox's shapes keep the launch path, the kernel idles out and
+is relaunched transparently, and bulk plans run beside it."""
+import time
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [1, 3, 63, 64, 65, 100, 511, 512, 513, 4095, 4096, 4097, 30000, 65535, 65536]
+
+
+def _crc_region(oracle, data, cs, ctype):
+    """[BE chunk CRCs | data] as _verify_crcdata reads a packet."""
+    crcs = oracle.compose_crcs([data.tobytes()], cs, ctype=ctype)
+    return np.frombuffer(crcs + data.tobytes(), np.uint8).copy(), len(crcs)
+
+
+def test_mailbox_dropin_and_chaining(engine, oracle):
+    rng = np.random.default_rng(5)
+    with engine.Mailbox() as mb:
+        for n in SIZES + [65537, 200001]:  # the last two: larger than the mailbox serves (launch paths)
+            data = rng.integers(0, 256, n, dtype=np.uint8)
+            for crc0 in (0, 0xDEADBEEF):
+                assert engine.crc32c(crc0, data) == oracle.crc32c(crc0, data), (n, crc0)
+            assert engine.crc32c(0, data, "_hdfs_sw_crc32c") == oracle.crc32c(0, data)
+        a, b = rng.integers(0, 256, 777, dtype=np.uint8), rng.integers(0, 256, 5000, dtype=np.uint8)
+        assert engine.crc32c(engine.crc32c(0, a), b) == oracle.crc32c(0, np.concatenate([a, b]))
+        calls, launches = mb.stats()
+        assert calls >= 2 * len(SIZES) and launches >= 1
+
+
+@pytest.mark.parametrize("ctype", [2, 1])  # CSUM_CRC32C, CSUM_CRC32
+def test_mailbox_verify_crcdata(engine, oracle, ctype):
+    rng = np.random.default_rng(ctype)
+    with engine.Mailbox() as mb:
+        for cs, dlen in ((512, 65536), (512, 40000), (512, 1), (4096, 65536), (64, 65536), (1024, 3000),
+                         (100, 5000), (65536, 65536), (1 << 20, 70000 - 4500)):
+            data = rng.integers(0, 256, dlen, dtype=np.uint8)
+            region, crcdlen = _crc_region(oracle, data, cs, ctype)
+            assert engine.verify_crcdata(region, cs, crcdlen, dlen, ctype) == (0, -1)
+            nch = crcdlen // 4
+            for bad in sorted({0, nch - 1, nch // 2}):
+                r = region.copy()
+                r[crcdlen + bad * cs + int(rng.integers(0, min(cs, dlen - bad * cs)))] ^= 0x10
+                got = engine.verify_crcdata(r, cs, crcdlen, dlen, ctype)
+                assert got == oracle.verify_crcdata(r, cs, crcdlen, dlen, ctype) == (engine.ERR_BAD_CHECKSUM, bad)
+            assert engine.verify_crcdata(region, cs, crcdlen + 4, dlen, ctype)[0] == engine.ERR_CRC_LEN
+        assert mb.stats()[0] > 0
+
+
+def test_mailbox_compose_crcs(engine, oracle):
+    rng = np.random.default_rng(8)
+    data = rng.integers(0, 256, 65536, dtype=np.uint8).tobytes()
+    with engine.Mailbox():
+        for cuts in ([0, 65536], [0, 1, 100, 513, 40000, 65536], [0, 30000]):
+            frags = [data[a:b] for a, b in zip(cuts[:-1], cuts[1:])]
+            for cs in (512, 4096, 100):
+                for ct in (engine.CSUM_CRC32C, engine.CSUM_CRC32):
+                    assert engine.compose_crcs(frags, cs, ctype=ct) == oracle.compose_crcs(frags, cs, ctype=ct)
+
+
+def test_mailbox_idle_exit_and_relaunch(engine, oracle):
+    """A 2 ms idle limit: the resident kernel exits between calls and the next
+    call relaunches it; results stay exact, and destroy after an idle exit is
+    clean."""
+    rng = np.random.default_rng(9)
+    with engine.Mailbox(idle_ms=2) as mb:
+        for i in range(6):
+            data = rng.integers(0, 256, 512 * (i + 1), dtype=np.uint8)
+            assert engine.crc32c(i, data) == oracle.crc32c(i, data)
+            time.sleep(0.02)
+        calls, launches = mb.stats()
+        assert calls == 6 and launches >= 3
+
+
+def test_mailbox_beside_bulk_plans(engine, oracle):
+    """Bulk verify plans (one workgroup per CU, one CU fewer while the
+    mailbox holds one) interleaved with mailbox calls: both exact."""
+    n, cs = 256 << 20, 512
+    per = n // cs
+    data = engine.DeviceBuffer(n)
+    engine.fill_splitmix64(data.ptr, n // 8, 3, 0)
+    crcs = engine.DeviceBuffer(per * 4)
+    bm = engine.DeviceBuffer(per // 8)
+    seg = [engine.Segment(data=data.ptr, len=n, chunk_size=cs, flags=engine.SEG_BE, crc_init=0, crcs=crcs.ptr,
+                          bitmap=bm.ptr)]
+    engine.Plan(engine.MODE_COMPUTE, seg).execute()
+    engine.device_sync()
+    engine.corrupt(data.ptr, n, cs, 0, 65537, 7919)
+    engine.device_sync()
+    rng = np.random.default_rng(10)
+    with engine.Mailbox() as mb:
+        vp = engine.Plan(engine.MODE_VERIFY, seg)
+        for _ in range(3):
+            vp.execute()
+            small = rng.integers(0, 256, 4096, dtype=np.uint8)
+            assert engine.crc32c(0, small) == oracle.crc32c(0, small)
+            fb, m = vp.results()
+            assert m == (per + 65536) // 65537 and fb[0] == 0
+        assert mb.stats()[0] == 3
+    vp.destroy()
+    for b in (data, crcs, bm):
+        b.free()
+
+
+def test_mailbox_one_per_device(engine):
+    with engine.Mailbox():
+        with pytest.raises(engine.CRC32CError):
+            engine.Mailbox()
+    with engine.Mailbox():  # reopened after close
+        pass

@@ -482,3 +482,44 @@ def test_bound_device_explicit(engine):
     engine.init(0)
     dev, bus = engine.bound_device()
     assert dev == 0 and bus.count(":") == 2 and bus.endswith(".0"), bus
+
+
+@pytest.mark.parametrize("cs,seg_chunks,nseg,tail", [
+    (512, 32768, 40, 0),        # 640 MiB: the global pool engaged
+    (512, 8 * 8 * 5 - 3, 64, 1),  # last main tile of each segment holds 5 chunks; one 64 KiB tail segment
+    (4096, 8 * 8 * 3, 20, 0),   # 8 rounds per tile: a run is 64 rounds of one wave
+    (1024, 8 * 8 * 40, 7, 0),
+])
+def test_compute_runs_schedule(engine, oracle, cs, seg_chunks, nseg, tail):
+    """Compute plans whose segments hold whole 8-tile groups run schedule 4:
+    one wave per group, the 64 CRCs of a group gathered in one register and
+    written with one store (src/datanode.c:2814-2860 computes the same chunk
+    CRCs one at a time).  CRC arrays equal the oracle's, nothing outside them
+    is written."""
+    seg_len = seg_chunks * cs
+    lens = [seg_len] * nseg + ([65536 + 100] if tail else [])
+    total = sum(lens)
+    host = oracle.splitmix((total + 7) // 8, seed=cs + nseg).view(np.uint8)[:total]
+    dbuf = engine.DeviceBuffer(total)
+    dbuf.upload(host)
+    nchs = [(n + cs - 1) // cs for n in lens]
+    crcs = engine.DeviceBuffer(4 * (sum(nchs) + 64))
+    crcs.fill(0xA5)
+    segs, off, coff = [], 0, 0
+    for n, c in zip(lens, nchs):
+        segs.append(engine.Segment(data=dbuf.ptr + off, len=n, chunk_size=cs, flags=engine.SEG_BE, crc_init=0,
+                                   crcs=crcs.ptr + 4 * coff, bitmap=None))
+        off += n
+        coff += c
+    p = engine.Plan(engine.MODE_COMPUTE, segs)
+    p.execute()
+    got = crcs.download(4 * (coff + 64), dtype=">u4").astype(np.uint32)
+    off, coff = 0, 0
+    for n, c in zip(lens, nchs):
+        np.testing.assert_array_equal(got[coff:coff + c], oracle.chunk_crcs(host[off:off + n], cs))
+        off += n
+        coff += c
+    assert (got[coff:] == 0xA5A5A5A5).all()
+    p.destroy()
+    dbuf.free()
+    crcs.free()

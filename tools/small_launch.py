@@ -85,4 +85,52 @@ t0 = time.perf_counter()
 for _ in range(200):
     h.verify_packets(pkt)
 out["verify_packets_1x64KiB_us"] = round((time.perf_counter() - t0) / 200 * 1e6, 1)
+
+
+def say(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def raw_call_us(prefix, iters=500):
+    """Per-call wall time of the C entry points called directly through
+    ctypes with prepared pointers (no numpy conversion per call)."""
+    lib = h.load()
+    reg = np.frombuffer(region, np.uint8).copy()
+    fb = ctypes.c_int32(-1)
+    for name, buf in [("512B", x512), ("4KiB", x4k), ("64KiB", x64k)]:
+        p, n = buf.ctypes.data, buf.nbytes
+        say(prefix, name)
+        lib._hdfs_crc32c(0, p, n)
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            lib._hdfs_crc32c(0, p, n)
+        out[f"{prefix}dropin_{name}_us"] = round((time.perf_counter() - t0) / iters * 1e6, 2)
+    rp = reg.ctypes.data
+    say(prefix, "verify_crcdata")
+    assert lib.hdfs_crc32c_verify_crcdata(rp, 512, len(be), 65536, 2, ctypes.byref(fb)) == 0
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        lib.hdfs_crc32c_verify_crcdata(rp, 512, len(be), 65536, 2, ctypes.byref(fb))
+    out[f"{prefix}verify_crcdata_64KiB_us"] = round((time.perf_counter() - t0) / iters * 1e6, 2)
+    # the same 64 KiB packet verified as 4 KiB packets (verify_crcdata per packet, 16 calls)
+    be4 = h.compose_crcs([x4k.tobytes()], 512)
+    r4 = np.frombuffer(be4 + x4k.tobytes(), np.uint8).copy()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        lib.hdfs_crc32c_verify_crcdata(r4.ctypes.data, 512, len(be4), 4096, 2, ctypes.byref(fb))
+    out[f"{prefix}verify_crcdata_4KiB_us"] = round((time.perf_counter() - t0) / iters * 1e6, 2)
+
+
+# ctypes overhead of a trivial call (subtract by eye)
+lib = h.load()
+t0 = time.perf_counter()
+for _ in range(20000):
+    lib.hdfs_crc32c_last_error()
+out["ctypes_call_overhead_us"] = round((time.perf_counter() - t0) / 20000 * 1e6, 3)
+say("launch path")
+raw_call_us("launch_")
+say("mailbox")
+with h.Mailbox() as mb:
+    raw_call_us("mailbox_")
+    out["mailbox_calls_launches"] = list(mb.stats())
 print(json.dumps(out))
