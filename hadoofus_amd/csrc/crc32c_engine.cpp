@@ -219,13 +219,19 @@ bool device_accessible(const void *p) {
   return a.devicePointer != nullptr;
 }
 
-int launch_verify_dyn(DevCtx &c, const SegDev *d_segs, const GridSummary *dyn, uint64_t gtiles_ub, uint32_t *d_fb,
-                      unsigned long long *d_mism, uint32_t *d_gctr, hipStream_t st, int ctype, bool copy) {
+int launch_verify_dyn(DevCtx &c, const SegDev *d_segs, const GridSummary *dyn, uint64_t rounds_ub, uint64_t gtiles_ub,
+                      uint32_t *d_fb, unsigned long long *d_mism, uint32_t *d_gctr, hipStream_t st, int ctype,
+                      bool copy) {
+  // grid from the upper bound of the run's rounds (>= 4 rounds per wave
+  // before adding workgroups, as launch_all): a short run must not make 256
+  // workgroups fill their 156 KiB LDS tables for a handful of tiles
+  const uint64_t want = (rounds_ub + 63) / 64;
+  const int grid = int(want < 1 ? 1 : (want > uint64_t(c.bulk_cus()) ? c.bulk_cus() : want));
   (void)d_gctr;  // zeroed by grid_build_kernel
   // schedule 3: a device-framed run is packets of one wire size, so its table
   // is uniform (dyn->utiles, no segment search per tile); the kernel falls
   // back to searching the table when it is not
-  const hipError_t le = launch_tiles(kModeVerify, 3, g_nt_loads, 3, 1, 1024, c.bulk_cus(), d_segs, 0, 0, 0,
+  const hipError_t le = launch_tiles(kModeVerify, 3, g_nt_loads, 3, 1, 1024, grid, d_segs, 0, 0, 0,
                                      c.d_tab_main_t[ctype], d_fb, d_mism, nullptr,
                                      (g_group_shift << 8) | (g_xcd_major << 12), d_gctr, st, copy ? 1 : 0, 1, dyn);
   if (le == hipErrorInvalidValue) return fail(HDFS_CRC32C_EINVAL, "verify kernel shape not built");

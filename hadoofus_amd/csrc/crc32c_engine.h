@@ -54,8 +54,12 @@ hipError_t launch_header_window(const uint8_t *s, uint64_t len, uint64_t base, u
 hipError_t launch_frame_grid(const uint8_t *s, uint64_t len, uint64_t base, uint32_t count, int proto, uint32_t cs,
                              int ctype, int verify, uint32_t sflags, uint8_t *bm_base, uint8_t *copy_base,
                              uint64_t copy_cap, GridBufs g, hipStream_t stream);
+// One workgroup: the bad-packet list to *bad (device) and, with its count and
+// then seq, to the pinned host area hsum2 (device address; first host_cap
+// entries after 256 bytes).
 hipError_t launch_grid_finalize(const SegDev *segs, uint32_t nseg, const uint32_t *seg2pkt, const uint32_t *fb,
-                                GridBad *bad, uint32_t bad_cap, GridSummary *sum, hipStream_t stream);
+                                GridBad *bad, uint32_t bad_cap, GridSummary *sum, uint8_t *hsum2, uint32_t host_cap,
+                                uint32_t seq, hipStream_t stream);
 
 // ---- errors ----
 extern thread_local char g_err[512];
@@ -210,8 +214,9 @@ uint32_t uniform_tiles(const SegDev *segs, size_t n);
 // sizes read by the kernels from *dyn; grid sized for rounds_ub / gtiles_ub
 // (upper bounds).  Schedule 3 with the uniform-table look-up the summary
 // enables for runs of equal packets, realigning kernel.
-int launch_verify_dyn(DevCtx &c, const SegDev *d_segs, const GridSummary *dyn, uint64_t gtiles_ub, uint32_t *d_fb,
-                      unsigned long long *d_mism, uint32_t *d_gctr, hipStream_t st, int ctype, bool copy);
+int launch_verify_dyn(DevCtx &c, const SegDev *d_segs, const GridSummary *dyn, uint64_t rounds_ub, uint64_t gtiles_ub,
+                      uint32_t *d_fb, unsigned long long *d_mism, uint32_t *d_gctr, hipStream_t st, int ctype,
+                      bool copy);
 // Any segment whose data is not 4-B aligned (selects the realigning kernel).
 bool any_unaligned(const SegDev *segs, size_t n);
 // Copy / compute streams, events and the small pipeline buffers.

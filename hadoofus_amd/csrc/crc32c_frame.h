@@ -69,6 +69,18 @@ HDFS_HD uint64_t varint_val(const uint8_t *p, size_t n) {
 }
 
 HDFS_HD bool decode_header(const uint8_t *p, size_t n, Header &h) {
+  // Canonical encoding (what HDFS and protobuf-c emit: fields 1..4 in order,
+  // one-byte bools, syncBlock only when present): read at fixed offsets.
+  // Gives exactly what the general scan below gives for these bytes.
+  if ((n == 25 || n == 27) && p[0] == 0x09 && p[9] == 0x11 && p[18] == 0x18 && p[19] < 0x80 && p[20] == 0x25 &&
+      (n == 25 || (p[25] == 0x28 && p[26] < 0x80))) {
+    h.offset = int64_t(le64(p + 1));
+    h.seqno = int64_t(le64(p + 10));
+    h.last = p[19] != 0;
+    h.dlen = int32_t(le32(p + 21));
+    h.sync = n == 27 && p[26] != 0;
+    return true;
+  }
   unsigned seen = 0;
   size_t pos = 0;
   while (pos < n) {

@@ -895,6 +895,9 @@ __global__ __launch_bounds__(256) void crc32c_generic_kernel(
     nseg = dyn->nseg;
     total_gtiles = dyn->gtiles;
   }
+  // blocks past the work leave before the table load (a device-built run
+  // usually has no generic tiles at all: the whole grid exits here)
+  if (static_cast<uint64_t>(blockIdx.x) * blockDim.x / kTileChunks >= total_gtiles) return;
   __shared__ uint32_t tt[1024];
   for (uint32_t i = threadIdx.x; i < 1024u; i += blockDim.x) tt[i] = gtab[i];
   __syncthreads();
@@ -1783,11 +1786,15 @@ __global__ __launch_bounds__(kGridBlock) void grid_build_kernel(
   }
   // 7. the last block to finish publishes the summary, packet 0's record and
   // the exceptions to pinned host memory, then (one system-scope fence later)
-  // the sequence number the host polls.  Every thread fences its own stores
-  // before the block counts itself done.
-  __threadfence();
+  // the sequence number the host polls.  The barrier makes every wave's
+  // stores complete (workgroup release: they are in this XCD's L2); ONE
+  // agent-scope fence then writes the L2 back for the other XCDs before the
+  // block counts itself done (not one fence per thread).
   __syncthreads();
-  if (t == 0) islast = atomicAdd(&done[0], 1u) == nblk - 1u ? 1u : 0u;
+  if (t == 0) {
+    __threadfence();
+    islast = atomicAdd(&done[0], 1u) == nblk - 1u ? 1u : 0u;
+  }
   __syncthreads();
   if (!islast) return;
   __threadfence();  // acquire: the other blocks' summary fields, flags and exception slots
@@ -1817,24 +1824,46 @@ __global__ __launch_bounds__(kGridBlock) void grid_build_kernel(
 
 // After verify: every segment with a bad chunk -> one compact GridBad entry
 // (packet index, first bad chunk, number of bad chunks from its bitmap).
-__global__ __launch_bounds__(256) void grid_finalize_kernel(const SegDev *__restrict__ segs, uint32_t nseg,
-                                                            const uint32_t *__restrict__ seg2pkt,
-                                                            const uint32_t *__restrict__ fb,
-                                                            GridBad *__restrict__ bad, uint32_t bad_cap,
-                                                            GridSummary *__restrict__ sum) {
-  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+// One workgroup, so it can publish without a cross-block protocol: the
+// first host_cap entries and the count go straight to pinned host memory
+// (hsum2: a GridSummary whose nbad / seq fields are written, then the list),
+// every entry to the device list; one system fence, then the sequence
+// number the host polls -- no copy launch behind the verify kernel.
+__global__ __launch_bounds__(1024) void grid_finalize_kernel(const SegDev *__restrict__ segs, uint32_t nseg,
+                                                             const uint32_t *__restrict__ seg2pkt,
+                                                             const uint32_t *__restrict__ fb,
+                                                             GridBad *__restrict__ bad, uint32_t bad_cap,
+                                                             GridSummary *__restrict__ sum, uint8_t *__restrict__ hsum2,
+                                                             uint32_t host_cap, uint32_t seq) {
+  __shared__ uint32_t nb;
+  if (threadIdx.x == 0) nb = 0u;
+  __syncthreads();
   if (nseg == 0xFFFFFFFFu) nseg = sum->nseg;  // launched before the host knows the run's size
-  if (i >= nseg || fb[i] == 0xFFFFFFFFu) return;
-  const SegDev d = segs[i];
-  const uint32_t nb = (d.nchunks + 7u) / 8u;
-  uint32_t n = 0;
-  for (uint32_t j = 0; j < nb; j++) {
-    uint32_t byte = d.bitmap[j];
-    if (j == d.nchunks / 8u) byte &= (1u << (d.nchunks % 8u)) - 1u;  // bits past the last chunk
-    n += __builtin_popcount(byte);
+  auto *hbad = reinterpret_cast<GridBad *>(hsum2 + 256);
+  for (uint32_t i = threadIdx.x; i < nseg; i += 1024u) {
+    if (fb[i] == 0xFFFFFFFFu) continue;
+    const SegDev d = segs[i];
+    const uint32_t nbyte = (d.nchunks + 7u) / 8u;
+    uint32_t n = 0;
+    for (uint32_t j = 0; j < nbyte; j++) {
+      uint32_t byte = d.bitmap[j];
+      if (j == d.nchunks / 8u) byte &= (1u << (d.nchunks % 8u)) - 1u;  // bits past the last chunk
+      n += __builtin_popcount(byte);
+    }
+    const uint32_t slot = atomicAdd(&nb, 1u);
+    const GridBad g{seg2pkt[i], int32_t(fb[i]), n, 0u};
+    if (slot < bad_cap) bad[slot] = g;
+    if (slot < host_cap) hbad[slot] = g;
   }
-  const uint32_t slot = atomicAdd(&sum->nbad, 1u);
-  if (slot < bad_cap) bad[slot] = GridBad{seg2pkt[i], int32_t(fb[i]), n, 0u};
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    sum->nbad = nb;
+    reinterpret_cast<GridSummary *>(hsum2)->nbad = nb;
+  }
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0)
+    __hip_atomic_store(&reinterpret_cast<GridSummary *>(hsum2)->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 hipError_t launch_frame_grid(const uint8_t *s, uint64_t len, uint64_t base, uint32_t count, int proto, uint32_t cs,
@@ -1854,12 +1883,11 @@ hipError_t launch_frame_grid(const uint8_t *s, uint64_t len, uint64_t base, uint
 }
 
 hipError_t launch_grid_finalize(const SegDev *segs, uint32_t nseg, const uint32_t *seg2pkt, const uint32_t *fb,
-                                GridBad *bad, uint32_t bad_cap, GridSummary *sum, hipStream_t stream) {
-  // nseg 0xFFFFFFFF: the run's size is read from *sum; the grid covers bad_cap segments
-  const uint32_t n = nseg == 0xFFFFFFFFu ? bad_cap : nseg;
-  if (!n) return hipSuccess;
-  hipLaunchKernelGGL(grid_finalize_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, segs, nseg, seg2pkt, fb,
-                     bad, bad_cap, sum);
+                                GridBad *bad, uint32_t bad_cap, GridSummary *sum, uint8_t *hsum2, uint32_t host_cap,
+                                uint32_t seq, hipStream_t stream) {
+  // nseg 0xFFFFFFFF: the run's size is read from *sum
+  hipLaunchKernelGGL(grid_finalize_kernel, dim3(1), dim3(1024), 0, stream, segs, nseg, seg2pkt, fb, bad, bad_cap, sum,
+                     hsum2, host_cap, seq);
   return hipGetLastError();
 }
 

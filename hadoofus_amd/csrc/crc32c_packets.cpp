@@ -545,6 +545,7 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
     size_t slot, off, n;
     uint32_t nseg, count;
     uint64_t bm_cap;
+    uint32_t seq;
   };
   std::vector<Pass> passes;
   uint64_t pos = 0, payload = 0;
@@ -599,16 +600,17 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
       // generic tiles: at most one per packet for chunk sizes the tiled
       // kernel takes, else every tile of every packet
       const uint64_t gtiles_ub = cs % kRoundBytes == 0 ? count : left / (uint64_t(cs) * kTileChunks) + 2ull * count;
-      rc = launch_verify_dyn(c, reinterpret_cast<const SegDev *>(dg + L.segs), sum, gtiles_ub,
+      // rounds: at most one per 512 B of the rest of the stream
+      rc = launch_verify_dyn(c, reinterpret_cast<const SegDev *>(dg + L.segs), sum, left / kRoundBytes, gtiles_ub,
                              reinterpret_cast<uint32_t *>(dg + L.fb), reinterpret_cast<unsigned long long *>(ctr + 16),
                              ctr, c.stream, tset, copy_dst != nullptr);
       if (rc) break;
       auto *bad = reinterpret_cast<GridBad *>(dg + L.bad);
+      __atomic_store_n(&reinterpret_cast<GridSummary *>(hg + L.h_sum2)->seq, 0u, __ATOMIC_RELEASE);
       HIPCHK(launch_grid_finalize(reinterpret_cast<const SegDev *>(dg + L.segs), 0xFFFFFFFFu,
                                   reinterpret_cast<const uint32_t *>(dg + L.seg2pkt),
-                                  reinterpret_cast<const uint32_t *>(dg + L.fb), bad, count, sum, c.stream));
-      HIPCHK(hipMemcpyAsync(hg + L.h_sum2, sum, 256 + size_t(std::min(kBadFirst, count)) * sizeof(GridBad),
-                            hipMemcpyDeviceToHost, c.stream));
+                                  reinterpret_cast<const uint32_t *>(dg + L.fb), bad, count, sum,
+                                  c.grid[si].hd + L.h_sum2, kBadFirst, gb.seq, c.stream));
     }
     // the summary lands in pinned memory with its sequence number last: poll
     // it (a fault is caught by the stream synchronisation after 200 ms)
@@ -664,7 +666,7 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
       }
     }
     t_fill += us_since(tf, clk::now());
-    passes.push_back({si, n, S.recorded, verify ? S.nseg : 0u, count, bm_cap});
+    passes.push_back({si, n, S.recorded, verify ? S.nseg : 0u, count, bm_cap, gb.seq});
     n += S.recorded;
     payload += S.payload;
     *consumed = S.consumed;
@@ -686,6 +688,22 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
     }
   }
   const auto t1d = clk::now();
+  // the last verify pass's finalize publishes its verdict count and seq to
+  // pinned memory: poll that (stream order: every earlier pass is done too)
+  // before the stream synchronisation, which then returns at once
+  if (!rc && !fallback && verify)
+    for (auto it = passes.rbegin(); it != passes.rend(); ++it) {
+      if (!it->nseg) continue;
+      const auto *s2 = reinterpret_cast<const GridSummary *>(c.grid[it->slot].h + GridLayout(it->count, it->bm_cap).h_sum2);
+      const auto tq = clk::now();
+      for (uint32_t spin = 1; __atomic_load_n(&s2->seq, __ATOMIC_ACQUIRE) != it->seq; spin++) {
+        if ((spin & 4095u) == 0 && clk::now() - tq > std::chrono::milliseconds(200)) break;  // the sync below reports
+#if defined(__x86_64__) || defined(__i386__)
+        __builtin_ia32_pause();
+#endif
+      }
+      break;
+    }
   // drained even after an error: the tables of queued work live in this context
   hipError_t e = hipStreamSynchronize(c.stream);
   const hipError_t e2 = hipStreamSynchronize(c.v_stream);
