@@ -78,8 +78,12 @@ uint32_t g_store_policy = uint32_t(HDFS_KNOB("HDFS_CRC32C_STORE", 0));
 uint32_t g_group_shift = uint32_t(HDFS_KNOB("HDFS_CRC32C_GROUP", 3)) & 15u;
 // Schedule 3: deal groups XCD-major (1) or by plain workgroup id (0).
 uint32_t g_xcd_major = uint32_t(HDFS_KNOB("HDFS_CRC32C_XCD", 1)) & 1u;
-// Compute mode on tables of whole 8-tile groups: schedule 4 (runs).
-int g_runs = HDFS_KNOB("HDFS_CRC32C_RUNS", 1);
+// Compute-mode CRC stores: 2 (product) schedule 3 with the LDS group gather
+// (one 256-B store per 8-tile group); diagnostic build only: 1 schedule 4
+// on tables of whole groups, 0 one 32-B store per tile
+// (profiles/r02/exp_compute_store_schedules.json: 0 / 1 / 2 = 6377 / 6595 /
+// 6626 GB/s of algorithmic bytes in one process).
+int g_runs = HDFS_KNOB("HDFS_CRC32C_RUNS", 2);
 // Diagnostic per-wave timestamps (device buffer, 3 x u64 per wave) or null.
 unsigned long long *g_diag = nullptr;
 
@@ -293,10 +297,13 @@ int launch_all(DevCtx &c, int mode, const SegDev *d_segs, uint32_t nseg, uint64_
     const int nt = order >= 3 ? g_nt_loads : std::min(g_nt_loads, 1);
     // the small-launch fallback always runs the product's schedule-2 shape
     const int depth = to_small ? 3 : g_depth, streams = to_small ? 1 : g_streams, block = to_small ? 1024 : g_block;
-    // compute over whole 8-tile groups: schedule 4 (runs), product shape only
-    if (order == 3 && runs && g_runs && mode == kModeCompute && !una && !copy && nt == 2 && depth == 3 &&
-        streams == 1 && block == 1024)
-      order = 4;
+    // compute mode, product shape: schedule 4 (runs, tables of whole 8-tile
+    // groups) or schedule 3 with the LDS group gather ("order 5")
+    if (order == 3 && mode == kModeCompute && !una && !copy && nt == 2 && depth == 3 && streams == 1 &&
+        block == 1024) {
+      if (g_runs == 1 && runs) order = 4;
+      else if (g_runs == 2) order = 5;
+    }
     // store policy 4 (diagnostic build): verify plans run the load-only twin
     const int kmode = (kDiag && mode == kModeVerify && g_store_policy == 4) ? int(kModeLoadOnly) : mode;
     const hipError_t le = launch_tiles(kmode, order, nt, depth, streams, block, grid, d_segs, nseg, rounds,
@@ -1302,7 +1309,8 @@ int hdfs_crc32c_set_store_policy(int policy) {
 }
 
 int hdfs_crc32c_set_runs(int on) {
-  g_runs = on ? 1 : 0;
+  if (on < 0 || on > 2) return fail(HDFS_CRC32C_EINVAL, "runs 0 (schedule 3), 1 (schedule 4) or 2 (gather)");
+  g_runs = on;
   return HDFS_CRC32C_OK;
 }
 

@@ -156,6 +156,7 @@ DEV const SegCache &hot(SegCache &k, SegP segs, uint32_t s) {
 struct Cursor {
   uint32_t seg, tile, r;
   bool valid;
+  uint32_t grp = 0;  // compute gather (RUN 2): workgroup-local group ordinal = ticket >> 3
 };
 
 // Work schedule of one wave.
@@ -194,7 +195,13 @@ struct Cursor {
 //    with < 32 rounds per wave skip the pool (one unit per workgroup would
 //    make the tail, not shorten it).
 constexpr uint32_t kUnitMaxShift = 8, kUnitMinShift = 4;
-constexpr uint32_t kSlots = 8;        // LDS slots for published units
+constexpr uint32_t kSlots = 8;  // LDS slots for published units
+// Compute gather (schedule 3, RUN 2): the CRCs of an 8-tile group, finished
+// by up to eight waves of the workgroup, collect in one of kGatherSlots LDS
+// slots (the 4 KiB the tables leave free) and the wave finishing the group
+// writes them as one 256-B store.  Slot s serves groups s, s + kGatherSlots,
+// ... in order; its owner word holds (group << 4) | tiles counted.
+constexpr uint32_t kGatherSlots = 15, kGatherWords = kGatherSlots * 65;
 constexpr uint64_t kPhase1Num = 23, kPhase1Den = 25;  // 92 % static
 
 struct Sched {
@@ -273,6 +280,28 @@ DEV Cursor locate(SegP segs, uint32_t s, uint64_t g) {
   return Cursor{rfl(s), rfl(static_cast<uint32_t>(g - segs[s].mtile_start)), 0u, true};
 }
 
+// Global tile g -> cursor, from the current cursor c (whose segment's hot
+// fields are sh).  Pool tiles may lie behind the slice or far ahead of it (a
+// table of thousands of packet-sized segments: a forward walk from the slice
+// to the pool cost 8x the whole kernel, tools/exp_packet_tables.py);
+// interleaved tiles jump G ahead.  Short hops walk, long ones search.
+template <int ORDER>
+DEV Cursor find_tile(const Cursor c, const SegHot &sh, SegP segs, uint32_t nseg, const Sched &w, uint64_t g) {
+  const uint64_t end = sh.mtile_start + sh.main_tiles;
+  if (w.ut && (g < sh.mtile_start || g >= end)) return ulocate(w, g);
+  if (g < sh.mtile_start || g >= end + (ORDER >= 3 ? 0u : kWalkTiles)) {
+    uint32_t lo = 0, hi = nseg;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (segs[mid].mtile_start <= g) lo = mid; else hi = mid;
+    }
+    return locate(segs, lo, g);
+  }
+  if (g < end)  // same segment (the common case): from the cached fields, no table read
+    return Cursor{c.seg, rfl(static_cast<uint32_t>(g - sh.mtile_start)), 0u, true};
+  return locate(segs, c.seg, g);
+}
+
 // Next round owned by this wave.  An exhausted cursor keeps its last
 // position (so speculative loads stay in bounds) with valid = false.
 template <int ORDER>
@@ -290,27 +319,14 @@ DEV Cursor advance(Cursor c, SegP segs, uint32_t nseg, const Sched &w, SegCache 
   }
   if (ORDER != 0) {
     uint64_t g;
-    if (!ticket_tile<ORDER>(w, grab(w), g)) {
+    const uint32_t tk = grab(w);
+    if (!ticket_tile<ORDER>(w, tk, g)) {
       c.valid = false;
       return c;
     }
-    // Pool tiles may lie behind the slice or far ahead of it (a table of
-    // thousands of packet-sized segments: a forward walk from the slice to
-    // the pool cost 8x the whole kernel, tools/exp_packet_tables.py);
-    // interleaved tiles jump G ahead.  Short hops walk, long ones search.
-    const uint64_t end = sh.mtile_start + sh.main_tiles;
-    if (w.ut && (g < sh.mtile_start || g >= end)) return ulocate(w, g);
-    if (g < sh.mtile_start || g >= end + (ORDER >= 3 ? 0u : kWalkTiles)) {
-      uint32_t lo = 0, hi = nseg;
-      while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (segs[mid].mtile_start <= g) lo = mid; else hi = mid;
-      }
-      return locate(segs, lo, g);
-    }
-    if (g < end)  // same segment (the common case): from the cached fields, no table read
-      return Cursor{c.seg, rfl(static_cast<uint32_t>(g - sh.mtile_start)), 0u, true};
-    return locate(segs, c.seg, g);
+    Cursor n = find_tile<ORDER>(c, sh, segs, nseg, w, g);
+    n.grp = tk >> 3;
+    return n;
   }
   uint32_t s = c.seg, t = c.tile + 1;
   while (s < nseg && t >= segs[s].main_tiles) {
@@ -429,6 +445,8 @@ DEV void issue(uint32_t (&d)[16], uint32_t &exp, uint32_t &tl, uint32_t &sh_a, c
 
 struct LaneConst {
   uint32_t lane, hsel, loff, lb0, lb1, qi, qg, zk, zbase, z448;
+  uint64_t ntiles;   // RUN 2: main tiles of the launch
+  uint32_t *gslot;   // RUN 2: LDS [kGatherSlots] owner words, then [kGatherSlots][64] CRC words
   // 0 default; diagnostic build only: 1 nontemporal, 2 drop result stores,
   // 3 full-line CRC writes (always 0 in the release build)
   uint32_t store_policy;
@@ -472,7 +490,53 @@ DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, ui
   if (MODE == kModeCompute) {
     const bool keep = last && !(kDiag && L.store_policy == 2);
     const uint32_t val = (flags & kSegBigEndian) ? __builtin_bswap32(out) : out;
-    if constexpr (RUN) {
+    if constexpr (RUN == 2) {
+      // schedule 3 gather: an eligible group's tiles (8 full tiles of one
+      // segment) park their CRCs in the group's LDS slot and the wave that
+      // finishes the group stores all 64; other groups' tiles store their own
+      // 32 B but still count in the slot, so it passes on to the next group
+      uint32_t sval = val, soff = leader ? L.qg * 4u : 0x80000000u, range = keep ? nch * 4u : 0u;
+      const uint32_t *sbase = sh.crcs + c.tile * kTileChunks;
+      if (last) {
+        const uint64_t g = sh.mtile_start + c.tile, gs = g & ~7ull;
+        const uint32_t expect = static_cast<uint32_t>(min<uint64_t>(8u, L.ntiles - gs));
+        const bool elig = expect == 8u && gs >= sh.mtile_start && gs + 8u <= sh.mtile_start + sh.main_tiles &&
+                          (gs + 8u - sh.mtile_start) * kTileChunks <= sh.nchunks;
+        const uint32_t s = c.grp % kGatherSlots;
+        uint32_t *own = L.gslot + s;
+        uint32_t *dat = L.gslot + kGatherSlots + s * 64u;
+        // the slot's previous group (grp - kGatherSlots) holds only older
+        // tickets, which never wait on newer ones: the wait ends
+        for (uint32_t spin = 0;; spin++) {
+          const uint32_t o = rfl(__hip_atomic_load(own, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+          if ((o >> 4) == c.grp) break;
+          if (spin > (1u << 24)) __builtin_trap();  // never expected: fail loudly rather than hang
+          __builtin_amdgcn_s_sleep(1);
+        }
+        if (elig && leader) dat[static_cast<uint32_t>(g & 7u) * kTileChunks + L.qg] = val;
+        uint32_t old = 0;
+        if (L.lane == 0) old = __hip_atomic_fetch_add(own, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+        old = rfl(old);
+        const bool fin = (old & 15u) + 1u == expect;
+        if (elig) range = 0u;
+        if (fin) {
+          if (elig) {
+            sval = dat[L.lane];
+            soff = L.lane * 4u;
+            sbase = sh.crcs + (gs - sh.mtile_start) * kTileChunks;
+            range = 256u;
+          }
+          if (L.lane == 0)
+            __hip_atomic_store(own, (c.grp + kGatherSlots) << 4, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+      }
+      const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(
+          reinterpret_cast<uint32_t *>(rfl64(reinterpret_cast<uint64_t>(sbase))), 0, static_cast<int>(rfl(range)),
+          0x00020000);
+      __builtin_amdgcn_raw_buffer_store_b32(sval, rg, soff, 0, 16);
+      return;
+    }
+    if constexpr (RUN == 1) {
       // ORDER 4: lane 8j + q collects chunk q of the run's tile j from that
       // chunk's leader lane 8q; the run's last tile writes the 64 CRCs of
       // its 8 tiles (256 B, whole lines) with one sc1 store
@@ -649,7 +713,8 @@ DEV void process(const uint32_t *lds, uint32_t (&d)[S][16], const uint32_t (&exp
 // rounds stay in flight while one is processed); S independent tile streams
 // per wave (S x 4 KiB per round, S chains of ILP); BLOCK threads per
 // workgroup (one workgroup per CU: the LDS image takes 156 KiB).
-template <int MODE, int ORDER, int NT, int DEPTH, int S, int BLOCK, int BUF = 0, int COPY = 0, int UNA = 0>
+template <int MODE, int ORDER, int NT, int DEPTH, int S, int BLOCK, int BUF = 0, int COPY = 0, int UNA = 0,
+          int GATHER = 0>
 __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
     const SegDev *__restrict__ segs, uint32_t nseg, uint64_t total_rounds, uint64_t total_tiles,
     const uint32_t *__restrict__ gtab, uint32_t *__restrict__ first_bad,
@@ -667,9 +732,13 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
     utiles = dyn->utiles;
   }
   // + ticket counter, pad, kSlots 64-bit pool slots
-  __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords + 2 + 2 * kSlots];
+  // + ticket counter, pad, kSlots 64-bit pool slots (+ GATHER: the group slots)
+  static_assert(GATHER == 0 || (MODE == kModeCompute && ORDER == 3 && S == 1), "gather: compute, schedule 3");
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords + 2 + 2 * kSlots + (GATHER ? kGatherWords : 0)];
 
   if (threadIdx.x < 2 + 2 * kSlots) lds[kLdsWords + threadIdx.x] = 0u;
+  // group slot s starts owned by group s, no tile counted
+  if (GATHER && threadIdx.x < kGatherSlots) lds[kLdsWords + 2 + 2 * kSlots + threadIdx.x] = threadIdx.x << 4;
   // LDS image: word (P*16384 + e*64 + h*32 + l) = t_{3-(2P+h)}[e] for all 32 l.
   // Filled with 16-B stores, consecutive lanes on consecutive 16 B (no bank
   // conflicts); the source words a lane needs are loaded up front so the
@@ -719,6 +788,8 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
   L.zk = 7u - L.qi;
   L.zbase = kLdsSliceBytes / 4 + (L.zk ? L.zk - 1u : 0u) * 1024u;
   L.z448 = kLdsSliceBytes / 4 + 6u * 1024u;
+  L.ntiles = total_tiles;
+  L.gslot = &lds[kLdsWords + 2 + 2 * kSlots];
 
   constexpr uint32_t wpb = BLOCK / 64;
   const uint32_t wave = rfl(blockIdx.x * wpb + (threadIdx.x >> 6));
@@ -791,7 +862,8 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
 #pragma unroll
     for (int s = 0; s < S; s++) {
       uint64_t g;
-      if (ticket_tile<ORDER>(w, grab(w), g)) {
+      const uint32_t tk = grab(w);
+      if (ticket_tile<ORDER>(w, tk, g)) {
         if (w.ut) {
           cur[0][s] = ulocate(w, g);
         } else {
@@ -802,6 +874,7 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
           }
           cur[0][s] = locate(sg, lo, g);
         }
+        cur[0][s].grp = tk >> 3;
       }
     }
   }
@@ -858,7 +931,7 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
   for (;;) {
 #pragma unroll
     for (int k = 0; k < DEPTH; k++) {
-      process<MODE, S, COPY, UNA, (ORDER == 4 && MODE == kModeCompute) ? 1 : 0>(lds, buf[k], ex[k], tl[k], sha[k],
+      process<MODE, S, COPY, UNA, (ORDER == 4 && MODE == kModeCompute) ? 1 : (GATHER ? 2 : 0)>(lds, buf[k], ex[k], tl[k], sha[k],
                                                                                 cur[k], sg, st, L, first_bad, mism,
                                                                                 kc, acc);
 #pragma unroll
@@ -1953,9 +2026,10 @@ hipError_t launch_tiles(int mode, int order, int nt, int depth, int streams, int
                         int una, const GridSummary *dyn, uint32_t utiles) {
   // uniform-table look-up: tile indices must fit 32 bits (multiply-high form)
   if (utiles && !dyn && (total_tiles >> 32)) utiles = 0;
-#define HDFS_LAUNCH_CU(M, O, N, D, S, B, BUF, C, U)                                                            \
-  hipLaunchKernelGGL((crc32c_tiles_kernel<M, O, N, D, S, B, BUF, C, U>), dim3(grid), dim3(B), 0, stream, segs, \
-                     nseg, total_rounds, total_tiles, gtab, first_bad, mism, diag, tune, gctr, dyn, utiles)
+#define HDFS_LAUNCH_CUG(M, O, N, D, S, B, BUF, C, U, G)                                                          \
+  hipLaunchKernelGGL((crc32c_tiles_kernel<M, O, N, D, S, B, BUF, C, U, G>), dim3(grid), dim3(B), 0, stream,      \
+                     segs, nseg, total_rounds, total_tiles, gtab, first_bad, mism, diag, tune, gctr, dyn, utiles)
+#define HDFS_LAUNCH_CU(M, O, N, D, S, B, BUF, C, U) HDFS_LAUNCH_CUG(M, O, N, D, S, B, BUF, C, U, 0)
 #define HDFS_LAUNCH_C(M, O, N, D, S, B, BUF, C) HDFS_LAUNCH_CU(M, O, N, D, S, B, BUF, C, 0)
 #define HDFS_LAUNCH(M, O, N, D, S, B, BUF) HDFS_LAUNCH_C(M, O, N, D, S, B, BUF, 0)
 #define HDFS_SHAPE(O, N, D, S, B) (order == (O) && nt == (N) && depth == (D) && streams == (S) && block == (B))
@@ -1993,7 +2067,7 @@ hipError_t launch_tiles(int mode, int order, int nt, int depth, int streams, int
     else return hipErrorInvalidValue;
   } else {
     HDFS_LAUNCH_PRODUCT(kModeCompute)
-    else if (HDFS_SHAPE(4, 2, 3, 1, 1024)) HDFS_LAUNCH(kModeCompute, 4, 1, 3, 1, 1024, 1);
+    else if (HDFS_SHAPE(5, 2, 3, 1, 1024)) HDFS_LAUNCH_CUG(kModeCompute, 3, 1, 3, 1, 1024, 1, 0, 0, 1);
     else return hipErrorInvalidValue;
   }
 #else
@@ -2026,6 +2100,7 @@ hipError_t launch_tiles(int mode, int order, int nt, int depth, int streams, int
   } else {
     HDFS_LAUNCH_ALL(kModeCompute)
     else if (HDFS_SHAPE(4, 2, 3, 1, 1024)) HDFS_LAUNCH(kModeCompute, 4, 1, 3, 1, 1024, 1);
+    else if (HDFS_SHAPE(5, 2, 3, 1, 1024)) HDFS_LAUNCH_CUG(kModeCompute, 3, 1, 3, 1, 1024, 1, 0, 0, 1);
     else return hipErrorInvalidValue;
   }
 #undef HDFS_LAUNCH_ALL
@@ -2035,6 +2110,7 @@ hipError_t launch_tiles(int mode, int order, int nt, int depth, int streams, int
 #undef HDFS_LAUNCH
 #undef HDFS_LAUNCH_C
 #undef HDFS_LAUNCH_CU
+#undef HDFS_LAUNCH_CUG
   return hipGetLastError();
 }
 

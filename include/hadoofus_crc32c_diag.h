@@ -63,8 +63,11 @@ int hdfs_crc32c_set_shape(int streams, int block);
  * undefined.
  * Env HDFS_CRC32C_STORE. */
 int hdfs_crc32c_set_store_policy(int policy);
-/* Compute plans over whole 8-tile groups run schedule 4 (one wave per group,
- * one 256-B CRC store per group): 1 (default) or 0 (schedule 3).
+/* Compute plans: 2 (default, the product) schedule 3 with the LDS group
+ * gather (a group's CRCs collected across the workgroup's waves, one 256-B
+ * store per 8-tile group); 1 schedule 4 on tables of whole 8-tile groups
+ * (one wave per group, one 256-B CRC store per group); 0 schedule 3 with a
+ * 32-B store per tile.
  * Env HDFS_CRC32C_RUNS. */
 int hdfs_crc32c_set_runs(int on);
 /* Empirical streaming-read bandwidth of `bytes` at dptr (GB/s, 1e9 B/s):

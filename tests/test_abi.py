@@ -65,18 +65,19 @@ def test_release_kernels_are_the_product_shapes(libpath, diagpath):
     3 with buffer loads, schedule 2) in their product variants only: compute
     and verify, each with and without the realigning path for byte-unaligned
     data, verify also with the fused copy-out -- twelve in all -- plus
-    compute on schedule 4 (runs of whole 8-tile groups); no load-only twin
-    (mode 2) and no read probes.  The diagnostic build has them."""
+    compute on schedule 3 with the LDS group gather; no load-only twin
+    (mode 2), no schedule 4 and no read probes.  The diagnostic build has
+    them."""
     import re as _re
     rel = open(libpath, "rb").read()
     dia = open(diagpath, "rb").read()
     pat = (rb"_ZN11hdfs_crc32c19crc32c_tiles_kernelILi(\d)ELi(\d)ELi(\d)ELi(\d)ELi(\d)ELi(\d+)ELi(\d)ELi(\d)"
-           rb"ELi(\d)EEE")
+           rb"ELi(\d)ELi(\d)EEE")
     shapes = set(_re.findall(pat, rel))
     variants = [(b"0", b"0", b"0"), (b"0", b"0", b"1")] + [(b"1", cp, un) for cp in (b"0", b"1") for un in (b"0", b"1")]
-    want = {(m, o, b"1", b"3", b"1", b"1024", buf, cp, un) for m, cp, un in variants
+    want = {(m, o, b"1", b"3", b"1", b"1024", buf, cp, un, b"0") for m, cp, un in variants
             for o, buf in ((b"3", b"1"), (b"2", b"0"))}
-    want.add((b"0", b"4", b"1", b"3", b"1", b"1024", b"1", b"0", b"0"))
+    want.add((b"0", b"3", b"1", b"3", b"1", b"1024", b"1", b"0", b"0", b"1"))  # compute: LDS group gather
     assert shapes == want, shapes ^ want
     assert b"probe_read_kernel" not in rel and b"probe2_kernel" not in rel
     dshapes = set(_re.findall(pat, dia))

@@ -161,3 +161,45 @@ def test_unaligned_realign_small_and_large(engine, oracle, shift, cs, nch):
     assert list(np.nonzero(bits)[0]) == picks
     # the drop-in stream CRC over the same unaligned device bytes
     assert engine.stream_crc_dev(0x5A5A5A5A, buf.ptr + shift, n) == oracle.crc32c(0x5A5A5A5A, host)
+
+
+@pytest.mark.parametrize("runs", [0, 1, 2])
+def test_compute_store_schedules(engine, diag, oracle, table, runs):
+    """Compute mode's three store schedules (diagnostic knob set_runs):
+    0 schedule 3 (one 32-B store per tile), 1 schedule 4 (a wave per 8-tile
+    group), 2 schedule 3 with the LDS group gather (a group's CRCs collected
+    across the workgroup's waves, one 256-B store by the wave finishing it).
+    On the C5-like table and on a table of 13-tile segments, where groups
+    straddle segments and fall back to per-tile stores."""
+    host, sizes, lens, want, dbuf = table
+    nch = [n // cs for cs, n in zip(sizes, lens)]
+    crcs = engine.DeviceBuffer(4 * (sum(nch) + 64))
+    try:
+        diag.reset()
+        diag.set_runs(runs)
+        for case in ("c5", "odd"):
+            if case == "c5":
+                segs_spec = [(i * SEG, n, cs) for i, (cs, n) in enumerate(zip(sizes, lens))]
+                wants = want
+            else:
+                segs_spec = [(i * 13 * 4096 + 7, 13 * 4096, 512) for i in range(4000)]  # 200 MiB, 13 tiles each
+                wants = None
+            crcs.fill(0xA5)
+            segs, off = [], 0
+            for base, n, cs in segs_spec:
+                segs.append(engine.Segment(data=dbuf.ptr + base, len=n, chunk_size=cs, flags=engine.SEG_BE,
+                                           crc_init=0, crcs=crcs.ptr + 4 * off, bitmap=None))
+                off += n // cs
+            p = diag.plan(engine.MODE_COMPUTE, segs)
+            p.execute()
+            got = crcs.download(4 * (off + 64), dtype=">u4").astype(np.uint32)
+            o = 0
+            for k, (base, n, cs) in enumerate(segs_spec):
+                w = wants[k] if wants is not None else oracle.chunk_crcs(host[base:base + n], cs)
+                np.testing.assert_array_equal(got[o:o + n // cs], w, err_msg=f"{case} segment {k}")
+                o += n // cs
+            assert (got[o:] == 0xA5A5A5A5).all()
+            p.destroy()
+    finally:
+        diag.reset()
+        crcs.free()

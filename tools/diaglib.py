@@ -60,8 +60,8 @@ class Diag:
     def set_store_policy(self, policy):
         self._c(self.lib.hdfs_crc32c_set_store_policy(policy))
 
-    def set_runs(self, on):
-        self._c(self.lib.hdfs_crc32c_set_runs(int(on)))
+    def set_runs(self, mode):
+        self._c(self.lib.hdfs_crc32c_set_runs(int(mode)))
 
     def set_probe(self, variant=0, grid_per_cu=2, block=1024):
         self._c(self.lib.hdfs_crc32c_set_probe(variant, grid_per_cu, block))
@@ -80,4 +80,4 @@ class Diag:
         self.set_group_shift(3)
         self.set_store_policy(0)
         self.set_xcd_major(1)
-        self.set_runs(1)
+        self.set_runs(2)
