@@ -229,8 +229,10 @@ int pipe_reserve(DevCtx &c, size_t piece, uint32_t cs, size_t npieces);
 // CRC32C, 1 CRC32).  Results: c.h_small_out[0] first bad, [1] mismatches,
 // CRCs from c.h_small_out + kSmallMeta.
 bool small_ok(uint64_t len, uint64_t cs);
+// hsrc (host bytes, len) / hcrc (wire CRCs, crc_bytes): staged by the call.
 int small_call(DevCtx &c, int mode, uint32_t len, uint32_t cs, uint32_t reg0, bool be, int ctype,
-               const uint8_t *dsrc = nullptr);
+               const uint8_t *dsrc = nullptr, const uint8_t *hsrc = nullptr, const uint8_t *hcrc = nullptr,
+               uint32_t crc_bytes = 0);
 // BE per-chunk CRCs (chunk cs; ctype HDFS_CRC32C_CSUM_*) of a host or
 // device buffer into host memory.
 int chunk_crcs_to_host(const void *data, uint64_t len, uint32_t cs, int ctype, uint32_t *out_be);

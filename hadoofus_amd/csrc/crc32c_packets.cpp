@@ -810,10 +810,8 @@ int verify_packets_impl(const uint8_t *stream, uint64_t len, int proto, uint32_t
     if (vidx.size() == 1 && small_ok(uint64_t(recs[vidx[0]].data_len), cs)) {
       hdfs_crc32c_packet &k = recs[vidx[0]];
       const uint8_t *crcp = stream + k.stream_off + k.header_len;
-      std::memcpy(c.h_small_in, crcp + k.crc_len, size_t(k.data_len));
-      std::memcpy(c.h_small_in + kSmallMax, crcp, size_t(k.crc_len));
       rc = small_call(c, kModeVerify, uint32_t(k.data_len), cs, 0xFFFFFFFFu, true,
-                      ctype == HDFS_CRC32C_CSUM_CRC32 ? 1 : 0);
+                      ctype == HDFS_CRC32C_CSUM_CRC32 ? 1 : 0, nullptr, crcp + k.crc_len, crcp, uint32_t(k.crc_len));
       if (rc) return rc;
       if (c.h_small_out[0] != 0xFFFFFFFFu) {
         k.error = HDFS_CRC32C_ERR_DATANODE_BAD_CHECKSUM;
