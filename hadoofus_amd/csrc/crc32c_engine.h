@@ -51,6 +51,12 @@ hipError_t launch_header_window(const uint8_t *s, uint64_t len, uint64_t base, u
 
 // device framing of device-resident packet streams (crc32c_kernels.hip)
 // frame_grid_kernel + grid_build_kernel: one device framing pass.
+// Short device-resident run in one launch (count <= kSmallRunMax grid
+// points, one workgroup each); hout: pinned host slots (device address),
+// kSrHostBytes.
+hipError_t launch_small_run(const uint8_t *s, uint64_t len, uint32_t count, int proto, uint32_t cs, int ctype,
+                            const uint32_t *tab, const uint32_t *pow2, uint8_t *hout, uint32_t seq,
+                            hipStream_t stream);
 hipError_t launch_frame_grid(const uint8_t *s, uint64_t len, uint64_t base, uint32_t count, int proto, uint32_t cs,
                              int ctype, int verify, uint32_t sflags, uint8_t *bm_base, uint8_t *copy_base,
                              uint64_t copy_cap, GridBufs g, hipStream_t stream);
@@ -161,6 +167,8 @@ struct DevCtx {
     uint8_t *hd = nullptr;  // device address of h (coherent, mapped)
   };
   uint32_t grid_seq = 0;
+  // short device runs (small_run_kernel): device scratch + pinned host area
+  uint8_t *sr_h = nullptr, *sr_hd = nullptr;
   hipStream_t r_stream = nullptr;  // device framing: record copies of runs with many exceptions
   std::vector<GridSlot> grid;
   // opt-in resident mailbox (guarded by mu): pinned request line ([0..3]

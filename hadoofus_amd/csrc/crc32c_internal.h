@@ -163,6 +163,16 @@ constexpr uint32_t kHdrWin = 64;          // header-window row bytes (device pac
 
 constexpr uint32_t kGridMaxCount = 65536;  // grid points per device framing pass
 
+// Short device-resident runs (the per-read case): small_run_kernel frames
+// and verifies up to kSmallRunMax packets of <= kSmallMax data bytes in ONE
+// launch, one workgroup per grid point.  Host area: one kSrSlot-byte slot
+// per grid point: the record (56 B), then u32 {status | unsupported << 8,
+// first bad chunk, bad chunks, seq} -- seq written last.
+constexpr uint32_t kSmallRunMax = 64;
+constexpr uint32_t kSrSlot = 128;
+constexpr uint32_t kSrHostBytes = kSmallRunMax * kSrSlot;
+constexpr uint64_t kSmallRunBytes = uint64_t(kSmallRunMax) * (65536 + 4096);  // streams up to this try it
+
 // Synchronous host-memory calls up to this size (and chunk count) run as one
 // small kernel reading pinned host memory (small_chunks_kernel).
 constexpr uint32_t kSmallMax = 65536;

@@ -1939,6 +1939,163 @@ __global__ __launch_bounds__(1024) void grid_finalize_kernel(const SegDev *__res
     __hip_atomic_store(&reinterpret_cast<GridSummary *>(hsum2)->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Short device-resident runs in one launch (the per-read case of a
+// GPU-direct receive: one or a few packets per call).  Workgroup k frames the
+// packet at k * stride (stride from packet 0's first bytes, the device
+// framing's grid) with the shared frame_step, and -- when it is a clean
+// packet with CRCs of <= 64 KiB -- verifies its chunks itself: one 64-B
+// piece per thread from HBM, slicing tables and the zeros operators it can
+// need in LDS, pieces shifted to their chunk's end and XOR-ed per chunk
+// (small_chunks_kernel's algebra).  The last workgroup to finish works out
+// the run (first grid point that is not On, as grid_build_kernel) and
+// publishes summary, records and verdicts to pinned memory, its sequence
+// number last.  A packet it cannot take (more data, too many chunks, a chunk
+// size that is not a multiple of 64 with several chunks) is flagged and the
+// host takes the regular path.
+__global__ __launch_bounds__(1024) void small_run_kernel(const uint8_t *__restrict__ s, uint64_t len, uint32_t count,
+                                                         int proto, uint32_t cs, int ctype,
+                                                         const uint32_t *__restrict__ tab,
+                                                         const uint32_t *__restrict__ pow2,
+                                                         uint8_t *__restrict__ hout, uint32_t seq) {
+  __shared__ uint32_t tt[1024];
+  __shared__ __attribute__((aligned(16))) uint32_t zt[16 * 1024];  // Z_{2^b}, b < 16 (the levels a shift can use)
+  __shared__ uint32_t acc[kSmallMaxChunks];
+  __shared__ __attribute__((aligned(16))) uint8_t win[kHdrWin];
+  __shared__ hdfs_crc32c_packet rec;
+  __shared__ uint32_t ctl[6];  // code, verify this packet, unsupported, first bad, bad chunks, levels
+  const uint32_t tid = threadIdx.x, k = blockIdx.x;
+  tt[tid] = tab[tid];
+  if (tid == 0) {
+    // the grid: header_len + plen - 4 of the packet at 0 (as frame_grid_kernel)
+    auto at0 = [&](uint64_t i) -> uint32_t { return i < len ? uint32_t(s[i]) : 0u; };
+    const int32_t plen = int32_t((at0(0) << 24) | (at0(1) << 16) | (at0(2) << 8) | at0(3));
+    const int64_t hl = proto == HDFS_CRC32C_PROTO_V2 ? 6 + int64_t((at0(4) << 8) | at0(5)) : 25;
+    const int64_t tot = hl + int64_t(plen) - 4;
+    const uint64_t stride = tot > 0 ? uint64_t(tot) : 0;
+    hdfs_crc32c_packet r{};
+    uint32_t code = kGridMore;
+    uint64_t total = 0;
+    const uint64_t pos = uint64_t(k) * stride;
+    if ((k == 0 || stride) && pos < len) {
+      stage_header(s, len, pos, win);
+      const int st = grid_frame(s, len, pos, win, proto, cs, ctype, r, total);
+      code = st == frame::kStepMore ? kGridMore : st == frame::kStepStop ? kGridStop : total == stride ? kGridOn : kGridOff;
+    }
+    const bool want = code != kGridMore && !r.error && r.crc_len > 0 && ctype != HDFS_CRC32C_CSUM_NULL;
+    const uint32_t nch = want ? uint32_t(r.crc_len) / 4u : 0u;
+    const bool fits = uint32_t(r.data_len) <= kSmallMax && nch <= kSmallMaxChunks && (cs % 64u == 0 || nch == 1u);
+    rec = r;
+    ctl[0] = code;
+    ctl[1] = want && fits ? 1u : 0u;
+    ctl[2] = want && !fits ? 1u : 0u;
+    ctl[3] = 0xFFFFFFFFu;
+    ctl[4] = 0u;
+    const uint32_t span = min(cs, uint32_t(r.data_len));  // longest shift: < one chunk
+    ctl[5] = span > 1u ? 32u - __builtin_clz(span - 1u) : 1u;
+  }
+  __syncthreads();
+  if (ctl[1]) {
+    const uint32_t nlev = ctl[5];
+    for (uint32_t q = tid; q < nlev * 256u; q += 1024u)
+      *reinterpret_cast<u32x4 *>(&zt[4u * q]) = gload16(pow2 + 4u * q);
+    const uint32_t dlen = uint32_t(rec.data_len), nch = uint32_t(rec.crc_len) / 4u;
+    const uint8_t *crcp = s + rec.stream_off + rec.header_len;
+    const uint8_t *dp = crcp + rec.crc_len;
+    for (uint32_t j = tid; j < nch; j += 1024u) acc[j] = 0u;
+    // the piece's 64 bytes (any byte alignment: buffer loads; past dlen: zeros)
+    const __amdgpu_buffer_rsrc_t rd =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(dp), 0, static_cast<int>(dlen), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rc =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(crcp), 0, static_cast<int>(nch * 4u), 0x00020000);
+    const uint32_t b0 = 64u * tid;
+    uint32_t d[16];
+#pragma unroll
+    for (uint32_t m = 0; m < 4; m++) {
+      const u32x4 x = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rd, b0 + 16u * m, 0, 0));
+      d[4 * m + 0] = x.x;
+      d[4 * m + 1] = x.y;
+      d[4 * m + 2] = x.z;
+      d[4 * m + 3] = x.w;
+    }
+    if (b0 < dlen && b0 + 64u > dlen && (dlen & 15u)) {
+      // the piece holding the packet's last bytes: a 16-B load that crosses
+      // the descriptor's range returns zeros, so the last partial 16 B are
+      // read byte by byte (one lane)
+      const uint32_t q0 = (dlen - b0) & ~15u;
+#pragma unroll
+      for (uint32_t q = 0; q < 16; q++) {
+        if (4u * q >= q0 && 4u * q < dlen - b0) {
+          uint32_t wv = 0;
+          for (uint32_t b = 0; b < 4u && b0 + 4u * q + b < dlen; b++)
+            wv |= uint32_t(__builtin_amdgcn_raw_buffer_load_b8(rd, b0 + 4u * q + b, 0, 0)) << (8u * b);
+          d[q] = wv;
+        }
+      }
+    }
+    uint32_t ev[2];
+#pragma unroll
+    for (uint32_t q = 0; q < 2; q++) ev[q] = __builtin_amdgcn_raw_buffer_load_b32(rc, 4u * (q * 1024u + tid), 0, 0);
+    __syncthreads();  // tables and acc ready
+    if (b0 < dlen) {
+      const uint32_t j = b0 / cs, ce = min((j + 1u) * cs, dlen), n = min(64u, ce - b0);
+      uint32_t c = (b0 == j * cs) ? 0xFFFFFFFFu : 0u;
+#pragma unroll
+      for (uint32_t q = 0; q < 16; q++) {
+        if (4u * q + 4u <= n) {
+          const uint32_t x = c ^ d[q];
+          c = tt[768u + (x & 0xffu)] ^ tt[512u + ((x >> 8) & 0xffu)] ^ tt[256u + ((x >> 16) & 0xffu)] ^ tt[x >> 24];
+        }
+      }
+      if (n & 3u) {
+        uint32_t tw = 0u;
+#pragma unroll
+        for (uint32_t q = 0; q < 16; q++) tw = (q == (n >> 2)) ? d[q] : tw;
+        for (uint32_t b = 0; b < (n & 3u); b++) c = tt[(c ^ (tw >> (8u * b))) & 0xffu] ^ (c >> 8);
+      }
+      for (uint32_t dd = ce - b0 - n, lvl = 0; dd; lvl++, dd >>= 1) {
+        if (dd & 1u) {
+          const uint32_t *z = zt + lvl * 1024u;
+          c = z[c & 0xffu] ^ z[256u + ((c >> 8) & 0xffu)] ^ z[512u + ((c >> 16) & 0xffu)] ^ z[768u + (c >> 24)];
+        }
+      }
+      atomicXor(&acc[j], c);
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t q = 0; q < 2; q++) {
+      const uint32_t j = q * 1024u + tid;
+      if (j < nch && __builtin_bswap32(ev[q]) != ~acc[j]) {
+        atomicMin(&ctl[3], j);
+        atomicAdd(&ctl[4], 1u);
+      }
+    }
+  }
+  __syncthreads();
+  // this packet's slot in pinned host memory: record, status, verdict, then
+  // (one system fence later) the call's sequence number.  No cross-workgroup
+  // step: the host reads the count slots and works out the run itself.
+  if (tid == 0) {
+    uint8_t *slot = hout + size_t(k) * kSrSlot;
+    const uint64_t *x = reinterpret_cast<const uint64_t *>(&rec);
+    uint64_t *y = reinterpret_cast<uint64_t *>(slot);
+    for (int q = 0; q < int(kGridRecBytes / 8); q++) y[q] = x[q];
+    uint32_t *w = reinterpret_cast<uint32_t *>(slot + kGridRecBytes);
+    w[0] = ctl[0] | (ctl[2] << 8);
+    w[1] = ctl[3];
+    w[2] = ctl[4];
+    __threadfence_system();
+    __hip_atomic_store(&w[3], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+hipError_t launch_small_run(const uint8_t *s, uint64_t len, uint32_t count, int proto, uint32_t cs, int ctype,
+                            const uint32_t *tab, const uint32_t *pow2, uint8_t *hout, uint32_t seq, hipStream_t stream) {
+  if (!count || count > kSmallRunMax) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(small_run_kernel, dim3(count), dim3(1024), 0, stream, s, len, count, proto, cs, ctype, tab, pow2,
+                     hout, seq);
+  return hipGetLastError();
+}
+
 hipError_t launch_frame_grid(const uint8_t *s, uint64_t len, uint64_t base, uint32_t count, int proto, uint32_t cs,
                              int ctype, int verify, uint32_t sflags, uint8_t *bm_base, uint8_t *copy_base,
                              uint64_t copy_cap, GridBufs g, hipStream_t stream) {

@@ -532,12 +532,104 @@ int reserve_grid(DevCtx &c, size_t si, const GridLayout &L) {
 // after at most two packets (a stream of mixed sizes) hands the rest to the
 // host window walk (walk_device_stream).  Same records, stopping rules and
 // consumed offset as parse_packet_stream.
+// Short runs (<= kSmallRunMax packets of <= 64 KiB, the per-read case):
+// framing and verify in ONE launch (small_run_kernel) instead of the framing
+// pass + verify + finalize chain.  Returns 1 when the run is fully resolved
+// there (records in dst), 0 when the regular path must run (a packet the
+// kernel cannot take, a packet off the grid, more packets than it covers),
+// < 0 on an engine error.
+int small_run(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs, int ctype, size_t max_pkts,
+              hdfs_crc32c_packet *dst, size_t *nout, uint64_t *consumed, uint64_t *payload) {
+  if (!c.sr_h) {
+    HIPCHK(hipHostMalloc(&c.sr_h, kSrHostBytes, hipHostMallocCoherent | hipHostMallocMapped));
+    std::memset(c.sr_h, 0, kSrHostBytes);
+    HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&c.sr_hd), c.sr_h, 0));
+  }
+  const uint32_t count = uint32_t(std::min<uint64_t>({uint64_t(kSmallRunMax), uint64_t(max_pkts), len / 6 + 1}));
+  const uint32_t seq = ++c.grid_seq;
+  const int tset = ctype == HDFS_CRC32C_CSUM_CRC32 ? 1 : 0;
+  HIPCHK(launch_small_run(d, len, count, proto, cs, ctype, c.d_tab_main_t[tset], c.d_tab_pow2_t[tset], c.sr_hd, seq,
+                          c.stream));
+  auto word = [&](uint32_t k, int i) -> const uint32_t * {
+    return reinterpret_cast<const uint32_t *>(c.sr_h + size_t(k) * kSrSlot + kGridRecBytes) + i;
+  };
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
+  for (uint32_t k = 0; k < count; k++) {
+    for (uint32_t spin = 1; __atomic_load_n(word(k, 3), __ATOMIC_ACQUIRE) != seq; spin++) {
+      if ((spin & 4095u) == 0 && clk::now() - t0 > std::chrono::milliseconds(200)) {
+        HIPCHK(hipStreamSynchronize(c.stream));
+        if (__atomic_load_n(word(k, 3), __ATOMIC_ACQUIRE) != seq) return fail(HDFS_CRC32C_EHIP, "short-run kernel");
+        break;
+      }
+#if defined(__x86_64__) || defined(__i386__)
+      __builtin_ia32_pause();
+#endif
+    }
+  }
+  // the run: grid points up to the first that is not On (grid_build_kernel's rule)
+  auto rec = [&](uint32_t k) {
+    hdfs_crc32c_packet r;
+    std::memcpy(&r, c.sr_h + size_t(k) * kSrSlot, sizeof(r));
+    return r;
+  };
+  uint32_t fbk = count, unsup = 0;
+  for (uint32_t k = 0; k < count; k++)
+    if ((*word(k, 0) & 0xffu) != kGridOn) {
+      fbk = k;
+      break;
+    }
+  const uint32_t st_fb = fbk < count ? (*word(fbk, 0) & 0xffu) : uint32_t(kGridOn);
+  const uint32_t recorded = fbk + (fbk < count && st_fb != kGridMore ? 1u : 0u);
+  const hdfs_crc32c_packet r0 = rec(0);
+  const uint64_t stride = recorded && (*word(0, 0) & 0xffu) == kGridOn
+                              ? uint64_t(r0.header_len) + uint64_t(r0.crc_len) + uint64_t(r0.data_len)
+                              : 0u;
+  uint64_t next = 0, used = 0, pay = 0;
+  if (fbk == count) {
+    used = next = uint64_t(count) * stride;
+  } else if (st_fb == kGridMore) {
+    used = next = uint64_t(fbk) * stride;
+  } else {
+    const hdfs_crc32c_packet rf = rec(fbk);
+    next = rf.stream_off + rf.header_len + uint64_t(rf.crc_len) + uint64_t(rf.data_len);
+    used = rf.error ? uint64_t(fbk) * stride : next;
+  }
+  for (uint32_t k = 0; k < recorded; k++) unsup |= *word(k, 0) >> 8;
+  const bool ended = st_fb == kGridStop || st_fb == kGridMore || (fbk == count && (count == max_pkts || next >= len));
+  if (unsup || !ended) return 0;
+  for (uint32_t k = 0; k < recorded; k++) {
+    dst[k] = rec(k);
+    if (!dst[k].error) pay += uint64_t(dst[k].data_len);
+    if (*word(k, 2)) {
+      dst[k].error = HDFS_CRC32C_ERR_DATANODE_BAD_CHECKSUM;
+      dst[k].first_bad = int32_t(*word(k, 1));
+      dst[k].bad_chunks = *word(k, 2);
+    }
+  }
+  *nout = recorded;
+  *consumed = used;
+  *payload = pay;
+  return 1;
+}
+
 int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs, int ctype, size_t max_pkts,
               bool verify, uint8_t *copy_dst, uint64_t copy_cap, hdfs_crc32c_packet *dst, size_t *nout,
               uint64_t *consumed, uint64_t *payload_out) {
   *nout = 0;
   *consumed = 0;
   verify = verify && ctype != HDFS_CRC32C_CSUM_NULL;
+  if (verify && !copy_dst && max_pkts && len <= kSmallRunBytes) {
+    uint64_t pay = 0;
+    const int r = small_run(c, d, len, proto, cs, ctype, max_pkts, dst, nout, consumed, &pay);
+    if (r < 0) return r;
+    if (r == 1) {
+      if (payload_out) *payload_out = pay;
+      return HDFS_CRC32C_OK;
+    }
+    *nout = 0;
+    *consumed = 0;
+  }
   if (!c.v_stream) HIPCHK(hipStreamCreateWithFlags(&c.v_stream, hipStreamNonBlocking));
   const uint32_t sflags = HDFS_CRC32C_SEG_BE | (ctype == HDFS_CRC32C_CSUM_CRC32 ? HDFS_CRC32C_SEG_CRC32 : 0u);
   const int tset = ctype == HDFS_CRC32C_CSUM_CRC32 ? 1 : 0;

@@ -398,3 +398,36 @@ def test_gpu_device_stream_irregular_headers(engine, oracle, proto, pattern):
         assert (rc, pkts, used) == want and dst.download(delivered).tobytes() == _payloads(s, want[1])
         keep.free()
         dst.free()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("proto,cs,ctype", [(2, 512, CSUM_CRC32C), (1, 512, CSUM_CRC32C), (2, 4096, CSUM_CRC32),
+                                            (2, 100, CSUM_CRC32C), (2, 64, CSUM_CRC32C)])
+def test_gpu_device_stream_short_runs(engine, oracle, proto, cs, ctype):
+    """Short device-resident runs (the per-read case) go through the one-launch
+    path (small_run_kernel: framing + verify per packet workgroup) when they
+    fit it and through the regular chain when they do not (more than 16
+    packets, a packet over 64 KiB, several chunks of a size that is not a
+    multiple of 64, packets off the grid): every case equals the oracle and
+    the host path."""
+    rng = np.random.default_rng(cs + proto + ctype)
+    cases = [[65536], [65536] * 3, [65536] * 16, [65536] * 17, [40000] * 5, [1], [777] * 4, [65536, 100, 65536],
+             [70000], [65536] * 15 + [12345], [4096] * 16]
+    for dl in cases:
+        corrupt = set()
+        for _ in range(3):
+            k = int(rng.integers(0, len(dl)))
+            corrupt.add((k, int(rng.integers(0, (dl[k] + cs - 1) // cs))))
+        for last_empty in (True, False):
+            s, bad = build_stream(oracle.crc32c, proto, cs, ctype, dl, seed=len(dl), corrupt=sorted(corrupt),
+                                  last_empty=last_empty)
+            want = oracle.verify_packets(s, proto, cs, ctype)
+            for shift in (0, 3):
+                keep, p = _dev(engine, s, shift)
+                got = engine.verify_packets(None, proto, cs, ctype, dptr=p, nbytes=len(s))
+                assert got == want, (dl, last_empty, shift)
+                for mp in (1, 2):
+                    assert engine.verify_packets(None, proto, cs, ctype, max_pkts=mp, dptr=p, nbytes=len(s)) == \
+                        oracle.verify_packets(s, proto, cs, ctype, max_pkts=mp), (dl, mp)
+                keep.free()
+            assert engine.verify_packets(s, proto, cs, ctype) == want
