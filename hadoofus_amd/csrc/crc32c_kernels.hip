@@ -1953,7 +1953,7 @@ __global__ __launch_bounds__(1024) void grid_finalize_kernel(const SegDev *__res
 // size that is not a multiple of 64 with several chunks) is flagged and the
 // host takes the regular path.
 __global__ __launch_bounds__(1024) void small_run_kernel(const uint8_t *__restrict__ s, uint64_t len, uint32_t count,
-                                                         int proto, uint32_t cs, int ctype,
+                                                         int proto, uint32_t cs, int ctype, int verify,
                                                          const uint32_t *__restrict__ tab,
                                                          const uint32_t *__restrict__ pow2,
                                                          uint8_t *__restrict__ hout, uint32_t seq) {
@@ -1981,7 +1981,7 @@ __global__ __launch_bounds__(1024) void small_run_kernel(const uint8_t *__restri
       const int st = grid_frame(s, len, pos, win, proto, cs, ctype, r, total);
       code = st == frame::kStepMore ? kGridMore : st == frame::kStepStop ? kGridStop : total == stride ? kGridOn : kGridOff;
     }
-    const bool want = code != kGridMore && !r.error && r.crc_len > 0 && ctype != HDFS_CRC32C_CSUM_NULL;
+    const bool want = verify && code != kGridMore && !r.error && r.crc_len > 0 && ctype != HDFS_CRC32C_CSUM_NULL;
     const uint32_t nch = want ? uint32_t(r.crc_len) / 4u : 0u;
     const bool fits = uint32_t(r.data_len) <= kSmallMax && nch <= kSmallMaxChunks && (cs % 64u == 0 || nch == 1u);
     rec = r;
@@ -2089,10 +2089,11 @@ __global__ __launch_bounds__(1024) void small_run_kernel(const uint8_t *__restri
 }
 
 hipError_t launch_small_run(const uint8_t *s, uint64_t len, uint32_t count, int proto, uint32_t cs, int ctype,
-                            const uint32_t *tab, const uint32_t *pow2, uint8_t *hout, uint32_t seq, hipStream_t stream) {
+                            int verify, const uint32_t *tab, const uint32_t *pow2, uint8_t *hout, uint32_t seq,
+                            hipStream_t stream) {
   if (!count || count > kSmallRunMax) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(small_run_kernel, dim3(count), dim3(1024), 0, stream, s, len, count, proto, cs, ctype, tab, pow2,
-                     hout, seq);
+  hipLaunchKernelGGL(small_run_kernel, dim3(count), dim3(1024), 0, stream, s, len, count, proto, cs, ctype, verify, tab,
+                     pow2, hout, seq);
   return hipGetLastError();
 }
 

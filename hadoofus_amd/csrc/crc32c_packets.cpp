@@ -532,14 +532,15 @@ int reserve_grid(DevCtx &c, size_t si, const GridLayout &L) {
 // after at most two packets (a stream of mixed sizes) hands the rest to the
 // host window walk (walk_device_stream).  Same records, stopping rules and
 // consumed offset as parse_packet_stream.
-// Short runs (<= kSmallRunMax packets of <= 64 KiB, the per-read case):
+// Short runs (<= kSmallRunMax packets of <= 64 KiB, the per-read case; verify
+// or framing only):
 // framing and verify in ONE launch (small_run_kernel) instead of the framing
 // pass + verify + finalize chain.  Returns 1 when the run is fully resolved
 // there (records in dst), 0 when the regular path must run (a packet the
 // kernel cannot take, a packet off the grid, more packets than it covers),
 // < 0 on an engine error.
-int small_run(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs, int ctype, size_t max_pkts,
-              hdfs_crc32c_packet *dst, size_t *nout, uint64_t *consumed, uint64_t *payload) {
+int small_run(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs, int ctype, bool verify,
+              size_t max_pkts, hdfs_crc32c_packet *dst, size_t *nout, uint64_t *consumed, uint64_t *payload) {
   if (!c.sr_h) {
     HIPCHK(hipHostMalloc(&c.sr_h, kSrHostBytes, hipHostMallocCoherent | hipHostMallocMapped));
     std::memset(c.sr_h, 0, kSrHostBytes);
@@ -548,8 +549,8 @@ int small_run(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
   const uint32_t count = uint32_t(std::min<uint64_t>({uint64_t(kSmallRunMax), uint64_t(max_pkts), len / 6 + 1}));
   const uint32_t seq = ++c.grid_seq;
   const int tset = ctype == HDFS_CRC32C_CSUM_CRC32 ? 1 : 0;
-  HIPCHK(launch_small_run(d, len, count, proto, cs, ctype, c.d_tab_main_t[tset], c.d_tab_pow2_t[tset], c.sr_hd, seq,
-                          c.stream));
+  HIPCHK(launch_small_run(d, len, count, proto, cs, ctype, verify ? 1 : 0, c.d_tab_main_t[tset], c.d_tab_pow2_t[tset],
+                          c.sr_hd, seq, c.stream));
   auto word = [&](uint32_t k, int i) -> const uint32_t * {
     return reinterpret_cast<const uint32_t *>(c.sr_h + size_t(k) * kSrSlot + kGridRecBytes) + i;
   };
@@ -619,9 +620,9 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
   *nout = 0;
   *consumed = 0;
   verify = verify && ctype != HDFS_CRC32C_CSUM_NULL;
-  if (verify && !copy_dst && max_pkts && len <= kSmallRunBytes) {
+  if (!copy_dst && max_pkts && len <= kSmallRunBytes) {  // framing only (parse) too
     uint64_t pay = 0;
-    const int r = small_run(c, d, len, proto, cs, ctype, max_pkts, dst, nout, consumed, &pay);
+    const int r = small_run(c, d, len, proto, cs, ctype, verify, max_pkts, dst, nout, consumed, &pay);
     if (r < 0) return r;
     if (r == 1) {
       if (payload_out) *payload_out = pay;
