@@ -55,8 +55,8 @@ hipError_t launch_header_window(const uint8_t *s, uint64_t len, uint64_t base, u
 // points, one workgroup each); hout: pinned host slots (device address),
 // kSrHostBytes.
 hipError_t launch_small_run(const uint8_t *s, uint64_t len, uint32_t count, int proto, uint32_t cs, int ctype,
-                            int verify, const uint32_t *tab, const uint32_t *pow2, uint8_t *hout, uint32_t seq,
-                            hipStream_t stream);
+                            int verify, const uint32_t *tab, const uint32_t *pow2, uint8_t *copy_dst,
+                            uint64_t copy_cap, uint8_t *hout, uint32_t seq, hipStream_t stream);
 hipError_t launch_frame_grid(const uint8_t *s, uint64_t len, uint64_t base, uint32_t count, int proto, uint32_t cs,
                              int ctype, int verify, uint32_t sflags, uint8_t *bm_base, uint8_t *copy_base,
                              uint64_t copy_cap, GridBufs g, hipStream_t stream);

@@ -1956,16 +1956,27 @@ __global__ __launch_bounds__(1024) void small_run_kernel(const uint8_t *__restri
                                                          int proto, uint32_t cs, int ctype, int verify,
                                                          const uint32_t *__restrict__ tab,
                                                          const uint32_t *__restrict__ pow2,
+                                                         uint8_t *__restrict__ copy_dst, uint64_t copy_cap,
                                                          uint8_t *__restrict__ hout, uint32_t seq) {
   __shared__ uint32_t tt[1024];
   __shared__ __attribute__((aligned(16))) uint32_t zt[16 * 1024];  // Z_{2^b}, b < 16 (the levels a shift can use)
   __shared__ uint32_t acc[kSmallMaxChunks];
-  __shared__ __attribute__((aligned(16))) uint8_t win[kHdrWin];
+  __shared__ __attribute__((aligned(16))) uint8_t win[kSmallRunMax][kHdrWin];
   __shared__ hdfs_crc32c_packet rec;
-  __shared__ uint32_t ctl[6];  // code, verify this packet, unsupported, first bad, bad chunks, levels
+  // code, verify this packet, unsupported, first bad, bad chunks, levels,
+  // copy-out: destination offset (lo, hi), every earlier packet On and clean
+  __shared__ uint32_t ctl[9];
+  __shared__ uint32_t sdl[kSmallRunMax], son[kSmallRunMax];
   const uint32_t tid = threadIdx.x, k = blockIdx.x;
   tt[tid] = tab[tid];
-  if (tid == 0) {
+  // Copy-out needs this packet's place in the de-framed payload: thread t
+  // frames packet t of the run for t <= k (k + 1 headers in parallel, one
+  // round trip) -- every earlier packet must be On and framing-clean, and
+  // their data lengths sum to the destination offset.  Without copy-out
+  // only thread 0 frames, packet k.
+  const uint32_t nfr = copy_dst ? k + 1u : 1u;
+  if (tid < nfr) {
+    const uint32_t pk = copy_dst ? tid : k;
     // the grid: header_len + plen - 4 of the packet at 0 (as frame_grid_kernel)
     auto at0 = [&](uint64_t i) -> uint32_t { return i < len ? uint32_t(s[i]) : 0u; };
     const int32_t plen = int32_t((at0(0) << 24) | (at0(1) << 16) | (at0(2) << 8) | at0(3));
@@ -1975,23 +1986,39 @@ __global__ __launch_bounds__(1024) void small_run_kernel(const uint8_t *__restri
     hdfs_crc32c_packet r{};
     uint32_t code = kGridMore;
     uint64_t total = 0;
-    const uint64_t pos = uint64_t(k) * stride;
-    if ((k == 0 || stride) && pos < len) {
-      stage_header(s, len, pos, win);
-      const int st = grid_frame(s, len, pos, win, proto, cs, ctype, r, total);
+    const uint64_t pos = uint64_t(pk) * stride;
+    if ((pk == 0 || stride) && pos < len) {
+      stage_header(s, len, pos, win[tid]);
+      const int st = grid_frame(s, len, pos, win[tid], proto, cs, ctype, r, total);
       code = st == frame::kStepMore ? kGridMore : st == frame::kStepStop ? kGridStop : total == stride ? kGridOn : kGridOff;
     }
-    const bool want = verify && code != kGridMore && !r.error && r.crc_len > 0 && ctype != HDFS_CRC32C_CSUM_NULL;
-    const uint32_t nch = want ? uint32_t(r.crc_len) / 4u : 0u;
-    const bool fits = uint32_t(r.data_len) <= kSmallMax && nch <= kSmallMaxChunks && (cs % 64u == 0 || nch == 1u);
-    rec = r;
-    ctl[0] = code;
-    ctl[1] = want && fits ? 1u : 0u;
-    ctl[2] = want && !fits ? 1u : 0u;
-    ctl[3] = 0xFFFFFFFFu;
-    ctl[4] = 0u;
-    const uint32_t span = min(cs, uint32_t(r.data_len));  // longest shift: < one chunk
-    ctl[5] = span > 1u ? 32u - __builtin_clz(span - 1u) : 1u;
+    sdl[tid] = (code != kGridMore && !r.error) ? uint32_t(r.data_len) : 0u;
+    son[tid] = code == kGridOn && !r.error ? 1u : 0u;
+    if (pk == k) {
+      const bool want = verify && code != kGridMore && !r.error && r.crc_len > 0 && ctype != HDFS_CRC32C_CSUM_NULL;
+      const uint32_t nch = want ? uint32_t(r.crc_len) / 4u : 0u;
+      const bool fits = uint32_t(r.data_len) <= kSmallMax && nch <= kSmallMaxChunks && (cs % 64u == 0 || nch == 1u);
+      rec = r;
+      ctl[0] = code;
+      ctl[1] = want && fits ? 1u : 0u;
+      ctl[2] = want && !fits ? 1u : 0u;
+      ctl[3] = 0xFFFFFFFFu;
+      ctl[4] = 0u;
+      const uint32_t span = min(cs, uint32_t(r.data_len));  // longest shift: < one chunk
+      ctl[5] = span > 1u ? 32u - __builtin_clz(span - 1u) : 1u;
+    }
+  }
+  __syncthreads();
+  if (tid == 0 && copy_dst) {
+    uint64_t off = 0;
+    uint32_t ok = 1;
+    for (uint32_t t = 0; t < k; t++) {
+      off += sdl[t];
+      ok &= son[t];
+    }
+    ctl[6] = uint32_t(off);
+    ctl[7] = uint32_t(off >> 32);
+    ctl[8] = ok && off + uint64_t(rec.data_len) <= copy_cap ? 1u : 0u;
   }
   __syncthreads();
   if (ctl[1]) {
@@ -2069,6 +2096,25 @@ __global__ __launch_bounds__(1024) void small_run_kernel(const uint8_t *__restri
         atomicAdd(&ctl[4], 1u);
       }
     }
+    if (copy_dst && ctl[8] && b0 < dlen) {
+      // verify + copy-out: the piece, still in registers, to its place in the
+      // de-framed payload (a 16-B store crossing the range is dropped, so the
+      // packet's last partial 16 B go byte by byte)
+      uint8_t *dst = copy_dst + ((uint64_t(ctl[7]) << 32) | ctl[6]);
+      const __amdgpu_buffer_rsrc_t rw =
+          __builtin_amdgcn_make_buffer_rsrc(dst, 0, static_cast<int>(dlen), 0x00020000);
+#pragma unroll
+      for (uint32_t m = 0; m < 4; m++) {
+        const uint32_t o = b0 + 16u * m;
+        if (o + 16u <= dlen) {
+          const u32x4 v = {d[4 * m], d[4 * m + 1], d[4 * m + 2], d[4 * m + 3]};
+          __builtin_amdgcn_raw_buffer_store_b128(v, rw, o, 0, 0);
+        } else if (o < dlen) {
+          for (uint32_t b = o; b < dlen; b++)
+            __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(d[(b - b0) >> 2] >> (8u * (b & 3u))), rw, b, 0, 0);
+        }
+      }
+    }
   }
   __syncthreads();
   // this packet's slot in pinned host memory: record, status, verdict, then
@@ -2089,11 +2135,11 @@ __global__ __launch_bounds__(1024) void small_run_kernel(const uint8_t *__restri
 }
 
 hipError_t launch_small_run(const uint8_t *s, uint64_t len, uint32_t count, int proto, uint32_t cs, int ctype,
-                            int verify, const uint32_t *tab, const uint32_t *pow2, uint8_t *hout, uint32_t seq,
-                            hipStream_t stream) {
+                            int verify, const uint32_t *tab, const uint32_t *pow2, uint8_t *copy_dst,
+                            uint64_t copy_cap, uint8_t *hout, uint32_t seq, hipStream_t stream) {
   if (!count || count > kSmallRunMax) return hipErrorInvalidValue;
   hipLaunchKernelGGL(small_run_kernel, dim3(count), dim3(1024), 0, stream, s, len, count, proto, cs, ctype, verify, tab,
-                     pow2, hout, seq);
+                     pow2, copy_dst, copy_cap, hout, seq);
   return hipGetLastError();
 }
 

@@ -540,7 +540,8 @@ int reserve_grid(DevCtx &c, size_t si, const GridLayout &L) {
 // kernel cannot take, a packet off the grid, more packets than it covers),
 // < 0 on an engine error.
 int small_run(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs, int ctype, bool verify,
-              size_t max_pkts, hdfs_crc32c_packet *dst, size_t *nout, uint64_t *consumed, uint64_t *payload) {
+              uint8_t *copy_dst, uint64_t copy_cap, size_t max_pkts, hdfs_crc32c_packet *dst, size_t *nout,
+              uint64_t *consumed, uint64_t *payload) {
   if (!c.sr_h) {
     HIPCHK(hipHostMalloc(&c.sr_h, kSrHostBytes, hipHostMallocCoherent | hipHostMallocMapped));
     std::memset(c.sr_h, 0, kSrHostBytes);
@@ -550,7 +551,7 @@ int small_run(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
   const uint32_t seq = ++c.grid_seq;
   const int tset = ctype == HDFS_CRC32C_CSUM_CRC32 ? 1 : 0;
   HIPCHK(launch_small_run(d, len, count, proto, cs, ctype, verify ? 1 : 0, c.d_tab_main_t[tset], c.d_tab_pow2_t[tset],
-                          c.sr_hd, seq, c.stream));
+                          copy_dst, copy_cap, c.sr_hd, seq, c.stream));
   auto word = [&](uint32_t k, int i) -> const uint32_t * {
     return reinterpret_cast<const uint32_t *>(c.sr_h + size_t(k) * kSrSlot + kGridRecBytes) + i;
   };
@@ -620,11 +621,15 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
   *nout = 0;
   *consumed = 0;
   verify = verify && ctype != HDFS_CRC32C_CSUM_NULL;
-  if (!copy_dst && max_pkts && len <= kSmallRunBytes) {  // framing only (parse) too
+  if (max_pkts && len <= kSmallRunBytes) {  // verify (+ copy-out) or framing only
     uint64_t pay = 0;
-    const int r = small_run(c, d, len, proto, cs, ctype, verify, max_pkts, dst, nout, consumed, &pay);
+    const int r = small_run(c, d, len, proto, cs, ctype, verify, copy_dst, copy_cap, max_pkts, dst, nout, consumed,
+                            &pay);
     if (r < 0) return r;
     if (r == 1) {
+      if (copy_dst && pay > copy_cap)
+        return fail(HDFS_CRC32C_EINVAL, "copy-out buffer of %llu bytes is too small (%llu needed)",
+                    (unsigned long long)copy_cap, (unsigned long long)pay);
       if (payload_out) *payload_out = pay;
       return HDFS_CRC32C_OK;
     }

@@ -405,14 +405,14 @@ def test_gpu_device_stream_irregular_headers(engine, oracle, proto, pattern):
                                             (2, 100, CSUM_CRC32C), (2, 64, CSUM_CRC32C)])
 def test_gpu_device_stream_short_runs(engine, oracle, proto, cs, ctype):
     """Short device-resident runs (the per-read case) go through the one-launch
-    path (small_run_kernel: framing + verify per packet workgroup) when they
-    fit it and through the regular chain when they do not (more than 16
-    packets, a packet over 64 KiB, several chunks of a size that is not a
-    multiple of 64, packets off the grid): every case equals the oracle and
-    the host path."""
+    path (small_run_kernel: framing + verify + optional copy-out per packet
+    workgroup) when they fit it and through the regular chain when they do
+    not (more than 64 packets, a packet over 64 KiB, several chunks of a size
+    that is not a multiple of 64, packets off the grid): every case equals
+    the oracle and the host path, and the copied-out payload is exact."""
     rng = np.random.default_rng(cs + proto + ctype)
-    cases = [[65536], [65536] * 3, [65536] * 16, [65536] * 17, [40000] * 5, [1], [777] * 4, [65536, 100, 65536],
-             [70000], [65536] * 15 + [12345], [4096] * 16]
+    cases = [[65536], [65536] * 3, [65536] * 16, [65536] * 64, [65536] * 65, [40000] * 5, [1], [777] * 4,
+             [65536, 100, 65536], [70000], [65536] * 15 + [12345], [4096] * 16]
     for dl in cases:
         corrupt = set()
         for _ in range(3):
@@ -429,5 +429,13 @@ def test_gpu_device_stream_short_runs(engine, oracle, proto, cs, ctype):
                 for mp in (1, 2):
                     assert engine.verify_packets(None, proto, cs, ctype, max_pkts=mp, dptr=p, nbytes=len(s)) == \
                         oracle.verify_packets(s, proto, cs, ctype, max_pkts=mp), (dl, mp)
+                # verify + copy-out: the payload before the first error, byte for byte
+                dstb = engine.DeviceBuffer(sum(dl) + 64)
+                dstb.fill(0xA5)
+                rc, pkts, used, delivered = engine.verify_packets_copy(p, len(s), dstb.ptr, sum(dl), proto, cs, ctype)
+                assert (rc, pkts, used) == want, (dl, "copy")
+                expect = _payloads(s, want[1])
+                assert delivered == len(expect) and dstb.download(delivered).tobytes() == expect, (dl, "copy")
+                dstb.free()
                 keep.free()
             assert engine.verify_packets(s, proto, cs, ctype) == want
