@@ -533,7 +533,13 @@ DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, ui
       const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(
           reinterpret_cast<uint32_t *>(rfl64(reinterpret_cast<uint64_t>(sbase))), 0, static_cast<int>(rfl(range)),
           0x00020000);
-      __builtin_amdgcn_raw_buffer_store_b32(sval, rg, soff, 0, 16);
+      // product: sc1; diagnostic build: the store policies' cache bits
+      if (kDiag && L.store_policy == 1) __builtin_amdgcn_raw_buffer_store_b32(sval, rg, soff, 0, 2);        // nt
+      else if (kDiag && L.store_policy == 6) __builtin_amdgcn_raw_buffer_store_b32(sval, rg, soff, 0, 17);  // sc0 sc1
+      else if (kDiag && L.store_policy == 7) __builtin_amdgcn_raw_buffer_store_b32(sval, rg, soff, 0, 18);  // nt sc1
+      else if (kDiag && L.store_policy == 8) __builtin_amdgcn_raw_buffer_store_b32(sval, rg, soff, 0, 1);   // sc0
+      else if (kDiag && L.store_policy == 11) __builtin_amdgcn_raw_buffer_store_b32(sval, rg, soff, 0, 0);  // default
+      else __builtin_amdgcn_raw_buffer_store_b32(sval, rg, soff, 0, 16);
       return;
     }
     if constexpr (RUN == 1) {
