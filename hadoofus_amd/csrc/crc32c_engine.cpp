@@ -385,7 +385,7 @@ int mb_launch(DevCtx &c, uint32_t seq0) {
 bool mb_exited(const DevCtx &c) { return __atomic_load_n(&c.h_mb[16], __ATOMIC_ACQUIRE) == (c.mb_epoch << 1); }
 
 int mailbox_call(DevCtx &c, int mode, uint32_t len, uint32_t cs, uint32_t reg0, bool be, int ctype,
-                 const uint8_t *hsrc, const uint8_t *hcrc, uint32_t crc_bytes) {
+                 const uint8_t *dsrc, const uint8_t *hsrc, const uint8_t *hcrc, uint32_t crc_bytes) {
   const uint32_t seq = ++c.small_seq;
   if (c.mb_alive && mb_exited(c)) c.mb_alive = false;  // idled out since the last call
   if (!c.mb_alive) {
@@ -401,8 +401,13 @@ int mailbox_call(DevCtx &c, int mode, uint32_t len, uint32_t cs, uint32_t reg0, 
     if (crc_bytes) std::memcpy(c.h_small_in + kSmallMax, hcrc, crc_bytes);
   }
   c.h_mb[1] = len;
-  c.h_mb[2] = cs | (mode == kModeVerify ? kMbVerifyFlag : 0u) | (be ? kMbBeFlag : 0u) | (ctype ? kMbCrc32Flag : 0u);
+  c.h_mb[2] = cs | (mode == kModeVerify ? kMbVerifyFlag : 0u) | (be ? kMbBeFlag : 0u) | (ctype ? kMbCrc32Flag : 0u) |
+              (dsrc ? kMbDevFlag : 0u);
   c.h_mb[3] = reg0;
+  if (dsrc) {  // device data is read in place (HBM), any alignment
+    c.h_mb[4] = uint32_t(reinterpret_cast<uintptr_t>(dsrc));
+    c.h_mb[5] = uint32_t(reinterpret_cast<uintptr_t>(dsrc) >> 32);
+  }
   __atomic_store_n(&c.h_mb[0], seq, __ATOMIC_RELEASE);  // staged data and fields first (x86-TSO / release)
   const auto t0 = std::chrono::steady_clock::now();
   for (uint32_t spin = 1;; spin++) {
@@ -435,8 +440,8 @@ int mailbox_call(DevCtx &c, int mode, uint32_t len, uint32_t cs, uint32_t reg0, 
 
 int small_call(DevCtx &c, int mode, uint32_t len, uint32_t cs, uint32_t reg0, bool be, int ctype,
                const uint8_t *dsrc, const uint8_t *hsrc, const uint8_t *hcrc, uint32_t crc_bytes) {
-  if (c.mb_on && !dsrc && (cs % 64u == 0 || len <= cs))  // one chunk: chunk size = len (fits the request line)
-    return mailbox_call(c, mode, len, len <= cs ? len : cs, reg0, be, ctype, hsrc, hcrc, crc_bytes);
+  if (c.mb_on && (cs % 64u == 0 || len <= cs))  // one chunk: chunk size = len (fits the request line)
+    return mailbox_call(c, mode, len, len <= cs ? len : cs, reg0, be, ctype, dsrc, hsrc, hcrc, crc_bytes);
   if (hsrc) {
     std::memcpy(c.h_small_in, hsrc, len);
     if (crc_bytes) std::memcpy(c.h_small_in + kSmallMax, hcrc, crc_bytes);
@@ -481,7 +486,8 @@ int stream_crc_any(uint32_t crc, const void *buf, uint64_t len, uint32_t *out, i
     return HDFS_CRC32C_OK;
   }
   if (device_accessible(buf)) {
-    if (small_ok(len, len) && (reinterpret_cast<uintptr_t>(buf) & 15u) == 0) {
+    // one launch needs a 16-B aligned source; the resident mailbox takes any
+    if (small_ok(len, len) && (c->mb_on || (reinterpret_cast<uintptr_t>(buf) & 15u) == 0)) {
       rc = small_call(*c, kModeCompute, uint32_t(len), uint32_t(len), ~crc, false, ctype,
                       static_cast<const uint8_t *>(buf));
       if (rc) return rc;

@@ -180,6 +180,8 @@ constexpr uint32_t kSmallMaxChunks = 2048;
 
 // Mailbox request line (resident small-call kernel): word 2 = chunk_size | flags.
 constexpr uint32_t kMbVerifyFlag = 1u << 24, kMbBeFlag = 1u << 25, kMbCrc32Flag = 1u << 26, kMbQuitFlag = 1u << 27;
+// device-memory source: its 64-bit address is the word pair after the line
+constexpr uint32_t kMbDevFlag = 1u << 28;
 
 
 constexpr uint32_t kRoundBytes = 512;  // sub-chunk handled by 8 lanes per round

@@ -1257,7 +1257,7 @@ __global__ __launch_bounds__(1024) void mailbox_kernel(const uint32_t *__restric
   __shared__ __attribute__((aligned(16))) uint32_t zt[2][16 * 1024];  // Z_{2^b}, b < 16, per type
   __shared__ uint32_t acc[kSmallMaxChunks];
   __shared__ uint32_t res[2];
-  __shared__ uint32_t ctl[4];
+  __shared__ uint32_t ctl[6];
   const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
   // tables once for the kernel's lifetime
   tt[0][tid] = tab0[tid];
@@ -1294,11 +1294,17 @@ __global__ __launch_bounds__(1024) void mailbox_kernel(const uint32_t *__restric
       ctl[1] = v.y;
       ctl[2] = v.z;
       ctl[3] = v.w;
+      if (v.z & kMbDevFlag) {  // device-memory source: its address follows the request line
+        const uint64_t p = *(const volatile GAS uint64_t *)(const GAS uint8_t *)(req + 4);
+        ctl[4] = uint32_t(p);
+        ctl[5] = uint32_t(p >> 32);
+      }
       res[0] = 0xFFFFFFFFu;
       res[1] = 0u;
     }
     __syncthreads();
     const uint32_t seq = ctl[0], len = ctl[1], csf = ctl[2], reg0 = ctl[3];
+    const bool dev = (csf & kMbDevFlag) != 0u;
     if (csf & kMbQuitFlag) break;  // uniform: every wave leaves here
     const uint32_t cs = csf & 0x1FFFFu, ct = (csf & kMbCrc32Flag) ? 1u : 0u;
     const bool verify = (csf & kMbVerifyFlag) != 0u, be = (csf & kMbBeFlag) != 0u;
@@ -1307,10 +1313,24 @@ __global__ __launch_bounds__(1024) void mailbox_kernel(const uint32_t *__restric
     // every load before any compute: one PCIe round trip
     uint32_t d[16] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
     const uint32_t base = 4096u * w;
+    // device source: exactly len bytes in range (a 16-B load that crosses
+    // the end returns zeros, so that piece is read byte by byte); host
+    // stage: the whole stage (bytes past len never enter a CRC)
+    const __amdgpu_buffer_rsrc_t rd =
+        dev ? __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<uint8_t *>((uint64_t(ctl[5]) << 32) | ctl[4]), 0,
+                                                static_cast<int>(len), 0x00020000)
+            : rin;
     if (base < len) {
 #pragma unroll
       for (uint32_t k = 0; k < 4; k++) {
-        const u32x4 x = sysload16(rin, base + (2u * k + hsel) * 512u + loff);
+        const uint32_t p = base + (2u * k + hsel) * 512u + loff;
+        u32x4 x = sysload16(rd, p);
+        if (dev && p < len && p + 16u > len) {
+          uint32_t wd[4] = {0u, 0u, 0u, 0u};
+          for (uint32_t b = p; b < len; b++)
+            wd[(b - p) >> 2] |= uint32_t(__builtin_amdgcn_raw_buffer_load_b8(rd, b, 0, 17)) << (8u * (b & 3u));
+          x = u32x4{wd[0], wd[1], wd[2], wd[3]};
+        }
         d[4 * k + 0] = x.x;
         d[4 * k + 1] = x.y;
         d[4 * k + 2] = x.z;

@@ -115,3 +115,59 @@ def test_mailbox_one_per_device(engine):
             engine.Mailbox()
     with engine.Mailbox():  # reopened after close
         pass
+
+
+def test_mailbox_concurrent_threads(engine, oracle):
+    """Eight host threads on the synchronous calls at once while a mailbox is
+    open (the engine serialises them on its context; each result must be its
+    own call's): drop-in CRCs and verify_crcdata verdicts stay exact."""
+    import threading
+
+    rng = np.random.default_rng(12)
+    bufs = [rng.integers(0, 256, int(n), dtype=np.uint8) for n in rng.integers(1, 65536, 32)]
+    want = [oracle.crc32c(0, b) for b in bufs]
+    regions = []
+    for b in bufs[:8]:
+        region, crcdlen = _crc_region(oracle, b, 512, 2)
+        regions.append((region, crcdlen, b.size))
+    errors = []
+
+    def work(tid):
+        try:
+            for it in range(20):
+                i = (tid * 7 + it) % len(bufs)
+                if engine.crc32c(0, bufs[i]) != want[i]:
+                    errors.append(("crc", tid, i))
+                region, crcdlen, dlen = regions[(tid + it) % len(regions)]
+                if engine.verify_crcdata(region, 512, crcdlen, dlen) != (0, -1):
+                    errors.append(("verify", tid, it))
+        except Exception as e:  # noqa: BLE001 -- reported by the assert below
+            errors.append(("exc", tid, repr(e)))
+
+    with engine.Mailbox() as mb:
+        ts = [threading.Thread(target=work, args=(t,)) for t in range(8)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        assert not errors, errors[:5]
+        assert mb.stats()[0] >= 8 * 40
+
+
+def test_mailbox_device_sources(engine, oracle):
+    """Device-memory sources (hdfs_crc32c_stream_dev and the drop-in symbols on
+    device pointers) through the mailbox: read in place from HBM at any byte
+    alignment, the last partial 16 B byte by byte; equal to the oracle."""
+    lib = engine.load()
+    host = oracle.splitmix(65536 // 8 + 4, seed=21).view(np.uint8)
+    dbuf = engine.DeviceBuffer(host.nbytes)
+    dbuf.upload(host)
+    with engine.Mailbox() as mb:
+        c0 = mb.stats()[0]
+        for off in range(0, 8):
+            for n in (1, 15, 16, 17, 100, 511, 4095, 4096, 30001, 65536 - off):
+                want = oracle.crc32c(0x1234 * off, host[off:off + n])
+                assert engine.stream_crc_dev(0x1234 * off, dbuf.ptr + off, n) == want, (off, n)
+                assert lib._hdfs_crc32c(0x1234 * off, dbuf.ptr + off, n) == want, (off, n)
+        assert mb.stats()[0] - c0 == 8 * 10 * 2
+    dbuf.free()

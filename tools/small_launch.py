@@ -119,6 +119,14 @@ def raw_call_us(prefix, iters=500):
     for _ in range(iters):
         lib.hdfs_crc32c_verify_crcdata(r4.ctypes.data, 512, len(be4), 4096, 2, ctypes.byref(fb))
     out[f"{prefix}verify_crcdata_4KiB_us"] = round((time.perf_counter() - t0) / iters * 1e6, 2)
+    # device-resident source (stream CRC of 64 KiB / 512 B in HBM, unaligned)
+    o = ctypes.c_uint32(0)
+    for name, n in (("64KiB", 65536), ("512B", 512)):
+        lib.hdfs_crc32c_stream_dev(0, dbuf.ptr + 3, n, ctypes.byref(o))
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            lib.hdfs_crc32c_stream_dev(0, dbuf.ptr + 3, n, ctypes.byref(o))
+        out[f"{prefix}stream_dev_{name}_unaligned_us"] = round((time.perf_counter() - t0) / iters * 1e6, 2)
 
 
 # ctypes overhead of a trivial call (subtract by eye)
