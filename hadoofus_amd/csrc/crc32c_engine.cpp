@@ -486,8 +486,8 @@ int stream_crc_any(uint32_t crc, const void *buf, uint64_t len, uint32_t *out, i
     return HDFS_CRC32C_OK;
   }
   if (device_accessible(buf)) {
-    // one launch needs a 16-B aligned source; the resident mailbox takes any
-    if (small_ok(len, len) && (c->mb_on || (reinterpret_cast<uintptr_t>(buf) & 15u) == 0)) {
+    // one launch (or the resident mailbox), any source alignment
+    if (small_ok(len, len)) {
       rc = small_call(*c, kModeCompute, uint32_t(len), uint32_t(len), ~crc, false, ctype,
                       static_cast<const uint8_t *>(buf));
       if (rc) return rc;
@@ -688,7 +688,7 @@ int chunk_crcs_to_host(const void *data, uint64_t len, uint32_t cs, int ctype, u
   if (rc) return rc;
   DeviceGuard g(c->dev);
   std::lock_guard<std::mutex> lk(c->mu);
-  if (small_ok(len, cs) && (!dev || (reinterpret_cast<uintptr_t>(data) & 15u) == 0)) {
+  if (small_ok(len, cs)) {  // device sources at any alignment
     if (!dev) std::memcpy(c->h_small_in, data, size_t(len));
     rc = small_call(*c, kModeCompute, uint32_t(len), cs, 0xFFFFFFFFu, true, tset,
                     dev ? static_cast<const uint8_t *>(data) : nullptr);

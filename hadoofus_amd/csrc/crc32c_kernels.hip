@@ -1125,6 +1125,10 @@ __global__ __launch_bounds__(1024) void small_chunks_kernel(const uint8_t *__res
   const uint32_t tv = tab[tid];
   u32x4 zv[4], dv[4];
   uint32_t ev[2] = {0u, 0u};
+  // device source (exact): buffer loads, which serve any byte address (a
+  // global dwordx4 load returns the aligned-down bytes)
+  const __amdgpu_buffer_rsrc_t rp =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(p), 0, static_cast<int>(len), 0x00020000);
 #pragma unroll
   for (uint32_t k = 0; k < 4; k++) {
     const uint32_t q = k * 1024u + tid;
@@ -1136,7 +1140,8 @@ __global__ __launch_bounds__(1024) void small_chunks_kernel(const uint8_t *__res
         for (uint32_t b = 16u * q; b < len; b++) wds[(b >> 2) & 3u] |= uint32_t(gload8(p + b)) << (8u * (b & 3u));
         dv[k] = u32x4{wds[0], wds[1], wds[2], wds[3]};
       } else {
-        dv[k] = gload16(p + 16ull * q);
+        dv[k] = exact ? __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rp, 16u * q, 0, 0))
+                      : gload16(p + 16ull * q);
       }
     }
   }
@@ -2457,7 +2462,7 @@ hipError_t launch_small_chunks(int mode, const uint8_t *p, uint32_t len, uint32_
                                uint32_t *meta, uint32_t *crcs, uint32_t seq, hipStream_t stream) {
   const uint32_t nch = cs ? (len + cs - 1) / cs : 0u;
   if (!len || len > kSmallMax || !cs || (cs % 4u && nch > 1) || nch > kSmallMaxChunks ||
-      (reinterpret_cast<uintptr_t>(p) & 15u))
+      (!exact && (reinterpret_cast<uintptr_t>(p) & 15u)))
     return hipErrorInvalidValue;
   if (mode == kModeVerify)
     hipLaunchKernelGGL(small_chunks_kernel<kModeVerify>, dim3(1), dim3(1024), 0, stream, p, len, exact, cs, reg0, be,
