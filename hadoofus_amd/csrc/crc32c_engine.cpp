@@ -84,6 +84,9 @@ uint32_t g_xcd_major = uint32_t(HDFS_KNOB("HDFS_CRC32C_XCD", 1)) & 1u;
 // (profiles/r02/exp_compute_store_schedules.json: 0 / 1 / 2 = 6377 / 6595 /
 // 6626 GB/s of algorithmic bytes in one process).
 int g_runs = HDFS_KNOB("HDFS_CRC32C_RUNS", 2);
+// Small-call input stage: 1 fine-grained VRAM written through the BAR when
+// the device is large-BAR, else (and 0) pinned host memory.
+int g_stage_vram = HDFS_KNOB("HDFS_CRC32C_MB_STAGE", 1);
 // Diagnostic per-wave timestamps (device buffer, 3 x u64 per wave) or null.
 unsigned long long *g_diag = nullptr;
 
@@ -140,6 +143,13 @@ int ctx_init(int device, DevCtx **out) {
     HIPCHK(hipMemcpy(c.d_tab_main_t[ct], main.data(), main.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(c.d_tab_pow2_t[ct], pow2.data(), pow2.size() * 4, hipMemcpyHostToDevice));
   }
+  {
+    std::vector<uint32_t> kx(2 * kTabKxWords);
+    make_kx(kx.data(), kPoly);
+    make_kx(kx.data() + kTabKxWords, kPolyZlib);
+    HIPCHK(hipMalloc(&c.d_tab_kx, kx.size() * 4));
+    HIPCHK(hipMemcpy(c.d_tab_kx, kx.data(), kx.size() * 4, hipMemcpyHostToDevice));
+  }
   // Blocking stream: it serialises with the legacy NULL stream, so the
   // synchronous helpers (hipMemcpy/hipMemset) see prior plan work.
   HIPCHK(hipStreamCreate(&c.stream));
@@ -147,10 +157,27 @@ int ctx_init(int device, DevCtx **out) {
   HIPCHK(hipMalloc(&c.d_stage, kStageCap));
   HIPCHK(hipMalloc(&c.d_seg, sizeof(SegDev)));
   HIPCHK(hipMalloc(&c.d_small, 64));  // [0] acc [1] first_bad [2..3] mism [8] pool counter
-  HIPCHK(hipHostMalloc(&c.h_small_in, kSmallIn, hipHostMallocCoherent | hipHostMallocMapped));
+  // Small-call input stage.  Large-BAR devices: fine-grained VRAM the host
+  // writes through the BAR (64 KiB in ~1.3 us), which the kernels then read
+  // from HBM instead of across PCIe; otherwise pinned host memory.
+  int large_bar = 0;
+  if (g_stage_vram == 1 && hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, device) == hipSuccess &&
+      large_bar) {
+    void *v = nullptr;
+    if (hipExtMallocWithFlags(&v, 256 + kSmallIn, hipDeviceMallocFinegrained) == hipSuccess) {
+      c.stage_vram = static_cast<uint8_t *>(v);
+      std::memset(c.stage_vram, 0, 256);
+      __builtin_ia32_sfence();
+      c.h_small_in = c.dv_small_in = c.stage_vram + 256;
+    }
+  }
+  (void)hipGetLastError();
+  if (!c.stage_vram) {
+    HIPCHK(hipHostMalloc(&c.h_small_in, kSmallIn, hipHostMallocCoherent | hipHostMallocMapped));
+    HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&c.dv_small_in), c.h_small_in, 0));
+  }
   HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&c.h_small_out), kSmallOut, hipHostMallocCoherent | hipHostMallocMapped));
   std::memset(c.h_small_out, 0, kSmallOut);
-  HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&c.dv_small_in), c.h_small_in, 0));
   HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&c.dv_small_out), c.h_small_out, 0));
   c.ready.store(true, std::memory_order_release);
   *out = &c;
@@ -374,12 +401,35 @@ static const bool g_small_trace = std::getenv("HDFS_CRC32C_SMALL_TRACE") != null
 int mb_launch(DevCtx &c, uint32_t seq0) {
   c.mb_epoch++;
   __atomic_store_n(&c.h_mb[16], (c.mb_epoch << 1) | 1u, __ATOMIC_RELEASE);
-  HIPCHK(launch_mailbox(c.dv_mb, c.dv_small_in, c.dv_small_out, c.dv_small_out + kSmallMeta, c.d_tab_main_t[0],
-                        c.d_tab_main_t[1], c.d_tab_pow2_t[0], c.d_tab_pow2_t[1], c.dv_mb + 16, c.mb_epoch, seq0,
-                        c.mb_idle_ticks, c.mb_stream));
+  HIPCHK(launch_mailbox(c.mb_req_d, c.dv_small_in, c.dv_small_out, c.dv_small_out + kSmallMeta, c.d_tab_main_t[0],
+                        c.d_tab_main_t[1], c.d_tab_kx, c.dv_mb + 16, c.mb_epoch, seq0, c.mb_idle_ticks, c.mb_stream));
   c.mb_alive = true;
   c.mb_launches++;
   return HDFS_CRC32C_OK;
+}
+
+// Writes one request line: the fields, then the sequence number the kernel
+// polls.  Pinned stage: x86-TSO store order is the order the device sees.
+// VRAM stage: the BAR mapping is write-combining, so a store fence drains
+// the staged bytes and fields before the sequence number, and a second one
+// pushes the sequence number out instead of leaving it in a WC buffer.
+void mb_post(DevCtx &c, uint32_t seq, uint32_t len, uint32_t csf, uint32_t reg0, const uint8_t *dsrc) {
+  volatile uint32_t *r = c.mb_req;
+  r[1] = len;
+  r[2] = csf;
+  r[3] = reg0;
+  if (dsrc) {  // device data is read in place (HBM), any alignment
+    r[4] = uint32_t(reinterpret_cast<uintptr_t>(dsrc));
+    r[5] = uint32_t(reinterpret_cast<uintptr_t>(dsrc) >> 32);
+  }
+  if (c.stage_vram) {
+    __builtin_ia32_sfence();
+    r[0] = seq;
+    __builtin_ia32_sfence();
+  } else {
+    __atomic_store_n(&c.mb_req[0], seq, __ATOMIC_RELEASE);  // staged data and fields first (x86-TSO / release)
+  }
+  c.mb_posted = seq;
 }
 
 bool mb_exited(const DevCtx &c) { return __atomic_load_n(&c.h_mb[16], __ATOMIC_ACQUIRE) == (c.mb_epoch << 1); }
@@ -387,9 +437,10 @@ bool mb_exited(const DevCtx &c) { return __atomic_load_n(&c.h_mb[16], __ATOMIC_A
 int mailbox_call(DevCtx &c, int mode, uint32_t len, uint32_t cs, uint32_t reg0, bool be, int ctype,
                  const uint8_t *dsrc, const uint8_t *hsrc, const uint8_t *hcrc, uint32_t crc_bytes) {
   const uint32_t seq = ++c.small_seq;
+  const auto ta = std::chrono::steady_clock::now();
   if (c.mb_alive && mb_exited(c)) c.mb_alive = false;  // idled out since the last call
   if (!c.mb_alive) {
-    const int rc = mb_launch(c, __atomic_load_n(&c.h_mb[0], __ATOMIC_ACQUIRE));
+    const int rc = mb_launch(c, c.mb_posted);
     if (rc) return rc;
   }
   // Staged before the request line.  (Staging 16 KiB pieces behind it with
@@ -400,19 +451,21 @@ int mailbox_call(DevCtx &c, int mode, uint32_t len, uint32_t cs, uint32_t reg0, 
     std::memcpy(c.h_small_in, hsrc, len);
     if (crc_bytes) std::memcpy(c.h_small_in + kSmallMax, hcrc, crc_bytes);
   }
-  c.h_mb[1] = len;
-  c.h_mb[2] = cs | (mode == kModeVerify ? kMbVerifyFlag : 0u) | (be ? kMbBeFlag : 0u) | (ctype ? kMbCrc32Flag : 0u) |
-              (dsrc ? kMbDevFlag : 0u);
-  c.h_mb[3] = reg0;
-  if (dsrc) {  // device data is read in place (HBM), any alignment
-    c.h_mb[4] = uint32_t(reinterpret_cast<uintptr_t>(dsrc));
-    c.h_mb[5] = uint32_t(reinterpret_cast<uintptr_t>(dsrc) >> 32);
-  }
-  __atomic_store_n(&c.h_mb[0], seq, __ATOMIC_RELEASE);  // staged data and fields first (x86-TSO / release)
+  const uint32_t csf = cs | (mode == kModeVerify ? kMbVerifyFlag : 0u) | (be ? kMbBeFlag : 0u) |
+                       (ctype ? kMbCrc32Flag : 0u) | (dsrc ? kMbDevFlag : 0u);
+  mb_post(c, seq, len, csf, reg0, dsrc);
   const auto t0 = std::chrono::steady_clock::now();
   for (uint32_t spin = 1;; spin++) {
     if (__atomic_load_n(&c.h_small_out[2], __ATOMIC_ACQUIRE) == seq) {
       c.mb_calls++;
+      if (g_small_trace) {  // diagnostic: host staging / wait, kernel phases (diag build, 10 ns ticks)
+        const auto t1 = std::chrono::steady_clock::now();
+        const uint32_t *m = c.h_small_out;
+        std::fprintf(stderr, "mailbox len=%u cs=%u stage_us=%.2f wait_us=%.2f load_us=%.2f comp_us=%.2f\n", len, cs,
+                     std::chrono::duration<double, std::micro>(t0 - ta).count(),
+                     std::chrono::duration<double, std::micro>(t1 - t0).count(), (m[5] - m[4]) / 100.0,
+                     (m[6] - m[5]) / 100.0);
+      }
       // a single chunk's CRC came with the completion word (one store)
       if (mode != kModeVerify && len <= cs) c.h_small_out[kSmallMeta] = c.h_small_out[3];
       return HDFS_CRC32C_OK;
@@ -438,19 +491,26 @@ int mailbox_call(DevCtx &c, int mode, uint32_t len, uint32_t cs, uint32_t reg0, 
   }
 }
 
+// Calls the open mailbox serves (chunk size a multiple of 64, or one chunk:
+// chunk size = len, which fits the request line).
+bool mb_serves(const DevCtx &c, uint32_t len, uint32_t cs) { return c.mb_on && (cs % 64u == 0 || len <= cs); }
+
 int small_call(DevCtx &c, int mode, uint32_t len, uint32_t cs, uint32_t reg0, bool be, int ctype,
                const uint8_t *dsrc, const uint8_t *hsrc, const uint8_t *hcrc, uint32_t crc_bytes) {
-  if (c.mb_on && (cs % 64u == 0 || len <= cs))  // one chunk: chunk size = len (fits the request line)
+  if (mb_serves(c, len, cs))
     return mailbox_call(c, mode, len, len <= cs ? len : cs, reg0, be, ctype, dsrc, hsrc, hcrc, crc_bytes);
   if (hsrc) {
     std::memcpy(c.h_small_in, hsrc, len);
     if (crc_bytes) std::memcpy(c.h_small_in + kSmallMax, hcrc, crc_bytes);
   }
+  // a VRAM stage is write-combining: drain it before the launch
+  if (c.stage_vram) __builtin_ia32_sfence();
   const uint32_t seq = ++c.small_seq;
   const auto tl = std::chrono::steady_clock::now();
   HIPCHK(launch_small_chunks(mode, dsrc ? dsrc : c.dv_small_in, len, dsrc ? 1u : 0u, cs, reg0, be ? 1u : 0u,
                              reinterpret_cast<const uint32_t *>(c.dv_small_in + kSmallMax), c.d_tab_main_t[ctype],
-                             c.d_tab_pow2_t[ctype], c.dv_small_out, c.dv_small_out + kSmallMeta, seq, c.stream));
+                             c.d_tab_kx + ctype * kTabKxWords, ctype ? kPolyZlib : kPoly, c.dv_small_out,
+                             c.dv_small_out + kSmallMeta, seq, c.stream));
   const auto t0 = std::chrono::steady_clock::now();
   for (uint32_t spin = 1;; spin++) {
     if (__atomic_load_n(&c.h_small_out[2], __ATOMIC_ACQUIRE) == seq) {
@@ -1276,6 +1336,15 @@ int hdfs_crc32c_mailbox_create(hdfs_crc32c_mailbox **mb, uint32_t idle_ms) {
     std::memset(c->h_mb, 0, 256);
     HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&c->dv_mb), c->h_mb, 0));
   }
+  if (!c->mb_req) {
+    if (c->stage_vram) {
+      c->mb_req = c->mb_req_d = reinterpret_cast<uint32_t *>(c->stage_vram);
+    } else {
+      c->mb_req = c->h_mb;
+      c->mb_req_d = c->dv_mb;
+    }
+    c->mb_posted = 0;
+  }
   if (!c->mb_stream) HIPCHK(hipStreamCreateWithFlags(&c->mb_stream, hipStreamNonBlocking));
   const uint64_t ms = idle_ms ? idle_ms : 50u;
   c->mb_idle_ticks = uint32_t(std::min<uint64_t>(ms * 100000u, 0xFFFFFFFFu));  // s_memrealtime: 100 MHz
@@ -1283,7 +1352,7 @@ int hdfs_crc32c_mailbox_create(hdfs_crc32c_mailbox **mb, uint32_t idle_ms) {
   // the bulk kernels' next launches leave the mailbox its CU
   HIPCHK(hipStreamSynchronize(c->stream));
   c->mb_on = true;
-  rc = mb_launch(*c, __atomic_load_n(&c->h_mb[0], __ATOMIC_ACQUIRE));
+  rc = mb_launch(*c, c->mb_posted);
   if (rc) {
     c->mb_on = false;
     return rc;
@@ -1310,8 +1379,7 @@ int hdfs_crc32c_mailbox_destroy(hdfs_crc32c_mailbox *mb) {
   if (!c.mb_on) return HDFS_CRC32C_OK;
   c.mb_on = false;
   if (c.mb_alive && !mb_exited(c)) {  // a quit request; the kernel acknowledges through its status word
-    c.h_mb[2] = kMbQuitFlag;
-    __atomic_store_n(&c.h_mb[0], ++c.small_seq, __ATOMIC_RELEASE);
+    mb_post(c, ++c.small_seq, 0u, kMbQuitFlag, 0u, nullptr);
   }
   c.mb_alive = false;
   HIPCHK(hipStreamSynchronize(c.mb_stream));

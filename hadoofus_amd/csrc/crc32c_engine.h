@@ -34,14 +34,14 @@ hipError_t launch_corrupt(uint8_t *data, uint64_t len, uint32_t cs, uint64_t chu
 hipError_t launch_composite(const SegDev *segs, uint32_t nseg, const uint64_t *run_prefix, uint64_t total_runs,
                             const uint32_t *pow2, uint32_t *out, hipStream_t stream);
 hipError_t launch_small_chunks(int mode, const uint8_t *p, uint32_t len, uint32_t exact, uint32_t cs, uint32_t reg0,
-                               uint32_t be, const uint32_t *expect, const uint32_t *tab, const uint32_t *pow2,
-                               uint32_t *meta, uint32_t *crcs, uint32_t seq, hipStream_t stream);
+                               uint32_t be, const uint32_t *expect, const uint32_t *tab, const uint32_t *kx,
+                               uint32_t poly, uint32_t *meta, uint32_t *crcs, uint32_t seq, hipStream_t stream);
 hipError_t launch_prep(uint32_t *fb, uint32_t nfb, unsigned long long *mism, uint32_t *gctr, hipStream_t stream);
 // Resident mailbox kernel (one workgroup; exits on a quit request or after
 // idle_ticks of 10 ns without one; status[0] = (epoch << 1) | alive).
 hipError_t launch_mailbox(const uint32_t *req, const uint8_t *in, uint32_t *meta, uint32_t *crcs, const uint32_t *tab0,
-                          const uint32_t *tab1, const uint32_t *pow0, const uint32_t *pow1, uint32_t *status,
-                          uint32_t epoch, uint32_t seq0, uint32_t idle_ticks, hipStream_t stream);
+                          const uint32_t *tab1, const uint32_t *kx, uint32_t *status, uint32_t epoch, uint32_t seq0,
+                          uint32_t idle_ticks, hipStream_t stream);
 hipError_t launch_gather(const uint8_t *raw, const PktDesc *descs, uint32_t npk, uint32_t units, uint8_t *arena,
                          uint8_t *crc_arena, hipStream_t stream);
 // proto 1 / 2: derive the stride from the packet at base (v1 / v2 header)
@@ -111,6 +111,7 @@ struct DevCtx {
   // table sets per checksum type: [0] CRC32C, [1] CRC32 (zlib polynomial)
   uint32_t *d_tab_main_t[2] = {nullptr, nullptr};
   uint32_t *d_tab_pow2_t[2] = {nullptr, nullptr};
+  uint32_t *d_tab_kx = nullptr;  // mailbox multipliers, kTabKxWords per type
   hipStream_t stream = nullptr;
   // one-shot scratch (guarded by mu)
   uint8_t *h_stage = nullptr;
@@ -123,6 +124,11 @@ struct DevCtx {
   // expected CRCs) and output block (meta words, then CRCs), read / written
   // by small_chunks_kernel directly (no DMA copies); seq = completion number
   uint8_t *h_small_in = nullptr, *dv_small_in = nullptr;
+  // large-BAR devices: the input stage is fine-grained VRAM the host writes
+  // through the BAR ([0, 256) the mailbox request line, then the stage at
+  // h_small_in == dv_small_in), so the kernels read HBM instead of PCIe;
+  // null: pinned host memory
+  uint8_t *stage_vram = nullptr;
   uint32_t *h_small_out = nullptr, *dv_small_out = nullptr;
   uint32_t small_seq = 0;
   // device CRC scratch of chunk_crcs_to_host (guarded by mu)
@@ -175,6 +181,12 @@ struct DevCtx {
   // seq, len, chunk_size | flags, register) and status word ([16])
   bool mb_on = false, mb_alive = false;
   uint32_t *h_mb = nullptr, *dv_mb = nullptr;
+  // request line the mailbox polls: in stage_vram when there is one, else
+  // h_mb (host-writable view mb_req, device view mb_req_d).  The host never
+  // reads VRAM back (uncached BAR reads), so mb_posted shadows the last
+  // sequence number written.
+  uint32_t *mb_req = nullptr, *mb_req_d = nullptr;
+  uint32_t mb_posted = 0;
   hipStream_t mb_stream = nullptr;
   uint32_t mb_epoch = 0, mb_idle_ticks = 0;
   uint64_t mb_calls = 0, mb_launches = 0;
@@ -231,9 +243,9 @@ bool any_unaligned(const SegDev *segs, size_t n);
 int pipe_reserve(DevCtx &c, size_t piece, uint32_t cs, size_t npieces);
 
 // One-launch path for synchronous calls on <= kSmallMax bytes
-// (small_chunks_kernel; caller holds c.mu and has staged the data in
-// c.h_small_in[0, len), wire CRCs at c.h_small_in + kSmallMax for verify,
-// unless dsrc names a 16-B aligned device source).  ctype: table set (0
+// (small_chunks_kernel or the open mailbox; caller holds c.mu and has staged
+// the data in c.h_small_in[0, len), wire CRCs at + kSmallMax for verify,
+// unless dsrc names a device source or hsrc / hcrc are given).  ctype: table set (0
 // CRC32C, 1 CRC32).  Results: c.h_small_out[0] first bad, [1] mismatches,
 // CRCs from c.h_small_out + kSmallMeta.
 bool small_ok(uint64_t len, uint64_t cs);

@@ -145,6 +145,12 @@ constexpr uint32_t kTabMainWords = kTabSliceWords + kTabZposWords;
 constexpr uint32_t kPow2Levels = 48;
 constexpr uint32_t kTabPow2Words = kPow2Levels * 1024;
 
+// Multiply-mod constants of the mailbox kernel, per checksum type:
+//  [0, 1024)     x^(512 m) mod P, m < 1024 (append 64 m zero bytes)
+//  [1024, 1088)  x^(8 r) mod P, r < 64
+// reflected polynomials, x^0 at bit 31; both types back to back.
+constexpr uint32_t kTabKxWords = 1088;
+
 // One received packet inside a de-framing piece (packet-stream verifier).
 // The piece's raw bytes are the wire bytes; the gather kernel copies each
 // packet's CRCs to a 4-B aligned CRC arena and its data to a 16-B aligned

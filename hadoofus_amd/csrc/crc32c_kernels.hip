@@ -1077,22 +1077,36 @@ __global__ __launch_bounds__(256) void crc32c_combine_kernel(
   if ((threadIdx.x & 63u) == 0 && v) atomicXor(acc, v);
 }
 
+// GF(2) product a * b mod P of two reflected polynomials (x^0 at bit 31),
+// branch-free: bit 31 - i of a is the x^i coefficient; b steps through
+// b * x^i.  About 5 VALU ops per bit and no table (the LDS stays free for
+// the replicated slicing tables).
+DEV uint32_t gf2_mulmod(uint32_t a, uint32_t b, uint32_t poly) {
+  uint32_t p = 0u;
+#pragma unroll
+  for (int i = 31; i >= 0; i--) {
+    p ^= b & (0u - ((a >> i) & 1u));
+    b = (b >> 1) ^ (poly & (0u - (b & 1u)));
+  }
+  return p;
+}
+
 // One-launch kernel for the synchronous host-memory calls on <= kSmallMax
 // bytes: the drop-in _hdfs_crc32c family (src/crc32c.h:13-24, one chunk of
 // `len` bytes continuing from the caller's register), the write loop mirror
 // (src/datanode.c:2814-2860, compute) and _verify_crcdata
 // (src/datanode.c:2931-2963, verify).  The caller's bytes are staged in
-// fine-grained pinned host memory and read by the kernel over PCIe
-// (coalesced 1 KiB per wave instruction, no DMA copy, no second launch);
-// results and a completion sequence number go straight back to pinned host
-// memory, which the host polls.
+// fine-grained VRAM written through the BAR (large-BAR devices) or pinned
+// host memory read over PCIe (coalesced 1 KiB per wave instruction, no DMA
+// copy, no second launch); results and a completion sequence number go
+// straight back to pinned host memory, which the host polls.
 //
-// Each chunk is split in 64-B pieces, one per thread: piece k of chunk j
-// yields the raw register r (the chunk's first piece starts from `reg0`),
-// shifted past the rest of its chunk with the power-of-two zeros operators
-// (the combine algebra of src/crc32c_sse42.c:99-200) and XOR-ed into the
-// chunk's accumulator in LDS.  Needs chunk_size % 4 == 0 and at most
-// kSmallMaxChunks chunks.
+// Each chunk is split in 16/32/64-B pieces, one per thread: piece k of chunk
+// j yields the raw register r (the chunk's first piece starts from `reg0`),
+// moved past the rest of its chunk (dd = 64 m + r bytes) by GF(2) multiplies
+// with x^(512 m) and x^(8 r) mod P (kx; the combine algebra of
+// src/crc32c_sse42.c:99-200) and XOR-ed into the chunk's accumulator in LDS.
+// Needs chunk_size % 4 == 0 and at most kSmallMaxChunks chunks.
 // meta: [0] first bad chunk (verify, 0xFFFFFFFF none) [1] mismatches
 //       [2] completion sequence number; crcs: compute output (u32, BE if be)
 template <int MODE>
@@ -1100,12 +1114,11 @@ __global__ __launch_bounds__(1024) void small_chunks_kernel(const uint8_t *__res
                                                              uint32_t exact, uint32_t cs, uint32_t reg0, uint32_t be,
                                                              const uint32_t *__restrict__ expect,
                                                              const uint32_t *__restrict__ tab,
-                                                             const uint32_t *__restrict__ pow2,
+                                                             const uint32_t *__restrict__ kx, uint32_t poly,
                                                              uint32_t *__restrict__ meta,
                                                              uint32_t *__restrict__ crcs, uint32_t seq) {
-  __shared__ uint32_t tt[1024];                                    // t0..t3
-  __shared__ __attribute__((aligned(16))) uint32_t zt[16 * 1024];  // Z_{2^b}, b < 16
-  __shared__ uint32_t dat[kSmallMax / 4 + kSmallMax / 64];         // one pad word per 16
+  __shared__ uint32_t tt[1024];                             // t0..t3
+  __shared__ uint32_t dat[kSmallMax / 4 + kSmallMax / 64];  // one pad word per 16
   __shared__ uint32_t acc[kSmallMaxChunks];
   __shared__ uint32_t res[2];
   const uint32_t tid = threadIdx.x;
@@ -1116,23 +1129,33 @@ __global__ __launch_bounds__(1024) void small_chunks_kernel(const uint8_t *__res
   while (psz < 64u && nch * ((cs + psz - 1) / psz) > 1024u) psz *= 2u;
   const uint32_t ppc = (cs + psz - 1) / psz;
   // Every global / host load of the prologue is issued before any LDS
-  // store (one PCIe round trip for the data, one HBM/L2 trip for tables).
-  // Only the operator levels a shift (< len) can use are loaded.
+  // store (one round trip for the data, one HBM/L2 trip for the table and
+  // this thread's first two multipliers).
   static_assert(kSmallMax / 16 == 4 * 1024 && kSmallMaxChunks == 2 * 1024, "prologue shape");
   const uint64_t ts0 = __builtin_amdgcn_s_memrealtime();  // phase stamps (100 MHz) -> meta[4..11]
-  const uint32_t nlev = len > 1u ? 32u - __builtin_clz(len - 1u) : 1u;
   const uint32_t nvec = (len + 15u) / 16u;
   const uint32_t tv = tab[tid];
-  u32x4 zv[4], dv[4];
+  // shift distance of this thread's first piece (the loop below starts there)
+  uint32_t km0 = 0x80000000u, kr0 = 0x80000000u;
+  if (tid < nch * ppc) {
+    const uint32_t j = tid / ppc, cend = min((j + 1u) * cs, len), b0 = j * cs + psz * (tid - j * ppc);
+    if (b0 < cend) {
+      const uint32_t dd = cend - min(b0 + psz, cend);
+      km0 = kx[dd >> 6];
+      kr0 = kx[1024u + (dd & 63u)];
+    }
+  }
+  u32x4 dv[4];
   uint32_t ev[2] = {0u, 0u};
-  // device source (exact): buffer loads, which serve any byte address (a
-  // global dwordx4 load returns the aligned-down bytes)
-  const __amdgpu_buffer_rsrc_t rp =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(p), 0, static_cast<int>(len), 0x00020000);
+  // buffer loads, sc0 sc1 (system-coherent: the stage is VRAM the host
+  // wrote through the BAR, or pinned memory): a device source (exact) at any
+  // byte address (a global dwordx4 load returns the aligned-down bytes), the
+  // stage in whole 16 B
+  const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t *>(p), 0, static_cast<int>(exact ? len : 16u * nvec), 0x00020000);
 #pragma unroll
   for (uint32_t k = 0; k < 4; k++) {
     const uint32_t q = k * 1024u + tid;
-    zv[k] = q < nlev * 256u ? gload16(pow2 + 4u * q) : u32x4{0u, 0u, 0u, 0u};
     dv[k] = u32x4{0u, 0u, 0u, 0u};
     if (q < nvec) {
       if (exact && 16u * q + 16u > len) {  // device source: never read past len
@@ -1140,15 +1163,16 @@ __global__ __launch_bounds__(1024) void small_chunks_kernel(const uint8_t *__res
         for (uint32_t b = 16u * q; b < len; b++) wds[(b >> 2) & 3u] |= uint32_t(gload8(p + b)) << (8u * (b & 3u));
         dv[k] = u32x4{wds[0], wds[1], wds[2], wds[3]};
       } else {
-        dv[k] = exact ? __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rp, 16u * q, 0, 0))
-                      : gload16(p + 16ull * q);
+        dv[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rp, 16u * q, 0, 17));
       }
     }
   }
   if (MODE == kModeVerify) {
+    const __amdgpu_buffer_rsrc_t re = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(expect), 0,
+                                                                        static_cast<int>(4u * nch), 0x00020000);
 #pragma unroll
     for (uint32_t k = 0; k < 2; k++)
-      if (k * 1024u + tid < nch) ev[k] = gload32(expect + k * 1024u + tid);
+      if (k * 1024u + tid < nch) ev[k] = __builtin_amdgcn_raw_buffer_load_b32(re, 4u * (k * 1024u + tid), 0, 17);
   }
   tt[tid] = tv;
   for (uint32_t j = tid; j < nch; j += 1024u) acc[j] = 0u;
@@ -1156,7 +1180,6 @@ __global__ __launch_bounds__(1024) void small_chunks_kernel(const uint8_t *__res
 #pragma unroll
   for (uint32_t k = 0; k < 4; k++) {
     const uint32_t q = k * 1024u + tid;
-    if (q < nlev * 256u) *reinterpret_cast<u32x4 *>(&zt[4u * q]) = zv[k];
     if (q < nvec) {
       const uint32_t w = 4u * q + (q >> 2);
       dat[w] = dv[k].x;
@@ -1167,31 +1190,42 @@ __global__ __launch_bounds__(1024) void small_chunks_kernel(const uint8_t *__res
   }
   __syncthreads();
   const uint64_t ts1 = __builtin_amdgcn_s_memrealtime();
-  for (uint32_t t = tid; t < nch * ppc; t += 1024u) {
+  // aligned groups of g pieces lie in one chunk (g = lowest set bit of the
+  // pieces per chunk, 64 for a single chunk): XOR-reduced across lanes
+  // before one LDS atomic per group
+  const uint32_t g = nch == 1u ? 64u : min(64u, ppc & (0u - ppc));
+  for (uint32_t t0 = 0; t0 < nch * ppc; t0 += 1024u) {  // uniform
+    const uint32_t t = t0 + tid;
     const uint32_t j = t / ppc, k = t - j * ppc;
     const uint32_t cend = min((j + 1u) * cs, len);
     const uint32_t b0 = j * cs + psz * k;
-    if (b0 >= cend) continue;  // last chunk is short
-    const uint32_t e = min(b0 + psz, cend);
-    uint32_t c = k == 0 ? reg0 : 0u;
-    uint32_t b = b0;
-    for (; b + 4u <= e; b += 4u) {
-      const uint32_t w = b >> 2;
-      const uint32_t x = c ^ dat[w + (w >> 4)];
-      c = tt[768u + (x & 0xffu)] ^ tt[512u + ((x >> 8) & 0xffu)] ^ tt[256u + ((x >> 16) & 0xffu)] ^ tt[x >> 24];
-    }
-    for (; b < e; b++) {
-      const uint32_t w = b >> 2;
-      const uint32_t byte = (dat[w + (w >> 4)] >> (8u * (b & 3u))) & 0xffu;
-      c = tt[(c ^ byte) & 0xffu] ^ (c >> 8);
-    }
-    for (uint32_t d = cend - e, lvl = 0; d; lvl++, d >>= 1) {
-      if (d & 1u) {
-        const uint32_t *z = zt + lvl * 1024u;
-        c = z[c & 0xffu] ^ z[256u + ((c >> 8) & 0xffu)] ^ z[512u + ((c >> 16) & 0xffu)] ^ z[768u + (c >> 24)];
+    uint32_t c = 0u;
+    if (t < nch * ppc && b0 < cend) {  // (the last chunk may be short)
+      const uint32_t e = min(b0 + psz, cend);
+      c = k == 0 ? reg0 : 0u;
+      uint32_t b = b0;
+      for (; b + 4u <= e; b += 4u) {
+        const uint32_t w = b >> 2;
+        const uint32_t x = c ^ dat[w + (w >> 4)];
+        c = tt[768u + (x & 0xffu)] ^ tt[512u + ((x >> 8) & 0xffu)] ^ tt[256u + ((x >> 16) & 0xffu)] ^ tt[x >> 24];
+      }
+      for (; b < e; b++) {
+        const uint32_t w = b >> 2;
+        const uint32_t byte = (dat[w + (w >> 4)] >> (8u * (b & 3u))) & 0xffu;
+        c = tt[(c ^ byte) & 0xffu] ^ (c >> 8);
+      }
+      const uint32_t dd = cend - e;
+      if (dd) {
+        const bool first = t0 == 0u;  // multipliers prefetched in the prologue
+        const uint32_t km = first ? km0 : kx[dd >> 6], kr = first ? kr0 : kx[1024u + (dd & 63u)];
+        if (dd & 63u) c = gf2_mulmod(kr, c, poly);
+        if (dd >> 6) c = gf2_mulmod(km, c, poly);
       }
     }
-    atomicXor(&acc[j], c);
+#pragma unroll
+    for (uint32_t sh = 1; sh < 64u; sh <<= 1)
+      if (sh < g) c ^= __shfl_xor(c, sh);
+    if ((tid & (g - 1u)) == 0u && c) atomicXor(&acc[j], c);
   }
   __syncthreads();
   const uint64_t ts2 = __builtin_amdgcn_s_memrealtime();
@@ -1231,48 +1265,65 @@ __global__ __launch_bounds__(1024) void small_chunks_kernel(const uint8_t *__res
 }
 
 // Resident "mailbox" variant of small_chunks_kernel (opt-in,
-// hdfs_crc32c_mailbox_create): ONE workgroup stays on one CU with both
-// table sets in LDS and serves the synchronous small calls (_hdfs_crc32c and
-// aliases, verify_crcdata, compose_crcs on <= 64 KiB of host memory,
-// src/datanode.c:2470-2476 is the per-packet call pattern) without a kernel
-// launch per call.  The host writes the caller's bytes to the pinned input
-// stage and then a 16-B request {seq, len, cs | flags, reg0}; wave 0 polls
-// that line over PCIe (system-coherent loads), the block reads the data with
-// coalesced system-coherent 1 KiB loads, and lane L of wave w ends up with
-// bytes [4096 w + 64 L, +64) (the tiled kernel's load order + permlane
-// transpose).  Results go to the same pinned output block as
-// small_chunks_kernel, its completion sequence number last.  Requests must
-// have chunk_size % 64 == 0 or a single chunk (else the host launches
-// small_chunks_kernel).  Exit: a quit request, or idle_ticks (100 MHz
-// s_memrealtime) without a request -- every wave leaves through the same
-// barrier-synchronised test; status[0] = (epoch << 1) | alive.
+// hdfs_crc32c_mailbox_create): ONE workgroup stays on one CU and serves the
+// synchronous small calls (_hdfs_crc32c and aliases, verify_crcdata,
+// compose_crcs on <= 64 KiB, src/datanode.c:2470-2476 is the per-packet call
+// pattern) without a kernel launch per call.  The host writes the caller's
+// bytes to the input stage and then a 16-B request {seq, len, cs | flags,
+// reg0}; the stage is fine-grained VRAM the host writes through the BAR
+// (large-BAR devices) or pinned host memory.  Wave 0 polls the request line
+// (system-coherent loads), the block reads the data with coalesced
+// system-coherent 1 KiB loads, and lane L of wave w ends up with bytes
+// [4096 w + 64 L, +64) (the tiled kernel's load order + permlane transpose).
+// Each lane runs 16 conflict-free slicing steps on the 32x replicated tables
+// and moves its state to the end of its chunk with ONE GF(2) multiply by
+// x^(8 dd) mod P (VALU, no table levels).  Results go to the same pinned
+// output block as small_chunks_kernel, its completion sequence number last.
+// Requests must have chunk_size % 64 == 0 or a single chunk (else the host
+// launches small_chunks_kernel).  Exit: a quit request, or idle_ticks
+// (100 MHz s_memrealtime) without a request -- every wave leaves through the
+// same barrier-synchronised test; status[0] = (epoch << 1) | alive.
 
 DEV u32x4 sysload16(const __amdgpu_buffer_rsrc_t r, uint32_t off) {
   // sc0 sc1: system-coherent, never served from a stale cache line
   return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 17));
 }
 
+// Replicated slicing-by-4 image of one table set (the tiled kernel's layout:
+// word P*16384 + e*64 + h*32 + l = t_{3-(2P+h)}[e] for every lane slot l),
+// filled by all 1024 threads with 16-B stores.
+DEV void fill_slices(uint32_t *lt, const uint32_t *__restrict__ gtab, uint32_t tid) {
+  constexpr uint32_t kPer = kLdsSliceBytes / 16 / 1024;
+  uint32_t v[kPer];
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; k++) {
+    const uint32_t idx = 4u * (k * 1024u + tid);
+    const uint32_t P = idx >> 14, e = (idx >> 6) & 255u, h = (idx >> 5) & 1u;
+    v[k] = gtab[(3u - (2u * P + h)) * 256u + e];
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; k++)
+    *reinterpret_cast<u32x4 *>(&lt[4u * (k * 1024u + tid)]) = u32x4{v[k], v[k], v[k], v[k]};
+}
+
 __global__ __launch_bounds__(1024) void mailbox_kernel(const uint32_t *__restrict__ req, const uint8_t *__restrict__ in,
                                                        uint32_t *__restrict__ meta, uint32_t *__restrict__ crcs,
                                                        const uint32_t *__restrict__ tab0, const uint32_t *__restrict__ tab1,
-                                                       const uint32_t *__restrict__ pow0, const uint32_t *__restrict__ pow1,
-                                                       uint32_t *__restrict__ status, uint32_t epoch, uint32_t seq0,
-                                                       uint32_t idle_ticks) {
-  __shared__ uint32_t tt[2][1024];                                    // t0..t3 per checksum type
-  __shared__ __attribute__((aligned(16))) uint32_t zt[2][16 * 1024];  // Z_{2^b}, b < 16, per type
+                                                       const uint32_t *__restrict__ kxg, uint32_t *__restrict__ status,
+                                                       uint32_t epoch, uint32_t seq0, uint32_t idle_ticks) {
+  // slicing tables of the current checksum type, replicated 32x (lane l reads
+  // bank l, as in the tiled kernel); a request of the other type refills them
+  __shared__ __attribute__((aligned(16))) uint32_t lt[kLdsSliceBytes / 4];
+  __shared__ uint32_t kx[2 * kTabKxWords];
   __shared__ uint32_t acc[kSmallMaxChunks];
   __shared__ uint32_t res[2];
   __shared__ uint32_t ctl[6];
+  __shared__ uint32_t tailacc;
   const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
-  // tables once for the kernel's lifetime
-  tt[0][tid] = tab0[tid];
-  tt[1][tid] = tab1[tid];
-#pragma unroll
-  for (uint32_t k = 0; k < 4; k++) {
-    const uint32_t q = k * 1024u + tid;
-    *reinterpret_cast<u32x4 *>(&zt[0][4u * q]) = gload16(pow0 + 4u * q);
-    *reinterpret_cast<u32x4 *>(&zt[1][4u * q]) = gload16(pow1 + 4u * q);
-  }
+  const uint32_t lb0 = (lane & 31u) * 4u, lb1 = 65536u + (lane & 31u) * 4u;
+  fill_slices(lt, tab0, tid);
+  for (uint32_t k = tid; k < 2u * kTabKxWords; k += 1024u) kx[k] = kxg[k];
+  uint32_t cur = 0u;
   const __amdgpu_buffer_rsrc_t rin =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(in), 0, static_cast<int>(kSmallMax + 4u * kSmallMaxChunks),
                                         0x00020000);
@@ -1306,7 +1357,11 @@ __global__ __launch_bounds__(1024) void mailbox_kernel(const uint32_t *__restric
       }
       res[0] = 0xFFFFFFFFu;
       res[1] = 0u;
+      tailacc = 0u;
     }
+#ifdef HDFS_CRC32C_DIAG
+    const uint64_t ts0 = __builtin_amdgcn_s_memrealtime();  // request seen
+#endif
     __syncthreads();
     const uint32_t seq = ctl[0], len = ctl[1], csf = ctl[2], reg0 = ctl[3];
     const bool dev = (csf & kMbDevFlag) != 0u;
@@ -1314,8 +1369,12 @@ __global__ __launch_bounds__(1024) void mailbox_kernel(const uint32_t *__restric
     const uint32_t cs = csf & 0x1FFFFu, ct = (csf & kMbCrc32Flag) ? 1u : 0u;
     const bool verify = (csf & kMbVerifyFlag) != 0u, be = (csf & kMbBeFlag) != 0u;
     const uint32_t nch = (len + cs - 1u) / cs;
+    if (ct != cur) {  // uniform
+      fill_slices(lt, ct ? tab1 : tab0, tid);
+      cur = ct;
+    }
     for (uint32_t j = tid; j < nch; j += 1024u) acc[j] = 0u;
-    // every load before any compute: one PCIe round trip
+    // every load before any compute: one round trip
     uint32_t d[16] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
     const uint32_t base = 4096u * w;
     // device source: exactly len bytes in range (a 16-B load that crosses
@@ -1349,38 +1408,72 @@ __global__ __launch_bounds__(1024) void mailbox_kernel(const uint32_t *__restric
         if (k * 1024u + tid < nch)
           ev[k] = __builtin_amdgcn_raw_buffer_load_b32(rin, kSmallMax + 4u * (k * 1024u + tid), 0, 17);
     }
-    __syncthreads();  // acc cleared
-    if (base < len) {
+    __syncthreads();  // acc cleared, tables of this type in place
+#ifdef HDFS_CRC32C_DIAG
+    // wave 0's loads landed (the barrier above does not wait for them)
+    if (w == 0) __builtin_amdgcn_s_waitcnt(0);
+    const uint64_t ts1 = __builtin_amdgcn_s_memrealtime();
+#endif
+    if (base < len) {  // uniform per wave
       transpose(d);
       const uint32_t b0 = 64u * (64u * w + lane);  // this lane's piece
+      const uint32_t j = b0 / cs;
+      uint32_t c = 0u, ctl_ = 0u;  // contribution to acc[j] / to tailacc
       if (b0 < len) {
-        const uint32_t j = b0 / cs, ce = min((j + 1u) * cs, len), n = min(64u, ce - b0);
-        const uint32_t *t = tt[ct];
-        uint32_t c = (b0 == j * cs) ? reg0 : 0u;
+        const uint32_t ce = min((j + 1u) * cs, len), n = min(64u, ce - b0);
+        c = (b0 == j * cs) ? reg0 : 0u;
+        if (n == 64u) {
+          uint32_t x = c ^ d[0];
 #pragma unroll
-        for (uint32_t q = 0; q < 16; q++) {
-          if (4u * q + 4u <= n) {
-            const uint32_t x = c ^ d[q];
-            c = t[768u + (x & 0xffu)] ^ t[512u + ((x >> 8) & 0xffu)] ^ t[256u + ((x >> 16) & 0xffu)] ^ t[x >> 24];
+          for (uint32_t q = 0; q < 15; q++) x = slice4(lt, x, d[q + 1], lb0, lb1);
+          c = slice4(lt, x, 0u, lb0, lb1);
+        } else {  // the last piece of a chunk
+#pragma unroll
+          for (uint32_t q = 0; q < 16; q++)
+            if (4u * q + 4u <= n) c = slice4(lt, c ^ d[q], 0u, lb0, lb1);
+          if (n & 3u) {
+            uint32_t tw = 0u;
+#pragma unroll
+            for (uint32_t q = 0; q < 16; q++) tw = (q == (n >> 2)) ? d[q] : tw;
+            for (uint32_t b = 0; b < (n & 3u); b++)  // byte table t0: pair 1, half 1
+              c = lds_at(lt, lb1 + 128u + (((c ^ (tw >> (8u * b))) & 0xffu) << 8)) ^ (c >> 8);
           }
         }
-        if (n & 3u) {
-          uint32_t tw = 0u;
+        // Bytes of the chunk after this piece: dd = 64 m + r.  r = ce mod 64
+        // is the same for every full piece of a chunk and non-zero only in
+        // the final chunk of a length that is not a multiple of 64: those
+        // pieces gather in tailacc, shifted by x^(8r) once below.
+        const uint32_t dd = ce - b0 - n, m = dd >> 6;
+        if (m) c = gf2_mulmod(kx[ct * kTabKxWords + m], c, ct ? 0xedb88320u : 0x82f63b78u);
+        if (dd & 63u) {
+          ctl_ = c;
+          c = 0u;
+        }
+      }
+      // XOR the lanes of one chunk together before the LDS atomic: groups
+      // of g aligned lanes lie in one chunk (g = the lanes per chunk's lowest
+      // set bit, 64 for a single chunk), so a 64 KiB single chunk costs 16
+      // atomics, not 1024 on one word
+      const uint32_t lpc = cs >> 6, g = nch == 1u ? 64u : min(64u, lpc & (0u - lpc));
+      const bool tail = (len & 63u) != 0u;  // uniform
 #pragma unroll
-          for (uint32_t q = 0; q < 16; q++) tw = (q == (n >> 2)) ? d[q] : tw;
-          for (uint32_t b = 0; b < (n & 3u); b++) c = t[(c ^ (tw >> (8u * b))) & 0xffu] ^ (c >> 8);
+      for (uint32_t sh = 1; sh < 64u; sh <<= 1) {
+        if (sh < g) {
+          c ^= __shfl_xor(c, sh);
+          if (tail) ctl_ ^= __shfl_xor(ctl_, sh);
         }
-        const uint32_t *z0 = zt[ct];
-        for (uint32_t dd = ce - b0 - n, lvl = 0; dd; lvl++, dd >>= 1) {
-          if (dd & 1u) {
-            const uint32_t *z = z0 + lvl * 1024u;
-            c = z[c & 0xffu] ^ z[256u + ((c >> 8) & 0xffu)] ^ z[512u + ((c >> 16) & 0xffu)] ^ z[768u + (c >> 24)];
-          }
-        }
-        atomicXor(&acc[j], c);
+      }
+      if ((lane & (g - 1u)) == 0u && b0 < len) {
+        if (c) atomicXor(&acc[j], c);
+        if (ctl_) atomicXor(&tailacc, ctl_);
       }
     }
     __syncthreads();
+    if (len & 63u) {  // uniform
+      if (tid == 0 && tailacc)
+        acc[nch - 1u] ^= gf2_mulmod(kx[ct * kTabKxWords + 1024u + (len & 63u)], tailacc, ct ? 0xedb88320u : 0x82f63b78u);
+      __syncthreads();
+    }
     if (verify) {
 #pragma unroll
       for (uint32_t k = 0; k < 2; k++) {
@@ -1406,6 +1499,13 @@ __global__ __launch_bounds__(1024) void mailbox_kernel(const uint32_t *__restric
       }
       if (lane == 0) {
         const uint32_t v0 = ~acc[0];
+#ifdef HDFS_CRC32C_DIAG
+        // diagnostic phase stamps (10 ns ticks): request seen, wave 0's data
+        // loaded, results ready; posted ahead of the completion store
+        const uint64_t ts2 = __builtin_amdgcn_s_memrealtime();
+        *(volatile GAS u32x4 *)(GAS uint8_t *)(meta + 4) =
+            u32x4{uint32_t(ts0), uint32_t(ts1), uint32_t(ts2), uint32_t(ts2 - ts0)};
+#endif
         *(volatile GAS u32x4 *)(GAS uint8_t *)meta = u32x4{res[0], res[1], seq, be ? __builtin_bswap32(v0) : v0};
       }
     }
@@ -1420,10 +1520,10 @@ __global__ __launch_bounds__(1024) void mailbox_kernel(const uint32_t *__restric
 }
 
 hipError_t launch_mailbox(const uint32_t *req, const uint8_t *in, uint32_t *meta, uint32_t *crcs, const uint32_t *tab0,
-                          const uint32_t *tab1, const uint32_t *pow0, const uint32_t *pow1, uint32_t *status,
-                          uint32_t epoch, uint32_t seq0, uint32_t idle_ticks, hipStream_t stream) {
-  hipLaunchKernelGGL(mailbox_kernel, dim3(1), dim3(1024), 0, stream, req, in, meta, crcs, tab0, tab1, pow0, pow1, status,
-                     epoch, seq0, idle_ticks);
+                          const uint32_t *tab1, const uint32_t *kx, uint32_t *status, uint32_t epoch, uint32_t seq0,
+                          uint32_t idle_ticks, hipStream_t stream) {
+  hipLaunchKernelGGL(mailbox_kernel, dim3(1), dim3(1024), 0, stream, req, in, meta, crcs, tab0, tab1, kx, status, epoch,
+                     seq0, idle_ticks);
   return hipGetLastError();
 }
 
@@ -2458,18 +2558,18 @@ hipError_t launch_composite(const SegDev *segs, uint32_t nseg, const uint64_t *r
 }
 
 hipError_t launch_small_chunks(int mode, const uint8_t *p, uint32_t len, uint32_t exact, uint32_t cs, uint32_t reg0,
-                               uint32_t be, const uint32_t *expect, const uint32_t *tab, const uint32_t *pow2,
-                               uint32_t *meta, uint32_t *crcs, uint32_t seq, hipStream_t stream) {
+                               uint32_t be, const uint32_t *expect, const uint32_t *tab, const uint32_t *kx,
+                               uint32_t poly, uint32_t *meta, uint32_t *crcs, uint32_t seq, hipStream_t stream) {
   const uint32_t nch = cs ? (len + cs - 1) / cs : 0u;
   if (!len || len > kSmallMax || !cs || (cs % 4u && nch > 1) || nch > kSmallMaxChunks ||
       (!exact && (reinterpret_cast<uintptr_t>(p) & 15u)))
     return hipErrorInvalidValue;
   if (mode == kModeVerify)
     hipLaunchKernelGGL(small_chunks_kernel<kModeVerify>, dim3(1), dim3(1024), 0, stream, p, len, exact, cs, reg0, be,
-                       expect, tab, pow2, meta, crcs, seq);
+                       expect, tab, kx, poly, meta, crcs, seq);
   else
     hipLaunchKernelGGL(small_chunks_kernel<kModeCompute>, dim3(1), dim3(1024), 0, stream, p, len, exact, cs, reg0,
-                       be, expect, tab, pow2, meta, crcs, seq);
+                       be, expect, tab, kx, poly, meta, crcs, seq);
   return hipGetLastError();
 }
 

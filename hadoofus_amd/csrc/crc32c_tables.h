@@ -73,6 +73,15 @@ inline Gf2 zeros_op(uint64_t n, uint32_t poly = kPoly) {
   return acc;
 }
 
+// Mailbox multipliers (kTabKxWords per type): x^(8n) mod P is the image of
+// the polynomial 1 (bit 31) under the n-zero-byte operator.
+inline void make_kx(uint32_t *out, uint32_t poly = kPoly) {
+  const Gf2 z64 = zeros_op(64, poly), z1 = zeros_op(1, poly);
+  out[0] = out[1024] = 0x80000000u;
+  for (int m = 1; m < 1024; m++) out[m] = z64.apply(out[m - 1]);
+  for (int r = 1; r < 64; r++) out[1024 + r] = z1.apply(out[1024 + r - 1]);
+}
+
 // Byte tables for an operator: out[m*256 + e] = op(e << 8m).
 inline void zeros_byte_tables(const Gf2 &op, uint32_t *out) {
   for (int m = 0; m < 4; m++)

@@ -13,7 +13,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import hadoofus_amd as h  # noqa: E402
 
-h.load()
+# --diag: the diagnostic build (HDFS_CRC32C_* knobs from the environment,
+# e.g. HDFS_CRC32C_MB_STAGE=0 for the pinned mailbox stage); --quick: skip
+# the plan timings
+DIAG = "--diag" in sys.argv
+QUICK = "--quick" in sys.argv
+h.load(os.path.join(ROOT, "hadoofus_amd", "lib", "libhadoofus_crc32c_diag.so") if DIAG else h.abi.LIB_PATH)
 cs = 512
 total = 256 << 20
 dbuf = h.DeviceBuffer(total)
@@ -44,7 +49,7 @@ def plan_us(segs, iters):
 for name, seg_bytes, n in [("1x64KiB", 65536, 1), ("1x1MiB", 1 << 20, 1), ("1x16MiB", 16 << 20, 1),
                            ("1x64MiB", 64 << 20, 1), ("1x256MiB", 256 << 20, 1),
                            ("1024x64KiB", 65536, 1024), ("4096x16KiB", 16384, 4096),
-                           ("16x16MiB", 16 << 20, 16)]:
+                           ("16x16MiB", 16 << 20, 16)][:1 if QUICK else None]:
     us = plan_us(segs_of(seg_bytes, n), 50 if seg_bytes * n <= (64 << 20) else 10)
     out[f"verify_{name}_us"] = round(us, 2)
     out[f"verify_{name}_GBps"] = round(seg_bytes * n * (1 + 4 / cs) / us / 1e3, 1)
@@ -141,4 +146,5 @@ say("mailbox")
 with h.Mailbox() as mb:
     raw_call_us("mailbox_")
     out["mailbox_calls_launches"] = list(mb.stats())
+out["mailbox_stage_env"] = os.environ.get("HDFS_CRC32C_MB_STAGE", "default")
 print(json.dumps(out))
