@@ -87,6 +87,8 @@ int g_runs = HDFS_KNOB("HDFS_CRC32C_RUNS", 2);
 // Small-call input stage: 1 fine-grained VRAM written through the BAR when
 // the device is large-BAR, else (and 0) pinned host memory.
 int g_stage_vram = HDFS_KNOB("HDFS_CRC32C_MB_STAGE", 1);
+// Mailbox timing experiments (diagnostic build only; see mailbox_kernel).
+int g_mb_exp = HDFS_KNOB("HDFS_CRC32C_MB_EXP", 0);
 // Diagnostic per-wave timestamps (device buffer, 3 x u64 per wave) or null.
 unsigned long long *g_diag = nullptr;
 
@@ -402,7 +404,8 @@ int mb_launch(DevCtx &c, uint32_t seq0) {
   c.mb_epoch++;
   __atomic_store_n(&c.h_mb[16], (c.mb_epoch << 1) | 1u, __ATOMIC_RELEASE);
   HIPCHK(launch_mailbox(c.mb_req_d, c.dv_small_in, c.dv_small_out, c.dv_small_out + kSmallMeta, c.d_tab_main_t[0],
-                        c.d_tab_main_t[1], c.d_tab_kx, c.dv_mb + 16, c.mb_epoch, seq0, c.mb_idle_ticks, c.mb_stream));
+                        c.d_tab_main_t[1], c.d_tab_kx, c.dv_mb + 16, c.mb_epoch, seq0, c.mb_idle_ticks,
+                        uint32_t(g_mb_exp), c.mb_stream));
   c.mb_alive = true;
   c.mb_launches++;
   return HDFS_CRC32C_OK;

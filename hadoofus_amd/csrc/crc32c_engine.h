@@ -41,7 +41,7 @@ hipError_t launch_prep(uint32_t *fb, uint32_t nfb, unsigned long long *mism, uin
 // idle_ticks of 10 ns without one; status[0] = (epoch << 1) | alive).
 hipError_t launch_mailbox(const uint32_t *req, const uint8_t *in, uint32_t *meta, uint32_t *crcs, const uint32_t *tab0,
                           const uint32_t *tab1, const uint32_t *kx, uint32_t *status, uint32_t epoch, uint32_t seq0,
-                          uint32_t idle_ticks, hipStream_t stream);
+                          uint32_t idle_ticks, uint32_t exp, hipStream_t stream);
 hipError_t launch_gather(const uint8_t *raw, const PktDesc *descs, uint32_t npk, uint32_t units, uint8_t *arena,
                          uint8_t *crc_arena, hipStream_t stream);
 // proto 1 / 2: derive the stride from the packet at base (v1 / v2 header)

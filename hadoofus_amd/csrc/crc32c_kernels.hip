@@ -1306,15 +1306,28 @@ DEV void fill_slices(uint32_t *lt, const uint32_t *__restrict__ gtab, uint32_t t
     *reinterpret_cast<u32x4 *>(&lt[4u * (k * 1024u + tid)]) = u32x4{v[k], v[k], v[k], v[k]};
 }
 
+// Z_64, Z_128, Z_256 byte tables (the main blob's Z_{64k}, k = 1, 2, 4) for
+// the mailbox's in-wave combine tree.
+DEV void fill_ztree(uint32_t *zt, const uint32_t *__restrict__ gtab, uint32_t tid) {
+#pragma unroll
+  for (uint32_t s = 0; s < 3; s++) zt[s * 1024u + tid] = gtab[kTabSliceWords + ((1u << s) - 1u) * 1024u + tid];
+}
+
 __global__ __launch_bounds__(1024) void mailbox_kernel(const uint32_t *__restrict__ req, const uint8_t *__restrict__ in,
                                                        uint32_t *__restrict__ meta, uint32_t *__restrict__ crcs,
                                                        const uint32_t *__restrict__ tab0, const uint32_t *__restrict__ tab1,
                                                        const uint32_t *__restrict__ kxg, uint32_t *__restrict__ status,
-                                                       uint32_t epoch, uint32_t seq0, uint32_t idle_ticks) {
+                                                       uint32_t epoch, uint32_t seq0, uint32_t idle_ticks,
+                                                       uint32_t exp) {
+  // exp (diagnostic build, timing experiments only -- wrong results): bit 0
+  // skips the GF(2) multiplies, bit 1 the slicing steps, bit 2 the lane XOR
+  if (!kDiag) exp = 0u;
   // slicing tables of the current checksum type, replicated 32x (lane l reads
   // bank l, as in the tiled kernel); a request of the other type refills them
   __shared__ __attribute__((aligned(16))) uint32_t lt[kLdsSliceBytes / 4];
   __shared__ uint32_t kx[2 * kTabKxWords];
+  __shared__ uint32_t zt[3 * 1024];                 // Z_64, Z_128, Z_256 of the current type
+  __shared__ uint32_t slot[2 * (kSmallMax / 512)];  // tree mode: 512-B group partials {crc, j | m << 16}
   __shared__ uint32_t acc[kSmallMaxChunks];
   __shared__ uint32_t res[2];
   __shared__ uint32_t ctl[6];
@@ -1322,6 +1335,7 @@ __global__ __launch_bounds__(1024) void mailbox_kernel(const uint32_t *__restric
   const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
   const uint32_t lb0 = (lane & 31u) * 4u, lb1 = 65536u + (lane & 31u) * 4u;
   fill_slices(lt, tab0, tid);
+  fill_ztree(zt, tab0, tid);
   for (uint32_t k = tid; k < 2u * kTabKxWords; k += 1024u) kx[k] = kxg[k];
   uint32_t cur = 0u;
   const __amdgpu_buffer_rsrc_t rin =
@@ -1371,6 +1385,7 @@ __global__ __launch_bounds__(1024) void mailbox_kernel(const uint32_t *__restric
     const uint32_t nch = (len + cs - 1u) / cs;
     if (ct != cur) {  // uniform
       fill_slices(lt, ct ? tab1 : tab0, tid);
+      fill_ztree(zt, ct ? tab1 : tab0, tid);
       cur = ct;
     }
     for (uint32_t j = tid; j < nch; j += 1024u) acc[j] = 0u;
@@ -1414,6 +1429,16 @@ __global__ __launch_bounds__(1024) void mailbox_kernel(const uint32_t *__restric
     if (w == 0) __builtin_amdgcn_s_waitcnt(0);
     const uint64_t ts1 = __builtin_amdgcn_s_memrealtime();
 #endif
+    // Tree mode (uniform): len a multiple of 512 and 8 | lanes per chunk, so
+    // every aligned 8-lane group holds 512 whole bytes of one chunk.  Three
+    // in-wave levels (shuffle + one Z_{64 2^s} table step) leave each group's
+    // CRC at the group end; a group not at its chunk's end is moved there by
+    // one GF(2) multiply in a second phase (at most 128 groups, two waves),
+    // instead of one multiply per lane.  Otherwise every lane multiplies.
+    const uint32_t lpc = cs >> 6, np = len >> 6;
+    const uint32_t poly = ct ? 0xedb88320u : 0x82f63b78u;
+    const bool tree = (len & 511u) == 0u && (nch == 1u || (lpc & 7u) == 0u);
+    const bool tree2 = tree && (nch == 1u ? np > 8u : lpc > 8u);
     if (base < len) {  // uniform per wave
       transpose(d);
       const uint32_t b0 = 64u * (64u * w + lane);  // this lane's piece
@@ -1422,7 +1447,9 @@ __global__ __launch_bounds__(1024) void mailbox_kernel(const uint32_t *__restric
       if (b0 < len) {
         const uint32_t ce = min((j + 1u) * cs, len), n = min(64u, ce - b0);
         c = (b0 == j * cs) ? reg0 : 0u;
-        if (n == 64u) {
+        if (kDiag && (exp & 2u)) {
+          c ^= d[0] ^ d[15];
+        } else if (n == 64u) {
           uint32_t x = c ^ d[0];
 #pragma unroll
           for (uint32_t q = 0; q < 15; q++) x = slice4(lt, x, d[q + 1], lb0, lb1);
@@ -1439,39 +1466,67 @@ __global__ __launch_bounds__(1024) void mailbox_kernel(const uint32_t *__restric
               c = lds_at(lt, lb1 + 128u + (((c ^ (tw >> (8u * b))) & 0xffu) << 8)) ^ (c >> 8);
           }
         }
-        // Bytes of the chunk after this piece: dd = 64 m + r.  r = ce mod 64
-        // is the same for every full piece of a chunk and non-zero only in
-        // the final chunk of a length that is not a multiple of 64: those
-        // pieces gather in tailacc, shifted by x^(8r) once below.
-        const uint32_t dd = ce - b0 - n, m = dd >> 6;
-        if (m) c = gf2_mulmod(kx[ct * kTabKxWords + m], c, ct ? 0xedb88320u : 0x82f63b78u);
-        if (dd & 63u) {
-          ctl_ = c;
-          c = 0u;
+        if (!tree) {
+          // Bytes of the chunk after this piece: dd = 64 m + r.  r = ce mod 64
+          // is the same for every full piece of a chunk and non-zero only in
+          // the final chunk of a length that is not a multiple of 64: those
+          // pieces gather in tailacc, shifted by x^(8r) once below.
+          const uint32_t dd = ce - b0 - n, m = dd >> 6;
+          if (m && !(kDiag && (exp & 1u))) c = gf2_mulmod(kx[ct * kTabKxWords + m], c, poly);
+          if (dd & 63u) {
+            ctl_ = c;
+            c = 0u;
+          }
         }
       }
-      // XOR the lanes of one chunk together before the LDS atomic: groups
-      // of g aligned lanes lie in one chunk (g = the lanes per chunk's lowest
-      // set bit, 64 for a single chunk), so a 64 KiB single chunk costs 16
-      // atomics, not 1024 on one word
-      const uint32_t lpc = cs >> 6, g = nch == 1u ? 64u : min(64u, lpc & (0u - lpc));
-      const bool tail = (len & 63u) != 0u;  // uniform
+      if (tree) {
 #pragma unroll
-      for (uint32_t sh = 1; sh < 64u; sh <<= 1) {
-        if (sh < g) {
-          c ^= __shfl_xor(c, sh);
-          if (tail) ctl_ ^= __shfl_xor(ctl_, sh);
+        for (uint32_t sl = 0; sl < 3; sl++) {  // the left block moves past its right neighbour
+          const uint32_t r = __shfl_xor(c, 1u << sl);
+          const uint32_t z = zshift(zt, sl * 1024u, c) ^ r;
+          c = (lane & (1u << sl)) ? c : z;
         }
-      }
-      if ((lane & (g - 1u)) == 0u && b0 < len) {
-        if (c) atomicXor(&acc[j], c);
-        if (ctl_) atomicXor(&tailacc, ctl_);
+        if ((lane & 7u) == 0u && b0 < len) {
+          if (tree2) {
+            const uint32_t ce = min((j + 1u) * cs, len), gid = b0 >> 9;
+            slot[2u * gid] = c;
+            slot[2u * gid + 1u] = j | (((ce - b0 - 512u) >> 6) << 16);
+          } else if (c) {
+            atomicXor(&acc[j], c);  // the group is its whole chunk
+          }
+        }
+      } else {
+        // XOR the lanes of one chunk together before the LDS atomic: groups
+        // of g aligned lanes lie in one chunk (g = the lanes per chunk's
+        // lowest set bit, 64 for a single chunk)
+        const uint32_t g = (kDiag && (exp & 4u)) ? 1u : nch == 1u ? 64u : min(64u, lpc & (0u - lpc));
+        const bool tail = (len & 63u) != 0u;  // uniform
+#pragma unroll
+        for (uint32_t sh = 1; sh < 64u; sh <<= 1) {
+          if (sh < g) {
+            c ^= __shfl_xor(c, sh);
+            if (tail) ctl_ ^= __shfl_xor(ctl_, sh);
+          }
+        }
+        if ((lane & (g - 1u)) == 0u && b0 < len) {
+          if (c) atomicXor(&acc[j], c);
+          if (ctl_) atomicXor(&tailacc, ctl_);
+        }
       }
     }
     __syncthreads();
+    if (tree2) {  // uniform: group partials to their chunk ends
+      if (tid < (np >> 3)) {
+        uint32_t v = slot[2u * tid];
+        const uint32_t jm = slot[2u * tid + 1u], mg = jm >> 16;
+        if (mg && !(kDiag && (exp & 1u))) v = gf2_mulmod(kx[ct * kTabKxWords + mg], v, poly);
+        if (v) atomicXor(&acc[jm & 0xFFFFu], v);
+      }
+      __syncthreads();
+    }
     if (len & 63u) {  // uniform
       if (tid == 0 && tailacc)
-        acc[nch - 1u] ^= gf2_mulmod(kx[ct * kTabKxWords + 1024u + (len & 63u)], tailacc, ct ? 0xedb88320u : 0x82f63b78u);
+        acc[nch - 1u] ^= gf2_mulmod(kx[ct * kTabKxWords + 1024u + (len & 63u)], tailacc, poly);
       __syncthreads();
     }
     if (verify) {
@@ -1521,9 +1576,9 @@ __global__ __launch_bounds__(1024) void mailbox_kernel(const uint32_t *__restric
 
 hipError_t launch_mailbox(const uint32_t *req, const uint8_t *in, uint32_t *meta, uint32_t *crcs, const uint32_t *tab0,
                           const uint32_t *tab1, const uint32_t *kx, uint32_t *status, uint32_t epoch, uint32_t seq0,
-                          uint32_t idle_ticks, hipStream_t stream) {
+                          uint32_t idle_ticks, uint32_t exp, hipStream_t stream) {
   hipLaunchKernelGGL(mailbox_kernel, dim3(1), dim3(1024), 0, stream, req, in, meta, crcs, tab0, tab1, kx, status, epoch,
-                     seq0, idle_ticks);
+                     seq0, idle_ticks, exp);
   return hipGetLastError();
 }
 

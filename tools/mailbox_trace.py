@@ -1,7 +1,8 @@
 """Mailbox phase trace (GPU box, diagnostic build): host staging and wait
 time per call plus the kernel's phase stamps, printed by the engine to stderr
 under HDFS_CRC32C_SMALL_TRACE=1.  HDFS_CRC32C_MB_STAGE selects the stage
-(0 pinned, 1 VRAM on large-BAR devices)."""
+(0 pinned, 1 VRAM on large-BAR devices); HDFS_CRC32C_MB_EXP the mailbox
+kernel's timing experiments (wrong results by design)."""
 import ctypes
 import os
 import sys
@@ -25,4 +26,5 @@ with h.Mailbox():
             lib._hdfs_crc32c(0, x64k.ctypes.data, n)
     print("-- verify_crcdata 64KiB", file=sys.stderr, flush=True)
     for _ in range(6):
-        assert lib.hdfs_crc32c_verify_crcdata(reg.ctypes.data, 512, len(be), 65536, 2, ctypes.byref(fb)) == 0
+        rc = lib.hdfs_crc32c_verify_crcdata(reg.ctypes.data, 512, len(be), 65536, 2, ctypes.byref(fb))
+        assert rc == 0 or os.environ.get("HDFS_CRC32C_MB_EXP"), rc  # timing experiments give wrong CRCs
