@@ -76,8 +76,10 @@ int g_block = HDFS_KNOB("HDFS_CRC32C_BLOCK", 1024);
 uint32_t g_store_policy = uint32_t(HDFS_KNOB("HDFS_CRC32C_STORE", 0));
 // Schedule 3: log2 tiles per round-robin group (0..6).
 uint32_t g_group_shift = uint32_t(HDFS_KNOB("HDFS_CRC32C_GROUP", 3)) & 15u;
-// Schedule 3: deal groups XCD-major (1) or by plain workgroup id (0).
-uint32_t g_xcd_major = uint32_t(HDFS_KNOB("HDFS_CRC32C_XCD", 1)) & 1u;
+// Schedule 3: deal groups XCD-major (1: each XCD sweeps a contiguous window
+// of G/8 groups per step), by plain workgroup id (0), or XCD-split (2: each
+// XCD sweeps its own contiguous eighth of the launch).
+uint32_t g_xcd_major = uint32_t(HDFS_KNOB("HDFS_CRC32C_XCD", 1)) & 3u;
 // Compute-mode CRC stores: 2 (product) schedule 3 with the LDS group gather
 // (one 256-B store per 8-tile group); diagnostic build only: 1 schedule 4
 // on tables of whole groups, 0 one 32-B store per tile
@@ -1392,7 +1394,7 @@ int hdfs_crc32c_mailbox_destroy(hdfs_crc32c_mailbox *mb) {
 #ifdef HDFS_CRC32C_DIAG
 // ---- diagnostic build only (include/hadoofus_crc32c_diag.h) ----
 int hdfs_crc32c_set_store_policy(int policy) {
-  if (policy < 0 || policy > 13) return fail(HDFS_CRC32C_EINVAL, "store policy 0..13");
+  if (policy < 0 || policy > 14) return fail(HDFS_CRC32C_EINVAL, "store policy 0..14");
   g_store_policy = uint32_t(policy);
   return HDFS_CRC32C_OK;
 }
@@ -1431,7 +1433,7 @@ int hdfs_crc32c_set_group_shift(int shift) {
 }
 
 int hdfs_crc32c_set_xcd_major(int on) {
-  if (on != 0 && on != 1) return fail(HDFS_CRC32C_EINVAL, "xcd_major must be 0 or 1");
+  if (on < 0 || on > 2) return fail(HDFS_CRC32C_EINVAL, "xcd_major must be 0, 1 or 2");
   g_xcd_major = uint32_t(on);
   return HDFS_CRC32C_OK;
 }

@@ -524,6 +524,13 @@ DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, ui
             sval = dat[L.lane];
             soff = L.lane * 4u;
             sbase = sh.crcs + (gs - sh.mtile_start) * kTileChunks;
+            if (kDiag && L.store_policy == 14) {
+              // diagnostic: the group's 256 B land at a scattered group
+              // position of the segment (q -> 37 q mod 2^k): same bytes and
+              // lines, written in no spatial order (the CRCs end up permuted)
+              const uint32_t ng = sh.main_tiles >> 3, q = static_cast<uint32_t>(gs - sh.mtile_start) >> 3;
+              if (ng && (ng & (ng - 1u)) == 0u) sbase = sh.crcs + ((q * 37u) & (ng - 1u)) * 64u;
+            }
             range = 256u;
           }
           if (L.lane == 0)
@@ -782,7 +789,7 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
 
   LaneConst L;
   // tune: [7:0] store policy (diagnostic build), [11:8] ORDER-3 group shift,
-  // [12] ORDER-3 XCD-major dealing (uniform: SGPR)
+  // [13:12] ORDER-3 dealing: 0 plain, 1 XCD-major, 2 XCD-split (uniform: SGPR)
   L.store_policy = kDiag ? rfl(tune & 0xffu) : 0u;
   L.lane = threadIdx.x & 63u;
   L.hsel = (L.lane >> 3) & 1u;                              // load: odd sub-chunk of each 1 KiB
@@ -840,14 +847,28 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
       // groups an XCD works on at one time are 8 apart; dealing by the
       // virtual id (blockIdx % 8) * (G / 8) + blockIdx / 8 gives each XCD
       // (and its L2) a contiguous run of G / 8 groups per sweep step.
-      const uint32_t b = blockIdx.x, G = gridDim.x;
-      w.gfirst = ((tune >> 12) & 1u) && (G % 8u) == 0 ? (b % 8u) * (G / 8u) + b / 8u : b;
-      w.gstride = gridDim.x;
-      // tickets of the static phase: tiles (ORDER 3) or whole groups (ORDER 4)
-      w.nk = ngroups > w.gfirst
-                 ? static_cast<uint32_t>(((ngroups - 1 - w.gfirst) / gridDim.x + 1) << (ORDER == 4 ? 0u : w.gshift))
-                 : 0u;
-      w.p2first = ngroups << w.gshift;
+      // tune bits 13:12 = 2: XCD-split dealing.  XCD x owns the contiguous
+      // eighth [x * ngx, (x + 1) * ngx) of the static groups and deals it over
+      // its G/8 workgroups, so the 8 XCDs sweep 8 separate windows (their
+      // compute-mode CRC writes land in 8 separate regions at any moment);
+      // the < 8 leftover groups go to the pool.
+      const uint32_t b = blockIdx.x, G = gridDim.x, xm = (tune >> 12) & 3u;
+      if (xm == 2u && (G % 8u) == 0 && ngroups >= 8ull * (G / 8u)) {
+        const uint64_t ngx = ngroups / 8u;
+        const uint32_t G8 = G / 8u, l = b / 8u;
+        w.gfirst = (b % 8u) * ngx + l;
+        w.gstride = G8;
+        w.nk = static_cast<uint32_t>(((ngx - 1 - l) / G8 + 1) << (ORDER == 4 ? 0u : w.gshift));
+        w.p2first = (ngx * 8u) << w.gshift;
+      } else {
+        w.gfirst = xm != 0u && (G % 8u) == 0 ? (b % 8u) * (G / 8u) + b / 8u : b;
+        w.gstride = gridDim.x;
+        // tickets of the static phase: tiles (ORDER 3) or whole groups (ORDER 4)
+        w.nk = ngroups > w.gfirst
+                   ? static_cast<uint32_t>(((ngroups - 1 - w.gfirst) / gridDim.x + 1) << (ORDER == 4 ? 0u : w.gshift))
+                   : 0u;
+        w.p2first = ngroups << w.gshift;
+      }
     } else {
       const uint64_t r_static = pool ? total_rounds * kPhase1Num / kPhase1Den : total_rounds;
       const uint64_t b0 = rfl64(r_static * blockIdx.x / gridDim.x);
