@@ -391,11 +391,13 @@ def main():
             alg_t = B * BLOCK * (1 + 4 / cs + 1 / (8 * cs))
             cands = {"load-only twin of crc32c_tiles_kernel<verify>": alg_t / (kt / nt * 1e-3) / 1e9}
             # streaming-read probes (crc32c_probes.hip): nontemporal buffer
-            # loads, grid-interleaved (14) or XCD-major (24), LDS-DMA XCD-major
-            # (26), and software-pipelined like the tiled kernel (30-32: 4 or
-            # 8 KiB rounds, 3-4 deep), over the same 128 GiB; best of 2 x 2
-            for var in (14, 24, 26, 30, 31, 32):
-                for gpc, blk in ((1, 1024), (2, 512)):
+            # loads, grid-interleaved (14) or XCD-major (24), LDS-DMA per-
+            # workgroup slices (17, 18: round 1's best, 7230 GB/s at 4 x 256
+            # threads per CU) or XCD-major (26), and software-pipelined like
+            # the tiled kernel (30-32: 4 or 8 KiB rounds, 3-4 deep), over the
+            # same 128 GiB; best of 2 x 2
+            for var in (14, 17, 18, 24, 26, 30, 31, 32):
+                for gpc, blk in ((1, 1024), (2, 512), (4, 256)):
                     dg.set_probe(var, gpc, blk)
                     g = max(dg.probe_read(data.ptr, B * BLOCK, 2, stream) for _ in range(2))
                     cands[f"read probe {var} ({gpc}x{blk} per CU)"] = g

@@ -506,20 +506,37 @@ DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, ui
         uint32_t *own = L.gslot + s;
         uint32_t *dat = L.gslot + kGatherSlots + s * 64u;
         // the slot's previous group (grp - kGatherSlots) holds only older
-        // tickets, which never wait on newer ones: the wait ends
+        // tickets, which never wait on newer ones: the wait ends.
+        // Ordering: the slot's words and owner live in LDS, so the fences are
+        // LDS-only ("local": s_waitcnt lgkmcnt(0)).  Plain acquire / release
+        // atomics also order global memory, i.e. wait vmcnt(0) -- that drained
+        // the wave's whole round pipeline (2 rounds of loads in flight) once
+        // per tile.
         for (uint32_t spin = 0;; spin++) {
-          const uint32_t o = rfl(__hip_atomic_load(own, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+          const uint32_t o = rfl(__hip_atomic_load(own, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
           if ((o >> 4) == c.grp) break;
-          if (spin > (1u << 24)) __builtin_trap();  // never expected: fail loudly rather than hang
+          // never expected: fail loudly rather than hang.  s_trap as an
+          // ordinary instruction: __builtin_trap() is noreturn, and the
+          // unreachable edge it adds made the CFG structurizer route a path
+          // back to the loop head on which the waitcnt pass saw the next
+          // round's loads as the newest -- s_waitcnt vmcnt(0) at every loop
+          // head, i.e. no loads in flight across the round boundary.
+          if (spin > (1u << 24)) {
+            asm volatile("s_trap 2");
+            break;
+          }
           __builtin_amdgcn_s_sleep(1);
         }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
         if (elig && leader) dat[static_cast<uint32_t>(g & 7u) * kTileChunks + L.qg] = val;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
         uint32_t old = 0;
-        if (L.lane == 0) old = __hip_atomic_fetch_add(own, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (L.lane == 0) old = __hip_atomic_fetch_add(own, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         old = rfl(old);
         const bool fin = (old & 15u) + 1u == expect;
         if (elig) range = 0u;
         if (fin) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
           if (elig) {
             sval = dat[L.lane];
             soff = L.lane * 4u;
@@ -531,10 +548,16 @@ DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, ui
               const uint32_t ng = sh.main_tiles >> 3, q = static_cast<uint32_t>(gs - sh.mtile_start) >> 3;
               if (ng && (ng & (ng - 1u)) == 0u) sbase = sh.crcs + ((q * 37u) & (ng - 1u)) * 64u;
             }
-            range = 256u;
+            // diagnostic: 15 every group store lands in the segment's first
+            // 256 KiB (an L2-resident window: the stores' CU / L2 cost without
+            // the HBM write-back), 2 group stores dropped
+            if (kDiag && L.store_policy == 15)
+              sbase = sh.crcs + ((static_cast<uint32_t>(gs - sh.mtile_start) * kTileChunks) & 65535u);
+            range = (kDiag && L.store_policy == 2) ? 0u : 256u;
           }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
           if (L.lane == 0)
-            __hip_atomic_store(own, (c.grp + kGatherSlots) << 4, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_store(own, (c.grp + kGatherSlots) << 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
       }
       const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(
