@@ -201,7 +201,10 @@ constexpr uint32_t kSlots = 8;  // LDS slots for published units
 // slots (the 4 KiB the tables leave free) and the wave finishing the group
 // writes them as one 256-B store.  Slot s serves groups s, s + kGatherSlots,
 // ... in order; its owner word holds (group << 4) | tiles counted.
-constexpr uint32_t kGatherSlots = 15, kGatherWords = kGatherSlots * 65;
+#ifndef HDFS_GATHER_SLOTS  // fewer only in A/B builds (tools/build_variant.sh -DHDFS_GATHER_SLOTS=n)
+#define HDFS_GATHER_SLOTS 15
+#endif
+constexpr uint32_t kGatherSlots = HDFS_GATHER_SLOTS, kGatherWords = kGatherSlots * 65;
 constexpr uint64_t kPhase1Num = 23, kPhase1Den = 25;  // 92 % static
 
 struct Sched {
