@@ -268,7 +268,8 @@ int launch_verify_dyn(DevCtx &c, const SegDev *d_segs, const GridSummary *dyn, u
   // back to searching the table when it is not
   const hipError_t le = launch_tiles(kModeVerify, 3, g_nt_loads, 3, 1, 1024, grid, d_segs, 0, 0, 0,
                                      c.d_tab_main_t[ctype], d_fb, d_mism, nullptr,
-                                     (g_group_shift << 8) | (g_xcd_major << 12), d_gctr, st, copy ? 1 : 0, 1, dyn);
+                                     (kDiag ? g_store_policy : 0u) | (g_group_shift << 8) | (g_xcd_major << 12), d_gctr,
+                                     st, copy ? 1 : 0, 1, dyn);
   if (le == hipErrorInvalidValue) return fail(HDFS_CRC32C_EINVAL, "verify kernel shape not built");
   HIPCHK(le);
   HIPCHK(launch_generic(kModeVerify, d_segs, 0, gtiles_ub, c.d_tab_main_t[ctype], d_fb, d_mism, st, dyn));
@@ -1394,7 +1395,7 @@ int hdfs_crc32c_mailbox_destroy(hdfs_crc32c_mailbox *mb) {
 #ifdef HDFS_CRC32C_DIAG
 // ---- diagnostic build only (include/hadoofus_crc32c_diag.h) ----
 int hdfs_crc32c_set_store_policy(int policy) {
-  if (policy < 0 || policy > 15) return fail(HDFS_CRC32C_EINVAL, "store policy 0..15");
+  if (policy < 0 || policy > 18) return fail(HDFS_CRC32C_EINVAL, "store policy 0..18");
   g_store_policy = uint32_t(policy);
   return HDFS_CRC32C_OK;
 }

@@ -16,7 +16,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import hadoofus_amd as h  # noqa: E402
 
-lib = h.load()
+if os.environ.get("DSB_DIAG"):  # the diagnostic build (takes HDFS_CRC32C_* knobs from the environment)
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import diaglib  # noqa: E402
+    lib = h.load(diaglib.DIAG_LIB_PATH)
+else:
+    lib = h.load()
 
 
 def wire_image(nbytes, seed):
@@ -70,6 +75,17 @@ assert rc == 0
 H0 = img.nbytes // npk - 65536
 want = img.reshape(npk, H0 + 65536)[:, H0:].reshape(-1)
 copy_ok = bool(np.array_equal(dst.download(), want))
+if os.environ.get("DSB_POLICIES"):  # diagnostic build: copy-out store policies, interleaved rounds
+    pols = [int(x) for x in os.environ["DSB_POLICIES"].split(",")]
+    res = {p: [] for p in pols}
+    for _ in range(4):
+        for p in pols:
+            assert lib.hdfs_crc32c_set_store_policy(p) == 0
+            t, rc, _ = timed(dev.ptr, img.nbytes, npk, dst=dst)
+            res[p].append(round(payload / t / 2**30, 1))
+            assert bool(np.array_equal(dst.download(), want)), p
+    lib.hdfs_crc32c_set_store_policy(0)
+    out["copy_policy_GiBps"] = {str(p): v for p, v in res.items()}
 t_parse, rc, _ = timed(dev.ptr, img.nbytes, npk, fn="hdfs_crc32c_parse_packets")
 assert rc == 0
 t_hparse, rc, _ = timed(pin.ptr, img.nbytes, npk, fn="hdfs_crc32c_parse_packets")
