@@ -670,11 +670,14 @@ DEV void copy_round(const uint32_t (&d)[16], const Cursor c, SegP segs, const La
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     const u32x4 v = {d[4 * k + 0], d[4 * k + 1], d[4 * k + 2], d[4 * k + 3]};
-    // diagnostic cache policies of the copy-out stores: 16 nt, 17 sc1, 18 nt sc1
+    // product: nt sc1 (streaming; 1 GiB device run, one process: default
+    // 2 083, sc1 2 172, nt 2 220, nt sc1 2 250 GiB/s verify + copy-out,
+    // profiles/r02/s6/exp_copy_store_policy.json); diagnostic build: 16 nt,
+    // 17 sc1, 19 default policy
     if (kDiag && L.store_policy == 16) __builtin_amdgcn_raw_buffer_store_b128(v, rs, (2u * k + L.hsel) * cs + L.loff, 0, 2);
     else if (kDiag && L.store_policy == 17) __builtin_amdgcn_raw_buffer_store_b128(v, rs, (2u * k + L.hsel) * cs + L.loff, 0, 16);
-    else if (kDiag && L.store_policy == 18) __builtin_amdgcn_raw_buffer_store_b128(v, rs, (2u * k + L.hsel) * cs + L.loff, 0, 18);
-    else __builtin_amdgcn_raw_buffer_store_b128(v, rs, (2u * k + L.hsel) * cs + L.loff, 0, 0);
+    else if (kDiag && L.store_policy == 19) __builtin_amdgcn_raw_buffer_store_b128(v, rs, (2u * k + L.hsel) * cs + L.loff, 0, 0);
+    else __builtin_amdgcn_raw_buffer_store_b128(v, rs, (2u * k + L.hsel) * cs + L.loff, 0, 18);
   }
 }
 
