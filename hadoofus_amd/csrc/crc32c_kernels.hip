@@ -455,6 +455,17 @@ struct LaneConst {
   uint32_t store_policy;
 };
 
+// Ordering of the gather's LDS slot protocol.  Default: LDS-only fences
+// (s_waitcnt lgkmcnt(0)).  HDFS_GATHER_ASMBAR (A/B builds): compiler
+// barriers only -- a wave's LDS instructions execute in issue order in the
+// CU's one LDS unit, so the hardware already orders a wave's slot writes
+// before its counter increment, and its data reads before the owner hand-off.
+#ifdef HDFS_GATHER_ASMBAR
+#define GATHER_ORDER(o) asm volatile("" ::: "memory")
+#else
+#define GATHER_ORDER(o) __builtin_amdgcn_fence(o, "workgroup", "local")
+#endif
+
 // Finish one round of one stream after its 16 slicing steps: on a tile's
 // last round, combine the 8 lanes of each chunk and write / compare.  The
 // finalize issues no vector-memory op (LDS and swizzles only).  The result
@@ -530,16 +541,16 @@ DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, ui
           }
           __builtin_amdgcn_s_sleep(1);
         }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+        GATHER_ORDER(__ATOMIC_ACQUIRE);
         if (elig && leader) dat[static_cast<uint32_t>(g & 7u) * kTileChunks + L.qg] = val;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+        GATHER_ORDER(__ATOMIC_RELEASE);
         uint32_t old = 0;
         if (L.lane == 0) old = __hip_atomic_fetch_add(own, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         old = rfl(old);
         const bool fin = (old & 15u) + 1u == expect;
         if (elig) range = 0u;
         if (fin) {
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+          GATHER_ORDER(__ATOMIC_ACQUIRE);
           if (elig) {
             sval = dat[L.lane];
             soff = L.lane * 4u;
@@ -558,7 +569,7 @@ DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, ui
               sbase = sh.crcs + ((static_cast<uint32_t>(gs - sh.mtile_start) * kTileChunks) & 65535u);
             range = (kDiag && L.store_policy == 2) ? 0u : 256u;
           }
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+          GATHER_ORDER(__ATOMIC_RELEASE);
           if (L.lane == 0)
             __hip_atomic_store(own, (c.grp + kGatherSlots) << 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
