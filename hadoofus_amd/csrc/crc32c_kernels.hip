@@ -455,17 +455,6 @@ struct LaneConst {
   uint32_t store_policy;
 };
 
-// Ordering of the gather's LDS slot protocol.  Default: LDS-only fences
-// (s_waitcnt lgkmcnt(0)).  HDFS_GATHER_ASMBAR (A/B builds): compiler
-// barriers only -- a wave's LDS instructions execute in issue order in the
-// CU's one LDS unit, so the hardware already orders a wave's slot writes
-// before its counter increment, and its data reads before the owner hand-off.
-#ifdef HDFS_GATHER_ASMBAR
-#define GATHER_ORDER(o) asm volatile("" ::: "memory")
-#else
-#define GATHER_ORDER(o) __builtin_amdgcn_fence(o, "workgroup", "local")
-#endif
-
 // Finish one round of one stream after its 16 slicing steps: on a tile's
 // last round, combine the 8 lanes of each chunk and write / compare.  The
 // finalize issues no vector-memory op (LDS and swizzles only).  The result
@@ -541,16 +530,16 @@ DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, ui
           }
           __builtin_amdgcn_s_sleep(1);
         }
-        GATHER_ORDER(__ATOMIC_ACQUIRE);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
         if (elig && leader) dat[static_cast<uint32_t>(g & 7u) * kTileChunks + L.qg] = val;
-        GATHER_ORDER(__ATOMIC_RELEASE);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
         uint32_t old = 0;
         if (L.lane == 0) old = __hip_atomic_fetch_add(own, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         old = rfl(old);
         const bool fin = (old & 15u) + 1u == expect;
         if (elig) range = 0u;
         if (fin) {
-          GATHER_ORDER(__ATOMIC_ACQUIRE);
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
           if (elig) {
             sval = dat[L.lane];
             soff = L.lane * 4u;
@@ -569,7 +558,7 @@ DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, ui
               sbase = sh.crcs + ((static_cast<uint32_t>(gs - sh.mtile_start) * kTileChunks) & 65535u);
             range = (kDiag && L.store_policy == 2) ? 0u : 256u;
           }
-          GATHER_ORDER(__ATOMIC_RELEASE);
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
           if (L.lane == 0)
             __hip_atomic_store(own, (c.grp + kGatherSlots) << 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
@@ -577,13 +566,15 @@ DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, ui
       const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(
           reinterpret_cast<uint32_t *>(rfl64(reinterpret_cast<uint64_t>(sbase))), 0, static_cast<int>(rfl(range)),
           0x00020000);
-      // product: sc1; diagnostic build: the store policies' cache bits
-      if (kDiag && L.store_policy == 1) __builtin_amdgcn_raw_buffer_store_b32(sval, rg, soff, 0, 2);        // nt
+      // product: nt (pipelined gather kernel, one process: sc1 6 797, nt 6 835,
+      // nt sc1 6 827, sc0 sc1 6 771 GB/s alg, profiles/r02/s6/exp_gather_store_policy.json);
+      // diagnostic build: the store policies' cache bits
+      if (kDiag && L.store_policy == 5) __builtin_amdgcn_raw_buffer_store_b32(sval, rg, soff, 0, 16);       // sc1
       else if (kDiag && L.store_policy == 6) __builtin_amdgcn_raw_buffer_store_b32(sval, rg, soff, 0, 17);  // sc0 sc1
       else if (kDiag && L.store_policy == 7) __builtin_amdgcn_raw_buffer_store_b32(sval, rg, soff, 0, 18);  // nt sc1
       else if (kDiag && L.store_policy == 8) __builtin_amdgcn_raw_buffer_store_b32(sval, rg, soff, 0, 1);   // sc0
       else if (kDiag && L.store_policy == 11) __builtin_amdgcn_raw_buffer_store_b32(sval, rg, soff, 0, 0);  // default
-      else __builtin_amdgcn_raw_buffer_store_b32(sval, rg, soff, 0, 16);
+      else __builtin_amdgcn_raw_buffer_store_b32(sval, rg, soff, 0, 2);
       return;
     }
     if constexpr (RUN == 1) {
