@@ -246,7 +246,7 @@ template <int ORDER>
 DEV bool ticket_tile(const Sched &w, uint32_t t, uint64_t &g) {
   if (t < w.nk) {
     if (ORDER == 4)
-      g = (w.gfirst + uint64_t(t) * w.gstride) << 3;
+      g = (w.gfirst + uint64_t(t) * w.gstride) << w.gshift;
     else if (ORDER == 3)
       g = ((w.gfirst + uint64_t(t >> w.gshift) * w.gstride) << w.gshift) + (t & ((1u << w.gshift) - 1u));
     else
@@ -254,8 +254,8 @@ DEV bool ticket_tile(const Sched &w, uint32_t t, uint64_t &g) {
     return true;
   }
   if (ORDER < 2) return false;
-  // ORDER 4: a ticket is 8 tiles, a pool unit 2^(ushift - 3) tickets
-  constexpr uint32_t tsh = ORDER == 4 ? 3u : 0u;
+  // ORDER 4: a ticket is 2^gshift tiles, a pool unit 2^(ushift - gshift) tickets
+  const uint32_t tsh = ORDER == 4 ? w.gshift : 0u;
   const uint32_t j = t - w.nk, u = j >> (w.ushift - tsh), o = (j & ((1u << (w.ushift - tsh)) - 1u)) << tsh,
                  s = u % kSlots;
   if (o == 0) {  // first ticket of local unit u: claim a pool unit and publish it
@@ -315,7 +315,7 @@ DEV Cursor advance(Cursor c, SegP segs, uint32_t nseg, const Sched &w, SegCache 
     c.r++;
     return c;
   }
-  if (ORDER == 4 && ((c.tile + 1u) & 7u) != 0u) {  // the run's next tile (main tiles come in whole groups)
+  if (ORDER == 4 && ((c.tile + 1u) & ((1u << w.gshift) - 1u)) != 0u) {  // the run's next tile (whole groups)
     c.tile++;
     c.r = 0;
     return c;
@@ -449,6 +449,7 @@ DEV void issue(uint32_t (&d)[16], uint32_t &exp, uint32_t &tl, uint32_t &sh_a, c
 struct LaneConst {
   uint32_t lane, hsel, loff, lb0, lb1, qi, qg, zk, zbase, z448;
   uint64_t ntiles;   // RUN 2: main tiles of the launch
+  uint32_t rmask;    // RUN 1: tiles per run - 1
   uint32_t *gslot;   // RUN 2: LDS [kGatherSlots] owner words, then [kGatherSlots][64] CRC words
   // 0 default; diagnostic build only: 1 nontemporal, 2 drop result stores,
   // 3 full-line CRC writes (always 0 in the release build)
@@ -579,15 +580,15 @@ DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, ui
     }
     if constexpr (RUN == 1) {
       // ORDER 4: lane 8j + q collects chunk q of the run's tile j from that
-      // chunk's leader lane 8q; the run's last tile writes the 64 CRCs of
-      // its 8 tiles (256 B, whole lines) with one sc1 store
-      const uint32_t j = c.tile & 7u;
+      // chunk's leader lane 8q; the run's last tile writes the CRCs of its
+      // R = rmask + 1 tiles (32 R bytes: whole lines for R >= 4) with one store
+      const uint32_t j = c.tile & L.rmask;
       const uint32_t v =
           static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(static_cast<int>((L.lane & 7u) * 32u), static_cast<int>(val)));
       acc = (last && (L.lane >> 3) == j) ? v : acc;
       const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
-          reinterpret_cast<uint32_t *>(rfl64(reinterpret_cast<uint64_t>(sh.crcs + (c.tile & ~7u) * kTileChunks))), 0,
-          static_cast<int>(rfl(last && j == 7u ? (56u + nch) * 4u : 0u)), 0x00020000);
+          reinterpret_cast<uint32_t *>(rfl64(reinterpret_cast<uint64_t>(sh.crcs + (c.tile & ~L.rmask) * kTileChunks))), 0,
+          static_cast<int>(rfl(last && j == L.rmask ? (8u * L.rmask + nch) * 4u : 0u)), 0x00020000);
       __builtin_amdgcn_raw_buffer_store_b32(acc, rr, L.lane * 4u, 0, 16);
       return;
     }
@@ -838,6 +839,7 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
   L.z448 = kLdsSliceBytes / 4 + 6u * 1024u;
   L.ntiles = total_tiles;
   L.gslot = &lds[kLdsWords + 2 + 2 * kSlots];
+  L.rmask = 7u;
 
   constexpr uint32_t wpb = BLOCK / 64;
   const uint32_t wave = rfl(blockIdx.x * wpb + (threadIdx.x >> 6));
@@ -875,7 +877,10 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
     const bool pool = ORDER >= 2 && total_rounds >= 32ull * nwaves * S;
     if (ORDER >= 3) {
       // static phase: whole groups only; the pool takes the rest
-      w.gshift = ORDER == 4 ? 3u : (tune >> 8) & 15u;
+      // ORDER 4: 2^gshift tiles per run (8 in the diagnostic default; 4 = one
+      // 128-B CRC line per run), at most 8 (one register of CRCs)
+      w.gshift = ORDER == 4 ? min((tune >> 8) & 15u, 3u) : (tune >> 8) & 15u;
+      if (ORDER == 4) L.rmask = (1u << w.gshift) - 1u;
       const uint64_t ngroups = (pool ? total_tiles * kPhase1Num / kPhase1Den : total_tiles) >> w.gshift;
       // tune bit 12: XCD-major dealing.  Workgroups are dispatched to the 8
       // XCDs round-robin (XCD = blockIdx % 8), so with the plain dealing the
