@@ -201,9 +201,10 @@ constexpr uint32_t kSlots = 8;  // LDS slots for published units
 // slots (the 4 KiB the tables leave free) and the wave finishing the group
 // writes them as one 256-B store.  Slot s serves groups s, s + kGatherSlots,
 // ... in order; its owner word holds (group << 4) | tiles counted.
-#ifndef HDFS_GATHER_SLOTS  // fewer only in A/B builds (tools/build_variant.sh -DHDFS_GATHER_SLOTS=n)
-#define HDFS_GATHER_SLOTS 15
+#ifndef HDFS_GATHER_SLOTS  // a power of two; fewer only in A/B builds (-DHDFS_GATHER_SLOTS=n)
+#define HDFS_GATHER_SLOTS 8
 #endif
+static_assert((HDFS_GATHER_SLOTS & (HDFS_GATHER_SLOTS - 1)) == 0, "gather slots: a power of two");
 constexpr uint32_t kGatherSlots = HDFS_GATHER_SLOTS, kGatherWords = kGatherSlots * 65;
 constexpr uint64_t kPhase1Num = 23, kPhase1Den = 25;  // 92 % static
 
@@ -502,11 +503,22 @@ DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, ui
       uint32_t sval = val, soff = leader ? L.qg * 4u : 0x80000000u, range = keep ? nch * 4u : 0u;
       const uint32_t *sbase = sh.crcs + c.tile * kTileChunks;
       if (last) {
-        const uint64_t g = sh.mtile_start + c.tile, gs = g & ~7ull;
-        const uint32_t expect = static_cast<uint32_t>(min<uint64_t>(8u, L.ntiles - gs));
-        const bool elig = expect == 8u && gs >= sh.mtile_start && gs + 8u <= sh.mtile_start + sh.main_tiles &&
-                          (gs + 8u - sh.mtile_start) * kTileChunks <= sh.nchunks;
-        const uint32_t s = c.grp % kGatherSlots;
+        // eligible: the group's 8 tiles are whole tiles of this segment.  A
+        // segment whose main tiles start and end on group boundaries (every
+        // block of a transfer) has only such groups, bar a partial last
+        // tile: decided in 32-bit scalar ops, the 64-bit tile arithmetic only
+        // for the other groups (they count their tiles up to the launch end)
+        const bool whole = ((static_cast<uint32_t>(sh.mtile_start) | sh.main_tiles) & 7u) == 0u;
+        bool elig = whole && (uint64_t(c.tile | 7u) + 1u) * kTileChunks <= sh.nchunks;
+        uint32_t expect = 8u;
+        if (!elig) {
+          const uint64_t gs = (sh.mtile_start + c.tile) & ~7ull;
+          expect = static_cast<uint32_t>(min<uint64_t>(8u, L.ntiles - gs));
+          elig = expect == 8u && gs >= sh.mtile_start && gs + 8u <= sh.mtile_start + sh.main_tiles &&
+                 (gs + 8u - sh.mtile_start) * kTileChunks <= sh.nchunks;
+        }
+        const uint32_t gt = static_cast<uint32_t>(sh.mtile_start) + c.tile;  // low bits of the global tile
+        const uint32_t s = c.grp & (kGatherSlots - 1u);
         uint32_t *own = L.gslot + s;
         uint32_t *dat = L.gslot + kGatherSlots + s * 64u;
         // the slot's previous group (grp - kGatherSlots) holds only older
@@ -532,7 +544,7 @@ DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, ui
           __builtin_amdgcn_s_sleep(1);
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-        if (elig && leader) dat[static_cast<uint32_t>(g & 7u) * kTileChunks + L.qg] = val;
+        if (elig && leader) dat[(gt & 7u) * kTileChunks + L.qg] = val;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
         uint32_t old = 0;
         if (L.lane == 0) old = __hip_atomic_fetch_add(own, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -544,19 +556,20 @@ DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, ui
           if (elig) {
             sval = dat[L.lane];
             soff = L.lane * 4u;
-            sbase = sh.crcs + (gs - sh.mtile_start) * kTileChunks;
+            // eligible: the group starts at segment tile (gt & ~7) - mtile_start
+            sbase = sh.crcs + static_cast<uint64_t>((gt & ~7u) - static_cast<uint32_t>(sh.mtile_start)) * kTileChunks;
             if (kDiag && L.store_policy == 14) {
               // diagnostic: the group's 256 B land at a scattered group
               // position of the segment (q -> 37 q mod 2^k): same bytes and
               // lines, written in no spatial order (the CRCs end up permuted)
-              const uint32_t ng = sh.main_tiles >> 3, q = static_cast<uint32_t>(gs - sh.mtile_start) >> 3;
+              const uint32_t ng = sh.main_tiles >> 3, q = ((gt & ~7u) - static_cast<uint32_t>(sh.mtile_start)) >> 3;
               if (ng && (ng & (ng - 1u)) == 0u) sbase = sh.crcs + ((q * 37u) & (ng - 1u)) * 64u;
             }
             // diagnostic: 15 every group store lands in the segment's first
             // 256 KiB (an L2-resident window: the stores' CU / L2 cost without
             // the HBM write-back), 2 group stores dropped
             if (kDiag && L.store_policy == 15)
-              sbase = sh.crcs + ((static_cast<uint32_t>(gs - sh.mtile_start) * kTileChunks) & 65535u);
+              sbase = sh.crcs + ((((gt & ~7u) - static_cast<uint32_t>(sh.mtile_start)) * kTileChunks) & 65535u);
             range = (kDiag && L.store_policy == 2) ? 0u : 256u;
           }
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
