@@ -502,7 +502,10 @@ DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, ui
       // 32 B but still count in the slot, so it passes on to the next group
       uint32_t sval = val, soff = leader ? L.qg * 4u : 0x80000000u, range = keep ? nch * 4u : 0u;
       const uint32_t *sbase = sh.crcs + c.tile * kTileChunks;
-      if (last) {
+      // diagnostic 20: the gather kernel with its slot protocol skipped and
+      // every CRC store dropped (what the protocol itself costs)
+      if (kDiag && L.store_policy == 20) range = 0u;
+      if (last && !(kDiag && L.store_policy == 20)) {
         // eligible: the group's 8 tiles are whole tiles of this segment.  A
         // segment whose main tiles start and end on group boundaries (every
         // block of a transfer) has only such groups, bar a partial last
