@@ -491,11 +491,12 @@ def test_bound_device_explicit(engine):
     (1024, 8 * 8 * 40, 7, 0),
 ])
 def test_compute_runs_schedule(engine, oracle, cs, seg_chunks, nseg, tail):
-    """Compute plans whose segments hold whole 8-tile groups run schedule 4:
-    one wave per group, the 64 CRCs of a group gathered in one register and
-    written with one store (src/datanode.c:2814-2860 computes the same chunk
-    CRCs one at a time).  CRC arrays equal the oracle's, nothing outside them
-    is written."""
+    """Compute plans over segments of whole 8-tile groups, on the product
+    schedule (the LDS group gather: a group's 64 CRCs collected across the
+    workgroup's waves and written with one store; groups holding a partial
+    last tile store per tile).  src/datanode.c:2814-2860 computes the same
+    chunk CRCs one at a time.  CRC arrays equal the oracle's, nothing outside
+    them is written."""
     seg_len = seg_chunks * cs
     lens = [seg_len] * nseg + ([65536 + 100] if tail else [])
     total = sum(lens)
