@@ -16,7 +16,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import hadoofus_amd as h  # noqa: E402
 
-if os.environ.get("DSB_DIAG"):  # the diagnostic build (takes HDFS_CRC32C_* knobs from the environment)
+if os.environ.get("DSB_LIB"):  # another build of the library (A/B of a change, same box)
+    lib = h.load(os.environ["DSB_LIB"])
+elif os.environ.get("DSB_DIAG"):  # the diagnostic build (takes HDFS_CRC32C_* knobs from the environment)
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import diaglib  # noqa: E402
     lib = h.load(diaglib.DIAG_LIB_PATH)
