@@ -386,7 +386,8 @@ struct LaneOff {
 // flight may belong to different segments).
 template <int MODE, int NT, int BUF, int UNA>
 DEV void issue(uint32_t (&d)[16], uint32_t &exp, uint32_t &tl, uint32_t &sh_a, const Cursor c, SegP segs,
-               uint32_t hsel, uint32_t loff, uint32_t qg, uint32_t lane, LaneOff &lo, SegCache &kc) {
+               uint32_t hsel, uint32_t loff, uint32_t qg, uint32_t lane, LaneOff &lo, SegCache &kc,
+               uint32_t pol = 0u) {
   const SegHot &sh = hot(kc, segs, c.seg).h;
   const uint32_t cs = sh.chunk_size;
   const uint32_t a = UNA ? static_cast<uint32_t>(reinterpret_cast<uintptr_t>(sh.data)) & 3u : 0u;
@@ -420,7 +421,9 @@ DEV void issue(uint32_t (&d)[16], uint32_t &exp, uint32_t &tl, uint32_t &sh_a, c
     if (MODE != kModeCompute) {
       const __amdgpu_buffer_rsrc_t re = __builtin_amdgcn_make_buffer_rsrc(
           sh.crcs + c.tile * kTileChunks, 0, static_cast<int>(nch * 4u), 0x00020000);
-      exp = __builtin_amdgcn_raw_buffer_load_b32(re, qg * 4u, 0, 0);
+      // diagnostic 21 / 23: the expected CRCs loaded nontemporal
+      if (kDiag && (pol == 21u || pol == 23u)) exp = __builtin_amdgcn_raw_buffer_load_b32(re, qg * 4u, 0, 2);
+      else exp = __builtin_amdgcn_raw_buffer_load_b32(re, qg * 4u, 0, 0);
     }
   } else {
     const uint32_t last = min(kTileChunks, segs[c.seg].nchunks - c.tile * kTileChunks) - 1u;
@@ -662,7 +665,11 @@ DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, ui
     const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
         reinterpret_cast<uint8_t *>(rfl64(reinterpret_cast<uint64_t>(sh.bitmap + c.tile))), 0,
         static_cast<int>(rfl((last && !(kDiag && L.store_policy == 2)) ? 1u : 0u)), 0x00020000);
-    __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(byte), rb, L.lane == 0 ? 0u : 0x80000000u, 0, 0);
+    // diagnostic 22 / 23: the bitmap bytes stored nontemporal
+    if (kDiag && (L.store_policy == 22u || L.store_policy == 23u))
+      __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(byte), rb, L.lane == 0 ? 0u : 0x80000000u, 0, 2);
+    else
+      __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(byte), rb, L.lane == 0 ? 0u : 0x80000000u, 0, 0);
     if (byte && L.lane == 0) {  // rare: only tiles with a mismatch
       atomicMin(&first_bad[c.seg], c.tile * kTileChunks + __builtin_ctz(byte));
       atomicAdd(mism, static_cast<unsigned long long>(__builtin_popcount(byte)));
@@ -1008,7 +1015,7 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
       tl[k][s] = 0u;
       sha[k][s] = 0u;
       issue<MODE, NT, BUF, UNA>(buf[k][s], ex[k][s], tl[k][s], sha[k][s], cur[k][s], sg, L.hsel, L.loff, L.qg, L.lane,
-                                lo, kc[s]);
+                                lo, kc[s], L.store_policy);
     }
   }
   for (;;) {
@@ -1024,7 +1031,7 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
       for (int s = 0; s < S; s++) {
         cur[k][s] = advance<ORDER>(cur[prev][s], sg, nseg, w, kc[s]);
         issue<MODE, NT, BUF, UNA>(buf[k][s], ex[k][s], tl[k][s], sha[k][s], cur[k][s], sg, L.hsel, L.loff, L.qg,
-                                  L.lane, lo, kc[s]);
+                                  L.lane, lo, kc[s], L.store_policy);
       }
     }
     bool more = false;
