@@ -1395,7 +1395,7 @@ int hdfs_crc32c_mailbox_destroy(hdfs_crc32c_mailbox *mb) {
 #ifdef HDFS_CRC32C_DIAG
 // ---- diagnostic build only (include/hadoofus_crc32c_diag.h) ----
 int hdfs_crc32c_set_store_policy(int policy) {
-  if (policy < 0 || policy > 23) return fail(HDFS_CRC32C_EINVAL, "store policy 0..23");
+  if (policy < 0 || policy > 25) return fail(HDFS_CRC32C_EINVAL, "store policy 0..25");
   g_store_policy = uint32_t(policy);
   return HDFS_CRC32C_OK;
 }

@@ -668,6 +668,10 @@ DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, ui
     // diagnostic 22 / 23: the bitmap bytes stored nontemporal
     if (kDiag && (L.store_policy == 22u || L.store_policy == 23u))
       __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(byte), rb, L.lane == 0 ? 0u : 0x80000000u, 0, 2);
+    else if (kDiag && L.store_policy == 24u)  // diagnostic: sc1
+      __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(byte), rb, L.lane == 0 ? 0u : 0x80000000u, 0, 16);
+    else if (kDiag && L.store_policy == 25u)  // diagnostic: sc0 sc1
+      __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(byte), rb, L.lane == 0 ? 0u : 0x80000000u, 0, 17);
     else
       __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(byte), rb, L.lane == 0 ? 0u : 0x80000000u, 0, 0);
     if (byte && L.lane == 0) {  // rare: only tiles with a mismatch
