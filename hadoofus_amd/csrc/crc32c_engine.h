@@ -265,7 +265,11 @@ struct HostRegistration {
     if (p) (void)hipHostUnregister(const_cast<void *>(p));
   }
   int ensure(const void *ptr, size_t n) {
-    if (!ptr || !n || is_pinned_host(ptr)) return HDFS_CRC32C_OK;
+    // pinned only if both ends are: a buffer that starts inside a pinned
+    // allocation and runs past it must not be DMA-ed as pinned (the GPU would
+    // fault on the unmapped rest); registering it fails loudly instead
+    if (!ptr || !n || (is_pinned_host(ptr) && is_pinned_host(static_cast<const uint8_t *>(ptr) + n - 1)))
+      return HDFS_CRC32C_OK;
     HIPCHK(hipHostRegister(const_cast<void *>(ptr), n, hipHostRegisterDefault));
     p = ptr;
     return HDFS_CRC32C_OK;
