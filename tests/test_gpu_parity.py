@@ -484,13 +484,15 @@ def test_bound_device_explicit(engine):
     assert dev == 0 and bus.count(":") == 2 and bus.endswith(".0"), bus
 
 
-@pytest.mark.parametrize("cs,seg_chunks,nseg,tail", [
-    (512, 32768, 40, 0),        # 640 MiB: the global pool engaged
-    (512, 8 * 8 * 5 - 3, 64, 1),  # last main tile of each segment holds 5 chunks; one 64 KiB tail segment
-    (4096, 8 * 8 * 3, 20, 0),   # 8 rounds per tile: a run is 64 rounds of one wave
-    (1024, 8 * 8 * 40, 7, 0),
+@pytest.mark.parametrize("cs,seg_chunks,nseg,tail,ctype,be", [
+    (512, 32768, 40, 0, 2, True),         # 640 MiB: the global pool engaged
+    (512, 8 * 8 * 5 - 3, 64, 1, 2, True),  # last main tile of each segment holds 5 chunks; one 64 KiB tail segment
+    (4096, 8 * 8 * 3, 20, 0, 2, True),    # 8 rounds per tile: a run is 64 rounds of one wave
+    (1024, 8 * 8 * 40, 7, 0, 2, True),
+    (512, 8 * 8 * 64, 24, 0, 1, True),    # CRC32 (zlib polynomial) through the gather
+    (512, 8 * 8 * 5 - 3, 40, 1, 2, False),  # little-endian CRC arrays through the gather
 ])
-def test_compute_runs_schedule(engine, oracle, cs, seg_chunks, nseg, tail):
+def test_compute_runs_schedule(engine, oracle, cs, seg_chunks, nseg, tail, ctype, be):
     """Compute plans over segments of whole 8-tile groups, on the product
     schedule (the LDS group gather: a group's 64 CRCs collected across the
     workgroup's waves and written with one store; groups holding a partial
@@ -500,7 +502,8 @@ def test_compute_runs_schedule(engine, oracle, cs, seg_chunks, nseg, tail):
     seg_len = seg_chunks * cs
     lens = [seg_len] * nseg + ([65536 + 100] if tail else [])
     total = sum(lens)
-    host = oracle.splitmix((total + 7) // 8, seed=cs + nseg).view(np.uint8)[:total]
+    host = oracle.splitmix((total + 7) // 8, seed=cs + nseg + 17 * ctype).view(np.uint8)[:total]
+    flags = (engine.SEG_BE if be else 0) | (engine.SEG_CRC32 if ctype == 1 else 0)
     dbuf = engine.DeviceBuffer(total)
     dbuf.upload(host)
     nchs = [(n + cs - 1) // cs for n in lens]
@@ -508,16 +511,16 @@ def test_compute_runs_schedule(engine, oracle, cs, seg_chunks, nseg, tail):
     crcs.fill(0xA5)
     segs, off, coff = [], 0, 0
     for n, c in zip(lens, nchs):
-        segs.append(engine.Segment(data=dbuf.ptr + off, len=n, chunk_size=cs, flags=engine.SEG_BE, crc_init=0,
+        segs.append(engine.Segment(data=dbuf.ptr + off, len=n, chunk_size=cs, flags=flags, crc_init=0,
                                    crcs=crcs.ptr + 4 * coff, bitmap=None))
         off += n
         coff += c
     p = engine.Plan(engine.MODE_COMPUTE, segs)
     p.execute()
-    got = crcs.download(4 * (coff + 64), dtype=">u4").astype(np.uint32)
+    got = crcs.download(4 * (coff + 64), dtype=">u4" if be else "<u4").astype(np.uint32)
     off, coff = 0, 0
     for n, c in zip(lens, nchs):
-        np.testing.assert_array_equal(got[coff:coff + c], oracle.chunk_crcs(host[off:off + n], cs))
+        np.testing.assert_array_equal(got[coff:coff + c], oracle.chunk_crcs(host[off:off + n], cs, ctype=ctype))
         off += n
         coff += c
     assert (got[coff:] == 0xA5A5A5A5).all()
