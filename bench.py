@@ -32,6 +32,7 @@ import argparse
 import json
 import os
 import platform
+import socket
 import sys
 import time
 
@@ -248,7 +249,8 @@ def main():
     h.load()
     h.init(d.local)  # explicit binding: this rank's GPU, whatever torch's current device is
     dev, bus = h.bound_device()
-    infos = d.gather({"rank": d.rank, "local_rank": d.local, "device": dev, "pci_bus_id": bus})
+    infos = d.gather({"rank": d.rank, "local_rank": d.local, "device": dev, "pci_bus_id": bus,
+                      "host": socket.gethostname()})
     ndev = shard.check_distinct_devices(infos)
     arch, ncu = h.device_info()
     cs = args.chunk
@@ -427,6 +429,16 @@ def main():
         k_avg_s = kms / max(1, nlaunch) * 1e-3
         achieved = alg / k_avg_s / 1e9
         traffic, traffic_src = pmc_traffic("verify", nbytes, cs)
+        # an empirical ceiling bounds the kernel only if it is at least the
+        # kernel's own rate; a slower "ceiling" (round 2: the load-only twin
+        # and every read probe below the verify kernel) is reported as a
+        # candidate, never as the peak
+        peak_ok = bool(ceiling) and ceiling >= achieved
+        if ceiling and not peak_ok:
+            extra["measured_peak_note"] = (
+                f"no ceiling candidate measured in this process ({round(ceiling, 1)} GB/s at best, "
+                f"{extra.get('ceiling_source', '')}) reaches the verify kernel's own {round(achieved, 1)} GB/s, "
+                "so no empirical peak is reported; frac is against the 8 TB/s spec only")
         if args.config == "C3":
             workload = ("C3 verify: 1024 x 128MiB HDFS blocks per GPU of splitmix64 data, 512B chunks, BE wire CRCs, "
                         "1/65537 chunks corrupted, bitmap + first-bad out")
@@ -454,8 +466,8 @@ def main():
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                 "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
-                "frac_of_measured_peak": round(achieved / ceiling, 4) if ceiling else None,
-                "measured_peak": round(ceiling, 1) if ceiling else None,
+                "frac_of_measured_peak": round(achieved / ceiling, 4) if peak_ok else None,
+                "measured_peak": round(ceiling, 1) if peak_ok else None,
                 "kernel": "crc32c_tiles_kernel<verify>", "kernel_avg_ms": round(k_avg_s * 1e3, 3),
                 "alg_bytes_per_launch": int(alg),
             },

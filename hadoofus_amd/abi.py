@@ -23,7 +23,10 @@ ERR_INVALID_PACKETHEADERPROTO = 18
 ERR_PACKET_SIZE = 25
 ERR_CRC_LEN = 26
 ERR_UNEXPECTED_CRC_LEN = 27
+ERR_UNEXPECTED_READ_OFFSET = 28
 ERR_BAD_CHECKSUM = 29
+ERR_BAD_LASTPACKET = 32
+READ_ALL = -1  # verify_packets_copy: whole payloads, no client read window
 MODE_COMPUTE, MODE_VERIFY = 0, 1
 PROTO_V1, PROTO_V2 = 1, 2
 SEG_BE, SEG_RAW, SEG_CRC32 = 1, 2, 4
@@ -126,8 +129,8 @@ def bind_product(lib):
         _bind(lib, name, _int, [_vp, _u64, _int, _u32, _int, ctypes.POINTER(Packet), _sz,
                                 ctypes.POINTER(_sz), ctypes.POINTER(_u64)])
     _bind(lib, "hdfs_crc32c_verify_packets_copy", _int,
-          [_vp, _u64, _int, _u32, _int, ctypes.POINTER(Packet), _sz, ctypes.POINTER(_sz), ctypes.POINTER(_u64), _vp,
-           _u64, ctypes.POINTER(_u64)])
+          [_vp, _u64, _int, _u32, _int, ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(Packet), _sz,
+           ctypes.POINTER(_sz), ctypes.POINTER(_u64), _vp, _u64, ctypes.POINTER(_u64)])
     _bind(lib, "hdfs_crc32c_session_create", _int, [ctypes.POINTER(_vp), _int, _u32, _int, _u64, _sz])
     _bind(lib, "hdfs_crc32c_session_buffer", _int, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_u64)])
     _bind(lib, "hdfs_crc32c_session_commit", _int, [_vp, _u64])
@@ -366,16 +369,18 @@ def verify_packets(stream, proto=PROTO_V2, chunk_size=512, ctype=CSUM_CRC32C, ma
 
 
 def verify_packets_copy(dptr, nbytes, dst, dst_cap, proto=PROTO_V2, chunk_size=512, ctype=CSUM_CRC32C,
-                        max_pkts=None):
+                        max_pkts=None, client_offset=0, read_len=READ_ALL):
     """Verify + copy-out of a device-resident stream (dptr, nbytes) into the
-    device buffer dst (dst_cap bytes): the payloads de-framed in stream order.
+    device buffer dst (dst_cap bytes): the payloads de-framed in stream order
+    (read_len READ_ALL), or the block bytes [client_offset, client_offset +
+    read_len) of a client read (src/datanode.c:2478-2549).
     -> (rc, [packet dicts], consumed, delivered)."""
     if max_pkts is None:
         max_pkts = nbytes // (25 if proto == PROTO_V1 else 6) + 1
     arr = (Packet * max(1, max_pkts))()
     npk, used, got = _sz(0), _u64(0), _u64(0)
-    rc = load().hdfs_crc32c_verify_packets_copy(dptr, nbytes, proto, chunk_size, ctype, arr, max_pkts,
-                                                ctypes.byref(npk), ctypes.byref(used), dst, dst_cap,
+    rc = load().hdfs_crc32c_verify_packets_copy(dptr, nbytes, proto, chunk_size, ctype, client_offset, read_len, arr,
+                                                max_pkts, ctypes.byref(npk), ctypes.byref(used), dst, dst_cap,
                                                 ctypes.byref(got))
     if rc < 0:
         _check(rc)

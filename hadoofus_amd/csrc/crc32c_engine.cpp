@@ -18,6 +18,8 @@
 #include <string>
 #include <vector>
 
+#include <unistd.h>
+
 #include "crc32c_engine.h"
 #include "crc32c_tables.h"
 #ifdef HDFS_CRC32C_DIAG
@@ -463,6 +465,9 @@ int mailbox_call(DevCtx &c, int mode, uint32_t len, uint32_t cs, uint32_t reg0, 
   const auto t0 = std::chrono::steady_clock::now();
   for (uint32_t spin = 1;; spin++) {
     if (__atomic_load_n(&c.h_small_out[2], __ATOMIC_ACQUIRE) == seq) {
+      // the completion line is the resident kernel's last memory operation
+      // for a request; a fault while serving it ends the kernel before it
+      // (caught by the stream query below after 200 ms)
       c.mb_calls++;
       if (g_small_trace) {  // diagnostic: host staging / wait, kernel phases (diag build, 10 ns ticks)
         const auto t1 = std::chrono::steady_clock::now();
@@ -520,6 +525,12 @@ int small_call(DevCtx &c, int mode, uint32_t len, uint32_t cs, uint32_t reg0, bo
   const auto t0 = std::chrono::steady_clock::now();
   for (uint32_t spin = 1;; spin++) {
     if (__atomic_load_n(&c.h_small_out[2], __ATOMIC_ACQUIRE) == seq) {
+      // the sequence number is the kernel's last memory operation (a fault of
+      // this launch cannot be followed by it); one query of the stream makes
+      // a fault of EARLIER work on it this call's error, not the next caller's
+      const hipError_t q = hipStreamQuery(c.stream);
+      if (q != hipSuccess && q != hipErrorNotReady)
+        return fail(HDFS_CRC32C_EHIP, "small kernel: %s", hipGetErrorString(q));
       if (g_small_trace) {  // diagnostic: host launch / wait time, kernel phase stamps (10 ns ticks)
         const auto t1 = std::chrono::steady_clock::now();
         const uint32_t *m = c.h_small_out;
@@ -584,13 +595,54 @@ int stream_crc_any(uint32_t crc, const void *buf, uint64_t len, uint32_t *out, i
   return HDFS_CRC32C_OK;
 }
 
-bool is_pinned_host(const void *p) {
-  hipPointerAttribute_t a;
-  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+// HIP side of the pinned-memory registry (crc32c_hostpin.h).
+namespace {
+struct HipPinBackend final : PinBackend {
+  int reg(uintptr_t p, size_t n) override {
+    const hipError_t e = hipHostRegister(reinterpret_cast<void *>(p), n, hipHostRegisterDefault);
+    if (e == hipSuccess) return kOk;
     (void)hipGetLastError();
-    return false;
+    // refused: "already pinned" only if the runtime knows the start as
+    // page-locked host memory (the registry then checks both ends of the
+    // caller's bytes); anything else is a failure
+    return pinned_elsewhere(p) ? kAlready : kFail;
   }
-  return a.type == hipMemoryTypeHost || a.devicePointer != nullptr;
+  int unreg(uintptr_t p) override {
+    const hipError_t e = hipHostUnregister(reinterpret_cast<void *>(p));
+    if (e == hipSuccess) return kOk;
+    (void)hipGetLastError();
+    return kFail;
+  }
+  bool pinned_elsewhere(uintptr_t p) override {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, reinterpret_cast<void *>(p)) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    return a.type == hipMemoryTypeHost;
+  }
+};
+HipPinBackend g_pin_backend;
+}  // namespace
+
+PinRegistry &pins() {
+  static PinRegistry r(&g_pin_backend, size_t(sysconf(_SC_PAGESIZE)));
+  return r;
+}
+
+int HostPins::pin(std::initializer_list<std::pair<const void *, size_t>> bufs) {
+  if (s.acquire(bufs)) return fail(HDFS_CRC32C_EHIP, "%s", pins().last_error());
+  return HDFS_CRC32C_OK;
+}
+
+int HostPins::done(int rc) {
+  for (hipStream_t st : drain) {
+    const hipError_t e = st ? hipStreamSynchronize(st) : hipSuccess;
+    if (e != hipSuccess && !rc) rc = fail(HDFS_CRC32C_EHIP, "stream: %s", hipGetErrorString(e));
+  }
+  finished = true;
+  if (s.release() && !rc) rc = fail(HDFS_CRC32C_EHIP, "%s", pins().last_error());
+  return rc;
 }
 
 
@@ -669,9 +721,10 @@ int host_pipeline(int mode, const uint8_t *data, uint64_t len, uint32_t cs, uint
   std::lock_guard<std::mutex> lk(c.mu);
   rc = pipe_reserve(c, piece, cs, npieces);
   if (rc) return rc;
-  HostRegistration reg_d, reg_c, reg_b;
-  if ((rc = reg_d.ensure(data, len)) || (rc = reg_c.ensure(crcs, nch * 4)) ||
-      (mode == kModeVerify && bitmap && (rc = reg_b.ensure(bitmap, (nch + 7) / 8))))
+  // the caller's buffers stay pinned until both streams are drained, on
+  // every return path (an early return drains in the destructor)
+  HostPins hp({c.copy_stream, c.comp_stream});
+  if ((rc = hp.pin({{data, len}, {crcs, nch * 4}, {mode == kModeVerify ? bitmap : nullptr, (nch + 7) / 8}})))
     return rc;
   // Per-piece descriptors (uploaded once).
   std::vector<SegDev> segs(npieces);
@@ -715,8 +768,7 @@ int host_pipeline(int mode, const uint8_t *data, uint64_t len, uint32_t cs, uint
       HIPCHK(hipMemcpyAsync(bitmap + c0 / 8, c.p_bm[b], (nc + 7) / 8, hipMemcpyDeviceToHost, c.comp_stream));
     HIPCHK(hipEventRecord(c.ev_comp[b], c.comp_stream));
   }
-  HIPCHK(hipStreamSynchronize(c.comp_stream));
-  HIPCHK(hipStreamSynchronize(c.copy_stream));
+  if ((rc = hp.done(HDFS_CRC32C_OK))) return rc;  // both streams drained, buffers unpinned
   if (mode == kModeVerify) {
     std::vector<uint32_t> fb(npieces);
     unsigned long long m = 0;
@@ -1094,13 +1146,13 @@ int hdfs_crc32c_verify_crcdata(const void *crcdata, int32_t chunksize, int32_t c
     const size_t off_crc = (size_t(dlen) + 255) & ~size_t(255);
     const size_t off_bm = off_crc + ((size_t(crcdlen) + 255) & ~size_t(255));
     if (off_bm + size_t((nch + 7) / 8) > kStageCap) {
-      HostRegistration whole;
-      int rc = whole.ensure(reg, size_t(crcdlen) + size_t(dlen));
+      HostPins whole({});  // host_pipeline drains its streams before it returns
+      int rc = whole.pin({{reg, size_t(crcdlen) + size_t(dlen)}});
       if (rc) return rc;
       uint64_t fb64 = UINT64_MAX, m = 0;
       rc = host_pipeline(kModeVerify, reg + crcdlen, uint64_t(dlen), uint32_t(chunksize), HDFS_CRC32C_SEG_BE | pflag, 0,
                          const_cast<uint8_t *>(reg), nullptr, 0, &fb64, &m);
-      if (rc) return rc;
+      if ((rc = whole.done(rc))) return rc;
       if (fb64 != UINT64_MAX) {
         if (first_bad) *first_bad = int32_t(fb64);
         return fail(HDFS_CRC32C_ERR_DATANODE_BAD_CHECKSUM, "chunk %llu: bad checksum", (unsigned long long)fb64);
@@ -1247,12 +1299,21 @@ int hdfs_crc32c_stream_create(void **stream) {
   DeviceGuard g(c->dev);
   hipStream_t s;
   HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->user_streams.push_back(s);
+  }
   *stream = s;
   return HDFS_CRC32C_OK;
 }
 
 int hdfs_crc32c_stream_destroy(void *stream) {
   HDFS_ON_ENGINE_DEVICE();
+  {
+    std::lock_guard<std::mutex> lk(ec_->mu);
+    auto &v = ec_->user_streams;
+    v.erase(std::remove(v.begin(), v.end(), static_cast<hipStream_t>(stream)), v.end());
+  }
   HIPCHK(hipStreamDestroy(static_cast<hipStream_t>(stream)));
   return HDFS_CRC32C_OK;
 }
@@ -1300,11 +1361,13 @@ int hdfs_crc32c_host_alloc(void **p, uint64_t bytes) {
   hipError_t e = hipHostMalloc(p, bytes ? bytes : 1, hipHostMallocDefault);
   if (e != hipSuccess) return fail(HDFS_CRC32C_ENOMEM, "hipHostMalloc(%llu): %s", (unsigned long long)bytes,
                                    hipGetErrorString(e));
+  pins().add_owned(*p, bytes ? bytes : 1);  // the host paths DMA it in place
   return HDFS_CRC32C_OK;
 }
 
 int hdfs_crc32c_host_free(void *p) {
   HDFS_ON_ENGINE_DEVICE();
+  if (p && !pins().remove_owned(p)) return fail(HDFS_CRC32C_EINVAL, "%p is not a hdfs_crc32c_host_alloc block", p);
   HIPCHK(hipHostFree(p));
   return HDFS_CRC32C_OK;
 }
@@ -1316,11 +1379,14 @@ int hdfs_crc32c_device_sync(void) {
     return HDFS_CRC32C_OK;
   }
   // a resident mailbox kernel never finishes while it is in use: every
-  // stream but its own
+  // stream but its own -- the engine's, the NULL stream and the caller's
+  // streams from hdfs_crc32c_stream_create (non-blocking, so the NULL
+  // stream does not order them)
   std::lock_guard<std::mutex> lk(ec_->mu);
   HIPCHK(hipStreamSynchronize(nullptr));
   for (hipStream_t s : {ec_->stream, ec_->v_stream, ec_->r_stream, ec_->copy_stream, ec_->comp_stream})
     if (s) HIPCHK(hipStreamSynchronize(s));
+  for (hipStream_t s : ec_->user_streams) HIPCHK(hipStreamSynchronize(s));
   return HDFS_CRC32C_OK;
 }
 

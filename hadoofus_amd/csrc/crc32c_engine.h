@@ -7,9 +7,11 @@
 #include <cstdarg>
 #include <cstddef>
 #include <cstdint>
+#include <initializer_list>
 #include <mutex>
 #include <vector>
 
+#include "crc32c_hostpin.h"
 #include "crc32c_internal.h"
 #include "hadoofus_crc32c.h"
 
@@ -54,12 +56,16 @@ hipError_t launch_header_window(const uint8_t *s, uint64_t len, uint64_t base, u
 // Short device-resident run in one launch (count <= kSmallRunMax grid
 // points, one workgroup each); hout: pinned host slots (device address),
 // kSrHostBytes.
+// Copy-out (copy_dst non-null): each packet delivers frame::read_avail bytes
+// (win: the client read window from client_offset; else whole payloads),
+// placed by frame::read_place within copy_cap bytes of copy_dst.
 hipError_t launch_small_run(const uint8_t *s, uint64_t len, uint32_t count, int proto, uint32_t cs, int ctype,
                             int verify, const uint32_t *tab, const uint32_t *pow2, uint8_t *copy_dst,
-                            uint64_t copy_cap, uint8_t *hout, uint32_t seq, hipStream_t stream);
+                            uint64_t copy_cap, int win, int64_t client_offset, uint8_t *hout, uint32_t seq,
+                            hipStream_t stream);
 hipError_t launch_frame_grid(const uint8_t *s, uint64_t len, uint64_t base, uint32_t count, int proto, uint32_t cs,
                              int ctype, int verify, uint32_t sflags, uint8_t *bm_base, uint8_t *copy_base,
-                             uint64_t copy_cap, GridBufs g, hipStream_t stream);
+                             uint64_t copy_cap, int win, int64_t client_offset, GridBufs g, hipStream_t stream);
 // One workgroup: the bad-packet list to *bad (device) and, with its count and
 // then seq, to the pinned host area hsum2 (device address; first host_cap
 // entries after 256 bytes).
@@ -190,6 +196,10 @@ struct DevCtx {
   hipStream_t mb_stream = nullptr;
   uint32_t mb_epoch = 0, mb_idle_ticks = 0;
   uint64_t mb_calls = 0, mb_launches = 0;
+  // streams handed out by hdfs_crc32c_stream_create (non-blocking: they do
+  // not serialise with the NULL stream, so device_sync with a mailbox open
+  // synchronises each of them)
+  std::vector<hipStream_t> user_streams;
   // CUs the bulk (one-workgroup-per-CU) kernels may use
   int bulk_cus() const { return num_cu - (mb_on ? 1 : 0); }
   std::mutex mu;
@@ -217,7 +227,6 @@ int fill_seg(const hdfs_crc32c_segment &in, int mode, SegDev &s, size_t idx);
 // Table set of a segment: 0 = CRC32C, 1 = CRC32 (zlib polynomial).
 inline int seg_ctype(uint32_t flags) { return (flags & HDFS_CRC32C_SEG_CRC32) ? 1 : 0; }
 bool device_accessible(const void *p);
-bool is_pinned_host(const void *p);
 // Enqueue one compute / verify pass (prep + tiled + generic kernels) on st.
 int launch_all(DevCtx &c, int mode, const SegDev *d_segs, uint32_t nseg, uint64_t rounds, uint64_t mtiles,
                uint64_t gtiles, uint32_t *d_fb, unsigned long long *d_mism, uint32_t *d_gctr, hipStream_t st,
@@ -259,21 +268,31 @@ int chunk_crcs_to_host(const void *data, uint64_t len, uint32_t cs, int ctype, u
 int host_pipeline(int mode, const uint8_t *data, uint64_t len, uint32_t cs, uint32_t flags, uint32_t crc_init,
                   void *crcs, uint8_t *bitmap, uint64_t piece_req, uint64_t *first_bad, uint64_t *mismatches);
 
-struct HostRegistration {
-  const void *p = nullptr;
-  ~HostRegistration() {
-    if (p) (void)hipHostUnregister(const_cast<void *>(p));
+// Pinned host memory of the host-memory paths (crc32c_hostpin.h): the
+// engine's registry, and the pins of one call.  HostPins::pin() pins the
+// caller buffers of the call (or finds it pinned: an engine allocation, a
+// range another call holds, memory its owner pinned); done(rc) drains the
+// streams that may still touch the buffers, then unpins, reporting a failed
+// unregistration.  An early return (rc already set, or HIPCHK) drains and
+// unpins in the destructor, so no GPU work queued by the call outlives the
+// registration of the memory it reads or writes.
+PinRegistry &pins();
+struct HostPins {
+  PinRegistry::Scope s;
+  std::vector<hipStream_t> drain;
+  bool finished = false;
+  explicit HostPins(std::initializer_list<hipStream_t> st) : s(pins()), drain(st) {}
+  HostPins(const HostPins &) = delete;
+  HostPins &operator=(const HostPins &) = delete;
+  ~HostPins() {
+    if (!finished)
+      for (hipStream_t st : drain)
+        if (st) (void)hipStreamSynchronize(st);
   }
-  int ensure(const void *ptr, size_t n) {
-    // pinned only if both ends are: a buffer that starts inside a pinned
-    // allocation and runs past it must not be DMA-ed as pinned (the GPU would
-    // fault on the unmapped rest); registering it fails loudly instead
-    if (!ptr || !n || (is_pinned_host(ptr) && is_pinned_host(static_cast<const uint8_t *>(ptr) + n - 1)))
-      return HDFS_CRC32C_OK;
-    HIPCHK(hipHostRegister(const_cast<void *>(ptr), n, hipHostRegisterDefault));
-    p = ptr;
-    return HDFS_CRC32C_OK;
-  }
+  // every host buffer of the call at once (buffers sharing a page become one
+  // registration: a DMA never straddles two)
+  int pin(std::initializer_list<std::pair<const void *, size_t>> bufs);
+  int done(int rc);
 };
 
 inline uint64_t align_up(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }

@@ -214,5 +214,37 @@ HDFS_HD int frame_step(const uint8_t *p, uint64_t rem, uint64_t pos, int proto, 
   return kStepNext;
 }
 
+// Client read window of the read path (_process_recv_packet /
+// _recv_packet_copy_data, src/datanode.c:2478-2549): a read of the block's
+// bytes [client_offset, client_offset + remains_tot) takes from a verified
+// packet its data from c_begin = client_offset - offsetInBlock on (0 when
+// the packet starts at or after client_offset); c_begin >= dataLen is
+// UNEXPECTED_READ_OFFSET (:2483-2486).  Returns avail = dataLen - c_begin,
+// the bytes the packet can deliver (0 for that error, for a packet with a
+// framing error and for an empty one).  win = false: whole payloads
+// (c_begin 0).  In 64 bits: the reference keeps c_begin in an int32_t, which
+// differs only for client_offset - offsetInBlock >= 2^31 (beyond any block;
+// dataLen <= 1 GiB, so such a packet is UNEXPECTED_READ_OFFSET here).
+HDFS_HD uint32_t read_avail(const hdfs_crc32c_packet &r, bool win, int64_t client_offset, uint32_t &c_begin) {
+  c_begin = 0;
+  if (r.error || r.data_len <= 0) return 0u;
+  if (win && r.offset_in_block < client_offset) {
+    const uint64_t cb = uint64_t(client_offset) - uint64_t(r.offset_in_block);
+    if (cb >= uint64_t(r.data_len)) return 0u;
+    c_begin = uint32_t(cb);
+  }
+  return uint32_t(r.data_len) - c_begin;
+}
+
+// Where packet k's delivered bytes go: `before` = the avail of every earlier
+// packet of the walk (their sum), `want` = bytes of the destination (the
+// read's remains_tot, or the buffer for whole payloads).  Bytes [c_begin,
+// c_begin + *len) of its data land at dst + *at; *len = 0 past the window.
+HDFS_HD void read_place(uint64_t before, uint32_t avail, uint64_t want, uint64_t &at, uint32_t &len) {
+  at = before < want ? before : want;
+  const uint64_t room = want - at;
+  len = uint32_t(avail < room ? avail : room);
+}
+
 }  // namespace frame
 }  // namespace hdfs_crc32c

@@ -49,8 +49,11 @@ struct SegDev {
   uint64_t len;          // bytes
   uint64_t round_start;  // global index of this segment's first main-path round
   uint64_t gtile_start;  // global index of this segment's first generic tile
-  uint8_t *copy_dst;     // verify + copy-out: the segment's data is also written here (or null)
-  uint64_t reserved;
+  // verify + copy-out: data bytes [copy_w0, copy_w1) of the segment are also
+  // written to copy_dst + (j - copy_w0) (copy_dst null: no copy-out) -- the
+  // whole payload, or the part of it a client read window takes
+  uint8_t *copy_dst;
+  uint32_t copy_w0, copy_w1;
 };
 static_assert(sizeof(SegDev) == 96, "SegDev layout");
 

@@ -356,6 +356,72 @@ DEV uint64_t tile_at_round(SegP segs, uint32_t nseg, uint64_t r, uint64_t total_
   return g < total_tiles ? g : total_tiles;
 }
 
+struct LaneConst {
+  uint32_t lane, hsel, loff, lb0, lb1, qi, qg, zk, zbase, z448;
+  uint64_t ntiles;   // RUN 2: main tiles of the launch
+  uint32_t rmask;    // RUN 1: tiles per run - 1
+  uint32_t *gslot;   // RUN 2: LDS [kGatherSlots] owner words, then [kGatherSlots][64] CRC words
+  // the diagnostic build's store-policy experiment (EP::policy); 0 in the
+  // release build, where no hook reads it
+  uint32_t store_policy;
+};
+
+// Store / load sites of the tiled kernel's epilogue.  The product kernels
+// use ReleaseEP: one instruction per site with the cache bits the
+// measurements chose, nothing else.  The diagnostic build
+// (-DHDFS_CRC32C_DIAG) instantiates the same kernels with DiagEP
+// (crc32c_diag_ep.h), which puts the store-policy experiments of
+// tools/exp_knobs.py behind these hooks -- the product functions below carry
+// no diagnostic branch of their own.
+struct ReleaseEP {
+  DEV static uint32_t policy(uint32_t) { return 0u; }
+  // verify: the expected CRC of the lane's chunk (default policy)
+  DEV static uint32_t exp_load(uint32_t, __amdgpu_buffer_rsrc_t re, uint32_t off) {
+    return __builtin_amdgcn_raw_buffer_load_b32(re, off, 0, 0);
+  }
+  // result records dropped (compute CRCs, verify bitmap bytes)
+  DEV static bool drop(uint32_t) { return false; }
+  // compute gather: the slot protocol skipped, its stores dropped
+  DEV static bool gather_off(uint32_t) { return false; }
+  // compute gather: where a whole group's 256 B go
+  DEV static const uint32_t *group_base(uint32_t, const uint32_t *b, const SegHot &, uint32_t) { return b; }
+  // compute gather: nt (pipelined gather kernel, one process: sc1 6 797,
+  // nt 6 835, nt sc1 6 827, sc0 sc1 6 771 GB/s alg,
+  // profiles/r02/s6/exp_gather_store_policy.json)
+  DEV static void group_store(uint32_t, uint32_t v, __amdgpu_buffer_rsrc_t r, uint32_t off) {
+    __builtin_amdgcn_raw_buffer_store_b32(v, r, off, 0, 2);
+  }
+  // compute, one store per tile: no other way of writing a tile
+  static constexpr bool kAltTileStores = false;
+  // compute, one store per tile: sc1.  Compute mode loses ~13 % to its CRC
+  // stores, per written-back line rather than per byte (4 B per tile costs
+  // as much as 32 B; an L2-resident window recovers half); sc1 stores
+  // measured +1.7 % compute, verify unchanged (tools/exp_knobs.py,
+  // profiles/r02/).
+  DEV static void tile_store(uint32_t, uint32_t v, __amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t) {
+    __builtin_amdgcn_raw_buffer_store_b32(v, r, off, 0, 16);
+  }
+  // verify: the tile's bitmap byte (default policy; nt / sc1 cost 6 %,
+  // profiles/r02/s8/exp_verify_cache_policies.json)
+  DEV static void bitmap_store(uint32_t, uint8_t b, __amdgpu_buffer_rsrc_t r, uint32_t off) {
+    __builtin_amdgcn_raw_buffer_store_b8(b, r, off, 0, 0);
+  }
+  // verify + copy-out: nt sc1 (streaming; 1 GiB device run, one process:
+  // default 2 083, sc1 2 172, nt 2 220, nt sc1 2 250 GiB/s,
+  // profiles/r02/s6/exp_copy_store_policy.json)
+  DEV static void copy_store(uint32_t, u32x4 v, __amdgpu_buffer_rsrc_t r, uint32_t off) {
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 18);
+  }
+};
+#ifdef HDFS_CRC32C_DIAG
+}  // namespace hdfs_crc32c
+#include "crc32c_diag_ep.h"
+namespace hdfs_crc32c {
+using EP = DiagEP;
+#else
+using EP = ReleaseEP;
+#endif
+
 // Issue the loads of one round: four fully coalesced 1 KiB dwordx4 loads
 // (lanes with bit 3 clear / set cover sub-chunks 2k / 2k+1, in the permuted
 // lane order the permlane transpose expects) plus, in verify mode, the
@@ -384,7 +450,7 @@ struct LaneOff {
 // byte read lies in a dword that also holds data of the segment, so no read
 // leaves the data's pages.  The shift rides with the round (rounds in
 // flight may belong to different segments).
-template <int MODE, int NT, int BUF, int UNA>
+template <int MODE, int NT, int BUF, int UNA, class P = EP>
 DEV void issue(uint32_t (&d)[16], uint32_t &exp, uint32_t &tl, uint32_t &sh_a, const Cursor c, SegP segs,
                uint32_t hsel, uint32_t loff, uint32_t qg, uint32_t lane, LaneOff &lo, SegCache &kc,
                uint32_t pol = 0u) {
@@ -421,9 +487,7 @@ DEV void issue(uint32_t (&d)[16], uint32_t &exp, uint32_t &tl, uint32_t &sh_a, c
     if (MODE != kModeCompute) {
       const __amdgpu_buffer_rsrc_t re = __builtin_amdgcn_make_buffer_rsrc(
           sh.crcs + c.tile * kTileChunks, 0, static_cast<int>(nch * 4u), 0x00020000);
-      // diagnostic 21 / 23: the expected CRCs loaded nontemporal
-      if (kDiag && (pol == 21u || pol == 23u)) exp = __builtin_amdgcn_raw_buffer_load_b32(re, qg * 4u, 0, 2);
-      else exp = __builtin_amdgcn_raw_buffer_load_b32(re, qg * 4u, 0, 0);
+      exp = P::exp_load(pol, re, qg * 4u);
     }
   } else {
     const uint32_t last = min(kTileChunks, segs[c.seg].nchunks - c.tile * kTileChunks) - 1u;
@@ -450,15 +514,6 @@ DEV void issue(uint32_t (&d)[16], uint32_t &exp, uint32_t &tl, uint32_t &sh_a, c
   }
 }
 
-struct LaneConst {
-  uint32_t lane, hsel, loff, lb0, lb1, qi, qg, zk, zbase, z448;
-  uint64_t ntiles;   // RUN 2: main tiles of the launch
-  uint32_t rmask;    // RUN 1: tiles per run - 1
-  uint32_t *gslot;   // RUN 2: LDS [kGatherSlots] owner words, then [kGatherSlots][64] CRC words
-  // 0 default; diagnostic build only: 1 nontemporal, 2 drop result stores,
-  // 3 full-line CRC writes (always 0 in the release build)
-  uint32_t store_policy;
-};
 
 // Finish one round of one stream after its 16 slicing steps: on a tile's
 // last round, combine the 8 lanes of each chunk and write / compare.  The
@@ -469,7 +524,7 @@ struct LaneConst {
 // them.  Every round therefore issues exactly the same vector-memory ops
 // (4 loads, [1 expected-CRC load], 1 store) and the compiler's vmcnt waits
 // stay exact.
-template <int MODE, int RUN>
+template <int MODE, int RUN, class P = EP>
 DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, uint32_t st, const LaneConst &L,
                 uint32_t *__restrict__ first_bad, unsigned long long *__restrict__ mism, SegCache &kc,
                 uint32_t &acc) {
@@ -478,6 +533,7 @@ DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, ui
   const uint32_t flags = sh.flags;
   const uint32_t nch = min(kTileChunks, sh.nchunks - c.tile * kTileChunks);
   const bool leader = last && (L.qi == 0) && (L.qg < nch);
+  const uint32_t pol = L.store_policy;
   uint32_t out = 0, byte = 0;
   if (last) {
     uint32_t v = L.zk ? zshift(lds, L.zbase, st) : st;
@@ -496,7 +552,7 @@ DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, ui
   }
   byte = rfl(byte);
   if (MODE == kModeCompute) {
-    const bool keep = last && !(kDiag && L.store_policy == 2);
+    const bool keep = last && !P::drop(pol);
     const uint32_t val = (flags & kSegBigEndian) ? __builtin_bswap32(out) : out;
     if constexpr (RUN == 2) {
       // schedule 3 gather: an eligible group's tiles (8 full tiles of one
@@ -505,10 +561,9 @@ DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, ui
       // 32 B but still count in the slot, so it passes on to the next group
       uint32_t sval = val, soff = leader ? L.qg * 4u : 0x80000000u, range = keep ? nch * 4u : 0u;
       const uint32_t *sbase = sh.crcs + c.tile * kTileChunks;
-      // diagnostic 20: the gather kernel with its slot protocol skipped and
-      // every CRC store dropped (what the protocol itself costs)
-      if (kDiag && L.store_policy == 20) range = 0u;
-      if (last && !(kDiag && L.store_policy == 20)) {
+      const bool off = P::gather_off(pol);
+      if (off) range = 0u;
+      if (last && !off) {
         // eligible: the group's 8 tiles are whole tiles of this segment.  A
         // segment whose main tiles start and end on group boundaries (every
         // block of a transfer) has only such groups, bar a partial last
@@ -563,20 +618,10 @@ DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, ui
             sval = dat[L.lane];
             soff = L.lane * 4u;
             // eligible: the group starts at segment tile (gt & ~7) - mtile_start
-            sbase = sh.crcs + static_cast<uint64_t>((gt & ~7u) - static_cast<uint32_t>(sh.mtile_start)) * kTileChunks;
-            if (kDiag && L.store_policy == 14) {
-              // diagnostic: the group's 256 B land at a scattered group
-              // position of the segment (q -> 37 q mod 2^k): same bytes and
-              // lines, written in no spatial order (the CRCs end up permuted)
-              const uint32_t ng = sh.main_tiles >> 3, q = ((gt & ~7u) - static_cast<uint32_t>(sh.mtile_start)) >> 3;
-              if (ng && (ng & (ng - 1u)) == 0u) sbase = sh.crcs + ((q * 37u) & (ng - 1u)) * 64u;
-            }
-            // diagnostic: 15 every group store lands in the segment's first
-            // 256 KiB (an L2-resident window: the stores' CU / L2 cost without
-            // the HBM write-back), 2 group stores dropped
-            if (kDiag && L.store_policy == 15)
-              sbase = sh.crcs + ((((gt & ~7u) - static_cast<uint32_t>(sh.mtile_start)) * kTileChunks) & 65535u);
-            range = (kDiag && L.store_policy == 2) ? 0u : 256u;
+            sbase = P::group_base(
+                pol, sh.crcs + static_cast<uint64_t>((gt & ~7u) - static_cast<uint32_t>(sh.mtile_start)) * kTileChunks,
+                sh, gt);
+            range = P::drop(pol) ? 0u : 256u;
           }
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
           if (L.lane == 0)
@@ -586,15 +631,7 @@ DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, ui
       const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(
           reinterpret_cast<uint32_t *>(rfl64(reinterpret_cast<uint64_t>(sbase))), 0, static_cast<int>(rfl(range)),
           0x00020000);
-      // product: nt (pipelined gather kernel, one process: sc1 6 797, nt 6 835,
-      // nt sc1 6 827, sc0 sc1 6 771 GB/s alg, profiles/r02/s6/exp_gather_store_policy.json);
-      // diagnostic build: the store policies' cache bits
-      if (kDiag && L.store_policy == 5) __builtin_amdgcn_raw_buffer_store_b32(sval, rg, soff, 0, 16);       // sc1
-      else if (kDiag && L.store_policy == 6) __builtin_amdgcn_raw_buffer_store_b32(sval, rg, soff, 0, 17);  // sc0 sc1
-      else if (kDiag && L.store_policy == 7) __builtin_amdgcn_raw_buffer_store_b32(sval, rg, soff, 0, 18);  // nt sc1
-      else if (kDiag && L.store_policy == 8) __builtin_amdgcn_raw_buffer_store_b32(sval, rg, soff, 0, 1);   // sc0
-      else if (kDiag && L.store_policy == 11) __builtin_amdgcn_raw_buffer_store_b32(sval, rg, soff, 0, 0);  // default
-      else __builtin_amdgcn_raw_buffer_store_b32(sval, rg, soff, 0, 2);
+      P::group_store(pol, sval, rg, soff);
       return;
     }
     if constexpr (RUN == 1) {
@@ -611,69 +648,20 @@ DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, ui
       __builtin_amdgcn_raw_buffer_store_b32(acc, rr, L.lane * 4u, 0, 16);
       return;
     }
-    if (kDiag && L.store_policy == 3) {
-      // diagnostic: 128-B full-line write per tile (crcs must hold 16 B per chunk)
-      const __amdgpu_buffer_rsrc_t r4 = __builtin_amdgcn_make_buffer_rsrc(
-          segs[c.seg].crcs + c.tile * kTileChunks * 4, 0, last ? static_cast<int>(nch * 16u) : 0, 0x00020000);
-      u32x4 v4 = {val, val, val, val};
-      __builtin_amdgcn_raw_buffer_store_b128(v4, r4, leader ? L.qg * 16u : 0x80000000u, 0, 0);
-    } else {
-      // descriptor fields forced uniform (readfirstlane): otherwise the
-      // compiler may treat them as divergent and wrap the store in a
-      // waterfall loop
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-          reinterpret_cast<uint32_t *>(rfl64(reinterpret_cast<uint64_t>(sh.crcs + c.tile * kTileChunks))), 0,
-          static_cast<int>(rfl(keep ? nch * 4u : 0u)), 0x00020000);
-      uint32_t off = leader ? L.qg * 4u : 0x80000000u;
-      if (kDiag && (L.store_policy == 12 || L.store_policy == 13)) {
-        // diagnostic: only the last tile of each 8-tile group stores -- 12: one
-        // 256-B store over the whole group's CRCs (64 lanes x 4 B, sc1; the
-        // values are not the group's CRCs), 13: its own 32 B as usual
-        const bool grp = keep && (c.tile & 7u) == 7u;
-        const bool full = L.store_policy == 12;
-        const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(
-            reinterpret_cast<uint32_t *>(rfl64(reinterpret_cast<uint64_t>(sh.crcs + (full ? (c.tile & ~7u) : c.tile) *
-                                                                                             kTileChunks))),
-            0, static_cast<int>(rfl(grp ? (full ? 256u : nch * 4u) : 0u)), 0x00020000);
-        __builtin_amdgcn_raw_buffer_store_b32(val, rg, full ? L.lane * 4u : off, 0, 16);
-        return;
-      }
-      if (kDiag && L.store_policy == 9) {
-        // diagnostic: every tile's 32 B lands in a 256 KiB window (L2-resident writes)
-        const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
-            reinterpret_cast<uint32_t *>(rfl64(reinterpret_cast<uint64_t>(sh.crcs))), 0,
-            static_cast<int>(rfl(keep ? 262144u : 0u)), 0x00020000);
-        const uint32_t wo = ((c.tile * 32u) & 262143u) + L.qg * 4u;
-        __builtin_amdgcn_raw_buffer_store_b32(val, rw, leader ? wo : 0x80000000u, 0, 0);
-        return;
-      }
-      if (kDiag && L.store_policy == 10 && L.qg != 0) off = 0x80000000u;  // diagnostic: 4 B per tile
-      // diagnostic cache policies of the CRC store (gfx940+ CPol: 1 sc0, 2 nt, 16 sc1)
-      if (kDiag && L.store_policy == 1) __builtin_amdgcn_raw_buffer_store_b32(val, rs, off, 0, 2);  // nt
-      else if (kDiag && L.store_policy == 5) __builtin_amdgcn_raw_buffer_store_b32(val, rs, off, 0, 16);  // sc1
-      else if (kDiag && L.store_policy == 6) __builtin_amdgcn_raw_buffer_store_b32(val, rs, off, 0, 17);  // sc0 sc1
-      else if (kDiag && L.store_policy == 7) __builtin_amdgcn_raw_buffer_store_b32(val, rs, off, 0, 18);  // nt sc1
-      else if (kDiag && L.store_policy == 8) __builtin_amdgcn_raw_buffer_store_b32(val, rs, off, 0, 1);   // sc0
-      else if (kDiag && L.store_policy == 11) __builtin_amdgcn_raw_buffer_store_b32(val, rs, off, 0, 0);  // default
-      // product: sc1.  Compute mode loses ~13 % to its CRC stores, per
-      // written-back line rather than per byte (4 B per tile costs as much as
-      // 32 B; an L2-resident window recovers half); sc1 stores measured +1.7 %
-      // compute, verify unchanged (tools/exp_knobs.py, profiles/r02/).
-      else __builtin_amdgcn_raw_buffer_store_b32(val, rs, off, 0, 16);
-    }
+    if constexpr (P::kAltTileStores)
+      if (P::tile_store_alt(pol, sh, segs, c, keep, nch, leader, L, val)) return;
+    // descriptor fields forced uniform (readfirstlane): otherwise the
+    // compiler may treat them as divergent and wrap the store in a
+    // waterfall loop
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<uint32_t *>(rfl64(reinterpret_cast<uint64_t>(sh.crcs + c.tile * kTileChunks))), 0,
+        static_cast<int>(rfl(keep ? nch * 4u : 0u)), 0x00020000);
+    P::tile_store(pol, val, rs, leader ? L.qg * 4u : 0x80000000u, L.qg);
   } else {
     const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
         reinterpret_cast<uint8_t *>(rfl64(reinterpret_cast<uint64_t>(sh.bitmap + c.tile))), 0,
-        static_cast<int>(rfl((last && !(kDiag && L.store_policy == 2)) ? 1u : 0u)), 0x00020000);
-    // diagnostic 22 / 23: the bitmap bytes stored nontemporal
-    if (kDiag && (L.store_policy == 22u || L.store_policy == 23u))
-      __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(byte), rb, L.lane == 0 ? 0u : 0x80000000u, 0, 2);
-    else if (kDiag && L.store_policy == 24u)  // diagnostic: sc1
-      __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(byte), rb, L.lane == 0 ? 0u : 0x80000000u, 0, 16);
-    else if (kDiag && L.store_policy == 25u)  // diagnostic: sc0 sc1
-      __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(byte), rb, L.lane == 0 ? 0u : 0x80000000u, 0, 17);
-    else
-      __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(byte), rb, L.lane == 0 ? 0u : 0x80000000u, 0, 0);
+        static_cast<int>(rfl((last && !P::drop(pol)) ? 1u : 0u)), 0x00020000);
+    P::bitmap_store(pol, static_cast<uint8_t>(byte), rb, L.lane == 0 ? 0u : 0x80000000u);
     if (byte && L.lane == 0) {  // rare: only tiles with a mismatch
       atomicMin(&first_bad[c.seg], c.tile * kTileChunks + __builtin_ctz(byte));
       atomicAdd(mism, static_cast<unsigned long long>(__builtin_popcount(byte)));
@@ -682,32 +670,49 @@ DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, ui
 }
 
 // Verify + copy-out (COPY kernels): the round's data, still in the loaded
-// lane order, is stored to the segment's copy_dst at the same offsets it was
-// loaded from (fully coalesced 1 KiB per instruction, the mirror of issue()).
-// The descriptor's range is the valid bytes of the round (0 for a parked
-// cursor or a segment without copy_dst), so out-of-range lanes are dropped.
+// lane order, goes to the segment's copy_dst at the offsets it was loaded
+// from (fully coalesced 1 KiB per instruction, the mirror of issue()),
+// restricted to the segment's copy window [copy_w0, copy_w1) -- the whole
+// payload, or the part of the packet a client read takes
+// (src/datanode.c:2478-2488, 2527-2540): data byte j lands at copy_dst +
+// (j - copy_w0).  A 16-B piece inside the window is one lane of the vector
+// store; a piece outside it (and every piece of a parked cursor or of a
+// segment without copy_dst) gets an out-of-range offset and is dropped; a
+// piece that straddles an edge of the window -- only where a read starts or
+// ends inside a packet, at most two pieces per read -- is stored byte by
+// byte.  (Tiled rounds cover whole chunks, so a window edge at the payload's
+// end never falls inside a piece.)
+template <class P = EP>
 DEV void copy_round(const uint32_t (&d)[16], const Cursor c, SegP segs, const LaneConst &L, SegCache &kc) {
   const SegHot &sh = hot(kc, segs, c.seg).h;
   const uint32_t cs = sh.chunk_size;
   uint8_t *dst = segs[c.seg].copy_dst;
+  const uint32_t w0 = segs[c.seg].copy_w0, w1 = segs[c.seg].copy_w1;
   const uint32_t nch = min(kTileChunks, sh.nchunks - c.tile * kTileChunks);
   const bool ok = c.valid && dst != nullptr;
-  uint8_t *base = ok ? dst + static_cast<uint64_t>(c.tile) * kTileChunks * cs + static_cast<uint64_t>(c.r) * kRoundBytes
-                     : dst;
+  // data offset of the round, and the window relative to it (payloads are
+  // < 2^31 bytes: int32 arithmetic)
+  const int32_t rp = static_cast<int32_t>(c.tile * kTileChunks * cs + c.r * kRoundBytes);
+  const int32_t lo = static_cast<int32_t>(w0) - rp, hi = static_cast<int32_t>(w1) - rp;
+  // descriptor base: where the round's first byte would land (may precede
+  // copy_dst when the window starts later; nothing below it is written)
+  uint8_t *base = ok ? dst - w0 + rp : dst;
+  const uint32_t valid = (nch - 1u) * cs + kRoundBytes;
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
       reinterpret_cast<uint8_t *>(rfl64(reinterpret_cast<uint64_t>(base))), 0,
-      static_cast<int>(rfl(ok ? (nch - 1u) * cs + kRoundBytes : 0u)), 0x00020000);
+      static_cast<int>(rfl(ok && hi > 0 ? min(valid, static_cast<uint32_t>(hi)) : 0u)), 0x00020000);
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     const u32x4 v = {d[4 * k + 0], d[4 * k + 1], d[4 * k + 2], d[4 * k + 3]};
-    // product: nt sc1 (streaming; 1 GiB device run, one process: default
-    // 2 083, sc1 2 172, nt 2 220, nt sc1 2 250 GiB/s verify + copy-out,
-    // profiles/r02/s6/exp_copy_store_policy.json); diagnostic build: 16 nt,
-    // 17 sc1, 19 default policy
-    if (kDiag && L.store_policy == 16) __builtin_amdgcn_raw_buffer_store_b128(v, rs, (2u * k + L.hsel) * cs + L.loff, 0, 2);
-    else if (kDiag && L.store_policy == 17) __builtin_amdgcn_raw_buffer_store_b128(v, rs, (2u * k + L.hsel) * cs + L.loff, 0, 16);
-    else if (kDiag && L.store_policy == 19) __builtin_amdgcn_raw_buffer_store_b128(v, rs, (2u * k + L.hsel) * cs + L.loff, 0, 0);
-    else __builtin_amdgcn_raw_buffer_store_b128(v, rs, (2u * k + L.hsel) * cs + L.loff, 0, 18);
+    const int32_t o = static_cast<int32_t>((2u * k + L.hsel) * cs + L.loff);
+    const bool inside = o >= lo && o + 16 <= hi;
+    P::copy_store(L.store_policy, v, rs, inside ? static_cast<uint32_t>(o) : 0x80000000u);
+    if (ok && !inside && o < hi && o + 16 > lo) {  // rare: the read starts or ends inside this piece
+      for (int b = 0; b < 16; b++)
+        if (o + b >= lo && o + b < hi)
+          __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(v[b >> 2] >> (8 * (b & 3))), rs,
+                                               static_cast<uint32_t>(o + b), 0, 0);
+    }
   }
 }
 
@@ -716,33 +721,18 @@ DEV void copy_round(const uint32_t (&d)[16], const Cursor c, SegP segs, const La
 // The S slicing chains are independent and interleaved step by step, so one
 // lane keeps S table lookups in flight (latency hiding by ILP, not waves).
 
-template <int MODE, int S, int COPY, int UNA, int RUN>
+template <int MODE, int S, int COPY, int UNA, int RUN, class P = EP>
 DEV void process(const uint32_t *lds, uint32_t (&d)[S][16], const uint32_t (&exp)[S], const uint32_t (&tl)[S],
                  const uint32_t (&sh_a)[S], const Cursor (&c)[S], SegP segs, uint32_t (&st)[S], const LaneConst &L,
                  uint32_t *__restrict__ first_bad, unsigned long long *__restrict__ mism, SegCache (&kc)[S],
                  uint32_t (&acc)[S]) {
-  if constexpr (kDiag && MODE == kModeLoadOnly) {
-    // Diagnostic twin of verify (diagnostic build only): the same loads and
-    // the same bitmap store op with its record dropped, no CRC arithmetic.
-    // The loaded words fold into st, and an impossible condition on st keeps
-    // them live (without it the compiler deletes the unused loads).
-#pragma unroll
-    for (int s = 0; s < S; s++) {
-      uint32_t v = exp[s];
-#pragma unroll
-      for (int w = 0; w < 16; w++) v ^= d[s][w];
-      st[s] ^= v;
-      const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
-          reinterpret_cast<uint8_t *>(rfl64(reinterpret_cast<uint64_t>(segs[c[s].seg].bitmap + c[s].tile))), 0, 0,
-          0x00020000);
-      __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(st[s]), rb, 0u, 0, 0);
-      if (st[s] == 0x9E3779B9u && c[s].r == 0xFFFFFFFFu) atomicAdd(mism, 1ull);
-    }
+  if constexpr (MODE == kModeLoadOnly) {  // diagnostic build only (the launcher refuses it otherwise)
+    P::template load_only_round<S>(d, exp, c, segs, st, mism);
     return;
   }
   if constexpr (COPY && !UNA) {
 #pragma unroll
-    for (int s = 0; s < S; s++) copy_round(d[s], c[s], segs, L, kc[s]);
+    for (int s = 0; s < S; s++) copy_round<P>(d[s], c[s], segs, L, kc[s]);
   }
   uint32_t x[S];
 #pragma unroll
@@ -765,7 +755,7 @@ DEV void process(const uint32_t *lds, uint32_t (&d)[S][16], const uint32_t (&exp
 #pragma unroll
         for (int j = 0; j < 16; j++) e[j] = d[s][j];
         transpose(e);
-        copy_round(e, c[s], segs, L, kc[s]);
+        copy_round<P>(e, c[s], segs, L, kc[s]);
       }
     }
     const uint32_t ri = hot(kc[s], segs, c[s].seg).reg_init;  // uniform control flow: kc stays in SGPRs
@@ -781,7 +771,7 @@ DEV void process(const uint32_t *lds, uint32_t (&d)[S][16], const uint32_t (&exp
 #pragma unroll
   for (int s = 0; s < S; s++) st[s] = slice4(lds, x[s], 0u, L.lb0, L.lb1);
 #pragma unroll
-  for (int s = 0; s < S; s++) finish<MODE, RUN>(lds, exp[s], c[s], segs, st[s], L, first_bad, mism, kc[s], acc[s]);
+  for (int s = 0; s < S; s++) finish<MODE, RUN, P>(lds, exp[s], c[s], segs, st[s], L, first_bad, mism, kc[s], acc[s]);
 }
 
 // Tiled kernel.  MODE compute / verify; ORDER schedule (above); NT
@@ -853,7 +843,7 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
   LaneConst L;
   // tune: [7:0] store policy (diagnostic build), [11:8] ORDER-3 group shift,
   // [13:12] ORDER-3 dealing: 0 plain, 1 XCD-major, 2 XCD-split (uniform: SGPR)
-  L.store_policy = kDiag ? rfl(tune & 0xffu) : 0u;
+  L.store_policy = EP::policy(tune & 0xffu);
   L.lane = threadIdx.x & 63u;
   L.hsel = (L.lane >> 3) & 1u;                              // load: odd sub-chunk of each 1 KiB
   L.loff = 16u * (4u * (L.lane & 7u) + (L.lane >> 4));      // load: byte offset in the sub-chunk
@@ -1094,9 +1084,9 @@ __global__ __launch_bounds__(256) void crc32c_generic_kernel(
       const uint64_t off = static_cast<uint64_t>(chunk) * sg.chunk_size;
       const uint8_t *p = sg.data + off;
       uint64_t n = min(static_cast<uint64_t>(sg.chunk_size), sg.len - off);
-      if (sg.copy_dst) {  // verify + copy-out: this lane's chunk (tails and odd chunk sizes only)
-        uint8_t *q = sg.copy_dst + off;
-        for (uint64_t i = 0; i < n; i++) gstore8(q + i, gload8(p + i));
+      if (sg.copy_dst) {  // verify + copy-out: this lane's chunk (tails and odd chunk sizes) inside the window
+        const uint64_t a = max<uint64_t>(off, sg.copy_w0), e = min<uint64_t>(off + n, sg.copy_w1);
+        for (uint64_t j = a; j < e; j++) gstore8(sg.copy_dst + (j - sg.copy_w0), gload8(sg.data + j));
       }
       uint32_t c = sg.reg_init;
       while (n && (reinterpret_cast<uintptr_t>(p) & 3u)) {
@@ -1839,10 +1829,11 @@ struct GridContrib {
   uint32_t nseg, rounds, mtiles, gtiles, bm, payload;
 };
 
-DEV GridContrib grid_contrib(const hdfs_crc32c_packet &r, uint32_t cs, int verify) {
+DEV GridContrib grid_contrib(const hdfs_crc32c_packet &r, uint32_t cs, int verify, int rwin, int64_t client_offset) {
   GridContrib a{0u, 0u, 0u, 0u, 0u, 0u};
   if (r.error) return a;
-  a.payload = uint32_t(r.data_len);
+  uint32_t cb = 0;
+  a.payload = frame::read_avail(r, rwin != 0, client_offset, cb);  // bytes the packet can deliver
   if (!verify || r.crc_len <= 0) return a;
   const uint32_t nch = uint32_t(r.crc_len) / 4u, ntiles = (nch + 7u) / 8u;
   const bool eligible = cs % kRoundBytes == 0;
@@ -1890,7 +1881,7 @@ constexpr uint32_t kGridBlock = 64;
 
 __global__ __launch_bounds__(kGridBlock) void frame_grid_kernel(
     const uint8_t *__restrict__ s, uint64_t len, uint64_t base, uint32_t count, int proto, uint32_t cs, int ctype,
-    int verify, hdfs_crc32c_packet *__restrict__ recs, uint32_t *__restrict__ status,
+    int verify, int rwin, int64_t client_offset, hdfs_crc32c_packet *__restrict__ recs, uint32_t *__restrict__ status,
     GridContrib *__restrict__ contrib, uint64_t *__restrict__ blk_sum, uint32_t *__restrict__ blk_min,
     GridSummary *__restrict__ sum, uint32_t *__restrict__ done) {
   __shared__ __attribute__((aligned(16))) uint8_t win[kGridBlock][kHdrWin];
@@ -1932,7 +1923,7 @@ __global__ __launch_bounds__(kGridBlock) void frame_grid_kernel(
                                     : kGridOff;
       if (code != kGridMore) {
         recs[k] = r;
-        a = grid_contrib(r, cs, verify);
+        a = grid_contrib(r, cs, verify, rwin, client_offset);
       }
     }
   }
@@ -1975,7 +1966,8 @@ __global__ __launch_bounds__(kGridBlock) void grid_build_kernel(
     const hdfs_crc32c_packet *__restrict__ recs, const uint32_t *__restrict__ status,
     const GridContrib *__restrict__ contrib, const uint64_t *__restrict__ blk_sum,
     const uint32_t *__restrict__ blk_min, uint32_t cs, uint32_t sflags, uint8_t *__restrict__ bm_base,
-    uint8_t *__restrict__ copy_base, uint64_t copy_cap, SegDev *__restrict__ segs, uint32_t *__restrict__ seg2pkt,
+    uint8_t *__restrict__ copy_base, uint64_t copy_cap, int rwin, int64_t client_offset, SegDev *__restrict__ segs,
+    uint32_t *__restrict__ seg2pkt,
     uint32_t *__restrict__ fb, uint32_t *__restrict__ gctr, uint32_t *__restrict__ done, uint32_t *__restrict__ exc,
     GridSummary *__restrict__ sum, uint8_t *__restrict__ hsum, uint32_t seq) {
   static_assert(sizeof(hdfs_crc32c_packet) == kGridRecBytes, "host record layout");
@@ -2065,10 +2057,16 @@ __global__ __launch_bounds__(kGridBlock) void grid_build_kernel(
       d.len = uint64_t(r.data_len);
       d.round_start = ex[1];
       d.gtile_start = ex[3];
-      // never past the caller's buffer: a packet that does not fit is not copied
-      // (the host sees the run's payload exceed the capacity and fails the call)
-      d.copy_dst = copy_base && ex[5] + own[5] <= copy_cap ? copy_base + ex[5] : nullptr;
-      d.reserved = 0;
+      // copy-out: the packet's delivered bytes [c_begin, c_begin + len) at
+      // their place in the destination, never past it (copy_cap: what is
+      // left of the read, or of the buffer, at this pass)
+      uint32_t cb = 0, clen = 0;
+      uint64_t at = 0;
+      (void)frame::read_avail(r, rwin != 0, client_offset, cb);
+      frame::read_place(ex[5], static_cast<uint32_t>(own[5]), copy_cap, at, clen);
+      d.copy_dst = copy_base && clen ? copy_base + at : nullptr;
+      d.copy_w0 = cb;
+      d.copy_w1 = cb + clen;
       segs[sg] = d;
       seg2pkt[sg] = k;
       fb[sg] = 0xFFFFFFFFu;
@@ -2231,6 +2229,7 @@ __global__ __launch_bounds__(1024) void small_run_kernel(const uint8_t *__restri
                                                          const uint32_t *__restrict__ tab,
                                                          const uint32_t *__restrict__ pow2,
                                                          uint8_t *__restrict__ copy_dst, uint64_t copy_cap,
+                                                         int rwin, int64_t client_offset,
                                                          uint8_t *__restrict__ hout, uint32_t seq) {
   __shared__ uint32_t tt[1024];
   __shared__ __attribute__((aligned(16))) uint32_t zt[16 * 1024];  // Z_{2^b}, b < 16 (the levels a shift can use)
@@ -2238,8 +2237,9 @@ __global__ __launch_bounds__(1024) void small_run_kernel(const uint8_t *__restri
   __shared__ __attribute__((aligned(16))) uint8_t win[kSmallRunMax][kHdrWin];
   __shared__ hdfs_crc32c_packet rec;
   // code, verify this packet, unsupported, first bad, bad chunks, levels,
-  // copy-out: destination offset (lo, hi), every earlier packet On and clean
-  __shared__ uint32_t ctl[9];
+  // copy-out: destination offset (lo, hi), copy it (every earlier packet On
+  // and clean, something to deliver), window [c_begin, c_begin + len)
+  __shared__ uint32_t ctl[11];
   __shared__ uint32_t sdl[kSmallRunMax], son[kSmallRunMax];
   const uint32_t tid = threadIdx.x, k = blockIdx.x;
   tt[tid] = tab[tid];
@@ -2266,7 +2266,8 @@ __global__ __launch_bounds__(1024) void small_run_kernel(const uint8_t *__restri
       const int st = grid_frame(s, len, pos, win[tid], proto, cs, ctype, r, total);
       code = st == frame::kStepMore ? kGridMore : st == frame::kStepStop ? kGridStop : total == stride ? kGridOn : kGridOff;
     }
-    sdl[tid] = (code != kGridMore && !r.error) ? uint32_t(r.data_len) : 0u;
+    uint32_t cb = 0;
+    sdl[tid] = code != kGridMore ? frame::read_avail(r, rwin != 0, client_offset, cb) : 0u;  // bytes it delivers
     son[tid] = code == kGridOn && !r.error ? 1u : 0u;
     if (pk == k) {
       const bool want = verify && code != kGridMore && !r.error && r.crc_len > 0 && ctype != HDFS_CRC32C_CSUM_NULL;
@@ -2284,15 +2285,19 @@ __global__ __launch_bounds__(1024) void small_run_kernel(const uint8_t *__restri
   }
   __syncthreads();
   if (tid == 0 && copy_dst) {
-    uint64_t off = 0;
-    uint32_t ok = 1;
+    uint64_t before = 0, at = 0;
+    uint32_t ok = 1, cb = 0, clen = 0;
     for (uint32_t t = 0; t < k; t++) {
-      off += sdl[t];
+      before += sdl[t];
       ok &= son[t];
     }
-    ctl[6] = uint32_t(off);
-    ctl[7] = uint32_t(off >> 32);
-    ctl[8] = ok && off + uint64_t(rec.data_len) <= copy_cap ? 1u : 0u;
+    (void)frame::read_avail(rec, rwin != 0, client_offset, cb);
+    frame::read_place(before, sdl[k], copy_cap, at, clen);
+    ctl[6] = uint32_t(at);
+    ctl[7] = uint32_t(at >> 32);
+    ctl[8] = ok && clen ? 1u : 0u;
+    ctl[9] = cb;
+    ctl[10] = cb + clen;
   }
   __syncthreads();
   if (ctl[1]) {
@@ -2372,19 +2377,22 @@ __global__ __launch_bounds__(1024) void small_run_kernel(const uint8_t *__restri
     }
     if (copy_dst && ctl[8] && b0 < dlen) {
       // verify + copy-out: the piece, still in registers, to its place in the
-      // de-framed payload (a 16-B store crossing the range is dropped, so the
-      // packet's last partial 16 B go byte by byte)
-      uint8_t *dst = copy_dst + ((uint64_t(ctl[7]) << 32) | ctl[6]);
-      const __amdgpu_buffer_rsrc_t rw =
-          __builtin_amdgcn_make_buffer_rsrc(dst, 0, static_cast<int>(dlen), 0x00020000);
+      // de-framed payload -- data bytes [w0, w1) of the packet (the whole
+      // payload, or the part a client read takes) at copy_dst + at + (j - w0).
+      // 16-B pieces inside the window go out whole; a piece at an edge of it
+      // (a read starting or ending inside the packet, the packet's last
+      // partial 16 B) byte by byte
+      const uint32_t w0 = ctl[9], w1 = ctl[10];
+      uint8_t *dst = copy_dst + ((uint64_t(ctl[7]) << 32) | ctl[6]) - w0;
+      const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(dst, 0, static_cast<int>(w1), 0x00020000);
 #pragma unroll
       for (uint32_t m = 0; m < 4; m++) {
         const uint32_t o = b0 + 16u * m;
-        if (o + 16u <= dlen) {
+        if (o >= w0 && o + 16u <= w1) {
           const u32x4 v = {d[4 * m], d[4 * m + 1], d[4 * m + 2], d[4 * m + 3]};
           __builtin_amdgcn_raw_buffer_store_b128(v, rw, o, 0, 0);
-        } else if (o < dlen) {
-          for (uint32_t b = o; b < dlen; b++)
+        } else if (o < w1 && o + 16u > w0) {
+          for (uint32_t b = max(o, w0); b < min(o + 16u, w1); b++)
             __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(d[(b - b0) >> 2] >> (8u * (b & 3u))), rw, b, 0, 0);
         }
       }
@@ -2410,25 +2418,27 @@ __global__ __launch_bounds__(1024) void small_run_kernel(const uint8_t *__restri
 
 hipError_t launch_small_run(const uint8_t *s, uint64_t len, uint32_t count, int proto, uint32_t cs, int ctype,
                             int verify, const uint32_t *tab, const uint32_t *pow2, uint8_t *copy_dst,
-                            uint64_t copy_cap, uint8_t *hout, uint32_t seq, hipStream_t stream) {
+                            uint64_t copy_cap, int win, int64_t client_offset, uint8_t *hout, uint32_t seq,
+                            hipStream_t stream) {
   if (!count || count > kSmallRunMax) return hipErrorInvalidValue;
   hipLaunchKernelGGL(small_run_kernel, dim3(count), dim3(1024), 0, stream, s, len, count, proto, cs, ctype, verify, tab,
-                     pow2, copy_dst, copy_cap, hout, seq);
+                     pow2, copy_dst, copy_cap, win, client_offset, hout, seq);
   return hipGetLastError();
 }
 
 hipError_t launch_frame_grid(const uint8_t *s, uint64_t len, uint64_t base, uint32_t count, int proto, uint32_t cs,
                              int ctype, int verify, uint32_t sflags, uint8_t *bm_base, uint8_t *copy_base,
-                             uint64_t copy_cap, GridBufs g, hipStream_t stream) {
+                             uint64_t copy_cap, int win, int64_t client_offset, GridBufs g, hipStream_t stream) {
   if (!count || base >= len) return hipErrorInvalidValue;
   const uint32_t nblk = (count + kGridBlock - 1) / kGridBlock;
   auto *contrib = reinterpret_cast<GridContrib *>(g.contrib);
   hipLaunchKernelGGL(frame_grid_kernel, dim3(nblk), dim3(kGridBlock), 0, stream, s, len, base, count, proto, cs,
-                     ctype, verify, g.recs, g.status, contrib, g.blk_sum, g.blk_min, g.sum, g.done);
+                     ctype, verify, win, client_offset, g.recs, g.status, contrib, g.blk_sum, g.blk_min, g.sum, g.done);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(grid_build_kernel, dim3(nblk), dim3(kGridBlock), 0, stream, s, base, count, nblk, g.recs,
-                     g.status, contrib, g.blk_sum, g.blk_min, cs, sflags, bm_base, copy_base, copy_cap, g.segs,
+                     g.status, contrib, g.blk_sum, g.blk_min, cs, sflags, bm_base, copy_base, copy_cap, win, client_offset,
+                     g.segs,
                      g.seg2pkt, g.fb, g.gctr, g.done, g.exc, g.sum, g.hsum, g.seq);
   return hipGetLastError();
 }

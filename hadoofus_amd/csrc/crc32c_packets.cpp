@@ -303,9 +303,26 @@ struct DevBatch {
   PieceLayout L;
 };
 
+// Copy-out of a device-resident verify (hdfs_crc32c_verify_packets_copy):
+// every framing-clean packet delivers frame::read_avail bytes (its whole
+// payload, or the part of it a client read window takes) to its place in
+// dst (frame::read_place), never past `cap` bytes -- the read's length, or
+// the buffer for whole payloads.
+struct CopyOut {
+  uint8_t *dst = nullptr;  // null: no copy-out
+  uint64_t cap = 0;
+  bool win = false;
+  int64_t client_offset = 0;
+};
+// Where one packet's copy goes (host-built segment tables).
+struct CopyPlace {
+  uint64_t at;
+  uint32_t w0, w1;
+};
+
 int submit_device_batch(DevCtx &c, const uint8_t *d, const std::vector<hdfs_crc32c_packet> &recs,
                         const std::vector<size_t> &vidx, size_t bi, DevBatch &b, uint32_t cs, int ctype,
-                        uint8_t *copy_dst, const std::vector<uint64_t> &vpay) {
+                        uint8_t *copy_dst, const std::vector<CopyPlace> &vpay) {
   PieceLayout &L = b.L;
   L = PieceLayout{};
   L.n = b.v1 - b.v0;
@@ -341,7 +358,12 @@ int submit_device_batch(DevCtx &c, const uint8_t *d, const std::vector<hdfs_crc3
                               const_cast<uint8_t *>(crcp), dm + L.off_bm + boff};
     int rc = fill_seg(in, HDFS_CRC32C_MODE_VERIFY, hs[v], v);
     if (rc) return rc;
-    if (copy_dst) hs[v].copy_dst = copy_dst + vpay[b.v0 + v];
+    if (copy_dst) {  // placed within the destination by the walk (never past it)
+      const CopyPlace &cp = vpay[b.v0 + v];
+      hs[v].copy_dst = cp.w1 > cp.w0 ? copy_dst + cp.at : nullptr;
+      hs[v].copy_w0 = cp.w0;
+      hs[v].copy_w1 = cp.w1;
+    }
     classify(hs[v], L.rounds, L.gtiles, L.mtiles);
     boff += (uint64_t(k.crc_len) / 4 + 7) / 8;
   }
@@ -364,18 +386,21 @@ int submit_device_batch(DevCtx &c, const uint8_t *d, const std::vector<hdfs_crc3
 // stream whose packets are not all one size.  Verifies as it goes when
 // `verify`: framing-clean packets with CRCs are submitted in batches of
 // 1 024 growing to 4 096 packets (the first launch starts early; later ones
-// amortise the launch), overlapped with the rest of the walk.  copy_dst:
-// verify + copy-out, each packet's data at copy_dst + *payload (advanced
-// by every framing-clean packet).  Caller holds c.mu.
+// amortise the launch), overlapped with the rest of the walk.  co: verify +
+// copy-out, each packet's delivered bytes placed by frame::read_place after
+// *payload bytes of earlier packets (advanced by every framing-clean
+// packet) -- inside co.cap, so a stream whose payload exceeds the buffer is
+// never written past it (the call then fails).  A client read window ends
+// the walk once no packet can deliver more.  Caller holds c.mu.
 int walk_device_stream(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs, int ctype,
                        size_t max_pkts, bool verify, std::vector<hdfs_crc32c_packet> &out, uint64_t *consumed,
-                       uint64_t pos, uint8_t *copy_dst, uint64_t *payload) {
+                       uint64_t pos, const CopyOut &co, uint64_t *payload) {
   verify = verify && ctype != HDFS_CRC32C_CSUM_NULL;
   if (verify && !c.v_stream) HIPCHK(hipStreamCreateWithFlags(&c.v_stream, hipStreamNonBlocking));
   HeaderWindows w{c, d, len, proto};
   std::vector<uint8_t> big;  // v2 headers longer than a window row
   std::vector<size_t> vidx;     // packets to verify
-  std::vector<uint64_t> vpay;   // their copy-out offsets
+  std::vector<CopyPlace> vpay;  // their copy-out placement
   std::vector<DevBatch> batches;
   size_t batch_cap = 1024, v_sub = 0;
   auto submit = [&]() -> int {
@@ -384,7 +409,7 @@ int walk_device_stream(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uin
     b.v1 = vidx.size();
     v_sub = b.v1;
     batches.push_back(b);
-    return submit_device_batch(c, d, out, vidx, batches.size() - 1, batches.back(), cs, ctype, copy_dst, vpay);
+    return submit_device_batch(c, d, out, vidx, batches.size() - 1, batches.back(), cs, ctype, co.dst, vpay);
   };
   uint64_t stride = 0;
   int rc = HDFS_CRC32C_OK;
@@ -414,9 +439,13 @@ int walk_device_stream(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uin
     const int st = frame_step(p, len - pos, pos, proto, cs, ctype, k, total);
     if (st == kStepMore) break;
     out.push_back(k);
+    uint32_t cb = 0, clen = 0;
+    const uint32_t avail = frame::read_avail(k, co.win, co.client_offset, cb);
     if (verify && !k.error && k.crc_len > 0) {
+      uint64_t at = 0;
+      frame::read_place(*payload, avail, co.cap, at, clen);
       vidx.push_back(out.size() - 1);
-      vpay.push_back(*payload);
+      vpay.push_back(CopyPlace{at, cb, cb + clen});
       if (vidx.size() - v_sub >= batch_cap) {
         const auto ts = clk::now();
         rc = submit();
@@ -425,7 +454,7 @@ int walk_device_stream(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uin
         batch_cap = std::min<size_t>(batch_cap * 2, 4096);
       }
     }
-    if (!k.error) *payload += uint64_t(k.data_len);
+    *payload += avail;
     if (st == kStepStop) {
       if (!k.error) *consumed = pos + total;
       break;
@@ -433,6 +462,10 @@ int walk_device_stream(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uin
     pos += total;
     stride = total;
     *consumed = pos;
+    // a read window is over: the read is complete, or this packet ends it
+    // (UNEXPECTED_READ_OFFSET, the last packet of the block) -- later
+    // packets are never taken (src/datanode.c:1476, 2483-2486, 2545-2546)
+    if (co.win && !k.error && (*payload >= co.cap || avail == 0 || k.last)) break;
   }
   const auto t1 = clk::now();
   if (!rc && vidx.size() > v_sub) rc = submit();
@@ -540,8 +573,8 @@ int reserve_grid(DevCtx &c, size_t si, const GridLayout &L) {
 // kernel cannot take, a packet off the grid, more packets than it covers),
 // < 0 on an engine error.
 int small_run(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs, int ctype, bool verify,
-              uint8_t *copy_dst, uint64_t copy_cap, size_t max_pkts, hdfs_crc32c_packet *dst, size_t *nout,
-              uint64_t *consumed, uint64_t *payload) {
+              const CopyOut &co, size_t max_pkts, hdfs_crc32c_packet *dst, size_t *nout, uint64_t *consumed,
+              uint64_t *payload) {
   if (!c.sr_h) {
     HIPCHK(hipHostMalloc(&c.sr_h, kSrHostBytes, hipHostMallocCoherent | hipHostMallocMapped));
     std::memset(c.sr_h, 0, kSrHostBytes);
@@ -551,7 +584,7 @@ int small_run(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
   const uint32_t seq = ++c.grid_seq;
   const int tset = ctype == HDFS_CRC32C_CSUM_CRC32 ? 1 : 0;
   HIPCHK(launch_small_run(d, len, count, proto, cs, ctype, verify ? 1 : 0, c.d_tab_main_t[tset], c.d_tab_pow2_t[tset],
-                          copy_dst, copy_cap, c.sr_hd, seq, c.stream));
+                          co.dst, co.cap, co.win ? 1 : 0, co.client_offset, c.sr_hd, seq, c.stream));
   auto word = [&](uint32_t k, int i) -> const uint32_t * {
     return reinterpret_cast<const uint32_t *>(c.sr_h + size_t(k) * kSrSlot + kGridRecBytes) + i;
   };
@@ -569,6 +602,11 @@ int small_run(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
 #endif
     }
   }
+  // every slot is published (each workgroup's sequence word is its last
+  // memory operation, so a fault of this launch cannot be followed by it);
+  // a fault of earlier work on the stream is this call's error, not the next
+  if (const hipError_t q = hipStreamQuery(c.stream); q != hipSuccess && q != hipErrorNotReady)
+    return fail(HDFS_CRC32C_EHIP, "short-run kernel: %s", hipGetErrorString(q));
   // the run: grid points up to the first that is not On (grid_build_kernel's rule)
   auto rec = [&](uint32_t k) {
     hdfs_crc32c_packet r;
@@ -602,7 +640,8 @@ int small_run(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
   if (unsup || !ended) return 0;
   for (uint32_t k = 0; k < recorded; k++) {
     dst[k] = rec(k);
-    if (!dst[k].error) pay += uint64_t(dst[k].data_len);
+    uint32_t cb = 0;
+    pay += frame::read_avail(dst[k], co.win, co.client_offset, cb);  // before the verdict is set
     if (*word(k, 2)) {
       dst[k].error = HDFS_CRC32C_ERR_DATANODE_BAD_CHECKSUM;
       dst[k].first_bad = int32_t(*word(k, 1));
@@ -616,20 +655,19 @@ int small_run(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
 }
 
 int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs, int ctype, size_t max_pkts,
-              bool verify, uint8_t *copy_dst, uint64_t copy_cap, hdfs_crc32c_packet *dst, size_t *nout,
-              uint64_t *consumed, uint64_t *payload_out) {
+              bool verify, const CopyOut &co, hdfs_crc32c_packet *dst, size_t *nout, uint64_t *consumed,
+              uint64_t *payload_out) {
   *nout = 0;
   *consumed = 0;
   verify = verify && ctype != HDFS_CRC32C_CSUM_NULL;
   if (max_pkts && len <= kSmallRunBytes) {  // verify (+ copy-out) or framing only
     uint64_t pay = 0;
-    const int r = small_run(c, d, len, proto, cs, ctype, verify, copy_dst, copy_cap, max_pkts, dst, nout, consumed,
-                            &pay);
+    const int r = small_run(c, d, len, proto, cs, ctype, verify, co, max_pkts, dst, nout, consumed, &pay);
     if (r < 0) return r;
     if (r == 1) {
-      if (copy_dst && pay > copy_cap)
+      if (co.dst && !co.win && pay > co.cap)
         return fail(HDFS_CRC32C_EINVAL, "copy-out buffer of %llu bytes is too small (%llu needed)",
-                    (unsigned long long)copy_cap, (unsigned long long)pay);
+                    (unsigned long long)co.cap, (unsigned long long)pay);
       if (payload_out) *payload_out = pay;
       return HDFS_CRC32C_OK;
     }
@@ -656,7 +694,8 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
   auto us_since = [](clk::time_point a, clk::time_point b) {
     return std::chrono::duration<double, std::micro>(b - a).count();
   };
-  while (n < max_pkts && pos < len) {
+  // (a read window that is full takes no further packets)
+  while (n < max_pkts && pos < len && !(co.win && payload >= co.cap)) {
     const uint64_t left = len - pos;
     const uint32_t count = uint32_t(std::min<uint64_t>({uint64_t(max_pkts - n), kGridMaxCount, left / 6 + 1}));
     const uint64_t bm_cap = left / 32 + count + 64;  // >= sum of ceil(chunks / 8) over the run
@@ -687,9 +726,12 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
     // framing and the segment table on c.stream; the verify of the run is
     // queued behind it right away, sized by the device-built summary (no host
     // round trip before the GPU starts verifying)
+    // copy-out: this pass fills the destination from what earlier passes
+    // delivered on, within what is left of it
+    const uint64_t done_b = std::min(payload, co.cap);
     hipError_t e = launch_frame_grid(d, len, pos, count, proto, cs, ctype, verify ? 1 : 0, sflags, dg + L.bm,
-                                     copy_dst ? copy_dst + payload : nullptr, copy_dst ? copy_cap - payload : 0, gb,
-                                     c.stream);
+                                     co.dst ? co.dst + done_b : nullptr, co.dst ? co.cap - done_b : 0, co.win ? 1 : 0,
+                                     co.client_offset, gb, c.stream);
     if (e != hipSuccess) {
       rc = fail(HDFS_CRC32C_EHIP, "device framing: %s", hipGetErrorString(e));
       break;
@@ -701,7 +743,7 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
       // rounds: at most one per 512 B of the rest of the stream
       rc = launch_verify_dyn(c, reinterpret_cast<const SegDev *>(dg + L.segs), sum, left / kRoundBytes, gtiles_ub,
                              reinterpret_cast<uint32_t *>(dg + L.fb), reinterpret_cast<unsigned long long *>(ctr + 16),
-                             ctr, c.stream, tset, copy_dst != nullptr);
+                             ctr, c.stream, tset, co.dst != nullptr);
       if (rc) break;
       auto *bad = reinterpret_cast<GridBad *>(dg + L.bad);
       __atomic_store_n(&reinterpret_cast<GridSummary *>(hg + L.h_sum2)->seq, 0u, __ATOMIC_RELEASE);
@@ -733,9 +775,9 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
     }
     GridSummary S;
     std::memcpy(&S, hsum, sizeof(S));
-    if (copy_dst && payload + S.payload > copy_cap) {
+    if (co.dst && !co.win && payload + S.payload > co.cap) {
       rc = fail(HDFS_CRC32C_EINVAL, "copy-out buffer of %llu bytes is too small (%llu needed so far)",
-                (unsigned long long)copy_cap, (unsigned long long)(payload + S.payload));
+                (unsigned long long)co.cap, (unsigned long long)(payload + S.payload));
       break;
     }
     // the pass's records, written while the verify kernel runs: predicted
@@ -778,8 +820,7 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
   const auto t1 = clk::now();
   if (!rc && fallback && n < max_pkts) {
     std::vector<hdfs_crc32c_packet> more;
-    rc = walk_device_stream(c, d, len, proto, cs, ctype, max_pkts - n, verify, more, consumed, pos, copy_dst,
-                            &payload);
+    rc = walk_device_stream(c, d, len, proto, cs, ctype, max_pkts - n, verify, more, consumed, pos, co, &payload);
     if (!rc && !more.empty()) {
       std::memcpy(dst + n, more.data(), more.size() * sizeof(hdfs_crc32c_packet));
       n += more.size();
@@ -808,9 +849,9 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
   const auto t1e = clk::now();
   if (!rc && e != hipSuccess) rc = fail(HDFS_CRC32C_EHIP, "verify: %s", hipGetErrorString(e));
   if (!rc && e2 != hipSuccess) rc = fail(HDFS_CRC32C_EHIP, "verify: %s", hipGetErrorString(e2));
-  if (!rc && copy_dst && payload > copy_cap)
+  if (!rc && co.dst && !co.win && payload > co.cap)
     rc = fail(HDFS_CRC32C_EINVAL, "copy-out buffer of %llu bytes is too small (%llu needed)",
-              (unsigned long long)copy_cap, (unsigned long long)payload);
+              (unsigned long long)co.cap, (unsigned long long)payload);
   if (rc) return rc;
   // verify verdicts: the compact list of packets with bad chunks
   for (const Pass &p : passes) {
@@ -846,10 +887,72 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
   return HDFS_CRC32C_OK;
 }
 
+// The read loop over a walked run, for a client read window
+// (_datanode_read's `while (remains_tot > 0) _recv_packet(...)`,
+// src/datanode.c:1476-1481, through _process_recv_packet and
+// _recv_packet_copy_data, :2448-2456, :2470-2549): packets are taken while
+// the read still wants bytes; an empty last packet then is BAD_LASTPACKET
+// (:2452-2454); after its CRCs are verified, a packet that starts past the
+// read (c_begin >= dataLen) is UNEXPECTED_READ_OFFSET (:2483-2486); a
+// packet delivers min(dataLen - c_begin, remains) bytes, and one flagged
+// lastPacketInBlock that leaves the read short is BAD_LASTPACKET after its
+// bytes are copied (:2545-2546).  The walk stops at the packet that
+// completes the read or raises one of these; records past it are dropped
+// (the reference never reads them).  As in the whole-payload mode, packets
+// after one with bad CRCs keep their own verdicts (the engine reports every
+// packet; the reference stops at the first): the window is a function of
+// the headers only, which is what lets the device place every packet's copy
+// before any verdict is known.  *delivered = the bytes the reference copies
+// before its loop returns an error.
+void apply_read_window(hdfs_crc32c_packet *p, size_t &n, uint64_t &consumed, const CopyOut &co,
+                       uint64_t *delivered) {
+  uint64_t remains = co.cap, got = 0;
+  bool err = false;
+  for (size_t k = 0; k < n; k++) {
+    hdfs_crc32c_packet &r = p[k];
+    const uint64_t end = r.stream_off + r.header_len + uint64_t(r.crc_len > 0 ? r.crc_len : 0) +
+                         uint64_t(r.data_len > 0 ? r.data_len : 0);
+    const bool crc_bad = r.error == HDFS_CRC32C_ERR_DATANODE_BAD_CHECKSUM;
+    if (r.error && !crc_bad) {  // framing error: the walk ended here
+      n = k + 1;
+      break;
+    }
+    bool stop = false;
+    if (r.data_len == 0) {  // the empty last packet (a non-last one is a framing error)
+      r.error = HDFS_CRC32C_ERR_DATANODE_BAD_LASTPACKET;
+      stop = true;
+    } else {
+      hdfs_crc32c_packet h = r;
+      h.error = 0;  // the window is a function of the header
+      uint32_t cb = 0;
+      const uint32_t avail = frame::read_avail(h, true, co.client_offset, cb);
+      if (avail == 0) {
+        if (!crc_bad) r.error = HDFS_CRC32C_ERR_DATANODE_UNEXPECTED_READ_OFFSET;
+        stop = true;
+      } else {
+        const uint64_t clen = std::min<uint64_t>(avail, remains);
+        remains -= clen;
+        if (!err && !crc_bad) got += clen;
+        if (r.last && remains > 0) {
+          if (!crc_bad) r.error = HDFS_CRC32C_ERR_DATANODE_BAD_LASTPACKET;
+          stop = true;
+        }
+        stop = stop || remains == 0;
+      }
+    }
+    if (r.error) err = true;
+    if (stop) {
+      n = k + 1;
+      consumed = end;
+      break;
+    }
+  }
+  if (delivered) *delivered = got;
+}
+
 int verify_packets_dev_impl(int dev, const uint8_t *stream, uint64_t len, int proto, uint32_t cs, int ctype,
                             hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts, uint64_t *consumed,
-                            bool verify, uint8_t *copy_dst = nullptr, uint64_t copy_cap = 0,
-                            uint64_t *delivered = nullptr) {
+                            bool verify, const CopyOut &co = CopyOut{}, uint64_t *delivered = nullptr) {
   DevCtx *cp = nullptr;
   int rc;
   if ((rc = ctx_init(dev, &cp))) return rc;
@@ -858,12 +961,10 @@ int verify_packets_dev_impl(int dev, const uint8_t *stream, uint64_t len, int pr
   std::lock_guard<std::mutex> lk(c.mu);
   uint64_t used = 0;
   size_t n = 0;
-  if ((rc = grid_walk(c, stream, len, proto, cs, ctype, max_pkts, verify, copy_dst, copy_cap, pkts, &n, &used,
-                      nullptr)))
-    return rc;
-  if (npkts) *npkts = n;
-  if (consumed) *consumed = used;
-  if (delivered) {  // what the reference copies out before its loop returns an error (src/datanode.c:2470-2486)
+  if ((rc = grid_walk(c, stream, len, proto, cs, ctype, max_pkts, verify, co, pkts, &n, &used, nullptr))) return rc;
+  if (co.win) {
+    apply_read_window(pkts, n, used, co, delivered);
+  } else if (delivered) {  // what the reference copies out before its loop returns an error (src/datanode.c:2470-2486)
     uint64_t b = 0;
     for (size_t i = 0; i < n; i++) {
       if (pkts[i].error) break;
@@ -871,6 +972,8 @@ int verify_packets_dev_impl(int dev, const uint8_t *stream, uint64_t len, int pr
     }
     *delivered = b;
   }
+  if (npkts) *npkts = n;
+  if (consumed) *consumed = used;
   return first_error(pkts, n);
 }
 
@@ -947,8 +1050,11 @@ int verify_packets_impl(const uint8_t *stream, uint64_t len, int proto, uint32_t
       c.k_hmeta_cap = htotal;
     }
     if ((rc = pipe_reserve(c, kGatherSlice, 512, 1))) return rc;  // copy / compute streams
-    HostRegistration reg;
-    if ((rc = reg.ensure(stream, len))) return rc;
+    // the wire bytes of the verified packets stay pinned until both streams
+    // are drained, on every return path (crc32c_hostpin.h)
+    HostPins hp({c.copy_stream, c.comp_stream});
+    const uint64_t w0 = wire_begin(recs[vidx.front()]), w1 = wire_end(recs[vidx.back()]);
+    if ((rc = hp.pin({{stream + w0, w1 - w0}}))) return rc;
     for (size_t i = 0; i < pieces.size(); i++) {
       PieceSlot &s = c.kslot[i & 1];
       if ((rc = reserve_slot(s, lay[i])) ||
@@ -956,8 +1062,7 @@ int verify_packets_impl(const uint8_t *stream, uint64_t len, int proto, uint32_t
           (rc = enqueue_piece(c, stream, lay[i], s, c.k_hmeta + hoff[i], ctype, c.copy_stream, c.comp_stream)))
         return rc;
     }
-    HIPCHK(hipStreamSynchronize(c.comp_stream));
-    HIPCHK(hipStreamSynchronize(c.copy_stream));
+    if ((rc = hp.done(HDFS_CRC32C_OK))) return rc;
     for (size_t i = 0; i < pieces.size(); i++)
       finish_piece(recs.data(), vidx.data() + pieces[i].first, lay[i], c.k_hmeta + hoff[i]);
   }
@@ -1111,7 +1216,10 @@ void session_free(hdfs_crc32c_session *s) {
   if (s->copy) (void)hipStreamSynchronize(s->copy);
   for (auto &d : s->dslot) release_slot(d);
   for (auto p : s->hslot)
-    if (p) (void)hipHostFree(p);
+    if (p) {
+      pins().remove_owned(p);
+      (void)hipHostFree(p);
+    }
   for (auto p : s->hmeta)
     if (p) (void)hipHostFree(p);
   for (auto e : s->hdone)
@@ -1192,8 +1300,9 @@ int hdfs_crc32c_verify_packets(const void *stream, uint64_t len, int proto, uint
 }
 
 int hdfs_crc32c_verify_packets_copy(const void *stream, uint64_t len, int proto, uint32_t chunk_size, int ctype,
-                                    hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts, uint64_t *consumed,
-                                    void *dst, uint64_t dst_cap, uint64_t *delivered) {
+                                    int64_t client_offset, int64_t read_len, hdfs_crc32c_packet *pkts,
+                                    size_t max_pkts, size_t *npkts, uint64_t *consumed, void *dst, uint64_t dst_cap,
+                                    uint64_t *delivered) {
   if (npkts) *npkts = 0;
   if (consumed) *consumed = 0;
   if (delivered) *delivered = 0;
@@ -1202,6 +1311,20 @@ int hdfs_crc32c_verify_packets_copy(const void *stream, uint64_t len, int proto,
   if (rc) return rc;
   if (ctype == HDFS_CRC32C_CSUM_NULL)
     return fail(HDFS_CRC32C_EINVAL, "verify + copy-out needs CRC32 or CRC32C (src/datanode.c:2470-2486)");
+  CopyOut co;
+  co.dst = static_cast<uint8_t *>(dst);
+  co.cap = dst_cap;
+  if (read_len != HDFS_CRC32C_READ_ALL) {  // a client read (src/datanode.c:1363-1377: bloff >= 0, len > 0)
+    if (read_len <= 0 || client_offset < 0)
+      return fail(HDFS_CRC32C_EINVAL, "read window: offset %lld, length %lld", (long long)client_offset,
+                  (long long)read_len);
+    if (dst_cap < uint64_t(read_len))
+      return fail(HDFS_CRC32C_EINVAL, "copy-out buffer of %llu bytes is smaller than the read (%lld)",
+                  (unsigned long long)dst_cap, (long long)read_len);
+    co.win = true;
+    co.client_offset = client_offset;
+    co.cap = uint64_t(read_len);
+  }
   if (!len) return HDFS_CRC32C_OK;
   if (!stream) return fail(HDFS_CRC32C_EINVAL, "null stream");
   const int dev = stream_device(stream);
@@ -1209,7 +1332,7 @@ int hdfs_crc32c_verify_packets_copy(const void *stream, uint64_t len, int proto,
   if (!dst || stream_device(dst) != dev)
     return fail(HDFS_CRC32C_EINVAL, "copy-out destination must be device memory of the stream's device");
   return verify_packets_dev_impl(dev, static_cast<const uint8_t *>(stream), len, proto, chunk_size, ctype, pkts,
-                                 max_pkts, npkts, consumed, true, static_cast<uint8_t *>(dst), dst_cap, delivered);
+                                 max_pkts, npkts, consumed, true, co, delivered);
 }
 
 int hdfs_crc32c_compose_packets(const void *data, uint64_t len, int64_t offset_in_block, int64_t seqno, int proto,
@@ -1323,6 +1446,7 @@ int hdfs_crc32c_session_create(hdfs_crc32c_session **out, int proto, uint32_t ch
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&s->comp, hipStreamNonBlocking);
   for (size_t i = 0; i < nslots && e == hipSuccess; i++) {
     e = hipHostMalloc(&s->hslot[i], slot_bytes, hipHostMallocDefault);
+    if (e == hipSuccess) pins().add_owned(s->hslot[i], slot_bytes);  // the caller receives into it
     if (e == hipSuccess) e = hipEventCreateWithFlags(&s->hdone[i], hipEventDisableTiming);
   }
   if (e != hipSuccess) {

@@ -53,17 +53,19 @@ def workload_blocks(config, rank, world, blocks=None):
 
 
 def check_distinct_devices(infos):
-    """infos: one dict per rank with 'rank' and 'pci_bus_id' (the GPU the
-    rank's engine is bound to).  Raises if two ranks share a GPU -- e.g. every
-    rank silently landing on device 0."""
+    """infos: one dict per rank with 'rank', 'pci_bus_id' (the GPU the rank's
+    engine is bound to) and 'host' (socket.gethostname(); ranks on different
+    nodes usually report the same bus ids).  Raises if two ranks of one host
+    share a GPU -- e.g. every rank silently landing on device 0."""
     seen = {}
     for inf in infos:
         bus = inf["pci_bus_id"]
         if not bus:
             raise RuntimeError(f"rank {inf['rank']} reported no PCI bus id")
-        if bus in seen:
-            raise RuntimeError(f"ranks {seen[bus]} and {inf['rank']} share GPU {bus}")
-        seen[bus] = inf["rank"]
+        key = (inf.get("host", ""), bus)
+        if key in seen:
+            raise RuntimeError(f"ranks {seen[key]} and {inf['rank']} share GPU {bus} on host {key[0]!r}")
+        seen[key] = inf["rank"]
     return len(seen)
 
 

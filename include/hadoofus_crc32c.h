@@ -53,7 +53,9 @@ uint32_t _hdfs_sw_crc32c(uint32_t crc, const void *buf, unsigned len);
 #define HDFS_CRC32C_ERR_DATANODE_PACKET_SIZE 25
 #define HDFS_CRC32C_ERR_DATANODE_CRC_LEN 26
 #define HDFS_CRC32C_ERR_DATANODE_UNEXPECTED_CRC_LEN 27
+#define HDFS_CRC32C_ERR_DATANODE_UNEXPECTED_READ_OFFSET 28
 #define HDFS_CRC32C_ERR_DATANODE_BAD_CHECKSUM 29
+#define HDFS_CRC32C_ERR_DATANODE_BAD_LASTPACKET 32
 
 /* enum hdfs_checksum_type (include/objects.h:169-175) */
 #define HDFS_CRC32C_CSUM_NULL 0
@@ -205,18 +207,36 @@ int hdfs_crc32c_verify_packets(const void *stream, uint64_t len, int proto, uint
 
 /* Verify + copy-out of a DEVICE-resident packet stream (GPU-direct
  * receive): hdfs_crc32c_verify_packets, and in the same pass over HBM the
- * data of every framing-clean packet is written, de-framed and in stream
- * order, to the device buffer dst (dst_cap bytes) -- the read path's
- * _recv_packet_copy_data (src/datanode.c:2496-2553) fused into the verify
- * kernel: each payload byte is read once and written once.  *delivered =
- * payload bytes of the packets before the first packet with an error, i.e.
- * what the reference copies to the caller before its packet loop returns
- * that error (src/datanode.c:2470-2486); bytes of dst past *delivered are
- * unspecified.  ctype must be CRC32 or CRC32C.  Returns as verify_packets;
- * EINVAL if dst is too small for the framed payload. */
+ * packets' data is written, de-framed and in stream order, to the device
+ * buffer dst (dst_cap bytes) -- the read path's _process_recv_packet /
+ * _recv_packet_copy_data (src/datanode.c:2470-2553) fused into the verify
+ * kernel: each payload byte is read once and written once.
+ *
+ * read_len = HDFS_CRC32C_READ_ALL: every framing-clean packet's whole
+ *   payload; *delivered = payload bytes of the packets before the first
+ *   packet with an error; EINVAL if dst is too small for the framed payload.
+ * read_len > 0: a client read of the block's bytes [client_offset,
+ *   client_offset + read_len) (hdfs_datanode_read's bloff / len,
+ *   src/datanode.c:1363-1377; dst_cap >= read_len).  Packets are taken while
+ *   the read wants bytes (src/datanode.c:1476): a packet that starts before
+ *   client_offset delivers from c_begin = client_offset - offsetInBlock on,
+ *   and c_begin >= dataLen is HDFS_CRC32C_ERR_DATANODE_UNEXPECTED_READ_OFFSET
+ *   (:2478-2486); a packet delivers at most what is left of the read; a
+ *   lastPacketInBlock packet that leaves the read short, or an empty last
+ *   packet before it is complete, is HDFS_CRC32C_ERR_DATANODE_BAD_LASTPACKET
+ *   (:2452-2454, :2545-2546).  The walk ends with the packet that completes
+ *   the read or raises one of those; later packets are not returned.
+ *   *delivered = the bytes the reference copies to the caller before its
+ *   loop returns an error (a BAD_LASTPACKET packet's own bytes included).
+ * Packets after one with bad CRCs are still verified and reported (as in
+ * hdfs_crc32c_verify_packets); bytes of dst past *delivered are unspecified,
+ * bytes past dst_cap (or read_len) are never written.  ctype must be CRC32
+ * or CRC32C.  Returns the first error in stream order, 0, or a negative
+ * status. */
+#define HDFS_CRC32C_READ_ALL (-1)
 int hdfs_crc32c_verify_packets_copy(const void *stream, uint64_t len, int proto, uint32_t chunk_size,
-    int ctype, hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts, uint64_t *consumed,
-    void *dst, uint64_t dst_cap, uint64_t *delivered);
+    int ctype, int64_t client_offset, int64_t read_len, hdfs_crc32c_packet *pkts, size_t max_pkts,
+    size_t *npkts, uint64_t *consumed, void *dst, uint64_t dst_cap, uint64_t *delivered);
 
 /* ---- write path: outgoing data packets ---------------------------------- */
 /* One outgoing data packet, as _send_packet sizes it and
@@ -296,6 +316,8 @@ int hdfs_crc32c_verify_host(const void *data, uint64_t len, uint32_t chunk_size,
     uint64_t *first_bad, uint64_t *mismatches);
 /* Pinned (page-locked) host memory for zero-copy-staging pipelines. */
 int hdfs_crc32c_host_alloc(void **p, uint64_t bytes);
+/* Only for blocks from hdfs_crc32c_host_alloc (EINVAL otherwise): the engine
+ * keeps them in its registry of pinned memory (DMA-ed in place). */
 int hdfs_crc32c_host_free(void *p);
 
 /* ---- resident mailbox for the synchronous small calls ------------------- */
@@ -311,6 +333,11 @@ int hdfs_crc32c_host_free(void *p);
  * While a mailbox is open the engine's bulk kernels use one CU fewer, and a
  * device-wide synchronisation (hipDeviceSynchronize, torch.cuda.synchronize)
  * waits for the resident kernel's idle exit: synchronise streams instead.
+ * The same holds for calls that free or re-allocate device or pinned memory
+ * (hdfs_crc32c_dev_free, hdfs_crc32c_host_free, and an engine call whose
+ * internal scratch has to grow): the runtime may wait for every stream of
+ * the device there, i.e. up to idle_ms for the resident kernel.  Allocate
+ * before opening a mailbox, or close it around re-allocations.
  * One mailbox per device (EBUSY-style HDFS_CRC32C_EINVAL for a second). */
 typedef struct hdfs_crc32c_mailbox hdfs_crc32c_mailbox;
 int hdfs_crc32c_mailbox_create(hdfs_crc32c_mailbox **mb, uint32_t idle_ms);
@@ -336,7 +363,8 @@ int hdfs_crc32c_corrupt(void *dptr, uint64_t len, uint32_t chunk, uint64_t chunk
  * measured with HIP events (ms per execution). */
 int hdfs_crc32c_plan_time(hdfs_crc32c_plan *plan, void *stream, int iters, double *ms_per_iter);
 /* hipDeviceSynchronize on the engine's device (with a mailbox open: the
- * engine's streams and the NULL stream, not the resident kernel). */
+ * engine's streams, the NULL stream and every stream hdfs_crc32c_stream_create
+ * handed out, not the resident kernel). */
 int hdfs_crc32c_device_sync(void);
 
 #ifdef __cplusplus

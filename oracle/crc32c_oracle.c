@@ -18,6 +18,9 @@
  *                            :214-381 (3-way interleaved crc32q loop)
  *   oracle_verify_crcdata <- src/datanode.c:2931-2963 (_verify_crcdata) and
  *                            the framing check of src/datanode.c:2438-2446
+ *   oracle_read_packets   <- src/datanode.c:1476-1481 (read loop), :2428-2549
+ *                            (_process_recv_packet read window +
+ *                            _recv_packet_copy_data)
  *   oracle_compose_crcs   <- src/datanode.c:2814-2860 (write-path CRC loop,
  *                            chained across iovec fragments)
  *   oracle_compose_packets <- src/datanode.c:2583-2609 (_send_packet packet
@@ -566,6 +569,69 @@ static void verify_one(const uint8_t *crcs, const uint8_t *data, int32_t dlen, u
 	}
 }
 
+/* One packet of the walk at stream offset pos (src/datanode.c:2345-2456):
+ * header decode (v1 / v2) and the framing checks of _process_recv_packet.
+ * Returns 2 (incomplete: nothing recorded), 1 (recorded and the walk ends:
+ * framing error, or the empty last packet -- *total = its header bytes) or
+ * 0 (a complete packet of *total wire bytes). */
+static int frame_one(const uint8_t *s, uint64_t len, uint64_t pos, int proto, uint32_t cs, int ctype,
+    struct oracle_packet *k, uint64_t *total)
+{
+	memset(k, 0, sizeof(*k));
+	k->stream_off = pos;
+	k->first_bad = -1;
+	const uint8_t *p = s + pos;
+	uint64_t rem = len - pos;
+	int64_t plen, dlen;
+	if (proto == 1) { /* v1: src/datanode.c:2363-2384 */
+		if (rem < 25)
+			return 2;
+		plen = rd_be(p, 4);
+		k->offset_in_block = rd_be(p + 4, 8);
+		k->seqno = rd_be(p + 12, 8);
+		k->last = rd_be(p + 20, 1) != 0;
+		dlen = rd_be(p + 21, 4);
+		k->header_len = 25;
+	} else { /* v2: src/datanode.c:2387-2418 */
+		if (rem < 6)
+			return 2;
+		plen = rd_be(p, 4);
+		uint16_t hlen = (uint16_t)rd_be(p + 4, 2);
+		if (rem < 6u + hlen)
+			return 2;
+		k->header_len = 6u + hlen;
+		int32_t d32 = 0;
+		if (pb_header(p + 6, hlen, &k->offset_in_block, &k->seqno, &k->last, &d32, &k->sync)) {
+			k->offset_in_block = k->seqno = 0;
+			k->last = k->sync = 0;
+			k->error = ORACLE_ERR_INVALID_PACKETHEADERPROTO;
+			return 1;
+		}
+		dlen = d32;
+	}
+	/* _process_recv_packet: src/datanode.c:2428-2446 */
+	int64_t crcdlen = plen - dlen - 4;
+	const int64_t onegb = 1024 * 1024 * 1024;
+	k->data_len = (int32_t)dlen;
+	k->crc_len = (int32_t)crcdlen;
+	if (plen < 0 || dlen < 0 || dlen > onegb || plen > onegb || crcdlen < 0)
+		k->error = ORACLE_ERR_PACKET_SIZE;
+	else if (ctype != 0 && crcdlen != ((dlen + cs - 1) / cs) * 4)
+		k->error = ORACLE_ERR_CRC_LEN;
+	else if (ctype == 0 && crcdlen > 0)
+		k->error = ORACLE_ERR_UNEXPECTED_CRC_LEN;
+	if (k->error)
+		return 1;
+	if (dlen == 0) { /* src/datanode.c:2448-2456 */
+		if (!k->last)
+			k->error = ORACLE_ERR_PACKET_SIZE;
+		*total = k->header_len;
+		return 1;
+	}
+	*total = k->header_len + (uint64_t)crcdlen + (uint64_t)dlen;
+	return rem < *total ? 2 : 0;
+}
+
 /* Returns the first packet error in stream order (0 if none); *npkts
  * records and *consumed bytes as documented for hdfs_crc32c_verify_packets. */
 int oracle_verify_packets(const uint8_t *s, uint64_t len, int proto, uint32_t cs, int ctype,
@@ -576,72 +642,108 @@ int oracle_verify_packets(const uint8_t *s, uint64_t len, int proto, uint32_t cs
 	*consumed = 0;
 	while (n < max_pkts) {
 		struct oracle_packet k;
-		memset(&k, 0, sizeof(k));
-		k.stream_off = pos;
-		k.first_bad = -1;
-		const uint8_t *p = s + pos;
-		uint64_t rem = len - pos;
-		int64_t plen, dlen;
-		if (proto == 1) { /* v1: src/datanode.c:2363-2384 */
-			if (rem < 25)
-				break;
-			plen = rd_be(p, 4);
-			k.offset_in_block = rd_be(p + 4, 8);
-			k.seqno = rd_be(p + 12, 8);
-			k.last = rd_be(p + 20, 1) != 0;
-			dlen = rd_be(p + 21, 4);
-			k.header_len = 25;
-		} else { /* v2: src/datanode.c:2387-2418 */
-			if (rem < 6)
-				break;
-			plen = rd_be(p, 4);
-			uint16_t hlen = (uint16_t)rd_be(p + 4, 2);
-			if (rem < 6u + hlen)
-				break;
-			k.header_len = 6u + hlen;
-			int32_t d32 = 0;
-			if (pb_header(p + 6, hlen, &k.offset_in_block, &k.seqno, &k.last, &d32, &k.sync)) {
-				k.offset_in_block = k.seqno = 0;
-				k.last = k.sync = 0;
-				k.error = ORACLE_ERR_INVALID_PACKETHEADERPROTO;
-				out[n++] = k;
-				break;
-			}
-			dlen = d32;
-		}
-		/* _process_recv_packet: src/datanode.c:2428-2446 */
-		int64_t crcdlen = plen - dlen - 4;
-		const int64_t onegb = 1024 * 1024 * 1024;
-		k.data_len = (int32_t)dlen;
-		k.crc_len = (int32_t)crcdlen;
-		if (plen < 0 || dlen < 0 || dlen > onegb || plen > onegb || crcdlen < 0)
-			k.error = ORACLE_ERR_PACKET_SIZE;
-		else if (ctype != 0 && crcdlen != ((dlen + cs - 1) / cs) * 4)
-			k.error = ORACLE_ERR_CRC_LEN;
-		else if (ctype == 0 && crcdlen > 0)
-			k.error = ORACLE_ERR_UNEXPECTED_CRC_LEN;
-		if (k.error) {
+		uint64_t total = 0;
+		const int st = frame_one(s, len, pos, proto, cs, ctype, &k, &total);
+		if (st == 2)
+			break;
+		if (st == 1) {
+			if (!k.error)
+				*consumed = pos + total;
 			out[n++] = k;
 			break;
 		}
-		if (dlen == 0) { /* src/datanode.c:2448-2456 */
-			if (!k.last)
-				k.error = ORACLE_ERR_PACKET_SIZE;
-			else
-				*consumed = pos + k.header_len;
-			out[n++] = k;
-			break;
-		}
-		uint64_t total = k.header_len + (uint64_t)crcdlen + (uint64_t)dlen;
-		if (rem < total)
-			break;
-		if (do_verify && crcdlen > 0)
-			verify_one(p + k.header_len, p + k.header_len + crcdlen, (int32_t)dlen, cs, ctype, &k);
+		if (do_verify && k.crc_len > 0)
+			verify_one(s + pos + k.header_len, s + pos + k.header_len + k.crc_len, k.data_len, cs, ctype, &k);
 		out[n++] = k;
 		pos += total;
 		*consumed = pos;
 	}
 	*npkts = n;
+	for (size_t i = 0; i < n; i++)
+		if (out[i].error)
+			return out[i].error;
+	return 0;
+}
+
+/* A client read over a packet stream: _datanode_read's loop
+ * `while (remains_tot > 0) _recv_packet(...)` (src/datanode.c:1476-1481)
+ * through _process_recv_packet and _recv_packet_copy_data
+ * (src/datanode.c:2428-2549) for the block bytes [client_offset,
+ * client_offset + read_len): an empty last packet while bytes are still
+ * wanted is BAD_LASTPACKET (:2452-2454); after the packet's CRCs are
+ * verified, c_begin = client_offset - offsetInBlock (0 when the packet
+ * starts later) >= dataLen is UNEXPECTED_READ_OFFSET (:2478-2486); the
+ * packet then gives min(dataLen - c_begin, remains) bytes from c_begin on
+ * (:2488, :2527-2540), and a lastPacketInBlock packet that leaves the read
+ * short is BAD_LASTPACKET (:2545-2546).  The loop ends when the read is
+ * complete or at one of those errors.  As the engine's packet API does, a
+ * packet with bad CRCs does not end the walk (its verdict is recorded, its
+ * bytes and every later packet's are not delivered: the reference returns
+ * there); c_begin is computed in 64 bits (the reference's int32_t differs
+ * only for client_offset - offsetInBlock >= 2^31).  dst receives the
+ * delivered bytes; returns the first error in stream order. */
+#define ORACLE_ERR_UNEXPECTED_READ_OFFSET 28 /* include/hadoofus/objects.h:91 */
+#define ORACLE_ERR_BAD_LASTPACKET 32        /* include/hadoofus/objects.h:98 */
+int oracle_read_packets(const uint8_t *s, uint64_t len, int proto, uint32_t cs, int ctype,
+    int64_t client_offset, int64_t read_len, struct oracle_packet *out, size_t max_pkts, size_t *npkts,
+    uint64_t *consumed, uint8_t *dst, uint64_t *delivered)
+{
+	size_t n = 0;
+	uint64_t pos = 0, got = 0;
+	int64_t remains = read_len;
+	int failed = 0;
+	*consumed = 0;
+	while (n < max_pkts && remains > 0) {
+		struct oracle_packet k;
+		uint64_t total = 0;
+		const int st = frame_one(s, len, pos, proto, cs, ctype, &k, &total);
+		if (st == 2)
+			break;
+		if (st == 1) {
+			if (!k.error) { /* the empty last packet: the read wanted more */
+				k.error = ORACLE_ERR_BAD_LASTPACKET;
+				*consumed = pos + total;
+			}
+			out[n++] = k;
+			break;
+		}
+		const uint8_t *crcs = s + pos + k.header_len, *data = crcs + k.crc_len;
+		if (k.crc_len > 0)
+			verify_one(crcs, data, k.data_len, cs, ctype, &k);
+		const int bad = k.error != 0;
+		int stop = 0;
+		int64_t c_begin = 0;
+		if (k.offset_in_block < client_offset) {
+			const uint64_t d = (uint64_t)client_offset - (uint64_t)k.offset_in_block;
+			c_begin = d >= (uint64_t)k.data_len ? k.data_len : (int64_t)d;
+		}
+		if (c_begin >= k.data_len) {
+			if (!bad)
+				k.error = ORACLE_ERR_UNEXPECTED_READ_OFFSET;
+			stop = 1;
+		} else {
+			const int64_t c_len = k.data_len - c_begin < remains ? k.data_len - c_begin : remains;
+			if (!bad && !failed) {
+				memcpy(dst + got, data + c_begin, (size_t)c_len);
+				got += (uint64_t)c_len;
+			}
+			remains -= c_len;
+			if (k.last && remains > 0) {
+				if (!bad)
+					k.error = ORACLE_ERR_BAD_LASTPACKET;
+				stop = 1;
+			}
+		}
+		if (k.error)
+			failed = 1;
+		out[n++] = k;
+		pos += total;
+		*consumed = pos;
+		if (stop)
+			break;
+	}
+	*npkts = n;
+	*delivered = got;
 	for (size_t i = 0; i < n; i++)
 		if (out[i].error)
 			return out[i].error;

@@ -6,10 +6,15 @@
  * corrupts one chunk, then verifies it (1) in one hdfs_crc32c_verify_packets
  * call and (2) through a streaming session fed in odd-sized "socket reads";
  * then (3) composes the packets of one write (hdfs_crc32c_compose_packets)
- * and reads them back through the verifier.
+ * and reads them back through the verifier; (4) uploads the stream to the
+ * GPU and reads two client windows out of it with the fused verify +
+ * copy-out (hdfs_crc32c_verify_packets_copy: c_begin, remains_tot,
+ * src/datanode.c:2478-2549); (5) maps an engine failure the way a datanode
+ * must -- an I/O error, never a checksum error.
  * Prints "0 failures" on success.  Test infrastructure (tests/test_abi.py
  * links it on CPU, tests/test_packets.py runs it on the GPU).
  */
+#include <errno.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -48,6 +53,29 @@ static size_t put_header(uint8_t *p, int64_t off, int64_t seq, int last, int32_t
 	p[n++] = 0x18; p[n++] = (uint8_t)(last != 0);
 	p[n++] = 0x25; memcpy(p + n, &dlen, 4); n += 4;
 	return n;
+}
+
+/* The datanode's mapping of an engine return code:
+ * > 0 is the reference's own hdfs_error_numeric (error_from_hdfs), < 0 an
+ * engine failure, which becomes an errno-kind error (error_from_errno(EIO))
+ * -- never HDFS_ERR_DATANODE_BAD_CHECKSUM, which would make
+ * _compose_client_read_status report ERROR_CHECKSUM for a healthy block
+ * (src/datanode.c:1012-1013).  Returned here as {kind, value}. */
+struct dn_error {
+	int kind; /* 0 success, 1 hdfs error number, 2 errno */
+	int num;
+};
+static struct dn_error map_engine_rc(int rc)
+{
+	struct dn_error e = { 0, 0 };
+	if (rc > 0) {
+		e.kind = 1;
+		e.num = rc;
+	} else if (rc < 0) {
+		e.kind = 2;
+		e.num = EIO;
+	}
+	return e;
 }
 
 int main(void)
@@ -152,6 +180,51 @@ int main(void)
 		free(opk);
 		free(hdr);
 		free(w);
+	}
+	/* (4) the stream in device memory (GPU-direct receive), two client reads
+	 * through the fused verify + copy-out */
+	{
+		void *dstream = NULL, *duser = NULL;
+		const uint64_t ucap = 8 * DLEN;
+		uint8_t *back = malloc(ucap);
+		check(hdfs_crc32c_dev_alloc(&dstream, total) == 0 && hdfs_crc32c_dev_alloc(&duser, ucap) == 0, "dev_alloc");
+		check(hdfs_crc32c_memcpy(dstream, s, total, 0) == 0, "upload");
+		uint64_t delivered = 0;
+		/* bloff = 8 * DLEN + 5, len = 2 * DLEN: the server starts at packet 8;
+		 * its first 5 bytes are skipped, packet 10 gives 5 bytes, the read ends */
+		rc = hdfs_crc32c_verify_packets_copy((uint8_t *)dstream + 8 * pk, total - 8 * pk, HDFS_CRC32C_PROTO_V2, CS,
+		    HDFS_CRC32C_CSUM_CRC32C, 8 * (int64_t)DLEN + 5, 2 * (int64_t)DLEN, rec, NPK + 1, &n, &used, duser,
+		    ucap, &delivered);
+		check(rc == 0 && n == 3 && delivered == 2 * DLEN && used == 3 * pk, "read window: clean read");
+		check(hdfs_crc32c_memcpy(back, duser, delivered, 1) == 0, "download");
+		for (size_t k = 0, at = 0; k < 3; k++) {
+			const size_t skip = k == 0 ? 5 : 0, take = k == 2 ? 5 : DLEN - skip;
+			check(memcmp(back + at, s + (8 + k) * pk + 31 + crclen + skip, take) == 0, "read window bytes");
+			at += take;
+		}
+		/* bloff = 3 * DLEN + 1000 over packets 3.. with packet 7 corrupt: the
+		 * read gets packets 3..6 (the first from byte 1000 on) and then
+		 * BAD_CHECKSUM; the window still ends in packet 8 */
+		rc = hdfs_crc32c_verify_packets_copy((uint8_t *)dstream + 3 * pk, total - 3 * pk, HDFS_CRC32C_PROTO_V2, CS,
+		    HDFS_CRC32C_CSUM_CRC32C, 3 * (int64_t)DLEN + 1000, 5 * (int64_t)DLEN + 777, rec, NPK + 1, &n, &used,
+		    duser, ucap, &delivered);
+		check(rc == HDFS_CRC32C_ERR_DATANODE_BAD_CHECKSUM && n == 6 && rec[4].first_bad == 3 &&
+		    delivered == 4 * DLEN - 1000, "read window: bad packet");
+		check(map_engine_rc(rc).kind == 1 && map_engine_rc(rc).num == HDFS_CRC32C_ERR_DATANODE_BAD_CHECKSUM,
+		    "checksum error maps to the reference's error");
+		hdfs_crc32c_dev_free(duser);
+		hdfs_crc32c_dev_free(dstream);
+		free(back);
+	}
+
+	/* (5) an engine failure (here: a host buffer where device memory is
+	 * required) is an I/O error for the datanode, not a checksum error */
+	{
+		uint64_t delivered = 0;
+		rc = hdfs_crc32c_verify_packets_copy(s, total, HDFS_CRC32C_PROTO_V2, CS, HDFS_CRC32C_CSUM_CRC32C, 0,
+		    HDFS_CRC32C_READ_ALL, rec, NPK + 1, &n, &used, data, DLEN, &delivered);
+		const struct dn_error e = map_engine_rc(rc);
+		check(rc == HDFS_CRC32C_EINVAL && e.kind == 2 && e.num == EIO, "engine failure -> EIO");
 	}
 	printf("%d failures\n", failures);
 	free(s);

@@ -76,13 +76,15 @@ def assemble(parts):
 
 
 def build_stream(crc32c, proto, cs, ctype, dlens, seed=0, corrupt=(), last_empty=True, sync_every=0,
-                 seqnos=None, offset_skew=None):
+                 seqnos=None, offset_skew=None, offset0=0, last_flag=None):
     """A clean stream of packets with the given data lengths (the last one
     flagged lastPacketInBlock unless last_empty adds the v2-style trailing
     empty packet).  corrupt: iterable of (packet, chunk) -> flip one bit of
     that chunk after its CRC is computed.  seqnos: header seqno per packet
     (default k); offset_skew: {packet: bytes added to its offsetInBlock} --
-    header fields off the regular progression, same wire sizes.  Returns
+    header fields off the regular progression, same wire sizes.  offset0:
+    offsetInBlock of the first packet (a read from inside a block);
+    last_flag: packet index flagged lastPacketInBlock instead.  Returns
     (stream bytes, expected per-packet bad chunk lists)."""
     out = []
     bad = {}
@@ -95,9 +97,9 @@ def build_stream(crc32c, proto, cs, ctype, dlens, seed=0, corrupt=(), last_empty
         for ch in bad.get(k, []):
             clen = min(cs, dl - ch * cs)
             d[ch * cs + (k * 7919 + ch) % clen] ^= np.uint8(1 << (ch % 8))
-        last = (k == len(dlens) - 1) and not last_empty
+        last = (k == len(dlens) - 1) and not last_empty if last_flag is None else k == last_flag
         seq = k if seqnos is None else seqnos[k]
-        ho = off + (offset_skew or {}).get(k, 0)
+        ho = offset0 + off + (offset_skew or {}).get(k, 0)
         if proto == 1:
             out.append(frame_v1(ho, seq, last, crcs, d.tobytes()))
         else:
@@ -107,7 +109,7 @@ def build_stream(crc32c, proto, cs, ctype, dlens, seed=0, corrupt=(), last_empty
     if last_empty:
         k = len(dlens)
         if proto == 1:
-            out.append(frame_v1(off, k, True, b"", b""))
+            out.append(frame_v1(offset0 + off, k, True, b"", b""))
         else:
-            out.append(frame_v2(header_v2(off, k, True, 0), b"", b""))
+            out.append(frame_v2(header_v2(offset0 + off, k, True, 0), b"", b""))
     return b"".join(out), {k: sorted(set(v)) for k, v in bad.items()}

@@ -30,7 +30,7 @@ def _worker(rank, world, port, q, config="C3", dup=False):
     # the device report bench.py gathers (a fake bus id per local rank; dup:
     # every rank claims GPU 0, which rank 0 must refuse)
     infos = col.gather({"rank": rank, "local_rank": rank, "device": 0 if dup else rank,
-                        "pci_bus_id": f"0000:{(0 if dup else rank) + 0x11:02x}:00.0"})
+                        "pci_bus_id": f"0000:{(0 if dup else rank) + 0x11:02x}:00.0", "host": socket.gethostname()})
     try:
         ndev = shard.check_distinct_devices(infos)
     except RuntimeError as e:
@@ -120,3 +120,9 @@ def test_check_distinct_devices_unit():
         shard.check_distinct_devices([{"rank": 0, "pci_bus_id": "x"}, {"rank": 1, "pci_bus_id": "x"}])
     with pytest.raises(RuntimeError):
         shard.check_distinct_devices([{"rank": 0, "pci_bus_id": ""}])
+    # multi-node: the same bus id on two hosts is two GPUs, on one host it is one
+    two_nodes = [{"rank": r, "host": f"node{r // 8}", "pci_bus_id": f"0000:{r % 8 + 0x11:02x}:00.0"}
+                 for r in range(16)]
+    assert shard.check_distinct_devices(two_nodes) == 16
+    with pytest.raises(RuntimeError):
+        shard.check_distinct_devices(two_nodes + [{"rank": 16, "host": "node1", "pci_bus_id": "0000:11:00.0"}])

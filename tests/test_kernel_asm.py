@@ -35,7 +35,10 @@ def release_asm(tmp_path_factory):
 
 
 def round_waits(lines):
-    """{tiled kernel symbol: [N of every vmcnt(N) wait that precedes a transpose]}"""
+    """{tiled kernel symbol: [N of every vmcnt(N) wait that precedes the first
+    use of a round's data]}: the permlane transpose, or in the verify +
+    copy-out kernels of aligned data the copy-out's 1 KiB stores of the
+    loaded registers, which come first."""
     name, res, kernels = None, {}, set()
     for i, line in enumerate(lines):
         m = re.match(r"^(_ZN11hdfs_crc32c\w*crc32c_tiles_kernel\w+):", line)
@@ -48,7 +51,7 @@ def round_waits(lines):
         m = re.search(r"s_waitcnt vmcnt\((\d+)\)", line)
         if m and name:
             nxt = [x for x in lines[i + 1:i + 12] if x.strip() and not x.strip().startswith(";")][:6]
-            if any("v_permlane16_swap" in x for x in nxt):
+            if any("v_permlane16_swap" in x or "buffer_store_dwordx4" in x for x in nxt):
                 res.setdefault(name, []).append(int(m.group(1)))
     return kernels, res
 
@@ -68,6 +71,14 @@ def test_round_wait_check_flags_a_drained_pipeline():
              "\tv_permlane16_swap_b32_e32 v6, v2", "\ts_endpgm"]
     kernels, waits = round_waits(lines)
     assert min(waits[next(iter(kernels))]) < MIN_OUTSTANDING
+
+
+def test_product_epilogue_has_no_diagnostic_branches():
+    # the store-policy experiments live in the diagnostic build's epilogue
+    # (crc32c_diag_ep.h); the product kernel source compares no policy
+    src = open(os.path.join(CSRC, "crc32c_kernels.hip")).read()
+    code = "\n".join(line.split("//")[0] for line in src.splitlines())
+    assert "store_policy ==" not in code and "kDiag && L." not in code
 
 
 def test_no_noreturn_trap_in_kernels():

@@ -439,3 +439,160 @@ def test_gpu_device_stream_short_runs(engine, oracle, proto, cs, ctype):
                 dstb.free()
                 keep.free()
             assert engine.verify_packets(s, proto, cs, ctype) == want
+
+
+# --- client read windows (hdfs_datanode_read's bloff / len) ------------------
+# The reference's read loop over a packet stream (src/datanode.c:1476-1481,
+# 2448-2456, 2478-2549).  The reference holds no packet fixtures (its read
+# tests need a live cluster): the expectations below follow from the
+# construction, the oracle restates the loop (oracle_read_packets), and the
+# GPU tests hold the engine to the oracle.
+def _payload_of(s, pkts, k):
+    p = pkts[k]
+    a = p["stream_off"] + p["header_len"] + p["crc_len"]
+    return s[a:a + p["data_len"]]
+
+
+def _read_cases(oracle):
+    """(name, stream, client_offset, read_len, expected rc, expected records,
+    expected delivered bytes) -- constructed."""
+    cs, dl = 512, [65536] * 6 + [12345]
+    s, _ = build_stream(oracle.crc32c, 2, cs, CSUM_CRC32C, dl, seed=1, offset0=3 * 65536)
+    whole = oracle.verify_packets(s)[1]
+    pay = b"".join(_payload_of(s, whole, k) for k in range(len(dl)))
+    base = 3 * 65536
+    out = []
+    # starts inside packet 0, ends inside packet 3
+    out.append(("mid_to_mid", s, base + 1000, 3 * 65536 - 500, 0, 4, pay[1000:1000 + 3 * 65536 - 500]))
+    # exactly the block's bytes: stops at the last data packet, the empty last packet unread
+    total = sum(dl)
+    out.append(("whole_block", s, base, total, 0, len(dl), pay))
+    # one byte, in the middle of packet 2 (the server starts the stream at packet 2)
+    out.append(("one_byte", s[whole[2]["stream_off"]:], base + 2 * 65536 + 7, 1, 0, 1,
+                pay[2 * 65536 + 7:2 * 65536 + 8]))
+    # more than the block holds: the empty last packet arrives while bytes are wanted
+    out.append(("past_block_end", s, base + 5, total, ERR_BAD_LASTPACKET, len(dl) + 1, pay[5:]))
+    # the read starts after the first packet's data: UNEXPECTED_READ_OFFSET
+    out.append(("read_offset", s, base + 65536 + 3, 100, ERR_UNEXPECTED_READ_OFFSET, 1, b""))
+    # a data packet flagged lastPacketInBlock with the read unfinished: its bytes, then the error
+    s2, _ = build_stream(oracle.crc32c, 2, cs, CSUM_CRC32C, [65536] * 4, seed=2, last_empty=False, last_flag=1)
+    w2 = oracle.verify_packets(s2)[1]
+    p2 = _payload_of(s2, w2, 0) + _payload_of(s2, w2, 1)
+    out.append(("last_flag_short", s2, 100, 3 * 65536, ERR_BAD_LASTPACKET, 2, p2[100:]))
+    # bad CRCs in packet 2: the bytes before it, the window's own end in packet 4
+    s3, _ = build_stream(oracle.crc32c, 2, cs, CSUM_CRC32C, [65536] * 6, seed=3, corrupt=[(2, 5)])
+    w3 = oracle.verify_packets(s3)[1]
+    p3 = b"".join(_payload_of(s3, w3, k) for k in range(2))
+    out.append(("bad_crc_mid", s3, 40, 4 * 65536 + 9, BAD, 5, p3[40:]))
+    return out
+
+
+def test_oracle_read_windows_constructed(oracle):
+    for name, s, co, rl, rc, npk, data in _read_cases(oracle):
+        got = oracle.read_packets(s, co, rl)
+        assert (got[0], len(got[1])) == (rc, npk), name
+        assert got[3] == data, name
+        assert got[2] == got[1][-1]["stream_off"] + got[1][-1]["header_len"] + got[1][-1]["crc_len"] + \
+            got[1][-1]["data_len"], name
+
+
+ERR_UNEXPECTED_READ_OFFSET, ERR_BAD_LASTPACKET = 28, 32
+
+
+def _dev_read(engine, s, shift, co, rl, proto=2, cs=512, ctype=CSUM_CRC32C, cap=None, mp=None):
+    keep, p = _dev(engine, s, shift)
+    cap = rl if cap is None else cap
+    dst = engine.DeviceBuffer(cap + 64)
+    dst.fill(0xA5)
+    try:
+        rc, pkts, used, delivered = engine.verify_packets_copy(p, len(s), dst.ptr, cap, proto, cs, ctype, max_pkts=mp,
+                                                               client_offset=co, read_len=rl)
+        guard = dst.download(64, offset=cap).tobytes()
+        return rc, pkts, used, dst.download(delivered).tobytes(), guard
+    finally:
+        keep.free()
+        dst.free()
+
+
+@pytest.mark.gpu
+def test_gpu_read_windows_constructed(engine, oracle):
+    """Every constructed read window through the fused verify + copy-out
+    equals the oracle's read loop: records, verdicts, consumed bytes and the
+    delivered bytes themselves; nothing is written past the read."""
+    for name, s, co, rl, rc, npk, data in _read_cases(oracle):
+        want = oracle.read_packets(s, co, rl)
+        for shift in (0, 3):
+            got = _dev_read(engine, s, shift, co, rl)
+            assert got[:3] == want[:3], (name, shift)
+            assert got[3] == want[3] == data, (name, shift)
+            assert got[4] == b"\xa5" * 64, (name, shift)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("proto,cs,ctype,sizes", [
+    (2, 512, CSUM_CRC32C, "regular"),   # device framing passes (grid), tiled kernel copies
+    (1, 512, CSUM_CRC32, "regular"),
+    (2, 512, CSUM_CRC32C, "short"),     # <= 64 packets: the one-launch short-run kernel
+    (2, 4096, CSUM_CRC32C, "mixed"),    # sizes change: grid passes + the host window walk
+    (2, 100, CSUM_CRC32C, "partial"),   # chunk 100: every chunk on the generic kernel
+    (2, 512, CSUM_CRC32C, "random"),
+])
+def test_gpu_read_windows_vs_oracle(engine, oracle, proto, cs, ctype, sizes):
+    """Reads starting and ending at many offsets -- inside packets, on packet
+    and chunk boundaries, at 16-B piece edges -- on every path of the device
+    stream verifier (grid, short run, host walk) and at odd stream
+    alignments: byte-exact against the oracle's read loop."""
+    rng = np.random.default_rng(cs + proto + len(sizes))
+    if sizes == "regular":
+        dl = [65536] * 300 + [12345]
+    elif sizes == "short":
+        dl = [65536] * 40 + [3000]
+    elif sizes == "mixed":
+        dl = [int(x) for x in np.repeat(rng.choice([4096, 61440, 30000, 65536], 40), rng.integers(1, 8, 40))]
+    elif sizes == "partial":
+        dl = [40000] * 60
+    else:
+        dl = [int(x) for x in rng.integers(1, 70000, 120)]
+    base = 7 * 65536
+    corrupt = [(len(dl) // 2, 1)]
+    s, _ = build_stream(oracle.crc32c, proto, cs, ctype, dl, seed=len(dl), corrupt=corrupt, offset0=base)
+    total = sum(dl)
+    cases = [(base, total), (base + 1, total - 1), (base + 15, 17), (base + 16, 32), (base + 65536 - 3, 10),
+             (base + 511, 513), (base + total - 5, 5), (base + total - 5, 50)]
+    for _ in range(6):
+        a = int(rng.integers(0, total))
+        cases.append((base + a, int(rng.integers(1, total - a + 1))))
+    cases.append((base + total // 2, 1000))  # the stream below starts at packet 0: UNEXPECTED_READ_OFFSET
+    whole = oracle.verify_packets(s, proto, cs, ctype)[1]
+    starts = np.cumsum([0] + dl[:-1])
+    for i, (co, rl) in enumerate(cases):
+        # the server starts the stream at the packet holding client_offset
+        k = int(np.searchsorted(starts, co - base, side="right")) - 1 if i + 1 < len(cases) else 0
+        sub = s[whole[k]["stream_off"]:]
+        want = oracle.read_packets(sub, co, rl, proto, cs, ctype)
+        shift = i % 4
+        got = _dev_read(engine, sub, shift, co, rl, proto, cs, ctype)
+        assert got[:3] == want[:3], (co - base, rl, shift)
+        assert got[3] == want[3], (co - base, rl, shift)
+        assert got[4] == b"\xa5" * 64, (co - base, rl, shift)
+    assert want[0] == ERR_UNEXPECTED_READ_OFFSET
+
+
+@pytest.mark.gpu
+def test_gpu_copy_out_mixed_sizes_never_past_cap(engine, oracle):
+    """Whole-payload copy-out into a buffer one byte too small, on a stream
+    whose packet sizes vary (the host window walk places the copies): the
+    call fails, and the bytes just past the buffer are untouched (ADVICE r2:
+    the walk used to place packets without checking the capacity)."""
+    rng = np.random.default_rng(9)
+    dl = [int(x) for x in np.repeat(rng.choice([4096, 61440, 30000, 65536], 30), rng.integers(1, 5, 30))]
+    s, _ = build_stream(oracle.crc32c, 2, 512, CSUM_CRC32C, dl, seed=9)
+    keep, p = _dev(engine, s, 1)
+    cap = sum(dl) - 1
+    dst = engine.DeviceBuffer(cap + 4096)
+    dst.fill(0xA5)
+    with pytest.raises(engine.CRC32CError):
+        engine.verify_packets_copy(p, len(s), dst.ptr, cap)
+    assert dst.download(4096, offset=cap).tobytes() == b"\xa5" * 4096
+    keep.free()
+    dst.free()

@@ -48,7 +48,7 @@ def timed(ptr, n, npk, reps=5, fn="hdfs_crc32c_verify_packets", dst=None):
     for i in range(reps + 1):  # the first call is a warm-up (buffer growth, clocks)
         t0 = time.perf_counter()
         if dst is not None:  # verify + fused copy-out
-            rc = lib.hdfs_crc32c_verify_packets_copy(ptr, n, h.PROTO_V2, 512, h.CSUM_CRC32C, arr, npk + 8,
+            rc = lib.hdfs_crc32c_verify_packets_copy(ptr, n, h.PROTO_V2, 512, h.CSUM_CRC32C, 0, h.READ_ALL, arr, npk + 8,
                                                      ctypes.byref(cnt), ctypes.byref(used), dst.ptr, dst.nbytes,
                                                      ctypes.byref(got))
         else:
