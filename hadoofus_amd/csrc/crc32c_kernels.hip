@@ -524,10 +524,61 @@ DEV void issue(uint32_t (&d)[16], uint32_t &exp, uint32_t &tl, uint32_t &sh_a, c
 // them.  Every round therefore issues exactly the same vector-memory ops
 // (4 loads, [1 expected-CRC load], 1 store) and the compiler's vmcnt waits
 // stay exact.
+// Per-stream epilogue state carried across rounds: RUN 1's run CRCs, and
+// RUN 3's pending tile (the lazy gather, below).
+struct Gst {
+  uint32_t acc;                              // RUN 1: lane 8j + q = tile j, chunk q
+  uint32_t chk, old, dat;                    // RUN 3 (VGPRs): slot check, returned count, finisher's word
+  uint32_t pslot, pgrp, pexpect, pelig, fin;  // RUN 3 (uniform): the pending tile (pslot ~0: none)
+  const uint32_t *pbase;                     // RUN 3: the pending eligible group's CRC destination
+};
+constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
+
+// RUN 3, before a round's slicing steps: the count the stream's previous
+// tile added to its group's slot (its add was issued a round ago) says
+// whether this wave finished that group -- then its word of the group's CRCs
+// is read now -- and, on a tile's last round, the owner word of the tile's
+// slot is loaded.  Both LDS reads complete under the 64 table reads of the
+// slicing: nothing is waited on.
+DEV void lazy_pre(Gst &g, const Cursor &c, SegP segs, SegCache &kc, const LaneConst &L) {
+  g.fin = 0u;
+  if (g.pslot != kNoSlot && (rfl(g.old) & 15u) + 1u == g.pexpect) {
+    g.fin = 1u;
+    if (g.pelig) g.dat = L.gslot[kGatherSlots + g.pslot * 64u + L.lane];
+  }
+  const SegHot &sh = hot(kc, segs, c.seg).h;
+  if (c.valid && c.r + 1 == sh.chunk_size / kRoundBytes)
+    g.chk = __hip_atomic_load(L.gslot + (c.grp & (kGatherSlots - 1u)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// RUN 3: the pending group's finisher stores the group's CRCs (256 B) and
+// hands the slot on to group + kGatherSlots.  Its word of the group was read
+// before the release is written, and a wave's LDS operations execute in
+// order, so the next group's writers cannot overwrite it first.
+template <class P>
+DEV void lazy_flush(Gst &g, const SegHot &sh, const LaneConst &L) {
+  uint32_t range = 0u;
+  const uint32_t *base = sh.crcs;
+  if (g.pslot != kNoSlot && g.fin) {
+    if (g.pelig) {
+      range = P::drop(L.store_policy) ? 0u : 256u;
+      base = g.pbase;
+    }
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    if (L.lane == 0)
+      __hip_atomic_store(L.gslot + g.pslot, (g.pgrp + kGatherSlots) << 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  g.pslot = kNoSlot;
+  const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<uint32_t *>(rfl64(reinterpret_cast<uint64_t>(base))), 0, static_cast<int>(rfl(range)),
+      0x00020000);
+  P::group_store(L.store_policy, g.dat, rg, L.lane * 4u);
+}
+
 template <int MODE, int RUN, class P = EP>
 DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, uint32_t st, const LaneConst &L,
                 uint32_t *__restrict__ first_bad, unsigned long long *__restrict__ mism, SegCache &kc,
-                uint32_t &acc) {
+                Gst &gs) {
   const SegHot &sh = hot(kc, segs, c.seg).h;
   const bool last = c.valid && (c.r + 1 == sh.chunk_size / kRoundBytes);
   const uint32_t flags = sh.flags;
@@ -641,11 +692,61 @@ DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, ui
       const uint32_t j = c.tile & L.rmask;
       const uint32_t v =
           static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(static_cast<int>((L.lane & 7u) * 32u), static_cast<int>(val)));
-      acc = (last && (L.lane >> 3) == j) ? v : acc;
+      gs.acc = (last && (L.lane >> 3) == j) ? v : gs.acc;
       const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
           reinterpret_cast<uint32_t *>(rfl64(reinterpret_cast<uint64_t>(sh.crcs + (c.tile & ~L.rmask) * kTileChunks))), 0,
           static_cast<int>(rfl(last && j == L.rmask ? (8u * L.rmask + nch) * 4u : 0u)), 0x00020000);
-      __builtin_amdgcn_raw_buffer_store_b32(acc, rr, L.lane * 4u, 0, 16);
+      __builtin_amdgcn_raw_buffer_store_b32(gs.acc, rr, L.lane * 4u, 0, 16);
+      return;
+    }
+    if constexpr (RUN == 3) {
+      // Lazy gather (schedule 3): as RUN 2, but no LDS round trip is waited
+      // on per tile -- the slot check was loaded before the slicing
+      // (lazy_pre), the count this tile adds is read one round later, and the
+      // group's finisher stores it then (lazy_flush).  A wave hands on the
+      // slot of its pending group before it ever waits for a slot itself, so
+      // the oldest unfinished group never waits: the wait ends.
+      lazy_flush<P>(gs, sh, L);
+      uint32_t range = keep ? nch * 4u : 0u;
+      if (last) {
+        const bool whole = ((static_cast<uint32_t>(sh.mtile_start) | sh.main_tiles) & 7u) == 0u;
+        bool elig = whole && (uint64_t(c.tile | 7u) + 1u) * kTileChunks <= sh.nchunks;
+        uint32_t expect = 8u;
+        if (!elig) {
+          const uint64_t gs0 = (sh.mtile_start + c.tile) & ~7ull;
+          expect = static_cast<uint32_t>(min<uint64_t>(8u, L.ntiles - gs0));
+          elig = expect == 8u && gs0 >= sh.mtile_start && gs0 + 8u <= sh.mtile_start + sh.main_tiles &&
+                 (gs0 + 8u - sh.mtile_start) * kTileChunks <= sh.nchunks;
+        }
+        const uint32_t gt = static_cast<uint32_t>(sh.mtile_start) + c.tile;
+        const uint32_t sl = c.grp & (kGatherSlots - 1u);
+        uint32_t *own = L.gslot + sl;
+        uint32_t o = rfl(gs.chk);
+        for (uint32_t spin = 0; (o >> 4) != c.grp; spin++) {  // rare: the slot's previous group is still open
+          if (spin > (1u << 24)) {  // never expected: fail loudly (s_trap, see RUN 2)
+            asm volatile("s_trap 2");
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          o = rfl(__hip_atomic_load(own, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        }
+        if (elig && leader) L.gslot[kGatherSlots + sl * 64u + (gt & 7u) * kTileChunks + L.qg] = val;
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);  // the CRC words before the count (in-order LDS)
+        uint32_t old = 0;
+        if (L.lane == 0) old = __hip_atomic_fetch_add(own, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        gs.old = old;  // read one round later (lazy_pre)
+        gs.pslot = sl;
+        gs.pgrp = c.grp;
+        gs.pexpect = expect;
+        gs.pelig = elig ? 1u : 0u;
+        gs.pbase = sh.crcs + static_cast<uint64_t>((gt & ~7u) - static_cast<uint32_t>(sh.mtile_start)) * kTileChunks;
+        if (elig) range = 0u;
+      }
+      // tiles of groups that are not 8 whole tiles of one segment: their own 32 B
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          reinterpret_cast<uint32_t *>(rfl64(reinterpret_cast<uint64_t>(sh.crcs + c.tile * kTileChunks))), 0,
+          static_cast<int>(rfl(range)), 0x00020000);
+      P::group_store(pol, val, rs, leader ? L.qg * 4u : 0x80000000u);
       return;
     }
     if constexpr (P::kAltTileStores)
@@ -725,7 +826,7 @@ template <int MODE, int S, int COPY, int UNA, int RUN, class P = EP>
 DEV void process(const uint32_t *lds, uint32_t (&d)[S][16], const uint32_t (&exp)[S], const uint32_t (&tl)[S],
                  const uint32_t (&sh_a)[S], const Cursor (&c)[S], SegP segs, uint32_t (&st)[S], const LaneConst &L,
                  uint32_t *__restrict__ first_bad, unsigned long long *__restrict__ mism, SegCache (&kc)[S],
-                 uint32_t (&acc)[S]) {
+                 Gst (&gs)[S]) {
   if constexpr (MODE == kModeLoadOnly) {  // diagnostic build only (the launcher refuses it otherwise)
     P::template load_only_round<S>(d, exp, c, segs, st, mism);
     return;
@@ -733,6 +834,10 @@ DEV void process(const uint32_t *lds, uint32_t (&d)[S][16], const uint32_t (&exp
   if constexpr (COPY && !UNA) {
 #pragma unroll
     for (int s = 0; s < S; s++) copy_round<P>(d[s], c[s], segs, L, kc[s]);
+  }
+  if constexpr (RUN == 3) {
+#pragma unroll
+    for (int s = 0; s < S; s++) lazy_pre(gs[s], c[s], segs, kc[s], L);
   }
   uint32_t x[S];
 #pragma unroll
@@ -771,7 +876,7 @@ DEV void process(const uint32_t *lds, uint32_t (&d)[S][16], const uint32_t (&exp
 #pragma unroll
   for (int s = 0; s < S; s++) st[s] = slice4(lds, x[s], 0u, L.lb0, L.lb1);
 #pragma unroll
-  for (int s = 0; s < S; s++) finish<MODE, RUN, P>(lds, exp[s], c[s], segs, st[s], L, first_bad, mism, kc[s], acc[s]);
+  for (int s = 0; s < S; s++) finish<MODE, RUN, P>(lds, exp[s], c[s], segs, st[s], L, first_bad, mism, kc[s], gs[s]);
 }
 
 // Tiled kernel.  MODE compute / verify; ORDER schedule (above); NT
@@ -799,6 +904,7 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
   }
   // + ticket counter, pad, kSlots 64-bit pool slots
   // + ticket counter, pad, kSlots 64-bit pool slots (+ GATHER: the group slots)
+  // GATHER 1: the compute gather (RUN 2); 2: the lazy gather (RUN 3)
   static_assert(GATHER == 0 || (MODE == kModeCompute && ORDER == 3 && S == 1), "gather: compute, schedule 3");
   __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords + 2 + 2 * kSlots + (GATHER ? kGatherWords : 0)];
 
@@ -987,13 +1093,13 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
   uint32_t tl[DEPTH][S];   // UNA: lanes 0..7, the dword after chunk lane's round part
   uint32_t sha[DEPTH][S];  // UNA: byte shift of the round's segment
   uint32_t st[S];
-  uint32_t acc[S];  // ORDER 4 compute: the current run's CRCs, lane 8j + q = tile j, chunk q
+  Gst gs[S];  // epilogue state: ORDER 4 compute's run CRCs, the lazy gather's pending tile
   LaneOff lo{0u, {0u, 0u, 0u, 0u}, 0u};
   SegCache kc[S];
 #pragma unroll
   for (int s = 0; s < S; s++) {
     st[s] = 0u;
-    acc[s] = 0u;
+    gs[s] = Gst{0u, 0u, 0u, 0u, kNoSlot, 0u, 0u, 0u, 0u, nullptr};
     kc[s].seg = 0xFFFFFFFFu;
   }
 #pragma unroll
@@ -1015,9 +1121,8 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
   for (;;) {
 #pragma unroll
     for (int k = 0; k < DEPTH; k++) {
-      process<MODE, S, COPY, UNA, (ORDER == 4 && MODE == kModeCompute) ? 1 : (GATHER ? 2 : 0)>(lds, buf[k], ex[k], tl[k], sha[k],
-                                                                                cur[k], sg, st, L, first_bad, mism,
-                                                                                kc, acc);
+      process<MODE, S, COPY, UNA, (ORDER == 4 && MODE == kModeCompute) ? 1 : GATHER == 2 ? 3 : GATHER ? 2 : 0>(
+          lds, buf[k], ex[k], tl[k], sha[k], cur[k], sg, st, L, first_bad, mism, kc, gs);
 #pragma unroll
       for (int s = 0; s < S; s++) nrounds += cur[k][s].valid ? 1u : 0u;
       const int prev = (k + DEPTH - 1) % DEPTH;
@@ -1032,6 +1137,13 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
 #pragma unroll
     for (int s = 0; s < S; s++) more |= cur[0][s].valid;
     if (!more) break;
+  }
+  if constexpr (GATHER == 2) {  // the lazy gather's last pending tile: its group may still be this wave's to store
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+      lazy_pre(gs[s], cur[0][s], sg, kc[s], L);
+      lazy_flush<EP>(gs[s], hot(kc[s], sg, cur[0][s].seg).h, L);
+    }
   }
   if (kDiag && diag && L.lane == 0) {
     diag[3 * wave + 1] = __builtin_amdgcn_s_memrealtime();
@@ -2589,6 +2701,7 @@ hipError_t launch_tiles(int mode, int order, int nt, int depth, int streams, int
     HDFS_LAUNCH_ALL(kModeCompute)
     else if (HDFS_SHAPE(4, 2, 3, 1, 1024)) HDFS_LAUNCH(kModeCompute, 4, 1, 3, 1, 1024, 1);
     else if (HDFS_SHAPE(5, 2, 3, 1, 1024)) HDFS_LAUNCH_CUG(kModeCompute, 3, 1, 3, 1, 1024, 1, 0, 0, 1);
+    else if (HDFS_SHAPE(6, 2, 3, 1, 1024)) HDFS_LAUNCH_CUG(kModeCompute, 3, 1, 3, 1, 1024, 1, 0, 0, 2);
     else return hipErrorInvalidValue;
   }
 #undef HDFS_LAUNCH_ALL

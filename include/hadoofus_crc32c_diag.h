@@ -67,7 +67,9 @@ int hdfs_crc32c_set_store_policy(int policy);
  * gather (a group's CRCs collected across the workgroup's waves, one 256-B
  * store per 8-tile group); 1 schedule 4 on tables of whole 8-tile groups
  * (one wave per group, one 256-B CRC store per group); 0 schedule 3 with a
- * 32-B store per tile.
+ * 32-B store per tile; 3 the lazy gather (schedule 3, the gather's slot
+ * check and count read off the critical path, the group stored one round
+ * after its last tile).
  * Env HDFS_CRC32C_RUNS. */
 int hdfs_crc32c_set_runs(int on);
 /* Empirical streaming-read bandwidth of `bytes` at dptr (GB/s, 1e9 B/s):

@@ -163,12 +163,14 @@ def test_unaligned_realign_small_and_large(engine, oracle, shift, cs, nch):
     assert engine.stream_crc_dev(0x5A5A5A5A, buf.ptr + shift, n) == oracle.crc32c(0x5A5A5A5A, host)
 
 
-@pytest.mark.parametrize("runs", [0, 1, 2])
+@pytest.mark.parametrize("runs", [0, 1, 2, 3])
 def test_compute_store_schedules(engine, diag, oracle, table, runs):
-    """Compute mode's three store schedules (diagnostic knob set_runs):
-    0 schedule 3 (one 32-B store per tile), 1 schedule 4 (a wave per 8-tile
-    group), 2 schedule 3 with the LDS group gather (a group's CRCs collected
-    across the workgroup's waves, one 256-B store by the wave finishing it).
+    """Compute mode's store schedules (diagnostic knob set_runs): 0 schedule
+    3 (one 32-B store per tile), 1 schedule 4 (a wave per 8-tile group), 2
+    schedule 3 with the LDS group gather (a group's CRCs collected across the
+    workgroup's waves, one 256-B store by the wave finishing it), 3 the lazy
+    gather (the same, with the slot check loaded before the slicing and the
+    count read one round later: no LDS round trip waited on per tile).
     On the C5-like table and on a table of 13-tile segments, where groups
     straddle segments and fall back to per-tile stores."""
     host, sizes, lens, want, dbuf = table
