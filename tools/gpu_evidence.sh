@@ -8,7 +8,7 @@ cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-ev}
-RND=${2:-r02}
+RND=${2:-r03}
 O=gpurun_out/${TAG}
 step() { local name=$1; shift; "$@"; local rc=$?; echo "[$name] rc=$rc" >&2; case $rc in 0) ;; *) exit $rc;; esac; }
 step tests timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread > ${O}_tests.log 2>&1
