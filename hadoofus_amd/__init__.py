@@ -18,6 +18,9 @@ from .abi import (  # noqa: F401
     ERR_PACKET_SIZE,
     ERR_INVALID_PACKETHEADERPROTO,
     ERR_UNEXPECTED_CRC_LEN,
+    ERR_UNEXPECTED_READ_OFFSET,
+    ERR_BAD_LASTPACKET,
+    READ_ALL,
     PROTO_V1,
     PROTO_V2,
     Packet,

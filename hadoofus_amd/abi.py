@@ -175,6 +175,7 @@ def bind_diag(lib):
     _bind(lib, "hdfs_crc32c_set_shape", _int, [_int, _int])
     _bind(lib, "hdfs_crc32c_set_store_policy", _int, [_int])
     _bind(lib, "hdfs_crc32c_set_runs", _int, [_int])
+    _bind(lib, "hdfs_crc32c_diag_device_checks", _int, [ctypes.POINTER(_u32), _int])
     return lib
 
 
@@ -257,7 +258,7 @@ def stream_ex(ctype, crc, buf):
     return out.value
 
 
-def _packets(fn, stream, proto, chunk_size, ctype, max_pkts, dptr=None, nbytes=None):
+def _packets(fn, stream, proto, chunk_size, ctype, max_pkts, dptr=None, nbytes=None, lib=None):
     if dptr is not None:  # device-resident stream
         keep, p, n = None, dptr, nbytes
     else:
@@ -266,9 +267,10 @@ def _packets(fn, stream, proto, chunk_size, ctype, max_pkts, dptr=None, nbytes=N
         max_pkts = n // (25 if proto == PROTO_V1 else 6) + 1
     arr = (Packet * max(1, max_pkts))()
     npk, used = _sz(0), _u64(0)
-    rc = getattr(load(), fn)(p, n, proto, chunk_size, ctype, arr, max_pkts, ctypes.byref(npk), ctypes.byref(used))
+    lib = lib or load()
+    rc = getattr(lib, fn)(p, n, proto, chunk_size, ctype, arr, max_pkts, ctypes.byref(npk), ctypes.byref(used))
     if rc < 0:
-        _check(rc)
+        _check(rc, lib)
     return rc, [arr[i].as_dict() for i in range(npk.value)], used.value
 
 
@@ -354,22 +356,24 @@ def composite_crcs(segments):
 
 
 def parse_packets(stream, proto=PROTO_V2, chunk_size=512, ctype=CSUM_CRC32C, max_pkts=None, dptr=None,
-                  nbytes=None):
+                  nbytes=None, lib=None):
     """Framing walk of a packet stream: host bytes `stream` (no device work),
-    or device memory (dptr, nbytes).  -> (rc, [packet dicts], consumed)."""
-    return _packets("hdfs_crc32c_parse_packets", stream, proto, chunk_size, ctype, max_pkts, dptr, nbytes)
+    or device memory (dptr, nbytes).  -> (rc, [packet dicts], consumed).
+    lib: the library to run on (default the product; tests pass the
+    diagnostic build)."""
+    return _packets("hdfs_crc32c_parse_packets", stream, proto, chunk_size, ctype, max_pkts, dptr, nbytes, lib)
 
 
 def verify_packets(stream, proto=PROTO_V2, chunk_size=512, ctype=CSUM_CRC32C, max_pkts=None, dptr=None,
-                   nbytes=None):
+                   nbytes=None, lib=None):
     """Framing + GPU verification of every packet's chunks, of host bytes
     `stream` or of device memory (dptr, nbytes).
     -> (rc, [packet dicts], consumed); rc = first error in stream order."""
-    return _packets("hdfs_crc32c_verify_packets", stream, proto, chunk_size, ctype, max_pkts, dptr, nbytes)
+    return _packets("hdfs_crc32c_verify_packets", stream, proto, chunk_size, ctype, max_pkts, dptr, nbytes, lib)
 
 
 def verify_packets_copy(dptr, nbytes, dst, dst_cap, proto=PROTO_V2, chunk_size=512, ctype=CSUM_CRC32C,
-                        max_pkts=None, client_offset=0, read_len=READ_ALL):
+                        max_pkts=None, client_offset=0, read_len=READ_ALL, lib=None):
     """Verify + copy-out of a device-resident stream (dptr, nbytes) into the
     device buffer dst (dst_cap bytes): the payloads de-framed in stream order
     (read_len READ_ALL), or the block bytes [client_offset, client_offset +
@@ -379,11 +383,12 @@ def verify_packets_copy(dptr, nbytes, dst, dst_cap, proto=PROTO_V2, chunk_size=5
         max_pkts = nbytes // (25 if proto == PROTO_V1 else 6) + 1
     arr = (Packet * max(1, max_pkts))()
     npk, used, got = _sz(0), _u64(0), _u64(0)
-    rc = load().hdfs_crc32c_verify_packets_copy(dptr, nbytes, proto, chunk_size, ctype, client_offset, read_len, arr,
-                                                max_pkts, ctypes.byref(npk), ctypes.byref(used), dst, dst_cap,
-                                                ctypes.byref(got))
+    lib = lib or load()
+    rc = lib.hdfs_crc32c_verify_packets_copy(dptr, nbytes, proto, chunk_size, ctype, client_offset, read_len, arr,
+                                             max_pkts, ctypes.byref(npk), ctypes.byref(used), dst, dst_cap,
+                                             ctypes.byref(got))
     if rc < 0:
-        _check(rc)
+        _check(rc, lib)
     return rc, [arr[i].as_dict() for i in range(npk.value)], used.value, got.value
 
 

@@ -1459,8 +1459,27 @@ int hdfs_crc32c_mailbox_destroy(hdfs_crc32c_mailbox *mb) {
   return HDFS_CRC32C_OK;
 }
 
+int device_checks(const char *call) {
+  if (!kDiag) return HDFS_CRC32C_OK;
+  static const char *const kName[] = {"check self-test", "frame_grid_kernel", "grid_build_kernel", "header_window_kernel",
+                                      "small_run_kernel", "grid_finalize_kernel"};
+  uint32_t v[3];
+  const hipError_t e = read_device_checks(v, 1);
+  if (e != hipSuccess) return fail(HDFS_CRC32C_EHIP, "%s: reading the device checks: %s", call, hipGetErrorString(e));
+  if (!v[2]) return HDFS_CRC32C_OK;
+  return fail(HDFS_CRC32C_EHIP, "%s: device check failed in %s at crc32c_kernels.hip:%u (%u violations)", call,
+              kName[v[0] < 6 ? v[0] : 0], v[1], v[2]);
+}
+
 #ifdef HDFS_CRC32C_DIAG
 // ---- diagnostic build only (include/hadoofus_crc32c_diag.h) ----
+int hdfs_crc32c_diag_device_checks(uint32_t *out3, int reset) {
+  if (!out3) return fail(HDFS_CRC32C_EINVAL, "null output");
+  const hipError_t e = read_device_checks(out3, reset);
+  if (e != hipSuccess) return fail(HDFS_CRC32C_EHIP, "reading the device checks: %s", hipGetErrorString(e));
+  return HDFS_CRC32C_OK;
+}
+
 int hdfs_crc32c_set_store_policy(int policy) {
   if (policy < 0 || policy > 25) return fail(HDFS_CRC32C_EINVAL, "store policy 0..25");
   g_store_policy = uint32_t(policy);

@@ -76,6 +76,10 @@ hipError_t launch_grid_finalize(const SegDev *segs, uint32_t nseg, const uint32_
 // ---- errors ----
 extern thread_local char g_err[512];
 int fail(int code, const char *fmt, ...);
+hipError_t read_device_checks(uint32_t out[3], int reset);
+// Diagnostic build: EHIP naming the kernel and line of a device-check
+// violation since the last call (then cleared); release build: 0, no work.
+int device_checks(const char *call);
 
 #define HIPCHK(expr)                                                                   \
   do {                                                                                 \

@@ -12,18 +12,25 @@
 //
 //  * the engine's own hipHostMalloc blocks (hdfs_crc32c_host_alloc, session
 //    slots) are recorded as OWNED ranges;
-//  * every other range a call needs is pinned by the call itself, page-
-//    rounded: the buffers of one call that share a page (data and CRCs side
-//    by side) are merged into ONE registration -- the runtime DMAs a copy
-//    only from inside a single registration, so a CRC array that began in
-//    the data's registration and ran on into a second one was refused
-//    ("invalid argument") -- and a range that lies inside a registration
-//    another call holds shares it (reference counted);
+//  * every other range a call needs is pinned by the call itself, over the
+//    caller's EXACT bytes: the buffers of one call that share a page (data
+//    and CRCs side by side) are merged into ONE registration spanning them
+//    -- the runtime DMAs a copy only from inside a single registration, so a
+//    CRC array that began in the data's registration and ran on into a
+//    second one was refused ("invalid argument") -- and a range that lies
+//    inside a registration another call holds shares it (reference counted).
+//    Registrations are NOT widened to whole pages: the runtime looks a
+//    pointer up by the registered byte range, so a page-rounded registration
+//    would capture unrelated heap objects on the same pages (the engine's
+//    own pageable staging vectors among them), whose copies then ran past
+//    the registration's end and were refused;
 //  * a scope releases its pins when the call ends -- after draining the
 //    streams that may still read or write them -- and the LAST reference
 //    unregisters, with the result checked and reported;
-//  * a range that only partly overlaps another call's registration cannot
-//    be one registration: the call is refused (no DMA straddles two);
+//  * a range that only partly overlaps the bytes of another call's
+//    registration cannot be one registration: the call is refused (no DMA
+//    straddles two); ranges of different calls that merely share a page are
+//    registered separately;
 //  * memory pinned by someone else (a torch pinned tensor) is detected by the
 //    runtime refusing the registration (already registered) and confirmed at
 //    both ends of the caller's bytes; it is used in place, never unregistered.
@@ -47,7 +54,7 @@ namespace hdfs_crc32c {
 struct PinBackend {
   enum { kOk = 0, kAlready = 1, kFail = -1 };
   virtual ~PinBackend() = default;
-  // page-aligned range; kOk, kAlready (the runtime has it pinned), kFail
+  // exact byte range; kOk, kAlready (the runtime has it pinned), kFail
   virtual int reg(uintptr_t p, size_t n) = 0;
   virtual int unreg(uintptr_t p) = 0;  // kOk / kFail
   // the runtime reports byte p as page-locked host memory (someone else's)
@@ -65,16 +72,15 @@ class PinRegistry {
   explicit PinRegistry(PinBackend *b, size_t page = 4096) : be_(b), page_(page) {}
   void set_backend(PinBackend *b) { be_ = b; }
 
-  // An engine allocation (hipHostMalloc'd, page-granular).
+  // An engine allocation (hipHostMalloc'd).
   void add_owned(const void *p, size_t n) {
     if (!p || !n) return;
     std::lock_guard<std::mutex> lk(mu_);
-    const uintptr_t s = down(uintptr_t(p)), e = up(uintptr_t(p) + n);
-    map_[s] = Entry{e, 0u, true};
+    map_[uintptr_t(p)] = Entry{uintptr_t(p) + n, 0u, true};
   }
   bool remove_owned(const void *p) {
     std::lock_guard<std::mutex> lk(mu_);
-    auto it = map_.find(down(uintptr_t(p)));
+    auto it = map_.find(uintptr_t(p));
     if (it == map_.end() || !it->second.owned) return false;
     map_.erase(it);
     return true;
@@ -126,7 +132,7 @@ class PinRegistry {
   int acquire(std::vector<std::pair<uintptr_t, size_t>> bufs, std::vector<uintptr_t> &held) {
     if (bufs.empty()) return 0;
     std::lock_guard<std::mutex> lk(mu_);
-    // page ranges of the buffers, merged where they share a page
+    // byte ranges of the buffers, merged where they share a page
     std::sort(bufs.begin(), bufs.end());
     struct Need {
       uintptr_t s, e;
@@ -134,8 +140,8 @@ class PinRegistry {
     };
     std::vector<Need> need;
     for (auto &b : bufs) {
-      const uintptr_t s = down(b.first), e = up(b.first + b.second);
-      if (!need.empty() && s < need.back().e) {
+      const uintptr_t s = b.first, e = b.first + b.second;
+      if (!need.empty() && down(s) < up(need.back().e)) {
         need.back().e = e > need.back().e ? e : need.back().e;
         need.back().parts.push_back(b);
       } else {
@@ -147,7 +153,7 @@ class PinRegistry {
       for (uintptr_t k : took) drop(k);
     };
     for (const Need &nd : need) {
-      // entries overlapping [nd.s, nd.e)
+      // entries whose bytes overlap [nd.s, nd.e)
       auto it = map_.upper_bound(nd.s);
       if (it != map_.begin() && std::prev(it)->second.end > nd.s) --it;
       const bool any = it != map_.end() && it->first < nd.e;

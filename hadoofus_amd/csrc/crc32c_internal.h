@@ -18,6 +18,16 @@ constexpr bool kDiag = true;
 constexpr bool kDiag = false;
 #endif
 
+// Kernels that carry device checks in the diagnostic build (DCHK,
+// crc32c_kernels.hip): the id recorded with a violation.
+enum DevCheckKernel : uint32_t {
+  kDkFrameGrid = 1,
+  kDkGridBuild = 2,
+  kDkHeaderWindow = 3,
+  kDkSmallRun = 4,
+  kDkGridFinalize = 5,
+};
+
 // Segment flags (also mirrored as HDFS_CRC32C_SEG_* in the public header).
 enum : uint32_t {
   kSegBigEndian = 1u,  // crcs[] are in wire byte order (src/util.h:68-92)

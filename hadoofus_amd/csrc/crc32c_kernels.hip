@@ -112,6 +112,29 @@ DEV uint64_t rfl64(uint64_t x) {
   return (static_cast<uint64_t>(rfl(static_cast<uint32_t>(x >> 32))) << 32) | rfl(static_cast<uint32_t>(x));
 }
 
+// Device checks (diagnostic build only): an invariant a kernel relies on
+// for an address it is about to touch -- a record slot inside the pass, a
+// packet's bytes inside the stream, a copy-out inside the destination.  A
+// violation is counted in g_dchk with the kernel and source line of the
+// first one, and the access it guards is skipped, so a broken invariant is
+// reported by the call that broke it (diag_device_checks(), read by the
+// engine after each device-stream call) instead of surfacing as an illegal
+// address in whatever runs next.  Release build: DCHK(c, k) is `true` and c
+// is never evaluated.
+#ifdef HDFS_CRC32C_DIAG
+__device__ uint32_t g_dchk[4];  // kernel of the first violation, its line, violations
+DEV bool dchk(bool ok, uint32_t kid, uint32_t line) {
+  if (!ok && atomicAdd(&g_dchk[2], 1u) == 0u) {
+    g_dchk[0] = kid;
+    g_dchk[1] = line;
+  }
+  return ok;
+}
+#define DCHK(c, kid) dchk((c), (kid), __LINE__)
+#else
+#define DCHK(c, kid) true
+#endif
+
 // The segment table is read through the constant address space: loads with
 // a wave-uniform index then always lower to s_load (scalar cache, lgkmcnt),
 // never to vector loads that would enter the vmcnt ordering the prefetch.
@@ -588,9 +611,13 @@ DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, ui
   uint32_t out = 0, byte = 0;
   if (last) {
     uint32_t v = L.zk ? zshift(lds, L.zbase, st) : st;
-    v ^= swizzle<0x041F>(v);  // xor lane 1
-    v ^= swizzle<0x081F>(v);  // xor lane 2
-    v ^= swizzle<0x101F>(v);  // xor lane 4
+    // XOR of the chunk's 8 lanes with DPP (VALU, which has headroom) rather
+    // than ds_swizzle (LDS instruction slots, which the table reads fill):
+    // quad_perm [1,0,3,2] and [2,3,0,1] give every lane its quad's XOR,
+    // row_half_mirror (lane i <-> 7 - i within 8) swaps the two quads' XORs
+    v ^= dpp<0xB1>(v);
+    v ^= dpp<0x4E>(v);
+    v ^= dpp<0x141>(v);
     out = (flags & kSegRaw) ? v : ~v;
     if (MODE == kModeVerify) {
       const uint32_t e = (flags & kSegBigEndian) ? __builtin_bswap32(exp) : exp;
@@ -1959,6 +1986,25 @@ DEV GridContrib grid_contrib(const hdfs_crc32c_packet &r, uint32_t cs, int verif
   return a;
 }
 
+// Wire size of the packet at base from its first six bytes (header_len +
+// plen - 4, 0 if not positive; src/datanode.c:2428 with the v1 / v2 header
+// length): the grid of a device framing pass.  The six byte loads go out
+// together through a buffer descriptor whose range ends with the stream
+// (bytes past it read 0) -- no per-byte bounds test, so no load waits for
+// the one before it.
+DEV uint64_t grid_stride(const uint8_t *s, uint64_t len, uint64_t base, int proto) {
+  const uint64_t rem = base < len ? len - base : 0;
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t *>(s + (base < len ? base : 0)), 0, static_cast<int>(rem < 8 ? rem : 8), 0x00020000);
+  uint32_t b[6];
+#pragma unroll
+  for (int i = 0; i < 6; i++) b[i] = __builtin_amdgcn_raw_buffer_load_b8(r, i, 0, 0);
+  const int32_t plen = int32_t((b[0] << 24) | (b[1] << 16) | (b[2] << 8) | b[3]);
+  const int64_t hl = proto == HDFS_CRC32C_PROTO_V2 ? 6 + int64_t((b[4] << 8) | b[5]) : 25;
+  const int64_t tot = hl + int64_t(plen) - 4;
+  return tot > 0 ? uint64_t(tot) : 0;
+}
+
 // A packet's first kHdrWin bytes, staged in LDS with four 16-B loads, so
 // frame_step's byte reads hit LDS instead of making ~30 dependent trips to
 // memory.  Only when the whole window lies inside the stream (a packet
@@ -2005,14 +2051,7 @@ __global__ __launch_bounds__(kGridBlock) void frame_grid_kernel(
   // packet, so no thread decodes packet 0's PacketHeaderProto just to find
   // the grid.  If packet 0 is not such a packet its status ends the run
   // (first_break = 0) and the other grid points are never read.
-  uint64_t stride = 0;
-  {
-    auto at0 = [&](uint64_t i) -> uint32_t { return base + i < len ? uint32_t(s[base + i]) : 0u; };
-    const int32_t plen = int32_t((at0(0) << 24) | (at0(1) << 16) | (at0(2) << 8) | at0(3));
-    const int64_t hl = proto == HDFS_CRC32C_PROTO_V2 ? 6 + int64_t((at0(4) << 8) | at0(5)) : 25;
-    const int64_t tot = hl + int64_t(plen) - 4;
-    stride = tot > 0 ? uint64_t(tot) : 0;
-  }
+  const uint64_t stride = grid_stride(s, len, base, proto);
   if (k == 0) {
     sum->stride = stride;
     sum->unaligned = 0u;  // OR-ed by grid_build_kernel
@@ -2033,13 +2072,18 @@ __global__ __launch_bounds__(kGridBlock) void frame_grid_kernel(
            : st == frame::kStepStop ? kGridStop
            : total == stride        ? kGridOn
                                     : kGridOff;
-      if (code != kGridMore) {
+      // a recorded clean packet's bytes lie inside the stream (the verify
+      // segments built from its record read them), the pass inside its buffers
+      if (code != kGridMore &&
+          DCHK(r.error || r.stream_off + r.header_len + uint64_t(r.crc_len) + uint64_t(r.data_len) <= len,
+               kDkFrameGrid) &&
+          DCHK(count <= kGridMaxCount, kDkFrameGrid)) {
         recs[k] = r;
         a = grid_contrib(r, cs, verify, rwin, client_offset);
       }
     }
   }
-  if (k < count) {
+  if (k < count && DCHK(count <= kGridMaxCount, kDkFrameGrid)) {
     status[k] = code;
     contrib[k] = a;
   }
@@ -2089,13 +2133,33 @@ __global__ __launch_bounds__(kGridBlock) void grid_build_kernel(
   __shared__ uint32_t islast;
   const uint32_t t = threadIdx.x, b = blockIdx.x, k = b * kGridBlock + t, lane = t & 63u, w = t >> 6;
   // 1. the run's end: the first grid point that is not On, over all blocks
+  // (at most kGridMaxCount / kGridBlock blocks: every load a thread needs is
+  // issued before the first is used -- one memory round trip, not one per
+  // block a thread covers)
+  constexpr uint32_t kPer = (kGridMaxCount / kGridBlock + kGridBlock - 1) / kGridBlock;
   uint32_t m = 0xFFFFFFFFu;
-  for (uint32_t j = t; j < nblk; j += kGridBlock) m = min(m, blk_min[j]);
-  // 2. shares of the blocks before this one
-  uint64_t v[6] = {0, 0, 0, 0, 0, 0};
-  for (uint32_t j = t; j < b; j += kGridBlock)
+  {
+    uint32_t x[kPer];
 #pragma unroll
-    for (int q = 0; q < 6; q++) v[q] += blk_sum[6 * j + q];
+    for (uint32_t u = 0; u < kPer; u++) x[u] = t + u * kGridBlock < nblk ? blk_min[t + u * kGridBlock] : 0xFFFFFFFFu;
+#pragma unroll
+    for (uint32_t u = 0; u < kPer; u++) m = min(m, x[u]);
+  }
+  // 2. shares of the blocks before this one (batches of 4 blocks per thread)
+  uint64_t v[6] = {0, 0, 0, 0, 0, 0};
+  for (uint32_t j0 = t; j0 < b; j0 += 4u * kGridBlock) {
+    uint64_t x[4][6];
+#pragma unroll
+    for (uint32_t u = 0; u < 4; u++) {
+      const uint32_t j = j0 + u * kGridBlock;
+#pragma unroll
+      for (int q = 0; q < 6; q++) x[u][q] = j < b ? blk_sum[6 * j + q] : 0ull;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < 4; u++)
+#pragma unroll
+      for (int q = 0; q < 6; q++) v[q] += x[u][q];
+  }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
 #pragma unroll
@@ -2179,9 +2243,14 @@ __global__ __launch_bounds__(kGridBlock) void grid_build_kernel(
       d.copy_dst = copy_base && clen ? copy_base + at : nullptr;
       d.copy_w0 = cb;
       d.copy_w1 = cb + clen;
-      segs[sg] = d;
-      seg2pkt[sg] = k;
-      fb[sg] = 0xFFFFFFFFu;
+      // one entry per recorded packet at most; a copy window inside the
+      // packet's data and its destination inside the read's
+      if (DCHK(sg <= k, kDkGridBuild) &&
+          DCHK(!clen || (uint64_t(cb) + clen <= uint64_t(r.data_len) && at + clen <= copy_cap), kDkGridBuild)) {
+        segs[sg] = d;
+        seg2pkt[sg] = k;
+        fb[sg] = 0xFFFFFFFFu;
+      }
     }
     // one atomic per wave that has a byte-unaligned tiled segment / a segment
     // off the uniform layout (per-thread atomics on one word serialise: 16 K of
@@ -2210,7 +2279,8 @@ __global__ __launch_bounds__(kGridBlock) void grid_build_kernel(
       uint32_t at = 0;
       if (lane == 0 && bal) at = atomicAdd(&done[1], static_cast<uint32_t>(__builtin_popcountll(bal)));
       at = static_cast<uint32_t>(__shfl(static_cast<int>(at), 0));
-      if (diff) exc[at + static_cast<uint32_t>(__builtin_popcountll(bal & ((1ull << lane) - 1ull)))] = k;
+      const uint32_t ix = at + static_cast<uint32_t>(__builtin_popcountll(bal & ((1ull << lane) - 1ull)));
+      if (diff && DCHK(ix < count, kDkGridBuild)) exc[ix] = k;
     }
     // 6. the summary, from the thread of the run's last packet
     if (k == last) {
@@ -2296,21 +2366,31 @@ __global__ __launch_bounds__(1024) void grid_finalize_kernel(const SegDev *__res
   if (threadIdx.x == 0) nb = 0u;
   __syncthreads();
   if (nseg == 0xFFFFFFFFu) nseg = sum->nseg;  // launched before the host knows the run's size
+  if (!DCHK(nseg <= bad_cap, kDkGridFinalize)) nseg = bad_cap;  // one segment per packet of the pass
   auto *hbad = reinterpret_cast<GridBad *>(hsum2 + 256);
-  for (uint32_t i = threadIdx.x; i < nseg; i += 1024u) {
-    if (fb[i] == 0xFFFFFFFFu) continue;
-    const SegDev d = segs[i];
-    const uint32_t nbyte = (d.nchunks + 7u) / 8u;
-    uint32_t n = 0;
-    for (uint32_t j = 0; j < nbyte; j++) {
-      uint32_t byte = d.bitmap[j];
-      if (j == d.nchunks / 8u) byte &= (1u << (d.nchunks % 8u)) - 1u;  // bits past the last chunk
-      n += __builtin_popcount(byte);
+  // first-bad words in batches of 16 per thread, every load of a batch issued
+  // before the first is tested (16 K segments: one round trip, not 16)
+  for (uint32_t i0 = threadIdx.x; i0 < nseg; i0 += 16u * 1024u) {
+    uint32_t f[16];
+#pragma unroll
+    for (uint32_t u = 0; u < 16; u++) f[u] = i0 + u * 1024u < nseg ? fb[i0 + u * 1024u] : 0xFFFFFFFFu;
+#pragma unroll
+    for (uint32_t u = 0; u < 16; u++) {
+      if (f[u] == 0xFFFFFFFFu) continue;  // rare: a segment with a bad chunk
+      const uint32_t i = i0 + u * 1024u;
+      const SegDev d = segs[i];
+      const uint32_t nbyte = (d.nchunks + 7u) / 8u;
+      uint32_t n = 0;
+      for (uint32_t j = 0; j < nbyte; j++) {
+        uint32_t byte = d.bitmap[j];
+        if (j == d.nchunks / 8u) byte &= (1u << (d.nchunks % 8u)) - 1u;  // bits past the last chunk
+        n += __builtin_popcount(byte);
+      }
+      const uint32_t slot = atomicAdd(&nb, 1u);
+      const GridBad g{seg2pkt[i], int32_t(f[u]), n, 0u};
+      if (slot < bad_cap) bad[slot] = g;
+      if (slot < host_cap) hbad[slot] = g;
     }
-    const uint32_t slot = atomicAdd(&nb, 1u);
-    const GridBad g{seg2pkt[i], int32_t(fb[i]), n, 0u};
-    if (slot < bad_cap) bad[slot] = g;
-    if (slot < host_cap) hbad[slot] = g;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -2361,14 +2441,9 @@ __global__ __launch_bounds__(1024) void small_run_kernel(const uint8_t *__restri
   // their data lengths sum to the destination offset.  Without copy-out
   // only thread 0 frames, packet k.
   const uint32_t nfr = copy_dst ? k + 1u : 1u;
-  if (tid < nfr) {
+  if (tid < nfr && DCHK(nfr <= kSmallRunMax && k < count, kDkSmallRun)) {
     const uint32_t pk = copy_dst ? tid : k;
-    // the grid: header_len + plen - 4 of the packet at 0 (as frame_grid_kernel)
-    auto at0 = [&](uint64_t i) -> uint32_t { return i < len ? uint32_t(s[i]) : 0u; };
-    const int32_t plen = int32_t((at0(0) << 24) | (at0(1) << 16) | (at0(2) << 8) | at0(3));
-    const int64_t hl = proto == HDFS_CRC32C_PROTO_V2 ? 6 + int64_t((at0(4) << 8) | at0(5)) : 25;
-    const int64_t tot = hl + int64_t(plen) - 4;
-    const uint64_t stride = tot > 0 ? uint64_t(tot) : 0;
+    const uint64_t stride = grid_stride(s, len, 0, proto);  // the grid, as frame_grid_kernel
     hdfs_crc32c_packet r{};
     uint32_t code = kGridMore;
     uint64_t total = 0;
@@ -2385,9 +2460,13 @@ __global__ __launch_bounds__(1024) void small_run_kernel(const uint8_t *__restri
       const bool want = verify && code != kGridMore && !r.error && r.crc_len > 0 && ctype != HDFS_CRC32C_CSUM_NULL;
       const uint32_t nch = want ? uint32_t(r.crc_len) / 4u : 0u;
       const bool fits = uint32_t(r.data_len) <= kSmallMax && nch <= kSmallMaxChunks && (cs % 64u == 0 || nch == 1u);
+      // the bytes this workgroup will load: inside the stream
+      const bool inside =
+          !(want && fits) ||
+          DCHK(r.stream_off + r.header_len + uint64_t(r.crc_len) + uint64_t(r.data_len) <= len, kDkSmallRun);
       rec = r;
       ctl[0] = code;
-      ctl[1] = want && fits ? 1u : 0u;
+      ctl[1] = want && fits && inside ? 1u : 0u;
       ctl[2] = want && !fits ? 1u : 0u;
       ctl[3] = 0xFFFFFFFFu;
       ctl[4] = 0u;
@@ -2407,12 +2486,16 @@ __global__ __launch_bounds__(1024) void small_run_kernel(const uint8_t *__restri
     frame::read_place(before, sdl[k], copy_cap, at, clen);
     ctl[6] = uint32_t(at);
     ctl[7] = uint32_t(at >> 32);
-    ctl[8] = ok && clen ? 1u : 0u;
+    // the window inside the packet's data, its place inside the destination
+    ctl[8] = ok && clen &&
+                     DCHK(uint64_t(cb) + clen <= uint64_t(uint32_t(rec.data_len)) && at + clen <= copy_cap, kDkSmallRun)
+                 ? 1u
+                 : 0u;
     ctl[9] = cb;
     ctl[10] = cb + clen;
   }
   __syncthreads();
-  if (ctl[1]) {
+  if (ctl[1] && DCHK(ctl[5] <= 16u, kDkSmallRun)) {  // zt holds 16 levels
     const uint32_t nlev = ctl[5];
     for (uint32_t q = tid; q < nlev * 256u; q += 1024u)
       *reinterpret_cast<u32x4 *>(&zt[4u * q]) = gload16(pow2 + 4u * q);
@@ -2593,20 +2676,53 @@ __global__ __launch_bounds__(256) void header_window_kernel(const uint8_t *__res
   const uint32_t t = blockIdx.x * 256u + threadIdx.x;
   constexpr uint32_t kWords = kHdrWin / 4;
   if (proto) {
-    auto at0 = [&](uint64_t i) -> uint32_t { return base + i < len ? uint32_t(s[base + i]) : 0u; };
-    const int32_t plen = int32_t((at0(0) << 24) | (at0(1) << 16) | (at0(2) << 8) | at0(3));
-    const int64_t hl = proto == 2 ? 6 + int64_t((at0(4) << 8) | at0(5)) : 25;
-    const int64_t tot = hl + int64_t(plen) - 4;
-    stride = tot > 0 ? uint64_t(tot) : 0;
-    if (t == 0) *stride_out = stride;
+    stride = grid_stride(s, len, base, proto);
+    // the stride slot follows the rows (one D2H copy takes both)
+    if (t == 0 && DCHK(reinterpret_cast<uintptr_t>(stride_out) >= reinterpret_cast<uintptr_t>(out + count * kWords),
+                       kDkHeaderWindow))
+      *stride_out = stride;
   }
-  if (t >= count * kWords) return;
+  if (t >= count * kWords || !DCHK(uint64_t(count) * kWords <= 0xFFFFFFFFull, kDkHeaderWindow)) return;
   const uint64_t at = base + uint64_t(t / kWords) * stride + 4ull * (t % kWords);
   uint32_t w = 0;
 #pragma unroll
   for (int b = 0; b < 4; b++)
     if (at + b < len) w |= uint32_t(s[at + b]) << (8 * b);
   out[t] = w;
+}
+
+// Device checks of the diagnostic build (DCHK above): {kernel id of the
+// first violation, its line, violations}; reset clears them.  The release
+// build has none and reports zeros.
+#ifdef HDFS_CRC32C_DIAG
+// reset < 0: record one violation from kernel id 0 (the plumbing's own test)
+__global__ void dchk_inject_kernel() { (void)DCHK(threadIdx.x != 0u, 0u); }
+#endif
+
+hipError_t read_device_checks(uint32_t out[3], int reset) {
+#ifdef HDFS_CRC32C_DIAG
+  if (reset < 0) {
+    hipLaunchKernelGGL(dchk_inject_kernel, dim3(1), dim3(64), 0, nullptr);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess) return e;
+    reset = 0;
+  }
+  uint32_t v[4] = {0u, 0u, 0u, 0u};
+  hipError_t e = hipMemcpyFromSymbol(v, HIP_SYMBOL(g_dchk), sizeof(v), 0, hipMemcpyDeviceToHost);
+  if (e == hipSuccess && reset && v[2]) {
+    const uint32_t z[4] = {0u, 0u, 0u, 0u};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_dchk), z, sizeof(z), 0, hipMemcpyHostToDevice);
+  }
+  out[0] = v[0];
+  out[1] = v[1];
+  out[2] = v[2];
+  return e;
+#else
+  (void)reset;
+  out[0] = out[1] = out[2] = 0u;
+  return hipSuccess;
+#endif
 }
 
 hipError_t launch_header_window(const uint8_t *s, uint64_t len, uint64_t base, uint64_t stride, uint32_t count,

@@ -961,7 +961,12 @@ int verify_packets_dev_impl(int dev, const uint8_t *stream, uint64_t len, int pr
   std::lock_guard<std::mutex> lk(c.mu);
   uint64_t used = 0;
   size_t n = 0;
-  if ((rc = grid_walk(c, stream, len, proto, cs, ctype, max_pkts, verify, co, pkts, &n, &used, nullptr))) return rc;
+  rc = grid_walk(c, stream, len, proto, cs, ctype, max_pkts, verify, co, pkts, &n, &used, nullptr);
+  if (kDiag) {  // a broken kernel invariant outranks whatever it led to
+    const int r2 = device_checks("device packet run");
+    if (r2) return r2;
+  }
+  if (rc) return rc;
   if (co.win) {
     apply_read_window(pkts, n, used, co, delivered);
   } else if (delivered) {  // what the reference copies out before its loop returns an error (src/datanode.c:2470-2486)

@@ -72,6 +72,17 @@ int hdfs_crc32c_set_store_policy(int policy);
  * after its last tile).
  * Env HDFS_CRC32C_RUNS. */
 int hdfs_crc32c_set_runs(int on);
+/* Device checks: the framing kernels (frame_grid, grid_build, header_window,
+ * small_run, grid_finalize) test, in this build, the invariants behind each
+ * address they touch (a record slot inside its pass, a packet's bytes inside
+ * the stream, a copy-out inside its window and destination) and skip an
+ * access whose invariant fails, counting it.  Every device-stream call reads
+ * the count at its end and fails with HDFS_CRC32C_EHIP naming the kernel and
+ * source line of the first violation.  out3 = {kernel id (1 frame_grid,
+ * 2 grid_build, 3 header_window, 4 small_run, 5 grid_finalize), line,
+ * violations}; reset > 0 clears them; reset < 0 first records one violation
+ * of kernel id 0 (a test of the reporting itself). */
+int hdfs_crc32c_diag_device_checks(uint32_t *out3, int reset);
 /* Empirical streaming-read bandwidth of `bytes` at dptr (GB/s, 1e9 B/s):
  * fully coalesced 16-B-per-lane loads, no compute; the measured roofline. */
 int hdfs_crc32c_probe_read(const void *dptr, uint64_t bytes, void *stream, int iters, double *gbps);

@@ -1,6 +1,6 @@
 // CPU self-test of the engine's pinned-memory registry
 // (hadoofus_amd/csrc/crc32c_hostpin.h) with a fake runtime backend that
-// models the HIP runtime's view of registrations: page ranges registered,
+// models the HIP runtime's view of registrations: byte ranges registered,
 // refused, failing to unregister.  Scenarios are the ones round 2's
 // illegal-address fault pointed at: buffers freed and re-allocated at the
 // same address (mmap reuse) between calls, buffers that share a page,
@@ -30,9 +30,9 @@ static int g_fail = 0;
     }                                                              \
   } while (0)
 
-// The runtime as the engine sees it: a set of registered page ranges (a
-// registration must not overlap another), plus ranges pinned by "another
-// allocator" (hipHostMalloc'd by someone else).
+// The runtime as the engine sees it: a set of registered byte ranges (a
+// registration must not overlap another's bytes; ranges may share a page),
+// plus ranges pinned by "another allocator" (hipHostMalloc'd by someone else).
 struct FakeRuntime final : PinBackend {
   std::set<std::pair<uintptr_t, uintptr_t>> regs, foreign;
   int nreg = 0, nunreg = 0, fail_unreg = 0, fail_reg = 0;
@@ -42,7 +42,6 @@ struct FakeRuntime final : PinBackend {
     return false;
   }
   int reg(uintptr_t p, size_t n) override {
-    if (p % 4096 || n % 4096) return kFail;  // the registry only asks for whole pages
     if (fail_reg) return kFail;
     if (overlaps(regs, p, p + n) || overlaps(foreign, p, p + n)) return pinned_elsewhere(p) ? kAlready : kFail;
     regs.insert({p, p + n});
@@ -70,6 +69,11 @@ struct FakeRuntime final : PinBackend {
       if (r.first <= p && p + n <= r.second) return true;
     for (auto &r : foreign)
       if (r.first <= p && p + n <= r.second) return true;
+    return false;
+  }
+  bool in_reg(uintptr_t p) const {  // the runtime would treat byte p as registered
+    for (auto &r : regs)
+      if (r.first <= p && p < r.second) return true;
     return false;
   }
   bool pinned(uintptr_t p, size_t n) const {  // every byte in a registration
@@ -135,6 +139,10 @@ int main() {
           rt.dma_ok(uintptr_t(buf) + 10103, 375));
     auto e = reg.entries();
     CHECK(e.size() == 1 && e[0].second.refs == 1);
+    // the pages' other bytes (a heap neighbour: the engine's own pageable
+    // staging vector) stay outside every registration -- a copy from there
+    // must not be taken for a registered one that runs past its end
+    CHECK(!rt.in_reg(uintptr_t(buf) + 99) && !rt.in_reg(uintptr_t(buf) + 10478) && !rt.in_reg(uintptr_t(buf)));
     CHECK(s.release() == 0);
     CHECK(rt.regs.empty() && reg.entries().empty());
     // buffers on separate pages of one call: separate registrations
@@ -240,6 +248,20 @@ int main() {
     auto e = reg.entries();
     CHECK(e.size() == 1 && e[0].second.refs == 1);
     CHECK(a.release() == 0);
+    CHECK(rt.regs.empty() && reg.entries().empty());
+  }
+
+  // 8b. two calls whose buffers share a page but no byte: separate
+  //     registrations, each DMA inside its own, released independently
+  {
+    alignas(4096) static uint8_t buf[4 * 4096];
+    PinRegistry::Scope a(reg), b(reg);
+    CHECK(a.acquire(buf + 16, 5000) == 0);
+    CHECK(b.acquire(buf + 5016, 7000) == 0);
+    CHECK(rt.regs.size() == 2 && rt.dma_ok(uintptr_t(buf) + 16, 5000) && rt.dma_ok(uintptr_t(buf) + 5016, 7000));
+    CHECK(a.release() == 0);
+    CHECK(rt.regs.size() == 1 && rt.dma_ok(uintptr_t(buf) + 5016, 7000));
+    CHECK(b.release() == 0);
     CHECK(rt.regs.empty() && reg.entries().empty());
   }
 

@@ -4,8 +4,8 @@ Round 2's one unexplained GPU fault (hipErrorIllegalAddress in the first
 H2D copy of a test that followed host-path packet calls on a pageable
 buffer) pointed at the engine's host registrations: "pinned already?" was
 answered by the runtime for any address, and a failed hipHostUnregister was
-dropped.  The engine now keeps its own registry (engine allocations, page-
-rounded refcounted registrations per call, checked unregistration, streams
+dropped.  The engine now keeps its own registry (engine allocations,
+refcounted registrations of each call's exact bytes, checked unregistration, streams
 drained before unpinning on every return path).
 
 CPU: the registry's bookkeeping against a fake runtime

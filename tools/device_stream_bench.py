@@ -24,6 +24,13 @@ elif os.environ.get("DSB_DIAG"):  # the diagnostic build (takes HDFS_CRC32C_* kn
     lib = h.load(diaglib.DIAG_LIB_PATH)
 else:
     lib = h.load()
+# DSB_OLD_COPY: a round-2 build (verify_packets_copy without the read window)
+OLD_COPY = bool(os.environ.get("DSB_OLD_COPY"))
+if OLD_COPY:
+    _P = ctypes.POINTER
+    lib.hdfs_crc32c_verify_packets_copy.argtypes = [
+        ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_uint32, ctypes.c_int, _P(h.abi.Packet), ctypes.c_size_t,
+        _P(ctypes.c_size_t), _P(ctypes.c_uint64), ctypes.c_void_p, ctypes.c_uint64, _P(ctypes.c_uint64)]
 
 
 def wire_image(nbytes, seed):
@@ -48,7 +55,8 @@ def timed(ptr, n, npk, reps=5, fn="hdfs_crc32c_verify_packets", dst=None):
     for i in range(reps + 1):  # the first call is a warm-up (buffer growth, clocks)
         t0 = time.perf_counter()
         if dst is not None:  # verify + fused copy-out
-            rc = lib.hdfs_crc32c_verify_packets_copy(ptr, n, h.PROTO_V2, 512, h.CSUM_CRC32C, 0, h.READ_ALL, arr, npk + 8,
+            win = () if OLD_COPY else (0, h.READ_ALL)
+            rc = lib.hdfs_crc32c_verify_packets_copy(ptr, n, h.PROTO_V2, 512, h.CSUM_CRC32C, *win, arr, npk + 8,
                                                      ctypes.byref(cnt), ctypes.byref(used), dst.ptr, dst.nbytes,
                                                      ctypes.byref(got))
         else:
