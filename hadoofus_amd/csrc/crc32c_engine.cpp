@@ -848,6 +848,18 @@ int chunk_crcs_to_host(const void *data, uint64_t len, uint32_t cs, int ctype, u
   std::abort();
 }
 
+int device_checks(const char *call) {
+  if (!kDiag) return HDFS_CRC32C_OK;
+  static const char *const kName[] = {"check self-test", "frame_grid_kernel", "grid_build_kernel", "header_window_kernel",
+                                      "small_run_kernel", "grid_finalize_kernel"};
+  uint32_t v[3];
+  const hipError_t e = read_device_checks(v, 1);
+  if (e != hipSuccess) return fail(HDFS_CRC32C_EHIP, "%s: reading the device checks: %s", call, hipGetErrorString(e));
+  if (!v[2]) return HDFS_CRC32C_OK;
+  return fail(HDFS_CRC32C_EHIP, "%s: device check failed in %s at crc32c_kernels.hip:%u (%u violations)", call,
+              kName[v[0] < 6 ? v[0] : 0], v[1], v[2]);
+}
+
 }  // namespace hdfs_crc32c
 
 using namespace hdfs_crc32c;
@@ -1457,18 +1469,6 @@ int hdfs_crc32c_mailbox_destroy(hdfs_crc32c_mailbox *mb) {
   c.mb_alive = false;
   HIPCHK(hipStreamSynchronize(c.mb_stream));
   return HDFS_CRC32C_OK;
-}
-
-int device_checks(const char *call) {
-  if (!kDiag) return HDFS_CRC32C_OK;
-  static const char *const kName[] = {"check self-test", "frame_grid_kernel", "grid_build_kernel", "header_window_kernel",
-                                      "small_run_kernel", "grid_finalize_kernel"};
-  uint32_t v[3];
-  const hipError_t e = read_device_checks(v, 1);
-  if (e != hipSuccess) return fail(HDFS_CRC32C_EHIP, "%s: reading the device checks: %s", call, hipGetErrorString(e));
-  if (!v[2]) return HDFS_CRC32C_OK;
-  return fail(HDFS_CRC32C_EHIP, "%s: device check failed in %s at crc32c_kernels.hip:%u (%u violations)", call,
-              kName[v[0] < 6 ? v[0] : 0], v[1], v[2]);
 }
 
 #ifdef HDFS_CRC32C_DIAG

@@ -1,5 +1,6 @@
 """CPU tests of the C-ABI boundary: the library builds, loads, exports every
 symbol include/*.h declares, and fails loudly (no CPU fallback) without a GPU."""
+import ctypes
 import os
 import re
 import subprocess
@@ -215,3 +216,13 @@ def test_struct_layouts_match_c(tmp_path):
     got = [int(x) for x in subprocess.check_output([str(exe)], text=True).split()]
     assert got == [ctypes.sizeof(OutPacket), OutPacket.data_len.offset, OutPacket.crc_len.offset,
                    OutPacket.last.offset, ctypes.sizeof(Packet), ctypes.sizeof(Segment)]
+
+
+def test_both_libraries_load_and_bind(libpath, diagpath):
+    """Both builds dlopen with every symbol resolved (RTLD_NOW, as the
+    diagnostic build is loaded by tools and tests on the GPU box) and bind
+    every function their headers declare."""
+    from hadoofus_amd import abi
+    mode = os.RTLD_NOW | os.RTLD_LOCAL
+    abi.bind_product(ctypes.CDLL(libpath, mode=mode))
+    abi.bind_diag(abi.bind_product(ctypes.CDLL(diagpath, mode=mode)))
