@@ -23,7 +23,21 @@ struct DiagEP : ReleaseEP {
   DEV static bool drop(uint32_t pol) { return pol == 2u; }
   // 20: the gather kernel with its slot protocol skipped and every CRC store
   // dropped (what the protocol itself costs)
-  DEV static bool gather_off(uint32_t pol) { return pol == 20u; }
+  // 26 / 27 / 28: as 20, plus a workgroup barrier every 1 / 2 / 4 iterations
+  // of the round loop (3 / 6 / 12 rounds) -- what a barrier-flushed gather (no
+  // slot protocol; CRCs staged in LDS and written behind a barrier) would pay
+  // for its barriers alone.  Never combined with the slot protocol: a wave
+  // waiting for a slot while the slot's finisher waits at the barrier is a
+  // deadlock (the protocol's spin limit traps it, as a first probe found).
+  // A wave that has left the loop no longer counts for s_barrier.
+  DEV static bool gather_off(uint32_t pol) { return pol == 20u || (pol >= 26u && pol <= 28u); }
+  DEV static void loop_hook(uint32_t pol, uint32_t it) {
+    if (pol >= 26u && pol <= 28u && (it & ((1u << (pol - 26u)) - 1u)) == 0u) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    }
+  }
   DEV static const uint32_t *group_base(uint32_t pol, const uint32_t *b, const SegHot &sh, uint32_t gt) {
     if (pol == 14u) {
       // the group's 256 B land at a scattered group position of the segment

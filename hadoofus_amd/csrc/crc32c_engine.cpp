@@ -259,22 +259,22 @@ bool device_accessible(const void *p) {
 int launch_verify_dyn(DevCtx &c, const SegDev *d_segs, const GridSummary *dyn, uint64_t rounds_ub, uint64_t gtiles_ub,
                       uint32_t *d_fb, unsigned long long *d_mism, uint32_t *d_gctr, hipStream_t st, int ctype,
                       bool copy) {
-  // grid from the upper bound of the run's rounds (>= 4 rounds per wave
-  // before adding workgroups, as launch_all): a short run must not make 256
-  // workgroups fill their 156 KiB LDS tables for a handful of tiles
-  const uint64_t want = (rounds_ub + 63) / 64;
+  // grid from the upper bounds of the run's rounds (>= 4 rounds per wave
+  // before adding workgroups, as launch_all) and generic tiles (>= 4 claims
+  // of 8 per wave): a short run must not make 256 workgroups fill their
+  // 156 KiB LDS tables for a handful of tiles
+  const uint64_t want = std::max((rounds_ub + 63) / 64, (gtiles_ub + 511) / 512);
   const int grid = int(want < 1 ? 1 : (want > uint64_t(c.bulk_cus()) ? c.bulk_cus() : want));
-  (void)d_gctr;  // zeroed by grid_build_kernel
+  (void)d_gctr;  // zeroed by frame_build_kernel
   // schedule 3: a device-framed run is packets of one wire size, so its table
   // is uniform (dyn->utiles, no segment search per tile); the kernel falls
   // back to searching the table when it is not
   const hipError_t le = launch_tiles(kModeVerify, 3, g_nt_loads, 3, 1, 1024, grid, d_segs, 0, 0, 0,
                                      c.d_tab_main_t[ctype], d_fb, d_mism, nullptr,
                                      (kDiag ? g_store_policy : 0u) | (g_group_shift << 8) | (g_xcd_major << 12), d_gctr,
-                                     st, copy ? 1 : 0, 1, dyn);
+                                     st, copy ? 1 : 0, 1, dyn, 0u, 1);
   if (le == hipErrorInvalidValue) return fail(HDFS_CRC32C_EINVAL, "verify kernel shape not built");
   HIPCHK(le);
-  HIPCHK(launch_generic(kModeVerify, d_segs, 0, gtiles_ub, c.d_tab_main_t[ctype], d_fb, d_mism, st, dyn));
   return HDFS_CRC32C_OK;
 }
 
@@ -850,7 +850,7 @@ int chunk_crcs_to_host(const void *data, uint64_t len, uint32_t cs, int ctype, u
 
 int device_checks(const char *call) {
   if (!kDiag) return HDFS_CRC32C_OK;
-  static const char *const kName[] = {"check self-test", "frame_grid_kernel", "grid_build_kernel", "header_window_kernel",
+  static const char *const kName[] = {"check self-test", "frame_build_kernel (framing)", "frame_build_kernel (table)", "header_window_kernel",
                                       "small_run_kernel", "grid_finalize_kernel"};
   uint32_t v[3];
   const hipError_t e = read_device_checks(v, 1);
@@ -1481,7 +1481,7 @@ int hdfs_crc32c_diag_device_checks(uint32_t *out3, int reset) {
 }
 
 int hdfs_crc32c_set_store_policy(int policy) {
-  if (policy < 0 || policy > 25) return fail(HDFS_CRC32C_EINVAL, "store policy 0..25");
+  if (policy < 0 || policy > 28) return fail(HDFS_CRC32C_EINVAL, "store policy 0..28");
   g_store_policy = uint32_t(policy);
   return HDFS_CRC32C_OK;
 }

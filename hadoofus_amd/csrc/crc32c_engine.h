@@ -22,7 +22,8 @@ hipError_t launch_tiles(int mode, int order, int nt, int depth, int streams, int
                         const SegDev *segs, uint32_t nseg, uint64_t total_rounds, uint64_t total_tiles,
                         const uint32_t *gtab, uint32_t *first_bad, unsigned long long *mism,
                         unsigned long long *diag, uint32_t tune, uint32_t *gctr, hipStream_t stream,
-                        int copy = 0, int una = 0, const GridSummary *dyn = nullptr, uint32_t utiles = 0);
+                        int copy = 0, int una = 0, const GridSummary *dyn = nullptr, uint32_t utiles = 0,
+                        int fuse_generic = 0);
 hipError_t launch_probe_read(const uint8_t *p, uint64_t nbytes, uint32_t *out, int grid, int block, int variant,
                              hipStream_t stream);
 hipError_t launch_generic(int mode, const SegDev *segs, uint32_t nseg, uint64_t total_gtiles,
@@ -52,7 +53,7 @@ hipError_t launch_header_window(const uint8_t *s, uint64_t len, uint64_t base, u
                                 int proto, uint8_t *out, uint64_t *stride_out, hipStream_t stream);
 
 // device framing of device-resident packet streams (crc32c_kernels.hip)
-// frame_grid_kernel + grid_build_kernel: one device framing pass.
+// frame_build_kernel: one device framing pass (framing, scan, segment table).
 // Short device-resident run in one launch (count <= kSmallRunMax grid
 // points, one workgroup each); hout: pinned host slots (device address),
 // kSrHostBytes.
@@ -243,10 +244,11 @@ bool whole_groups(const SegDev *segs, size_t n);
 // Main tiles per segment when the table is uniform (every segment but the
 // last has the same main_tiles T, the last at most T), else 0.
 uint32_t uniform_tiles(const SegDev *segs, size_t n);
-// Verify pass over a segment table built on the device (grid_build_kernel):
-// sizes read by the kernels from *dyn; grid sized for rounds_ub / gtiles_ub
+// Verify pass over a segment table built on the device (frame_build_kernel):
+// sizes read by the kernel from *dyn; grid sized for rounds_ub / gtiles_ub
 // (upper bounds).  Schedule 3 with the uniform-table look-up the summary
-// enables for runs of equal packets, realigning kernel.
+// enables for runs of equal packets, realigning kernel; the run's generic
+// tiles in the same launch.
 int launch_verify_dyn(DevCtx &c, const SegDev *d_segs, const GridSummary *dyn, uint64_t rounds_ub, uint64_t gtiles_ub,
                       uint32_t *d_fb, unsigned long long *d_mism, uint32_t *d_gctr, hipStream_t st, int ctype,
                       bool copy);

@@ -1,5 +1,5 @@
 // Packet framing shared by the host walk (crc32c_packets.cpp) and the
-// device framing kernel (crc32c_kernels.hip, frame_grid_kernel): ONE source
+// device framing kernel (crc32c_kernels.hip, frame_build_kernel): ONE source
 // for the sequential part of _recv_packet / _process_recv_packet
 // (src/datanode.c:2345-2446), so a packet framed on the GPU gets exactly the
 // record the host walk would give it.

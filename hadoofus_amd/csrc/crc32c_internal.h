@@ -25,7 +25,7 @@ enum DevCheckKernel : uint32_t {
   kDkGridBuild = 2,
   kDkHeaderWindow = 3,
   kDkSmallRun = 4,
-  kDkGridFinalize = 5,
+  kDkFinalize = 5,
 };
 
 // Segment flags (also mirrored as HDFS_CRC32C_SEG_* in the public header).
@@ -67,8 +67,8 @@ struct SegDev {
 };
 static_assert(sizeof(SegDev) == 96, "SegDev layout");
 
-// Device framing of a device-resident packet stream (frame_grid_kernel ->
-// grid_scan_kernel): packets at base + k * stride, stride = the wire size of
+// Device framing of a device-resident packet stream (frame_build_kernel):
+// packets at base + k * stride, stride = the wire size of
 // the packet at base.  Status per grid point k:
 enum : uint32_t {
   kGridOn = 0,    // complete, framing-clean, wire size == stride: the walk goes on at k + 1
@@ -89,8 +89,8 @@ struct GridSummary {
   uint64_t bm_bytes;     // bitmap bytes of the segment table
   uint32_t nbad;         // verify: packets with bad chunks (grid_finalize_kernel)
   uint32_t unaligned;    // some tiled segment's data is not 4-B aligned (realigning kernel)
-  uint32_t seq;          // host copy only: written last (after a system fence) by grid_build_kernel
-  uint32_t nonuni;       // some segment breaks the uniform layout (OR-ed by grid_build_kernel)
+  uint32_t seq;          // host copy only: written last (after a system fence) by frame_build_kernel
+  uint32_t nonuni;       // some segment breaks the uniform layout (OR-ed by frame_build_kernel)
   uint32_t utiles;       // main tiles per segment of a uniform table (0: not uniform), for the verify kernel
   uint32_t nexc;         // recorded packets whose record differs from the prediction from packet 0
 };
@@ -111,24 +111,22 @@ constexpr uint32_t kGridHostBytes = kGridHostExc + kExcMax * kGridRecBytes;
 // Device tables of one framing pass (count grid points).
 struct GridBufs {
   ::hdfs_crc32c_packet *recs;  // [count] records
-  uint32_t *status;            // [count] kGrid*
-  void *contrib;               // [count] per-packet shares of the segment table (24 B each)
-  uint64_t *blk_sum;           // [blocks][6] block sums of the shares
-  uint32_t *blk_min;           // [blocks] first grid point of the block that is not kGridOn
+  void *look;                  // [blocks] look-back records of the scan (kGridLookBytes each; zeroed when allocated)
   SegDev *segs;                // [count] verify segments
   uint32_t *seg2pkt;           // [count] segment -> grid point
   uint32_t *fb;                // [count] first bad chunk per segment
-  uint32_t *gctr;              // tiled-kernel pool counter (zeroed by grid_build_kernel)
-  uint32_t *done;              // [2]: grid_build blocks finished, exceptions found (zeroed by frame_grid_kernel)
+  uint32_t *gctr;              // tiled-kernel pool counter (zeroed by frame_build_kernel)
+  uint32_t *done;              // [2]: blocks finished, exceptions found (reset by block 0 of the pass)
   uint32_t *exc;               // [count] grid indices of the exceptions
   GridSummary *sum;
   // pinned host memory mapped into the device: the summary, packet 0's
-  // record and the exceptions (kGridHost*) are written there by the last
-  // grid_build block (no copy launch, which would queue behind the verify
-  // kernel for CUs)
+  // record and the exceptions (kGridHost*) are written there by the pass's
+  // last block (no copy launch, which would queue behind the verify kernel
+  // for CUs)
   uint8_t *hsum;
-  uint32_t seq;                // written to the host summary's seq once the area is complete
+  uint32_t seq;                // written to the host summary's seq once the area is complete (> 0)
 };
+constexpr uint32_t kGridLookBytes = 256;
 
 // Compact verify verdict of one packet (grid_finalize_kernel).
 struct GridBad {
@@ -137,6 +135,7 @@ struct GridBad {
   uint32_t bad_chunks;
   uint32_t pad;
 };
+
 
 // LDS image of the tiled kernel (bytes).
 //  [0, 128 KiB)          slicing-by-4 tables, each replicated 32x so that

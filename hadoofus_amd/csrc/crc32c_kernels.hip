@@ -406,6 +406,8 @@ struct ReleaseEP {
   DEV static bool drop(uint32_t) { return false; }
   // compute gather: the slot protocol skipped, its stores dropped
   DEV static bool gather_off(uint32_t) { return false; }
+  // once per iteration of the round loop (diagnostic barrier probes)
+  DEV static void loop_hook(uint32_t, uint32_t) {}
   // compute gather: where a whole group's 256 B go
   DEV static const uint32_t *group_base(uint32_t, const uint32_t *b, const SegHot &, uint32_t) { return b; }
   // compute gather: nt (pipelined gather kernel, one process: sc1 6 797,
@@ -906,6 +908,141 @@ DEV void process(const uint32_t *lds, uint32_t (&d)[S][16], const uint32_t (&exp
   for (int s = 0; s < S; s++) finish<MODE, RUN, P>(lds, exp[s], c[s], segs, st[s], L, first_bad, mism, kc[s], gs[s]);
 }
 
+// Generic tiles inside a device-framed verify launch.  One lane per
+// chunk of a generic tile, as crc32c_generic_kernel, but on the tiled
+// kernel's replicated LDS tables (lane l reads its own copy: lb0 / lb1).
+// gt: the lane's generic tile of the run (8 lanes per tile).
+DEV void fused_generic_chunk(const uint32_t *lds, const SegDev *__restrict__ segs, uint32_t nseg, uint64_t gt,
+                             bool active, const LaneConst &L, uint32_t *__restrict__ first_bad,
+                             unsigned long long *__restrict__ mism) {
+  const uint32_t g = L.lane & 7u;
+  uint32_t s = 0, tile = 0, chunk = 0, out = 0, flags = 0;
+  bool valid = false;
+  if (active) {
+    uint32_t lo = 0, hi = nseg;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (segs[mid].gtile_start <= gt) lo = mid; else hi = mid;
+    }
+    s = lo;
+    const SegDev &sg = segs[s];
+    tile = sg.main_tiles + static_cast<uint32_t>(gt - sg.gtile_start);
+    chunk = tile * kTileChunks + g;
+    flags = sg.flags;
+    valid = chunk < sg.nchunks;
+    if (valid) {
+      const uint64_t off = static_cast<uint64_t>(chunk) * sg.chunk_size;
+      const uint8_t *p = sg.data + off;
+      uint64_t n = min(static_cast<uint64_t>(sg.chunk_size), sg.len - off);
+      if (sg.copy_dst) {  // verify + copy-out: the chunk's bytes inside the window
+        const uint64_t a = max<uint64_t>(off, sg.copy_w0), e = min<uint64_t>(off + n, sg.copy_w1);
+        for (uint64_t j = a; j < e; j++) gstore8(sg.copy_dst + (j - sg.copy_w0), gload8(sg.data + j));
+      }
+      uint32_t c = sg.reg_init;
+      // byte steps on t0 (pair 1, half 1 of the image), word steps by slice4
+      while (n && (reinterpret_cast<uintptr_t>(p) & 3u)) {
+        c = lds_at(lds, L.lb1 + 128u + (((c ^ gload8(p++)) & 0xffu) << 8)) ^ (c >> 8);
+        n--;
+      }
+      while (n >= 4) {
+        c = slice4(lds, c ^ gload32(p), 0u, L.lb0, L.lb1);
+        p += 4;
+        n -= 4;
+      }
+      while (n) {
+        c = lds_at(lds, L.lb1 + 128u + (((c ^ gload8(p++)) & 0xffu) << 8)) ^ (c >> 8);
+        n--;
+      }
+      out = (flags & kSegRaw) ? c : ~c;
+    }
+  }
+  bool bad = false;
+  if (valid) {
+    uint32_t e = gload32(segs[s].crcs + chunk);
+    if (flags & kSegBigEndian) e = __builtin_bswap32(e);
+    bad = e != out;
+  }
+  const uint64_t m = __ballot(bad);
+  if (active && g == 0) {
+    const uint32_t byte = static_cast<uint32_t>((m >> (L.lane & 56u)) & 0xffu);
+    gstore8(segs[s].bitmap + tile, static_cast<uint8_t>(byte));
+    if (byte) {
+      atomicMin(&first_bad[s], tile * kTileChunks + __builtin_ctz(byte));
+      atomicAdd(mism, static_cast<unsigned long long>(__builtin_popcount(byte)));
+    }
+  }
+}
+
+// The bad-packet list of a verified run (one workgroup of BLOCK threads):
+// every segment with a bad chunk -> one GridBad (packet, first bad chunk,
+// bad chunks from its bitmap), to the device list and the first host_cap to
+// pinned host memory, the count, then (one system fence later) the sequence
+// number the host polls.  nb: an LDS word.
+template <int BLOCK>
+DEV void bad_list(const SegDev *__restrict__ segs, uint32_t nseg, const uint32_t *__restrict__ seg2pkt,
+                  const uint32_t *__restrict__ fb, GridBad *__restrict__ bad, uint32_t bad_cap,
+                  GridSummary *__restrict__ sum, uint8_t *__restrict__ hsum2, uint32_t host_cap, uint32_t seq,
+                  uint32_t *nb) {
+  if (threadIdx.x == 0) *nb = 0u;
+  __syncthreads();
+  auto *hbad = reinterpret_cast<GridBad *>(hsum2 + 256);
+  // first-bad words in batches of 16 per thread, every load of a batch issued
+  // before the first is tested (16 K segments: one round trip, not 16)
+  for (uint32_t i0 = threadIdx.x; i0 < nseg; i0 += 16u * BLOCK) {
+    uint32_t f[16];
+#pragma unroll
+    for (uint32_t u = 0; u < 16; u++) f[u] = i0 + u * BLOCK < nseg ? fb[i0 + u * BLOCK] : 0xFFFFFFFFu;
+#pragma unroll
+    for (uint32_t u = 0; u < 16; u++) {
+      if (f[u] == 0xFFFFFFFFu) continue;  // rare: a segment with a bad chunk
+      const uint32_t i = i0 + u * BLOCK;
+      const SegDev d = segs[i];
+      const uint32_t nbyte = (d.nchunks + 7u) / 8u;
+      uint32_t n = 0;
+      for (uint32_t j = 0; j < nbyte; j++) {
+        uint32_t byte = d.bitmap[j];
+        if (j == d.nchunks / 8u) byte &= (1u << (d.nchunks % 8u)) - 1u;  // bits past the last chunk
+        n += __builtin_popcount(byte);
+      }
+      const uint32_t slot = atomicAdd(nb, 1u);
+      const GridBad g{seg2pkt[i], int32_t(f[u]), n, 0u};
+      if (slot < bad_cap) bad[slot] = g;
+      if (slot < host_cap) hbad[slot] = g;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    sum->nbad = *nb;
+    reinterpret_cast<GridSummary *>(hsum2)->nbad = *nb;
+  }
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0)
+    __hip_atomic_store(&reinterpret_cast<GridSummary *>(hsum2)->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// The generic tiles of a device-framed run, taken by the verify launch's
+// own waves once they have no tiled round left: 8 tiles per wave and step,
+// dealt statically over the launch's waves (one atomic per wave on one
+// counter would serialise: 16 K waves cost ~50 us even with no generic tile
+// to take).  No completion protocol: the bad-packet list is the next launch
+// (grid_finalize_kernel), after the kernel boundary has made every bitmap
+// store visible -- a last-workgroup-done protocol here needed an agent-scope
+// fence (L2 write-back) per workgroup and cost more (+14 us per GiB) than
+// the launch it saved.
+template <int BLOCK>
+DEV void fused_generic(const uint32_t *lds, const SegDev *__restrict__ segs, const GridSummary *__restrict__ dyn,
+                       const LaneConst &L, uint32_t *__restrict__ first_bad, unsigned long long *__restrict__ mism) {
+  const uint32_t nseg = dyn->nseg;
+  const uint64_t ngt = dyn->gtiles;
+  const uint64_t nw = uint64_t(gridDim.x) * (BLOCK / 64);
+  const uint64_t wid = uint64_t(blockIdx.x) * (BLOCK / 64) + (threadIdx.x >> 6);
+  for (uint64_t g0 = wid * 8u; g0 < ngt; g0 += nw * 8u) {
+    const uint64_t gt = g0 + (L.lane >> 3);
+    fused_generic_chunk(lds, segs, nseg, gt, gt < ngt, L, first_bad, mism);
+  }
+}
+
 // Tiled kernel.  MODE compute / verify; ORDER schedule (above); NT
 // nontemporal data loads; DEPTH register round buffers per stream (DEPTH-1
 // rounds stay in flight while one is processed); S independent tile streams
@@ -917,10 +1054,12 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
     const SegDev *__restrict__ segs, uint32_t nseg, uint64_t total_rounds, uint64_t total_tiles,
     const uint32_t *__restrict__ gtab, uint32_t *__restrict__ first_bad,
     unsigned long long *__restrict__ mism, unsigned long long *__restrict__ diag, uint32_t tune,
-    uint32_t *__restrict__ gctr, const GridSummary *__restrict__ dyn, uint32_t utiles) {
+    uint32_t *__restrict__ gctr, const GridSummary *__restrict__ dyn, uint32_t utiles, uint32_t fuse) {
   static_assert(ORDER != 0 || S == 1, "static per-wave slices serve one stream");
+  // fused epilogue (verify with a device-built table only; uniform)
+  const bool fused = MODE == kModeVerify && dyn && fuse;
   static_assert(DEPTH >= 2 && DEPTH <= 4 && S >= 1 && S <= 4, "shape");
-  // dyn: sizes of a segment table built on the device (grid_build_kernel),
+  // dyn: sizes of a segment table built on the device (frame_build_kernel),
   // read here instead of passed by the host -- no host round trip between
   // framing and verify
   if (dyn) {
@@ -1099,6 +1238,8 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
 #pragma unroll
   for (int s = 0; s < S; s++) any |= cur[0][s].valid;
   if (!any) {
+    if constexpr (MODE == kModeVerify)
+      if (fused) fused_generic<BLOCK>(lds, segs, dyn, L, first_bad, mism);
     if (kDiag && diag && L.lane == 0) diag[3 * wave + 1] = __builtin_amdgcn_s_memrealtime();
     return;
   }
@@ -1145,7 +1286,8 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
                                 lo, kc[s], L.store_policy);
     }
   }
-  for (;;) {
+  for (uint32_t it = 0;; it++) {
+    EP::loop_hook(L.store_policy, it);
 #pragma unroll
     for (int k = 0; k < DEPTH; k++) {
       process<MODE, S, COPY, UNA, (ORDER == 4 && MODE == kModeCompute) ? 1 : GATHER == 2 ? 3 : GATHER ? 2 : 0>(
@@ -1172,6 +1314,8 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
       lazy_flush<EP>(gs[s], hot(kc[s], sg, cur[0][s].seg).h, L);
     }
   }
+  if constexpr (MODE == kModeVerify)
+    if (fused) fused_generic<BLOCK>(lds, segs, dyn, L, first_bad, mism);
   if (kDiag && diag && L.lane == 0) {
     diag[3 * wave + 1] = __builtin_amdgcn_s_memrealtime();
     diag[3 * wave + 2] = nrounds;
@@ -2029,7 +2173,11 @@ DEV int grid_frame(const uint8_t *s, uint64_t len, uint64_t pos, const uint8_t *
   const uint64_t rem = len - pos;
   const bool fits = rem >= kHdrWin && (proto == HDFS_CRC32C_PROTO_V1 ||
                                        6u + ((uint32_t(win[4]) << 8) | win[5]) <= kHdrWin);
-  return frame::frame_step(fits ? win : s + pos, rem, pos, proto, cs, ctype, r, total);
+  // two calls, not one on a selected pointer: each inlined copy then knows
+  // its address space (ds_read_u8 from the staged window instead of flat
+  // loads, which wait on both the LDS and the vector-memory counters)
+  if (fits) return frame::frame_step(win, rem, pos, proto, cs, ctype, r, total);
+  return frame::frame_step(s + pos, rem, pos, proto, cs, ctype, r, total);
 }
 
 // 64 threads (one wave) per block: a pass of 16 K packets spreads over all
@@ -2037,28 +2185,62 @@ DEV int grid_frame(const uint8_t *s, uint64_t len, uint64_t pos, const uint8_t *
 // matters less than CUs engaged)
 constexpr uint32_t kGridBlock = 64;
 
-__global__ __launch_bounds__(kGridBlock) void frame_grid_kernel(
+// One device framing pass in one launch: frame the grid points, then a
+// single-pass scan of their shares of the segment table over the blocks
+// (decoupled look-back: a block publishes its own sums at once and takes the
+// sums of the blocks before it from their published records, 64 at a time,
+// stopping at the nearest block whose inclusive prefix is out), then the
+// verify segment entries of the run's packets, the run's summary and, from
+// the last block to finish, the host copy.  Block b only waits for blocks
+// < b, which the dispatcher started before it, so the wait ends.
+// Look-back record of one block; flag = (pass seq << 2) | state, state 1:
+// agg / amin out, 2: inc / imin out too.  Tagging with the pass's sequence
+// number means no reset between passes (the area is zeroed once when it is
+// allocated; seqs start at 1).  Every field is written and read with
+// agent-scope relaxed atomics (write-through stores, loads past this XCD's
+// L2) and a record's flag is stored only after its fields' stores are
+// acknowledged (s_waitcnt vmcnt(0)): no L2 write-back or invalidate per
+// publish -- with an agent-scope fence per publish and per look-back window
+// the pass took 62 us instead of ~35.
+struct GridLook {
+  uint64_t agg[6];   // the block's shares of the recorded packets' table
+  uint64_t inc[6];   // shares of blocks 0..b
+  uint64_t mins;     // amin | imin << 32: first grid point that is not On (~0: none), in the block / blocks 0..b
+  uint64_t flag;
+  uint64_t rec0[7];  // block 0 only: packet 0's record (the prediction of the others)
+  uint64_t T;        // block 0 only: main tiles of packet 0's segment (the uniform layout's tiles per segment)
+  uint64_t pad[10];
+};
+static_assert(sizeof(GridLook) == kGridLookBytes, "look-back record");
+static_assert(sizeof(hdfs_crc32c_packet) == 7 * 8, "packet 0's record in the look-back area");
+
+DEV uint64_t at_ld(const uint64_t *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+DEV void at_st(uint64_t *p, uint64_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+DEV void at_st32(uint32_t *p, uint32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+// every store of this wave acknowledged (write-through stores: at the point
+// of coherence) before the next one
+DEV void stores_done() { __builtin_amdgcn_s_waitcnt(0x0F70); }  // s_waitcnt vmcnt(0)
+
+__global__ __launch_bounds__(kGridBlock) void frame_build_kernel(
     const uint8_t *__restrict__ s, uint64_t len, uint64_t base, uint32_t count, int proto, uint32_t cs, int ctype,
-    int verify, int rwin, int64_t client_offset, hdfs_crc32c_packet *__restrict__ recs, uint32_t *__restrict__ status,
-    GridContrib *__restrict__ contrib, uint64_t *__restrict__ blk_sum, uint32_t *__restrict__ blk_min,
-    GridSummary *__restrict__ sum, uint32_t *__restrict__ done) {
+    int verify, uint32_t sflags, uint8_t *__restrict__ bm_base, uint8_t *__restrict__ copy_base, uint64_t copy_cap,
+    int rwin, int64_t client_offset, hdfs_crc32c_packet *__restrict__ recs, GridLook *__restrict__ look,
+    SegDev *__restrict__ segs, uint32_t *__restrict__ seg2pkt, uint32_t *__restrict__ fb, uint32_t *__restrict__ gctr,
+    uint32_t *__restrict__ done, uint32_t *__restrict__ exc, GridSummary *__restrict__ sum, uint8_t *__restrict__ hsum,
+    uint32_t seq) {
+  static_assert(kGridBlock == 64, "one wave per block: the scans are wave-wide");
+  static_assert(sizeof(hdfs_crc32c_packet) == kGridRecBytes, "host record layout");
   __shared__ __attribute__((aligned(16))) uint8_t win[kGridBlock][kHdrWin];
-  __shared__ uint64_t red[6][kGridBlock / 64];
-  __shared__ uint32_t redm[kGridBlock / 64];
-  const uint32_t t = threadIdx.x, k = blockIdx.x * kGridBlock + t, lane = t & 63u, w = t >> 6;
-  // The stride from the first 6 bytes of the packet at base: header_len +
-  // plen - 4 is exactly the wire size frame_step gives a complete, clean
-  // packet, so no thread decodes packet 0's PacketHeaderProto just to find
-  // the grid.  If packet 0 is not such a packet its status ends the run
-  // (first_break = 0) and the other grid points are never read.
+  __shared__ uint32_t islast;
+  const uint32_t t = threadIdx.x, b = blockIdx.x, k = b * kGridBlock + t, lane = t;
+  const uint32_t nblk = gridDim.x;
+  const uint64_t tag = uint64_t(seq) << 2;
+  // 1. frame this thread's grid point.  The stride comes from the first 6
+  // bytes of the packet at base: header_len + plen - 4 is exactly the wire
+  // size frame_step gives a complete, clean packet, so no thread decodes
+  // packet 0's PacketHeaderProto just to find the grid.  If packet 0 is not
+  // such a packet its status ends the run (first_break = 0).
   const uint64_t stride = grid_stride(s, len, base, proto);
-  if (k == 0) {
-    sum->stride = stride;
-    sum->unaligned = 0u;  // OR-ed by grid_build_kernel
-    sum->nonuni = 0u;     // OR-ed by grid_build_kernel
-    done[0] = 0u;         // grid_build_kernel: blocks finished
-    done[1] = 0u;         // grid_build_kernel: exceptions found
-  }
   hdfs_crc32c_packet r{};
   uint64_t total = 0;
   uint32_t code = kGridMore;
@@ -2083,116 +2265,124 @@ __global__ __launch_bounds__(kGridBlock) void frame_grid_kernel(
       }
     }
   }
-  if (k < count && DCHK(count <= kGridMaxCount, kDkFrameGrid)) {
-    status[k] = code;
-    contrib[k] = a;
-  }
-  // block sums of the shares and the block's first grid point that is not On
+  const uint32_t mk = (k < count && code != kGridOn) ? k : 0xFFFFFFFFu;
+  // 2. the block's aggregate: shares of its grid points (a point past the
+  // run's end is excluded later, where the end is known) and its first point
+  // that is not On
   uint64_t v[6] = {a.nseg, a.rounds, a.mtiles, a.gtiles, a.bm, a.payload};
-  uint32_t m = (k < count && code != kGridOn) ? k : 0xFFFFFFFFu;
+  uint32_t m = mk;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
 #pragma unroll
     for (int q = 0; q < 6; q++) v[q] += __shfl_xor(v[q], off);
     m = min(m, static_cast<uint32_t>(__shfl_xor(static_cast<int>(m), off)));
   }
+  // Block 0 also publishes packet 0's record and resets the pass's counters
+  // before its flag: every other block waits for block 0's flag before it
+  // touches them.
   if (lane == 0) {
+    GridLook &L = look[b];
 #pragma unroll
-    for (int q = 0; q < 6; q++) red[q][w] = v[q];
-    redm[w] = m;
-  }
-  __syncthreads();
-  if (t < 6) {
-    uint64_t x = 0;
-    for (uint32_t j = 0; j < kGridBlock / 64; j++) x += red[t][j];
-    blk_sum[6 * blockIdx.x + t] = x;
-  }
-  if (t == 6) {
-    uint32_t x = 0xFFFFFFFFu;
-    for (uint32_t j = 0; j < kGridBlock / 64; j++) x = min(x, redm[j]);
-    blk_min[blockIdx.x] = x;
-  }
-}
-
-// Exclusive prefix of the shares, then the verify segment entries of the
-// run's packets and (one thread) the run's summary.  Same grid as
-// frame_grid_kernel; each block first reduces the other blocks' results.
-__global__ __launch_bounds__(kGridBlock) void grid_build_kernel(
-    const uint8_t *__restrict__ s, uint64_t base, uint32_t count, uint32_t nblk,
-    const hdfs_crc32c_packet *__restrict__ recs, const uint32_t *__restrict__ status,
-    const GridContrib *__restrict__ contrib, const uint64_t *__restrict__ blk_sum,
-    const uint32_t *__restrict__ blk_min, uint32_t cs, uint32_t sflags, uint8_t *__restrict__ bm_base,
-    uint8_t *__restrict__ copy_base, uint64_t copy_cap, int rwin, int64_t client_offset, SegDev *__restrict__ segs,
-    uint32_t *__restrict__ seg2pkt,
-    uint32_t *__restrict__ fb, uint32_t *__restrict__ gctr, uint32_t *__restrict__ done, uint32_t *__restrict__ exc,
-    GridSummary *__restrict__ sum, uint8_t *__restrict__ hsum, uint32_t seq) {
-  static_assert(sizeof(hdfs_crc32c_packet) == kGridRecBytes, "host record layout");
-  __shared__ uint64_t red[6][kGridBlock / 64];
-  __shared__ uint32_t redm[kGridBlock / 64];
-  __shared__ uint64_t pre[6];
-  __shared__ uint32_t islast;
-  const uint32_t t = threadIdx.x, b = blockIdx.x, k = b * kGridBlock + t, lane = t & 63u, w = t >> 6;
-  // 1. the run's end: the first grid point that is not On, over all blocks
-  // (at most kGridMaxCount / kGridBlock blocks: every load a thread needs is
-  // issued before the first is used -- one memory round trip, not one per
-  // block a thread covers)
-  constexpr uint32_t kPer = (kGridMaxCount / kGridBlock + kGridBlock - 1) / kGridBlock;
-  uint32_t m = 0xFFFFFFFFu;
-  {
-    uint32_t x[kPer];
+    for (int q = 0; q < 6; q++) at_st(&L.agg[q], v[q]);
+    if (b == 0) {
 #pragma unroll
-    for (uint32_t u = 0; u < kPer; u++) x[u] = t + u * kGridBlock < nblk ? blk_min[t + u * kGridBlock] : 0xFFFFFFFFu;
+      for (int q = 0; q < 6; q++) at_st(&L.inc[q], v[q]);
+      at_st(&L.mins, uint64_t(m) | (uint64_t(m) << 32));
+      const uint64_t *x = reinterpret_cast<const uint64_t *>(&r);
 #pragma unroll
-    for (uint32_t u = 0; u < kPer; u++) m = min(m, x[u]);
-  }
-  // 2. shares of the blocks before this one (batches of 4 blocks per thread)
-  uint64_t v[6] = {0, 0, 0, 0, 0, 0};
-  for (uint32_t j0 = t; j0 < b; j0 += 4u * kGridBlock) {
-    uint64_t x[4][6];
-#pragma unroll
-    for (uint32_t u = 0; u < 4; u++) {
-      const uint32_t j = j0 + u * kGridBlock;
-#pragma unroll
-      for (int q = 0; q < 6; q++) x[u][q] = j < b ? blk_sum[6 * j + q] : 0ull;
+      for (int q = 0; q < 7; q++) at_st(&L.rec0[q], x[q]);
+      at_st(&L.T, a.nseg ? a.mtiles : 0u);
+      at_st32(&sum->unaligned, 0u);
+      at_st32(&sum->nonuni, 0u);
+      at_st32(&done[0], 0u);  // blocks finished
+      at_st32(&done[1], 0u);  // exceptions found
+      sum->stride = stride;
+    } else {
+      at_st(&L.mins, uint64_t(m) | 0xFFFFFFFF00000000ull);
     }
-#pragma unroll
-    for (uint32_t u = 0; u < 4; u++)
-#pragma unroll
-      for (int q = 0; q < 6; q++) v[q] += x[u][q];
+    stores_done();
+    at_st(&L.flag, tag | (b == 0 ? 2u : 1u));
   }
+  // 3. look back: the shares and first break of blocks 0..b-1.  Lane i looks
+  // at block j0 - i; a window is used up to its nearest block with an
+  // inclusive prefix (that block's inc, the aggregates of the blocks after
+  // it), and read only when every block it needs has published.
+  uint64_t pre[6] = {0, 0, 0, 0, 0, 0};
+  uint32_t pmin = 0xFFFFFFFFu;
+  if (b > 0) {
+    for (int64_t j0 = int64_t(b) - 1; j0 >= 0; j0 -= 64) {
+      const int64_t j = j0 - int64_t(lane);
+      uint32_t state = 0, spins = 0;
+      uint64_t bal2 = 0, need = 0;
+      for (;;) {
+        const uint64_t f = j >= 0 ? at_ld(&look[j].flag) : (tag | 2u);  // before block 0: an empty inclusive prefix
+        state = (f >> 2) == uint64_t(seq) ? uint32_t(f & 3u) : 0u;
+        bal2 = __ballot(state == 2u);
+        const uint32_t lim = bal2 ? static_cast<uint32_t>(__builtin_ctzll(bal2)) : 63u;
+        need = lim == 63u ? ~0ull : ((2ull << lim) - 1ull);
+        if ((__ballot(state == 0u) & need) == 0ull) break;
+        if (++spins > (1u << 24)) {  // never expected (blocks < b run to their publish): fail loudly, see the gather
+          asm volatile("s_trap 2");
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      // (the fields are read after their flags: these loads issue only once
+      // the loop above has seen the flags)
+      const uint32_t lim = bal2 ? static_cast<uint32_t>(__builtin_ctzll(bal2)) : 63u;
+      uint64_t x[6] = {0, 0, 0, 0, 0, 0};
+      uint32_t xm = 0xFFFFFFFFu;
+      if (j >= 0 && ((need >> lane) & 1ull)) {
+        const GridLook &L = look[j];
+        const bool useinc = bal2 && lane == lim;
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
+        for (int q = 0; q < 6; q++) x[q] = at_ld(useinc ? &L.inc[q] : &L.agg[q]);
+        const uint64_t mm = at_ld(&L.mins);
+        xm = static_cast<uint32_t>(useinc ? mm >> 32 : mm);
+      }
 #pragma unroll
-    for (int q = 0; q < 6; q++) v[q] += __shfl_xor(v[q], off);
-    m = min(m, static_cast<uint32_t>(__shfl_xor(static_cast<int>(m), off)));
-  }
-  if (lane == 0) {
+      for (int off = 32; off > 0; off >>= 1) {
 #pragma unroll
-    for (int q = 0; q < 6; q++) red[q][w] = v[q];
-    redm[w] = m;
+        for (int q = 0; q < 6; q++) x[q] += __shfl_xor(x[q], off);
+        xm = min(xm, static_cast<uint32_t>(__shfl_xor(static_cast<int>(xm), off)));
+      }
+#pragma unroll
+      for (int q = 0; q < 6; q++) pre[q] += x[q];
+      pmin = min(pmin, xm);
+      if (bal2) break;
+    }
+    // publish the inclusive prefix for the blocks after this one
+    if (lane == 0) {
+      GridLook &L = look[b];
+#pragma unroll
+      for (int q = 0; q < 6; q++) at_st(&L.inc[q], pre[q] + v[q]);
+      at_st(&L.mins, uint64_t(m) | (uint64_t(min(pmin, m)) << 32));
+      stores_done();
+      at_st(&L.flag, tag | 2u);
+    }
+    // block 0's record (and its counter resets) before this block uses them
+    // (usually already seen through the look-back)
+    for (uint32_t spins = 0; (at_ld(&look[0].flag) >> 2) != uint64_t(seq);) {
+      if (++spins > (1u << 24)) {
+        asm volatile("s_trap 2");
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
   }
-  __syncthreads();
-  uint32_t fbk = 0xFFFFFFFFu;
-  for (uint32_t j = 0; j < kGridBlock / 64; j++) fbk = min(fbk, redm[j]);
-  fbk = min(fbk, count);
-  if (t < 6) {
-    uint64_t x = 0;
-    for (uint32_t j = 0; j < kGridBlock / 64; j++) x += red[t][j];
-    pre[t] = x;
-  }
-  const uint32_t st_fb = fbk < count ? status[fbk] : uint32_t(kGridOn);
-  const uint32_t recorded = fbk + (fbk < count && st_fb != kGridMore ? 1u : 0u);
-  const uint32_t last = recorded ? recorded - 1u : 0u;  // the packet whose block writes the summary
-  // the first segment's main tiles: the uniform layout's tiles per segment
-  // (a run with any segment has one at packet 0: a packet without CRCs ends it)
-  const GridContrib c0 = contrib[0];
-  const uint32_t T = c0.nseg ? c0.mtiles : 0u;
-  if (b * kGridBlock <= last) {  // uniform per block: blocks past the run only count themselves done
-    __syncthreads();
-    // 3. in-block exclusive scan of the shares of recorded packets
-    const GridContrib a = k < recorded ? contrib[k] : GridContrib{0u, 0u, 0u, 0u, 0u, 0u};
-    uint64_t incl[6] = {a.nseg, a.rounds, a.mtiles, a.gtiles, a.bm, a.payload};
-    const uint64_t own[6] = {a.nseg, a.rounds, a.mtiles, a.gtiles, a.bm, a.payload};
+  // 4. the run's end as this block sees it: the first point that is not On
+  // (before this block: the block is past the run; in it; or none up to
+  // here).  A point is recorded if it lies before the end, or is the end and
+  // was framed (Off / Stop).
+  const uint32_t fbk = min(min(pmin, m), count);
+  const bool past = pmin != 0xFFFFFFFFu;
+  const bool inrun = !past && (k < fbk || (k == fbk && k < count && code != kGridMore));
+  const uint32_t T = static_cast<uint32_t>(at_ld(&look[0].T));
+  if (!past) {
+    // in-block exclusive scan of the recorded points' shares
+    const uint64_t own[6] = {inrun ? a.nseg : 0u, inrun ? a.rounds : 0u, inrun ? a.mtiles : 0u,
+                             inrun ? a.gtiles : 0u, inrun ? a.bm : 0u, inrun ? uint64_t(a.payload) : 0u};
+    uint64_t incl[6] = {own[0], own[1], own[2], own[3], own[4], own[5]};
 #pragma unroll
     for (int q = 0; q < 6; q++) {
 #pragma unroll
@@ -2201,21 +2391,11 @@ __global__ __launch_bounds__(kGridBlock) void grid_build_kernel(
         if (lane >= off) incl[q] += o;
       }
     }
-    __syncthreads();
-    if (lane == 63) {
-#pragma unroll
-      for (int q = 0; q < 6; q++) red[q][w] = incl[q];
-    }
-    __syncthreads();
     uint64_t ex[6];
 #pragma unroll
-    for (int q = 0; q < 6; q++) {
-      ex[q] = pre[q] + incl[q] - own[q];
-      for (uint32_t j = 0; j < w; j++) ex[q] += red[q][j];
-    }
-    const hdfs_crc32c_packet r = k < recorded ? recs[k] : hdfs_crc32c_packet{};
-    // 4. the segment entry of a recorded packet with CRCs
-    if (k < recorded && a.nseg) {
+    for (int q = 0; q < 6; q++) ex[q] = pre[q] + incl[q] - own[q];
+    // the segment entry of a recorded packet with CRCs
+    if (inrun && a.nseg) {
       const uint32_t nch = uint32_t(r.crc_len) / 4u, ntiles = (nch + 7u) / 8u;
       const uint32_t sg = static_cast<uint32_t>(ex[0]);
       const uint8_t *crcp = s + r.stream_off + r.header_len;
@@ -2253,21 +2433,22 @@ __global__ __launch_bounds__(kGridBlock) void grid_build_kernel(
       }
     }
     // one atomic per wave that has a byte-unaligned tiled segment / a segment
-    // off the uniform layout (per-thread atomics on one word serialise: 16 K of
-    // them cost ~150 us)
+    // off the uniform layout (per-thread atomics on one word serialise)
     {
-      const bool una = k < recorded && a.nseg && a.mtiles &&
+      const bool una = inrun && a.nseg && a.mtiles &&
                        ((reinterpret_cast<uintptr_t>(s) + r.stream_off + r.header_len + uint32_t(r.crc_len)) & 3u);
       if (__ballot(una) && lane == 0) atomicOr(&sum->unaligned, 1u);
-      const bool off_layout = k < recorded && a.nseg && (ex[2] != ex[0] * T || a.mtiles > T);
+      const bool off_layout = inrun && a.nseg && (ex[2] != ex[0] * T || a.mtiles > T);
       if (__ballot(off_layout) && lane == 0) atomicOr(&sum->nonuni, 1u);
     }
-    // 5. records that differ from the prediction from packet 0 (wave-aggregated slots)
+    // records that differ from the prediction from packet 0 (wave-aggregated slots)
     {
-      const uint64_t stride = sum->stride;
       bool diff = false;
-      if (k >= 1 && k < recorded) {
-        hdfs_crc32c_packet p = recs[0];
+      if (k >= 1 && inrun) {
+        hdfs_crc32c_packet p;
+        uint64_t *px = reinterpret_cast<uint64_t *>(&p);
+#pragma unroll
+        for (int q = 0; q < 7; q++) px[q] = at_ld(&look[0].rec0[q]);
         p.stream_off = base + uint64_t(k) * stride;
         p.offset_in_block += int64_t(k) * p.data_len;
         p.seqno += int64_t(k);
@@ -2282,36 +2463,45 @@ __global__ __launch_bounds__(kGridBlock) void grid_build_kernel(
       const uint32_t ix = at + static_cast<uint32_t>(__builtin_popcountll(bal & ((1ull << lane) - 1ull)));
       if (diff && DCHK(ix < count, kDkGridBuild)) exc[ix] = k;
     }
-    // 6. the summary, from the thread of the run's last packet
-    if (k == last) {
-      const uint64_t stride = sum->stride;
+    // the summary, from the thread at the run's end (the break point, or the
+    // pass's last point when every point is On): the table's totals are this
+    // block's prefix plus its recorded points
+    uint64_t tot[6];
+#pragma unroll
+    for (int q = 0; q < 6; q++) tot[q] = pre[q] + static_cast<uint64_t>(__shfl(static_cast<long long>(incl[q]), 63));
+    if (fbk < count ? k == fbk : k == count - 1u) {
       uint64_t consumed, next;
+      uint32_t recorded, st_fb;
       if (fbk == count) {
         consumed = next = base + uint64_t(count) * stride;
-      } else if (st_fb == kGridMore) {
+        recorded = count;
+        st_fb = kGridOn;
+      } else if (code == kGridMore) {
         consumed = next = base + uint64_t(fbk) * stride;
+        recorded = fbk;
+        st_fb = code;
       } else {
-        const hdfs_crc32c_packet &rf = recs[fbk];
-        next = rf.stream_off + rf.header_len + uint64_t(rf.crc_len) + uint64_t(rf.data_len);
-        consumed = rf.error ? base + uint64_t(fbk) * stride : next;
+        next = r.stream_off + r.header_len + uint64_t(r.crc_len) + uint64_t(r.data_len);
+        consumed = r.error ? base + uint64_t(fbk) * stride : next;
+        recorded = fbk + 1u;
+        st_fb = code;
       }
-      const bool any = recorded > 0;
       sum->first_break = fbk;
       sum->recorded = recorded;
       sum->last_status = st_fb;
-      sum->nseg = any ? static_cast<uint32_t>(ex[0] + own[0]) : 0u;
-      sum->rounds = any ? ex[1] + own[1] : 0u;
-      sum->mtiles = any ? ex[2] + own[2] : 0u;
-      sum->gtiles = any ? ex[3] + own[3] : 0u;
-      sum->bm_bytes = any ? ex[4] + own[4] : 0u;
-      sum->payload = any ? ex[5] + own[5] : 0u;
+      sum->nseg = static_cast<uint32_t>(tot[0]);
+      sum->rounds = tot[1];
+      sum->mtiles = tot[2];
+      sum->gtiles = tot[3];
+      sum->bm_bytes = tot[4];
+      sum->payload = tot[5];
       sum->consumed = consumed;
       sum->next_pos = next;
       sum->nbad = 0;
-      *gctr = 0u;  // the verify launch's pool counter (no separate reset launch)
+      *gctr = 0u;    // the verify launch's pool counter (no separate reset launch)
     }
   }
-  // 7. the last block to finish publishes the summary, packet 0's record and
+  // 5. the last block to finish publishes the summary, packet 0's record and
   // the exceptions to pinned host memory, then (one system-scope fence later)
   // the sequence number the host polls.  The barrier makes every wave's
   // stores complete (workgroup release: they are in this XCD's L2); ONE
@@ -2363,44 +2553,9 @@ __global__ __launch_bounds__(1024) void grid_finalize_kernel(const SegDev *__res
                                                              GridSummary *__restrict__ sum, uint8_t *__restrict__ hsum2,
                                                              uint32_t host_cap, uint32_t seq) {
   __shared__ uint32_t nb;
-  if (threadIdx.x == 0) nb = 0u;
-  __syncthreads();
   if (nseg == 0xFFFFFFFFu) nseg = sum->nseg;  // launched before the host knows the run's size
-  if (!DCHK(nseg <= bad_cap, kDkGridFinalize)) nseg = bad_cap;  // one segment per packet of the pass
-  auto *hbad = reinterpret_cast<GridBad *>(hsum2 + 256);
-  // first-bad words in batches of 16 per thread, every load of a batch issued
-  // before the first is tested (16 K segments: one round trip, not 16)
-  for (uint32_t i0 = threadIdx.x; i0 < nseg; i0 += 16u * 1024u) {
-    uint32_t f[16];
-#pragma unroll
-    for (uint32_t u = 0; u < 16; u++) f[u] = i0 + u * 1024u < nseg ? fb[i0 + u * 1024u] : 0xFFFFFFFFu;
-#pragma unroll
-    for (uint32_t u = 0; u < 16; u++) {
-      if (f[u] == 0xFFFFFFFFu) continue;  // rare: a segment with a bad chunk
-      const uint32_t i = i0 + u * 1024u;
-      const SegDev d = segs[i];
-      const uint32_t nbyte = (d.nchunks + 7u) / 8u;
-      uint32_t n = 0;
-      for (uint32_t j = 0; j < nbyte; j++) {
-        uint32_t byte = d.bitmap[j];
-        if (j == d.nchunks / 8u) byte &= (1u << (d.nchunks % 8u)) - 1u;  // bits past the last chunk
-        n += __builtin_popcount(byte);
-      }
-      const uint32_t slot = atomicAdd(&nb, 1u);
-      const GridBad g{seg2pkt[i], int32_t(f[u]), n, 0u};
-      if (slot < bad_cap) bad[slot] = g;
-      if (slot < host_cap) hbad[slot] = g;
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    sum->nbad = nb;
-    reinterpret_cast<GridSummary *>(hsum2)->nbad = nb;
-  }
-  __threadfence_system();
-  __syncthreads();
-  if (threadIdx.x == 0)
-    __hip_atomic_store(&reinterpret_cast<GridSummary *>(hsum2)->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (!DCHK(nseg <= bad_cap, kDkFinalize)) nseg = bad_cap;  // one segment per packet of the pass
+  bad_list<1024>(segs, nseg, seg2pkt, fb, bad, bad_cap, sum, hsum2, host_cap, seq, &nb);
 }
 
 // Short device-resident runs in one launch (the per-read case of a
@@ -2411,7 +2566,7 @@ __global__ __launch_bounds__(1024) void grid_finalize_kernel(const SegDev *__res
 // piece per thread from HBM, slicing tables and the zeros operators it can
 // need in LDS, pieces shifted to their chunk's end and XOR-ed per chunk
 // (small_chunks_kernel's algebra).  The last workgroup to finish works out
-// the run (first grid point that is not On, as grid_build_kernel) and
+// the run (first grid point that is not On, as frame_build_kernel) and
 // publishes summary, records and verdicts to pinned memory, its sequence
 // number last.  A packet it cannot take (more data, too many chunks, a chunk
 // size that is not a multiple of 64 with several chunks) is flagged and the
@@ -2443,7 +2598,7 @@ __global__ __launch_bounds__(1024) void small_run_kernel(const uint8_t *__restri
   const uint32_t nfr = copy_dst ? k + 1u : 1u;
   if (tid < nfr && DCHK(nfr <= kSmallRunMax && k < count, kDkSmallRun)) {
     const uint32_t pk = copy_dst ? tid : k;
-    const uint64_t stride = grid_stride(s, len, 0, proto);  // the grid, as frame_grid_kernel
+    const uint64_t stride = grid_stride(s, len, 0, proto);  // the grid, as frame_build_kernel
     hdfs_crc32c_packet r{};
     uint32_t code = kGridMore;
     uint64_t total = 0;
@@ -2621,23 +2776,6 @@ hipError_t launch_small_run(const uint8_t *s, uint64_t len, uint32_t count, int 
   return hipGetLastError();
 }
 
-hipError_t launch_frame_grid(const uint8_t *s, uint64_t len, uint64_t base, uint32_t count, int proto, uint32_t cs,
-                             int ctype, int verify, uint32_t sflags, uint8_t *bm_base, uint8_t *copy_base,
-                             uint64_t copy_cap, int win, int64_t client_offset, GridBufs g, hipStream_t stream) {
-  if (!count || base >= len) return hipErrorInvalidValue;
-  const uint32_t nblk = (count + kGridBlock - 1) / kGridBlock;
-  auto *contrib = reinterpret_cast<GridContrib *>(g.contrib);
-  hipLaunchKernelGGL(frame_grid_kernel, dim3(nblk), dim3(kGridBlock), 0, stream, s, len, base, count, proto, cs,
-                     ctype, verify, win, client_offset, g.recs, g.status, contrib, g.blk_sum, g.blk_min, g.sum, g.done);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(grid_build_kernel, dim3(nblk), dim3(kGridBlock), 0, stream, s, base, count, nblk, g.recs,
-                     g.status, contrib, g.blk_sum, g.blk_min, cs, sflags, bm_base, copy_base, copy_cap, win, client_offset,
-                     g.segs,
-                     g.seg2pkt, g.fb, g.gctr, g.done, g.exc, g.sum, g.hsum, g.seq);
-  return hipGetLastError();
-}
-
 hipError_t launch_grid_finalize(const SegDev *segs, uint32_t nseg, const uint32_t *seg2pkt, const uint32_t *fb,
                                 GridBad *bad, uint32_t bad_cap, GridSummary *sum, uint8_t *hsum2, uint32_t host_cap,
                                 uint32_t seq, hipStream_t stream) {
@@ -2646,6 +2784,19 @@ hipError_t launch_grid_finalize(const SegDev *segs, uint32_t nseg, const uint32_
                      hsum2, host_cap, seq);
   return hipGetLastError();
 }
+
+hipError_t launch_frame_grid(const uint8_t *s, uint64_t len, uint64_t base, uint32_t count, int proto, uint32_t cs,
+                             int ctype, int verify, uint32_t sflags, uint8_t *bm_base, uint8_t *copy_base,
+                             uint64_t copy_cap, int win, int64_t client_offset, GridBufs g, hipStream_t stream) {
+  if (!count || count > kGridMaxCount || base >= len || !g.seq) return hipErrorInvalidValue;
+  const uint32_t nblk = (count + kGridBlock - 1) / kGridBlock;
+  hipLaunchKernelGGL(frame_build_kernel, dim3(nblk), dim3(kGridBlock), 0, stream, s, len, base, count, proto, cs,
+                     ctype, verify, sflags, bm_base, copy_base, copy_cap, win, client_offset, g.recs,
+                     reinterpret_cast<GridLook *>(g.look), g.segs, g.seg2pkt, g.fb, g.gctr, g.done, g.exc, g.sum,
+                     g.hsum, g.seq);
+  return hipGetLastError();
+}
+
 
 // ---------------------------------------------------------------------------
 // Host-side launchers (used by crc32c_engine.cpp).
@@ -2739,12 +2890,13 @@ hipError_t launch_tiles(int mode, int order, int nt, int depth, int streams, int
                         const SegDev *segs, uint32_t nseg, uint64_t total_rounds, uint64_t total_tiles,
                         const uint32_t *gtab, uint32_t *first_bad, unsigned long long *mism,
                         unsigned long long *diag, uint32_t tune, uint32_t *gctr, hipStream_t stream, int copy,
-                        int una, const GridSummary *dyn, uint32_t utiles) {
+                        int una, const GridSummary *dyn, uint32_t utiles, int fuse_generic) {
+  const uint32_t fn = dyn && fuse_generic ? 1u : 0u;
   // uniform-table look-up: tile indices must fit 32 bits (multiply-high form)
   if (utiles && !dyn && (total_tiles >> 32)) utiles = 0;
 #define HDFS_LAUNCH_CUG(M, O, N, D, S, B, BUF, C, U, G)                                                          \
   hipLaunchKernelGGL((crc32c_tiles_kernel<M, O, N, D, S, B, BUF, C, U, G>), dim3(grid), dim3(B), 0, stream,      \
-                     segs, nseg, total_rounds, total_tiles, gtab, first_bad, mism, diag, tune, gctr, dyn, utiles)
+                     segs, nseg, total_rounds, total_tiles, gtab, first_bad, mism, diag, tune, gctr, dyn, utiles, fn)
 #define HDFS_LAUNCH_CU(M, O, N, D, S, B, BUF, C, U) HDFS_LAUNCH_CUG(M, O, N, D, S, B, BUF, C, U, 0)
 #define HDFS_LAUNCH_C(M, O, N, D, S, B, BUF, C) HDFS_LAUNCH_CU(M, O, N, D, S, B, BUF, C, 0)
 #define HDFS_LAUNCH(M, O, N, D, S, B, BUF) HDFS_LAUNCH_C(M, O, N, D, S, B, BUF, 0)

@@ -496,29 +496,37 @@ int stream_device(const void *stream) {
   return -1;
 }
 
-// ---- device framing (frame_grid_kernel / grid_scan_kernel) ----
+// ---- device framing (frame_build_kernel) ----
+// Sequence number of a device framing pass or short run: what the host
+// polls for in pinned memory and what tags the pass's look-back records --
+// never 0 (the value of zeroed memory)
+static uint32_t next_grid_seq(DevCtx &c) {
+  if (++c.grid_seq == 0u) ++c.grid_seq;
+  return c.grid_seq;
+}
+
 // Layout of one pass's device tables and pinned landing area.
 constexpr uint32_t kBadFirst = 1024;  // bad-packet entries copied back with the verify summary
 struct GridLayout {
-  size_t recs, status, contrib, blk_sum, blk_min, segs, seg2pkt, fb, sum, bad, ctr, done, exc, bm, dtotal;  // device
+  size_t look, recs, segs, seg2pkt, fb, sum, bad, ctr, done, exc, bm, dtotal;  // device
   size_t h_sum, h_sum2, htotal;  // pinned offsets (h_sum: summary + packet 0 + exceptions, kGridHost*;
                                  // h_sum2: summary after verify, then the bad list)
   GridLayout(uint32_t count, uint64_t bm_cap) {
-    const size_t nblk = (count + 63) / 64;  // frame_grid_kernel blocks (kGridBlock)
     size_t o = 0;
     auto take = [&](size_t n) { const size_t at = o; o += align_up(n, 256); return at; };
+    // the look-back records first, sized for the largest pass: always the
+    // same bytes of the slot, zeroed when the slot is allocated and written
+    // by nothing else, so a record's flag is either 0 or tagged with the
+    // sequence number of the pass that wrote it
+    look = take(size_t(kGridMaxCount / 64) * kGridLookBytes);
     recs = take(size_t(count) * sizeof(hdfs_crc32c_packet));
-    status = take(size_t(count) * 4);
-    contrib = take(size_t(count) * 24);
-    blk_sum = take(nblk * 48);
-    blk_min = take(nblk * 4);
     segs = take(size_t(count) * sizeof(SegDev));
     seg2pkt = take(size_t(count) * 4);
     fb = take(size_t(count) * 4);
     sum = take(256);  // the bad list follows the summary: one copy back
     bad = take(size_t(count) * sizeof(GridBad));
     ctr = take(128);  // pool counter, mismatch count
-    done = take(64);  // grid_build_kernel: blocks finished, exceptions found
+    done = take(64);  // frame_build_kernel: blocks finished, exceptions found
     exc = take(size_t(count) * 4);
     bm = take(size_t(bm_cap));
     dtotal = o;
@@ -539,13 +547,14 @@ int reserve_grid(DevCtx &c, size_t si, const GridLayout &L) {
     g.d = nullptr;
     g.dcap = 0;
     HIPCHK(hipMalloc(&g.d, L.dtotal));
+    HIPCHK(hipMemset(g.d, 0, L.recs));  // the look-back records: no flag of any pass
     g.dcap = L.dtotal;
   }
   if (L.htotal > g.hcap) {
     if (g.h) HIPCHK(hipHostFree(g.h));
     g.h = g.hd = nullptr;
     g.hcap = 0;
-    // fine-grained (coherent) and mapped: grid_build_kernel writes the
+    // fine-grained (coherent) and mapped: frame_build_kernel writes the
     // summary, packet 0's record and the exceptions here directly
     HIPCHK(hipHostMalloc(&g.h, L.htotal, hipHostMallocCoherent | hipHostMallocMapped));
     HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&g.hd), g.h, 0));
@@ -556,8 +565,8 @@ int reserve_grid(DevCtx &c, size_t si, const GridLayout &L) {
 
 // Framing + verify of a device-resident stream, run by run on the device:
 // each pass frames up to kGridMaxCount packets on the grid of the first
-// packet's size (frame_grid_kernel), builds their verify segment table in
-// HBM (grid_build_kernel) and returns only a summary, packet 0's record and
+// packet's size, builds their verify segment table in HBM (one launch of
+// frame_build_kernel) and returns only a summary, packet 0's record and
 // the records that differ from the prediction from it; the verify launch
 // (plus the optional fused copy-out) is queued behind them straight from the
 // device-built summary.  The host writes the pass's records into the
@@ -568,7 +577,7 @@ int reserve_grid(DevCtx &c, size_t si, const GridLayout &L) {
 // Short runs (<= kSmallRunMax packets of <= 64 KiB, the per-read case; verify
 // or framing only):
 // framing and verify in ONE launch (small_run_kernel) instead of the framing
-// pass + verify + finalize chain.  Returns 1 when the run is fully resolved
+// pass + verify chain.  Returns 1 when the run is fully resolved
 // there (records in dst), 0 when the regular path must run (a packet the
 // kernel cannot take, a packet off the grid, more packets than it covers),
 // < 0 on an engine error.
@@ -581,7 +590,7 @@ int small_run(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
     HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&c.sr_hd), c.sr_h, 0));
   }
   const uint32_t count = uint32_t(std::min<uint64_t>({uint64_t(kSmallRunMax), uint64_t(max_pkts), len / 6 + 1}));
-  const uint32_t seq = ++c.grid_seq;
+  const uint32_t seq = next_grid_seq(c);
   const int tset = ctype == HDFS_CRC32C_CSUM_CRC32 ? 1 : 0;
   HIPCHK(launch_small_run(d, len, count, proto, cs, ctype, verify ? 1 : 0, c.d_tab_main_t[tset], c.d_tab_pow2_t[tset],
                           co.dst, co.cap, co.win ? 1 : 0, co.client_offset, c.sr_hd, seq, c.stream));
@@ -708,10 +717,7 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
     auto *sum = reinterpret_cast<GridSummary *>(dg + L.sum);
     auto *ctr = reinterpret_cast<uint32_t *>(dg + L.ctr);
     const GridBufs gb{recs,
-                      reinterpret_cast<uint32_t *>(dg + L.status),
-                      dg + L.contrib,
-                      reinterpret_cast<uint64_t *>(dg + L.blk_sum),
-                      reinterpret_cast<uint32_t *>(dg + L.blk_min),
+                      dg + L.look,
                       reinterpret_cast<SegDev *>(dg + L.segs),
                       reinterpret_cast<uint32_t *>(dg + L.seg2pkt),
                       reinterpret_cast<uint32_t *>(dg + L.fb),
@@ -720,7 +726,7 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
                       reinterpret_cast<uint32_t *>(dg + L.exc),
                       sum,
                       c.grid[si].hd + L.h_sum,
-                      ++c.grid_seq};
+                      next_grid_seq(c)};
     auto *hsum = reinterpret_cast<GridSummary *>(hg + L.h_sum);
     __atomic_store_n(&hsum->seq, 0u, __ATOMIC_RELEASE);
     // framing and the segment table on c.stream; the verify of the run is
@@ -741,6 +747,7 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
       // kernel takes, else every tile of every packet
       const uint64_t gtiles_ub = cs % kRoundBytes == 0 ? count : left / (uint64_t(cs) * kTileChunks) + 2ull * count;
       // rounds: at most one per 512 B of the rest of the stream
+      // (the generic tiles ride in the verify launch)
       rc = launch_verify_dyn(c, reinterpret_cast<const SegDev *>(dg + L.segs), sum, left / kRoundBytes, gtiles_ub,
                              reinterpret_cast<uint32_t *>(dg + L.fb), reinterpret_cast<unsigned long long *>(ctr + 16),
                              ctr, c.stream, tset, co.dst != nullptr);

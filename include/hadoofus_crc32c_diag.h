@@ -60,7 +60,10 @@ int hdfs_crc32c_set_shape(int streams, int block);
  * default-policy (no cache bits) CRC stores; 12: only the last tile of each
  * 8-tile group stores, one 256-B store over the group's CRC area; 13: only
  * that tile stores its own 32 B -- 12 / 13 timing experiments only, output
- * undefined.
+ * undefined; 14..25 further store / load-policy experiments
+ * (hadoofus_amd/csrc/crc32c_diag_ep.h); 20 the compute gather with its slot
+ * protocol skipped and its stores dropped; 26 / 27 / 28 as 20 plus a
+ * workgroup barrier every 3 / 6 / 12 rounds (the barriers' own cost).
  * Env HDFS_CRC32C_STORE. */
 int hdfs_crc32c_set_store_policy(int policy);
 /* Compute plans: 2 (default, the product) schedule 3 with the LDS group
@@ -72,14 +75,14 @@ int hdfs_crc32c_set_store_policy(int policy);
  * after its last tile).
  * Env HDFS_CRC32C_RUNS. */
 int hdfs_crc32c_set_runs(int on);
-/* Device checks: the framing kernels (frame_grid, grid_build, header_window,
- * small_run, grid_finalize) test, in this build, the invariants behind each
- * address they touch (a record slot inside its pass, a packet's bytes inside
+/* Device checks: the framing kernels (frame_build, header_window, small_run,
+ * grid_finalize) test, in this build, the invariants
+ * behind each address they touch (a record slot inside its pass, a packet's bytes inside
  * the stream, a copy-out inside its window and destination) and skip an
  * access whose invariant fails, counting it.  Every device-stream call reads
  * the count at its end and fails with HDFS_CRC32C_EHIP naming the kernel and
- * source line of the first violation.  out3 = {kernel id (1 frame_grid,
- * 2 grid_build, 3 header_window, 4 small_run, 5 grid_finalize), line,
+ * source line of the first violation.  out3 = {kernel id (1 frame_build framing,
+ * 2 frame_build table, 3 header_window, 4 small_run, 5 grid_finalize), line,
  * violations}; reset > 0 clears them; reset < 0 first records one violation
  * of kernel id 0 (a test of the reporting itself). */
 int hdfs_crc32c_diag_device_checks(uint32_t *out3, int reset);

@@ -1,7 +1,7 @@
 """Device checks of the framing kernels (diagnostic build).
 
-libhadoofus_crc32c_diag.so compiles, into frame_grid_kernel,
-grid_build_kernel, header_window_kernel, small_run_kernel and
+libhadoofus_crc32c_diag.so compiles, into frame_build_kernel (framing and
+table phases), header_window_kernel, small_run_kernel and
 grid_finalize_kernel, a test of the invariant behind each address they touch
 (DCHK, hadoofus_amd/csrc/crc32c_kernels.hip): a record slot inside its pass,
 a packet's bytes inside the stream, a copy-out window inside the packet's

@@ -364,6 +364,30 @@ def test_gpu_device_stream_many_passes(engine, oracle):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("dlen,cs", [(4096, 512), (3000, 512), (4096, 100)])
+def test_gpu_device_stream_many_bad_packets(engine, oracle, dlen, cs):
+    """More bad packets than the verdict area beside the summary holds (1 024):
+    the verify launch's bad-packet list spills to HBM and every verdict still
+    comes back exact -- tiled chunks only (4 096 B), a partial last chunk per
+    packet (3 000 B: one generic tile each, taken by the same launch's waves
+    after their tiled rounds), every chunk generic (chunk size 100)."""
+    npk = 3000
+    rng = np.random.default_rng(dlen + cs)
+    ks = sorted(int(k) for k in rng.choice(npk, 1700, replace=False))
+    corrupt = [(k, int(rng.integers(0, (dlen + cs - 1) // cs))) for k in ks]
+    dl = [dlen] * npk
+    s, bad = build_stream(oracle.crc32c, 2, cs, CSUM_CRC32C, dl, seed=npk + dlen, corrupt=corrupt)
+    want = oracle.verify_packets(s, 2, cs, CSUM_CRC32C)
+    assert sum(1 for q in want[1] if q["error"]) == 1700
+    keep, p = _dev(engine, s, 1)
+    got = engine.verify_packets(None, 2, cs, CSUM_CRC32C, dptr=p, nbytes=len(s))
+    assert got == want
+    assert {k: (q["first_bad"], q["bad_chunks"]) for k, q in enumerate(got[1]) if q["error"]} == \
+        {k: (v[0], len(v)) for k, v in bad.items()}
+    keep.free()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("proto,pattern", [(2, "few"), (1, "few"), (2, "all"), (2, "last")])
 def test_gpu_device_stream_irregular_headers(engine, oracle, proto, pattern):
     """Runs of equal-size packets whose headers leave the regular progression

@@ -140,6 +140,17 @@ t0 = time.perf_counter()
 for _ in range(20000):
     lib.hdfs_crc32c_last_error()
 out["ctypes_call_overhead_us"] = round((time.perf_counter() - t0) / 20000 * 1e6, 3)
+# what the launch-path calls pay for attributing faults: one hipStreamQuery
+# of an idle stream after the completion word (small_call, small_run)
+hip = ctypes.CDLL("libamdhip64.so.7")
+hip.hipStreamQuery.argtypes = [ctypes.c_void_p]
+sq = h.stream_create()
+h.stream_sync(sq)
+assert hip.hipStreamQuery(sq) == 0
+t0 = time.perf_counter()
+for _ in range(20000):
+    hip.hipStreamQuery(sq)
+out["hip_stream_query_us"] = round((time.perf_counter() - t0) / 20000 * 1e6 - out["ctypes_call_overhead_us"], 3)
 say("launch path")
 raw_call_us("launch_")
 say("mailbox")
