@@ -51,6 +51,11 @@ struct DiagEP : ReleaseEP {
     if (pol == 15u) return sh.crcs + ((((gt & ~7u) - static_cast<uint32_t>(sh.mtile_start)) * kTileChunks) & 65535u);
     return b;
   }
+  // columns: 15 as for the gather (every run's 128 B inside the segment's
+  // first 256 KiB of CRCs: an L2-resident window)
+  DEV static const uint32_t *col_base(uint32_t pol, const uint32_t *b, const SegHot &sh, uint32_t tile) {
+    return pol == 15u ? sh.crcs + ((tile * kTileChunks) & 65535u) : b;
+  }
   DEV static void group_store(uint32_t pol, uint32_t v, __amdgpu_buffer_rsrc_t r, uint32_t off) {
     if (pol == 5u) __builtin_amdgcn_raw_buffer_store_b32(v, r, off, 0, 16);        // sc1
     else if (pol == 6u) __builtin_amdgcn_raw_buffer_store_b32(v, r, off, 0, 17);   // sc0 sc1

@@ -338,6 +338,7 @@ int launch_all(DevCtx &c, int mode, const SegDev *d_segs, uint32_t nseg, uint64_
       if (g_runs == 1 && runs) order = 4;
       else if (g_runs == 2) order = 5;
       else if (g_runs == 3) order = 6;  // diagnostic build: the lazy gather
+      else if (g_runs == 4) order = runs ? 7 : 5;  // diagnostic build: columns on whole 8-tile groups
     }
     // store policy 4 (diagnostic build): verify plans run the load-only twin
     const int kmode = (kDiag && mode == kModeVerify && g_store_policy == 4) ? int(kModeLoadOnly) : mode;
@@ -1487,8 +1488,8 @@ int hdfs_crc32c_set_store_policy(int policy) {
 }
 
 int hdfs_crc32c_set_runs(int on) {
-  if (on < 0 || on > 3)
-    return fail(HDFS_CRC32C_EINVAL, "runs 0 (schedule 3), 1 (schedule 4), 2 (gather) or 3 (lazy gather)");
+  if (on < 0 || on > 4)
+    return fail(HDFS_CRC32C_EINVAL, "runs 0 (schedule 3), 1 (schedule 4), 2 (gather), 3 (lazy gather) or 4 (columns)");
   g_runs = on;
   return HDFS_CRC32C_OK;
 }

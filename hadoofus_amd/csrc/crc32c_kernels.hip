@@ -217,7 +217,21 @@ struct Cursor {
 //    a power of two in [16, 256]) targets >= 4 units per workgroup; launches
 //    with < 32 rounds per wave skip the pool (one unit per workgroup would
 //    make the tail, not shorten it).
+//  ORDER 7 (columns, compute mode): ORDER 4's dealing with 4-tile tickets
+//    (32 chunks, one 128-B line of CRCs), but a round is a COLUMN of the
+//    run: 128 B of each of its 32 chunks instead of 512 B of each of 8.
+//    Each 1 KiB load instruction still reads 8 whole 128-B lines; after the
+//    transpose lane L holds 64 B of chunk L>>1 (half L&1), the lane pair
+//    combines every round (Z_64 on the even lane, one DPP XOR) and carries
+//    the chunk's register into the next column, so after the last column the
+//    even lanes hold the run's 32 CRCs and write them as ONE 128-B store.  No
+//    cross-wave LDS protocol (the gather's cost) and no per-tile stores.
+//    Diagnostic build only: measured 1-2 % below the gather in one process
+//    (the column reads cost ~1.6 % with stores dropped, the 128-B stores
+//    5-6.5 % even inside an L2-sized window; profiles/r03/exp_columns*.json).
 constexpr uint32_t kUnitMaxShift = 8, kUnitMinShift = 4;
+constexpr uint32_t kColBytes = 128;  // ORDER 7: bytes of each chunk per round
+constexpr uint32_t kColShift = 2;    // ORDER 7: log2 tiles per ticket (32 chunks)
 constexpr uint32_t kSlots = 8;  // LDS slots for published units
 // Compute gather (schedule 3, RUN 2): the CRCs of an 8-tile group, finished
 // by up to eight waves of the workgroup, collect in one of kGatherSlots LDS
@@ -269,7 +283,7 @@ DEV uint32_t grab(const Sched &w) {
 template <int ORDER>
 DEV bool ticket_tile(const Sched &w, uint32_t t, uint64_t &g) {
   if (t < w.nk) {
-    if (ORDER == 4)
+    if (ORDER == 4 || ORDER == 7)
       g = (w.gfirst + uint64_t(t) * w.gstride) << w.gshift;
     else if (ORDER == 3)
       g = ((w.gfirst + uint64_t(t >> w.gshift) * w.gstride) << w.gshift) + (t & ((1u << w.gshift) - 1u));
@@ -278,8 +292,8 @@ DEV bool ticket_tile(const Sched &w, uint32_t t, uint64_t &g) {
     return true;
   }
   if (ORDER < 2) return false;
-  // ORDER 4: a ticket is 2^gshift tiles, a pool unit 2^(ushift - gshift) tickets
-  const uint32_t tsh = ORDER == 4 ? w.gshift : 0u;
+  // ORDER 4 / 7: a ticket is 2^gshift tiles, a pool unit 2^(ushift - gshift) tickets
+  const uint32_t tsh = (ORDER == 4 || ORDER == 7) ? w.gshift : 0u;
   const uint32_t j = t - w.nk, u = j >> (w.ushift - tsh), o = (j & ((1u << (w.ushift - tsh)) - 1u)) << tsh,
                  s = u % kSlots;
   if (o == 0) {  // first ticket of local unit u: claim a pool unit and publish it
@@ -335,7 +349,8 @@ template <int ORDER>
 DEV Cursor advance(Cursor c, SegP segs, uint32_t nseg, const Sched &w, SegCache &kc) {
   if (!c.valid) return c;
   const SegHot &sh = hot(kc, segs, c.seg).h;
-  if (c.r + 1 < sh.chunk_size / kRoundBytes) {
+  // ORDER 7: a cursor is a whole 4-tile run, one round per 128-B column
+  if (c.r + 1 < (ORDER == 7 ? sh.chunk_size / kColBytes : sh.chunk_size / kRoundBytes)) {
     c.r++;
     return c;
   }
@@ -380,7 +395,7 @@ DEV uint64_t tile_at_round(SegP segs, uint32_t nseg, uint64_t r, uint64_t total_
 }
 
 struct LaneConst {
-  uint32_t lane, hsel, loff, lb0, lb1, qi, qg, zk, zbase, z448;
+  uint32_t lane, hsel, loff, lb0, lb1, qi, qg, zk, zbase, z448, z64;
   uint64_t ntiles;   // RUN 2: main tiles of the launch
   uint32_t rmask;    // RUN 1: tiles per run - 1
   uint32_t *gslot;   // RUN 2: LDS [kGatherSlots] owner words, then [kGatherSlots][64] CRC words
@@ -410,6 +425,8 @@ struct ReleaseEP {
   DEV static void loop_hook(uint32_t, uint32_t) {}
   // compute gather: where a whole group's 256 B go
   DEV static const uint32_t *group_base(uint32_t, const uint32_t *b, const SegHot &, uint32_t) { return b; }
+  // columns (ORDER 7): where a run's 128 B go
+  DEV static const uint32_t *col_base(uint32_t, const uint32_t *b, const SegHot &, uint32_t) { return b; }
   // compute gather: nt (pipelined gather kernel, one process: sc1 6 797,
   // nt 6 835, nt sc1 6 827, sc0 sc1 6 771 GB/s alg,
   // profiles/r02/s6/exp_gather_store_policy.json)
@@ -475,10 +492,11 @@ struct LaneOff {
 // byte read lies in a dword that also holds data of the segment, so no read
 // leaves the data's pages.  The shift rides with the round (rounds in
 // flight may belong to different segments).
-template <int MODE, int NT, int BUF, int UNA, class P = EP>
+template <int MODE, int NT, int BUF, int UNA, int COL = 0, class P = EP>
 DEV void issue(uint32_t (&d)[16], uint32_t &exp, uint32_t &tl, uint32_t &sh_a, const Cursor c, SegP segs,
                uint32_t hsel, uint32_t loff, uint32_t qg, uint32_t lane, LaneOff &lo, SegCache &kc,
                uint32_t pol = 0u) {
+  static_assert(!COL || (BUF && !UNA && MODE == kModeCompute), "columns: compute, buffer loads, aligned data");
   const SegHot &sh = hot(kc, segs, c.seg).h;
   const uint32_t cs = sh.chunk_size;
   const uint32_t a = UNA ? static_cast<uint32_t>(reinterpret_cast<uintptr_t>(sh.data)) & 3u : 0u;
@@ -488,18 +506,25 @@ DEV void issue(uint32_t (&d)[16], uint32_t &exp, uint32_t &tl, uint32_t &sh_a, c
     // cache, and the descriptor's range (the valid bytes of this round's
     // chunks) returns zeros for chunks past a partial tile's end instead of
     // clamping addresses.
-    const uint32_t nch = min(kTileChunks, sh.nchunks - c.tile * kTileChunks);
+    // COL (ORDER 7): the round is column r of a 32-chunk run -- bytes
+    // [128 r, 128 r + 128) of each chunk; quad Q = 16k + (L & 15) of load k
+    // is half Q & 1 of chunk Q >> 1, so load k reads chunks 8k .. 8k + 7,
+    // one whole 128-B line each
+    constexpr uint32_t kRb = COL ? kColBytes : kRoundBytes;
+    const uint32_t nch = min(COL ? kTileChunks << kColShift : kTileChunks, sh.nchunks - c.tile * kTileChunks);
     const uint8_t *base = sh.data + static_cast<uint64_t>(c.tile) * kTileChunks * cs +
-                          static_cast<uint64_t>(c.r) * kRoundBytes - a;
+                          static_cast<uint64_t>(c.r) * kRb - a;
     if (lo.cs != cs) {
       lo.cs = cs;
 #pragma unroll
-      for (int k = 0; k < 4; k++) lo.v[k] = (2u * k + hsel) * cs + loff;
+      for (int k = 0; k < 4; k++)
+        lo.v[k] = COL ? (8u * k + ((lane >> 1) & 7u)) * cs + (lane & 1u) * 64u + 16u * (lane >> 4)
+                      : (2u * k + hsel) * cs + loff;
       if (UNA) lo.t = lane < kTileChunks ? lane * cs + kRoundBytes : 0x80000000u;
     }
     // UNA: the range ends with the dword holding the last data byte
     const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t *>(base), 0, static_cast<int>((nch - 1u) * cs + kRoundBytes + (a ? 4u : 0u)), 0x00020000);
+        const_cast<uint8_t *>(base), 0, static_cast<int>((nch - 1u) * cs + kRb + (a ? 4u : 0u)), 0x00020000);
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       const u32x4 v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rd, lo.v[k], 0, NT ? 2 : 0));
@@ -605,6 +630,22 @@ DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, ui
                 uint32_t *__restrict__ first_bad, unsigned long long *__restrict__ mism, SegCache &kc,
                 Gst &gs) {
   const SegHot &sh = hot(kc, segs, c.seg).h;
+  if constexpr (RUN == 4) {
+    // ORDER 7 (columns): st is each chunk's register through this column
+    // (process() combined the lane pair); after the last column the even
+    // lanes hold the run's 32 CRCs -> one 128-B store (dropped otherwise)
+    static_assert(MODE == kModeCompute, "columns: compute mode");
+    const bool lastc = c.valid && (c.r + 1 == sh.chunk_size / kColBytes);
+    const uint32_t nch = min(kTileChunks << kColShift, sh.nchunks - c.tile * kTileChunks);
+    const uint32_t out = (sh.flags & kSegRaw) ? st : ~st;
+    const uint32_t val = (sh.flags & kSegBigEndian) ? __builtin_bswap32(out) : out;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<uint32_t *>(
+            rfl64(reinterpret_cast<uint64_t>(P::col_base(L.store_policy, sh.crcs + c.tile * kTileChunks, sh, c.tile)))),
+        0, static_cast<int>(rfl(lastc && !P::drop(L.store_policy) ? nch * 4u : 0u)), 0x00020000);
+    P::group_store(L.store_policy, val, rs, (L.lane & 1u) ? 0x80000000u : (L.lane >> 1) * 4u);
+    return;
+  }
   const bool last = c.valid && (c.r + 1 == sh.chunk_size / kRoundBytes);
   const uint32_t flags = sh.flags;
   const uint32_t nch = min(kTileChunks, sh.nchunks - c.tile * kTileChunks);
@@ -893,8 +934,15 @@ DEV void process(const uint32_t *lds, uint32_t (&d)[S][16], const uint32_t (&exp
       }
     }
     const uint32_t ri = hot(kc[s], segs, c[s].seg).reg_init;  // uniform control flow: kc stays in SGPRs
-    if (c[s].r == 0) st[s] = (L.qi == 0) ? ri : 0u;
-    else st[s] = zshift(lds, L.z448, st[s]);
+    if constexpr (RUN == 4) {
+      // columns: the even lane of a chunk's pair continues the chunk's
+      // register (reg_init in column 0), the odd lane starts from zero
+      if (c[s].r == 0) st[s] = (L.lane & 1u) ? 0u : ri;
+      else st[s] = (L.lane & 1u) ? 0u : st[s];
+    } else {
+      if (c[s].r == 0) st[s] = (L.qi == 0) ? ri : 0u;
+      else st[s] = zshift(lds, L.z448, st[s]);
+    }
     x[s] = st[s] ^ d[s][0];
   }
 #pragma unroll
@@ -904,6 +952,16 @@ DEV void process(const uint32_t *lds, uint32_t (&d)[S][16], const uint32_t (&exp
   }
 #pragma unroll
   for (int s = 0; s < S; s++) st[s] = slice4(lds, x[s], 0u, L.lb0, L.lb1);
+  if constexpr (RUN == 4) {
+    // columns: register of the chunk through this column = Z_64(even) ^ odd
+    // (CRC linearity); quad_perm [1,0,3,2] hands it to both lanes of the pair
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+      const uint32_t z = zshift(lds, L.z64, st[s]);
+      const uint32_t v = (L.lane & 1u) ? st[s] : z;
+      st[s] = v ^ dpp<0xB1>(v);
+    }
+  }
 #pragma unroll
   for (int s = 0; s < S; s++) finish<MODE, RUN, P>(lds, exp[s], c[s], segs, st[s], L, first_bad, mism, kc[s], gs[s]);
 }
@@ -1056,6 +1114,7 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
     unsigned long long *__restrict__ mism, unsigned long long *__restrict__ diag, uint32_t tune,
     uint32_t *__restrict__ gctr, const GridSummary *__restrict__ dyn, uint32_t utiles, uint32_t fuse) {
   static_assert(ORDER != 0 || S == 1, "static per-wave slices serve one stream");
+  static_assert(ORDER != 7 || (MODE == kModeCompute && S == 1 && BUF && !COPY && !UNA && !GATHER), "columns shape");
   // fused epilogue (verify with a device-built table only; uniform)
   const bool fused = MODE == kModeVerify && dyn && fuse;
   static_assert(DEPTH >= 2 && DEPTH <= 4 && S >= 1 && S <= 4, "shape");
@@ -1126,6 +1185,7 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
   L.zk = 7u - L.qi;
   L.zbase = kLdsSliceBytes / 4 + (L.zk ? L.zk - 1u : 0u) * 1024u;
   L.z448 = kLdsSliceBytes / 4 + 6u * 1024u;
+  L.z64 = kLdsSliceBytes / 4;  // ORDER 7: Z_64
   L.ntiles = total_tiles;
   L.gslot = &lds[kLdsWords + 2 + 2 * kSlots];
   L.rmask = 7u;
@@ -1168,7 +1228,7 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
       // static phase: whole groups only; the pool takes the rest
       // ORDER 4: 2^gshift tiles per run (8 in the diagnostic default; 4 = one
       // 128-B CRC line per run), at most 8 (one register of CRCs)
-      w.gshift = ORDER == 4 ? min((tune >> 8) & 15u, 3u) : (tune >> 8) & 15u;
+      w.gshift = ORDER == 7 ? kColShift : ORDER == 4 ? min((tune >> 8) & 15u, 3u) : (tune >> 8) & 15u;
       if (ORDER == 4) L.rmask = (1u << w.gshift) - 1u;
       const uint64_t ngroups = (pool ? total_tiles * kPhase1Num / kPhase1Den : total_tiles) >> w.gshift;
       // tune bit 12: XCD-major dealing.  Workgroups are dispatched to the 8
@@ -1187,14 +1247,14 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
         const uint32_t G8 = G / 8u, l = b / 8u;
         w.gfirst = (b % 8u) * ngx + l;
         w.gstride = G8;
-        w.nk = static_cast<uint32_t>(((ngx - 1 - l) / G8 + 1) << (ORDER == 4 ? 0u : w.gshift));
+        w.nk = static_cast<uint32_t>(((ngx - 1 - l) / G8 + 1) << (ORDER == 4 || ORDER == 7 ? 0u : w.gshift));
         w.p2first = (ngx * 8u) << w.gshift;
       } else {
         w.gfirst = xm != 0u && (G % 8u) == 0 ? (b % 8u) * (G / 8u) + b / 8u : b;
         w.gstride = gridDim.x;
         // tickets of the static phase: tiles (ORDER 3) or whole groups (ORDER 4)
         w.nk = ngroups > w.gfirst
-                   ? static_cast<uint32_t>(((ngroups - 1 - w.gfirst) / gridDim.x + 1) << (ORDER == 4 ? 0u : w.gshift))
+                   ? static_cast<uint32_t>(((ngroups - 1 - w.gfirst) / gridDim.x + 1) << (ORDER == 4 || ORDER == 7 ? 0u : w.gshift))
                    : 0u;
         w.p2first = ngroups << w.gshift;
       }
@@ -1282,7 +1342,7 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
       ex[k][s] = 0u;
       tl[k][s] = 0u;
       sha[k][s] = 0u;
-      issue<MODE, NT, BUF, UNA>(buf[k][s], ex[k][s], tl[k][s], sha[k][s], cur[k][s], sg, L.hsel, L.loff, L.qg, L.lane,
+      issue<MODE, NT, BUF, UNA, ORDER == 7>(buf[k][s], ex[k][s], tl[k][s], sha[k][s], cur[k][s], sg, L.hsel, L.loff, L.qg, L.lane,
                                 lo, kc[s], L.store_policy);
     }
   }
@@ -1290,7 +1350,8 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
     EP::loop_hook(L.store_policy, it);
 #pragma unroll
     for (int k = 0; k < DEPTH; k++) {
-      process<MODE, S, COPY, UNA, (ORDER == 4 && MODE == kModeCompute) ? 1 : GATHER == 2 ? 3 : GATHER ? 2 : 0>(
+      process<MODE, S, COPY, UNA,
+              ORDER == 7 ? 4 : (ORDER == 4 && MODE == kModeCompute) ? 1 : GATHER == 2 ? 3 : GATHER ? 2 : 0>(
           lds, buf[k], ex[k], tl[k], sha[k], cur[k], sg, st, L, first_bad, mism, kc, gs);
 #pragma unroll
       for (int s = 0; s < S; s++) nrounds += cur[k][s].valid ? 1u : 0u;
@@ -1298,7 +1359,7 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
 #pragma unroll
       for (int s = 0; s < S; s++) {
         cur[k][s] = advance<ORDER>(cur[prev][s], sg, nseg, w, kc[s]);
-        issue<MODE, NT, BUF, UNA>(buf[k][s], ex[k][s], tl[k][s], sha[k][s], cur[k][s], sg, L.hsel, L.loff, L.qg,
+        issue<MODE, NT, BUF, UNA, ORDER == 7>(buf[k][s], ex[k][s], tl[k][s], sha[k][s], cur[k][s], sg, L.hsel, L.loff, L.qg,
                                   L.lane, lo, kc[s], L.store_policy);
       }
     }
@@ -2970,6 +3031,7 @@ hipError_t launch_tiles(int mode, int order, int nt, int depth, int streams, int
     else if (HDFS_SHAPE(4, 2, 3, 1, 1024)) HDFS_LAUNCH(kModeCompute, 4, 1, 3, 1, 1024, 1);
     else if (HDFS_SHAPE(5, 2, 3, 1, 1024)) HDFS_LAUNCH_CUG(kModeCompute, 3, 1, 3, 1, 1024, 1, 0, 0, 1);
     else if (HDFS_SHAPE(6, 2, 3, 1, 1024)) HDFS_LAUNCH_CUG(kModeCompute, 3, 1, 3, 1, 1024, 1, 0, 0, 2);
+    else if (HDFS_SHAPE(7, 2, 3, 1, 1024)) HDFS_LAUNCH(kModeCompute, 7, 1, 3, 1, 1024, 1);
     else return hipErrorInvalidValue;
   }
 #undef HDFS_LAUNCH_ALL

@@ -14,7 +14,7 @@ import sys
 import numpy as np
 import pytest
 
-from oracle import splitmix64_np
+from oracle import CSUM_CRC32, CSUM_CRC32C, splitmix64_np
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
 
@@ -163,14 +163,17 @@ def test_unaligned_realign_small_and_large(engine, oracle, shift, cs, nch):
     assert engine.stream_crc_dev(0x5A5A5A5A, buf.ptr + shift, n) == oracle.crc32c(0x5A5A5A5A, host)
 
 
-@pytest.mark.parametrize("runs", [0, 1, 2, 3])
+@pytest.mark.parametrize("runs", [0, 1, 2, 3, 4])
 def test_compute_store_schedules(engine, diag, oracle, table, runs):
     """Compute mode's store schedules (diagnostic knob set_runs): 0 schedule
     3 (one 32-B store per tile), 1 schedule 4 (a wave per 8-tile group), 2
     schedule 3 with the LDS group gather (a group's CRCs collected across the
     workgroup's waves, one 256-B store by the wave finishing it), 3 the lazy
     gather (the same, with the slot check loaded before the slicing and the
-    count read one round later: no LDS round trip waited on per tile).
+    count read one round later: no LDS round trip waited on per tile), 4
+    columns (schedule 7: a wave reads a 32-chunk run 128 B of every chunk per
+    round and writes its 32 CRCs as one 128-B line; the gather on tables
+    that are not whole 8-tile groups).
     On the C5-like table and on a table of 13-tile segments, where groups
     straddle segments and fall back to per-tile stores."""
     host, sizes, lens, want, dbuf = table
@@ -202,6 +205,60 @@ def test_compute_store_schedules(engine, diag, oracle, table, runs):
                 o += n // cs
             assert (got[o:] == 0xA5A5A5A5).all()
             p.destroy()
+    finally:
+        diag.reset()
+        crcs.free()
+
+
+@pytest.mark.parametrize("variant", ["le", "crc32_be", "init", "raw"])
+def test_compute_columns_flags(engine, diag, oracle, table, variant):
+    """The column schedule (set_runs(4), schedule 7) on 1 GiB of 512-B chunks
+    in 64 segments of whole 8-tile groups, the last tile of each segment 0..4
+    chunks short: little-endian CRC arrays, the CRC32 (zlib) tables with
+    wire-order CRCs, a non-zero crc_init (sampled chunks vs the oracle) and
+    raw registers (SEG_RAW: init 0, no final inversion).  Bit-exact; the
+    guard words past the array stay untouched."""
+    host, _, _, _, dbuf = table
+    cs = 512
+    lens = [SEG - (i % 5) * cs for i in range(NSEG)]
+    nch = [n // cs for n in lens]
+    crcs = engine.DeviceBuffer(4 * (sum(nch) + 64))
+    flags = {"le": 0, "crc32_be": engine.SEG_BE | engine.SEG_CRC32, "init": engine.SEG_BE,
+             "raw": engine.SEG_BE | engine.SEG_RAW}[variant]
+    init = 0x1234ABCD if variant == "init" else 0
+    try:
+        diag.reset()
+        diag.set_runs(4)
+        crcs.fill(0xA5)
+        segs, off = [], 0
+        for i, n in enumerate(lens):
+            segs.append(engine.Segment(data=dbuf.ptr + i * SEG, len=n, chunk_size=cs, flags=flags, crc_init=init,
+                                       crcs=crcs.ptr + 4 * off, bitmap=None))
+            off += n // cs
+        p = diag.plan(engine.MODE_COMPUTE, segs)
+        p.execute()
+        got = crcs.download(4 * (off + 64), dtype="<u4" if variant == "le" else ">u4").astype(np.uint32)
+        assert (got[off:] == 0xA5A5A5A5).all()
+        o = 0
+        rng = np.random.default_rng(7)
+        for i, n in enumerate(lens):
+            seg = host[i * SEG:i * SEG + n]
+            if variant in ("le", "crc32_be"):
+                ct = CSUM_CRC32 if variant == "crc32_be" else CSUM_CRC32C
+                np.testing.assert_array_equal(got[o:o + n // cs], oracle.chunk_crcs(seg, cs, ctype=ct),
+                                              err_msg=f"segment {i}")
+            else:
+                # every chunk of the last run plus a sample
+                picks = set(range(max(0, n // cs - 40), n // cs)) | set(rng.integers(0, n // cs, 24).tolist())
+                for c in sorted(picks):
+                    chunk = seg[c * cs:(c + 1) * cs]
+                    if variant == "init":
+                        w = oracle.crc32c(init, chunk)
+                    else:
+                        w = ~oracle.crc32c(0xFFFFFFFF, chunk) & 0xFFFFFFFF
+                    assert got[o + c] == w, (i, c)
+            o += n // cs
+        p.destroy()
     finally:
         diag.reset()
         crcs.free()
