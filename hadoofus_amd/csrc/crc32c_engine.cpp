@@ -333,7 +333,8 @@ int launch_all(DevCtx &c, int mode, const SegDev *d_segs, uint32_t nseg, uint64_
     const int depth = to_small ? 3 : g_depth, streams = to_small ? 1 : g_streams, block = to_small ? 1024 : g_block;
     // compute mode, product shape: schedule 4 (runs, tables of whole 8-tile
     // groups) or schedule 3 with the LDS group gather ("order 5")
-    if (order == 3 && mode == kModeCompute && !una && !copy && nt == 2 && depth == 3 && streams == 1 &&
+    if (order == 3 && mode == kModeCompute && !una && !copy && nt == 2 && (depth == 3 || (kDiag && depth == 4)) &&
+        streams == 1 &&
         block == 1024) {
       if (g_runs == 1 && runs) order = 4;
       else if (g_runs == 2) order = 5;

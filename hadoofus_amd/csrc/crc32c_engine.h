@@ -66,7 +66,13 @@ hipError_t launch_small_run(const uint8_t *s, uint64_t len, uint32_t count, int 
                             hipStream_t stream);
 hipError_t launch_frame_grid(const uint8_t *s, uint64_t len, uint64_t base, uint32_t count, int proto, uint32_t cs,
                              int ctype, int verify, uint32_t sflags, uint8_t *bm_base, uint8_t *copy_base,
-                             uint64_t copy_cap, int win, int64_t client_offset, GridBufs g, hipStream_t stream);
+                             uint64_t copy_cap, int win, int64_t client_offset, GridBufs g, hipStream_t stream,
+                             unsigned long long *stamps = nullptr);
+// diagnostic build: per-wave / per-block s_memrealtime stamps (set_tuning)
+extern unsigned long long *g_diag;
+// frame_build_kernel's stamps sit after the tiled kernel's per-wave words
+// (3 per wave, at most 4 096 waves): 8 per block from this word on
+constexpr size_t kFrameStampOff = 65536;
 // One workgroup: the bad-packet list to *bad (device) and, with its count and
 // then seq, to the pinned host area hsum2 (device address; first host_cap
 // entries after 256 bytes).

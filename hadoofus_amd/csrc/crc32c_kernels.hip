@@ -2288,8 +2288,14 @@ __global__ __launch_bounds__(kGridBlock) void frame_build_kernel(
     int rwin, int64_t client_offset, hdfs_crc32c_packet *__restrict__ recs, GridLook *__restrict__ look,
     SegDev *__restrict__ segs, uint32_t *__restrict__ seg2pkt, uint32_t *__restrict__ fb, uint32_t *__restrict__ gctr,
     uint32_t *__restrict__ done, uint32_t *__restrict__ exc, GridSummary *__restrict__ sum, uint8_t *__restrict__ hsum,
-    uint32_t seq) {
+    uint32_t seq, unsigned long long *__restrict__ stamps) {
   static_assert(kGridBlock == 64, "one wave per block: the scans are wave-wide");
+  // diagnostic build: s_memrealtime (100 MHz) per block at the end of each
+  // phase -> stamps[8 b + phase] (tools/frame_phases.py)
+  auto stamp = [&](uint32_t ph) {
+    if (kDiag && stamps && threadIdx.x == 0) stamps[8u * blockIdx.x + ph] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
   static_assert(sizeof(hdfs_crc32c_packet) == kGridRecBytes, "host record layout");
   __shared__ __attribute__((aligned(16))) uint8_t win[kGridBlock][kHdrWin];
   __shared__ uint32_t islast;
@@ -2302,11 +2308,32 @@ __global__ __launch_bounds__(kGridBlock) void frame_build_kernel(
   // packet 0's PacketHeaderProto just to find the grid.  If packet 0 is not
   // such a packet its status ends the run (first_break = 0).
   const uint64_t stride = grid_stride(s, len, base, proto);
+  // Grid points past the stream's end are kGridMore, so the run ends at the
+  // latest at k0 = ceil((len - base) / stride), the first point at or past
+  // the end: the pass acts on points [0, ceff), ceff = k0 + 1 (1 without a
+  // grid), which decides exactly what the whole count would.  Blocks past
+  // ceff only count themselves done -- a pass is sized before the host knows
+  // the stride (up to kGridMaxCount points: 1 024 blocks for a 1 GiB run of
+  // 16 384 packets), and without this the look-back chain ran through every
+  // block (16 windows deep instead of 4).
+  const uint32_t ceff =
+      stride ? static_cast<uint32_t>(min<uint64_t>(count, (len - base + stride - 1) / stride + 1)) : 1u;
+  if (b * kGridBlock >= ceff) {
+    // block 0 resets the counters before its flag: wait for it before counting
+    if (lane == 0)
+      for (uint32_t spins = 0; (at_ld(&look[0].flag) >> 2) != uint64_t(seq);) {
+        if (++spins > (1u << 24)) {  // never expected: fail loudly, see the gather
+          asm volatile("s_trap 2");
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+  } else {
   hdfs_crc32c_packet r{};
   uint64_t total = 0;
   uint32_t code = kGridMore;
   GridContrib a{0u, 0u, 0u, 0u, 0u, 0u};
-  if (k < count && (k == 0 || stride)) {
+  if (k < ceff && (k == 0 || stride)) {
     const uint64_t pos = base + uint64_t(k) * stride;
     if (pos < len) {
       stage_header(s, len, pos, win[t]);
@@ -2326,7 +2353,8 @@ __global__ __launch_bounds__(kGridBlock) void frame_build_kernel(
       }
     }
   }
-  const uint32_t mk = (k < count && code != kGridOn) ? k : 0xFFFFFFFFu;
+  stamp(1);
+  const uint32_t mk = (k < ceff && code != kGridOn) ? k : 0xFFFFFFFFu;
   // 2. the block's aggregate: shares of its grid points (a point past the
   // run's end is excluded later, where the end is known) and its first point
   // that is not On
@@ -2364,6 +2392,7 @@ __global__ __launch_bounds__(kGridBlock) void frame_build_kernel(
     stores_done();
     at_st(&L.flag, tag | (b == 0 ? 2u : 1u));
   }
+  stamp(2);
   // 3. look back: the shares and first break of blocks 0..b-1.  Lane i looks
   // at block j0 - i; a window is used up to its nearest block with an
   // inclusive prefix (that block's inc, the aggregates of the blocks after
@@ -2431,13 +2460,14 @@ __global__ __launch_bounds__(kGridBlock) void frame_build_kernel(
       __builtin_amdgcn_s_sleep(1);
     }
   }
+  stamp(3);
   // 4. the run's end as this block sees it: the first point that is not On
   // (before this block: the block is past the run; in it; or none up to
   // here).  A point is recorded if it lies before the end, or is the end and
   // was framed (Off / Stop).
-  const uint32_t fbk = min(min(pmin, m), count);
+  const uint32_t fbk = min(min(pmin, m), ceff);
   const bool past = pmin != 0xFFFFFFFFu;
-  const bool inrun = !past && (k < fbk || (k == fbk && k < count && code != kGridMore));
+  const bool inrun = !past && (k < fbk || (k == fbk && k < ceff && code != kGridMore));
   const uint32_t T = static_cast<uint32_t>(at_ld(&look[0].T));
   if (!past) {
     // in-block exclusive scan of the recorded points' shares
@@ -2530,12 +2560,12 @@ __global__ __launch_bounds__(kGridBlock) void frame_build_kernel(
     uint64_t tot[6];
 #pragma unroll
     for (int q = 0; q < 6; q++) tot[q] = pre[q] + static_cast<uint64_t>(__shfl(static_cast<long long>(incl[q]), 63));
-    if (fbk < count ? k == fbk : k == count - 1u) {
+    if (fbk < ceff ? k == fbk : k == ceff - 1u) {
       uint64_t consumed, next;
       uint32_t recorded, st_fb;
-      if (fbk == count) {
-        consumed = next = base + uint64_t(count) * stride;
-        recorded = count;
+      if (fbk == ceff) {  // only when ceff == count (else point ceff - 1 is past the stream: a break)
+        consumed = next = base + uint64_t(ceff) * stride;
+        recorded = ceff;
         st_fb = kGridOn;
       } else if (code == kGridMore) {
         consumed = next = base + uint64_t(fbk) * stride;
@@ -2562,6 +2592,8 @@ __global__ __launch_bounds__(kGridBlock) void frame_build_kernel(
       *gctr = 0u;    // the verify launch's pool counter (no separate reset launch)
     }
   }
+  }  // active block
+  stamp(4);
   // 5. the last block to finish publishes the summary, packet 0's record and
   // the exceptions to pinned host memory, then (one system-scope fence later)
   // the sequence number the host polls.  The barrier makes every wave's
@@ -2574,11 +2606,13 @@ __global__ __launch_bounds__(kGridBlock) void frame_build_kernel(
     islast = atomicAdd(&done[0], 1u) == nblk - 1u ? 1u : 0u;
   }
   __syncthreads();
+  stamp(5);
   if (!islast) return;
   __threadfence();  // acquire: the other blocks' summary fields, flags and exception slots
   const uint32_t nexc = done[1];
   if (t == 0) {
     sum->nexc = nexc;
+    const uint32_t T = static_cast<uint32_t>(at_ld(&look[0].T));
     sum->utiles = (sum->nonuni || (sum->mtiles >> 32)) ? 0u : T;  // read by the verify kernel
     GridSummary h = *sum;
     h.seq = 0u;
@@ -2598,6 +2632,7 @@ __global__ __launch_bounds__(kGridBlock) void frame_build_kernel(
   __syncthreads();
   if (t == 0)
     __hip_atomic_store(&reinterpret_cast<GridSummary *>(hsum)->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  stamp(6);
 }
 
 // After verify: every segment with a bad chunk -> one compact GridBad entry
@@ -2848,13 +2883,14 @@ hipError_t launch_grid_finalize(const SegDev *segs, uint32_t nseg, const uint32_
 
 hipError_t launch_frame_grid(const uint8_t *s, uint64_t len, uint64_t base, uint32_t count, int proto, uint32_t cs,
                              int ctype, int verify, uint32_t sflags, uint8_t *bm_base, uint8_t *copy_base,
-                             uint64_t copy_cap, int win, int64_t client_offset, GridBufs g, hipStream_t stream) {
+                             uint64_t copy_cap, int win, int64_t client_offset, GridBufs g, hipStream_t stream,
+                             unsigned long long *stamps) {
   if (!count || count > kGridMaxCount || base >= len || !g.seq) return hipErrorInvalidValue;
   const uint32_t nblk = (count + kGridBlock - 1) / kGridBlock;
   hipLaunchKernelGGL(frame_build_kernel, dim3(nblk), dim3(kGridBlock), 0, stream, s, len, base, count, proto, cs,
                      ctype, verify, sflags, bm_base, copy_base, copy_cap, win, client_offset, g.recs,
                      reinterpret_cast<GridLook *>(g.look), g.segs, g.seg2pkt, g.fb, g.gctr, g.done, g.exc, g.sum,
-                     g.hsum, g.seq);
+                     g.hsum, g.seq, kDiag ? stamps : nullptr);
   return hipGetLastError();
 }
 
@@ -3004,6 +3040,7 @@ hipError_t launch_tiles(int mode, int order, int nt, int depth, int streams, int
   // tests/test_gpu_shapes.py, each launched only when requested exactly.
 #define HDFS_LAUNCH_ALL(M)                                                                      \
   HDFS_LAUNCH_PRODUCT(M)                                                                        \
+  else if (HDFS_SHAPE(3, 2, 4, 1, 1024)) HDFS_LAUNCH(M, 3, 1, 4, 1, 1024, 1);                   \
   else if (HDFS_SHAPE(3, 1, 3, 1, 1024)) HDFS_LAUNCH(M, 3, 1, 3, 1, 1024, 0);                   \
   else if (HDFS_SHAPE(3, 1, 4, 1, 1024)) HDFS_LAUNCH(M, 3, 1, 4, 1, 1024, 0);                   \
   else if (HDFS_SHAPE(3, 1, 2, 2, 1024)) HDFS_LAUNCH(M, 3, 1, 2, 2, 1024, 0);                   \
@@ -3032,6 +3069,8 @@ hipError_t launch_tiles(int mode, int order, int nt, int depth, int streams, int
     else if (HDFS_SHAPE(5, 2, 3, 1, 1024)) HDFS_LAUNCH_CUG(kModeCompute, 3, 1, 3, 1, 1024, 1, 0, 0, 1);
     else if (HDFS_SHAPE(6, 2, 3, 1, 1024)) HDFS_LAUNCH_CUG(kModeCompute, 3, 1, 3, 1, 1024, 1, 0, 0, 2);
     else if (HDFS_SHAPE(7, 2, 3, 1, 1024)) HDFS_LAUNCH(kModeCompute, 7, 1, 3, 1, 1024, 1);
+    else if (HDFS_SHAPE(7, 2, 4, 1, 1024)) HDFS_LAUNCH(kModeCompute, 7, 1, 4, 1, 1024, 1);
+    else if (HDFS_SHAPE(5, 2, 4, 1, 1024)) HDFS_LAUNCH_CUG(kModeCompute, 3, 1, 4, 1, 1024, 1, 0, 0, 1);
     else return hipErrorInvalidValue;
   }
 #undef HDFS_LAUNCH_ALL

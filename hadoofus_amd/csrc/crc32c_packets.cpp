@@ -737,7 +737,8 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
     const uint64_t done_b = std::min(payload, co.cap);
     hipError_t e = launch_frame_grid(d, len, pos, count, proto, cs, ctype, verify ? 1 : 0, sflags, dg + L.bm,
                                      co.dst ? co.dst + done_b : nullptr, co.dst ? co.cap - done_b : 0, co.win ? 1 : 0,
-                                     co.client_offset, gb, c.stream);
+                                     co.client_offset, gb, c.stream,
+                                     (kDiag && g_diag) ? g_diag + kFrameStampOff : nullptr);
     if (e != hipSuccess) {
       rc = fail(HDFS_CRC32C_EHIP, "device framing: %s", hipGetErrorString(e));
       break;
