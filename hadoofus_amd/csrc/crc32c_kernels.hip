@@ -2216,14 +2216,27 @@ DEV uint64_t grid_stride(const uint8_t *s, uint64_t len, uint64_t base, int prot
 // within kHdrWin bytes of the stream end is framed from memory directly).
 // (Buffer loads: they serve any byte address; a global_load_dwordx4 at an
 // address that is not 4-B aligned returns the aligned-down bytes.)
-DEV void stage_header(const uint8_t *s, uint64_t len, uint64_t pos, uint8_t *win) {
-  if (len - pos < kHdrWin) return;
-  const __amdgpu_buffer_rsrc_t rs =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(s + pos), 0, static_cast<int>(kHdrWin), 0x00020000);
+// The packet sits at ub + voff: ub wave-uniform (the descriptor's base, in
+// SGPRs), voff per lane.  A descriptor built from a per-lane address is a
+// waterfall loop -- one pass per distinct lane address, and the compiler
+// waited for each of the four loads before issuing the next: four
+// dependent HBM round trips, 12.8 of a 1 GiB framing pass's 31 us
+// (tools/frame_phases.py); now the four loads of every lane go out together.
+DEV void stage_header(const uint8_t *s, uint64_t len, uint64_t ub, uint32_t voff, uint8_t *win) {
+  const uint64_t pos = ub + voff;
+  const uint64_t span = len > ub ? len - ub : 0;
+  const uint32_t nrec = span > 0xFFFFFFFFull ? 0xFFFFFFFFu : static_cast<uint32_t>(span);
+  // readfirstlane: the fields are uniform, and the compiler must see it (a
+  // descriptor it takes for divergent is a waterfall loop again)
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<uint8_t *>(rfl64(reinterpret_cast<uint64_t>(s + ub))), 0, static_cast<int>(rfl(nrec)), 0x00020000);
+  if (pos > len || len - pos < kHdrWin) return;
+  u32x4 v[kHdrWin / 16];
 #pragma unroll
   for (int k = 0; k < int(kHdrWin / 16); k++)
-    *reinterpret_cast<u32x4 *>(win + 16 * k) =
-        __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * k, 0, 0));
+    v[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff + 16u * k, 0, 0));
+#pragma unroll
+  for (int k = 0; k < int(kHdrWin / 16); k++) *reinterpret_cast<u32x4 *>(win + 16 * k) = v[k];
 }
 
 // frame_step on the staged header when it holds the whole header, on the
@@ -2248,30 +2261,33 @@ constexpr uint32_t kGridBlock = 64;
 
 // One device framing pass in one launch: frame the grid points, then a
 // single-pass scan of their shares of the segment table over the blocks
-// (decoupled look-back: a block publishes its own sums at once and takes the
-// sums of the blocks before it from their published records, 64 at a time,
-// stopping at the nearest block whose inclusive prefix is out), then the
-// verify segment entries of the run's packets, the run's summary and, from
-// the last block to finish, the host copy.  Block b only waits for blocks
-// < b, which the dispatcher started before it, so the wait ends.
-// Look-back record of one block; flag = (pass seq << 2) | state, state 1:
-// agg / amin out, 2: inc / imin out too.  Tagging with the pass's sequence
-// number means no reset between passes (the area is zeroed once when it is
-// allocated; seqs start at 1).  Every field is written and read with
-// agent-scope relaxed atomics (write-through stores, loads past this XCD's
-// L2) and a record's flag is stored only after its fields' stores are
-// acknowledged (s_waitcnt vmcnt(0)): no L2 write-back or invalidate per
-// publish -- with an agent-scope fence per publish and per look-back window
-// the pass took 62 us instead of ~35.
+// (each block publishes its own sums at once and adds up the published
+// sums of every block before it: at most kGridMaxCount / 64 = 1 024 blocks,
+// so at most 16 records per lane, read in one batch once all are out), then
+// the verify segment entries of the run's packets, the run's summary and,
+// from the last block to finish, the host copy.  Block b only waits for
+// blocks < b, which the dispatcher started before it, so the wait ends.
+// (A decoupled look-back -- windows of 64 predecessors back to the nearest
+// published inclusive prefix -- chained 4 windows deep for a 1 GiB run:
+// look-back done at 22 us median, tools/frame_phases.py.)
+// Aggregate record of one block; flag = (pass seq << 2) | 1 once agg / mins
+// are out.  Tagging with the pass's sequence number means no reset between
+// passes (the area is zeroed once when it is allocated; seqs start at 1).
+// Every field is written and read with agent-scope relaxed atomics
+// (write-through stores, loads past this XCD's L2) and a record's flag is
+// stored only after its fields' stores are acknowledged (s_waitcnt
+// vmcnt(0)): no L2 write-back or invalidate per publish -- with an
+// agent-scope fence per publish and per look-back window the pass took
+// 62 us instead of ~35.
 struct GridLook {
   uint64_t agg[6];   // the block's shares of the recorded packets' table
-  uint64_t inc[6];   // shares of blocks 0..b
-  uint64_t mins;     // amin | imin << 32: first grid point that is not On (~0: none), in the block / blocks 0..b
+  uint64_t mins;     // first grid point of the block that is not On (~0: none)
   uint64_t flag;
   uint64_t rec0[7];  // block 0 only: packet 0's record (the prediction of the others)
   uint64_t T;        // block 0 only: main tiles of packet 0's segment (the uniform layout's tiles per segment)
-  uint64_t pad[10];
+  uint64_t pad[16];
 };
+constexpr uint32_t kGridLookPerLane = kGridMaxCount / kGridBlock / 64;  // predecessor records per lane, at most
 static_assert(sizeof(GridLook) == kGridLookBytes, "look-back record");
 static_assert(sizeof(hdfs_crc32c_packet) == 7 * 8, "packet 0's record in the look-back area");
 
@@ -2307,7 +2323,7 @@ __global__ __launch_bounds__(kGridBlock) void frame_build_kernel(
   // size frame_step gives a complete, clean packet, so no thread decodes
   // packet 0's PacketHeaderProto just to find the grid.  If packet 0 is not
   // such a packet its status ends the run (first_break = 0).
-  const uint64_t stride = grid_stride(s, len, base, proto);
+  const uint64_t stride = rfl64(grid_stride(s, len, base, proto));  // one value in every lane
   // Grid points past the stream's end are kGridMore, so the run ends at the
   // latest at k0 = ceil((len - base) / stride), the first point at or past
   // the end: the pass acts on points [0, ceff), ceff = k0 + 1 (1 without a
@@ -2336,7 +2352,10 @@ __global__ __launch_bounds__(kGridBlock) void frame_build_kernel(
   if (k < ceff && (k == 0 || stride)) {
     const uint64_t pos = base + uint64_t(k) * stride;
     if (pos < len) {
-      stage_header(s, len, pos, win[t]);
+      // the block's headers through one descriptor at its first point when
+      // the block's points lie within 2^32 bytes of it (strides < 64 MiB)
+      if (stride < (1ull << 26)) stage_header(s, len, base + uint64_t(b) * kGridBlock * stride, t * uint32_t(stride), win[t]);
+      else stage_header(s, len, pos, 0u, win[t]);
       const int st = grid_frame(s, len, pos, win[t], proto, cs, ctype, r, total);
       code = st == frame::kStepMore ? kGridMore
            : st == frame::kStepStop ? kGridStop
@@ -2373,10 +2392,8 @@ __global__ __launch_bounds__(kGridBlock) void frame_build_kernel(
     GridLook &L = look[b];
 #pragma unroll
     for (int q = 0; q < 6; q++) at_st(&L.agg[q], v[q]);
+    at_st(&L.mins, uint64_t(m) | 0xFFFFFFFF00000000ull);
     if (b == 0) {
-#pragma unroll
-      for (int q = 0; q < 6; q++) at_st(&L.inc[q], v[q]);
-      at_st(&L.mins, uint64_t(m) | (uint64_t(m) << 32));
       const uint64_t *x = reinterpret_cast<const uint64_t *>(&r);
 #pragma unroll
       for (int q = 0; q < 7; q++) at_st(&L.rec0[q], x[q]);
@@ -2386,78 +2403,49 @@ __global__ __launch_bounds__(kGridBlock) void frame_build_kernel(
       at_st32(&done[0], 0u);  // blocks finished
       at_st32(&done[1], 0u);  // exceptions found
       sum->stride = stride;
-    } else {
-      at_st(&L.mins, uint64_t(m) | 0xFFFFFFFF00000000ull);
     }
     stores_done();
-    at_st(&L.flag, tag | (b == 0 ? 2u : 1u));
+    at_st(&L.flag, tag | 1u);
   }
   stamp(2);
-  // 3. look back: the shares and first break of blocks 0..b-1.  Lane i looks
-  // at block j0 - i; a window is used up to its nearest block with an
-  // inclusive prefix (that block's inc, the aggregates of the blocks after
-  // it), and read only when every block it needs has published.
+  // 3. the shares and first break of blocks 0..b-1: lane i adds up the
+  // records of blocks i, i + 64, ... < b, read once every one of them is out
+  // (all flag loads of a lane issued together, then all field loads), then
+  // one wave reduction.  Block 0's flag is among them: its record and counter
+  // resets are out before this block uses them.
   uint64_t pre[6] = {0, 0, 0, 0, 0, 0};
   uint32_t pmin = 0xFFFFFFFFu;
   if (b > 0) {
-    for (int64_t j0 = int64_t(b) - 1; j0 >= 0; j0 -= 64) {
-      const int64_t j = j0 - int64_t(lane);
-      uint32_t state = 0, spins = 0;
-      uint64_t bal2 = 0, need = 0;
-      for (;;) {
-        const uint64_t f = j >= 0 ? at_ld(&look[j].flag) : (tag | 2u);  // before block 0: an empty inclusive prefix
-        state = (f >> 2) == uint64_t(seq) ? uint32_t(f & 3u) : 0u;
-        bal2 = __ballot(state == 2u);
-        const uint32_t lim = bal2 ? static_cast<uint32_t>(__builtin_ctzll(bal2)) : 63u;
-        need = lim == 63u ? ~0ull : ((2ull << lim) - 1ull);
-        if ((__ballot(state == 0u) & need) == 0ull) break;
-        if (++spins > (1u << 24)) {  // never expected (blocks < b run to their publish): fail loudly, see the gather
-          asm volatile("s_trap 2");
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
+    for (uint32_t spins = 0;;) {
+      bool out = true;
+#pragma unroll
+      for (uint32_t q = 0; q < kGridLookPerLane; q++) {
+        const uint32_t j = lane + 64u * q;
+        if (j < b) out &= at_ld(&look[j].flag) == (tag | 1u);
       }
-      // (the fields are read after their flags: these loads issue only once
-      // the loop above has seen the flags)
-      const uint32_t lim = bal2 ? static_cast<uint32_t>(__builtin_ctzll(bal2)) : 63u;
-      uint64_t x[6] = {0, 0, 0, 0, 0, 0};
-      uint32_t xm = 0xFFFFFFFFu;
-      if (j >= 0 && ((need >> lane) & 1ull)) {
-        const GridLook &L = look[j];
-        const bool useinc = bal2 && lane == lim;
-#pragma unroll
-        for (int q = 0; q < 6; q++) x[q] = at_ld(useinc ? &L.inc[q] : &L.agg[q]);
-        const uint64_t mm = at_ld(&L.mins);
-        xm = static_cast<uint32_t>(useinc ? mm >> 32 : mm);
-      }
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) {
-#pragma unroll
-        for (int q = 0; q < 6; q++) x[q] += __shfl_xor(x[q], off);
-        xm = min(xm, static_cast<uint32_t>(__shfl_xor(static_cast<int>(xm), off)));
-      }
-#pragma unroll
-      for (int q = 0; q < 6; q++) pre[q] += x[q];
-      pmin = min(pmin, xm);
-      if (bal2) break;
-    }
-    // publish the inclusive prefix for the blocks after this one
-    if (lane == 0) {
-      GridLook &L = look[b];
-#pragma unroll
-      for (int q = 0; q < 6; q++) at_st(&L.inc[q], pre[q] + v[q]);
-      at_st(&L.mins, uint64_t(m) | (uint64_t(min(pmin, m)) << 32));
-      stores_done();
-      at_st(&L.flag, tag | 2u);
-    }
-    // block 0's record (and its counter resets) before this block uses them
-    // (usually already seen through the look-back)
-    for (uint32_t spins = 0; (at_ld(&look[0].flag) >> 2) != uint64_t(seq);) {
-      if (++spins > (1u << 24)) {
+      if (__ballot(!out) == 0ull) break;
+      if (++spins > (1u << 24)) {  // never expected (blocks < b run to their publish): fail loudly, see the gather
         asm volatile("s_trap 2");
         break;
       }
       __builtin_amdgcn_s_sleep(1);
+    }
+    // (the fields are read after their flags: these loads issue only once the
+    // loop above has seen every flag)
+#pragma unroll
+    for (uint32_t q = 0; q < kGridLookPerLane; q++) {
+      const uint32_t j = lane + 64u * q;
+      if (j < b) {
+#pragma unroll
+        for (int f = 0; f < 6; f++) pre[f] += at_ld(&look[j].agg[f]);
+        pmin = min(pmin, static_cast<uint32_t>(at_ld(&look[j].mins)));
+      }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+#pragma unroll
+      for (int f = 0; f < 6; f++) pre[f] += __shfl_xor(pre[f], off);
+      pmin = min(pmin, static_cast<uint32_t>(__shfl_xor(static_cast<int>(pmin), off)));
     }
   }
   stamp(3);
@@ -2700,7 +2688,7 @@ __global__ __launch_bounds__(1024) void small_run_kernel(const uint8_t *__restri
     uint64_t total = 0;
     const uint64_t pos = uint64_t(pk) * stride;
     if ((pk == 0 || stride) && pos < len) {
-      stage_header(s, len, pos, win[tid]);
+      stage_header(s, len, 0u, static_cast<uint32_t>(pos), win[tid]);  // pos < len <= kSmallRunBytes
       const int st = grid_frame(s, len, pos, win[tid], proto, cs, ctype, r, total);
       code = st == frame::kStepMore ? kGridMore : st == frame::kStepStop ? kGridStop : total == stride ? kGridOn : kGridOff;
     }
@@ -2754,11 +2742,14 @@ __global__ __launch_bounds__(1024) void small_run_kernel(const uint8_t *__restri
     const uint8_t *crcp = s + rec.stream_off + rec.header_len;
     const uint8_t *dp = crcp + rec.crc_len;
     for (uint32_t j = tid; j < nch; j += 1024u) acc[j] = 0u;
-    // the piece's 64 bytes (any byte alignment: buffer loads; past dlen: zeros)
-    const __amdgpu_buffer_rsrc_t rd =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(dp), 0, static_cast<int>(dlen), 0x00020000);
-    const __amdgpu_buffer_rsrc_t rc =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(crcp), 0, static_cast<int>(nch * 4u), 0x00020000);
+    // the piece's 64 bytes (any byte alignment: buffer loads; past dlen: zeros).
+    // rec is in LDS, so the compiler takes its fields for divergent:
+    // readfirstlane keeps the descriptors in SGPRs (no waterfall loops)
+    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<uint8_t *>(rfl64(reinterpret_cast<uint64_t>(dp))), 0, static_cast<int>(rfl(dlen)), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<uint8_t *>(rfl64(reinterpret_cast<uint64_t>(crcp))), 0, static_cast<int>(rfl(nch * 4u)),
+        0x00020000);
     const uint32_t b0 = 64u * tid;
     uint32_t d[16];
 #pragma unroll
@@ -2828,8 +2819,8 @@ __global__ __launch_bounds__(1024) void small_run_kernel(const uint8_t *__restri
       // 16-B pieces inside the window go out whole; a piece at an edge of it
       // (a read starting or ending inside the packet, the packet's last
       // partial 16 B) byte by byte
-      const uint32_t w0 = ctl[9], w1 = ctl[10];
-      uint8_t *dst = copy_dst + ((uint64_t(ctl[7]) << 32) | ctl[6]) - w0;
+      const uint32_t w0 = rfl(ctl[9]), w1 = rfl(ctl[10]);  // LDS words: uniform, in SGPRs
+      uint8_t *dst = copy_dst + ((uint64_t(rfl(ctl[7])) << 32) | rfl(ctl[6])) - w0;
       const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(dst, 0, static_cast<int>(w1), 0x00020000);
 #pragma unroll
       for (uint32_t m = 0; m < 4; m++) {

@@ -11,3 +11,5 @@ timeout -k 10 600 python -u -m pytest tests/test_packets.py tests/test_device_ch
 tail -3 gpurun_out/${TAG}_tests.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python tools/device_stream_bench.py > gpurun_out/${TAG}_dstream.json 2> gpurun_out/${TAG}_dstream.err \
   && cat gpurun_out/${TAG}_dstream.json
+timeout -k 10 300 python tools/frame_phases.py > gpurun_out/${TAG}_phases.json 2> gpurun_out/${TAG}_phases.err \
+  && cat gpurun_out/${TAG}_phases.json
