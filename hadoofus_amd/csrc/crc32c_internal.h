@@ -180,6 +180,7 @@ constexpr uint32_t kGatherSlice = 65536;  // data bytes per gather workgroup
 constexpr uint32_t kHdrWin = 64;          // header-window row bytes (device packet streams)
 
 constexpr uint32_t kGridMaxCount = 65536;  // grid points per device framing pass
+constexpr uint32_t kGridGroups = kGridMaxCount / 64 / 64;  // frame_build_kernel: group totals after the block records
 
 // Short device-resident runs (the per-read case): small_run_kernel frames
 // and verifies up to kSmallRunMax packets of <= kSmallMax data bytes in ONE

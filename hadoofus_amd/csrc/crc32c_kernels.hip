@@ -2261,9 +2261,10 @@ constexpr uint32_t kGridBlock = 64;
 
 // One device framing pass in one launch: frame the grid points, then a
 // single-pass scan of their shares of the segment table over the blocks
-// (each block publishes its own sums at once and adds up the published
-// sums of every block before it: at most kGridMaxCount / 64 = 1 024 blocks,
-// so at most 16 records per lane, read in one batch once all are out), then
+// (each block publishes its own sums at once; the sums before it are the
+// records of its group of 64 blocks before it plus the totals of the
+// earlier groups, which each group's last block publishes: two levels, no
+// chain), then
 // the verify segment entries of the run's packets, the run's summary and,
 // from the last block to finish, the host copy.  Block b only waits for
 // blocks < b, which the dispatcher started before it, so the wait ends.
@@ -2287,7 +2288,6 @@ struct GridLook {
   uint64_t T;        // block 0 only: main tiles of packet 0's segment (the uniform layout's tiles per segment)
   uint64_t pad[16];
 };
-constexpr uint32_t kGridLookPerLane = kGridMaxCount / kGridBlock / 64;  // predecessor records per lane, at most
 static_assert(sizeof(GridLook) == kGridLookBytes, "look-back record");
 static_assert(sizeof(hdfs_crc32c_packet) == 7 * 8, "packet 0's record in the look-back area");
 
@@ -2408,21 +2408,34 @@ __global__ __launch_bounds__(kGridBlock) void frame_build_kernel(
     at_st(&L.flag, tag | 1u);
   }
   stamp(2);
-  // 3. the shares and first break of blocks 0..b-1: lane i adds up the
-  // records of blocks i, i + 64, ... < b, read once every one of them is out
-  // (all flag loads of a lane issued together, then all field loads), then
-  // one wave reduction.  Block 0's flag is among them: its record and counter
-  // resets are out before this block uses them.
+  // 3. the shares and first break of blocks 0..b-1, in two levels with no
+  // chain between them: (a) lane l < i reads block 64 g + l of this block's
+  // group of 64 (g = b / 64, i = b % 64); (c) the group's last block then
+  // publishes the group's total (its 64 aggregates) at once; (b) lane h < g
+  // reads the total of group h.  A block waits for at most 63 block records
+  // and 15 group records, each lane's flag loads issued together, then its
+  // field loads: O(64 + B / 64) records per block for B blocks.  Block 0's
+  // flag is seen through (a) or through group 0's total (published after
+  // its last block saw block 0's flag; every record is acknowledged at the
+  // point of coherence before its flag): its record and counter resets are
+  // out before this block uses them.
   uint64_t pre[6] = {0, 0, 0, 0, 0, 0};
   uint32_t pmin = 0xFFFFFFFFu;
-  if (b > 0) {
-    for (uint32_t spins = 0;;) {
-      bool out = true;
+  // packet 0's record and T (the prediction step 4 checks against): block
+  // 0's own lane 0, or loaded by lane 0 once block 0 is known to be out (one
+  // request per block on block 0's record, not one per use)
+  uint64_t r0w[7];
+  uint64_t T64 = a.nseg ? a.mtiles : 0u;
+  {
+    const uint64_t *x = reinterpret_cast<const uint64_t *>(&r);
 #pragma unroll
-      for (uint32_t q = 0; q < kGridLookPerLane; q++) {
-        const uint32_t j = lane + 64u * q;
-        if (j < b) out &= at_ld(&look[j].flag) == (tag | 1u);
-      }
+    for (int q = 0; q < 7; q++) r0w[q] = x[q];
+  }
+  const uint32_t gi = b / 64u, ii = b % 64u;
+  GridLook *const grp = look + kGridMaxCount / kGridBlock;  // kGridGroups group records
+  auto wait_flag = [&](const GridLook *rec, bool want) {
+    for (uint32_t spins = 0;;) {
+      const bool out = !want || at_ld(&rec->flag) == (tag | 1u);
       if (__ballot(!out) == 0ull) break;
       if (++spins > (1u << 24)) {  // never expected (blocks < b run to their publish): fail loudly, see the gather
         asm volatile("s_trap 2");
@@ -2430,16 +2443,14 @@ __global__ __launch_bounds__(kGridBlock) void frame_build_kernel(
       }
       __builtin_amdgcn_s_sleep(1);
     }
-    // (the fields are read after their flags: these loads issue only once the
-    // loop above has seen every flag)
+  };
+  if (ii > 0) {  // (a)
+    const GridLook *rec = &look[gi * 64u + lane];
+    wait_flag(rec, lane < ii);
+    if (lane < ii) {
 #pragma unroll
-    for (uint32_t q = 0; q < kGridLookPerLane; q++) {
-      const uint32_t j = lane + 64u * q;
-      if (j < b) {
-#pragma unroll
-        for (int f = 0; f < 6; f++) pre[f] += at_ld(&look[j].agg[f]);
-        pmin = min(pmin, static_cast<uint32_t>(at_ld(&look[j].mins)));
-      }
+      for (int f = 0; f < 6; f++) pre[f] = at_ld(&rec->agg[f]);
+      pmin = static_cast<uint32_t>(at_ld(&rec->mins));
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
@@ -2447,6 +2458,43 @@ __global__ __launch_bounds__(kGridBlock) void frame_build_kernel(
       for (int f = 0; f < 6; f++) pre[f] += __shfl_xor(pre[f], off);
       pmin = min(pmin, static_cast<uint32_t>(__shfl_xor(static_cast<int>(pmin), off)));
     }
+  }
+  if (ii == 63u && (uint64_t(b) + 1u) * kGridBlock < ceff && lane == 0) {  // (c) a later block needs it
+    GridLook &G = grp[gi];
+#pragma unroll
+    for (int f = 0; f < 6; f++) at_st(&G.agg[f], pre[f] + v[f]);
+    at_st(&G.mins, uint64_t(min(pmin, m)) | 0xFFFFFFFF00000000ull);
+    stores_done();
+    at_st(&G.flag, tag | 1u);
+  }
+  if (gi > 0) {  // (b)
+    const GridLook *rec = &grp[lane];
+    wait_flag(rec, lane < gi);
+    uint64_t x[6] = {0, 0, 0, 0, 0, 0};
+    uint32_t xm = 0xFFFFFFFFu;
+    if (lane < gi) {
+#pragma unroll
+      for (int f = 0; f < 6; f++) x[f] = at_ld(&rec->agg[f]);
+      xm = static_cast<uint32_t>(at_ld(&rec->mins));
+    }
+    if (lane == 0) {  // (group 0's total is out: so is block 0)
+#pragma unroll
+      for (int q = 0; q < 7; q++) r0w[q] = at_ld(&look[0].rec0[q]);
+      T64 = at_ld(&look[0].T);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+#pragma unroll
+      for (int f = 0; f < 6; f++) x[f] += __shfl_xor(x[f], off);
+      xm = min(xm, static_cast<uint32_t>(__shfl_xor(static_cast<int>(xm), off)));
+    }
+#pragma unroll
+    for (int f = 0; f < 6; f++) pre[f] += x[f];
+    pmin = min(pmin, xm);
+  } else if (b > 0 && lane == 0) {  // group 0: block 0 was seen in (a)
+#pragma unroll
+    for (int q = 0; q < 7; q++) r0w[q] = at_ld(&look[0].rec0[q]);
+    T64 = at_ld(&look[0].T);
   }
   stamp(3);
   // 4. the run's end as this block sees it: the first point that is not On
@@ -2456,7 +2504,9 @@ __global__ __launch_bounds__(kGridBlock) void frame_build_kernel(
   const uint32_t fbk = min(min(pmin, m), ceff);
   const bool past = pmin != 0xFFFFFFFFu;
   const bool inrun = !past && (k < fbk || (k == fbk && k < ceff && code != kGridMore));
-  const uint32_t T = static_cast<uint32_t>(at_ld(&look[0].T));
+#pragma unroll
+  for (int q = 0; q < 7; q++) r0w[q] = static_cast<uint64_t>(__shfl(static_cast<long long>(r0w[q]), 0));
+  const uint32_t T = static_cast<uint32_t>(__shfl(static_cast<long long>(T64), 0));
   if (!past) {
     // in-block exclusive scan of the recorded points' shares
     const uint64_t own[6] = {inrun ? a.nseg : 0u, inrun ? a.rounds : 0u, inrun ? a.mtiles : 0u,
@@ -2527,7 +2577,7 @@ __global__ __launch_bounds__(kGridBlock) void frame_build_kernel(
         hdfs_crc32c_packet p;
         uint64_t *px = reinterpret_cast<uint64_t *>(&p);
 #pragma unroll
-        for (int q = 0; q < 7; q++) px[q] = at_ld(&look[0].rec0[q]);
+        for (int q = 0; q < 7; q++) px[q] = r0w[q];
         p.stream_off = base + uint64_t(k) * stride;
         p.offset_in_block += int64_t(k) * p.data_len;
         p.seqno += int64_t(k);

@@ -518,7 +518,7 @@ struct GridLayout {
     // same bytes of the slot, zeroed when the slot is allocated and written
     // by nothing else, so a record's flag is either 0 or tagged with the
     // sequence number of the pass that wrote it
-    look = take(size_t(kGridMaxCount / 64) * kGridLookBytes);
+    look = take(size_t(kGridMaxCount / 64 + kGridGroups) * kGridLookBytes);
     recs = take(size_t(count) * sizeof(hdfs_crc32c_packet));
     segs = take(size_t(count) * sizeof(SegDev));
     seg2pkt = take(size_t(count) * 4);

@@ -620,3 +620,57 @@ def test_gpu_copy_out_mixed_sizes_never_past_cap(engine, oracle):
     assert dst.download(4096, offset=cap).tobytes() == b"\xa5" * 4096
     keep.free()
     dst.free()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["v1_regular", "v2_seq_jump", "v1_break_group1", "v1_max_pkts", "v2_read_window"])
+def test_gpu_device_stream_many_blocks(engine, oracle, case):
+    """Device framing passes of 9 000 small packets: 141 framing blocks in 3
+    groups of 64, so a block's prefix comes from both levels of
+    frame_build_kernel's scan (its group's block records and earlier groups'
+    totals).  Regular v1 runs with bad chunks spread over the groups; v2
+    with a seqno jump and a skewed offsetInBlock in later groups (records
+    off the prediction, same wire size: exceptions, no break); a packet of
+    another size in group 1 (the pass breaks there, the walk goes on);
+    max_pkts inside group 1; a client read window starting and ending in
+    later groups.  Records, verdicts, consumed bytes and copied bytes equal
+    the oracle's."""
+    n, cs = 9000, 512
+    proto = 2 if case.startswith("v2") else 1
+    dl = [512] * n
+    kw = {}
+    if case == "v1_break_group1":
+        dl[5000] = 700
+    if proto == 2:
+        # header varints of one length over the whole run (offsetInBlock in
+        # [2^21, 2^28), seqno in [2^14, 2^21)): every packet on one grid
+        kw["offset0"] = 1 << 21
+        kw["seqnos"] = [20000 + k for k in range(n)]
+    if case == "v2_seq_jump":
+        kw["seqnos"] = [20000 + k + (100 if k >= 6000 else 0) for k in range(n)]
+        kw["offset_skew"] = {8500: 4096}
+    corrupt = [(3, 0), (4100, 0), (6000, 0), (8999, 0)]
+    s, bad = build_stream(oracle.crc32c, proto, cs, CSUM_CRC32C, dl, seed=11, corrupt=corrupt, last_empty=False, **kw)
+    keep, p = _dev(engine, s, 0)
+    try:
+        if case == "v2_read_window":
+            co, rl = (1 << 21) + 4600 * 512 + 77, 3000 * 512
+            want = oracle.read_packets(s, co, rl, proto, cs, CSUM_CRC32C)
+            dst = engine.DeviceBuffer(rl + 64)
+            dst.fill(0xA5)
+            got = engine.verify_packets_copy(p, len(s), dst.ptr, rl, proto, cs, CSUM_CRC32C, client_offset=co,
+                                             read_len=rl)
+            assert got[:3] == want[:3]
+            assert dst.download(got[3]).tobytes() == want[3]
+            assert dst.download(64, offset=rl).tobytes() == b"\xa5" * 64
+            dst.free()
+            return
+        mp = 8000 if case == "v1_max_pkts" else None
+        want = oracle.verify_packets(s, proto, cs, CSUM_CRC32C, max_pkts=mp)
+        got = engine.verify_packets(None, proto, cs, CSUM_CRC32C, max_pkts=mp, dptr=p, nbytes=len(s))
+        assert got == want
+        if mp is None:
+            assert {k: (q["first_bad"], q["bad_chunks"]) for k, q in enumerate(got[1]) if q["error"] == BAD} == \
+                {k: (v[0], len(v)) for k, v in bad.items()}
+    finally:
+        keep.free()
