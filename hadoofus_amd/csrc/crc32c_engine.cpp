@@ -519,6 +519,12 @@ int small_call(DevCtx &c, int mode, uint32_t len, uint32_t cs, uint32_t reg0, bo
   }
   // a VRAM stage is write-combining: drain it before the launch
   if (c.stage_vram) __builtin_ia32_sfence();
+  // a fault of EARLIER work on the stream is this call's error, not the next
+  // caller's: one query before the launch, while the stream is idle (0.1 us;
+  // a query right after the kernel's completion word, with the dispatch
+  // still retiring, cost every call ~5 us: profiles/r03/small_launch_query_*)
+  if (const hipError_t q = hipStreamQuery(c.stream); q != hipSuccess && q != hipErrorNotReady)
+    return fail(HDFS_CRC32C_EHIP, "earlier work on the stream: %s", hipGetErrorString(q));
   const uint32_t seq = ++c.small_seq;
   const auto tl = std::chrono::steady_clock::now();
   HIPCHK(launch_small_chunks(mode, dsrc ? dsrc : c.dv_small_in, len, dsrc ? 1u : 0u, cs, reg0, be ? 1u : 0u,
@@ -528,12 +534,8 @@ int small_call(DevCtx &c, int mode, uint32_t len, uint32_t cs, uint32_t reg0, bo
   const auto t0 = std::chrono::steady_clock::now();
   for (uint32_t spin = 1;; spin++) {
     if (__atomic_load_n(&c.h_small_out[2], __ATOMIC_ACQUIRE) == seq) {
-      // the sequence number is the kernel's last memory operation (a fault of
-      // this launch cannot be followed by it); one query of the stream makes
-      // a fault of EARLIER work on it this call's error, not the next caller's
-      const hipError_t q = hipStreamQuery(c.stream);
-      if (q != hipSuccess && q != hipErrorNotReady)
-        return fail(HDFS_CRC32C_EHIP, "small kernel: %s", hipGetErrorString(q));
+      // the sequence number is the kernel's last memory operation: a fault of
+      // this launch cannot be followed by it (earlier work: queried above)
       if (g_small_trace) {  // diagnostic: host launch / wait time, kernel phase stamps (10 ns ticks)
         const auto t1 = std::chrono::steady_clock::now();
         const uint32_t *m = c.h_small_out;

@@ -590,6 +590,11 @@ int small_run(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
     HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&c.sr_hd), c.sr_h, 0));
   }
   const uint32_t count = uint32_t(std::min<uint64_t>({uint64_t(kSmallRunMax), uint64_t(max_pkts), len / 6 + 1}));
+  // a fault of earlier work on the stream is this call's error, not the next
+  // caller's: queried before the launch, on an idle stream (after the
+  // completion words, with the dispatch still retiring, the query cost ~5 us)
+  if (const hipError_t q = hipStreamQuery(c.stream); q != hipSuccess && q != hipErrorNotReady)
+    return fail(HDFS_CRC32C_EHIP, "earlier work on the stream: %s", hipGetErrorString(q));
   const uint32_t seq = next_grid_seq(c);
   const int tset = ctype == HDFS_CRC32C_CSUM_CRC32 ? 1 : 0;
   HIPCHK(launch_small_run(d, len, count, proto, cs, ctype, verify ? 1 : 0, c.d_tab_main_t[tset], c.d_tab_pow2_t[tset],
@@ -612,10 +617,7 @@ int small_run(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
     }
   }
   // every slot is published (each workgroup's sequence word is its last
-  // memory operation, so a fault of this launch cannot be followed by it);
-  // a fault of earlier work on the stream is this call's error, not the next
-  if (const hipError_t q = hipStreamQuery(c.stream); q != hipSuccess && q != hipErrorNotReady)
-    return fail(HDFS_CRC32C_EHIP, "short-run kernel: %s", hipGetErrorString(q));
+  // memory operation, so a fault of this launch cannot be followed by it)
   // the run: grid points up to the first that is not On (grid_build_kernel's rule)
   auto rec = [&](uint32_t k) {
     hdfs_crc32c_packet r;
