@@ -519,18 +519,19 @@ int small_call(DevCtx &c, int mode, uint32_t len, uint32_t cs, uint32_t reg0, bo
   }
   // a VRAM stage is write-combining: drain it before the launch
   if (c.stage_vram) __builtin_ia32_sfence();
-  // a fault of EARLIER work on the stream is this call's error, not the next
-  // caller's: one query before the launch, while the stream is idle (0.1 us;
-  // a query right after the kernel's completion word, with the dispatch
-  // still retiring, cost every call ~5 us: profiles/r03/small_launch_query_*)
-  if (const hipError_t q = hipStreamQuery(c.stream); q != hipSuccess && q != hipErrorNotReady)
-    return fail(HDFS_CRC32C_EHIP, "earlier work on the stream: %s", hipGetErrorString(q));
   const uint32_t seq = ++c.small_seq;
   const auto tl = std::chrono::steady_clock::now();
   HIPCHK(launch_small_chunks(mode, dsrc ? dsrc : c.dv_small_in, len, dsrc ? 1u : 0u, cs, reg0, be ? 1u : 0u,
                              reinterpret_cast<const uint32_t *>(c.dv_small_in + kSmallMax), c.d_tab_main_t[ctype],
                              c.d_tab_kx + ctype * kTabKxWords, ctype ? kPolyZlib : kPoly, c.dv_small_out,
                              c.dv_small_out + kSmallMeta, seq, c.stream));
+  // a fault of EARLIER work on the stream is this call's error, not the next
+  // caller's: one query while this call's kernel is in flight, so the
+  // runtime's bookkeeping of the previous dispatch overlaps the wait (a
+  // query after the completion word cost every call ~5 us, one before the
+  // launch ~3 us: profiles/r03/e2, e4 small_launch.json)
+  if (const hipError_t q = hipStreamQuery(c.stream); q != hipSuccess && q != hipErrorNotReady)
+    return fail(HDFS_CRC32C_EHIP, "earlier work on the stream: %s", hipGetErrorString(q));
   const auto t0 = std::chrono::steady_clock::now();
   for (uint32_t spin = 1;; spin++) {
     if (__atomic_load_n(&c.h_small_out[2], __ATOMIC_ACQUIRE) == seq) {

@@ -590,15 +590,14 @@ int small_run(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
     HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&c.sr_hd), c.sr_h, 0));
   }
   const uint32_t count = uint32_t(std::min<uint64_t>({uint64_t(kSmallRunMax), uint64_t(max_pkts), len / 6 + 1}));
-  // a fault of earlier work on the stream is this call's error, not the next
-  // caller's: queried before the launch, on an idle stream (after the
-  // completion words, with the dispatch still retiring, the query cost ~5 us)
-  if (const hipError_t q = hipStreamQuery(c.stream); q != hipSuccess && q != hipErrorNotReady)
-    return fail(HDFS_CRC32C_EHIP, "earlier work on the stream: %s", hipGetErrorString(q));
   const uint32_t seq = next_grid_seq(c);
   const int tset = ctype == HDFS_CRC32C_CSUM_CRC32 ? 1 : 0;
   HIPCHK(launch_small_run(d, len, count, proto, cs, ctype, verify ? 1 : 0, c.d_tab_main_t[tset], c.d_tab_pow2_t[tset],
                           co.dst, co.cap, co.win ? 1 : 0, co.client_offset, c.sr_hd, seq, c.stream));
+  // a fault of earlier work on the stream is this call's error, not the next
+  // caller's: queried while the kernel is in flight (as small_call)
+  if (const hipError_t q = hipStreamQuery(c.stream); q != hipSuccess && q != hipErrorNotReady)
+    return fail(HDFS_CRC32C_EHIP, "earlier work on the stream: %s", hipGetErrorString(q));
   auto word = [&](uint32_t k, int i) -> const uint32_t * {
     return reinterpret_cast<const uint32_t *>(c.sr_h + size_t(k) * kSrSlot + kGridRecBytes) + i;
   };
