@@ -1799,7 +1799,10 @@ __global__ __launch_bounds__(1024) void mailbox_kernel(const uint32_t *__restric
     const uint64_t ts0 = __builtin_amdgcn_s_memrealtime();  // request seen
 #endif
     __syncthreads();
-    const uint32_t seq = ctl[0], len = ctl[1], csf = ctl[2], reg0 = ctl[3];
+    // the request words are the same in every lane (LDS): readfirstlane lets
+    // the compiler see them uniform -- scalar branches, and descriptors in
+    // SGPRs instead of waterfall loops
+    const uint32_t seq = rfl(ctl[0]), len = rfl(ctl[1]), csf = rfl(ctl[2]), reg0 = rfl(ctl[3]);
     const bool dev = (csf & kMbDevFlag) != 0u;
     if (csf & kMbQuitFlag) break;  // uniform: every wave leaves here
     const uint32_t cs = csf & 0x1FFFFu, ct = (csf & kMbCrc32Flag) ? 1u : 0u;
@@ -1818,8 +1821,8 @@ __global__ __launch_bounds__(1024) void mailbox_kernel(const uint32_t *__restric
     // the end returns zeros, so that piece is read byte by byte); host
     // stage: the whole stage (bytes past len never enter a CRC)
     const __amdgpu_buffer_rsrc_t rd =
-        dev ? __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<uint8_t *>((uint64_t(ctl[5]) << 32) | ctl[4]), 0,
-                                                static_cast<int>(len), 0x00020000)
+        dev ? __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<uint8_t *>((uint64_t(rfl(ctl[5])) << 32) | rfl(ctl[4])),
+                                                0, static_cast<int>(len), 0x00020000)
             : rin;
     if (base < len) {
 #pragma unroll

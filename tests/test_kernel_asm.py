@@ -87,3 +87,30 @@ def test_no_noreturn_trap_in_kernels():
     src = open(os.path.join(CSRC, "crc32c_kernels.hip")).read()
     code = "\n".join(line.split("//")[0] for line in src.splitlines())
     assert "__builtin_trap" not in code
+
+
+def waterfall_loops(lines):
+    """{kernel symbol: number of buffer memory ops sitting in a waterfall loop}:
+    a buffer descriptor the compiler takes for divergent is rebuilt per
+    distinct lane value -- the op is followed by `s_xor_b64 exec, exec, ...`
+    and a branch back."""
+    name, res = None, {}
+    for i, line in enumerate(lines):
+        m = re.match(r"^(_ZN11hdfs_crc32c\w+):", line)
+        if m:
+            name = m.group(1)
+            continue
+        if name and re.search(r"\bbuffer_(load|store)_", line):
+            nxt = [x for x in lines[i + 1:i + 4] if x.strip() and not x.strip().startswith(";")][:1]
+            if nxt and "s_xor_b64 exec, exec" in nxt[0]:
+                res[name] = res.get(name, 0) + 1
+    return res
+
+
+def test_release_kernels_have_no_waterfall_buffer_ops(release_asm):
+    """Every buffer load / store of the release kernels uses a uniform
+    descriptor.  Round 3 found the device framing kernel's header staging
+    built from a per-lane address: a waterfall loop that also waited for
+    each of its four loads before the next (12.8 of the pass's 34 us,
+    DESIGN.md §4.2)."""
+    assert waterfall_loops(release_asm) == {}
