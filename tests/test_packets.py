@@ -623,24 +623,27 @@ def test_gpu_copy_out_mixed_sizes_never_past_cap(engine, oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["v1_regular", "v2_seq_jump", "v1_break_group1", "v1_max_pkts", "v2_read_window"])
+@pytest.mark.parametrize("case", ["v1_regular", "v2_seq_jump", "v1_break_group1", "v1_max_pkts", "v2_read_window",
+                                  "v1_two_level", "v2_two_level_break"])
 def test_gpu_device_stream_many_blocks(engine, oracle, case):
-    """Device framing passes of 9 000 small packets: 141 framing blocks in 3
-    groups of 64, so a block's prefix comes from both levels of
-    frame_build_kernel's scan (its group's block records and earlier groups'
-    totals).  Regular v1 runs with bad chunks spread over the groups; v2
+    """Device framing passes of 9 000 small packets (141 framing blocks in 3
+    groups of 64) and of 24 000 (376 blocks in 6 groups), so a block's
+    prefix comes from both levels of frame_build_kernel's scan (its group's
+    block records and earlier groups' totals).  Regular v1 runs with bad chunks spread over the groups; v2
     with a seqno jump and a skewed offsetInBlock in later groups (records
     off the prediction, same wire size: exceptions, no break); a packet of
     another size in group 1 (the pass breaks there, the walk goes on);
     max_pkts inside group 1; a client read window starting and ending in
     later groups.  Records, verdicts, consumed bytes and copied bytes equal
     the oracle's."""
-    n, cs = 9000, 512
+    n, cs = (24000 if "two_level" in case else 9000), 512
     proto = 2 if case.startswith("v2") else 1
     dl = [512] * n
     kw = {}
     if case == "v1_break_group1":
         dl[5000] = 700
+    if case == "v2_two_level_break":
+        dl[20000] = 700  # group 4 of the two-level scan
     if proto == 2:
         # header varints of one length over the whole run (offsetInBlock in
         # [2^21, 2^28), seqno in [2^14, 2^21)): every packet on one grid
@@ -649,7 +652,7 @@ def test_gpu_device_stream_many_blocks(engine, oracle, case):
     if case == "v2_seq_jump":
         kw["seqnos"] = [20000 + k + (100 if k >= 6000 else 0) for k in range(n)]
         kw["offset_skew"] = {8500: 4096}
-    corrupt = [(3, 0), (4100, 0), (6000, 0), (8999, 0)]
+    corrupt = [(3, 0), (4100, 0), (6000, 0), (8999, 0)] + ([(15000, 0), (23999, 0)] if n > 9000 else [])
     s, bad = build_stream(oracle.crc32c, proto, cs, CSUM_CRC32C, dl, seed=11, corrupt=corrupt, last_empty=False, **kw)
     keep, p = _dev(engine, s, 0)
     try:
