@@ -66,7 +66,8 @@ struct DiagEP : ReleaseEP {
   }
   // compute, one store per tile: true if a policy wrote the tile another way
   static constexpr bool kAltTileStores = true;
-  DEV static bool tile_store_alt(uint32_t pol, const SegHot &sh, SegP segs, const Cursor &c, bool keep, uint32_t nch,
+  template <class Tab>
+  DEV static bool tile_store_alt(uint32_t pol, const SegHot &sh, Tab segs, const Cursor &c, bool keep, uint32_t nch,
                                  bool leader, const LaneConst &L, uint32_t val) {
     if (pol == 3u) {
       // 128-B full-line write per tile (crcs must hold 16 B per chunk)
@@ -126,8 +127,8 @@ struct DiagEP : ReleaseEP {
   // bitmap store op with its record dropped, no CRC arithmetic.  The loaded
   // words fold into st, and an impossible condition on st keeps them live
   // (without it the compiler deletes the unused loads).
-  template <int S>
-  DEV static void load_only_round(const uint32_t (&d)[S][16], const uint32_t (&exp)[S], const Cursor (&c)[S], SegP segs,
+  template <int S, class Tab>
+  DEV static void load_only_round(const uint32_t (&d)[S][16], const uint32_t (&exp)[S], const Cursor (&c)[S], Tab segs,
                                   uint32_t (&st)[S], unsigned long long *__restrict__ mism) {
 #pragma unroll
     for (int s = 0; s < S; s++) {

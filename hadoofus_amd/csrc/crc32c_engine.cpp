@@ -88,6 +88,10 @@ uint32_t g_xcd_major = uint32_t(HDFS_KNOB("HDFS_CRC32C_XCD", 1)) & 3u;
 // (profiles/r02/exp_compute_store_schedules.json: 0 / 1 / 2 = 6377 / 6595 /
 // 6626 GB/s of algorithmic bytes in one process).
 int g_runs = HDFS_KNOB("HDFS_CRC32C_RUNS", 2);
+// Device-resident packet runs: try the speculative one-launch verify first
+// (spec_verify_kernel; 1, the product) or always frame the run (0,
+// diagnostic build only: the A/B of round 4).
+int g_spec = HDFS_KNOB("HDFS_CRC32C_SPEC", 1);
 // Small-call input stage: 1 fine-grained VRAM written through the BAR when
 // the device is large-BAR, else (and 0) pinned host memory.
 int g_stage_vram = HDFS_KNOB("HDFS_CRC32C_MB_STAGE", 1);
@@ -255,6 +259,8 @@ bool device_accessible(const void *p) {
   }
   return a.devicePointer != nullptr;
 }
+
+uint32_t tile_tune() { return (kDiag ? g_store_policy : 0u) | (g_group_shift << 8) | (g_xcd_major << 12); }
 
 int launch_verify_dyn(DevCtx &c, const SegDev *d_segs, const GridSummary *dyn, uint64_t rounds_ub, uint64_t gtiles_ub,
                       uint32_t *d_fb, unsigned long long *d_mism, uint32_t *d_gctr, hipStream_t st, int ctype,
@@ -1488,6 +1494,12 @@ int hdfs_crc32c_diag_device_checks(uint32_t *out3, int reset) {
 int hdfs_crc32c_set_store_policy(int policy) {
   if (policy < 0 || policy > 28) return fail(HDFS_CRC32C_EINVAL, "store policy 0..28");
   g_store_policy = uint32_t(policy);
+  return HDFS_CRC32C_OK;
+}
+
+int hdfs_crc32c_set_speculation(int on) {
+  if (on != 0 && on != 1) return fail(HDFS_CRC32C_EINVAL, "speculation 0 or 1");
+  g_spec = on;
   return HDFS_CRC32C_OK;
 }
 

@@ -68,6 +68,12 @@ hipError_t launch_frame_grid(const uint8_t *s, uint64_t len, uint64_t base, uint
                              int ctype, int verify, uint32_t sflags, uint8_t *bm_base, uint8_t *copy_base,
                              uint64_t copy_cap, int win, int64_t client_offset, GridBufs g, hipStream_t stream,
                              unsigned long long *stamps = nullptr);
+// Speculative one-launch verify of a run of equal packets (spec_verify_kernel;
+// crc32c_internal.h, SpecArgs): grid workgroups of 1024 threads.
+hipError_t launch_spec_verify(const SpecArgs &a, int grid, int copy, hipStream_t stream);
+// device-resident packet runs: try spec_verify_kernel first (diagnostic
+// build: hdfs_crc32c_set_speculation)
+extern int g_spec;
 // diagnostic build: per-wave / per-block s_memrealtime stamps (set_tuning)
 extern unsigned long long *g_diag;
 // frame_build_kernel's stamps sit after the tiled kernel's per-wave words
@@ -194,6 +200,15 @@ struct DevCtx {
   uint8_t *sr_h = nullptr, *sr_hd = nullptr;
   hipStream_t r_stream = nullptr;  // device framing: record copies of runs with many exceptions
   std::vector<GridSlot> grid;
+  // speculative one-launch verify (spec_verify_kernel; guarded by mu): the
+  // control-word ring [2] (zeroed when allocated), per-workgroup table
+  // copies, the pinned landing area (SpecEarly | SpecFinal) and the number of
+  // launches so far (its parity picks the ring slot)
+  SpecCtl *spec_ctl = nullptr;
+  SpecExc *spec_exc = nullptr;
+  SpecTabData *spec_tabs = nullptr;
+  uint8_t *spec_h = nullptr, *spec_hd = nullptr;
+  uint64_t spec_n = 0;
   // opt-in resident mailbox (guarded by mu): pinned request line ([0..3]
   // seq, len, chunk_size | flags, register) and status word ([16])
   bool mb_on = false, mb_alive = false;
@@ -258,6 +273,9 @@ uint32_t uniform_tiles(const SegDev *segs, size_t n);
 int launch_verify_dyn(DevCtx &c, const SegDev *d_segs, const GridSummary *dyn, uint64_t rounds_ub, uint64_t gtiles_ub,
                       uint32_t *d_fb, unsigned long long *d_mism, uint32_t *d_gctr, hipStream_t st, int ctype,
                       bool copy);
+// The tiled kernel's tune word (schedule-3 group shift, XCD dealing; the
+// diagnostic build's store policy).
+uint32_t tile_tune();
 // Any segment whose data is not 4-B aligned (selects the realigning kernel).
 bool any_unaligned(const SegDev *segs, size_t n);
 // Copy / compute streams, events and the small pipeline buffers.

@@ -128,6 +128,94 @@ struct GridBufs {
 };
 constexpr uint32_t kGridLookBytes = 256;
 
+// Speculative one-launch verify of a device-resident run of equal packets
+// (spec_verify_kernel, round 4).  Every workgroup decodes packet 0 itself;
+// if it is a canonical, framing-clean packet of whole 512-B-multiple chunks,
+// the run is the `count` packets at base + k * stride and every segment of
+// the verify is a closed-form function of k (SpecTab) -- no framing pass,
+// no segment table.  The workgroups check the headers of the run against
+// the prediction from packet 0 (byte-equal but for offsetInBlock and seqno,
+// which must continue packet 0's).  A header that differs is framed on the
+// spot: a clean packet of the same wire size (a seqno jump, a skewed
+// offset, lastPacketInBlock on the last data packet of a v1 block) is an
+// EXCEPTION -- its layout is the run's, only its record differs, and it
+// goes to the host with the results (up to kSpecExcMax; with a client read
+// window only if its offsetInBlock is the predicted one, which places its
+// copy); anything else raises `exc`, and the host discards the launch's
+// results and frames the run the regular way.  Control words live in a
+// ring of two SpecCtl slots: launch n uses slot n & 1 (zero when it starts)
+// and zeroes slot (n + 1) & 1 for the next launch, so no reset command runs
+// between launches.
+constexpr uint32_t kSpecExcMax = 64;
+struct SpecExc {
+  uint64_t rec[7];  // the packet's record (hdfs_crc32c_packet)
+  uint32_t k, pad;  // its index in the run
+};
+static_assert(sizeof(SpecExc) == 64, "SpecExc");
+struct SpecCtl {
+  unsigned long long mism;  // mismatching chunks of the run
+  uint32_t gctr;            // tiled-kernel pool counter
+  uint32_t done;            // workgroups finished
+  uint32_t exc;             // a header off the run: the launch's results are void
+  uint32_t tail_status;     // kGrid* of the point after the run (kGridOn: the run was cut, not ended)
+  uint64_t tail_total;      // its wire size when kGridStop
+  uint64_t tail[7];         // its record (hdfs_crc32c_packet) when kGridStop
+  uint32_t nexc, pad0;      // exceptions found (entries past kSpecExcMax are not kept: exc is raised)
+  uint64_t pad[20];
+};
+static_assert(sizeof(SpecCtl) == 256, "SpecCtl");
+// Pinned host area of one speculative launch: [0, 128) early block, written
+// by workgroup 0 right after its decode of packet 0 (the host fills the
+// run's records while the kernel verifies); [128, 256) final block and then
+// the exceptions (kSpecExcMax SpecExc), written by the last workgroup to
+// finish.  Sequence numbers last.
+struct SpecEarly {
+  uint64_t r0[7];           // packet 0's record (hdfs_crc32c_packet)
+  uint64_t stride;
+  uint32_t eligible;        // 0: not a run this launch takes (every workgroup returned)
+  uint32_t count;           // packets of the run
+  uint32_t seq;
+  uint32_t pad[13];
+};
+struct SpecFinal {
+  unsigned long long mism;
+  uint32_t exc, tail_status;
+  uint64_t tail_total;
+  uint64_t tail[7];
+  uint32_t seq, nexc;
+  uint32_t pad[10];
+};
+static_assert(sizeof(SpecEarly) == 128 && sizeof(SpecFinal) == 128, "spec host blocks");
+constexpr size_t kSpecHostBytes = 256 + size_t(kSpecExcMax) * sizeof(SpecExc);
+// Parameters of the closed-form segment table (SpecTab, crc32c_kernels.hip).
+struct SpecTabData {
+  const uint8_t *crc0;          // packet 0's CRCs
+  uint8_t *bm0, *copy_base;
+  uint64_t stride, copy_cap;
+  uint32_t nch, cs, cb0, pad;   // dataLen = nch * cs (whole chunks), crc_len = 4 * nch
+};
+static_assert(sizeof(SpecTabData) == 56, "SpecTabData");
+struct SpecArgs {
+  const uint8_t *s;
+  uint64_t len, base;
+  uint32_t max_count;       // grid points the pass may take (max_pkts, kGridMaxCount)
+  int proto, ctype;
+  uint32_t cs, sflags;
+  int rwin;                 // copy-out: client read window from client_offset
+  int64_t client_offset;
+  uint8_t *bm;              // bitmap area (>= count * T bytes)
+  uint8_t *copy_base;       // copy-out destination (null: none)
+  uint64_t copy_cap;        // bytes left in it for this pass
+  const uint32_t *gtab;     // slicing / zeros tables of the checksum type
+  uint32_t *fb;             // first-bad scratch (>= count words; results unused)
+  SpecCtl *ctl;             // [2] ring
+  SpecExc *exc;             // [2][kSpecExcMax] exception records, by ring slot
+  uint32_t parity, seq, tune;
+  uint8_t *hout;            // pinned host area (device address): SpecEarly, SpecFinal
+  SpecTabData *tabs;        // [gridDim.x] per-workgroup copies of the closed-form table
+};
+constexpr uint64_t kSpecMaxStride = uint64_t(1) << 26;  // per-lane header offsets within a wave fit 32 bits
+
 // Compact verify verdict of one packet (grid_finalize_kernel).
 struct GridBad {
   uint32_t pkt;

@@ -157,6 +157,62 @@ DEV SegHot seg_hot(SegP segs, uint32_t s) {
   return SegHot{p->data, p->crcs, p->bitmap, p->mtile_start, p->chunk_size, p->flags, p->nchunks, p->main_tiles};
 }
 
+// A closed-form segment table (spec_verify_kernel): segment k is packet k of
+// a run of equal packets at crc0 + k * stride -- its CRCs there, its data
+// 4 * nch bytes later, its bitmap at bm0 + k * T -- with every field a
+// function of k and packet 0's header, so no table is built or read.  The
+// tiled kernel's helpers take either this or a SegP (`segs[s].field`).
+// Copy-out: packet k delivers dataLen bytes (packet 0: dataLen - cb0, the
+// client read window's c_begin), placed after the avail of the packets
+// before it, never past copy_cap (frame::read_avail / read_place in closed
+// form).  The parameters sit in HBM (each workgroup writes its own copy
+// after decoding packet 0) and are read, like a SegDev, with scalar loads
+// through the constant address space: carried in SGPRs across the work
+// loop they pushed the kernel past the SGPR budget and into spills.
+struct SpecTab {
+  const CAS SpecTabData *p;
+  DEV SegDev operator[](uint32_t k) const {
+    SegDev d;
+    SpecTabData q;
+    q.crc0 = p->crc0;
+    q.bm0 = p->bm0;
+    q.copy_base = p->copy_base;
+    q.stride = p->stride;
+    q.copy_cap = p->copy_cap;
+    q.nch = p->nch;
+    q.cs = p->cs;
+    q.cb0 = p->cb0;
+    const uint32_t T = (q.nch + kTileChunks - 1u) / kTileChunks, dlen = q.nch * q.cs;
+    const uint8_t *c = q.crc0 + static_cast<uint64_t>(k) * q.stride;
+    d.data = c + 4u * q.nch;
+    d.crcs = reinterpret_cast<uint32_t *>(const_cast<uint8_t *>(c));
+    d.bitmap = q.bm0 + static_cast<uint64_t>(k) * T;
+    d.mtile_start = static_cast<uint64_t>(k) * T;
+    d.chunk_size = q.cs;
+    d.flags = kSegBigEndian;  // wire CRCs; the table set is the launch's
+    d.nchunks = q.nch;
+    d.main_tiles = T;
+    d.reg_init = 0xFFFFFFFFu;
+    d.gen_tiles = 0u;
+    d.len = dlen;
+    d.round_start = static_cast<uint64_t>(k) * T * (q.cs / kRoundBytes);
+    d.gtile_start = 0u;
+    const uint32_t w0 = k ? 0u : q.cb0;
+    const uint64_t before = k ? static_cast<uint64_t>(k) * dlen - q.cb0 : 0u;
+    uint64_t at = 0;
+    uint32_t clen = 0;
+    frame::read_place(before, dlen - w0, q.copy_cap, at, clen);
+    d.copy_dst = q.copy_base && clen ? q.copy_base + at : nullptr;
+    d.copy_w0 = w0;
+    d.copy_w1 = w0 + clen;
+    return d;
+  }
+};
+DEV SegHot seg_hot(const SpecTab &t, uint32_t k) {
+  const SegDev d = t[k];
+  return SegHot{d.data, d.crcs, d.bitmap, d.mtile_start, d.chunk_size, d.flags, d.nchunks, d.main_tiles};
+}
+
 // Per-stream copy of the current segment's hot fields (and reg_init), kept
 // in SGPRs across rounds: issue / process / finish / advance of a round
 // re-read the table only when the cursor's segment changed (a wave-uniform
@@ -166,7 +222,8 @@ struct SegCache {
   uint32_t reg_init;
   SegHot h;
 };
-DEV const SegCache &hot(SegCache &k, SegP segs, uint32_t s) {
+template <class Tab>
+DEV const SegCache &hot(SegCache &k, Tab segs, uint32_t s) {
   if (s != k.seg) {
     k.h = seg_hot(segs, s);
     k.reg_init = segs[s].reg_init;
@@ -316,7 +373,8 @@ DEV bool ticket_tile(const Sched &w, uint32_t t, uint64_t &g) {
 constexpr uint64_t kWalkTiles = 64;  // forward hops of up to this many tiles walk the table
 
 // Global tile g -> (segment, tile), walking forward from segment s.
-DEV Cursor locate(SegP segs, uint32_t s, uint64_t g) {
+template <class Tab>
+DEV Cursor locate(Tab segs, uint32_t s, uint64_t g) {
   while (g >= segs[s].mtile_start + segs[s].main_tiles) s++;
   return Cursor{rfl(s), rfl(static_cast<uint32_t>(g - segs[s].mtile_start)), 0u, true};
 }
@@ -326,8 +384,8 @@ DEV Cursor locate(SegP segs, uint32_t s, uint64_t g) {
 // table of thousands of packet-sized segments: a forward walk from the slice
 // to the pool cost 8x the whole kernel, tools/exp_packet_tables.py);
 // interleaved tiles jump G ahead.  Short hops walk, long ones search.
-template <int ORDER>
-DEV Cursor find_tile(const Cursor c, const SegHot &sh, SegP segs, uint32_t nseg, const Sched &w, uint64_t g) {
+template <int ORDER, class Tab>
+DEV Cursor find_tile(const Cursor c, const SegHot &sh, Tab segs, uint32_t nseg, const Sched &w, uint64_t g) {
   const uint64_t end = sh.mtile_start + sh.main_tiles;
   if (w.ut && (g < sh.mtile_start || g >= end)) return ulocate(w, g);
   if (g < sh.mtile_start || g >= end + (ORDER >= 3 ? 0u : kWalkTiles)) {
@@ -345,8 +403,8 @@ DEV Cursor find_tile(const Cursor c, const SegHot &sh, SegP segs, uint32_t nseg,
 
 // Next round owned by this wave.  An exhausted cursor keeps its last
 // position (so speculative loads stay in bounds) with valid = false.
-template <int ORDER>
-DEV Cursor advance(Cursor c, SegP segs, uint32_t nseg, const Sched &w, SegCache &kc) {
+template <int ORDER, class Tab>
+DEV Cursor advance(Cursor c, Tab segs, uint32_t nseg, const Sched &w, SegCache &kc) {
   if (!c.valid) return c;
   const SegHot &sh = hot(kc, segs, c.seg).h;
   // ORDER 7: a cursor is a whole 4-tile run, one round per 128-B column
@@ -383,7 +441,8 @@ DEV Cursor advance(Cursor c, SegP segs, uint32_t nseg, const Sched &w, SegCache 
 }
 
 // Global index of the first tile whose first round is >= r.
-DEV uint64_t tile_at_round(SegP segs, uint32_t nseg, uint64_t r, uint64_t total_tiles) {
+template <class Tab>
+DEV uint64_t tile_at_round(Tab segs, uint32_t nseg, uint64_t r, uint64_t total_tiles) {
   uint32_t lo = 0, hi = nseg;
   while (hi - lo > 1) {
     const uint32_t mid = (lo + hi) >> 1;
@@ -492,8 +551,8 @@ struct LaneOff {
 // byte read lies in a dword that also holds data of the segment, so no read
 // leaves the data's pages.  The shift rides with the round (rounds in
 // flight may belong to different segments).
-template <int MODE, int NT, int BUF, int UNA, int COL = 0, class P = EP>
-DEV void issue(uint32_t (&d)[16], uint32_t &exp, uint32_t &tl, uint32_t &sh_a, const Cursor c, SegP segs,
+template <int MODE, int NT, int BUF, int UNA, int COL = 0, class P = EP, class Tab = SegP>
+DEV void issue(uint32_t (&d)[16], uint32_t &exp, uint32_t &tl, uint32_t &sh_a, const Cursor c, Tab segs,
                uint32_t hsel, uint32_t loff, uint32_t qg, uint32_t lane, LaneOff &lo, SegCache &kc,
                uint32_t pol = 0u) {
   static_assert(!COL || (BUF && !UNA && MODE == kModeCompute), "columns: compute, buffer loads, aligned data");
@@ -590,7 +649,8 @@ constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
 // is read now -- and, on a tile's last round, the owner word of the tile's
 // slot is loaded.  Both LDS reads complete under the 64 table reads of the
 // slicing: nothing is waited on.
-DEV void lazy_pre(Gst &g, const Cursor &c, SegP segs, SegCache &kc, const LaneConst &L) {
+template <class Tab>
+DEV void lazy_pre(Gst &g, const Cursor &c, Tab segs, SegCache &kc, const LaneConst &L) {
   g.fin = 0u;
   if (g.pslot != kNoSlot && (rfl(g.old) & 15u) + 1u == g.pexpect) {
     g.fin = 1u;
@@ -625,8 +685,8 @@ DEV void lazy_flush(Gst &g, const SegHot &sh, const LaneConst &L) {
   P::group_store(L.store_policy, g.dat, rg, L.lane * 4u);
 }
 
-template <int MODE, int RUN, class P = EP>
-DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, uint32_t st, const LaneConst &L,
+template <int MODE, int RUN, class P = EP, class Tab = SegP>
+DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, Tab segs, uint32_t st, const LaneConst &L,
                 uint32_t *__restrict__ first_bad, unsigned long long *__restrict__ mism, SegCache &kc,
                 Gst &gs) {
   const SegHot &sh = hot(kc, segs, c.seg).h;
@@ -853,8 +913,8 @@ DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, SegP segs, ui
 // ends inside a packet, at most two pieces per read -- is stored byte by
 // byte.  (Tiled rounds cover whole chunks, so a window edge at the payload's
 // end never falls inside a piece.)
-template <class P = EP>
-DEV void copy_round(const uint32_t (&d)[16], const Cursor c, SegP segs, const LaneConst &L, SegCache &kc) {
+template <class P = EP, class Tab = SegP>
+DEV void copy_round(const uint32_t (&d)[16], const Cursor c, Tab segs, const LaneConst &L, SegCache &kc) {
   const SegHot &sh = hot(kc, segs, c.seg).h;
   const uint32_t cs = sh.chunk_size;
   uint8_t *dst = segs[c.seg].copy_dst;
@@ -892,9 +952,9 @@ DEV void copy_round(const uint32_t (&d)[16], const Cursor c, SegP segs, const La
 // The S slicing chains are independent and interleaved step by step, so one
 // lane keeps S table lookups in flight (latency hiding by ILP, not waves).
 
-template <int MODE, int S, int COPY, int UNA, int RUN, class P = EP>
+template <int MODE, int S, int COPY, int UNA, int RUN, class P = EP, class Tab = SegP>
 DEV void process(const uint32_t *lds, uint32_t (&d)[S][16], const uint32_t (&exp)[S], const uint32_t (&tl)[S],
-                 const uint32_t (&sh_a)[S], const Cursor (&c)[S], SegP segs, uint32_t (&st)[S], const LaneConst &L,
+                 const uint32_t (&sh_a)[S], const Cursor (&c)[S], Tab segs, uint32_t (&st)[S], const LaneConst &L,
                  uint32_t *__restrict__ first_bad, unsigned long long *__restrict__ mism, SegCache (&kc)[S],
                  Gst (&gs)[S]) {
   if constexpr (MODE == kModeLoadOnly) {  // diagnostic build only (the launcher refuses it otherwise)
@@ -1110,76 +1170,67 @@ DEV void fused_generic(const uint32_t *lds, const SegDev *__restrict__ segs, con
   }
 }
 
-// Tiled kernel.  MODE compute / verify; ORDER schedule (above); NT
-// nontemporal data loads; DEPTH register round buffers per stream (DEPTH-1
-// rounds stay in flight while one is processed); S independent tile streams
-// per wave (S x 4 KiB per round, S chains of ILP); BLOCK threads per
-// workgroup (one workgroup per CU: the LDS image takes 156 KiB).
-template <int MODE, int ORDER, int NT, int DEPTH, int S, int BLOCK, int BUF = 0, int COPY = 0, int UNA = 0,
-          int GATHER = 0>
-__global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
-    const SegDev *__restrict__ segs, uint32_t nseg, uint64_t total_rounds, uint64_t total_tiles,
-    const uint32_t *__restrict__ gtab, uint32_t *__restrict__ first_bad,
-    unsigned long long *__restrict__ mism, unsigned long long *__restrict__ diag, uint32_t tune,
-    uint32_t *__restrict__ gctr, const GridSummary *__restrict__ dyn, uint32_t utiles, uint32_t fuse) {
-  static_assert(ORDER != 0 || S == 1, "static per-wave slices serve one stream");
-  static_assert(ORDER != 7 || (MODE == kModeCompute && S == 1 && BUF && !COPY && !UNA && !GATHER), "columns shape");
-  // fused epilogue (verify with a device-built table only; uniform)
-  const bool fused = MODE == kModeVerify && dyn && fuse;
-  static_assert(DEPTH >= 2 && DEPTH <= 4 && S >= 1 && S <= 4, "shape");
-  // dyn: sizes of a segment table built on the device (frame_build_kernel),
-  // read here instead of passed by the host -- no host round trip between
-  // framing and verify
-  if (dyn) {
-    nseg = dyn->nseg;
-    total_rounds = dyn->rounds;
-    total_tiles = dyn->mtiles;
-    utiles = dyn->utiles;
-  }
-  // + ticket counter, pad, kSlots 64-bit pool slots
-  // + ticket counter, pad, kSlots 64-bit pool slots (+ GATHER: the group slots)
-  // GATHER 1: the compute gather (RUN 2); 2: the lazy gather (RUN 3)
-  static_assert(GATHER == 0 || (MODE == kModeCompute && ORDER == 3 && S == 1), "gather: compute, schedule 3");
-  __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords + 2 + 2 * kSlots + (GATHER ? kGatherWords : 0)];
-
+// LDS image of the tiled kernels (+ ticket counter, pad, kSlots 64-bit pool
+// slots, + GATHER: the group slots), filled by every thread of the
+// workgroup; no barrier (the caller's __syncthreads follows).
+// LDS image: word (P*16384 + e*64 + h*32 + l) = t_{3-(2P+h)}[e] for all 32 l.
+// Filled with 16-B stores, consecutive lanes on consecutive 16 B (no bank
+// conflicts); the source words a lane needs are loaded up front so the
+// fill costs about one L2 round trip, not one per store.
+template <int BLOCK, int GATHER>
+DEV void fill_tables(uint32_t *lds, const uint32_t *__restrict__ gtab) {
   if (threadIdx.x < 2 + 2 * kSlots) lds[kLdsWords + threadIdx.x] = 0u;
   // group slot s starts owned by group s, no tile counted
   if (GATHER && threadIdx.x < kGatherSlots) lds[kLdsWords + 2 + 2 * kSlots + threadIdx.x] = threadIdx.x << 4;
-  // LDS image: word (P*16384 + e*64 + h*32 + l) = t_{3-(2P+h)}[e] for all 32 l.
-  // Filled with 16-B stores, consecutive lanes on consecutive 16 B (no bank
-  // conflicts); the source words a lane needs are loaded up front so the
-  // fill costs about one L2 round trip, not one per store.
-  {
-    constexpr uint32_t kStores = kLdsSliceBytes / 16;
-    constexpr uint32_t kQ = (kStores + BLOCK - 1) / BLOCK;  // 16-B stores per thread
-    constexpr uint32_t kZ = (kTabZposWords / 4 + BLOCK - 1) / BLOCK;
-    uint32_t v[kQ];
+  constexpr uint32_t kStores = kLdsSliceBytes / 16;
+  constexpr uint32_t kQ = (kStores + BLOCK - 1) / BLOCK;  // 16-B stores per thread
+  constexpr uint32_t kZ = (kTabZposWords / 4 + BLOCK - 1) / BLOCK;
+  uint32_t v[kQ];
 #pragma unroll
-    for (uint32_t k = 0; k < kQ; k++) {
-      const uint32_t idx = 4u * min(k * BLOCK + threadIdx.x, kStores - 1u);
-      const uint32_t P = idx >> 14, e = (idx >> 6) & 255u, h = (idx >> 5) & 1u;
-      v[k] = gtab[(3u - (2u * P + h)) * 256u + e];
-    }
-    u32x4 z[kZ];
-#pragma unroll
-    for (uint32_t k = 0; k < kZ; k++) {
-      const uint32_t q = k * BLOCK + threadIdx.x;
-      z[k] = q < kTabZposWords / 4 ? gload16(gtab + kTabSliceWords + 4u * q) : u32x4{0u, 0u, 0u, 0u};
-    }
-#pragma unroll
-    for (uint32_t k = 0; k < kQ; k++) {
-      const uint32_t q = k * BLOCK + threadIdx.x;
-      if (kStores % BLOCK == 0 || q < kStores)
-        *reinterpret_cast<u32x4 *>(&lds[4u * q]) = u32x4{v[k], v[k], v[k], v[k]};
-    }
-#pragma unroll
-    for (uint32_t k = 0; k < kZ; k++) {
-      const uint32_t q = k * BLOCK + threadIdx.x;
-      if (q < kTabZposWords / 4) *reinterpret_cast<u32x4 *>(&lds[kLdsSliceBytes / 4 + 4u * q]) = z[k];
-    }
+  for (uint32_t k = 0; k < kQ; k++) {
+    const uint32_t idx = 4u * min(k * BLOCK + threadIdx.x, kStores - 1u);
+    const uint32_t P = idx >> 14, e = (idx >> 6) & 255u, h = (idx >> 5) & 1u;
+    v[k] = gtab[(3u - (2u * P + h)) * 256u + e];
   }
-  __syncthreads();
+  u32x4 z[kZ];
+#pragma unroll
+  for (uint32_t k = 0; k < kZ; k++) {
+    const uint32_t q = k * BLOCK + threadIdx.x;
+    z[k] = q < kTabZposWords / 4 ? gload16(gtab + kTabSliceWords + 4u * q) : u32x4{0u, 0u, 0u, 0u};
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < kQ; k++) {
+    const uint32_t q = k * BLOCK + threadIdx.x;
+    if (kStores % BLOCK == 0 || q < kStores)
+      *reinterpret_cast<u32x4 *>(&lds[4u * q]) = u32x4{v[k], v[k], v[k], v[k]};
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < kZ; k++) {
+    const uint32_t q = k * BLOCK + threadIdx.x;
+    if (q < kTabZposWords / 4) *reinterpret_cast<u32x4 *>(&lds[kLdsSliceBytes / 4 + 4u * q]) = z[k];
+  }
+}
 
+// The tiled kernels' work loop after the LDS tables are in place: schedule,
+// round pipeline, epilogue.  MODE compute / verify; ORDER schedule (above);
+// NT nontemporal data loads; DEPTH register round buffers per stream (DEPTH-1
+// rounds stay in flight while one is processed); S independent tile streams
+// per wave (S x 4 KiB per round, S chains of ILP); BLOCK threads per
+// workgroup (one workgroup per CU: the LDS image takes 156 KiB).  Tab: the
+// segment table -- a SegP in HBM (crc32c_tiles_kernel) or the closed form of
+// a run of equal packets (SpecTab, spec_verify_kernel).  segs: the table in
+// HBM for the fused generic tiles (fused only).
+template <int MODE, int ORDER, int NT, int DEPTH, int S, int BLOCK, int BUF, int COPY, int UNA, int GATHER,
+          class Tab>
+DEV void tiles_run(uint32_t *lds, const Tab sg, const SegDev *__restrict__ segs, uint32_t nseg, uint64_t total_rounds,
+                   uint64_t total_tiles, uint32_t *__restrict__ first_bad, unsigned long long *__restrict__ mism,
+                   unsigned long long *__restrict__ diag, uint32_t tune, uint32_t *__restrict__ gctr,
+                   const GridSummary *__restrict__ dyn, uint32_t utiles, bool fused) {
+  static_assert(ORDER != 0 || S == 1, "static per-wave slices serve one stream");
+  static_assert(ORDER != 7 || (MODE == kModeCompute && S == 1 && BUF && !COPY && !UNA && !GATHER), "columns shape");
+  static_assert(DEPTH >= 2 && DEPTH <= 4 && S >= 1 && S <= 4, "shape");
+  // GATHER 1: the compute gather (RUN 2); 2: the lazy gather (RUN 3)
+  static_assert(GATHER == 0 || (MODE == kModeCompute && ORDER == 3 && S == 1), "gather: compute, schedule 3");
   LaneConst L;
   // tune: [7:0] store policy (diagnostic build), [11:8] ORDER-3 group shift,
   // [13:12] ORDER-3 dealing: 0 plain, 1 XCD-major, 2 XCD-split (uniform: SGPR)
@@ -1202,7 +1253,6 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
   constexpr uint32_t wpb = BLOCK / 64;
   const uint32_t wave = rfl(blockIdx.x * wpb + (threadIdx.x >> 6));
   const uint32_t nwaves = gridDim.x * wpb;
-  const SegP sg = (SegP)(segs);
   // Diagnostic build path (diag != nullptr): per-wave start / end wall clock
   // (s_memrealtime, 100 MHz) and rounds processed; nothing is computed from it.
   if (kDiag && diag && L.lane == 0) diag[3 * wave] = __builtin_amdgcn_s_memrealtime();
@@ -1390,6 +1440,33 @@ __global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
     diag[3 * wave + 1] = __builtin_amdgcn_s_memrealtime();
     diag[3 * wave + 2] = nrounds;
   }
+}
+
+// Tiled kernel over a segment table in HBM (plans, packet pieces, device-
+// framed runs).  dyn: sizes of a segment table built on the device
+// (frame_build_kernel), read here instead of passed by the host -- no host
+// round trip between framing and verify.
+template <int MODE, int ORDER, int NT, int DEPTH, int S, int BLOCK, int BUF = 0, int COPY = 0, int UNA = 0,
+          int GATHER = 0>
+__global__ __launch_bounds__(BLOCK) void crc32c_tiles_kernel(
+    const SegDev *__restrict__ segs, uint32_t nseg, uint64_t total_rounds, uint64_t total_tiles,
+    const uint32_t *__restrict__ gtab, uint32_t *__restrict__ first_bad,
+    unsigned long long *__restrict__ mism, unsigned long long *__restrict__ diag, uint32_t tune,
+    uint32_t *__restrict__ gctr, const GridSummary *__restrict__ dyn, uint32_t utiles, uint32_t fuse) {
+  // fused epilogue (verify with a device-built table only; uniform)
+  const bool fused = MODE == kModeVerify && dyn && fuse;
+  if (dyn) {
+    nseg = dyn->nseg;
+    total_rounds = dyn->rounds;
+    total_tiles = dyn->mtiles;
+    utiles = dyn->utiles;
+  }
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords + 2 + 2 * kSlots + (GATHER ? kGatherWords : 0)];
+  fill_tables<BLOCK, GATHER>(lds, gtab);
+  __syncthreads();
+  tiles_run<MODE, ORDER, NT, DEPTH, S, BLOCK, BUF, COPY, UNA, GATHER>(lds, (SegP)(segs), segs, nseg, total_rounds,
+                                                                       total_tiles, first_bad, mism, diag, tune, gctr,
+                                                                       dyn, utiles, fused);
 }
 
 
@@ -2702,6 +2779,316 @@ __global__ __launch_bounds__(1024) void grid_finalize_kernel(const SegDev *__res
   if (nseg == 0xFFFFFFFFu) nseg = sum->nseg;  // launched before the host knows the run's size
   if (!DCHK(nseg <= bad_cap, kDkFinalize)) nseg = bad_cap;  // one segment per packet of the pass
   bad_list<1024>(segs, nseg, seg2pkt, fb, bad, bad_cap, sum, hsum2, host_cap, seq, &nb);
+}
+
+// ---------------------------------------------------------------------------
+// Speculative one-launch verify of a device-resident packet run (round 4).
+// The device framing chain (frame_build_kernel -> verify -> finalize) pays
+// ~21 + 7 us of dependent global round trips per pass before and after the
+// verify; a block transfer is a run of equal packets, so this kernel takes
+// the run's layout from packet 0 alone (every workgroup decodes it in its
+// prologue, beside the LDS table fill), verifies it through the closed-form
+// table (SpecTab), and checks the headers on the side: packet k must carry
+// packet 0's header bytes but for offsetInBlock = off0 + k * dataLen and
+// seqno = seq0 + k -- then frame_step gives it exactly the record predicted
+// from packet 0, as frame_build_kernel would.  One differing header raises
+// SpecCtl::exc and the host frames the run the regular way (the launch's
+// results are discarded; its copy-out stayed inside the destination).
+// crc32c_internal.h (SpecCtl) has the control-word ring.
+// Positions of offsetInBlock / seqno in a canonical header: v1 big-endian at
+// 4 / 12 (src/datanode.c:2363-2384); v2 little-endian sfixed64 at 7 / 16 of
+// [plen][hlen][PacketHeaderProto] in protobuf-c's field order (decode_header's
+// fast path).
+DEV bool spec_canonical(const uint8_t *w, int proto, uint32_t hl) {
+  if (proto == HDFS_CRC32C_PROTO_V1) return hl == 25u;
+  const uint32_t n = hl - 6u;
+  const uint8_t *p = w + 6;
+  return (n == 25u || n == 27u) && p[0] == 0x09 && p[9] == 0x11 && p[18] == 0x18 && p[19] < 0x80 && p[20] == 0x25 &&
+         (n == 25u || (p[25] == 0x28 && p[26] < 0x80));
+}
+
+// Header byte j (a compile-time constant after unrolling) of packet k of the
+// run: packet 0's byte b0 but inside the offsetInBlock / seqno fields.
+template <uint32_t J>
+DEV uint32_t spec_hdr_byte(uint32_t b0, bool v1, uint64_t off, uint64_t sq) {
+  uint32_t e1 = b0, e2 = b0;
+  if constexpr (J >= 4 && J < 12) e1 = static_cast<uint32_t>(off >> (8 * (11 - J))) & 0xffu;
+  if constexpr (J >= 12 && J < 20) e1 = static_cast<uint32_t>(sq >> (8 * (19 - J))) & 0xffu;
+  if constexpr (J >= 7 && J < 15) e2 = static_cast<uint32_t>(off >> (8 * (J - 7))) & 0xffu;
+  if constexpr (J >= 16 && J < 24) e2 = static_cast<uint32_t>(sq >> (8 * (J - 16))) & 0xffu;
+  return v1 ? e1 : e2;
+}
+
+template <uint32_t D>
+DEV uint32_t spec_hdr_word(const uint8_t *w0, bool v1, uint64_t off, uint64_t sq) {
+  return spec_hdr_byte<4 * D>(w0[4 * D], v1, off, sq) | (spec_hdr_byte<4 * D + 1>(w0[4 * D + 1], v1, off, sq) << 8) |
+         (spec_hdr_byte<4 * D + 2>(w0[4 * D + 2], v1, off, sq) << 16) |
+         (spec_hdr_byte<4 * D + 3>(w0[4 * D + 3], v1, off, sq) << 24);
+}
+
+// The run a speculative launch takes, decoded from packet 0 (LDS, shared by
+// the workgroup's waves).
+struct SpecRun {
+  uint32_t eligible, count, hl, crc_len, dlen, nch, T, cb0, v1;
+  uint64_t stride, off0, seq0;
+};
+
+constexpr uint32_t kSpecHdrBytes = 48;  // header bytes compared per packet (canonical headers: <= 33)
+
+template <int COPY>
+__global__ __launch_bounds__(1024) void spec_verify_kernel(SpecArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords + 2 + 2 * kSlots];
+  __shared__ __attribute__((aligned(16))) uint8_t win[2][kHdrWin];  // packet 0, the point after the run
+  __shared__ SpecRun run;
+  // what the epilogue needs, parked in LDS: kept in SGPRs across the work
+  // loop they pushed it past the SGPR budget (spills)
+  __shared__ SpecCtl *ep_ctl;
+  __shared__ SpecExc *ep_exc;
+  __shared__ uint8_t *ep_hout;
+  __shared__ uint32_t ep_seq;
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  if (t == 0) {
+    ep_ctl = a.ctl + a.parity;
+    ep_exc = a.exc + a.parity * kSpecExcMax;
+    ep_hout = a.hout;
+    ep_seq = a.seq;
+  }
+  SpecCtl *const ctl = a.ctl + a.parity;
+  const uint64_t rem = a.len > a.base ? a.len - a.base : 0u;
+  if (wv == 0) {
+    // packet 0's first kHdrWin bytes (zeros past the stream) -> win[0]
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t *>(a.s + (rem ? a.base : 0u)), 0, static_cast<int>(rem < kHdrWin ? rem : kHdrWin),
+        0x00020000);
+    if (lane < kHdrWin / 16)
+      *reinterpret_cast<u32x4 *>(&win[0][16 * lane]) =
+          __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 16u * lane, 0, 0));
+  }
+  fill_tables<1024, 0>(lds, a.gtab);
+  if (wv == 0 && lane == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");  // the window's LDS stores, this wave's own
+    SpecRun d{};
+    hdfs_crc32c_packet r{};
+    uint64_t total = 0;
+    const uint32_t hl = a.proto == HDFS_CRC32C_PROTO_V2 ? 6u + ((uint32_t(win[0][4]) << 8) | win[0][5]) : 25u;
+    const bool fits = rem >= 6u && hl <= kHdrWin;
+    const int st = fits ? frame::frame_step(win[0], rem, a.base, a.proto, a.cs, a.ctype, r, total) : frame::kStepMore;
+    uint32_t cb0 = 0;
+    const uint32_t avail0 = st == frame::kStepNext ? frame::read_avail(r, a.rwin != 0, a.client_offset, cb0) : 0u;
+    bool ok = st == frame::kStepNext && !r.error && !r.last && r.crc_len > 0 && r.data_len > 0 &&
+              a.cs % kRoundBytes == 0 && uint32_t(r.data_len) % a.cs == 0 && total < kSpecMaxStride &&
+              spec_canonical(win[0], a.proto, hl) && avail0 > 0u;
+    uint32_t count = 0;
+    if (ok) {
+      const uint64_t by_len = rem / total;
+      uint64_t cnt = min<uint64_t>(by_len, a.max_count);
+      // a client read takes the packets up to the one that completes it
+      if (a.rwin && a.copy_cap > avail0)
+        cnt = min<uint64_t>(cnt, 1u + (a.copy_cap - avail0 + uint64_t(r.data_len) - 1u) / uint64_t(r.data_len));
+      else if (a.rwin)
+        cnt = 1u;
+      count = static_cast<uint32_t>(cnt);
+      ok = count >= 2u;
+      d.stride = total;
+      d.hl = r.header_len;
+      d.crc_len = uint32_t(r.crc_len);
+      d.dlen = uint32_t(r.data_len);
+      d.nch = uint32_t(r.crc_len) / 4u;
+      d.T = (d.nch + kTileChunks - 1u) / kTileChunks;
+      d.cb0 = cb0;
+      d.v1 = a.proto == HDFS_CRC32C_PROTO_V1 ? 1u : 0u;
+      d.off0 = uint64_t(r.offset_in_block);
+      d.seq0 = uint64_t(r.seqno);
+      if (ok && blockIdx.x == 0) {
+        // the point after the run: where the walk goes on, or what ends it
+        uint32_t ts = kGridOn;
+        uint64_t ttot = 0;
+        hdfs_crc32c_packet tr{};
+        // (the caller's record array holds count + 1 records only when the
+        // pass was not cut at max_count)
+        if (count == by_len && count < a.max_count) {  // the run ends with the stream's whole strides
+          const uint64_t pt = a.base + uint64_t(count) * total;
+          if (pt >= a.len) {
+            ts = kGridMore;
+          } else {
+            stage_header(a.s, a.len, pt, 0u, win[1]);
+            const int tst = grid_frame(a.s, a.len, pt, win[1], a.proto, a.cs, a.ctype, tr, ttot);
+            ts = tst == frame::kStepMore ? kGridMore : tst == frame::kStepStop ? kGridStop : kGridOff;
+          }
+        }
+        const uint64_t *x = reinterpret_cast<const uint64_t *>(&tr);
+#pragma unroll
+        for (int q = 0; q < 7; q++) at_st(&ctl->tail[q], x[q]);
+        at_st(&ctl->tail_total, ttot);
+        at_st32(&ctl->tail_status, ts);
+        stores_done();
+      }
+    }
+    d.eligible = ok ? 1u : 0u;
+    d.count = count;
+    run = d;
+    if (blockIdx.x == 0) {
+      // the next launch's control slot starts at zero (this launch's was
+      // zeroed by the one before)
+      SpecCtl *nx = a.ctl + (a.parity ^ 1u);
+      nx->mism = 0ull;
+      nx->gctr = 0u;
+      nx->done = 0u;
+      nx->exc = 0u;
+      nx->nexc = 0u;
+      // early block: the host fills the run's records while it verifies
+      auto *e = reinterpret_cast<SpecEarly *>(a.hout);
+      const uint64_t *x = reinterpret_cast<const uint64_t *>(&r);
+#pragma unroll
+      for (int q = 0; q < 7; q++) e->r0[q] = x[q];
+      e->stride = total;
+      e->eligible = d.eligible;
+      e->count = count;
+      __threadfence_system();
+      __hip_atomic_store(&e->seq, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  __syncthreads();
+  // uniform: readfirstlane'd into SGPRs (read from LDS, the compiler would
+  // keep them in VGPRs and build every descriptor of the loop from them)
+  SpecRun d;
+  d.eligible = rfl(run.eligible);
+  d.count = rfl(run.count);
+  d.hl = rfl(run.hl);
+  d.crc_len = rfl(run.crc_len);
+  d.dlen = rfl(run.dlen);
+  d.nch = rfl(run.nch);
+  d.T = rfl(run.T);
+  d.cb0 = rfl(run.cb0);
+  d.v1 = rfl(run.v1);
+  d.stride = rfl64(run.stride);
+  d.off0 = rfl64(run.off0);
+  d.seq0 = rfl64(run.seq0);
+  if (!d.eligible) return;
+  const bool v1 = d.v1 != 0u;
+  // header checks: runs of 64 packets, run j on wave (j / G) % 16 of
+  // workgroup j % G; lane l compares packet 64 j + l (packet 0 is the
+  // prediction itself)
+  {
+    const uint32_t G = gridDim.x;
+    for (uint32_t j = wv * G + blockIdx.x; 64u * j < d.count; j += 16u * G) {
+      const uint64_t p0 = a.base + uint64_t(64u * j) * d.stride;
+      const uint64_t span = a.len - p0;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          reinterpret_cast<uint8_t *>(rfl64(reinterpret_cast<uint64_t>(a.s + p0))), 0,
+          static_cast<int>(rfl(span > 0xFFFFFFFFull ? 0xFFFFFFFFu : static_cast<uint32_t>(span))), 0x00020000);
+      const uint32_t k = 64u * j + lane;
+      const uint32_t vo = lane * static_cast<uint32_t>(d.stride);
+      u32x4 h[kSpecHdrBytes / 16];
+#pragma unroll
+      for (int q = 0; q < int(kSpecHdrBytes / 16); q++)
+        h[q] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 16u * q, 0, 0));
+      const uint64_t off = d.off0 + uint64_t(k) * d.dlen, sq = d.seq0 + k;
+      uint32_t e[kSpecHdrBytes / 4];
+      e[0] = spec_hdr_word<0>(win[0], v1, off, sq);
+      e[1] = spec_hdr_word<1>(win[0], v1, off, sq);
+      e[2] = spec_hdr_word<2>(win[0], v1, off, sq);
+      e[3] = spec_hdr_word<3>(win[0], v1, off, sq);
+      e[4] = spec_hdr_word<4>(win[0], v1, off, sq);
+      e[5] = spec_hdr_word<5>(win[0], v1, off, sq);
+      e[6] = spec_hdr_word<6>(win[0], v1, off, sq);
+      e[7] = spec_hdr_word<7>(win[0], v1, off, sq);
+      e[8] = spec_hdr_word<8>(win[0], v1, off, sq);
+      e[9] = spec_hdr_word<9>(win[0], v1, off, sq);
+      e[10] = spec_hdr_word<10>(win[0], v1, off, sq);
+      e[11] = spec_hdr_word<11>(win[0], v1, off, sq);
+      uint32_t diff = 0;
+#pragma unroll
+      for (uint32_t w = 0; w < kSpecHdrBytes / 4; w++) {
+        // bytes of the header only (hl <= 33)
+        const uint32_t m = 4u * w >= d.hl ? 0u : 4u * w + 4u <= d.hl ? 0xFFFFFFFFu : (1u << (8u * (d.hl - 4u * w))) - 1u;
+        diff |= (h[w / 4][w % 4] ^ e[w]) & m;
+      }
+      if (k < d.count && diff != 0u) {
+        // rare: frame the packet as frame_build_kernel would.  Same wire
+        // size and clean: an exception (the run's layout, its own record);
+        // anything else voids the launch
+        hdfs_crc32c_packet r{};
+        uint64_t tot = 0;
+        const uint64_t pos = p0 + vo;
+        const int st = frame::frame_step(a.s + pos, a.len - pos, pos, a.proto, a.cs, a.ctype, r, tot);
+        bool keep = st == frame::kStepNext && !r.error && tot == d.stride &&
+                    (!a.rwin || static_cast<uint64_t>(r.offset_in_block) == off);
+        if (keep) {
+          const uint32_t slot = __hip_atomic_fetch_add(&ctl->nexc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (slot < kSpecExcMax) {
+            SpecExc *x = a.exc + a.parity * kSpecExcMax + slot;
+            const uint64_t *w = reinterpret_cast<const uint64_t *>(&r);
+#pragma unroll
+            for (int q = 0; q < 7; q++) at_st(&x->rec[q], w[q]);
+            at_st32(&x->k, k);
+          } else {
+            keep = false;
+          }
+        }
+        if (!keep) __hip_atomic_fetch_or(&ctl->exc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+  // this workgroup's copy of the closed-form table (read back with scalar
+  // loads: written with vector stores, acknowledged before the barrier)
+  if (t == 0) {
+    SpecTabData *q = a.tabs + blockIdx.x;
+    q->crc0 = a.s + a.base + d.hl;
+    q->bm0 = a.bm;
+    q->copy_base = COPY ? a.copy_base : nullptr;
+    q->stride = d.stride;
+    q->copy_cap = COPY ? a.copy_cap : 0u;
+    q->nch = d.nch;
+    q->cs = a.cs;
+    q->cb0 = COPY ? d.cb0 : 0u;
+    q->pad = 0u;
+    stores_done();
+  }
+  __syncthreads();
+  const SpecTab tab{(const CAS SpecTabData *)(a.tabs + blockIdx.x)};
+  const uint64_t tiles = uint64_t(d.count) * d.T;
+  tiles_run<kModeVerify, 3, 1, 3, 1, 1024, 1, COPY, 1, 0>(lds, tab, nullptr, d.count, tiles * (a.cs / kRoundBytes),
+                                                          tiles, a.fb, &ctl->mism, nullptr, a.tune, &ctl->gctr,
+                                                          nullptr, d.T, false);
+  // every wave's stores and atomics (mismatch count, exception flag) are
+  // acknowledged before its workgroup counts itself done; the last
+  // workgroup then reads the counters and publishes the final block
+  stores_done();
+  __syncthreads();
+  if (t == 0) {
+    SpecCtl *const c = ep_ctl;
+    const uint32_t n = __hip_atomic_fetch_add(&c->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (n == gridDim.x - 1u) {
+      auto *f = reinterpret_cast<SpecFinal *>(ep_hout + sizeof(SpecEarly));
+      f->mism = at_ld(reinterpret_cast<const uint64_t *>(&c->mism));
+      f->exc = static_cast<uint32_t>(__hip_atomic_load(&c->exc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      f->tail_status =
+          static_cast<uint32_t>(__hip_atomic_load(&c->tail_status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      f->tail_total = at_ld(&c->tail_total);
+#pragma unroll
+      for (int q = 0; q < 7; q++) f->tail[q] = at_ld(&c->tail[q]);
+      const uint32_t nexc =
+          static_cast<uint32_t>(__hip_atomic_load(&c->nexc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      f->nexc = nexc;
+      const SpecExc *x = ep_exc;
+      SpecExc *hx = reinterpret_cast<SpecExc *>(ep_hout + 256);
+      for (uint32_t j = 0; j < min(nexc, kSpecExcMax); j++) {
+#pragma unroll
+        for (int q = 0; q < 7; q++) hx[j].rec[q] = at_ld(&x[j].rec[q]);
+        hx[j].k = static_cast<uint32_t>(__hip_atomic_load(&x[j].k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      }
+      __threadfence_system();
+      __hip_atomic_store(&f->seq, ep_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+hipError_t launch_spec_verify(const SpecArgs &a, int grid, int copy, hipStream_t stream) {
+  if (grid < 1 || !a.seq || !a.ctl || !a.exc || !a.hout || !a.tabs || a.parity > 1u) return hipErrorInvalidValue;
+  if (copy) hipLaunchKernelGGL(spec_verify_kernel<1>, dim3(grid), dim3(1024), 0, stream, a);
+  else hipLaunchKernelGGL(spec_verify_kernel<0>, dim3(grid), dim3(1024), 0, stream, a);
+  return hipGetLastError();
 }
 
 // Short device-resident runs in one launch (the per-read case of a

@@ -664,6 +664,190 @@ int small_run(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
   return 1;
 }
 
+// ---- speculative one-launch verify (spec_verify_kernel) ----
+// A run of equal packets (a block transfer) verified in ONE launch that
+// takes the run's layout from packet 0 and checks the other headers on the
+// side (crc32c_internal.h, SpecCtl); the host fills the records from packet
+// 0 while the kernel runs.  Not taken (the caller frames the run the regular
+// way from the same offset) when packet 0 does not start such a run or a
+// header differs from the prediction.
+struct SpecResult {
+  bool taken = false;     // verified by the speculative launch
+  bool end = false;       // the walk ends with this pass
+  uint32_t recorded = 0;  // records written to dst
+  uint64_t payload = 0;   // bytes the recorded packets deliver (frame::read_avail)
+  uint64_t consumed = 0, next = 0;
+};
+
+// diagnostic build: {launches, eligible, taken, header exceptions}
+// (hdfs_crc32c_diag_spec_stats)
+uint64_t g_spec_stats[4] = {0, 0, 0, 0};
+
+int spec_alloc(DevCtx &c) {
+  if (c.spec_ctl) return HDFS_CRC32C_OK;
+  SpecCtl *ctl = nullptr;
+  SpecExc *exc = nullptr;
+  SpecTabData *tabs = nullptr;
+  uint8_t *h = nullptr, *hd = nullptr;
+  hipError_t e = hipMalloc(&ctl, 2 * sizeof(SpecCtl));
+  if (e == hipSuccess) e = hipMemset(ctl, 0, 2 * sizeof(SpecCtl));  // the ring starts at zero
+  if (e == hipSuccess) e = hipMalloc(&exc, 2 * kSpecExcMax * sizeof(SpecExc));
+  if (e == hipSuccess) e = hipMalloc(&tabs, size_t(std::max(c.num_cu, 1)) * sizeof(SpecTabData));
+  if (e == hipSuccess) e = hipHostMalloc(&h, kSpecHostBytes, hipHostMallocCoherent | hipHostMallocMapped);
+  if (e == hipSuccess) {
+    std::memset(h, 0, kSpecHostBytes);
+    e = hipHostGetDevicePointer(reinterpret_cast<void **>(&hd), h, 0);
+  }
+  if (e != hipSuccess) {
+    if (ctl) (void)hipFree(ctl);
+    if (exc) (void)hipFree(exc);
+    if (tabs) (void)hipFree(tabs);
+    if (h) (void)hipHostFree(h);
+    return fail(HDFS_CRC32C_EHIP, "speculative verify buffers: %s", hipGetErrorString(e));
+  }
+  c.spec_exc = exc;
+  c.spec_tabs = tabs;
+  c.spec_h = h;
+  c.spec_hd = hd;
+  c.spec_n = 0;
+  c.spec_ctl = ctl;
+  return HDFS_CRC32C_OK;
+}
+
+// Wait for a sequence number a kernel publishes to pinned memory as its last
+// memory operation; after 200 ms the stream synchronisation reports a fault.
+int poll_seq(DevCtx &c, const uint32_t *word, uint32_t seq, const char *what) {
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
+  for (uint32_t spin = 1; __atomic_load_n(word, __ATOMIC_ACQUIRE) != seq; spin++) {
+    if ((spin & 4095u) == 0 && clk::now() - t0 > std::chrono::milliseconds(200)) {
+      HIPCHK(hipStreamSynchronize(c.stream));
+      if (__atomic_load_n(word, __ATOMIC_ACQUIRE) != seq) return fail(HDFS_CRC32C_EHIP, "%s: no completion word", what);
+      break;
+    }
+#if defined(__x86_64__) || defined(__i386__)
+    __builtin_ia32_pause();
+#endif
+  }
+  return HDFS_CRC32C_OK;
+}
+
+int spec_pass(DevCtx &c, const uint8_t *d, uint64_t len, uint64_t pos, uint32_t max_count, int proto, uint32_t cs,
+              int ctype, const CopyOut &co, uint64_t done_b, uint8_t *bm, uint32_t *fb, hdfs_crc32c_packet *dst,
+              SpecResult &res) {
+  res = SpecResult{};
+  int rc = spec_alloc(c);
+  if (rc) return rc;
+  const uint64_t left = len - pos;
+  const uint64_t want = (left / kRoundBytes + 63) / 64;  // >= 4 rounds per wave (launch_verify_dyn)
+  const int grid = int(std::max<uint64_t>(1, std::min<uint64_t>(want, uint64_t(c.bulk_cus()))));
+  const uint32_t seq = next_grid_seq(c);
+  auto *early = reinterpret_cast<SpecEarly *>(c.spec_h);
+  auto *fin = reinterpret_cast<SpecFinal *>(c.spec_h + sizeof(SpecEarly));
+  __atomic_store_n(&early->seq, 0u, __ATOMIC_RELEASE);
+  __atomic_store_n(&fin->seq, 0u, __ATOMIC_RELEASE);
+  SpecArgs a{};
+  a.s = d;
+  a.len = len;
+  a.base = pos;
+  a.max_count = max_count;
+  a.proto = proto;
+  a.ctype = ctype;
+  a.cs = cs;
+  a.sflags = HDFS_CRC32C_SEG_BE | (ctype == HDFS_CRC32C_CSUM_CRC32 ? HDFS_CRC32C_SEG_CRC32 : 0u);
+  a.rwin = co.win ? 1 : 0;
+  a.client_offset = co.client_offset;
+  a.bm = bm;
+  a.copy_base = co.dst ? co.dst + done_b : nullptr;
+  a.copy_cap = co.dst ? co.cap - done_b : 0u;
+  a.gtab = c.d_tab_main_t[ctype == HDFS_CRC32C_CSUM_CRC32 ? 1 : 0];
+  a.fb = fb;
+  a.ctl = c.spec_ctl;
+  a.exc = c.spec_exc;
+  a.parity = uint32_t(c.spec_n & 1u);
+  a.seq = seq;
+  a.tune = tile_tune();
+  a.hout = c.spec_hd;
+  a.tabs = c.spec_tabs;
+  HIPCHK(launch_spec_verify(a, grid, co.dst ? 1 : 0, c.stream));
+  c.spec_n++;
+  if (kDiag) g_spec_stats[0]++;
+  if ((rc = poll_seq(c, &early->seq, seq, "speculative verify"))) return rc;
+  SpecEarly E;
+  std::memcpy(&E, early, sizeof(E));
+  if (!E.eligible) return HDFS_CRC32C_OK;  // every workgroup has returned; the regular pass queues behind them
+  if (kDiag) g_spec_stats[1]++;
+  hdfs_crc32c_packet r0;
+  std::memcpy(&r0, E.r0, sizeof(r0));
+  // the run's records while the kernel verifies it
+  for (uint32_t k = 0; k < E.count; k++) {
+    hdfs_crc32c_packet &r = dst[k];
+    r = r0;
+    r.stream_off = pos + uint64_t(k) * E.stride;
+    r.offset_in_block = r0.offset_in_block + int64_t(k) * r0.data_len;
+    r.seqno = r0.seqno + int64_t(k);
+  }
+  if ((rc = poll_seq(c, &fin->seq, seq, "speculative verify"))) return rc;
+  SpecFinal F;
+  std::memcpy(&F, fin, sizeof(F));
+  if (F.exc) {  // a header off the prediction: frame the run instead
+    if (kDiag) g_spec_stats[3]++;
+    return HDFS_CRC32C_OK;
+  }
+  res.taken = true;
+  if (kDiag) g_spec_stats[2]++;
+  // same-size packets whose headers left the prediction: their own records
+  const auto *hx = reinterpret_cast<const SpecExc *>(c.spec_h + 256);
+  for (uint32_t j = 0; j < F.nexc; j++) {  // (more than kSpecExcMax raised exc)
+    SpecExc x;
+    std::memcpy(&x, hx + j, sizeof(x));
+    if (x.k >= E.count) return fail(HDFS_CRC32C_EHIP, "speculative verify: exception record %u of %u", x.k, E.count);
+    std::memcpy(&dst[x.k], x.rec, sizeof(hdfs_crc32c_packet));
+  }
+  if (F.mism) {
+    // packets with bad chunks: first bad chunk and count from the bitmap
+    // (rare; the kernel's results are complete once the copy, queued
+    // behind it, has run)
+    const uint32_t nch = uint32_t(r0.crc_len) / 4u, nb = (nch + 7u) / 8u;
+    std::vector<uint8_t> bmh(size_t(E.count) * nb);
+    HIPCHK(hipMemcpyAsync(bmh.data(), bm, bmh.size(), hipMemcpyDeviceToHost, c.stream));
+    HIPCHK(hipStreamSynchronize(c.stream));
+    for (uint32_t k = 0; k < E.count; k++) {
+      const uint8_t *b = bmh.data() + size_t(k) * nb;
+      uint32_t bad = 0;
+      int32_t first = -1;
+      for (uint32_t j = 0; j < nb; j++) {
+        uint32_t byte = b[j];
+        if (j == nch / 8u) byte &= (1u << (nch % 8u)) - 1u;  // bits past the last chunk
+        if (!byte) continue;
+        if (first < 0) first = int32_t(8u * j + uint32_t(__builtin_ctz(byte)));
+        bad += uint32_t(__builtin_popcount(byte));
+      }
+      if (bad) {
+        dst[k].error = HDFS_CRC32C_ERR_DATANODE_BAD_CHECKSUM;
+        dst[k].first_bad = first;
+        dst[k].bad_chunks = bad;
+      }
+    }
+  }
+  uint32_t cb0 = 0;
+  const uint64_t avail0 = frame::read_avail(r0, co.win, co.client_offset, cb0);
+  res.payload = uint64_t(E.count - 1u) * uint64_t(r0.data_len) + avail0;
+  const uint64_t run_end = pos + uint64_t(E.count) * E.stride;
+  res.recorded = E.count;
+  res.consumed = res.next = run_end;
+  if (F.tail_status == kGridStop) {  // the empty last packet or a framing error ends the walk
+    hdfs_crc32c_packet &t = dst[E.count];
+    std::memcpy(&t, F.tail, sizeof(t));
+    if (!t.error) res.consumed = run_end + F.tail_total;
+    res.recorded++;
+    res.end = true;
+  } else if (F.tail_status == kGridMore) {  // the stream ends inside the next packet
+    res.end = true;
+  }  // kGridOff (another size) / kGridOn (the pass was cut): the walk goes on at run_end
+  return HDFS_CRC32C_OK;
+}
+
 int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs, int ctype, size_t max_pkts,
               bool verify, const CopyOut &co, hdfs_crc32c_packet *dst, size_t *nout, uint64_t *consumed,
               uint64_t *payload_out) {
@@ -698,6 +882,11 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
   size_t n = 0;  // records in dst
   int rc = HDFS_CRC32C_OK;
   bool fallback = false;
+  // speculation: tried at each pass of a large enough stream until a launch
+  // meets a header off its prediction (an irregular stream: later passes
+  // frame); last_spec = the call's last command was a taken speculative
+  // launch, whose completion word the host has seen
+  bool try_spec = verify && g_spec, last_spec = false;
   using clk = std::chrono::steady_clock;
   const auto t0 = clk::now();
   double t_enq = 0, t_sync = 0, t_fill = 0;
@@ -736,6 +925,30 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
     // copy-out: this pass fills the destination from what earlier passes
     // delivered on, within what is left of it
     const uint64_t done_b = std::min(payload, co.cap);
+    if (try_spec && left > kSmallRunBytes) {
+      SpecResult sr;
+      if ((rc = spec_pass(c, d, len, pos, count, proto, cs, ctype, co, done_b, dg + L.bm,
+                          reinterpret_cast<uint32_t *>(dg + L.fb), dst + n, sr)))
+        break;
+      if (sr.taken) {
+        if (co.dst && !co.win && payload + sr.payload > co.cap) {
+          rc = fail(HDFS_CRC32C_EINVAL, "copy-out buffer of %llu bytes is too small (%llu needed so far)",
+                    (unsigned long long)co.cap, (unsigned long long)(payload + sr.payload));
+          break;
+        }
+        n += sr.recorded;
+        payload += sr.payload;
+        *consumed = sr.consumed;
+        last_spec = true;
+        if (sr.end) break;
+        pos = sr.next;
+        continue;
+      }
+      // not taken: the regular pass from the same offset (an irregular run
+      // gets no further speculative launches in this call)
+      try_spec = false;
+    }
+    last_spec = false;
     hipError_t e = launch_frame_grid(d, len, pos, count, proto, cs, ctype, verify ? 1 : 0, sflags, dg + L.bm,
                                      co.dst ? co.dst + done_b : nullptr, co.dst ? co.cap - done_b : 0, co.win ? 1 : 0,
                                      co.client_offset, gb, c.stream,
@@ -846,8 +1059,8 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
   // runtime's completion bookkeeping (HDFS_CRC32C_DSTREAM_TRACE) -- is
   // skipped; otherwise (an error, a poll timeout) it drains the stream and
   // reports the fault.
-  bool all_done = false;
-  if (!rc && !fallback && !passes.empty()) {
+  bool all_done = !rc && !fallback && last_spec;
+  if (!rc && !fallback && !last_spec && !passes.empty()) {
     if (!verify) {
       all_done = true;
     } else {
@@ -1362,6 +1575,17 @@ int hdfs_crc32c_verify_packets_copy(const void *stream, uint64_t len, int proto,
   return verify_packets_dev_impl(dev, static_cast<const uint8_t *>(stream), len, proto, chunk_size, ctype, pkts,
                                  max_pkts, npkts, consumed, true, co, delivered);
 }
+
+#ifdef HDFS_CRC32C_DIAG
+int hdfs_crc32c_diag_spec_stats(uint64_t *out4, int reset) {
+  if (!out4) return fail(HDFS_CRC32C_EINVAL, "null out4");
+  for (int i = 0; i < 4; i++) {
+    out4[i] = g_spec_stats[i];
+    if (reset) g_spec_stats[i] = 0;
+  }
+  return HDFS_CRC32C_OK;
+}
+#endif
 
 int hdfs_crc32c_compose_packets(const void *data, uint64_t len, int64_t offset_in_block, int64_t seqno, int proto,
                                 int ctype, int finish, void *hdr_out, uint64_t hdr_cap, hdfs_crc32c_out_packet *pkts,

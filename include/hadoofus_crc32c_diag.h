@@ -75,6 +75,15 @@ int hdfs_crc32c_set_store_policy(int policy);
  * after its last tile).
  * Env HDFS_CRC32C_RUNS. */
 int hdfs_crc32c_set_runs(int on);
+/* Device-resident packet runs (hdfs_crc32c_verify_packets and the copy-out
+ * entry): 1 (default, the product) tries the speculative one-launch verify
+ * of a run of equal packets first, 0 always frames the run on the device
+ * first (the round-3 path) -- for same-process A/Bs.  Env HDFS_CRC32C_SPEC. */
+int hdfs_crc32c_set_speculation(int on);
+/* Speculative one-launch verifies since the last reset: out4 = {launches,
+ * eligible (packet 0 starts a run of equal packets), taken (no header off
+ * the prediction), header exceptions}; reset != 0 clears them. */
+int hdfs_crc32c_diag_spec_stats(uint64_t *out4, int reset);
 /* Device checks: the framing kernels (frame_build, header_window, small_run,
  * grid_finalize) test, in this build, the invariants
  * behind each address they touch (a record slot inside its pass, a packet's bytes inside
