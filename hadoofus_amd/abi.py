@@ -26,7 +26,9 @@ ERR_UNEXPECTED_CRC_LEN = 27
 ERR_UNEXPECTED_READ_OFFSET = 28
 ERR_BAD_CHECKSUM = 29
 ERR_BAD_LASTPACKET = 32
-READ_ALL = -1  # verify_packets_copy: whole payloads, no client read window
+READ_ALL = -1  # read_packets: whole payloads, no client read window
+AGAIN = 1000   # read_packets: the destination filled before the read completed (resumable)
+ABI_VERSION = 4  # include/hadoofus_crc32c.h HDFS_CRC32C_ABI_VERSION these bindings are written for
 MODE_COMPUTE, MODE_VERIFY = 0, 1
 PROTO_V1, PROTO_V2 = 1, 2
 SEG_BE, SEG_RAW, SEG_CRC32 = 1, 2, 4
@@ -52,6 +54,11 @@ class Segment(ctypes.Structure):
         ("crcs", _vp),
         ("bitmap", _vp),
     ]
+
+
+class IoVec(ctypes.Structure):
+    """hdfs_crc32c_iovec: one device buffer of a read's destination."""
+    _fields_ = [("base", ctypes.c_void_p), ("len", ctypes.c_uint64)]
 
 
 class Packet(ctypes.Structure):
@@ -128,9 +135,10 @@ def bind_product(lib):
     for name in ("hdfs_crc32c_parse_packets", "hdfs_crc32c_verify_packets"):
         _bind(lib, name, _int, [_vp, _u64, _int, _u32, _int, ctypes.POINTER(Packet), _sz,
                                 ctypes.POINTER(_sz), ctypes.POINTER(_u64)])
-    _bind(lib, "hdfs_crc32c_verify_packets_copy", _int,
-          [_vp, _u64, _int, _u32, _int, ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(Packet), _sz,
-           ctypes.POINTER(_sz), ctypes.POINTER(_u64), _vp, _u64, ctypes.POINTER(_u64)])
+    _bind(lib, "hdfs_crc32c_read_packets", _int,
+          [_vp, _u64, _int, _u32, _int, ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(IoVec), _int,
+           ctypes.POINTER(Packet), _sz, ctypes.POINTER(_sz), ctypes.POINTER(_u64), ctypes.POINTER(_u64)])
+    _bind(lib, "hdfs_crc32c_abi_version", _int, [])
     _bind(lib, "hdfs_crc32c_session_create", _int, [ctypes.POINTER(_vp), _int, _u32, _int, _u64, _sz])
     _bind(lib, "hdfs_crc32c_session_buffer", _int, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_u64)])
     _bind(lib, "hdfs_crc32c_session_commit", _int, [_vp, _u64])
@@ -160,7 +168,7 @@ def bind_product(lib):
           [_vp, _u64, _u32, _u32, _u32, _vp, _vp, _u64, ctypes.POINTER(_u64), ctypes.POINTER(_u64)])
     _bind(lib, "hdfs_crc32c_host_alloc", _int, [ctypes.POINTER(_vp), _u64])
     _bind(lib, "hdfs_crc32c_host_free", _int, [_vp])
-    return lib
+    return check_abi(lib)
 
 
 def bind_diag(lib):
@@ -191,6 +199,15 @@ def load(path=LIB_PATH):
                           "(or __graft_entry__.build())")
     _lib = bind_product(ctypes.CDLL(path))
     return _lib
+
+
+def check_abi(lib):
+    """The library's ABI version is the one these bindings were written for
+    (a ctypes prototype cannot detect a changed signature by itself)."""
+    v = lib.hdfs_crc32c_abi_version()
+    if v != ABI_VERSION:
+        raise ImportError(f"library ABI version {v}, bindings written for {ABI_VERSION}")
+    return lib
 
 
 def _check(rc, lib=None):
@@ -374,21 +391,26 @@ def verify_packets(stream, proto=PROTO_V2, chunk_size=512, ctype=CSUM_CRC32C, ma
     return _packets("hdfs_crc32c_verify_packets", stream, proto, chunk_size, ctype, max_pkts, dptr, nbytes, lib)
 
 
-def verify_packets_copy(dptr, nbytes, dst, dst_cap, proto=PROTO_V2, chunk_size=512, ctype=CSUM_CRC32C,
-                        max_pkts=None, client_offset=0, read_len=READ_ALL, lib=None):
-    """Verify + copy-out of a device-resident stream (dptr, nbytes) into the
-    device buffer dst (dst_cap bytes): the payloads de-framed in stream order
-    (read_len READ_ALL), or the block bytes [client_offset, client_offset +
-    read_len) of a client read (src/datanode.c:2478-2549).
+def read_packets(dptr, nbytes, dst, dst_cap, proto=PROTO_V2, chunk_size=512, ctype=CSUM_CRC32C,
+                 max_pkts=None, client_offset=0, read_len=READ_ALL, lib=None, iov=None):
+    """hdfs_crc32c_read_packets: verify + copy-out of a device-resident stream
+    (dptr, nbytes) into the device buffer dst (dst_cap bytes) -- or into the
+    scatter list iov = [(ptr, len), ...] -- the payloads de-framed in stream
+    order (read_len READ_ALL), or the block bytes [client_offset,
+    client_offset + read_len) of a client read (src/datanode.c:2478-2549).
+    rc AGAIN: the destination filled first; resume at stream + consumed,
+    client_offset + delivered, read_len - delivered.
     -> (rc, [packet dicts], consumed, delivered)."""
     if max_pkts is None:
         max_pkts = nbytes // (25 if proto == PROTO_V1 else 6) + 1
     arr = (Packet * max(1, max_pkts))()
     npk, used, got = _sz(0), _u64(0), _u64(0)
     lib = lib or load()
-    rc = lib.hdfs_crc32c_verify_packets_copy(dptr, nbytes, proto, chunk_size, ctype, client_offset, read_len, arr,
-                                             max_pkts, ctypes.byref(npk), ctypes.byref(used), dst, dst_cap,
-                                             ctypes.byref(got))
+    if iov is None:
+        iov = [(dst, dst_cap)]
+    vec = (IoVec * len(iov))(*[IoVec(p, n) for p, n in iov])
+    rc = lib.hdfs_crc32c_read_packets(dptr, nbytes, proto, chunk_size, ctype, client_offset, read_len, vec, len(iov),
+                                      arr, max_pkts, ctypes.byref(npk), ctypes.byref(used), ctypes.byref(got))
     if rc < 0:
         _check(rc, lib)
     return rc, [arr[i].as_dict() for i in range(npk.value)], used.value, got.value

@@ -895,6 +895,8 @@ struct hdfs_crc32c_plan {
 
 extern "C" {
 
+int hdfs_crc32c_abi_version(void) { return HDFS_CRC32C_ABI_VERSION; }
+
 const char *hdfs_crc32c_last_error(void) { return g_err; }
 
 int hdfs_crc32c_init(int device) {

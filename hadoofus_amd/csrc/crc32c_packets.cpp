@@ -303,16 +303,17 @@ struct DevBatch {
   PieceLayout L;
 };
 
-// Copy-out of a device-resident verify (hdfs_crc32c_verify_packets_copy):
+// Copy-out of a device-resident verify (hdfs_crc32c_read_packets):
 // every framing-clean packet delivers frame::read_avail bytes (its whole
 // payload, or the part of it a client read window takes) to its place in
 // dst (frame::read_place), never past `cap` bytes -- the read's length, or
 // the buffer for whole payloads.
 struct CopyOut {
   uint8_t *dst = nullptr;  // null: no copy-out
-  uint64_t cap = 0;
+  uint64_t cap = 0;        // bytes of dst the copies may fill (placement: never past it)
   bool win = false;
   int64_t client_offset = 0;
+  uint64_t want = 0;       // win: bytes the read still wants (remains_tot; >= cap)
 };
 // Where one packet's copy goes (host-built segment tables).
 struct CopyPlace {
@@ -769,10 +770,14 @@ int spec_pass(DevCtx &c, const uint8_t *d, uint64_t len, uint64_t pos, uint32_t 
   a.tune = tile_tune();
   a.hout = c.spec_hd;
   a.tabs = c.spec_tabs;
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
   HIPCHK(launch_spec_verify(a, grid, co.dst ? 1 : 0, c.stream));
   c.spec_n++;
   if (kDiag) g_spec_stats[0]++;
+  const auto t1 = clk::now();
   if ((rc = poll_seq(c, &early->seq, seq, "speculative verify"))) return rc;
+  const auto t2 = clk::now();
   SpecEarly E;
   std::memcpy(&E, early, sizeof(E));
   if (!E.eligible) return HDFS_CRC32C_OK;  // every workgroup has returned; the regular pass queues behind them
@@ -787,7 +792,13 @@ int spec_pass(DevCtx &c, const uint8_t *d, uint64_t len, uint64_t pos, uint32_t 
     r.offset_in_block = r0.offset_in_block + int64_t(k) * r0.data_len;
     r.seqno = r0.seqno + int64_t(k);
   }
+  const auto t3 = clk::now();
   if ((rc = poll_seq(c, &fin->seq, seq, "speculative verify"))) return rc;
+  if (g_dstream_trace) {  // diagnostic: where a speculative launch spends its time (us)
+    auto us = [](clk::time_point x, clk::time_point y) { return std::chrono::duration<double, std::micro>(y - x).count(); };
+    std::fprintf(stderr, "dstream spec grid=%d count=%u launch_us=%.1f early_us=%.1f fill_us=%.1f final_us=%.1f\n", grid,
+                 E.count, us(t0, t1), us(t1, t2), us(t2, t3), us(t3, clk::now()));
+  }
   SpecFinal F;
   std::memcpy(&F, fin, sizeof(F));
   if (F.exc) {  // a header off the prediction: frame the run instead
@@ -1134,16 +1145,23 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
 // lastPacketInBlock that leaves the read short is BAD_LASTPACKET after its
 // bytes are copied (:2545-2546).  The walk stops at the packet that
 // completes the read or raises one of these; records past it are dropped
-// (the reference never reads them).  As in the whole-payload mode, packets
-// after one with bad CRCs keep their own verdicts (the engine reports every
-// packet; the reference stops at the first): the window is a function of
-// the headers only, which is what lets the device place every packet's copy
-// before any verdict is known.  *delivered = the bytes the reference copies
-// before its loop returns an error.
-void apply_read_window(hdfs_crc32c_packet *p, size_t &n, uint64_t &consumed, const CopyOut &co,
-                       uint64_t *delivered) {
-  uint64_t remains = co.cap, got = 0;
+// (the reference never reads them).  The destination (co.cap bytes) may be
+// smaller than the read (co.want): once it is full the walk stops with
+// AGAIN (`rlen == 0 && remains_tot > 0`, :2547-2549) -- a packet whose bytes
+// were only partly delivered is dropped from the records and `consumed`
+// ends before it (the caller re-passes it with client_offset advanced, so
+// its new c_begin skips what it delivered: the reference's remains_pkt,
+// :2356-2361).  As in the whole-payload mode, packets after one with bad
+// CRCs keep their own verdicts (the engine reports every packet; the
+// reference stops at the first): the window is a function of the headers
+// only, which is what lets the device place every packet's copy before
+// any verdict is known.  *delivered = the bytes the reference copies before
+// its loop returns an error.  Returns 1 for AGAIN, else 0.
+int apply_read_window(hdfs_crc32c_packet *p, size_t &n, uint64_t &consumed, const CopyOut &co,
+                      uint64_t *delivered) {
+  uint64_t remains = co.want, room = co.cap, got = 0;
   bool err = false;
+  int again = 0;
   for (size_t k = 0; k < n; k++) {
     hdfs_crc32c_packet &r = p[k];
     const uint64_t end = r.stream_off + r.header_len + uint64_t(r.crc_len > 0 ? r.crc_len : 0) +
@@ -1166,14 +1184,31 @@ void apply_read_window(hdfs_crc32c_packet *p, size_t &n, uint64_t &consumed, con
         if (!crc_bad) r.error = HDFS_CRC32C_ERR_DATANODE_UNEXPECTED_READ_OFFSET;
         stop = true;
       } else {
-        const uint64_t clen = std::min<uint64_t>(avail, remains);
+        const uint64_t want = std::min<uint64_t>(avail, remains);  // remains_pkt
+        if (want > room && !crc_bad) {
+          // the destination fills inside this packet: its rest is the next
+          // call's (the reference returns AGAIN here with remains_pkt > 0)
+          if (!err) got += room;
+          n = k;
+          consumed = r.stream_off;
+          again = 1;
+          break;
+        }
+        const uint64_t clen = std::min(want, room);
         remains -= clen;
+        room -= clen;
         if (!err && !crc_bad) got += clen;
         if (r.last && remains > 0) {
           if (!crc_bad) r.error = HDFS_CRC32C_ERR_DATANODE_BAD_LASTPACKET;
           stop = true;
         }
         stop = stop || remains == 0;
+        if (!stop && room == 0 && !crc_bad) {  // full exactly at this packet's end
+          n = k + 1;
+          consumed = end;
+          again = 1;
+          break;
+        }
       }
     }
     if (r.error) err = true;
@@ -1184,6 +1219,7 @@ void apply_read_window(hdfs_crc32c_packet *p, size_t &n, uint64_t &consumed, con
     }
   }
   if (delivered) *delivered = got;
+  return again;
 }
 
 int verify_packets_dev_impl(int dev, const uint8_t *stream, uint64_t len, int proto, uint32_t cs, int ctype,
@@ -1203,8 +1239,9 @@ int verify_packets_dev_impl(int dev, const uint8_t *stream, uint64_t len, int pr
     if (r2) return r2;
   }
   if (rc) return rc;
+  int again = 0;
   if (co.win) {
-    apply_read_window(pkts, n, used, co, delivered);
+    again = apply_read_window(pkts, n, used, co, delivered);
   } else if (delivered) {  // what the reference copies out before its loop returns an error (src/datanode.c:2470-2486)
     uint64_t b = 0;
     for (size_t i = 0; i < n; i++) {
@@ -1215,7 +1252,8 @@ int verify_packets_dev_impl(int dev, const uint8_t *stream, uint64_t len, int pr
   }
   if (npkts) *npkts = n;
   if (consumed) *consumed = used;
-  return first_error(pkts, n);
+  rc = first_error(pkts, n);
+  return rc ? rc : again ? HDFS_CRC32C_AGAIN : HDFS_CRC32C_OK;
 }
 
 // Synchronous packet-run verify: framing, then pieces of <= 64 MiB of wire
@@ -1540,10 +1578,10 @@ int hdfs_crc32c_verify_packets(const void *stream, uint64_t len, int proto, uint
                              npkts, consumed, true);
 }
 
-int hdfs_crc32c_verify_packets_copy(const void *stream, uint64_t len, int proto, uint32_t chunk_size, int ctype,
-                                    int64_t client_offset, int64_t read_len, hdfs_crc32c_packet *pkts,
-                                    size_t max_pkts, size_t *npkts, uint64_t *consumed, void *dst, uint64_t dst_cap,
-                                    uint64_t *delivered) {
+int hdfs_crc32c_read_packets(const void *stream, uint64_t len, int proto, uint32_t chunk_size, int ctype,
+                             int64_t client_offset, int64_t read_len, const hdfs_crc32c_iovec *iov, int iovcnt,
+                             hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts, uint64_t *consumed,
+                             uint64_t *delivered) {
   if (npkts) *npkts = 0;
   if (consumed) *consumed = 0;
   if (delivered) *delivered = 0;
@@ -1552,28 +1590,57 @@ int hdfs_crc32c_verify_packets_copy(const void *stream, uint64_t len, int proto,
   if (rc) return rc;
   if (ctype == HDFS_CRC32C_CSUM_NULL)
     return fail(HDFS_CRC32C_EINVAL, "verify + copy-out needs CRC32 or CRC32C (src/datanode.c:2470-2486)");
-  CopyOut co;
-  co.dst = static_cast<uint8_t *>(dst);
-  co.cap = dst_cap;
-  if (read_len != HDFS_CRC32C_READ_ALL) {  // a client read (src/datanode.c:1363-1377: bloff >= 0, len > 0)
-    if (read_len <= 0 || client_offset < 0)
-      return fail(HDFS_CRC32C_EINVAL, "read window: offset %lld, length %lld", (long long)client_offset,
-                  (long long)read_len);
-    if (dst_cap < uint64_t(read_len))
-      return fail(HDFS_CRC32C_EINVAL, "copy-out buffer of %llu bytes is smaller than the read (%lld)",
-                  (unsigned long long)dst_cap, (long long)read_len);
-    co.win = true;
-    co.client_offset = client_offset;
-    co.cap = uint64_t(read_len);
-  }
+  if (iovcnt < 1 || !iov) return fail(HDFS_CRC32C_EINVAL, "no destination (iovcnt %d)", iovcnt);
+  const bool win = read_len != HDFS_CRC32C_READ_ALL;
+  if (win && (read_len <= 0 || client_offset < 0))  // a client read (src/datanode.c:1363-1377: bloff >= 0, len > 0)
+    return fail(HDFS_CRC32C_EINVAL, "read window: offset %lld, length %lld", (long long)client_offset,
+                (long long)read_len);
+  if (!win && iovcnt != 1) return fail(HDFS_CRC32C_EINVAL, "whole payloads (READ_ALL) go to one buffer");
   if (!len) return HDFS_CRC32C_OK;
   if (!stream) return fail(HDFS_CRC32C_EINVAL, "null stream");
   const int dev = stream_device(stream);
   if (dev < 0) return fail(HDFS_CRC32C_EINVAL, "verify + copy-out takes device-resident streams only");
-  if (!dst || stream_device(dst) != dev)
-    return fail(HDFS_CRC32C_EINVAL, "copy-out destination must be device memory of the stream's device");
-  return verify_packets_dev_impl(dev, static_cast<const uint8_t *>(stream), len, proto, chunk_size, ctype, pkts,
-                                 max_pkts, npkts, consumed, true, co, delivered);
+  for (int i = 0; i < iovcnt; i++)
+    if (iov[i].len && (!iov[i].base || stream_device(iov[i].base) != dev))
+      return fail(HDFS_CRC32C_EINVAL, "iovec %d: device memory of the stream's device needed", i);
+  // One pass per buffer: each delivers into its buffer and stops with AGAIN
+  // when the buffer is full, and the next resumes where the read stands
+  // (the stream from the packet it stopped in, the client offset advanced
+  // by what was delivered) -- the reference's re-entry with remains_pkt > 0.
+  const auto *s = static_cast<const uint8_t *>(stream);
+  uint64_t off = 0, got_all = 0;
+  size_t n_all = 0;
+  int64_t co_off = client_offset, rl = read_len;
+  rc = HDFS_CRC32C_OK;
+  for (int i = 0; i < iovcnt; i++) {
+    if (!iov[i].len) continue;
+    CopyOut co;
+    co.dst = static_cast<uint8_t *>(iov[i].base);
+    co.cap = iov[i].len;
+    if (win) {
+      co.win = true;
+      co.client_offset = co_off;
+      co.want = uint64_t(rl);
+      co.cap = std::min<uint64_t>(co.cap, co.want);
+    }
+    size_t n = 0;
+    uint64_t used = 0, got = 0;
+    rc = verify_packets_dev_impl(dev, s + off, len - off, proto, chunk_size, ctype, pkts ? pkts + n_all : nullptr,
+                                 max_pkts - n_all, &n, &used, true, co, &got);
+    if (rc < 0) return rc;
+    for (size_t k = 0; k < n; k++) pkts[n_all + k].stream_off += off;
+    n_all += n;
+    got_all += got;
+    off += used;
+    if (npkts) *npkts = n_all;
+    if (consumed) *consumed = off;
+    if (delivered) *delivered = got_all;
+    if (rc != HDFS_CRC32C_AGAIN) return rc;  // the read completed or ended with an error
+    co_off += int64_t(got);
+    rl -= int64_t(got);
+    if (n_all >= max_pkts && i + 1 < iovcnt) return rc;  // no room for more records: the caller resumes
+  }
+  return rc;
 }
 
 #ifdef HDFS_CRC32C_DIAG

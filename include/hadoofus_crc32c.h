@@ -62,6 +62,18 @@ uint32_t _hdfs_sw_crc32c(uint32_t crc, const void *buf, unsigned len);
 #define HDFS_CRC32C_CSUM_CRC32 1
 #define HDFS_CRC32C_CSUM_CRC32C 2
 
+/* ABI version of this header.  Every exported symbol carries the version
+ * node HADOOFUS_CRC32C_<n> (hadoofus_amd/csrc/exports.map), and a function
+ * whose signature changes gets a new name: a caller built against another
+ * version fails to bind instead of passing shifted arguments.  Bindings that
+ * load the library at run time (ctypes, dlsym) compare
+ * hdfs_crc32c_abi_version() with the version they were written for.
+ *   3: round 3 (unversioned exports)
+ *   4: hdfs_crc32c_verify_packets_copy -> hdfs_crc32c_read_packets (iovecs,
+ *      resumable reads); versioned exports */
+#define HDFS_CRC32C_ABI_VERSION 4
+int hdfs_crc32c_abi_version(void);
+
 const char *hdfs_crc32c_last_error(void);
 /* Initialise the engine on `device`.  device >= 0 also BINDS the engine to
  * it: every later call that names no device (all of them) runs there, with
@@ -205,22 +217,28 @@ int hdfs_crc32c_parse_packets(const void *stream, uint64_t len, int proto, uint3
 int hdfs_crc32c_verify_packets(const void *stream, uint64_t len, int proto, uint32_t chunk_size,
     int ctype, hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts, uint64_t *consumed);
 
-/* Verify + copy-out of a DEVICE-resident packet stream (GPU-direct
- * receive): hdfs_crc32c_verify_packets, and in the same pass over HBM the
- * packets' data is written, de-framed and in stream order, to the device
- * buffer dst (dst_cap bytes) -- the read path's _process_recv_packet /
- * _recv_packet_copy_data (src/datanode.c:2470-2553) fused into the verify
- * kernel: each payload byte is read once and written once.
+/* Read of a DEVICE-resident packet stream (GPU-direct receive):
+ * hdfs_crc32c_verify_packets, and in the same pass over HBM the packets'
+ * data is written, de-framed and in stream order, to the caller's device
+ * buffers -- the read path's _process_recv_packet / _recv_packet_copy_data
+ * (src/datanode.c:2470-2553) fused into the verify kernel: each payload
+ * byte is read once and written once.  (Round 4: replaces round 3's
+ * hdfs_crc32c_verify_packets_copy, whose signature had changed under the
+ * same name; see HDFS_CRC32C_ABI_VERSION.)
  *
+ * iov / iovcnt: the destination, device buffers filled in order (the
+ * reference's iovec array, :2509-2537); total capacity cap = sum of
+ * iov[i].len.
  * read_len = HDFS_CRC32C_READ_ALL: every framing-clean packet's whole
- *   payload; *delivered = payload bytes of the packets before the first
- *   packet with an error; EINVAL if dst is too small for the framed payload.
+ *   payload (iovcnt must be 1); *delivered = payload bytes of the packets
+ *   before the first packet with an error; EINVAL if the buffer is too
+ *   small for the framed payload.
  * read_len > 0: a client read of the block's bytes [client_offset,
  *   client_offset + read_len) (hdfs_datanode_read's bloff / len,
- *   src/datanode.c:1363-1377; dst_cap >= read_len).  Packets are taken while
- *   the read wants bytes (src/datanode.c:1476): a packet that starts before
- *   client_offset delivers from c_begin = client_offset - offsetInBlock on,
- *   and c_begin >= dataLen is HDFS_CRC32C_ERR_DATANODE_UNEXPECTED_READ_OFFSET
+ *   src/datanode.c:1363-1377).  Packets are taken while the read wants
+ *   bytes (src/datanode.c:1476): a packet that starts before client_offset
+ *   delivers from c_begin = client_offset - offsetInBlock on, and c_begin >=
+ *   dataLen is HDFS_CRC32C_ERR_DATANODE_UNEXPECTED_READ_OFFSET
  *   (:2478-2486); a packet delivers at most what is left of the read; a
  *   lastPacketInBlock packet that leaves the read short, or an empty last
  *   packet before it is complete, is HDFS_CRC32C_ERR_DATANODE_BAD_LASTPACKET
@@ -228,15 +246,32 @@ int hdfs_crc32c_verify_packets(const void *stream, uint64_t len, int proto, uint
  *   the read or raises one of those; later packets are not returned.
  *   *delivered = the bytes the reference copies to the caller before its
  *   loop returns an error (a BAD_LASTPACKET packet's own bytes included).
+ *   A destination smaller than the rest of the read is RESUMABLE, as the
+ *   reference's read is (`rlen == 0 && remains_tot > 0` -> HDFS_AGAIN,
+ *   :2547-2549, re-entered with remains_pkt > 0, :2356-2361): once the
+ *   buffers are full the call returns HDFS_CRC32C_AGAIN with *delivered =
+ *   cap, and *consumed = where the stream must resume -- the start of the
+ *   packet whose bytes were only partly delivered (its record is returned
+ *   by the call that completes it), or the end of the last packet if the
+ *   buffers filled exactly there.  The caller continues with stream +
+ *   consumed, client_offset + delivered and read_len - delivered: the
+ *   re-passed packet then delivers from its new c_begin on.
  * Packets after one with bad CRCs are still verified and reported (as in
- * hdfs_crc32c_verify_packets); bytes of dst past *delivered are unspecified,
- * bytes past dst_cap (or read_len) are never written.  ctype must be CRC32
- * or CRC32C.  Returns the first error in stream order, 0, or a negative
- * status. */
+ * hdfs_crc32c_verify_packets); bytes of the buffers past *delivered are
+ * unspecified, bytes past them (or past the read) are never written.  ctype
+ * must be CRC32 or CRC32C.  Returns the first error in stream order, 0,
+ * HDFS_CRC32C_AGAIN, or a negative status. */
 #define HDFS_CRC32C_READ_ALL (-1)
-int hdfs_crc32c_verify_packets_copy(const void *stream, uint64_t len, int proto, uint32_t chunk_size,
-    int ctype, int64_t client_offset, int64_t read_len, hdfs_crc32c_packet *pkts, size_t max_pkts,
-    size_t *npkts, uint64_t *consumed, void *dst, uint64_t dst_cap, uint64_t *delivered);
+/* Not an error: the destination filled before the read completed (the
+ * reference's HDFS_AGAIN); outside the range of the datanode errors. */
+#define HDFS_CRC32C_AGAIN 1000
+typedef struct hdfs_crc32c_iovec {
+	void *base;     /* device memory of the stream's device */
+	uint64_t len;
+} hdfs_crc32c_iovec;
+int hdfs_crc32c_read_packets(const void *stream, uint64_t len, int proto, uint32_t chunk_size, int ctype,
+    int64_t client_offset, int64_t read_len, const hdfs_crc32c_iovec *iov, int iovcnt,
+    hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts, uint64_t *consumed, uint64_t *delivered);
 
 /* ---- write path: outgoing data packets ---------------------------------- */
 /* One outgoing data packet, as _send_packet sizes it and

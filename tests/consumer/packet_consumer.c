@@ -8,8 +8,9 @@
  * then (3) composes the packets of one write (hdfs_crc32c_compose_packets)
  * and reads them back through the verifier; (4) uploads the stream to the
  * GPU and reads two client windows out of it with the fused verify +
- * copy-out (hdfs_crc32c_verify_packets_copy: c_begin, remains_tot,
- * src/datanode.c:2478-2549); (5) maps an engine failure the way a datanode
+ * copy-out (hdfs_crc32c_read_packets: c_begin, remains_tot,
+ * src/datanode.c:2478-2549), once into one buffer and once resumed over a
+ * scatter list of small buffers (HDFS_CRC32C_AGAIN); (5) maps an engine failure the way a datanode
  * must -- an I/O error, never a checksum error.
  * Prints "0 failures" on success.  Test infrastructure (tests/test_abi.py
  * links it on CPU, tests/test_packets.py runs it on the GPU).
@@ -192,9 +193,10 @@ int main(void)
 		uint64_t delivered = 0;
 		/* bloff = 8 * DLEN + 5, len = 2 * DLEN: the server starts at packet 8;
 		 * its first 5 bytes are skipped, packet 10 gives 5 bytes, the read ends */
-		rc = hdfs_crc32c_verify_packets_copy((uint8_t *)dstream + 8 * pk, total - 8 * pk, HDFS_CRC32C_PROTO_V2, CS,
-		    HDFS_CRC32C_CSUM_CRC32C, 8 * (int64_t)DLEN + 5, 2 * (int64_t)DLEN, rec, NPK + 1, &n, &used, duser,
-		    ucap, &delivered);
+		hdfs_crc32c_iovec iov1 = {duser, ucap};
+		rc = hdfs_crc32c_read_packets((uint8_t *)dstream + 8 * pk, total - 8 * pk, HDFS_CRC32C_PROTO_V2, CS,
+		    HDFS_CRC32C_CSUM_CRC32C, 8 * (int64_t)DLEN + 5, 2 * (int64_t)DLEN, &iov1, 1, rec, NPK + 1, &n, &used,
+		    &delivered);
 		check(rc == 0 && n == 3 && delivered == 2 * DLEN && used == 3 * pk, "read window: clean read");
 		check(hdfs_crc32c_memcpy(back, duser, delivered, 1) == 0, "download");
 		for (size_t k = 0, at = 0; k < 3; k++) {
@@ -205,13 +207,50 @@ int main(void)
 		/* bloff = 3 * DLEN + 1000 over packets 3.. with packet 7 corrupt: the
 		 * read gets packets 3..6 (the first from byte 1000 on) and then
 		 * BAD_CHECKSUM; the window still ends in packet 8 */
-		rc = hdfs_crc32c_verify_packets_copy((uint8_t *)dstream + 3 * pk, total - 3 * pk, HDFS_CRC32C_PROTO_V2, CS,
-		    HDFS_CRC32C_CSUM_CRC32C, 3 * (int64_t)DLEN + 1000, 5 * (int64_t)DLEN + 777, rec, NPK + 1, &n, &used,
-		    duser, ucap, &delivered);
+		rc = hdfs_crc32c_read_packets((uint8_t *)dstream + 3 * pk, total - 3 * pk, HDFS_CRC32C_PROTO_V2, CS,
+		    HDFS_CRC32C_CSUM_CRC32C, 3 * (int64_t)DLEN + 1000, 5 * (int64_t)DLEN + 777, &iov1, 1, rec, NPK + 1, &n,
+		    &used, &delivered);
 		check(rc == HDFS_CRC32C_ERR_DATANODE_BAD_CHECKSUM && n == 6 && rec[4].first_bad == 3 &&
 		    delivered == 4 * DLEN - 1000, "read window: bad packet");
 		check(map_engine_rc(rc).kind == 1 && map_engine_rc(rc).num == HDFS_CRC32C_ERR_DATANODE_BAD_CHECKSUM,
 		    "checksum error maps to the reference's error");
+		/* the clean read again, into a user buffer of 3 pieces smaller than
+		 * the read, in calls of one piece each: AGAIN until the last, each
+		 * resuming where the previous stopped (stream + consumed, bloff +
+		 * delivered, len - delivered), the bytes identical */
+		{
+			const uint64_t piece = DLEN / 2 + 3;  /* every piece ends inside a packet */
+			uint64_t at_stream = 8 * pk, got_tot = 0;
+			int64_t bloff = 8 * (int64_t)DLEN + 5, left = 2 * (int64_t)DLEN;
+			int calls = 0;
+			do {
+				hdfs_crc32c_iovec iv = {(uint8_t *)duser + got_tot, piece};
+				rc = hdfs_crc32c_read_packets((uint8_t *)dstream + at_stream, total - at_stream, HDFS_CRC32C_PROTO_V2,
+				    CS, HDFS_CRC32C_CSUM_CRC32C, bloff, left, &iv, 1, rec, NPK + 1, &n, &used, &delivered);
+				at_stream += used;
+				got_tot += delivered;
+				bloff += (int64_t)delivered;
+				left -= (int64_t)delivered;
+				calls++;
+			} while (rc == HDFS_CRC32C_AGAIN && calls < 16);
+			check(rc == 0 && got_tot == 2 * DLEN && calls == 4, "resumed read: AGAIN until complete");
+			check(hdfs_crc32c_memcpy(back, duser, got_tot, 1) == 0, "download");
+			for (size_t k = 0, at = 0; k < 3; k++) {
+				const size_t skip = k == 0 ? 5 : 0, take = k == 2 ? 5 : DLEN - skip;
+				check(memcmp(back + at, s + (8 + k) * pk + 31 + crclen + skip, take) == 0, "resumed read bytes");
+				at += take;
+			}
+			/* the same read as one call over a scatter list of the pieces */
+			hdfs_crc32c_iovec iv4[4];
+			for (int j = 0; j < 4; j++) {
+				iv4[j].base = (uint8_t *)duser + (uint64_t)j * piece;
+				iv4[j].len = piece;
+			}
+			rc = hdfs_crc32c_read_packets((uint8_t *)dstream + 8 * pk, total - 8 * pk, HDFS_CRC32C_PROTO_V2, CS,
+			    HDFS_CRC32C_CSUM_CRC32C, 8 * (int64_t)DLEN + 5, 2 * (int64_t)DLEN, iv4, 4, rec, NPK + 1, &n, &used,
+			    &delivered);
+			check(rc == 0 && delivered == 2 * DLEN && n == 3 && used == 3 * pk, "scatter read");
+		}
 		hdfs_crc32c_dev_free(duser);
 		hdfs_crc32c_dev_free(dstream);
 		free(back);
@@ -221,8 +260,9 @@ int main(void)
 	 * required) is an I/O error for the datanode, not a checksum error */
 	{
 		uint64_t delivered = 0;
-		rc = hdfs_crc32c_verify_packets_copy(s, total, HDFS_CRC32C_PROTO_V2, CS, HDFS_CRC32C_CSUM_CRC32C, 0,
-		    HDFS_CRC32C_READ_ALL, rec, NPK + 1, &n, &used, data, DLEN, &delivered);
+		hdfs_crc32c_iovec hv = {data, DLEN};
+		rc = hdfs_crc32c_read_packets(s, total, HDFS_CRC32C_PROTO_V2, CS, HDFS_CRC32C_CSUM_CRC32C, 0,
+		    HDFS_CRC32C_READ_ALL, &hv, 1, rec, NPK + 1, &n, &used, &delivered);
 		const struct dn_error e = map_engine_rc(rc);
 		check(rc == HDFS_CRC32C_EINVAL && e.kind == 2 && e.num == EIO, "engine failure -> EIO");
 	}

@@ -40,8 +40,9 @@ def diagpath(libpath):
 
 
 def _exported(path):
+    """Defined dynamic symbols, version suffixes (name@@NODE) stripped."""
     out = subprocess.check_output(["nm", "-D", "--defined-only", path], text=True)
-    return set(l.split()[-1] for l in out.splitlines() if l.strip())
+    return set(l.split()[-1].split("@")[0] for l in out.splitlines() if l.strip())
 
 
 def test_release_has_no_diagnostic_knobs(libpath, diagpath):
@@ -87,8 +88,7 @@ def test_release_kernels_are_the_product_shapes(libpath, diagpath):
 
 
 def test_exports_every_declared_symbol(libpath):
-    out = subprocess.check_output(["nm", "-D", "--defined-only", libpath], text=True)
-    exported = set(l.split()[-1] for l in out.splitlines() if l.strip())
+    exported = _exported(libpath)
     for h in ("crc32c.h", "hadoofus_crc32c.h"):
         decl = _declared(h)
         assert decl, h
@@ -109,8 +109,8 @@ def test_exports_nothing_else(libpath):
         parts = line.split()
         if len(parts) < 3 or parts[1] not in "TW":
             continue
-        name = parts[2]
-        if name in decl or name in ("_init", "_fini"):
+        name = parts[2].split("@")[0]
+        if name in decl or name in ("_init", "_fini", "HADOOFUS_CRC32C_%d" % _abi_version()):
             continue
         if name.startswith("_ZN11hdfs_crc32c") and "_kernel" in name:
             continue
@@ -226,3 +226,79 @@ def test_both_libraries_load_and_bind(libpath, diagpath):
     mode = os.RTLD_NOW | os.RTLD_LOCAL
     abi.bind_product(ctypes.CDLL(libpath, mode=mode))
     abi.bind_diag(abi.bind_product(ctypes.CDLL(diagpath, mode=mode)))
+
+
+def _signature_sections():
+    """tests/golden/abi_signatures.txt -> {version: {name: prototype}}."""
+    sec, cur = {}, None
+    with open(os.path.join(ROOT, "tests", "golden", "abi_signatures.txt")) as f:
+        for line in f:
+            line = line.rstrip("\n")
+            if not line or line.startswith("#"):
+                continue
+            if line.startswith("["):
+                cur = int(line.strip("[]"))
+                sec[cur] = {}
+                continue
+            name, proto = line.split(": ", 1)
+            sec[cur][name] = proto
+    return sec
+
+
+def _abi_version():
+    txt = open(os.path.join(ROOT, "include", "hadoofus_crc32c.h")).read()
+    return int(re.search(r"#define HDFS_CRC32C_ABI_VERSION (\d+)", txt).group(1))
+
+
+def test_header_prototypes_are_the_committed_abi():
+    """The headers' prototypes are exactly the committed list of the current
+    ABI version, and no function of it kept a name an earlier version gave a
+    different signature: a caller built against another version fails to
+    bind instead of passing shifted arguments (round 3 broke this rule:
+    verify_packets_copy gained two arguments in the middle under the same
+    name, and a tool holding the round-2 prototype crashed -- DESIGN 10.1)."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import abi_signatures
+    sec = _signature_sections()
+    v = _abi_version()
+    assert max(sec) == v, (sorted(sec), v)
+    assert abi_signatures.header_prototypes() == sec[v]
+    for old in sec:
+        if old == v:
+            continue
+        for name, proto in sec[v].items():
+            if name in sec[old]:
+                assert sec[old][name] == proto, (name, old, sec[old][name], proto)
+
+
+def test_exports_carry_the_version_node(libpath, diagpath):
+    """Every exported engine symbol (the C ABI and the drop-in trio) is in the
+    version node HADOOFUS_CRC32C_<ABI version> of exports.map."""
+    v = _abi_version()
+    for path in (libpath, diagpath):
+        out = subprocess.check_output(["objdump", "-T", path], text=True)
+        seen = {}
+        for line in out.splitlines():
+            parts = line.split()
+            if len(parts) >= 3 and (parts[-1].startswith("hdfs_crc32c_") or parts[-1].startswith("_hdfs_")):
+                seen[parts[-1]] = parts[-2]
+        assert "hdfs_crc32c_read_packets" in seen and "_hdfs_crc32c" in seen
+        bad = {n: ver for n, ver in seen.items() if ver != f"HADOOFUS_CRC32C_{v}"}
+        assert not bad, bad
+    assert "hdfs_crc32c_verify_packets_copy" not in _exported(libpath)
+
+
+def test_abi_version_call_and_binding_check(libpath):
+    """hdfs_crc32c_abi_version() needs no GPU and equals the header's
+    version; the Python bindings refuse a library of another version."""
+    from hadoofus_amd import abi
+    lib = ctypes.CDLL(libpath)
+    lib.hdfs_crc32c_abi_version.restype = ctypes.c_int
+    assert lib.hdfs_crc32c_abi_version() == _abi_version() == abi.ABI_VERSION
+
+    class Old:
+        @staticmethod
+        def hdfs_crc32c_abi_version():
+            return 3
+    with pytest.raises(ImportError):
+        abi.check_abi(Old())

@@ -106,12 +106,12 @@ def test_gpu_device_paths_no_check_fires(engine, diag, oracle, proto, cs, ctype,
         assert engine.verify_packets(None, proto, cs, ctype, dptr=p, nbytes=cut, lib=diag) == \
             oracle.verify_packets(stream[:cut], proto, cs, ctype)
         dst = engine.DeviceBuffer(total + 4096)
-        rc, pkts, used, got = engine.verify_packets_copy(p, len(stream), dst.ptr, total, proto, cs, ctype, lib=diag)
+        rc, pkts, used, got = engine.read_packets(p, len(stream), dst.ptr, total, proto, cs, ctype, lib=diag)
         assert (rc, pkts, used) == want
         assert dst.download(got).tobytes() == _payloads(stream, want[1])
         # client reads: windows starting inside a packet, ending inside another
         for co, rl in ((0, 1), (dl[0] - 3, 10), (total // 3 + 5, total // 4), (total - 1, 1)):
-            rc2, pk2, used2, got2 = engine.verify_packets_copy(p, len(stream), dst.ptr, rl, proto, cs, ctype,
+            rc2, pk2, used2, got2 = engine.read_packets(p, len(stream), dst.ptr, rl, proto, cs, ctype,
                                                                client_offset=co, read_len=rl, lib=diag)
             wrc, wpk, wused, wdata = oracle.read_packets(stream, co, rl, proto, cs, ctype)
             assert (rc2, pk2, used2, got2) == (wrc, wpk, wused, len(wdata)), (co, rl)

@@ -285,7 +285,7 @@ def _payloads(s, pkts):
     (2, 512, CSUM_CRC32C, "random", 1, 150),
 ])
 def test_gpu_device_stream_copy_out(engine, oracle, proto, cs, ctype, sizes, shift, corrupt_at):
-    """Verify + fused copy-out (hdfs_crc32c_verify_packets_copy): records equal
+    """Verify + fused copy-out (hdfs_crc32c_read_packets): records equal
     the oracle's, and the destination holds exactly the de-framed payload of
     every packet before the first error, byte for byte."""
     rng = np.random.default_rng(cs + proto + shift)
@@ -305,7 +305,7 @@ def test_gpu_device_stream_copy_out(engine, oracle, proto, cs, ctype, sizes, shi
     total = sum(dl)
     dst = engine.DeviceBuffer(total + 64)
     dst.fill(0xA5)
-    rc, pkts, used, delivered = engine.verify_packets_copy(p, len(s), dst.ptr, total, proto, cs, ctype, max_pkts=mp)
+    rc, pkts, used, delivered = engine.read_packets(p, len(s), dst.ptr, total, proto, cs, ctype, max_pkts=mp)
     assert (rc, pkts, used) == want
     expect = _payloads(s, want[1])
     assert delivered == len(expect)
@@ -326,16 +326,16 @@ def test_gpu_device_stream_copy_out_errors(engine, oracle):
     keep, p = _dev(engine, s)
     dst = engine.DeviceBuffer(8 * 65536)
     with pytest.raises(engine.CRC32CError):
-        engine.verify_packets_copy(p, len(s), dst.ptr, 8 * 65536 - 1)
+        engine.read_packets(p, len(s), dst.ptr, 8 * 65536 - 1)
     host = np.zeros(8 * 65536, np.uint8)
     with pytest.raises(engine.CRC32CError):
-        engine.verify_packets_copy(p, len(s), host.ctypes.data, host.nbytes)
+        engine.read_packets(p, len(s), host.ctypes.data, host.nbytes)
     with pytest.raises(engine.CRC32CError):
-        engine.verify_packets_copy(p, len(s), dst.ptr, dst.nbytes, ctype=0)
+        engine.read_packets(p, len(s), dst.ptr, dst.nbytes, ctype=0)
     src = np.frombuffer(s, np.uint8).copy()
     with pytest.raises(engine.CRC32CError):
-        engine.verify_packets_copy(src.ctypes.data, len(s), dst.ptr, dst.nbytes)
-    rc, pkts, used, delivered = engine.verify_packets_copy(p, len(s), dst.ptr, dst.nbytes)
+        engine.read_packets(src.ctypes.data, len(s), dst.ptr, dst.nbytes)
+    rc, pkts, used, delivered = engine.read_packets(p, len(s), dst.ptr, dst.nbytes)
     assert rc == 0 and delivered == 8 * 65536 and used == len(s)
     keep.free()
     dst.free()
@@ -356,7 +356,7 @@ def test_gpu_device_stream_many_passes(engine, oracle):
     got = engine.verify_packets(None, max_pkts=mp, dptr=p, nbytes=len(s))
     assert got == want
     dst = engine.DeviceBuffer(sum(dl))
-    rc, pkts, used, delivered = engine.verify_packets_copy(p, len(s), dst.ptr, dst.nbytes, max_pkts=mp)
+    rc, pkts, used, delivered = engine.read_packets(p, len(s), dst.ptr, dst.nbytes, max_pkts=mp)
     assert (rc, pkts, used) == want and delivered == 5 * 2048
     assert dst.download(delivered).tobytes() == _payloads(s, want[1])
     keep.free()
@@ -418,7 +418,7 @@ def test_gpu_device_stream_irregular_headers(engine, oracle, proto, pattern):
         assert engine.parse_packets(None, proto, 512, CSUM_CRC32C, dptr=p, nbytes=len(s))[1] == \
             _framing_only(want[1])
         dst = engine.DeviceBuffer(sum(dl))
-        rc, pkts, used, delivered = engine.verify_packets_copy(p, len(s), dst.ptr, dst.nbytes, proto)
+        rc, pkts, used, delivered = engine.read_packets(p, len(s), dst.ptr, dst.nbytes, proto)
         assert (rc, pkts, used) == want and dst.download(delivered).tobytes() == _payloads(s, want[1])
         keep.free()
         dst.free()
@@ -456,7 +456,7 @@ def test_gpu_device_stream_short_runs(engine, oracle, proto, cs, ctype):
                 # verify + copy-out: the payload before the first error, byte for byte
                 dstb = engine.DeviceBuffer(sum(dl) + 64)
                 dstb.fill(0xA5)
-                rc, pkts, used, delivered = engine.verify_packets_copy(p, len(s), dstb.ptr, sum(dl), proto, cs, ctype)
+                rc, pkts, used, delivered = engine.read_packets(p, len(s), dstb.ptr, sum(dl), proto, cs, ctype)
                 assert (rc, pkts, used) == want, (dl, "copy")
                 expect = _payloads(s, want[1])
                 assert delivered == len(expect) and dstb.download(delivered).tobytes() == expect, (dl, "copy")
@@ -529,7 +529,7 @@ def _dev_read(engine, s, shift, co, rl, proto=2, cs=512, ctype=CSUM_CRC32C, cap=
     dst = engine.DeviceBuffer(cap + 64)
     dst.fill(0xA5)
     try:
-        rc, pkts, used, delivered = engine.verify_packets_copy(p, len(s), dst.ptr, cap, proto, cs, ctype, max_pkts=mp,
+        rc, pkts, used, delivered = engine.read_packets(p, len(s), dst.ptr, cap, proto, cs, ctype, max_pkts=mp,
                                                                client_offset=co, read_len=rl)
         guard = dst.download(64, offset=cap).tobytes()
         return rc, pkts, used, dst.download(delivered).tobytes(), guard
@@ -616,7 +616,7 @@ def test_gpu_copy_out_mixed_sizes_never_past_cap(engine, oracle):
     dst = engine.DeviceBuffer(cap + 4096)
     dst.fill(0xA5)
     with pytest.raises(engine.CRC32CError):
-        engine.verify_packets_copy(p, len(s), dst.ptr, cap)
+        engine.read_packets(p, len(s), dst.ptr, cap)
     assert dst.download(4096, offset=cap).tobytes() == b"\xa5" * 4096
     keep.free()
     dst.free()
@@ -661,7 +661,7 @@ def test_gpu_device_stream_many_blocks(engine, oracle, case):
             want = oracle.read_packets(s, co, rl, proto, cs, CSUM_CRC32C)
             dst = engine.DeviceBuffer(rl + 64)
             dst.fill(0xA5)
-            got = engine.verify_packets_copy(p, len(s), dst.ptr, rl, proto, cs, CSUM_CRC32C, client_offset=co,
+            got = engine.read_packets(p, len(s), dst.ptr, rl, proto, cs, CSUM_CRC32C, client_offset=co,
                                              read_len=rl)
             assert got[:3] == want[:3]
             assert dst.download(got[3]).tobytes() == want[3]
@@ -676,4 +676,95 @@ def test_gpu_device_stream_many_blocks(engine, oracle, case):
             assert {k: (q["first_bad"], q["bad_chunks"]) for k, q in enumerate(got[1]) if q["error"] == BAD} == \
                 {k: (v[0], len(v)) for k, v in bad.items()}
     finally:
+        keep.free()
+
+
+# --- resumable reads and scatter lists (round 4) ------------------------------
+def _resumed_read(engine, p, n, co, rl, piece, dst, proto, cs, ctype):
+    """A client read through hdfs_crc32c_read_packets in calls whose buffer is
+    `piece` bytes, each resuming where the previous stopped (AGAIN:
+    stream + consumed, client_offset + delivered, read_len - delivered) --
+    the reference's re-entry with remains_pkt > 0 (src/datanode.c:2356-2361,
+    2547-2549).  -> (rc, records, consumed, bytes, calls)."""
+    at, tot, recs, calls = 0, 0, [], 0
+    while True:
+        cap = min(piece, rl - tot)
+        rc, pk, used, got = engine.read_packets(p + at, n - at, dst.ptr + tot, cap, proto, cs, ctype,
+                                                client_offset=co + tot, read_len=rl - tot)
+        calls += 1
+        for q in pk:
+            q["stream_off"] += at
+        recs += pk
+        at += used
+        tot += got
+        if rc != engine.AGAIN:
+            return rc, recs, at, dst.download(tot).tobytes(), calls
+        assert got == cap and calls < 10000
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("proto,cs,ctype,sizes", [
+    (2, 512, CSUM_CRC32C, "regular"),   # speculative launches / device framing passes
+    (1, 512, CSUM_CRC32, "regular"),
+    (2, 512, CSUM_CRC32C, "short"),     # the one-launch short-run kernel
+    (2, 4096, CSUM_CRC32C, "mixed"),    # the host window walk
+    (2, 100, CSUM_CRC32C, "partial"),   # generic chunks
+])
+def test_gpu_read_resumable_and_scatter(engine, oracle, proto, cs, ctype, sizes):
+    """A client read into a destination smaller than the read: resumed call
+    by call (AGAIN), and in one call over a scatter list of buffers (the
+    reference's iovec array, src/datanode.c:2509-2537) -- the bytes, the
+    records (each packet once, from the call that completes it), consumed
+    and the final status equal the oracle's single read loop, and no byte
+    lands past a buffer."""
+    rng = np.random.default_rng(cs + proto + len(sizes) + 17)
+    if sizes == "regular":
+        dl = [65536] * 150 + [12345]
+    elif sizes == "short":
+        dl = [65536] * 40 + [3000]
+    elif sizes == "mixed":
+        dl = [int(x) for x in np.repeat(rng.choice([4096, 61440, 30000, 65536], 30), rng.integers(1, 6, 30))]
+    else:
+        dl = [40000] * 60
+    base = 3 * 65536
+    s, _ = build_stream(oracle.crc32c, proto, cs, ctype, dl, seed=len(dl) + 5, corrupt=[(len(dl) - 5, 1)],
+                        offset0=base)
+    total = sum(dl)
+    whole = oracle.verify_packets(s, proto, cs, ctype)[1]
+    starts = np.cumsum([0] + dl[:-1])
+    cases = [(base + 1000, total // 3), (base + 7, total), (base + total // 2 + 11, total // 4)]
+    for ci, (co, rl) in enumerate(cases):
+        k = int(np.searchsorted(starts, co - base, side="right")) - 1
+        sub = s[whole[k]["stream_off"]:]
+        want = oracle.read_packets(sub, co, rl, proto, cs, ctype)
+        keep, p = _dev(engine, sub, ci % 3)
+        dst = engine.DeviceBuffer(rl + 4096)
+        for piece in (65536 + 3, 100003, 1 << 20):
+            dst.fill(0xA5)
+            rc, recs, used, data, calls = _resumed_read(engine, p, len(sub), co, rl, piece, dst, proto, cs, ctype)
+            assert (rc, recs, used) == want[:3], (co - base, rl, piece)
+            assert data == want[3], (co - base, rl, piece)
+            assert calls >= min(len(want[3]) // piece, 2) or rc != 0
+        # one call over a scatter list: buffers of uneven sizes, a 16-B guard after each
+        sizes_l = [int(x) for x in rng.integers(20000, 300000, 64)]
+        iov, off = [], 0
+        while off < rl + 4096 and len(iov) < 64:
+            n = min(sizes_l[len(iov)], rl + 4096 - off)
+            iov.append((off, n))
+            off += n + 16
+        big = engine.DeviceBuffer(off + 64)
+        big.fill(0xA5)
+        rc, recs, used, got = engine.read_packets(p, len(sub), None, 0, proto, cs, ctype, client_offset=co, read_len=rl,
+                                                  iov=[(big.ptr + a, n) for a, n in iov])
+        assert (rc, recs, used) == want[:3], (co - base, rl, "iov")
+        flat = big.download(off).tobytes()
+        data, left = b"", got
+        for a, n in iov:
+            take = min(n, left)
+            data += flat[a:a + take]
+            left -= take
+            assert flat[a + n:a + n + 16] == b"\xa5" * 16  # guards untouched
+        assert data == want[3]
+        big.free()
+        dst.free()
         keep.free()

@@ -113,7 +113,7 @@ def test_gpu_spec_runs_vs_oracle(engine, diag, oracle, name, proto, cs, ctype, d
         # verify + copy-out: the payload before the first error, byte for byte
         dst = engine.DeviceBuffer(sum(dl) + 64)
         dst.fill(0xA5)
-        rc, pkts, used, got = engine.verify_packets_copy(p, len(s), dst.ptr, sum(dl), proto, cs, ctype, lib=diag)
+        rc, pkts, used, got = engine.read_packets(p, len(s), dst.ptr, sum(dl), proto, cs, ctype, lib=diag)
         assert (rc, pkts, used) == want
         expect = _payloads(s, want[1])
         assert got == len(expect) and dst.download(got).tobytes() == expect
@@ -173,7 +173,7 @@ def test_gpu_spec_many_passes(engine, diag, oracle):
     assert on == want == off
     assert st["taken"] == 2 and st["exc"] == 0, st
     dst = engine.DeviceBuffer(sum(dl))
-    rc, pkts, used, delivered = engine.verify_packets_copy(p, len(s), dst.ptr, dst.nbytes, max_pkts=mp, lib=diag)
+    rc, pkts, used, delivered = engine.read_packets(p, len(s), dst.ptr, dst.nbytes, max_pkts=mp, lib=diag)
     assert (rc, pkts, used) == want and delivered == 5 * 2048
     assert dst.download(delivered).tobytes() == _payloads(s, want[1])
     keep.free()
@@ -203,7 +203,7 @@ def test_gpu_spec_read_windows(engine, diag, oracle):
         for spec in (1, 0):
             assert diag.hdfs_crc32c_set_speculation(spec) == 0
             dst.fill(0xA5)
-            got = engine.verify_packets_copy(p, len(st_), dst.ptr, rl, client_offset=co, read_len=rl, lib=diag)
+            got = engine.read_packets(p, len(st_), dst.ptr, rl, client_offset=co, read_len=rl, lib=diag)
             assert got[:3] == want[:3], (i, spec)
             assert dst.download(got[3]).tobytes() == want[3], (i, spec)
             assert dst.download(64, offset=rl).tobytes() == b"\xa5" * 64, (i, spec)
@@ -224,7 +224,7 @@ def test_gpu_spec_copy_out_too_small(engine, diag, oracle):
     dst.fill(0xA5)
     _stats(diag)
     with pytest.raises(engine.CRC32CError):
-        engine.verify_packets_copy(p, len(s), dst.ptr, cap, lib=diag)
+        engine.read_packets(p, len(s), dst.ptr, cap, lib=diag)
     assert _stats(diag)["taken"] == 1
     assert dst.download(4096, offset=cap).tobytes() == b"\xa5" * 4096
     keep.free()
