@@ -532,17 +532,23 @@ int small_call(DevCtx &c, int mode, uint32_t len, uint32_t cs, uint32_t reg0, bo
                              c.d_tab_kx + ctype * kTabKxWords, ctype ? kPolyZlib : kPoly, c.dv_small_out,
                              c.dv_small_out + kSmallMeta, seq, c.stream));
   // a fault of EARLIER work on the stream is this call's error, not the next
-  // caller's: one query while this call's kernel is in flight, so the
-  // runtime's bookkeeping of the previous dispatch overlaps the wait (a
-  // query after the completion word cost every call ~5 us, one before the
-  // launch ~3 us: profiles/r03/e2, e4 small_launch.json)
-  if (const hipError_t q = hipStreamQuery(c.stream); q != hipSuccess && q != hipErrorNotReady)
-    return fail(HDFS_CRC32C_EHIP, "earlier work on the stream: %s", hipGetErrorString(q));
+  // caller's: while work nobody has seen complete is queued before this
+  // call's kernel (c.unconfirmed), one query while the kernel is in flight,
+  // so the runtime's bookkeeping of the previous dispatch overlaps the wait
+  // (a query after the completion word cost every call ~5 us, one before
+  // the launch ~3 us: profiles/r03/e2, e4 small_launch.json)
+  if (c.unconfirmed.load(std::memory_order_acquire)) {
+    if (kDiag) c.stream_queries++;
+    if (const hipError_t q = hipStreamQuery(c.stream); q != hipSuccess && q != hipErrorNotReady)
+      return fail(HDFS_CRC32C_EHIP, "earlier work on the stream: %s", hipGetErrorString(q));
+  }
   const auto t0 = std::chrono::steady_clock::now();
   for (uint32_t spin = 1;; spin++) {
     if (__atomic_load_n(&c.h_small_out[2], __ATOMIC_ACQUIRE) == seq) {
       // the sequence number is the kernel's last memory operation: a fault of
-      // this launch cannot be followed by it (earlier work: queried above)
+      // this launch cannot be followed by it, and everything queued before
+      // it has completed
+      c.unconfirmed.store(false, std::memory_order_release);
       if (g_small_trace) {  // diagnostic: host launch / wait time, kernel phase stamps (10 ns ticks)
         const auto t1 = std::chrono::steady_clock::now();
         const uint32_t *m = c.h_small_out;
@@ -1032,6 +1038,7 @@ int hdfs_crc32c_plan_execute(hdfs_crc32c_plan *p, void *stream) {
   DevCtx &c = g_ctx[p->dev];
   DeviceGuard g(p->dev);
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : c.stream;
+  if (st == c.stream) c.unconfirmed.store(true, std::memory_order_release);  // the next synchronous call checks it
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (p->timing && p->rounds) {
     if (p->next_event == p->events.size()) {  // pool exhausted: grow (outside any timed loop
@@ -1496,6 +1503,15 @@ int hdfs_crc32c_diag_device_checks(uint32_t *out3, int reset) {
 int hdfs_crc32c_set_store_policy(int policy) {
   if (policy < 0 || policy > 28) return fail(HDFS_CRC32C_EINVAL, "store policy 0..28");
   g_store_policy = uint32_t(policy);
+  return HDFS_CRC32C_OK;
+}
+
+int hdfs_crc32c_diag_stream_queries(uint64_t *out) {
+  DevCtx *c = nullptr;
+  int rc = ctx_init(-1, &c);
+  if (rc) return rc;
+  if (!out) return fail(HDFS_CRC32C_EINVAL, "null out");
+  *out = c->stream_queries;
   return HDFS_CRC32C_OK;
 }
 

@@ -154,6 +154,14 @@ struct DevCtx {
   uint8_t *stage_vram = nullptr;
   uint32_t *h_small_out = nullptr, *dv_small_out = nullptr;
   uint32_t small_seq = 0;
+  // Work enqueued on `stream` whose completion no call has observed (an
+  // asynchronous plan execute): the next synchronous call queries the
+  // stream for a fault of it; a call that sees its own completion word
+  // clears it (its kernel ran after everything before it, which therefore
+  // completed: a fault stops the stream).  Back-to-back synchronous calls
+  // skip the query (~2 us per launch-path call, profiles/r03/e8).
+  std::atomic<bool> unconfirmed{false};
+  uint64_t stream_queries = 0;  // diagnostic build: queries made (hdfs_crc32c_diag_stream_queries)
   // device CRC scratch of chunk_crcs_to_host (guarded by mu)
   void *d_crc_scratch = nullptr;
   uint64_t crc_scratch_cap = 0;

@@ -596,9 +596,13 @@ int small_run(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
   HIPCHK(launch_small_run(d, len, count, proto, cs, ctype, verify ? 1 : 0, c.d_tab_main_t[tset], c.d_tab_pow2_t[tset],
                           co.dst, co.cap, co.win ? 1 : 0, co.client_offset, c.sr_hd, seq, c.stream));
   // a fault of earlier work on the stream is this call's error, not the next
-  // caller's: queried while the kernel is in flight (as small_call)
-  if (const hipError_t q = hipStreamQuery(c.stream); q != hipSuccess && q != hipErrorNotReady)
-    return fail(HDFS_CRC32C_EHIP, "earlier work on the stream: %s", hipGetErrorString(q));
+  // caller's: queried while the kernel is in flight when unconfirmed work
+  // is queued before it (as small_call)
+  if (c.unconfirmed.load(std::memory_order_acquire)) {
+    if (kDiag) c.stream_queries++;
+    if (const hipError_t q = hipStreamQuery(c.stream); q != hipSuccess && q != hipErrorNotReady)
+      return fail(HDFS_CRC32C_EHIP, "earlier work on the stream: %s", hipGetErrorString(q));
+  }
   auto word = [&](uint32_t k, int i) -> const uint32_t * {
     return reinterpret_cast<const uint32_t *>(c.sr_h + size_t(k) * kSrSlot + kGridRecBytes) + i;
   };
@@ -617,7 +621,9 @@ int small_run(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
     }
   }
   // every slot is published (each workgroup's sequence word is its last
-  // memory operation, so a fault of this launch cannot be followed by it)
+  // memory operation, so a fault of this launch cannot be followed by it;
+  // and everything queued before the launch has completed)
+  c.unconfirmed.store(false, std::memory_order_release);
   // the run: grid points up to the first that is not On (grid_build_kernel's rule)
   auto rec = [&](uint32_t k) {
     hdfs_crc32c_packet r;

@@ -84,6 +84,10 @@ int hdfs_crc32c_set_speculation(int on);
  * eligible (packet 0 starts a run of equal packets), taken (no header off
  * the prediction), header exceptions}; reset != 0 clears them. */
 int hdfs_crc32c_diag_spec_stats(uint64_t *out4, int reset);
+/* Stream queries the synchronous calls made so far (a fault check of
+ * earlier work on the engine stream, made only while work no call has seen
+ * complete -- an asynchronous plan execute -- is queued before them). */
+int hdfs_crc32c_diag_stream_queries(uint64_t *out);
 /* Device checks: the framing kernels (frame_build, header_window, small_run,
  * grid_finalize) test, in this build, the invariants
  * behind each address they touch (a record slot inside its pass, a packet's bytes inside
