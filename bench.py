@@ -419,6 +419,31 @@ def main():
         except (ImportError, OSError) as e:
             extra["ceiling_error"] = str(e)[:200]
 
+    # C4 strong scaling predicted on one GPU: the verify
+    # kernel time of the whole 64 GiB workload (512 blocks) and of one rank's
+    # shard at 2 / 4 / 8 ranks (256 / 128 / 64 blocks), same process; the
+    # speed-up bound at N ranks is T(512) / T(512 / N) -- independent chunks,
+    # no exchange (src/datanode.c:2945-2954), so launch ramp and tail are
+    # what the shard size changes.
+    if d.world == 1 and not args.no_extra and B >= 64:
+        shard_ms = {}
+        for nb in (512, 256, 128, 64):
+            if nb > B:
+                continue
+            sp = h.Plan(h.MODE_VERIFY, segs(lambda g: cs, crcs.ptr, bms.ptr)[:nb])
+            sp.execute(stream)
+            h.stream_sync(stream)
+            sp.set_timing(10)
+            for _ in range(10):
+                sp.execute(stream)
+            k_ms, k_n = sp.kernel_ms()
+            sp.destroy()
+            shard_ms[nb] = k_ms / k_n
+        extra["c4_shard_ms"] = {f"blocks_{k}": round(v, 3) for k, v in shard_ms.items()}
+        if 512 in shard_ms:
+            extra["c4_speedup_bound"] = {f"{g}gpu": round(shard_ms[512] / shard_ms[512 // g], 3)
+                                         for g in (2, 4, 8) if 512 // g in shard_ms}
+
     tot_bytes, tot_mism, ok, t_max = d.aggregate(B * BLOCK * args.steps, m, parity_ok, elapsed)
     n = d.world
 
@@ -477,8 +502,29 @@ def main():
                        "pci_bus_ids": [i["pci_bus_id"] for i in infos]},
             "extra": extra,
         }
+        if n == 1 and not args.no_extra:
+            # the packet-stream path on HBM-resident runs (1 GiB, one 128 MiB
+            # block) beside a plan over the same packets, and the host-resident
+            # rates (the datanode's socket buffers are host memory: PCIe-bound)
+            sys.path.insert(0, os.path.join(ROOT, "tools"))
+            try:
+                import device_stream_bench
+                extra["device_stream"] = device_stream_bench.block_and_run(plan_GiBps=gib_s)
+            except Exception as e:  # reported, never fatal to the headline line
+                extra["device_stream_error"] = repr(e)[:300]
+            try:
+                import h2d_bench
+                hr = h2d_bench.measure(8 << 30, (64,), 3)
+                if "device_stream" in extra:
+                    hr["packets_1GiB_pinned_GiBps"] = extra["device_stream"]["run_1GiB"].get("host_pinned_GiBps")
+                extra["host_resident"] = hr
+            except Exception as e:
+                extra["host_resident_error"] = repr(e)[:300]
         if n == 1 and not args.no_cpu:
             line["cpu_baseline"] = cpu_baseline(args.cpu_gib)
+            if "host_resident" in extra:
+                extra["host_resident"]["vs_cpu_baseline"] = round(
+                    extra["host_resident"]["pinned_verify_GiBps_piece64MiB"] / line["cpu_baseline"]["value"], 3)
         print(json.dumps(line), flush=True)
     d.close()
 

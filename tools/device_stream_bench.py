@@ -25,14 +25,17 @@ sys.path.insert(0, ROOT)
 import hadoofus_amd as h  # noqa: E402
 
 SPEC_AB = os.environ.get("DSB_SPEC_AB", "0") not in ("", "0")
-if os.environ.get("DSB_LIB"):  # another build of the library (A/B of a change, same box)
-    lib = h.load(os.environ["DSB_LIB"])
-elif os.environ.get("DSB_DIAG", "0") not in ("", "0") or SPEC_AB:  # the diagnostic build
-    sys.path.insert(0, os.path.join(ROOT, "tools"))
-    import diaglib  # noqa: E402
-    lib = h.abi.bind_diag(h.load(diaglib.DIAG_LIB_PATH))
-else:
-    lib = h.load()
+lib = None  # the library the calls go through (main(), or block_and_run() for bench.py)
+
+
+def _load():
+    if os.environ.get("DSB_LIB"):  # another build of the library (A/B of a change, same box)
+        return h.load(os.environ["DSB_LIB"])
+    if os.environ.get("DSB_DIAG", "0") not in ("", "0") or SPEC_AB:  # the diagnostic build
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import diaglib
+        return h.abi.bind_diag(h.load(diaglib.DIAG_LIB_PATH))
+    return h.load()
 
 
 def wire_image(nbytes, seed, empty_last=False):
@@ -122,67 +125,103 @@ def run_size(out, key, img, npk_data, npk_all, reps):
     return dev
 
 
-out = {}
-N = 1 << 30
-img, npk = wire_image(N, 7)
-payload = npk * 65536
-dev = run_size(out, "run_1GiB", img, npk, npk, 5)
-dst = h.DeviceBuffer(payload)
-t_copy, rc, _ = timed(dev.ptr, img.nbytes, npk, dst=dst)
-assert rc == 0
-# the copied-out payload is the de-framed data, byte for byte
-H0 = img.nbytes // npk - 65536
-want = img.reshape(npk, H0 + 65536)[:, H0:].reshape(-1)
-copy_ok = bool(np.array_equal(dst.download(), want))
-# ceiling for verify + copy-out: a plain device-to-device copy of the same
-# payload bytes (hipMemcpy D2D: one read and one write of HBM, no CRC work)
-best_cp = 1e9
-for _ in range(5):
+def block_and_run(plan_GiBps=None):
+    """bench.py's extra.device_stream: the 1 GiB run and one 128 MiB block,
+    end to end per call, beside a verify plan over the same packets (same
+    size, same process); plan_GiBps: the headline plan rate to compare with
+    too.  The product library."""
+    global lib
+    lib = h.load()
+    out = {}
+    img, npk = wire_image(1 << 30, 7)
+    dev = run_size(out, "run_1GiB", img, npk, npk, 5)
+    dev.free()
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import h2d_bench
+    out["run_1GiB"]["host_pinned_GiBps"] = h2d_bench.packets_pinned(img, npk)
+    del img
+    blk, nblk = wire_image(128 << 20, 9, empty_last=True)
+    dev = run_size(out, "block_128MiB", blk, 2048, nblk, 10)
+    dev.free()
+    if plan_GiBps:
+        for k in ("run_1GiB", "block_128MiB"):
+            out[k]["frac_of_headline"] = round(out[k]["GiBps"] / plan_GiBps, 3)
+    out["note"] = ("hdfs_crc32c_verify_packets on v2 packet runs resident in HBM (64 KiB packets, 512 B chunks, "
+                   "CRC32C), C call, records to host, best of N; plan_* = a verify plan over the same packets' "
+                   "segments (table given), frac_of_plan = plan time / call time at the same size; "
+                   "frac_of_headline = call rate / this run's C3 rate; host_pinned = the same run in pinned "
+                   "host memory (H2D pipeline)")
+    return out
+
+
+def main():
+    global lib
+    lib = _load()
+    out = {}
+    N = 1 << 30
+    img, npk = wire_image(N, 7)
+    payload = npk * 65536
+    dev = run_size(out, "run_1GiB", img, npk, npk, 5)
+    dst = h.DeviceBuffer(payload)
+    t_copy, rc, _ = timed(dev.ptr, img.nbytes, npk, dst=dst)
+    assert rc == 0
+    # the copied-out payload is the de-framed data, byte for byte
+    H0 = img.nbytes // npk - 65536
+    want = img.reshape(npk, H0 + 65536)[:, H0:].reshape(-1)
+    copy_ok = bool(np.array_equal(dst.download(), want))
+    # ceiling for verify + copy-out: a plain device-to-device copy of the same
+    # payload bytes (hipMemcpy D2D: one read and one write of HBM, no CRC work)
+    best_cp = 1e9
+    for _ in range(5):
+        h.device_sync()
+        t0 = time.perf_counter()
+        assert lib.hdfs_crc32c_memcpy(dst.ptr, dev.ptr, payload, 2) == 0
+        h.device_sync()
+        best_cp = min(best_cp, time.perf_counter() - t0)
+    out["d2d_copy_GiBps"] = round(payload / best_cp / 2**30, 1)
+    pin = h.PinnedBuffer(img.nbytes)
+    pin.array[:] = img
+    t_parse, rc, _ = timed(dev.ptr, img.nbytes, npk, fn="hdfs_crc32c_parse_packets")
+    assert rc == 0
+    t_hparse, rc, _ = timed(pin.ptr, img.nbytes, npk, fn="hdfs_crc32c_parse_packets")
+    assert rc == 0
+    t_pin, rc, _ = timed(pin.ptr, img.nbytes, npk, reps=3)
+    assert rc == 0
+    out.update(packets=npk, wire_bytes=int(img.nbytes), device_GiBps=out["run_1GiB"]["GiBps"],
+               device_ms=round(out["run_1GiB"]["us"] / 1e3, 3), device_parse_ms=round(t_parse * 1e3, 3),
+               host_parse_ms=round(t_hparse * 1e3, 3), pinned_GiBps=round(payload / t_pin / 2**30, 1),
+               device_copy_GiBps=round(payload / t_copy / 2**30, 1), device_copy_ms=round(t_copy * 1e3, 3),
+               copy_bytes_exact=copy_ok)
+    pin.free()
+    # one flipped bit per 1000th packet: verdicts come back for exactly those
+    flips = list(range(5, npk, 1000))
+    H = img.nbytes // npk - 65536
+    bad_img = img.copy()
+    for k in flips:
+        bad_img[k * (H + 65536) + H + 100] ^= 1
+    dev.upload(bad_img)
     h.device_sync()
-    t0 = time.perf_counter()
-    assert lib.hdfs_crc32c_memcpy(dst.ptr, dev.ptr, payload, 2) == 0
+    t_bad, rc, arr = timed(dev.ptr, img.nbytes, npk)
+    assert rc == 29 and [i for i in range(npk) if arr[i].error] == flips
+    assert all(arr[i].first_bad == 0 and arr[i].bad_chunks == 1 for i in flips)
+    out["device_corrupt_ms"] = round(t_bad * 1e3, 3)
+    dev.upload(img)
     h.device_sync()
-    best_cp = min(best_cp, time.perf_counter() - t0)
-out["d2d_copy_GiBps"] = round(payload / best_cp / 2**30, 1)
-pin = h.PinnedBuffer(img.nbytes)
-pin.array[:] = img
-t_parse, rc, _ = timed(dev.ptr, img.nbytes, npk, fn="hdfs_crc32c_parse_packets")
-assert rc == 0
-t_hparse, rc, _ = timed(pin.ptr, img.nbytes, npk, fn="hdfs_crc32c_parse_packets")
-assert rc == 0
-t_pin, rc, _ = timed(pin.ptr, img.nbytes, npk, reps=3)
-assert rc == 0
-out.update(packets=npk, wire_bytes=int(img.nbytes), device_GiBps=out["run_1GiB"]["GiBps"],
-           device_ms=round(out["run_1GiB"]["us"] / 1e3, 3), device_parse_ms=round(t_parse * 1e3, 3),
-           host_parse_ms=round(t_hparse * 1e3, 3), pinned_GiBps=round(payload / t_pin / 2**30, 1),
-           device_copy_GiBps=round(payload / t_copy / 2**30, 1), device_copy_ms=round(t_copy * 1e3, 3),
-           copy_bytes_exact=copy_ok)
-pin.free()
-# one flipped bit per 1000th packet: verdicts come back for exactly those
-flips = list(range(5, npk, 1000))
-H = img.nbytes // npk - 65536
-bad_img = img.copy()
-for k in flips:
-    bad_img[k * (H + 65536) + H + 100] ^= 1
-dev.upload(bad_img)
-h.device_sync()
-t_bad, rc, arr = timed(dev.ptr, img.nbytes, npk)
-assert rc == 29 and [i for i in range(npk) if arr[i].error] == flips
-assert all(arr[i].first_bad == 0 and arr[i].bad_chunks == 1 for i in flips)
-out["device_corrupt_ms"] = round(t_bad * 1e3, 3)
-dev.upload(img)
-h.device_sync()
-# small runs: one 64 KiB packet, and 64 packets (4 MiB)
-for npk_s in (1, 64):
-    n = npk_s * (H + 65536)
-    t, rc, _ = timed(dev.ptr, n, npk_s, reps=20)
-    out[f"device_{npk_s}pkt_us"] = round(t * 1e6, 1)
-    t, rc, _ = timed(dev.ptr, n, npk_s, reps=20, dst=dst)
-    out[f"device_copy_{npk_s}pkt_us"] = round(t * 1e6, 1)
-dst.free()
-dev.free()
-# one 128 MiB HDFS block: 2 048 packets and the empty last packet
-blk, nblk = wire_image(128 << 20, 9, empty_last=True)
-dev = run_size(out, "block_128MiB", blk, 2048, nblk, 10)
-dev.free()
-print(json.dumps(out))
+    # small runs: one 64 KiB packet, and 64 packets (4 MiB)
+    for npk_s in (1, 64):
+        n = npk_s * (H + 65536)
+        t, rc, _ = timed(dev.ptr, n, npk_s, reps=20)
+        out[f"device_{npk_s}pkt_us"] = round(t * 1e6, 1)
+        t, rc, _ = timed(dev.ptr, n, npk_s, reps=20, dst=dst)
+        out[f"device_copy_{npk_s}pkt_us"] = round(t * 1e6, 1)
+    dst.free()
+    dev.free()
+    # one 128 MiB HDFS block: 2 048 packets and the empty last packet
+    blk, nblk = wire_image(128 << 20, 9, empty_last=True)
+    dev = run_size(out, "block_128MiB", blk, 2048, nblk, 10)
+    dev.free()
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
