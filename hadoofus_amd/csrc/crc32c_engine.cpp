@@ -739,12 +739,12 @@ int host_pipeline(int mode, const uint8_t *data, uint64_t len, uint32_t cs, uint
   std::lock_guard<std::mutex> lk(c.mu);
   rc = pipe_reserve(c, piece, cs, npieces);
   if (rc) return rc;
-  // the caller's buffers stay pinned until both streams are drained, on
-  // every return path (an early return drains in the destructor)
-  HostPins hp({c.copy_stream, c.comp_stream});
-  if ((rc = hp.pin({{data, len}, {crcs, nch * 4}, {mode == kModeVerify ? bitmap : nullptr, (nch + 7) / 8}})))
-    return rc;
-  // Per-piece descriptors (uploaded once).
+  // Per-piece descriptors, uploaded once -- BEFORE the caller's buffers are
+  // registered: buffers of one call that share a page are one registration
+  // spanning the bytes between them (crc32c_hostpin.h), and a heap block of
+  // the engine that landed in such a gap would look pinned to the runtime
+  // and be DMA-ed as if it were; no engine heap object is copied
+  // while the call's pins exist.
   std::vector<SegDev> segs(npieces);
   std::vector<uint64_t> rounds(npieces), mt(npieces), gt(npieces);
   for (uint64_t i = 0; i < npieces; i++) {
@@ -760,6 +760,12 @@ int host_pipeline(int mode, const uint8_t *data, uint64_t len, uint32_t cs, uint
     gt[i] = gg;
   }
   HIPCHK(hipMemcpyAsync(c.p_segs, segs.data(), npieces * sizeof(SegDev), hipMemcpyHostToDevice, c.comp_stream));
+  HIPCHK(hipStreamSynchronize(c.comp_stream));  // the pageable source consumed before any pin exists
+  // the caller's buffers stay pinned until both streams are drained, on
+  // every return path (an early return drains in the destructor)
+  HostPins hp({c.copy_stream, c.comp_stream});
+  if ((rc = hp.pin({{data, len}, {crcs, nch * 4}, {mode == kModeVerify ? bitmap : nullptr, (nch + 7) / 8}})))
+    return rc;
   if (mode == kModeVerify) {
     HIPCHK(hipMemsetAsync(c.p_fb, 0xFF, npieces * 4, c.comp_stream));
     HIPCHK(hipMemsetAsync(c.p_mism, 0, 8, c.comp_stream));

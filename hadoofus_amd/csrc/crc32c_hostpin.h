@@ -221,7 +221,10 @@ class PinRegistry {
   size_t page_;
   std::mutex mu_;
   std::map<uintptr_t, Entry> map_;
-  char err_[160] = "";
+  // per thread: a call reads the message its own acquire / release wrote
+  // (a registry-wide buffer read after mu_ was dropped could carry another
+  // thread's message, or a torn one -- ADVICE r3)
+  static inline thread_local char err_[160] = "";
 };
 
 }  // namespace hdfs_crc32c

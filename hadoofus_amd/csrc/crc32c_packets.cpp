@@ -679,6 +679,7 @@ int small_run(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
 // way from the same offset) when packet 0 does not start such a run or a
 // header differs from the prediction.
 struct SpecResult {
+  std::vector<uint32_t> exc_idx;  // records that are not the prediction from packet 0 (exceptions, the tail)
   bool taken = false;     // verified by the speculative launch
   bool end = false;       // the walk ends with this pass
   uint32_t recorded = 0;  // records written to dst
@@ -820,6 +821,7 @@ int spec_pass(DevCtx &c, const uint8_t *d, uint64_t len, uint64_t pos, uint32_t 
     std::memcpy(&x, hx + j, sizeof(x));
     if (x.k >= E.count) return fail(HDFS_CRC32C_EHIP, "speculative verify: exception record %u of %u", x.k, E.count);
     std::memcpy(&dst[x.k], x.rec, sizeof(hdfs_crc32c_packet));
+    res.exc_idx.push_back(x.k);
   }
   if (F.mism) {
     // packets with bad chunks: first bad chunk and count from the bitmap
@@ -857,12 +859,42 @@ int spec_pass(DevCtx &c, const uint8_t *d, uint64_t len, uint64_t pos, uint32_t 
     hdfs_crc32c_packet &t = dst[E.count];
     std::memcpy(&t, F.tail, sizeof(t));
     if (!t.error) res.consumed = run_end + F.tail_total;
+    res.exc_idx.push_back(E.count);
     res.recorded++;
     res.end = true;
   } else if (F.tail_status == kGridMore) {  // the stream ends inside the next packet
     res.end = true;
   }  // kGridOff (another size) / kGridOn (the pass was cut): the walk goes on at run_end
   return HDFS_CRC32C_OK;
+}
+
+// A client read is decided by a packet that ends apply_read_window's walk
+// -- an empty packet, a lastPacketInBlock packet, or one that starts past
+// the read (UNEXPECTED_READ_OFFSET) -- so once a pass holds one, no later
+// pass is framed or verified (a read that ended early kept
+// framing and verifying the rest of the stream, possibly GiBs, only to drop
+// it).
+bool read_stopper(const hdfs_crc32c_packet &r, const CopyOut &co) {
+  if (r.data_len <= 0 || r.last) return true;
+  hdfs_crc32c_packet h = r;
+  h.error = 0;
+  uint32_t cb = 0;
+  return frame::read_avail(h, true, co.client_offset, cb) == 0;
+}
+// Records of a pass predicted from its first packet (offsetInBlock rising by
+// dataLen: avail never falls) but for the exceptions at idx[0, nidx) (all
+// n records when idx is null): only those can hold a stopper.
+bool read_window_over(const hdfs_crc32c_packet *p, size_t n, const CopyOut &co, const uint32_t *idx, size_t nidx) {
+  if (!n) return false;
+  if (!idx) {
+    for (size_t k = 0; k < n; k++)
+      if (read_stopper(p[k], co)) return true;
+    return false;
+  }
+  if (read_stopper(p[0], co) || read_stopper(p[n - 1], co)) return true;
+  for (size_t j = 0; j < nidx; j++)
+    if (idx[j] < n && read_stopper(p[idx[j]], co)) return true;
+  return false;
 }
 
 int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs, int ctype, size_t max_pkts,
@@ -953,11 +985,13 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
                     (unsigned long long)co.cap, (unsigned long long)(payload + sr.payload));
           break;
         }
+        const bool read_over = co.win && read_window_over(dst + n, sr.recorded, co, sr.exc_idx.data(),
+                                                          sr.exc_idx.size());
         n += sr.recorded;
         payload += sr.payload;
         *consumed = sr.consumed;
         last_spec = true;
-        if (sr.end) break;
+        if (sr.end || read_over) break;
         pos = sr.next;
         continue;
       }
@@ -1046,10 +1080,15 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
     }
     t_fill += us_since(tf, clk::now());
     passes.push_back({si, n, S.recorded, verify ? S.nseg : 0u, count, bm_cap, gb.seq});
+    const bool read_over =
+        co.win && read_window_over(dst + n, S.recorded, co,
+                                   S.nexc <= kExcMax ? reinterpret_cast<const uint32_t *>(hg + L.h_sum + kGridHostIdx)
+                                                     : nullptr,
+                                   S.nexc);
     n += S.recorded;
     payload += S.payload;
     *consumed = S.consumed;
-    if (S.last_status == kGridStop || S.last_status == kGridMore) break;
+    if (S.last_status == kGridStop || S.last_status == kGridMore || read_over) break;
     pos = S.next_pos;
     if (S.last_status == kGridOff && S.recorded <= 2) {
       fallback = true;

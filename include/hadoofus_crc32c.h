@@ -351,8 +351,10 @@ int hdfs_crc32c_verify_host(const void *data, uint64_t len, uint32_t chunk_size,
     uint64_t *first_bad, uint64_t *mismatches);
 /* Pinned (page-locked) host memory for zero-copy-staging pipelines. */
 int hdfs_crc32c_host_alloc(void **p, uint64_t bytes);
-/* Only for blocks from hdfs_crc32c_host_alloc (EINVAL otherwise): the engine
- * keeps them in its registry of pinned memory (DMA-ed in place). */
+/* Only for blocks from hdfs_crc32c_host_alloc OF THE SAME LIBRARY (EINVAL
+ * otherwise, and the block stays allocated): each loaded copy of the engine
+ * (the release and the diagnostic build loaded side by side, say) keeps its
+ * own registry of pinned memory (DMA-ed in place). */
 int hdfs_crc32c_host_free(void *p);
 
 /* ---- resident mailbox for the synchronous small calls ------------------- */
