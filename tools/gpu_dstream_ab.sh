@@ -11,7 +11,7 @@ BASE=${2:-build/ab/base/libhadoofus_crc32c.so}
 timeout -k 10 600 python -u -m pytest tests/test_packets.py -m gpu -q -x -p no:cacheprovider --timeout 300 \
   --timeout-method thread > gpurun_out/${TAG}_tests.log 2>&1; rc=$?; tail -2 gpurun_out/${TAG}_tests.log; [ $rc -eq 0 ] || exit $rc
 for i in 1 2; do
-  DSB_OLD_COPY=$([ "${OLD_COPY:-1}" = 1 ] && echo 1) DSB_LIB=$BASE timeout -k 10 300 python tools/device_stream_bench.py > gpurun_out/${TAG}_base$i.json 2>> gpurun_out/${TAG}.err || exit $?
+  DSB_LIB=$BASE timeout -k 10 300 python tools/device_stream_bench.py > gpurun_out/${TAG}_base$i.json 2>> gpurun_out/${TAG}.err || exit $?
   timeout -k 10 300 python tools/device_stream_bench.py > gpurun_out/${TAG}_new$i.json 2>> gpurun_out/${TAG}.err || exit $?
 done
 cat gpurun_out/${TAG}_base*.json gpurun_out/${TAG}_new*.json
