@@ -4,7 +4,8 @@
 # PMC passes, the RCCL path at world 1, the C4 config, device-stream and
 # small-call latency benches.   tools/gpu_evidence.sh TAG ROUND [PARTS]
 # PARTS: any of t (tests + smoke), b (bench + rocprof), p (PMC + torchrun +
-# C4), d (device-stream + small-call benches); default all, one call.
+# C4), d (device-stream + small-call benches), q (SQ/TA/TCP counters of the
+# compute and verify kernels, tools/pmc_sq.py); default tbpd, one call.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
@@ -32,4 +33,6 @@ has d && step dstream timeout -k 10 300 python tools/device_stream_bench.py > ${
 has d && cat ${O}_dstream.json
 has d && step small timeout -k 10 300 python tools/small_launch.py > ${O}_small.json 2> ${O}_small.err
 has d && cat ${O}_small.json
+has q && step pmc_sq timeout -k 10 900 python tools/pmc_sq.py ${O}_pmc_sq.json > /dev/null 2> ${O}_pmc_sq.err
+has q && cat ${O}_pmc_sq.json
 exit 0
