@@ -947,6 +947,23 @@ DEV void copy_round(const uint32_t (&d)[16], const Cursor c, Tab segs, const Lan
   }
 }
 
+// Vector-memory stores process() issues per stream and round, on every path
+// (dropped ones included): the bitmap byte (verify) or the CRC store
+// (compute; the lazy gather also flushes its pending group; the load-only
+// twin's byte), plus four copy stores (COPY).
+template <int MODE, int COPY, int RUN>
+constexpr int round_stores() {
+  return (RUN == 3 ? 2 : 1) + (COPY ? 4 : 0);
+}
+
+// A vector store that writes nothing (a zero-size buffer range): it counts in
+// vmcnt exactly as a dropped store of process() does.
+DEV void pad_store(const void *base) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<uint32_t *>(rfl64(reinterpret_cast<uint64_t>(base))), 0, 0, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b32(0u, r, 0x80000000u, 0, 0);
+}
+
 // Process one round of each of the wave's S streams (d[s] for cursor c[s]);
 // st[s] is stream s's running lane register across the rounds of a tile.
 // The S slicing chains are independent and interleaved step by step, so one
@@ -1403,6 +1420,20 @@ DEV void tiles_run(uint32_t *lds, const Tab sg, const SegDev *__restrict__ segs,
       sha[k][s] = 0u;
       issue<MODE, NT, BUF, UNA, ORDER == 7>(buf[k][s], ex[k][s], tl[k][s], sha[k][s], cur[k][s], sg, L.hsel, L.loff, L.qg, L.lane,
                                 lo, kc[s], L.store_policy);
+    }
+    // In the loop every round's loads are separated from the next round's by
+    // that round's stores; the prologue issues as many empty stores between
+    // its rounds, so the loop head -- where the compiler's vmcnt count merges
+    // the prologue with the back edge -- sees the same number of younger
+    // operations.  Without them the count assumed no stores in flight and the
+    // first two of the three unrolled rounds waited for 2 and 1 operations
+    // more than their own loads (vmcnt(13)/(11)/(10) instead of (15)/(13)/(12)
+    // in verify): the oldest store and the next round's first load, a load
+    // issued one round later than the data being waited for.
+    if (k + 1 < DEPTH) {
+      constexpr int RUN = ORDER == 7 ? 4 : (ORDER == 4 && MODE == kModeCompute) ? 1 : GATHER == 2 ? 3 : GATHER ? 2 : 0;
+#pragma unroll
+      for (int j = 0; j < S * round_stores<MODE, COPY, RUN>(); j++) pad_store(first_bad);
     }
   }
   for (uint32_t it = 0;; it++) {
