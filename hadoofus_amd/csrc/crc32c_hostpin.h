@@ -19,6 +19,11 @@
 //    CRC array that began in the data's registration and ran on into a
 //    second one was refused ("invalid argument") -- and a range that lies
 //    inside a registration another call holds shares it (reference counted).
+//    The merged registration also spans the gap bytes between the merged
+//    buffers (less than a page, not the caller's): an object in
+//    the gap is used in place when it fits inside the registration, and one
+//    that runs on past its end is refused as a partial overlap -- an error
+//    with a message, never a DMA across the end (self-test case 2);
 //    Registrations are NOT widened to whole pages: the runtime looks a
 //    pointer up by the registered byte range, so a page-rounded registration
 //    would capture unrelated heap objects on the same pages (the engine's

@@ -143,6 +143,23 @@ int main() {
     // staging vector) stay outside every registration -- a copy from there
     // must not be taken for a registered one that runs past its end
     CHECK(!rt.in_reg(uintptr_t(buf) + 99) && !rt.in_reg(uintptr_t(buf) + 10478) && !rt.in_reg(uintptr_t(buf)));
+    // the gap between two merged buffers (bytes 6100..6102, not the
+    // caller's) IS inside the registration: an object there is
+    // used in place when it fits inside (one reference more, nothing
+    // registered), and one that runs on past the registration's end is
+    // refused with a message -- never DMA-ed across the end
+    CHECK(rt.in_reg(uintptr_t(buf) + 6100) && rt.in_reg(uintptr_t(buf) + 6102));
+    {
+      PinRegistry::Scope g(reg);
+      const int nreg0 = rt.nreg;
+      CHECK(g.acquire(buf + 6100, 3) == 0);
+      CHECK(rt.nreg == nreg0 && reg.entries()[0].second.refs == 2);
+      PinRegistry::Scope h(reg);
+      CHECK(h.acquire(buf + 6100, 5000) != 0);
+      CHECK(std::strstr(reg.last_error(), "partly overlaps") != nullptr);
+      CHECK(h.held() == 0 && rt.nreg == nreg0);
+    }
+    CHECK(reg.entries().size() == 1 && reg.entries()[0].second.refs == 1);
     CHECK(s.release() == 0);
     CHECK(rt.regs.empty() && reg.entries().empty());
     // buffers on separate pages of one call: separate registrations
