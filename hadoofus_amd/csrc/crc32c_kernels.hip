@@ -2997,70 +2997,6 @@ __global__ __launch_bounds__(1024) void spec_verify_kernel(SpecArgs a) {
   d.seq0 = rfl64(run.seq0);
   if (!d.eligible) return;
   const bool v1 = d.v1 != 0u;
-  // header checks: runs of 64 packets, run j on wave (j / G) % 16 of
-  // workgroup j % G; lane l compares packet 64 j + l (packet 0 is the
-  // prediction itself)
-  {
-    const uint32_t G = gridDim.x;
-    for (uint32_t j = wv * G + blockIdx.x; 64u * j < d.count; j += 16u * G) {
-      const uint64_t p0 = a.base + uint64_t(64u * j) * d.stride;
-      const uint64_t span = a.len - p0;
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-          reinterpret_cast<uint8_t *>(rfl64(reinterpret_cast<uint64_t>(a.s + p0))), 0,
-          static_cast<int>(rfl(span > 0xFFFFFFFFull ? 0xFFFFFFFFu : static_cast<uint32_t>(span))), 0x00020000);
-      const uint32_t k = 64u * j + lane;
-      const uint32_t vo = lane * static_cast<uint32_t>(d.stride);
-      u32x4 h[kSpecHdrBytes / 16];
-#pragma unroll
-      for (int q = 0; q < int(kSpecHdrBytes / 16); q++)
-        h[q] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 16u * q, 0, 0));
-      const uint64_t off = d.off0 + uint64_t(k) * d.dlen, sq = d.seq0 + k;
-      uint32_t e[kSpecHdrBytes / 4];
-      e[0] = spec_hdr_word<0>(win[0], v1, off, sq);
-      e[1] = spec_hdr_word<1>(win[0], v1, off, sq);
-      e[2] = spec_hdr_word<2>(win[0], v1, off, sq);
-      e[3] = spec_hdr_word<3>(win[0], v1, off, sq);
-      e[4] = spec_hdr_word<4>(win[0], v1, off, sq);
-      e[5] = spec_hdr_word<5>(win[0], v1, off, sq);
-      e[6] = spec_hdr_word<6>(win[0], v1, off, sq);
-      e[7] = spec_hdr_word<7>(win[0], v1, off, sq);
-      e[8] = spec_hdr_word<8>(win[0], v1, off, sq);
-      e[9] = spec_hdr_word<9>(win[0], v1, off, sq);
-      e[10] = spec_hdr_word<10>(win[0], v1, off, sq);
-      e[11] = spec_hdr_word<11>(win[0], v1, off, sq);
-      uint32_t diff = 0;
-#pragma unroll
-      for (uint32_t w = 0; w < kSpecHdrBytes / 4; w++) {
-        // bytes of the header only (hl <= 33)
-        const uint32_t m = 4u * w >= d.hl ? 0u : 4u * w + 4u <= d.hl ? 0xFFFFFFFFu : (1u << (8u * (d.hl - 4u * w))) - 1u;
-        diff |= (h[w / 4][w % 4] ^ e[w]) & m;
-      }
-      if (k < d.count && diff != 0u) {
-        // rare: frame the packet as frame_build_kernel would.  Same wire
-        // size and clean: an exception (the run's layout, its own record);
-        // anything else voids the launch
-        hdfs_crc32c_packet r{};
-        uint64_t tot = 0;
-        const uint64_t pos = p0 + vo;
-        const int st = frame::frame_step(a.s + pos, a.len - pos, pos, a.proto, a.cs, a.ctype, r, tot);
-        bool keep = st == frame::kStepNext && !r.error && tot == d.stride &&
-                    (!a.rwin || static_cast<uint64_t>(r.offset_in_block) == off);
-        if (keep) {
-          const uint32_t slot = __hip_atomic_fetch_add(&ctl->nexc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (slot < kSpecExcMax) {
-            SpecExc *x = a.exc + a.parity * kSpecExcMax + slot;
-            const uint64_t *w = reinterpret_cast<const uint64_t *>(&r);
-#pragma unroll
-            for (int q = 0; q < 7; q++) at_st(&x->rec[q], w[q]);
-            at_st32(&x->k, k);
-          } else {
-            keep = false;
-          }
-        }
-        if (!keep) __hip_atomic_fetch_or(&ctl->exc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-  }
   // this workgroup's copy of the closed-form table (read back with scalar
   // loads: written with vector stores, acknowledged before the barrier)
   if (t == 0) {
@@ -3076,12 +3012,94 @@ __global__ __launch_bounds__(1024) void spec_verify_kernel(SpecArgs a) {
     q->pad = 0u;
     stores_done();
   }
+  // header checks: runs of 64 packets, run j on wave (j / G) % 16 of
+  // workgroup j % G; lane l compares packet 64 j + l (packet 0 is the
+  // prediction itself).  A wave's first run is loaded here and compared after
+  // the verify loop: its loads ride ahead of the loop's first rounds instead
+  // of holding every wave of the workgroup at the barrier for a round trip
+  // (a 1 GiB run has one run per workgroup; longer runs load the rest later)
+  const uint32_t G = gridDim.x;
+  const uint32_t j0 = wv * G + blockIdx.x;
+  auto hdr_rsrc = [&](uint32_t j) {
+    const uint64_t p0 = a.base + uint64_t(64u * j) * d.stride;
+    const uint64_t span = a.len - p0;
+    return __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<uint8_t *>(rfl64(reinterpret_cast<uint64_t>(a.s + p0))), 0,
+        static_cast<int>(rfl(span > 0xFFFFFFFFull ? 0xFFFFFFFFu : static_cast<uint32_t>(span))), 0x00020000);
+  };
+  const uint32_t vo = lane * static_cast<uint32_t>(d.stride);
+  u32x4 h0[kSpecHdrBytes / 16];
+  if (64u * j0 < d.count) {
+    const __amdgpu_buffer_rsrc_t rs = hdr_rsrc(j0);
+#pragma unroll
+    for (int q = 0; q < int(kSpecHdrBytes / 16); q++)
+      h0[q] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 16u * q, 0, 0));
+  }
   __syncthreads();
   const SpecTab tab{(const CAS SpecTabData *)(a.tabs + blockIdx.x)};
   const uint64_t tiles = uint64_t(d.count) * d.T;
   tiles_run<kModeVerify, 3, 1, 3, 1, 1024, 1, COPY, 1, 0>(lds, tab, nullptr, d.count, tiles * (a.cs / kRoundBytes),
                                                           tiles, a.fb, &ctl->mism, nullptr, a.tune, &ctl->gctr,
                                                           nullptr, d.T, false);
+  for (uint32_t j = j0; 64u * j < d.count; j += 16u * G) {
+    u32x4 h[kSpecHdrBytes / 16];
+    if (j == j0) {
+#pragma unroll
+      for (int q = 0; q < int(kSpecHdrBytes / 16); q++) h[q] = h0[q];
+    } else {
+      const __amdgpu_buffer_rsrc_t rs = hdr_rsrc(j);
+#pragma unroll
+      for (int q = 0; q < int(kSpecHdrBytes / 16); q++)
+        h[q] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 16u * q, 0, 0));
+    }
+    const uint64_t p0 = a.base + uint64_t(64u * j) * d.stride;
+    const uint32_t k = 64u * j + lane;
+    const uint64_t off = d.off0 + uint64_t(k) * d.dlen, sq = d.seq0 + k;
+    uint32_t e[kSpecHdrBytes / 4];
+    e[0] = spec_hdr_word<0>(win[0], v1, off, sq);
+    e[1] = spec_hdr_word<1>(win[0], v1, off, sq);
+    e[2] = spec_hdr_word<2>(win[0], v1, off, sq);
+    e[3] = spec_hdr_word<3>(win[0], v1, off, sq);
+    e[4] = spec_hdr_word<4>(win[0], v1, off, sq);
+    e[5] = spec_hdr_word<5>(win[0], v1, off, sq);
+    e[6] = spec_hdr_word<6>(win[0], v1, off, sq);
+    e[7] = spec_hdr_word<7>(win[0], v1, off, sq);
+    e[8] = spec_hdr_word<8>(win[0], v1, off, sq);
+    e[9] = spec_hdr_word<9>(win[0], v1, off, sq);
+    e[10] = spec_hdr_word<10>(win[0], v1, off, sq);
+    e[11] = spec_hdr_word<11>(win[0], v1, off, sq);
+    uint32_t diff = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kSpecHdrBytes / 4; w++) {
+      // bytes of the header only (hl <= 33)
+      const uint32_t m = 4u * w >= d.hl ? 0u : 4u * w + 4u <= d.hl ? 0xFFFFFFFFu : (1u << (8u * (d.hl - 4u * w))) - 1u;
+      diff |= (h[w / 4][w % 4] ^ e[w]) & m;
+    }
+    if (k < d.count && diff != 0u) {
+      // rare: frame the packet as frame_build_kernel would.  Same wire
+      // size and clean: an exception (the run's layout, its own record);
+      // anything else voids the launch
+      hdfs_crc32c_packet r{};
+      uint64_t tot = 0;
+      const uint64_t pos = p0 + vo;
+      const int st = frame::frame_step(a.s + pos, a.len - pos, pos, a.proto, a.cs, a.ctype, r, tot);
+      bool keep = st == frame::kStepNext && !r.error && tot == d.stride &&
+                  (!a.rwin || static_cast<uint64_t>(r.offset_in_block) == off);
+      if (keep) {
+        const uint32_t slot = __hip_atomic_fetch_add(&ctl->nexc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (slot < kSpecExcMax) {
+          SpecExc *x = a.exc + a.parity * kSpecExcMax + slot;
+          const uint64_t *w = reinterpret_cast<const uint64_t *>(&r);
+#pragma unroll
+          for (int q = 0; q < 7; q++) at_st(&x->rec[q], w[q]);
+          at_st32(&x->k, k);
+        } else {
+          keep = false;
+        }
+      }
+      if (!keep) __hip_atomic_fetch_or(&ctl->exc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
   // every wave's stores and atomics (mismatch count, exception flag) are
   // acknowledged before its workgroup counts itself done; the last
   // workgroup then reads the counters and publishes the final block
