@@ -526,6 +526,7 @@ int small_call(DevCtx &c, int mode, uint32_t len, uint32_t cs, uint32_t reg0, bo
   // a VRAM stage is write-combining: drain it before the launch
   if (c.stage_vram) __builtin_ia32_sfence();
   const uint32_t seq = ++c.small_seq;
+  const uint64_t epoch = c.queued_epoch.load(std::memory_order_acquire);  // before the launch
   const auto tl = std::chrono::steady_clock::now();
   HIPCHK(launch_small_chunks(mode, dsrc ? dsrc : c.dv_small_in, len, dsrc ? 1u : 0u, cs, reg0, be ? 1u : 0u,
                              reinterpret_cast<const uint32_t *>(c.dv_small_in + kSmallMax), c.d_tab_main_t[ctype],
@@ -533,11 +534,11 @@ int small_call(DevCtx &c, int mode, uint32_t len, uint32_t cs, uint32_t reg0, bo
                              c.dv_small_out + kSmallMeta, seq, c.stream));
   // a fault of EARLIER work on the stream is this call's error, not the next
   // caller's: while work nobody has seen complete is queued before this
-  // call's kernel (c.unconfirmed), one query while the kernel is in flight,
+  // call's kernel (c.unconfirmed()), one query while the kernel is in flight,
   // so the runtime's bookkeeping of the previous dispatch overlaps the wait
   // (a query after the completion word cost every call ~5 us, one before
   // the launch ~3 us: profiles/r03/e2, e4 small_launch.json)
-  if (c.unconfirmed.load(std::memory_order_acquire)) {
+  if (c.unconfirmed()) {
     if (kDiag) c.stream_queries++;
     if (const hipError_t q = hipStreamQuery(c.stream); q != hipSuccess && q != hipErrorNotReady)
       return fail(HDFS_CRC32C_EHIP, "earlier work on the stream: %s", hipGetErrorString(q));
@@ -548,7 +549,7 @@ int small_call(DevCtx &c, int mode, uint32_t len, uint32_t cs, uint32_t reg0, bo
       // the sequence number is the kernel's last memory operation: a fault of
       // this launch cannot be followed by it, and everything queued before
       // it has completed
-      c.unconfirmed.store(false, std::memory_order_release);
+      c.confirm(epoch);
       if (g_small_trace) {  // diagnostic: host launch / wait time, kernel phase stamps (10 ns ticks)
         const auto t1 = std::chrono::steady_clock::now();
         const uint32_t *m = c.h_small_out;
@@ -1044,7 +1045,6 @@ int hdfs_crc32c_plan_execute(hdfs_crc32c_plan *p, void *stream) {
   DevCtx &c = g_ctx[p->dev];
   DeviceGuard g(p->dev);
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : c.stream;
-  if (st == c.stream) c.unconfirmed.store(true, std::memory_order_release);  // the next synchronous call checks it
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (p->timing && p->rounds) {
     if (p->next_event == p->events.size()) {  // pool exhausted: grow (outside any timed loop
@@ -1057,8 +1057,12 @@ int hdfs_crc32c_plan_execute(hdfs_crc32c_plan *p, void *stream) {
     e1 = p->events[p->next_event].second;
     p->next_event++;
   }
-  return launch_all(c, p->mode, p->d_segs, p->nseg, p->rounds, p->mtiles, p->gtiles, p->d_first_bad,
-                    p->d_mism, p->d_gctr, st, e0, e1, true, p->ctype, false, false, p->una, p->utiles, p->runs);
+  const int rc = launch_all(c, p->mode, p->d_segs, p->nseg, p->rounds, p->mtiles, p->gtiles, p->d_first_bad,
+                            p->d_mism, p->d_gctr, st, e0, e1, true, p->ctype, false, false, p->una, p->utiles, p->runs);
+  // after the enqueue (failed or not: part of it may be queued), so a
+  // synchronous call that read the old epoch cannot confirm this work
+  if (st == c.stream) c.queued_epoch.fetch_add(1, std::memory_order_acq_rel);
+  return rc;
 }
 
 int hdfs_crc32c_plan_results(hdfs_crc32c_plan *p, void *stream, uint32_t *first_bad, size_t nseg,

@@ -156,11 +156,24 @@ struct DevCtx {
   uint32_t small_seq = 0;
   // Work enqueued on `stream` whose completion no call has observed (an
   // asynchronous plan execute): the next synchronous call queries the
-  // stream for a fault of it; a call that sees its own completion word
-  // clears it (its kernel ran after everything before it, which therefore
-  // completed: a fault stops the stream).  Back-to-back synchronous calls
-  // skip the query (~2 us per launch-path call, profiles/r03/e8).
-  std::atomic<bool> unconfirmed{false};
+  // stream for a fault of it.  Epochs, not a flag (a plan
+  // enqueued by another thread after a synchronous call's launch must stay
+  // unconfirmed when that call completes): plan_execute bumps queued_epoch
+  // AFTER its enqueue; a synchronous call reads queued_epoch BEFORE its
+  // launch and, once it sees its own completion word, raises confirmed_epoch
+  // to that value -- its kernel ran after everything enqueued before the
+  // read, which therefore completed (a fault stops the stream).
+  // Back-to-back synchronous calls skip the query (~2 us per launch-path
+  // call, profiles/r03/e8).
+  std::atomic<uint64_t> queued_epoch{0}, confirmed_epoch{0};
+  bool unconfirmed() const {
+    return queued_epoch.load(std::memory_order_acquire) != confirmed_epoch.load(std::memory_order_acquire);
+  }
+  void confirm(uint64_t e) {
+    uint64_t cur = confirmed_epoch.load(std::memory_order_acquire);
+    while (cur < e && !confirmed_epoch.compare_exchange_weak(cur, e, std::memory_order_acq_rel)) {
+    }
+  }
   uint64_t stream_queries = 0;  // diagnostic build: queries made (hdfs_crc32c_diag_stream_queries)
   // device CRC scratch of chunk_crcs_to_host (guarded by mu)
   void *d_crc_scratch = nullptr;

@@ -3076,14 +3076,18 @@ __global__ __launch_bounds__(1024) void spec_verify_kernel(SpecArgs a) {
       diff |= (h[w / 4][w % 4] ^ e[w]) & m;
     }
     if (k < d.count && diff != 0u) {
-      // rare: frame the packet as frame_build_kernel would.  Same wire
-      // size and clean: an exception (the run's layout, its own record);
-      // anything else voids the launch
+      // rare: frame the packet as frame_build_kernel would.  Clean and in
+      // the run's layout -- same header length, dataLen and CRC length, so
+      // its CRCs and data sit where the closed-form table puts them (the
+      // same wire size alone is not enough: a 27-B syncBlock header with
+      // dataLen cut by 2 has packet 0's stride) -- an exception with its own
+      // record; anything else voids the launch
       hdfs_crc32c_packet r{};
       uint64_t tot = 0;
       const uint64_t pos = p0 + vo;
       const int st = frame::frame_step(a.s + pos, a.len - pos, pos, a.proto, a.cs, a.ctype, r, tot);
-      bool keep = st == frame::kStepNext && !r.error && tot == d.stride &&
+      bool keep = st == frame::kStepNext && !r.error && tot == d.stride && r.header_len == d.hl &&
+                  static_cast<uint32_t>(r.data_len) == d.dlen && static_cast<uint32_t>(r.crc_len) == d.crc_len &&
                   (!a.rwin || static_cast<uint64_t>(r.offset_in_block) == off);
       if (keep) {
         const uint32_t slot = __hip_atomic_fetch_add(&ctl->nexc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

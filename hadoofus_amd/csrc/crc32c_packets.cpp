@@ -593,12 +593,13 @@ int small_run(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
   const uint32_t count = uint32_t(std::min<uint64_t>({uint64_t(kSmallRunMax), uint64_t(max_pkts), len / 6 + 1}));
   const uint32_t seq = next_grid_seq(c);
   const int tset = ctype == HDFS_CRC32C_CSUM_CRC32 ? 1 : 0;
+  const uint64_t epoch = c.queued_epoch.load(std::memory_order_acquire);  // before the launch
   HIPCHK(launch_small_run(d, len, count, proto, cs, ctype, verify ? 1 : 0, c.d_tab_main_t[tset], c.d_tab_pow2_t[tset],
                           co.dst, co.cap, co.win ? 1 : 0, co.client_offset, c.sr_hd, seq, c.stream));
   // a fault of earlier work on the stream is this call's error, not the next
   // caller's: queried while the kernel is in flight when unconfirmed work
   // is queued before it (as small_call)
-  if (c.unconfirmed.load(std::memory_order_acquire)) {
+  if (c.unconfirmed()) {
     if (kDiag) c.stream_queries++;
     if (const hipError_t q = hipStreamQuery(c.stream); q != hipSuccess && q != hipErrorNotReady)
       return fail(HDFS_CRC32C_EHIP, "earlier work on the stream: %s", hipGetErrorString(q));
@@ -623,7 +624,7 @@ int small_run(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
   // every slot is published (each workgroup's sequence word is its last
   // memory operation, so a fault of this launch cannot be followed by it;
   // and everything queued before the launch has completed)
-  c.unconfirmed.store(false, std::memory_order_release);
+  c.confirm(epoch);
   // the run: grid points up to the first that is not On (grid_build_kernel's rule)
   auto rec = [&](uint32_t k) {
     hdfs_crc32c_packet r;
@@ -1182,84 +1183,74 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
 // The read loop over a walked run, for a client read window
 // (_datanode_read's `while (remains_tot > 0) _recv_packet(...)`,
 // src/datanode.c:1476-1481, through _process_recv_packet and
-// _recv_packet_copy_data, :2448-2456, :2470-2549): packets are taken while
-// the read still wants bytes; an empty last packet then is BAD_LASTPACKET
-// (:2452-2454); after its CRCs are verified, a packet that starts past the
-// read (c_begin >= dataLen) is UNEXPECTED_READ_OFFSET (:2483-2486); a
-// packet delivers min(dataLen - c_begin, remains) bytes, and one flagged
-// lastPacketInBlock that leaves the read short is BAD_LASTPACKET after its
-// bytes are copied (:2545-2546).  The walk stops at the packet that
-// completes the read or raises one of these; records past it are dropped
-// (the reference never reads them).  The destination (co.cap bytes) may be
-// smaller than the read (co.want): once it is full the walk stops with
-// AGAIN (`rlen == 0 && remains_tot > 0`, :2547-2549) -- a packet whose bytes
-// were only partly delivered is dropped from the records and `consumed`
-// ends before it (the caller re-passes it with client_offset advanced, so
-// its new c_begin skips what it delivered: the reference's remains_pkt,
-// :2356-2361).  As in the whole-payload mode, packets after one with bad
-// CRCs keep their own verdicts (the engine reports every packet; the
-// reference stops at the first): the window is a function of the headers
-// only, which is what lets the device place every packet's copy before
-// any verdict is known.  *delivered = the bytes the reference copies before
-// its loop returns an error.  Returns 1 for AGAIN, else 0.
+// _recv_packet_copy_data, :2439-2456, :2470-2549).  The read ends at its
+// first error, as the reference's does:
+//   - a framing error (:2439-2446) or bad CRCs (:2470-2475: bad_crcs, the
+//     loop breaks at :1478 and the call returns BAD_CHECKSUM, :1500-1505):
+//     the packet is recorded, delivers nothing and is not consumed;
+//   - an empty last packet while the read wants bytes is BAD_LASTPACKET
+//     (:2450-2456; its header is consumed);
+//   - a packet that starts past the read (c_begin >= dataLen) is
+//     UNEXPECTED_READ_OFFSET (:2483-2486), not consumed;
+//   - a packet delivers min(dataLen - c_begin, remains) bytes, and one
+//     flagged lastPacketInBlock that leaves the read short is BAD_LASTPACKET
+//     after its bytes are copied (:2545-2546).
+// Records past the packet that ends the read are dropped (the device may have
+// verified them: the window is a function of the headers only, which lets it
+// place every copy before any verdict is known; the reference never reads
+// them), so the result does not depend on how the destination is split.  The
+// destination (co.cap bytes) may be smaller than the read (co.want): once it
+// is full the walk stops with AGAIN (`rlen == 0 && remains_tot > 0`,
+// :2547-2549) -- a packet whose bytes were only partly delivered is dropped
+// from the records and `consumed` ends before it (the caller re-passes it
+// with client_offset advanced, so its new c_begin skips what it delivered:
+// the reference's remains_pkt, :2356-2361).  *delivered = the bytes the
+// reference copies before its loop returns.  Returns 1 for AGAIN, else 0.
 int apply_read_window(hdfs_crc32c_packet *p, size_t &n, uint64_t &consumed, const CopyOut &co,
                       uint64_t *delivered) {
   uint64_t remains = co.want, room = co.cap, got = 0;
-  bool err = false;
   int again = 0;
   for (size_t k = 0; k < n; k++) {
     hdfs_crc32c_packet &r = p[k];
     const uint64_t end = r.stream_off + r.header_len + uint64_t(r.crc_len > 0 ? r.crc_len : 0) +
                          uint64_t(r.data_len > 0 ? r.data_len : 0);
-    const bool crc_bad = r.error == HDFS_CRC32C_ERR_DATANODE_BAD_CHECKSUM;
-    if (r.error && !crc_bad) {  // framing error: the walk ended here
+    if (r.error) {  // framing error or bad CRCs
       n = k + 1;
+      consumed = r.stream_off;
       break;
     }
-    bool stop = false;
     if (r.data_len == 0) {  // the empty last packet (a non-last one is a framing error)
       r.error = HDFS_CRC32C_ERR_DATANODE_BAD_LASTPACKET;
-      stop = true;
-    } else {
-      hdfs_crc32c_packet h = r;
-      h.error = 0;  // the window is a function of the header
-      uint32_t cb = 0;
-      const uint32_t avail = frame::read_avail(h, true, co.client_offset, cb);
-      if (avail == 0) {
-        if (!crc_bad) r.error = HDFS_CRC32C_ERR_DATANODE_UNEXPECTED_READ_OFFSET;
-        stop = true;
-      } else {
-        const uint64_t want = std::min<uint64_t>(avail, remains);  // remains_pkt
-        if (want > room && !crc_bad) {
-          // the destination fills inside this packet: its rest is the next
-          // call's (the reference returns AGAIN here with remains_pkt > 0)
-          if (!err) got += room;
-          n = k;
-          consumed = r.stream_off;
-          again = 1;
-          break;
-        }
-        const uint64_t clen = std::min(want, room);
-        remains -= clen;
-        room -= clen;
-        if (!err && !crc_bad) got += clen;
-        if (r.last && remains > 0) {
-          if (!crc_bad) r.error = HDFS_CRC32C_ERR_DATANODE_BAD_LASTPACKET;
-          stop = true;
-        }
-        stop = stop || remains == 0;
-        if (!stop && room == 0 && !crc_bad) {  // full exactly at this packet's end
-          n = k + 1;
-          consumed = end;
-          again = 1;
-          break;
-        }
-      }
-    }
-    if (r.error) err = true;
-    if (stop) {
       n = k + 1;
       consumed = end;
+      break;
+    }
+    uint32_t cb = 0;
+    const uint32_t avail = frame::read_avail(r, true, co.client_offset, cb);
+    if (avail == 0) {
+      r.error = HDFS_CRC32C_ERR_DATANODE_UNEXPECTED_READ_OFFSET;
+      n = k + 1;
+      consumed = r.stream_off;
+      break;
+    }
+    const uint64_t want = std::min<uint64_t>(avail, remains);  // remains_pkt
+    if (want > room) {
+      // the destination fills inside this packet: its rest is the next
+      // call's (the reference returns AGAIN here with remains_pkt > 0)
+      got += room;
+      n = k;
+      consumed = r.stream_off;
+      again = 1;
+      break;
+    }
+    remains -= want;
+    room -= want;
+    got += want;
+    if (r.last && remains > 0) r.error = HDFS_CRC32C_ERR_DATANODE_BAD_LASTPACKET;
+    if (r.error || remains == 0 || room == 0) {
+      n = k + 1;
+      consumed = end;
+      again = !r.error && remains > 0;  // full exactly at this packet's end
       break;
     }
   }

@@ -230,22 +230,36 @@ int hdfs_crc32c_verify_packets(const void *stream, uint64_t len, int proto, uint
  * reference's iovec array, :2509-2537); total capacity cap = sum of
  * iov[i].len.
  * read_len = HDFS_CRC32C_READ_ALL: every framing-clean packet's whole
- *   payload (iovcnt must be 1); *delivered = payload bytes of the packets
- *   before the first packet with an error; EINVAL if the buffer is too
- *   small for the framed payload.
+ *   payload (iovcnt must be 1): hdfs_crc32c_verify_packets with the payload
+ *   copied -- records for every packet of the run, verdicts past an error
+ *   included; *delivered = payload bytes of the packets before the first
+ *   packet with an error.  This mode has no read position (no client
+ *   offset) to resume from, so a buffer too small for the framed payload is
+ *   a sizing error: EINVAL, nothing written past the buffer (size it from
+ *   hdfs_crc32c_parse_packets, or use a read window, which resumes).
  * read_len > 0: a client read of the block's bytes [client_offset,
  *   client_offset + read_len) (hdfs_datanode_read's bloff / len,
- *   src/datanode.c:1363-1377).  Packets are taken while the read wants
- *   bytes (src/datanode.c:1476): a packet that starts before client_offset
- *   delivers from c_begin = client_offset - offsetInBlock on, and c_begin >=
- *   dataLen is HDFS_CRC32C_ERR_DATANODE_UNEXPECTED_READ_OFFSET
- *   (:2478-2486); a packet delivers at most what is left of the read; a
- *   lastPacketInBlock packet that leaves the read short, or an empty last
- *   packet before it is complete, is HDFS_CRC32C_ERR_DATANODE_BAD_LASTPACKET
- *   (:2452-2454, :2545-2546).  The walk ends with the packet that completes
- *   the read or raises one of those; later packets are not returned.
- *   *delivered = the bytes the reference copies to the caller before its
- *   loop returns an error (a BAD_LASTPACKET packet's own bytes included).
+ *   src/datanode.c:1363-1377), the reference's read loop
+ *   (src/datanode.c:1476-1481).  Packets are taken while the read wants
+ *   bytes.  The read ENDS AT ITS FIRST ERROR, which is the call's return
+ *   value and its last record:
+ *     - a framing error, or bad CRCs (HDFS_CRC32C_ERR_DATANODE_BAD_CHECKSUM:
+ *       the reference stops its loop there, :1476-1479, :2470-2475): the
+ *       packet delivers nothing and *consumed ends before it;
+ *     - c_begin = client_offset - offsetInBlock >= dataLen:
+ *       HDFS_CRC32C_ERR_DATANODE_UNEXPECTED_READ_OFFSET (:2478-2486), *consumed
+ *       ends before the packet;
+ *     - a lastPacketInBlock packet that leaves the read short (after its
+ *       bytes are delivered), or an empty last packet before the read is
+ *       complete: HDFS_CRC32C_ERR_DATANODE_BAD_LASTPACKET (:2452-2454,
+ *       :2545-2546), *consumed ends after it.
+ *   A packet that starts before client_offset delivers from c_begin on; a
+ *   packet delivers at most what is left of the read.  Without an error the
+ *   walk ends with the packet that completes the read; later packets are
+ *   not returned.  *delivered = the bytes the reference copies to the
+ *   caller before its loop returns (a BAD_LASTPACKET packet's own bytes
+ *   included).  Records, *consumed, *delivered and the status do not depend
+ *   on how the destination is split.
  *   A destination smaller than the rest of the read is RESUMABLE, as the
  *   reference's read is (`rlen == 0 && remains_tot > 0` -> HDFS_AGAIN,
  *   :2547-2549, re-entered with remains_pkt > 0, :2356-2361): once the
@@ -255,12 +269,13 @@ int hdfs_crc32c_verify_packets(const void *stream, uint64_t len, int proto, uint
  *   by the call that completes it), or the end of the last packet if the
  *   buffers filled exactly there.  The caller continues with stream +
  *   consumed, client_offset + delivered and read_len - delivered: the
- *   re-passed packet then delivers from its new c_begin on.
- * Packets after one with bad CRCs are still verified and reported (as in
- * hdfs_crc32c_verify_packets); bytes of the buffers past *delivered are
- * unspecified, bytes past them (or past the read) are never written.  ctype
- * must be CRC32 or CRC32C.  Returns the first error in stream order, 0,
- * HDFS_CRC32C_AGAIN, or a negative status. */
+ *   re-passed packet then delivers from its new c_begin on.  (Bad CRCs in a
+ *   packet that would overflow the buffers end the read: the reference
+ *   verifies a packet before it copies any of it.)
+ * Bytes of the buffers past *delivered are unspecified, bytes past them (or
+ * past the read) are never written.  ctype must be CRC32 or CRC32C.
+ * Returns the error that ended the read (READ_ALL: the first error in stream
+ * order), 0, HDFS_CRC32C_AGAIN, or a negative status. */
 #define HDFS_CRC32C_READ_ALL (-1)
 /* Not an error: the destination filled before the read completed (the
  * reference's HDFS_AGAIN); outside the range of the datanode errors. */

@@ -669,29 +669,41 @@ int oracle_verify_packets(const uint8_t *s, uint64_t len, int proto, uint32_t cs
  * `while (remains_tot > 0) _recv_packet(...)` (src/datanode.c:1476-1481)
  * through _process_recv_packet and _recv_packet_copy_data
  * (src/datanode.c:2428-2549) for the block bytes [client_offset,
- * client_offset + read_len): an empty last packet while bytes are still
- * wanted is BAD_LASTPACKET (:2452-2454); after the packet's CRCs are
- * verified, c_begin = client_offset - offsetInBlock (0 when the packet
- * starts later) >= dataLen is UNEXPECTED_READ_OFFSET (:2478-2486); the
- * packet then gives min(dataLen - c_begin, remains) bytes from c_begin on
- * (:2488, :2527-2540), and a lastPacketInBlock packet that leaves the read
- * short is BAD_LASTPACKET (:2545-2546).  The loop ends when the read is
- * complete or at one of those errors.  As the engine's packet API does, a
- * packet with bad CRCs does not end the walk (its verdict is recorded, its
- * bytes and every later packet's are not delivered: the reference returns
- * there); c_begin is computed in 64 bits (the reference's int32_t differs
- * only for client_offset - offsetInBlock >= 2^31).  dst receives the
- * delivered bytes; returns the first error in stream order. */
+ * client_offset + read_len), into a destination of cap bytes
+ * (UINT64_MAX: as large as the read).  Per packet, in the reference's order:
+ *   - a framing error ends the read (:2439-2446);
+ *   - an empty last packet while bytes are still wanted is BAD_LASTPACKET
+ *     (:2450-2456; its header is consumed, :2455);
+ *   - bad CRCs end the read (:2470-2475 set bad_crcs, the loop breaks on it
+ *     at :1478, the call returns BAD_CHECKSUM at :1500-1505): the packet is
+ *     recorded, none of its bytes are delivered and it is not consumed;
+ *   - c_begin = client_offset - offsetInBlock (0 when the packet starts
+ *     later) >= dataLen is UNEXPECTED_READ_OFFSET (:2478-2486), not consumed;
+ *   - the packet gives min(dataLen - c_begin, remains) bytes from c_begin on
+ *     (:2488, :2507-2542); a lastPacketInBlock packet that leaves the read
+ *     short is BAD_LASTPACKET after its bytes are copied (:2545-2546);
+ *   - a destination that fills before the read is complete returns AGAIN
+ *     (`rlen == 0 && remains_tot > 0`, :2547-2549).  A packet only partly
+ *     delivered is not recorded and *consumed stays at its start: the caller
+ *     re-enters with stream + consumed, client_offset + delivered and
+ *     read_len - delivered (the reference re-enters with remains_pkt > 0,
+ *     :2356-2361; here the packet is framed and verified again and delivers
+ *     from its new c_begin).  Filled exactly at a packet's end: that packet
+ *     is recorded and consumed.
+ * c_begin is computed in 64 bits (the reference's int32_t differs only for
+ * client_offset - offsetInBlock >= 2^31).  dst receives the delivered bytes;
+ * returns the error that ended the read, ORACLE_AGAIN, or 0. */
 #define ORACLE_ERR_UNEXPECTED_READ_OFFSET 28 /* include/hadoofus/objects.h:91 */
 #define ORACLE_ERR_BAD_LASTPACKET 32        /* include/hadoofus/objects.h:98 */
+#define ORACLE_AGAIN 1000                   /* HDFS_CRC32C_AGAIN (the reference's HDFS_AGAIN) */
 int oracle_read_packets(const uint8_t *s, uint64_t len, int proto, uint32_t cs, int ctype,
-    int64_t client_offset, int64_t read_len, struct oracle_packet *out, size_t max_pkts, size_t *npkts,
-    uint64_t *consumed, uint8_t *dst, uint64_t *delivered)
+    int64_t client_offset, int64_t read_len, uint64_t cap, struct oracle_packet *out, size_t max_pkts,
+    size_t *npkts, uint64_t *consumed, uint8_t *dst, uint64_t *delivered)
 {
 	size_t n = 0;
 	uint64_t pos = 0, got = 0;
 	int64_t remains = read_len;
-	int failed = 0;
+	int rc = 0;
 	*consumed = 0;
 	while (n < max_pkts && remains > 0) {
 		struct oracle_packet k;
@@ -705,49 +717,56 @@ int oracle_read_packets(const uint8_t *s, uint64_t len, int proto, uint32_t cs, 
 				*consumed = pos + total;
 			}
 			out[n++] = k;
+			rc = k.error;
 			break;
 		}
 		const uint8_t *crcs = s + pos + k.header_len, *data = crcs + k.crc_len;
 		if (k.crc_len > 0)
 			verify_one(crcs, data, k.data_len, cs, ctype, &k);
-		const int bad = k.error != 0;
-		int stop = 0;
+		if (k.error) { /* bad CRCs: recorded, not consumed, nothing delivered */
+			out[n++] = k;
+			rc = k.error;
+			break;
+		}
 		int64_t c_begin = 0;
 		if (k.offset_in_block < client_offset) {
 			const uint64_t d = (uint64_t)client_offset - (uint64_t)k.offset_in_block;
 			c_begin = d >= (uint64_t)k.data_len ? k.data_len : (int64_t)d;
 		}
 		if (c_begin >= k.data_len) {
-			if (!bad)
-				k.error = ORACLE_ERR_UNEXPECTED_READ_OFFSET;
-			stop = 1;
-		} else {
-			const int64_t c_len = k.data_len - c_begin < remains ? k.data_len - c_begin : remains;
-			if (!bad && !failed) {
-				memcpy(dst + got, data + c_begin, (size_t)c_len);
-				got += (uint64_t)c_len;
-			}
-			remains -= c_len;
-			if (k.last && remains > 0) {
-				if (!bad)
-					k.error = ORACLE_ERR_BAD_LASTPACKET;
-				stop = 1;
-			}
+			k.error = ORACLE_ERR_UNEXPECTED_READ_OFFSET;
+			out[n++] = k;
+			rc = k.error;
+			break;
 		}
-		if (k.error)
-			failed = 1;
-		out[n++] = k;
+		const int64_t c_len = k.data_len - c_begin < remains ? k.data_len - c_begin : remains;
+		const uint64_t room = cap - got;
+		if ((uint64_t)c_len > room) { /* the destination fills inside this packet */
+			memcpy(dst + got, data + c_begin, (size_t)room);
+			got += room;
+			rc = ORACLE_AGAIN;
+			break;
+		}
+		memcpy(dst + got, data + c_begin, (size_t)c_len);
+		got += (uint64_t)c_len;
+		remains -= c_len;
 		pos += total;
 		*consumed = pos;
-		if (stop)
+		if (k.last && remains > 0)
+			k.error = ORACLE_ERR_BAD_LASTPACKET;
+		out[n++] = k;
+		if (k.error) {
+			rc = k.error;
 			break;
+		}
+		if (remains > 0 && got == cap) { /* full exactly at this packet's end */
+			rc = ORACLE_AGAIN;
+			break;
+		}
 	}
 	*npkts = n;
 	*delivered = got;
-	for (size_t i = 0; i < n; i++)
-		if (out[i].error)
-			return out[i].error;
-	return 0;
+	return rc;
 }
 
 /* ------------------------------------------------------------------ */

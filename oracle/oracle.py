@@ -80,7 +80,7 @@ class Oracle:
                          [_vp, _u64, ctypes.c_int, _u32, ctypes.c_int, ctypes.c_int,
                           ctypes.POINTER(OraclePacket), _sz, ctypes.POINTER(_sz), ctypes.POINTER(_u64)])
         self._rd = _bind(lib, "oracle_read_packets", ctypes.c_int,
-                         [_vp, _u64, ctypes.c_int, _u32, ctypes.c_int, ctypes.c_int64, ctypes.c_int64,
+                         [_vp, _u64, ctypes.c_int, _u32, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, _u64,
                           ctypes.POINTER(OraclePacket), _sz, ctypes.POINTER(_sz), ctypes.POINTER(_u64), _vp,
                           ctypes.POINTER(_u64)])
         self._opk = _bind(lib, "oracle_compose_packets", ctypes.c_int,
@@ -162,18 +162,21 @@ class Oracle:
         return rc, out, used.value
 
     def read_packets(self, stream, client_offset, read_len, proto=2, chunk_size=512, ctype=CSUM_CRC32C,
-                     max_pkts=None):
+                     max_pkts=None, cap=None):
         """A client read of block bytes [client_offset, +read_len) over a packet
-        stream (src/datanode.c:1476-1481, 2428-2549).
+        stream into a destination of `cap` bytes (None: the whole read) --
+        src/datanode.c:1476-1481, 2428-2549.  The read ends at the first
+        error; a destination that fills first returns AGAIN (1000).
         -> (rc, [packet dicts], consumed, delivered bytes)."""
         p, n = self._buf(stream)
         if max_pkts is None:
             max_pkts = n // (25 if proto == 1 else 6) + 1
         arr = (OraclePacket * max(1, max_pkts))()
         npk, used, got = _sz(0), _u64(0), _u64(0)
-        dst = np.zeros(max(1, read_len), np.uint8)
-        rc = self._rd(p, n, proto, chunk_size, ctype, client_offset, read_len, arr, max_pkts, ctypes.byref(npk),
-                      ctypes.byref(used), dst.ctypes.data, ctypes.byref(got))
+        cap = (1 << 64) - 1 if cap is None else int(cap)
+        dst = np.zeros(max(1, min(read_len, cap)), np.uint8)
+        rc = self._rd(p, n, proto, chunk_size, ctype, client_offset, read_len, cap, arr, max_pkts,
+                      ctypes.byref(npk), ctypes.byref(used), dst.ctypes.data, ctypes.byref(got))
         out = [{f: getattr(arr[i], f) for f, _ in OraclePacket._fields_ if f != "reserved"}
                for i in range(npk.value)]
         return rc, out, used.value, dst[:got.value].tobytes()

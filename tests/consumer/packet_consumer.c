@@ -205,12 +205,14 @@ int main(void)
 			at += take;
 		}
 		/* bloff = 3 * DLEN + 1000 over packets 3.. with packet 7 corrupt: the
-		 * read gets packets 3..6 (the first from byte 1000 on) and then
-		 * BAD_CHECKSUM; the window still ends in packet 8 */
+		 * read gets packets 3..6 (the first from byte 1000 on) and ends at
+		 * packet 7 with BAD_CHECKSUM (src/datanode.c:1476-1479, 2470-2475):
+		 * its record is the last, and the stream is consumed up to it */
 		rc = hdfs_crc32c_read_packets((uint8_t *)dstream + 3 * pk, total - 3 * pk, HDFS_CRC32C_PROTO_V2, CS,
 		    HDFS_CRC32C_CSUM_CRC32C, 3 * (int64_t)DLEN + 1000, 5 * (int64_t)DLEN + 777, &iov1, 1, rec, NPK + 1, &n,
 		    &used, &delivered);
-		check(rc == HDFS_CRC32C_ERR_DATANODE_BAD_CHECKSUM && n == 6 && rec[4].first_bad == 3 &&
+		check(rc == HDFS_CRC32C_ERR_DATANODE_BAD_CHECKSUM && n == 5 && rec[4].first_bad == 3 &&
+		    rec[4].error == HDFS_CRC32C_ERR_DATANODE_BAD_CHECKSUM && used == 4 * pk &&
 		    delivered == 4 * DLEN - 1000, "read window: bad packet");
 		check(map_engine_rc(rc).kind == 1 && map_engine_rc(rc).num == HDFS_CRC32C_ERR_DATANODE_BAD_CHECKSUM,
 		    "checksum error maps to the reference's error");

@@ -76,7 +76,7 @@ def assemble(parts):
 
 
 def build_stream(crc32c, proto, cs, ctype, dlens, seed=0, corrupt=(), last_empty=True, sync_every=0,
-                 seqnos=None, offset_skew=None, offset0=0, last_flag=None):
+                 seqnos=None, offset_skew=None, offset0=0, last_flag=None, sync_at=()):
     """A clean stream of packets with the given data lengths (the last one
     flagged lastPacketInBlock unless last_empty adds the v2-style trailing
     empty packet).  corrupt: iterable of (packet, chunk) -> flip one bit of
@@ -84,7 +84,8 @@ def build_stream(crc32c, proto, cs, ctype, dlens, seed=0, corrupt=(), last_empty
     (default k); offset_skew: {packet: bytes added to its offsetInBlock} --
     header fields off the regular progression, same wire sizes.  offset0:
     offsetInBlock of the first packet (a read from inside a block);
-    last_flag: packet index flagged lastPacketInBlock instead.  Returns
+    last_flag: packet index flagged lastPacketInBlock instead; sync_at:
+    packets whose v2 header carries syncBlock (27-B headers).  Returns
     (stream bytes, expected per-packet bad chunk lists)."""
     out = []
     bad = {}
@@ -103,7 +104,7 @@ def build_stream(crc32c, proto, cs, ctype, dlens, seed=0, corrupt=(), last_empty
         if proto == 1:
             out.append(frame_v1(ho, seq, last, crcs, d.tobytes()))
         else:
-            sync = (k % sync_every == 0) if sync_every else None
+            sync = (k % sync_every == 0) if sync_every else (True if k in sync_at else None)
             out.append(frame_v2(header_v2(ho, seq, last, dl, sync), crcs, d.tobytes()))
         off += dl
     if last_empty:

@@ -503,12 +503,24 @@ def _read_cases(oracle):
     w2 = oracle.verify_packets(s2)[1]
     p2 = _payload_of(s2, w2, 0) + _payload_of(s2, w2, 1)
     out.append(("last_flag_short", s2, 100, 3 * 65536, ERR_BAD_LASTPACKET, 2, p2[100:]))
-    # bad CRCs in packet 2: the bytes before it, the window's own end in packet 4
+    # bad CRCs in packet 2 end the read (src/datanode.c:1476-1479, 2470-2475):
+    # the bytes before it; the window's own end in packet 4 is never reached
     s3, _ = build_stream(oracle.crc32c, 2, cs, CSUM_CRC32C, [65536] * 6, seed=3, corrupt=[(2, 5)])
     w3 = oracle.verify_packets(s3)[1]
     p3 = b"".join(_payload_of(s3, w3, k) for k in range(2))
-    out.append(("bad_crc_mid", s3, 40, 4 * 65536 + 9, BAD, 5, p3[40:]))
+    out.append(("bad_crc_mid", s3, 40, 4 * 65536 + 9, BAD, 3, p3[40:]))
+    # bad CRCs in the packet the read starts in: nothing delivered
+    out.append(("bad_crc_first", s3[w3[2]["stream_off"]:], 2 * 65536 + 5, 1000, BAD, 1, b""))
     return out
+
+
+def _read_consumed(pk):
+    """Where a read that ended with record pk stands in the stream: a packet
+    whose header, CRCs or read offset raised the error is not consumed
+    (src/datanode.c:2445-2446, 2472-2475, 2483-2486); any other is."""
+    if pk["error"] in (BAD, ERR_UNEXPECTED_READ_OFFSET):
+        return pk["stream_off"]
+    return pk["stream_off"] + pk["header_len"] + pk["crc_len"] + pk["data_len"]
 
 
 def test_oracle_read_windows_constructed(oracle):
@@ -516,8 +528,40 @@ def test_oracle_read_windows_constructed(oracle):
         got = oracle.read_packets(s, co, rl)
         assert (got[0], len(got[1])) == (rc, npk), name
         assert got[3] == data, name
-        assert got[2] == got[1][-1]["stream_off"] + got[1][-1]["header_len"] + got[1][-1]["crc_len"] + \
-            got[1][-1]["data_len"], name
+        assert got[2] == _read_consumed(got[1][-1]), name
+        assert all(q["error"] == 0 for q in got[1][:-1]), name  # the read ends at its first error
+
+
+def test_oracle_read_capacity_resumes(oracle):
+    """The oracle's read into a destination smaller than the read (AGAIN,
+    src/datanode.c:2547-2549), resumed call by call, gives the single read's
+    records, consumed bytes, delivered bytes and final status -- for every
+    constructed case and destination sizes that end inside packets, exactly
+    on a packet's end, and on one byte."""
+    for name, s, co, rl, rc, npk, data in _read_cases(oracle):
+        want = oracle.read_packets(s, co, rl)
+        for piece in (1, 4096, 65536, 65536 + 3, 100003):
+            if piece == 1 and rl > 70000:
+                continue
+            at, tot, recs, calls = 0, 0, [], 0
+            out = b""
+            while True:
+                r, pk, used, got = oracle.read_packets(s[at:], co + tot, rl - tot, cap=min(piece, rl - tot))
+                calls += 1
+                for q in pk:
+                    q["stream_off"] += at
+                recs += pk
+                at += used
+                tot += len(got)
+                out += got
+                if r != AGAIN:
+                    break
+                assert len(got) == min(piece, rl - tot + len(got)), (name, piece)
+            assert (r, recs, at) == want[:3], (name, piece)
+            assert out == want[3] == data, (name, piece)
+
+
+AGAIN = 1000
 
 
 ERR_UNEXPECTED_READ_OFFSET, ERR_BAD_LASTPACKET = 28, 32

@@ -79,6 +79,11 @@ RUNS = [
      "taken"),
     ("v2_offset_skew", 2, 512, CSUM_CRC32C, [65536] * 100, {"offset_skew": {30: 512, 31: -9}}, "taken"),
     ("v2_sync_every", 2, 512, CSUM_CRC32C, [65536] * 100, {"sync_every": 3}, "handed_back"),  # 27-B headers mixed in
+    # packet 40 has a 27-B syncBlock header and dataLen cut by 2 --
+    # packet 0's stride and CRC length, another layout (later offsets skewed
+    # back onto the prediction, so it is the run's only exception)
+    ("v2_sync_same_stride", 2, 512, CSUM_CRC32C, [65536] * 40 + [65534] + [65536] * 59,
+     {"sync_at": (40,), "offset_skew": {k: 2 for k in range(41, 100)}}, "handed_back"),
     ("v2_size_break", 2, 512, CSUM_CRC32C, [65536] * 60 + [30000] + [65536] * 40, {}, "handed_back"),
     ("v2_many_exceptions", 2, 512, CSUM_CRC32C, [65536] * 100, {"seqnos": [3 * k for k in range(100)]},
      "handed_back"),
@@ -215,7 +220,10 @@ def test_gpu_spec_read_windows(engine, diag, oracle):
 @pytest.mark.gpu
 def test_gpu_spec_copy_out_too_small(engine, diag, oracle):
     """Whole-payload copy-out into a buffer one byte short of a regular run:
-    refused (EINVAL), and nothing is written past the buffer."""
+    refused (EINVAL: READ_ALL has no read position to resume from), and
+    nothing is written past the buffer.  A client read of the same bytes into
+    the same buffer returns AGAIN and resumes (the one rule for a short
+    destination in the mode that can resume, include/hadoofus_crc32c.h)."""
     dl = [65536] * 100
     s, _ = build_stream(oracle.crc32c, 2, 512, CSUM_CRC32C, dl, seed=8)
     keep, p = _dev(engine, s)
@@ -227,6 +235,19 @@ def test_gpu_spec_copy_out_too_small(engine, diag, oracle):
         engine.read_packets(p, len(s), dst.ptr, cap, lib=diag)
     assert _stats(diag)["taken"] == 1
     assert dst.download(4096, offset=cap).tobytes() == b"\xa5" * 4096
+    # the same stream and buffer as a client read of the whole block (the
+    # mode with a read position): AGAIN with the buffer full, and the
+    # resumed call delivers the last byte -- the oracle's read, split the same way
+    want = oracle.read_packets(s, 0, sum(dl), cap=cap)
+    assert want[0] == 1000 and len(want[3]) == cap
+    dst.fill(0xA5)
+    got = engine.read_packets(p, len(s), dst.ptr, cap, client_offset=0, read_len=sum(dl), lib=diag)
+    assert got[0] == engine.AGAIN and got[:3] == want[:3] and got[3] == cap
+    assert dst.download(cap).tobytes() == want[3]
+    assert dst.download(4096, offset=cap).tobytes() == b"\xa5" * 4096
+    rest = oracle.read_packets(s[got[2]:], cap, 1, cap=1)
+    got2 = engine.read_packets(p + got[2], len(s) - got[2], dst.ptr, 1, client_offset=cap, read_len=1, lib=diag)
+    assert got2[:3] == rest[:3] and got2[0] == 0 and dst.download(1).tobytes() == rest[3]
     keep.free()
     dst.free()
 
