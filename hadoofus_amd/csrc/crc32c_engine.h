@@ -230,6 +230,12 @@ struct DevCtx {
   SpecTabData *spec_tabs = nullptr;
   uint8_t *spec_h = nullptr, *spec_hd = nullptr;
   uint64_t spec_n = 0;
+  // client reads into host memory (hdfs_crc32c_read_packets with host
+  // iovecs): the device staging the fused copy-out fills before the D2H
+  // scatter; rd_mu is held across the verify and the scatter (taken before mu)
+  std::mutex rd_mu;
+  uint8_t *rd_stage = nullptr;
+  uint64_t rd_stage_cap = 0;
   // opt-in resident mailbox (guarded by mu): pinned request line ([0..3]
   // seq, len, chunk_size | flags, register) and status word ([16])
   bool mb_on = false, mb_alive = false;

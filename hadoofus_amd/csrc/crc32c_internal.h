@@ -213,7 +213,12 @@ struct SpecArgs {
   uint32_t parity, seq, tune;
   uint8_t *hout;            // pinned host area (device address): SpecEarly, SpecFinal
   SpecTabData *tabs;        // [gridDim.x] per-workgroup copies of the closed-form table
+  // diagnostic build only (null in the release build): per-wave start / end
+  // stamps of the work loop at [3 * wave], and per-workgroup phase stamps at
+  // [kSpecStampOff + 8 * block + phase] (s_memrealtime, 100 MHz)
+  unsigned long long *stamps;
 };
+constexpr size_t kSpecStampOff = 98304;
 constexpr uint64_t kSpecMaxStride = uint64_t(1) << 26;  // per-lane header offsets within a wave fit 32 bits
 
 // Compact verify verdict of one packet (grid_finalize_kernel).

@@ -2878,6 +2878,14 @@ __global__ __launch_bounds__(1024) void spec_verify_kernel(SpecArgs a) {
   __shared__ uint8_t *ep_hout;
   __shared__ uint32_t ep_seq;
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  // diagnostic build: phase stamps of this workgroup (0 entry, 1 tables +
+  // packet 0 decoded, 2 work loop entered, 3 header checks done, 4 the last
+  // workgroup's final block published)
+  unsigned long long *const ps = kDiag && a.stamps ? a.stamps + kSpecStampOff + 8u * blockIdx.x : nullptr;
+  auto stamp = [&](int ph) {
+    if (kDiag && ps && t == 0) ps[ph] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
   if (t == 0) {
     ep_ctl = a.ctl + a.parity;
     ep_exc = a.exc + a.parity * kSpecExcMax;
@@ -2980,6 +2988,7 @@ __global__ __launch_bounds__(1024) void spec_verify_kernel(SpecArgs a) {
     }
   }
   __syncthreads();
+  stamp(1);
   // uniform: readfirstlane'd into SGPRs (read from LDS, the compiler would
   // keep them in VGPRs and build every descriptor of the loop from them)
   SpecRun d;
@@ -3036,11 +3045,12 @@ __global__ __launch_bounds__(1024) void spec_verify_kernel(SpecArgs a) {
       h0[q] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 16u * q, 0, 0));
   }
   __syncthreads();
+  stamp(2);
   const SpecTab tab{(const CAS SpecTabData *)(a.tabs + blockIdx.x)};
   const uint64_t tiles = uint64_t(d.count) * d.T;
   tiles_run<kModeVerify, 3, 1, 3, 1, 1024, 1, COPY, 1, 0>(lds, tab, nullptr, d.count, tiles * (a.cs / kRoundBytes),
-                                                          tiles, a.fb, &ctl->mism, nullptr, a.tune, &ctl->gctr,
-                                                          nullptr, d.T, false);
+                                                          tiles, a.fb, &ctl->mism, kDiag ? a.stamps : nullptr, a.tune,
+                                                          &ctl->gctr, nullptr, d.T, false);
   for (uint32_t j = j0; 64u * j < d.count; j += 16u * G) {
     u32x4 h[kSpecHdrBytes / 16];
     if (j == j0) {
@@ -3109,6 +3119,7 @@ __global__ __launch_bounds__(1024) void spec_verify_kernel(SpecArgs a) {
   // workgroup then reads the counters and publishes the final block
   stores_done();
   __syncthreads();
+  stamp(3);
   if (t == 0) {
     SpecCtl *const c = ep_ctl;
     const uint32_t n = __hip_atomic_fetch_add(&c->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -3133,6 +3144,7 @@ __global__ __launch_bounds__(1024) void spec_verify_kernel(SpecArgs a) {
       }
       __threadfence_system();
       __hip_atomic_store(&f->seq, ep_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      stamp(4);
     }
   }
 }

@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <thread>
 #include <vector>
 
 #include "crc32c_engine.h"
@@ -778,6 +779,7 @@ int spec_pass(DevCtx &c, const uint8_t *d, uint64_t len, uint64_t pos, uint32_t 
   a.tune = tile_tune();
   a.hout = c.spec_hd;
   a.tabs = c.spec_tabs;
+  a.stamps = kDiag ? g_diag : nullptr;
   using clk = std::chrono::steady_clock;
   const auto t0 = clk::now();
   HIPCHK(launch_spec_verify(a, grid, co.dst ? 1 : 0, c.stream));
@@ -1206,14 +1208,25 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
 // with client_offset advanced, so its new c_begin skips what it delivered:
 // the reference's remains_pkt, :2356-2361).  *delivered = the bytes the
 // reference copies before its loop returns.  Returns 1 for AGAIN, else 0.
+// pieces (optional): the delivered bytes as (stream offset, length) in
+// delivery order -- what a host-memory copy-out copies.
+using Pieces = std::vector<std::pair<uint64_t, uint64_t>>;
+// examined (optional): records the walk looked at (the one it stopped at
+// included, a partly delivered packet too).
 int apply_read_window(hdfs_crc32c_packet *p, size_t &n, uint64_t &consumed, const CopyOut &co,
-                      uint64_t *delivered) {
+                      uint64_t *delivered, Pieces *pieces = nullptr, size_t *examined = nullptr) {
   uint64_t remains = co.want, room = co.cap, got = 0;
   int again = 0;
+  if (pieces) pieces->clear();
+  if (examined) *examined = n;
+  auto piece = [&](const hdfs_crc32c_packet &r, uint32_t cb, uint64_t bytes) {
+    if (pieces && bytes) pieces->push_back({r.stream_off + r.header_len + uint64_t(r.crc_len) + cb, bytes});
+  };
   for (size_t k = 0; k < n; k++) {
     hdfs_crc32c_packet &r = p[k];
     const uint64_t end = r.stream_off + r.header_len + uint64_t(r.crc_len > 0 ? r.crc_len : 0) +
                          uint64_t(r.data_len > 0 ? r.data_len : 0);
+    if (examined) *examined = k + 1;
     if (r.error) {  // framing error or bad CRCs
       n = k + 1;
       consumed = r.stream_off;
@@ -1238,6 +1251,7 @@ int apply_read_window(hdfs_crc32c_packet *p, size_t &n, uint64_t &consumed, cons
       // the destination fills inside this packet: its rest is the next
       // call's (the reference returns AGAIN here with remains_pkt > 0)
       got += room;
+      piece(r, cb, room);
       n = k;
       consumed = r.stream_off;
       again = 1;
@@ -1246,6 +1260,7 @@ int apply_read_window(hdfs_crc32c_packet *p, size_t &n, uint64_t &consumed, cons
     remains -= want;
     room -= want;
     got += want;
+    piece(r, cb, want);
     if (r.last && remains > 0) r.error = HDFS_CRC32C_ERR_DATANODE_BAD_LASTPACKET;
     if (r.error || remains == 0 || room == 0) {
       n = k + 1;
@@ -1385,6 +1400,179 @@ int verify_packets_impl(const uint8_t *stream, uint64_t len, int proto, uint32_t
   if (npkts) *npkts = recs.size();
   if (consumed) *consumed = used;
   return first_error(recs.data(), recs.size());
+}
+
+// ---- client reads into host memory (hdfs_crc32c_read_packets, host iovecs) ----
+// The read path of a datanode whose user buffers are host memory: the
+// reference verifies a packet and then memcpy()s its payload into the
+// caller's iovecs (src/datanode.c:2470-2476, 2509-2537).
+struct CopyJob {
+  const uint8_t *src;
+  uint8_t *dst;
+  uint64_t len;
+};
+// Lay `pieces` (offsets into src) end to end over the iovecs, in order.
+void scatter_jobs(const uint8_t *src, const Pieces &pieces, const hdfs_crc32c_iovec *iov, int iovcnt,
+                  std::vector<CopyJob> &jobs) {
+  jobs.clear();
+  int i = 0;
+  uint64_t io = 0;
+  for (const auto &pc : pieces) {
+    uint64_t off = pc.first, left = pc.second;
+    while (left) {
+      while (i < iovcnt && io == iov[i].len) {
+        i++;
+        io = 0;
+      }
+      if (i == iovcnt) return;  // (the pieces never exceed the iovecs' capacity)
+      const uint64_t take = std::min(left, iov[i].len - io);
+      jobs.push_back({src + off, static_cast<uint8_t *>(iov[i].base) + io, take});
+      off += take;
+      left -= take;
+      io += take;
+    }
+  }
+}
+// Host-to-host copies (the reference's memcpy), split over a few threads for
+// large reads.
+void run_host_jobs(const std::vector<CopyJob> &jobs) {
+  uint64_t total = 0;
+  for (const auto &j : jobs) total += j.len;
+  const unsigned nt = total >= (64ull << 20) ? std::min(8u, std::max(1u, std::thread::hardware_concurrency())) : 1u;
+  auto work = [&](unsigned t) {
+    const uint64_t a = total * t / nt, b = total * (t + 1) / nt;
+    uint64_t pos = 0;
+    for (const auto &j : jobs) {
+      const uint64_t s0 = std::max(a, pos), e0 = std::min(b, pos + j.len);
+      if (s0 < e0) std::memcpy(j.dst + (s0 - pos), j.src + (s0 - pos), e0 - s0);
+      pos += j.len;
+      if (pos >= b) break;
+    }
+  };
+  std::vector<std::thread> th;
+  for (unsigned t = 1; t < nt; t++) th.emplace_back(work, t);
+  work(0);
+  for (auto &x : th) x.join();
+}
+
+// Device-resident stream, host destination: the fused verify + copy-out into
+// a device staging area (one pass, the whole capacity), then D2H per iovec.
+int read_dev_to_host(int dev, const uint8_t *s, uint64_t len, int proto, uint32_t cs, int ctype, int64_t client_offset,
+                     int64_t read_len, const hdfs_crc32c_iovec *iov, int iovcnt, uint64_t total,
+                     hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts, uint64_t *consumed,
+                     uint64_t *delivered) {
+  DevCtx *cp = nullptr;
+  int rc;
+  if ((rc = ctx_init(dev, &cp))) return rc;
+  DevCtx &c = *cp;
+  DeviceGuard g(c.dev);
+  std::lock_guard<std::mutex> lk(c.rd_mu);
+  const bool win = read_len != HDFS_CRC32C_READ_ALL;
+  const uint64_t cap = win ? std::min<uint64_t>(total, uint64_t(read_len)) : total;
+  if (cap > c.rd_stage_cap) {
+    if (c.rd_stage) HIPCHK(hipFree(c.rd_stage));
+    c.rd_stage = nullptr;
+    c.rd_stage_cap = 0;
+    const uint64_t want = align_up(cap, uint64_t(1) << 20);
+    if (hipMalloc(&c.rd_stage, want) != hipSuccess) {
+      (void)hipGetLastError();
+      return fail(HDFS_CRC32C_ENOMEM, "read staging of %llu bytes", (unsigned long long)want);
+    }
+    c.rd_stage_cap = want;
+  }
+  CopyOut co;
+  co.dst = c.rd_stage;
+  co.cap = cap;
+  if (win) {
+    co.win = true;
+    co.client_offset = client_offset;
+    co.want = uint64_t(read_len);
+  }
+  size_t n = 0;
+  uint64_t used = 0, got = 0;
+  rc = verify_packets_dev_impl(dev, s, len, proto, cs, ctype, pkts, max_pkts, &n, &used, true, co, &got);
+  if (rc < 0) return rc;
+  std::vector<CopyJob> jobs;
+  scatter_jobs(c.rd_stage, Pieces{{0, got}}, iov, iovcnt, jobs);
+  {
+    std::lock_guard<std::mutex> lk2(c.mu);
+    for (const auto &j : jobs) HIPCHK(hipMemcpyAsync(j.dst, j.src, j.len, hipMemcpyDeviceToHost, c.stream));
+    HIPCHK(hipStreamSynchronize(c.stream));
+  }
+  *npkts = n;
+  *consumed = used;
+  *delivered = got;
+  return rc;
+}
+
+// Host-resident stream, host destination: framed on the host, the packets
+// the read takes verified on the GPU (hdfs_crc32c_verify_packets' host
+// pipeline), then their delivered bytes copied.
+int read_host_to_host(const uint8_t *s, uint64_t len, int proto, uint32_t cs, int ctype, int64_t client_offset,
+                      int64_t read_len, const hdfs_crc32c_iovec *iov, int iovcnt, uint64_t total,
+                      hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts, uint64_t *consumed,
+                      uint64_t *delivered) {
+  const bool win = read_len != HDFS_CRC32C_READ_ALL;
+  std::vector<hdfs_crc32c_packet> recs;
+  uint64_t used = 0;
+  int rc;
+  Pieces pieces;
+  uint64_t got = 0;
+  int again = 0;
+  size_t n = 0;
+  if (win) {
+    CopyOut co;
+    co.win = true;
+    co.client_offset = client_offset;
+    co.want = uint64_t(read_len);
+    co.cap = std::min<uint64_t>(total, uint64_t(read_len));
+    // the window is a function of the headers: which packets the read takes
+    if ((rc = parse_packet_stream(s, len, proto, cs, ctype, max_pkts, recs, &used, g_err, sizeof(g_err)))) return rc;
+    size_t nh = recs.size(), seen = 0;
+    uint64_t ch = used;
+    (void)apply_read_window(recs.data(), nh, ch, co, nullptr, nullptr, &seen);
+    // verified: up to the start of the first packet the walk did not look at
+    const uint64_t vlen = seen < recs.size() ? recs[seen].stream_off : len;
+    recs.assign(seen, hdfs_crc32c_packet{});
+    size_t nv = 0;
+    rc = verify_packets_impl(s, vlen, proto, cs, ctype, recs.data(), recs.size(), &nv, &used, true);
+    if (rc < 0) return rc;
+    n = nv;
+    again = apply_read_window(recs.data(), n, used, co, &got, &pieces);
+  } else {
+    // straight into the caller's records (max_pkts of them)
+    size_t nv = 0;
+    rc = verify_packets_impl(s, len, proto, cs, ctype, pkts, max_pkts, &nv, &used, true);
+    if (rc < 0) return rc;
+    n = nv;
+    recs.assign(pkts, pkts + n);
+    // every framing-clean packet's payload must fit (as on the device path);
+    // the packets before the first error are delivered
+    uint64_t payload = 0;
+    bool err = false;
+    for (size_t k = 0; k < n; k++) {
+      const hdfs_crc32c_packet &r = recs[k];
+      const bool clean = !r.error || r.error == HDFS_CRC32C_ERR_DATANODE_BAD_CHECKSUM;
+      if (clean && r.data_len > 0) payload += uint64_t(r.data_len);
+      if (r.error) err = true;
+      if (!err && r.data_len > 0) {
+        pieces.push_back({wire_begin(r) + uint64_t(r.crc_len), uint64_t(r.data_len)});
+        got += uint64_t(r.data_len);
+      }
+    }
+    if (payload > total)
+      return fail(HDFS_CRC32C_EINVAL, "copy-out buffer of %llu bytes is too small (%llu needed)",
+                  (unsigned long long)total, (unsigned long long)payload);
+  }
+  std::vector<CopyJob> jobs;
+  scatter_jobs(s, pieces, iov, iovcnt, jobs);
+  run_host_jobs(jobs);
+  if (n) std::memcpy(pkts, recs.data(), n * sizeof(hdfs_crc32c_packet));
+  *npkts = n;
+  *consumed = used;
+  *delivered = got;
+  rc = first_error(recs.data(), n);
+  return rc ? rc : again ? HDFS_CRC32C_AGAIN : HDFS_CRC32C_OK;
 }
 
 }  // namespace
@@ -1635,10 +1823,35 @@ int hdfs_crc32c_read_packets(const void *stream, uint64_t len, int proto, uint32
   if (!len) return HDFS_CRC32C_OK;
   if (!stream) return fail(HDFS_CRC32C_EINVAL, "null stream");
   const int dev = stream_device(stream);
-  if (dev < 0) return fail(HDFS_CRC32C_EINVAL, "verify + copy-out takes device-resident streams only");
-  for (int i = 0; i < iovcnt; i++)
-    if (iov[i].len && (!iov[i].base || stream_device(iov[i].base) != dev))
-      return fail(HDFS_CRC32C_EINVAL, "iovec %d: device memory of the stream's device needed", i);
+  // destinations: all device memory of the stream's device (the fused
+  // de-framing copy), or all host memory
+  bool any_host = false, any_dev = false;
+  uint64_t total = 0;
+  for (int i = 0; i < iovcnt; i++) {
+    if (!iov[i].len) continue;
+    if (!iov[i].base) return fail(HDFS_CRC32C_EINVAL, "iovec %d: null base", i);
+    const int d = stream_device(iov[i].base);
+    if (d < 0) any_host = true;
+    else if (d == dev) any_dev = true;
+    else return fail(HDFS_CRC32C_EINVAL, "iovec %d: memory of device %d, the stream is on %d", i, d, dev);
+    total += iov[i].len;
+  }
+  if (any_host && any_dev) return fail(HDFS_CRC32C_EINVAL, "iovecs mix host and device memory");
+  if (!total) return HDFS_CRC32C_OK;
+  if (dev < 0 && any_dev) return fail(HDFS_CRC32C_EINVAL, "a host-resident stream copies out to host memory");
+  if (dev < 0 || any_host) {
+    size_t n = 0;
+    uint64_t used = 0, got = 0;
+    rc = dev < 0 ? read_host_to_host(static_cast<const uint8_t *>(stream), len, proto, chunk_size, ctype,
+                                     client_offset, read_len, iov, iovcnt, total, pkts, max_pkts, &n, &used, &got)
+                 : read_dev_to_host(dev, static_cast<const uint8_t *>(stream), len, proto, chunk_size, ctype,
+                                    client_offset, read_len, iov, iovcnt, total, pkts, max_pkts, &n, &used, &got);
+    if (rc < 0) return rc;
+    if (npkts) *npkts = n;
+    if (consumed) *consumed = used;
+    if (delivered) *delivered = got;
+    return rc;
+  }
   // One pass per buffer: each delivers into its buffer and stops with AGAIN
   // when the buffer is full, and the next resumes where the read stands
   // (the stream from the packet it stopped in, the client offset advanced

@@ -217,17 +217,28 @@ int hdfs_crc32c_parse_packets(const void *stream, uint64_t len, int proto, uint3
 int hdfs_crc32c_verify_packets(const void *stream, uint64_t len, int proto, uint32_t chunk_size,
     int ctype, hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts, uint64_t *consumed);
 
-/* Read of a DEVICE-resident packet stream (GPU-direct receive):
- * hdfs_crc32c_verify_packets, and in the same pass over HBM the packets'
- * data is written, de-framed and in stream order, to the caller's device
- * buffers -- the read path's _process_recv_packet / _recv_packet_copy_data
- * (src/datanode.c:2470-2553) fused into the verify kernel: each payload
- * byte is read once and written once.  (Round 4: replaces round 3's
+/* Read of a packet stream: hdfs_crc32c_verify_packets, and the packets'
+ * data delivered, de-framed and in stream order, to the caller's buffers --
+ * the read path's _process_recv_packet / _recv_packet_copy_data
+ * (src/datanode.c:2470-2553).  (Round 4: replaces round 3's
  * hdfs_crc32c_verify_packets_copy, whose signature had changed under the
- * same name; see HDFS_CRC32C_ABI_VERSION.)
+ * same name; see HDFS_CRC32C_ABI_VERSION.)  Where the bytes live:
+ *   - device stream, device buffers (GPU-direct receive): the copy is fused
+ *     into the verify kernel, each payload byte read once and written once;
+ *   - device stream, host buffers: the same fused pass into an engine-owned
+ *     device staging area (grown to the read's size on demand), then one
+ *     D2H copy per iovec;
+ *   - host stream, host buffers (a datanode receiving into host memory):
+ *     framed on the host, the packets the read takes verified on the GPU
+ *     (the host pipeline of hdfs_crc32c_verify_packets), then their bytes
+ *     memcpy()ed into the iovecs as the reference does (:2516);
+ *   - host stream, device buffers: EINVAL.
+ * (Host buffers since round 5; the signature and symbol are unchanged, a
+ * round-4 library refuses them with EINVAL.)
  *
- * iov / iovcnt: the destination, device buffers filled in order (the
- * reference's iovec array, :2509-2537); total capacity cap = sum of
+ * iov / iovcnt: the destination, buffers filled in order (the reference's
+ * iovec array, :2509-2537), all device memory of the stream's device or all
+ * host memory (pageable or pinned); total capacity cap = sum of
  * iov[i].len.
  * read_len = HDFS_CRC32C_READ_ALL: every framing-clean packet's whole
  *   payload (iovcnt must be 1): hdfs_crc32c_verify_packets with the payload
@@ -281,7 +292,7 @@ int hdfs_crc32c_verify_packets(const void *stream, uint64_t len, int proto, uint
  * reference's HDFS_AGAIN); outside the range of the datanode errors. */
 #define HDFS_CRC32C_AGAIN 1000
 typedef struct hdfs_crc32c_iovec {
-	void *base;     /* device memory of the stream's device */
+	void *base;     /* device memory of the stream's device, or host memory */
 	uint64_t len;
 } hdfs_crc32c_iovec;
 int hdfs_crc32c_read_packets(const void *stream, uint64_t len, int proto, uint32_t chunk_size, int ctype,

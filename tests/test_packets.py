@@ -320,16 +320,17 @@ def test_gpu_device_stream_copy_out(engine, oracle, proto, cs, ctype, sizes, shi
 
 @pytest.mark.gpu
 def test_gpu_device_stream_copy_out_errors(engine, oracle):
-    """Refused: a destination smaller than the payload, a host stream, a
-    host destination and CSUM_NULL (no verify to fuse the copy into)."""
+    """Refused: a destination smaller than the payload, a host stream into
+    device buffers and CSUM_NULL (no verify to fuse the copy into).  A host
+    destination is accepted (round 5, tests/test_read_host.py)."""
     s, _ = build_stream(oracle.crc32c, 2, 512, CSUM_CRC32C, [65536] * 8, seed=3)
     keep, p = _dev(engine, s)
     dst = engine.DeviceBuffer(8 * 65536)
     with pytest.raises(engine.CRC32CError):
         engine.read_packets(p, len(s), dst.ptr, 8 * 65536 - 1)
     host = np.zeros(8 * 65536, np.uint8)
-    with pytest.raises(engine.CRC32CError):
-        engine.read_packets(p, len(s), host.ctypes.data, host.nbytes)
+    rc, pkts, used, delivered = engine.read_packets(p, len(s), host.ctypes.data, host.nbytes)
+    assert rc == 0 and delivered == 8 * 65536 and used == len(s)
     with pytest.raises(engine.CRC32CError):
         engine.read_packets(p, len(s), dst.ptr, dst.nbytes, ctype=0)
     src = np.frombuffer(s, np.uint8).copy()

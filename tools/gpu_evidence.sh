@@ -3,9 +3,11 @@
 # bench line, bench under rocprofv3 (kernel trace + stats), HBM traffic from
 # PMC passes, the RCCL path at world 1, the C4 config, device-stream and
 # small-call latency benches.   tools/gpu_evidence.sh TAG ROUND [PARTS]
-# PARTS: any of t (tests + smoke), b (bench + rocprof), p (PMC + torchrun +
+# PARTS: any of t (tests + smoke), b (bench, and the same command under
+# rocprofv3 with its trace-vs-line comparison), p (PMC + torchrun +
 # C4), d (device-stream + small-call benches), q (SQ/TA/TCP counters of the
-# compute and verify kernels, tools/pmc_sq.py); default tbpd, one call.
+# compute and verify kernels, tools/pmc_sq.py), s (phase stamps of the
+# speculative verify, tools/spec_phases.py); default tbpd, one call.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
@@ -21,7 +23,10 @@ has t && tail -2 ${O}_tests.log
 has t && step smoke timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()"
 has b && step bench timeout -k 10 600 python bench.py > ${O}_bench.json 2> ${O}_bench.err
 has b && cat ${O}_bench.json
-has b && step prof timeout -k 10 600 rocprofv3 --kernel-trace --stats -d ${O}_prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu > ${O}_prof.log 2>&1
+# the driver's own command under the profiler: its bench line and its trace
+# come from one process (tools/trace_vs_line.py compares the timed launches)
+has b && step prof timeout -k 10 900 rocprofv3 --kernel-trace --stats -d ${O}_prof -o run --output-format csv -- python3 bench.py > ${O}_prof.log 2>&1
+has b && step trace_vs_line python tools/trace_vs_line.py ${O}_prof/run_kernel_trace.csv ${O}_prof.log ${O}_trace_vs_line.json
 has b && grep -h crc32c_tiles ${O}_prof/run_kernel_stats.csv | cut -c1-200
 has p && step pmc timeout -k 10 900 python tools/pmc_traffic.py ${RND} > ${O}_pmc.json 2> ${O}_pmc.err
 has p && cat ${O}_pmc.json
@@ -35,4 +40,6 @@ has d && step small timeout -k 10 300 python tools/small_launch.py > ${O}_small.
 has d && cat ${O}_small.json
 has q && step pmc_sq timeout -k 10 900 python tools/pmc_sq.py ${O}_pmc_sq.json > /dev/null 2> ${O}_pmc_sq.err
 has q && cat ${O}_pmc_sq.json
+has s && step spec_phases timeout -k 10 300 python tools/spec_phases.py ${O}_spec_phases.json > /dev/null 2> ${O}_spec_phases.err
+has s && cat ${O}_spec_phases.json
 exit 0
