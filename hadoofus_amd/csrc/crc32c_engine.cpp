@@ -82,6 +82,10 @@ uint32_t g_group_shift = uint32_t(HDFS_KNOB("HDFS_CRC32C_GROUP", 3)) & 15u;
 // of G/8 groups per step), by plain workgroup id (0), or XCD-split (2: each
 // XCD sweeps its own contiguous eighth of the launch).
 uint32_t g_xcd_major = uint32_t(HDFS_KNOB("HDFS_CRC32C_XCD", 1)) & 3u;
+// Speculative verify (spec_verify_kernel): rounds per wave from which the
+// launch keeps the last 8 % of its tiles in the global pool (schedule 3's
+// two-phase split; the plan kernels use 32).
+uint32_t g_spec_pool_min = uint32_t(HDFS_KNOB("HDFS_CRC32C_SPEC_POOL", 32)) & 255u;
 // Compute-mode CRC stores: 2 (product) schedule 3 with the LDS group gather
 // (one 256-B store per 8-tile group); diagnostic build only: 1 schedule 4
 // on tables of whole groups, 0 one 32-B store per tile

@@ -303,6 +303,9 @@ int launch_verify_dyn(DevCtx &c, const SegDev *d_segs, const GridSummary *dyn, u
 // The tiled kernel's tune word (schedule-3 group shift, XCD dealing; the
 // diagnostic build's store policy).
 uint32_t tile_tune();
+// spec_verify_kernel: rounds per wave from which the global pool is used
+// (tune bits 23:16 of the tiled kernel; 0 there means 32)
+extern uint32_t g_spec_pool_min;
 // Any segment whose data is not 4-B aligned (selects the realigning kernel).
 bool any_unaligned(const SegDev *segs, size_t n);
 // Copy / compute streams, events and the small pipeline buffers.

@@ -1250,7 +1250,8 @@ DEV void tiles_run(uint32_t *lds, const Tab sg, const SegDev *__restrict__ segs,
   static_assert(GATHER == 0 || (MODE == kModeCompute && ORDER == 3 && S == 1), "gather: compute, schedule 3");
   LaneConst L;
   // tune: [7:0] store policy (diagnostic build), [11:8] ORDER-3 group shift,
-  // [13:12] ORDER-3 dealing: 0 plain, 1 XCD-major, 2 XCD-split (uniform: SGPR)
+  // [13:12] ORDER-3 dealing: 0 plain, 1 XCD-major, 2 XCD-split, [23:16] pool
+  // threshold in rounds per wave (uniform: SGPR)
   L.store_policy = EP::policy(tune & 0xffu);
   L.lane = threadIdx.x & 63u;
   L.hsel = (L.lane >> 3) & 1u;                              // load: odd sub-chunk of each 1 KiB
@@ -1299,7 +1300,9 @@ DEV void tiles_run(uint32_t *lds, const Tab sg, const SegDev *__restrict__ segs,
       }
     }
   } else {
-    const bool pool = ORDER >= 2 && total_rounds >= 32ull * nwaves * S;
+    // tune bits 23:16: rounds per wave from which the pool is used (0: 32)
+    const uint32_t pmin = (tune >> 16) & 0xffu;
+    const bool pool = ORDER >= 2 && total_rounds >= uint64_t(pmin ? pmin : 32u) * nwaves * S;
     if (ORDER >= 3) {
       // static phase: whole groups only; the pool takes the rest
       // ORDER 4: 2^gshift tiles per run (8 in the diagnostic default; 4 = one

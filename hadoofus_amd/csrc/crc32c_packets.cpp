@@ -583,9 +583,14 @@ int reserve_grid(DevCtx &c, size_t si, const GridLayout &L) {
 // there (records in dst), 0 when the regular path must run (a packet the
 // kernel cannot take, a packet off the grid, more packets than it covers),
 // < 0 on an engine error.
+// truncated: len is the first kSmallRunBytes of a longer stream, for a
+// client read that wants little of it (a read resumed into a small buffer):
+// resolved only when the read is decided inside what was framed -- the
+// destination fills there, or a packet ends the read (read_stopper).
+bool read_window_over(const hdfs_crc32c_packet *p, size_t n, const CopyOut &co, const uint32_t *idx, size_t nidx);
 int small_run(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs, int ctype, bool verify,
               const CopyOut &co, size_t max_pkts, hdfs_crc32c_packet *dst, size_t *nout, uint64_t *consumed,
-              uint64_t *payload) {
+              uint64_t *payload, bool truncated = false) {
   if (!c.sr_h) {
     HIPCHK(hipHostMalloc(&c.sr_h, kSrHostBytes, hipHostMallocCoherent | hipHostMallocMapped));
     std::memset(c.sr_h, 0, kSrHostBytes);
@@ -656,7 +661,7 @@ int small_run(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
   }
   for (uint32_t k = 0; k < recorded; k++) unsup |= *word(k, 0) >> 8;
   const bool ended = st_fb == kGridStop || st_fb == kGridMore || (fbk == count && (count == max_pkts || next >= len));
-  if (unsup || !ended) return 0;
+  if (unsup || !(ended || truncated)) return 0;
   for (uint32_t k = 0; k < recorded; k++) {
     dst[k] = rec(k);
     uint32_t cb = 0;
@@ -666,6 +671,14 @@ int small_run(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
       dst[k].first_bad = int32_t(*word(k, 1));
       dst[k].bad_chunks = *word(k, 2);
     }
+  }
+  // a truncated stream: the records must decide the read (a framing error
+  // among them does too: the read ends there)
+  if (truncated) {
+    bool decided = co.win && pay >= co.cap;
+    for (uint32_t k = 0; k < recorded && !decided; k++) decided = dst[k].error && dst[k].error != HDFS_CRC32C_ERR_DATANODE_BAD_CHECKSUM;
+    if (!decided) decided = co.win && read_window_over(dst, recorded, co, nullptr, 0);
+    if (!decided) return 0;
   }
   *nout = recorded;
   *consumed = used;
@@ -776,7 +789,7 @@ int spec_pass(DevCtx &c, const uint8_t *d, uint64_t len, uint64_t pos, uint32_t 
   a.exc = c.spec_exc;
   a.parity = uint32_t(c.spec_n & 1u);
   a.seq = seq;
-  a.tune = tile_tune();
+  a.tune = tile_tune() | (g_spec_pool_min << 16);
   a.hout = c.spec_hd;
   a.tabs = c.spec_tabs;
   a.stamps = kDiag ? g_diag : nullptr;
@@ -906,9 +919,15 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
   *nout = 0;
   *consumed = 0;
   verify = verify && ctype != HDFS_CRC32C_CSUM_NULL;
-  if (max_pkts && len <= kSmallRunBytes) {  // verify (+ copy-out) or framing only
+  // a stream of at most kSmallRunBytes, or a client read whose destination
+  // is at most 64 KiB of a longer one (a read resumed into a small buffer:
+  // the packets it needs lie in the stream's first kSmallRunBytes unless
+  // they are not all 64 KiB ones -- then the regular path runs)
+  const bool small_win = co.win && co.dst && co.cap <= kSmallMax && len > kSmallRunBytes;
+  if (max_pkts && (len <= kSmallRunBytes || small_win)) {  // verify (+ copy-out) or framing only
     uint64_t pay = 0;
-    const int r = small_run(c, d, len, proto, cs, ctype, verify, co, max_pkts, dst, nout, consumed, &pay);
+    const int r = small_run(c, d, std::min<uint64_t>(len, kSmallRunBytes), proto, cs, ctype, verify, co, max_pkts, dst,
+                            nout, consumed, &pay, small_win);
     if (r < 0) return r;
     if (r == 1) {
       if (co.dst && !co.win && pay > co.cap)

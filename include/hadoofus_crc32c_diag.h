@@ -10,7 +10,7 @@
  * that does no CRC arithmetic).  Used by tools/ experiments and by
  * bench.py's empirical-ceiling measurement; never by a datanode.
  * Environment overrides (HDFS_CRC32C_TILE_ORDER, _NT, _DEPTH, _STREAMS,
- * _BLOCK, _STORE, _GROUP, _ALIGN, _SMALL_RULE) are read by this build only.
+ * _BLOCK, _STORE, _GROUP, _ALIGN, _SMALL_RULE, _SPEC_POOL) are read by this build only.
  */
 #ifndef HADOOFUS_CRC32C_DIAG_H
 #define HADOOFUS_CRC32C_DIAG_H

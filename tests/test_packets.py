@@ -784,7 +784,9 @@ def test_gpu_read_resumable_and_scatter(engine, oracle, proto, cs, ctype, sizes)
         want = oracle.read_packets(sub, co, rl, proto, cs, ctype)
         keep, p = _dev(engine, sub, ci % 3)
         dst = engine.DeviceBuffer(rl + 4096)
-        for piece in (65536 + 3, 100003, 1 << 20):
+        # <= 64 KiB: the short-run kernel over the stream's first 4 MiB
+        # (grid_walk's small_win); larger: the speculative / framing passes
+        for piece in (4099, 65536, 65536 + 3, 100003, 1 << 20):
             dst.fill(0xA5)
             rc, recs, used, data, calls = _resumed_read(engine, p, len(sub), co, rl, piece, dst, proto, cs, ctype)
             assert (rc, recs, used) == want[:3], (co - base, rl, piece)

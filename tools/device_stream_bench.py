@@ -159,6 +159,71 @@ def run_size(out, key, img, npk_data, npk_all, reps):
     return dev
 
 
+def resumed_reads(ptr, n, npk, payload, reps=3):
+    """Client reads of a whole block (client_offset 0, read_len = its payload)
+    the way a datanode's caller makes them (src/datanode.c:1476-1481,
+    2547-2549): one call into one buffer; resumed call by call (AGAIN)
+    through 64 KiB and 1 MiB buffers (stream + consumed, client_offset +
+    delivered, read_len - delivered); one call over a 64-entry scatter list;
+    one call into pinned and into pageable host memory.  Best of reps, GiB/s
+    of delivered payload, calls per read, and the rate as a fraction of the
+    single call's."""
+    arr = (h.abi.Packet * (npk + 8))()
+    cnt, used, got = ctypes.c_size_t(0), ctypes.c_uint64(0), ctypes.c_uint64(0)
+    dst = h.DeviceBuffer(payload)
+
+    def read(piece, iov_list=None):
+        at, tot, calls = 0, 0, 0
+        while True:
+            if iov_list is None:
+                vec = (h.abi.IoVec * 1)(h.abi.IoVec(dst.ptr + tot, min(piece, payload - tot)))
+                nv = 1
+            else:
+                vec = (h.abi.IoVec * len(iov_list))(*[h.abi.IoVec(p, m) for p, m in iov_list])
+                nv = len(iov_list)
+            rc = lib.hdfs_crc32c_read_packets(ptr + at, n - at, h.PROTO_V2, 512, h.CSUM_CRC32C, tot, payload - tot,
+                                              vec, nv, arr, npk + 8, ctypes.byref(cnt), ctypes.byref(used),
+                                              ctypes.byref(got))
+            calls += 1
+            at += used.value
+            tot += got.value
+            if rc != h.AGAIN:
+                assert rc == 0 and tot == payload, (rc, tot, payload)
+                return calls
+
+    def best(fn):
+        fn()  # warm-up (staging growth)
+        t, calls = 1e9, 0
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            calls = fn()
+            t = min(t, time.perf_counter() - t0)
+        return t, calls
+
+    res = {}
+    t1, _ = best(lambda: read(payload))
+    res["single_call"] = {"GiBps": round(payload / t1 / 2**30, 1), "us": round(t1 * 1e6, 1), "calls": 1}
+    for name, piece in (("resumed_64KiB", 64 << 10), ("resumed_1MiB", 1 << 20)):
+        t, calls = best(lambda: read(piece))
+        res[name] = {"GiBps": round(payload / t / 2**30, 2), "us": round(t * 1e6, 1), "calls": calls,
+                     "us_per_call": round(t * 1e6 / calls, 2), "frac_of_single_call": round(t1 / t, 4)}
+    sl = payload // 64
+    iov64 = [(dst.ptr + k * sl, sl) for k in range(64)]
+    t, calls = best(lambda: read(payload, iov64))
+    res["scatter_64"] = {"GiBps": round(payload / t / 2**30, 1), "us": round(t * 1e6, 1), "calls": calls,
+                         "frac_of_single_call": round(t1 / t, 4)}
+    pin = h.PinnedBuffer(payload)
+    t, _ = best(lambda: read(payload, [(pin.ptr, payload)]))
+    res["host_pinned_dst"] = {"GiBps": round(payload / t / 2**30, 1), "us": round(t * 1e6, 1)}
+    pin.free()
+    pg = np.empty(payload, np.uint8)
+    t, _ = best(lambda: read(payload, [(pg.ctypes.data, payload)]))
+    res["host_pageable_dst"] = {"GiBps": round(payload / t / 2**30, 1), "us": round(t * 1e6, 1)}
+    del pg
+    dst.free()
+    return res
+
+
 def block_and_run(plan_GiBps=None):
     """bench.py's extra.device_stream: the 1 GiB run and one 128 MiB block,
     end to end per call, beside a verify plan over the same packets (same
@@ -176,6 +241,7 @@ def block_and_run(plan_GiBps=None):
     del img
     blk, nblk = wire_image(128 << 20, 9, empty_last=True)
     dev = run_size(out, "block_128MiB", blk, 2048, nblk, 10)
+    out["block_128MiB"]["client_reads"] = resumed_reads(dev.ptr, blk.nbytes, nblk, 2048 * 65536)
     dev.free()
     if plan_GiBps:
         for k in ("run_1GiB", "block_128MiB"):
@@ -253,6 +319,7 @@ def main():
     # one 128 MiB HDFS block: 2 048 packets and the empty last packet
     blk, nblk = wire_image(128 << 20, 9, empty_last=True)
     dev = run_size(out, "block_128MiB", blk, 2048, nblk, 10)
+    out["block_128MiB"]["client_reads"] = resumed_reads(dev.ptr, blk.nbytes, nblk, 2048 * 65536)
     dev.free()
     print(json.dumps(out))
 
