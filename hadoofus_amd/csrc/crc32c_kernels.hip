@@ -2874,6 +2874,8 @@ __global__ __launch_bounds__(1024) void spec_verify_kernel(SpecArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords + 2 + 2 * kSlots];
   __shared__ __attribute__((aligned(16))) uint8_t win[2][kHdrWin];  // packet 0, the point after the run
   __shared__ SpecRun run;
+  __shared__ uint64_t run_r0[7];  // packet 0's record, for the early block
+  __shared__ uint64_t run_total;
   // what the epilogue needs, parked in LDS: kept in SGPRs across the work
   // loop they pushed it past the SGPR budget (spills)
   __shared__ SpecCtl *ep_ctl;
@@ -2882,8 +2884,8 @@ __global__ __launch_bounds__(1024) void spec_verify_kernel(SpecArgs a) {
   __shared__ uint32_t ep_seq;
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
   // diagnostic build: phase stamps of this workgroup (0 entry, 1 tables +
-  // packet 0 decoded, 2 work loop entered, 3 header checks done, 4 the last
-  // workgroup's final block published)
+  // packet 0 decoded + closed-form table written, 2 work loop entered, 3
+  // header checks done, 4 the last workgroup's final block published)
   unsigned long long *const ps = kDiag && a.stamps ? a.stamps + kSpecStampOff + 8u * blockIdx.x : nullptr;
   auto stamp = [&](int ph) {
     if (kDiag && ps && t == 0) ps[ph] = __builtin_amdgcn_s_memrealtime();
@@ -2908,6 +2910,12 @@ __global__ __launch_bounds__(1024) void spec_verify_kernel(SpecArgs a) {
   }
   fill_tables<1024, 0>(lds, a.gtab);
   if (wv == 0 && lane == 0) {
+    // The critical path of every workgroup: packet 0's decode and this
+    // workgroup's copy of the closed-form table (written with vector stores,
+    // acknowledged before the barrier; read back with scalar loads in the
+    // work loop).  What only the host or the epilogue needs -- the point
+    // after the run, the early block, the next launch's control slot -- is
+    // left to one wave of workgroup 0 after the barrier.
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");  // the window's LDS stores, this wave's own
     SpecRun d{};
     hdfs_crc32c_packet r{};
@@ -2941,53 +2949,26 @@ __global__ __launch_bounds__(1024) void spec_verify_kernel(SpecArgs a) {
       d.v1 = a.proto == HDFS_CRC32C_PROTO_V1 ? 1u : 0u;
       d.off0 = uint64_t(r.offset_in_block);
       d.seq0 = uint64_t(r.seqno);
-      if (ok && blockIdx.x == 0) {
-        // the point after the run: where the walk goes on, or what ends it
-        uint32_t ts = kGridOn;
-        uint64_t ttot = 0;
-        hdfs_crc32c_packet tr{};
-        // (the caller's record array holds count + 1 records only when the
-        // pass was not cut at max_count)
-        if (count == by_len && count < a.max_count) {  // the run ends with the stream's whole strides
-          const uint64_t pt = a.base + uint64_t(count) * total;
-          if (pt >= a.len) {
-            ts = kGridMore;
-          } else {
-            stage_header(a.s, a.len, pt, 0u, win[1]);
-            const int tst = grid_frame(a.s, a.len, pt, win[1], a.proto, a.cs, a.ctype, tr, ttot);
-            ts = tst == frame::kStepMore ? kGridMore : tst == frame::kStepStop ? kGridStop : kGridOff;
-          }
-        }
-        const uint64_t *x = reinterpret_cast<const uint64_t *>(&tr);
-#pragma unroll
-        for (int q = 0; q < 7; q++) at_st(&ctl->tail[q], x[q]);
-        at_st(&ctl->tail_total, ttot);
-        at_st32(&ctl->tail_status, ts);
-        stores_done();
-      }
     }
     d.eligible = ok ? 1u : 0u;
     d.count = count;
     run = d;
-    if (blockIdx.x == 0) {
-      // the next launch's control slot starts at zero (this launch's was
-      // zeroed by the one before)
-      SpecCtl *nx = a.ctl + (a.parity ^ 1u);
-      nx->mism = 0ull;
-      nx->gctr = 0u;
-      nx->done = 0u;
-      nx->exc = 0u;
-      nx->nexc = 0u;
-      // early block: the host fills the run's records while it verifies
-      auto *e = reinterpret_cast<SpecEarly *>(a.hout);
-      const uint64_t *x = reinterpret_cast<const uint64_t *>(&r);
+    const uint64_t *x = reinterpret_cast<const uint64_t *>(&r);
 #pragma unroll
-      for (int q = 0; q < 7; q++) e->r0[q] = x[q];
-      e->stride = total;
-      e->eligible = d.eligible;
-      e->count = count;
-      __threadfence_system();
-      __hip_atomic_store(&e->seq, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    for (int q = 0; q < 7; q++) run_r0[q] = x[q];
+    run_total = total;
+    if (ok) {
+      SpecTabData *q = a.tabs + blockIdx.x;
+      q->crc0 = a.s + a.base + d.hl;
+      q->bm0 = a.bm;
+      q->copy_base = COPY ? a.copy_base : nullptr;
+      q->stride = d.stride;
+      q->copy_cap = COPY ? a.copy_cap : 0u;
+      q->nch = d.nch;
+      q->cs = a.cs;
+      q->cb0 = COPY ? d.cb0 : 0u;
+      q->pad = 0u;
+      stores_done();
     }
   }
   __syncthreads();
@@ -3007,23 +2988,55 @@ __global__ __launch_bounds__(1024) void spec_verify_kernel(SpecArgs a) {
   d.stride = rfl64(run.stride);
   d.off0 = rfl64(run.off0);
   d.seq0 = rfl64(run.seq0);
+  // Workgroup 0, last wave, lane 0: the point after the run (where the walk
+  // goes on, or what ends it) into the control slot, the next launch's slot
+  // zeroed, and the early block to the host (which fills the run's records
+  // while the kernel verifies it).  This wave joins the work loop after it;
+  // the other waves take the workgroup's tiles meanwhile (LDS tickets).
+  if (blockIdx.x == 0 && wv == 15u && lane == 0) {
+    if (d.eligible) {
+      uint32_t ts = kGridOn;
+      uint64_t ttot = 0;
+      hdfs_crc32c_packet tr{};
+      const uint64_t by_len = rem / d.stride;
+      // (the caller's record array holds count + 1 records only when the
+      // pass was not cut at max_count)
+      if (d.count == by_len && d.count < a.max_count) {  // the run ends with the stream's whole strides
+        const uint64_t pt = a.base + uint64_t(d.count) * d.stride;
+        if (pt >= a.len) {
+          ts = kGridMore;
+        } else {
+          stage_header(a.s, a.len, pt, 0u, win[1]);
+          const int tst = grid_frame(a.s, a.len, pt, win[1], a.proto, a.cs, a.ctype, tr, ttot);
+          ts = tst == frame::kStepMore ? kGridMore : tst == frame::kStepStop ? kGridStop : kGridOff;
+        }
+      }
+      const uint64_t *x = reinterpret_cast<const uint64_t *>(&tr);
+#pragma unroll
+      for (int q = 0; q < 7; q++) at_st(&ctl->tail[q], x[q]);
+      at_st(&ctl->tail_total, ttot);
+      at_st32(&ctl->tail_status, ts);
+    }
+    // the next launch's control slot starts at zero (this launch's was
+    // zeroed by the one before)
+    SpecCtl *nx = a.ctl + (a.parity ^ 1u);
+    nx->mism = 0ull;
+    nx->gctr = 0u;
+    nx->done = 0u;
+    nx->exc = 0u;
+    nx->nexc = 0u;
+    stores_done();
+    auto *e = reinterpret_cast<SpecEarly *>(a.hout);
+#pragma unroll
+    for (int q = 0; q < 7; q++) e->r0[q] = run_r0[q];
+    e->stride = run_total;
+    e->eligible = d.eligible;
+    e->count = d.count;
+    __threadfence_system();
+    __hip_atomic_store(&e->seq, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   if (!d.eligible) return;
   const bool v1 = d.v1 != 0u;
-  // this workgroup's copy of the closed-form table (read back with scalar
-  // loads: written with vector stores, acknowledged before the barrier)
-  if (t == 0) {
-    SpecTabData *q = a.tabs + blockIdx.x;
-    q->crc0 = a.s + a.base + d.hl;
-    q->bm0 = a.bm;
-    q->copy_base = COPY ? a.copy_base : nullptr;
-    q->stride = d.stride;
-    q->copy_cap = COPY ? a.copy_cap : 0u;
-    q->nch = d.nch;
-    q->cs = a.cs;
-    q->cb0 = COPY ? d.cb0 : 0u;
-    q->pad = 0u;
-    stores_done();
-  }
   // header checks: runs of 64 packets, run j on wave (j / G) % 16 of
   // workgroup j % G; lane l compares packet 64 j + l (packet 0 is the
   // prediction itself).  A wave's first run is loaded here and compared after
@@ -3047,7 +3060,6 @@ __global__ __launch_bounds__(1024) void spec_verify_kernel(SpecArgs a) {
     for (int q = 0; q < int(kSpecHdrBytes / 16); q++)
       h0[q] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 16u * q, 0, 0));
   }
-  __syncthreads();
   stamp(2);
   const SpecTab tab{(const CAS SpecTabData *)(a.tabs + blockIdx.x)};
   const uint64_t tiles = uint64_t(d.count) * d.T;

@@ -8,6 +8,7 @@ are kept.
 
     python tools/pmc_sq.py [out.json]   # driver
     python tools/pmc_sq.py run          # child
+    python tools/pmc_sq.py derive f.json  # recompute the derived figures
 
 Derived (per kernel): effective clock, instructions per 4 KiB round, the
 average number of vector-memory instructions in flight per wave
@@ -104,6 +105,22 @@ def main(out_path):
                 ns = big.pop("_ns")
                 res[k].update(big)
                 res[k][f"dispatch_ms_{tag}"] = round(ns / 1e6, 4)
+    derive(res)
+    res["method"] = ("rocprofv3 --pmc, one pass per counter group (tools/pmc_sq.py), kernel-trace only beside it; "
+                     "child: 3 compute then 3 verify launches over 512 x 128 MiB blocks, product library; per kernel "
+                     "the longest dispatch; SQ cycle counters in quad-cycles, FETCH/WRITE_SIZE in KiB (FETCH_SIZE "
+                     "doubled for traffic_over_alg, the gfx950 correction); GRBM counters summed over the 8 XCDs")
+    s = json.dumps(res, indent=1)
+    if out_path:
+        open(out_path, "w").write(s)
+    print(s)
+
+
+XCDS = 8  # MI355X: GRBM_GUI_ACTIVE / GRBM_COUNT come summed over the XCDs
+
+
+def derive(res):
+    """Per-kernel derived figures from the raw counters (in place)."""
     rounds = B * BLOCK // 4096
     for k, c in res.items():
         if k not in ("compute", "verify") or not c:
@@ -111,7 +128,7 @@ def main(out_path):
         der = {}
         ms = c.get("dispatch_ms_clk")
         if "GRBM_GUI_ACTIVE" in c and ms:
-            der["effective_clock_GHz"] = round(c["GRBM_GUI_ACTIVE"] / (ms * 1e-3) / 1e9, 3)
+            der["effective_clock_GHz"] = round(c["GRBM_GUI_ACTIVE"] / XCDS / (ms * 1e-3) / 1e9, 3)
         for n in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SALU", "SQ_INSTS_SMEM", "SQ_INSTS_VMEM_RD",
                   "SQ_INSTS_VMEM_WR", "SQ_INSTS_BRANCH"):
             if n in c:
@@ -132,18 +149,14 @@ def main(out_path):
             # (MI355X_MICROARCH.md, HBM/rocprofv3 section): doubled
             der["traffic_over_alg"] = round((2 * c.get("FETCH_SIZE", 0) + c.get("WRITE_SIZE", 0)) * 1024 / alg, 4)
         c["derived"] = der
-    res["method"] = ("rocprofv3 --pmc, one pass per counter group (tools/pmc_sq.py), kernel-trace only beside it; "
-                     "child: 3 compute then 3 verify launches over 512 x 128 MiB blocks, product library; per kernel "
-                     "the longest dispatch; SQ cycle counters in quad-cycles, FETCH/WRITE_SIZE in KiB (FETCH_SIZE "
-                     "doubled for traffic_over_alg, the gfx950 correction)")
-    s = json.dumps(res, indent=1)
-    if out_path:
-        open(out_path, "w").write(s)
-    print(s)
 
 
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "run":
         child()
+    elif len(sys.argv) > 2 and sys.argv[1] == "derive":  # re-derive a committed result (no GPU)
+        r = json.load(open(sys.argv[2]))
+        derive(r)
+        open(sys.argv[2], "w").write(json.dumps(r, indent=1))
     else:
         main(sys.argv[1] if len(sys.argv) > 1 else None)

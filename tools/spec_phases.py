@@ -12,7 +12,7 @@ Phases (per workgroup): 0 entry, 1 LDS tables filled + packet 0 decoded
 barrier), 3 header checks done (last barrier), 4 the last workgroup's final
 block published.  Per wave: loop start / end and rounds processed.
 
-    python tools/spec_phases.py [out.json]"""
+    python tools/spec_phases.py [out.json]     (SPH_LIB=<diag .so>: another build)"""
 import ctypes
 import json
 import os
@@ -27,7 +27,8 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 import diaglib  # noqa: E402
 import hadoofus_amd as h  # noqa: E402
 
-lib = h.load(diaglib.DIAG_LIB_PATH)
+# SPH_LIB: another diagnostic build (an A/B of a kernel change on one box)
+lib = h.load(os.environ.get("SPH_LIB") or diaglib.DIAG_LIB_PATH)
 D = diaglib.Diag(lib=lib)
 NBLK = 1024
 NWAVES = 4096
