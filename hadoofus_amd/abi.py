@@ -28,7 +28,7 @@ ERR_BAD_CHECKSUM = 29
 ERR_BAD_LASTPACKET = 32
 READ_ALL = -1  # read_packets: whole payloads, no client read window
 AGAIN = 1000   # read_packets: the destination filled before the read completed (resumable)
-ABI_VERSION = 4  # include/hadoofus_crc32c.h HDFS_CRC32C_ABI_VERSION these bindings are written for
+ABI_VERSION = 5  # include/hadoofus_crc32c.h HDFS_CRC32C_ABI_VERSION these bindings are written for
 MODE_COMPUTE, MODE_VERIFY = 0, 1
 PROTO_V1, PROTO_V2 = 1, 2
 SEG_BE, SEG_RAW, SEG_CRC32 = 1, 2, 4
@@ -138,6 +138,10 @@ def bind_product(lib):
     _bind(lib, "hdfs_crc32c_read_packets", _int,
           [_vp, _u64, _int, _u32, _int, ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(IoVec), _int,
            ctypes.POINTER(Packet), _sz, ctypes.POINTER(_sz), ctypes.POINTER(_u64), ctypes.POINTER(_u64)])
+    _bind(lib, "hdfs_crc32c_verify_packets_submit", _int,
+          [_vp, _u64, _int, _u32, _int, _sz, ctypes.POINTER(_vp)])
+    _bind(lib, "hdfs_crc32c_job_wait", _int,
+          [_vp, ctypes.POINTER(Packet), _sz, ctypes.POINTER(_sz), ctypes.POINTER(_u64)])
     _bind(lib, "hdfs_crc32c_abi_version", _int, [])
     _bind(lib, "hdfs_crc32c_session_create", _int, [ctypes.POINTER(_vp), _int, _u32, _int, _u64, _sz])
     _bind(lib, "hdfs_crc32c_session_buffer", _int, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_u64)])
@@ -415,6 +419,28 @@ def read_packets(dptr, nbytes, dst, dst_cap, proto=PROTO_V2, chunk_size=512, cty
     if rc < 0:
         _check(rc, lib)
     return rc, [arr[i].as_dict() for i in range(npk.value)], used.value, got.value
+
+
+class VerifyJob:
+    """An asynchronous hdfs_crc32c_verify_packets of a device-resident stream
+    (hdfs_crc32c_verify_packets_submit); wait() -> (rc, [packet dicts],
+    consumed), exactly verify_packets' result."""
+
+    def __init__(self, dptr, nbytes, proto=PROTO_V2, chunk_size=512, ctype=CSUM_CRC32C, max_pkts=None, lib=None):
+        self.lib = lib or load()
+        self.max_pkts = nbytes // (25 if proto == PROTO_V1 else 6) + 1 if max_pkts is None else max_pkts
+        self.job = _vp()
+        _check(self.lib.hdfs_crc32c_verify_packets_submit(dptr, nbytes, proto, chunk_size, ctype, self.max_pkts,
+                                                           ctypes.byref(self.job)), self.lib)
+
+    def wait(self):
+        arr = (Packet * max(1, self.max_pkts))()
+        npk, used = _sz(0), _u64(0)
+        job, self.job = self.job, None
+        rc = self.lib.hdfs_crc32c_job_wait(job, arr, self.max_pkts, ctypes.byref(npk), ctypes.byref(used))
+        if rc < 0:
+            _check(rc, self.lib)
+        return rc, [arr[i].as_dict() for i in range(npk.value)], used.value
 
 
 def compose_packets(data, offset_in_block=0, seqno=0, proto=PROTO_V2, ctype=CSUM_CRC32C, finish=False,

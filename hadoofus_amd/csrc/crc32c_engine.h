@@ -124,6 +124,24 @@ struct PieceSlot {
   hipEvent_t done = nullptr;           // compute stream: slot free again
 };
 
+// State of one speculative launch at a time (spec_verify_kernel): the
+// control-word ring [2] (zeroed when allocated), per-workgroup table copies,
+// the pinned landing area (SpecEarly | SpecFinal | exceptions) and the number
+// of launches so far (its parity picks the ring slot).  Asynchronous job
+// slots also own a stream and the run's bitmap / first-bad scratch.
+struct SpecSlot {
+  SpecCtl *ctl = nullptr;
+  SpecExc *exc = nullptr;
+  SpecTabData *tabs = nullptr;
+  uint8_t *h = nullptr, *hd = nullptr;
+  uint64_t n = 0;
+  hipStream_t stream = nullptr;
+  uint8_t *scratch = nullptr;
+  uint64_t scratch_cap = 0;
+};
+// asynchronous verify jobs in flight per device
+constexpr int kMaxJobs = 4;
+
 struct DevCtx {
   // published with release after every field below is set up; the unlocked
   // fast path of ctx_init reads it with acquire
@@ -222,14 +240,12 @@ struct DevCtx {
   hipStream_t r_stream = nullptr;  // device framing: record copies of runs with many exceptions
   std::vector<GridSlot> grid;
   // speculative one-launch verify (spec_verify_kernel; guarded by mu): the
-  // control-word ring [2] (zeroed when allocated), per-workgroup table
-  // copies, the pinned landing area (SpecEarly | SpecFinal) and the number of
-  // launches so far (its parity picks the ring slot)
-  SpecCtl *spec_ctl = nullptr;
-  SpecExc *spec_exc = nullptr;
-  SpecTabData *spec_tabs = nullptr;
-  uint8_t *spec_h = nullptr, *spec_hd = nullptr;
-  uint64_t spec_n = 0;
+  // synchronous calls' slot, and the slots of asynchronous jobs
+  // (hdfs_crc32c_verify_packets_submit), each with its own stream and
+  // bitmap / first-bad scratch
+  SpecSlot spec;
+  SpecSlot job_slot[kMaxJobs];
+  bool job_busy[kMaxJobs] = {};
   // client reads into host memory (hdfs_crc32c_read_packets with host
   // iovecs): the device staging the fused copy-out fills before the D2H
   // scatter; rd_mu is held across the verify and the scatter (taken before mu)

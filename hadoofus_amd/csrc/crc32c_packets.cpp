@@ -706,8 +706,8 @@ struct SpecResult {
 // (hdfs_crc32c_diag_spec_stats)
 uint64_t g_spec_stats[4] = {0, 0, 0, 0};
 
-int spec_alloc(DevCtx &c) {
-  if (c.spec_ctl) return HDFS_CRC32C_OK;
+int spec_alloc(DevCtx &c, SpecSlot &S) {
+  if (S.ctl) return HDFS_CRC32C_OK;
   SpecCtl *ctl = nullptr;
   SpecExc *exc = nullptr;
   SpecTabData *tabs = nullptr;
@@ -728,23 +728,23 @@ int spec_alloc(DevCtx &c) {
     if (h) (void)hipHostFree(h);
     return fail(HDFS_CRC32C_EHIP, "speculative verify buffers: %s", hipGetErrorString(e));
   }
-  c.spec_exc = exc;
-  c.spec_tabs = tabs;
-  c.spec_h = h;
-  c.spec_hd = hd;
-  c.spec_n = 0;
-  c.spec_ctl = ctl;
+  S.exc = exc;
+  S.tabs = tabs;
+  S.h = h;
+  S.hd = hd;
+  S.n = 0;
+  S.ctl = ctl;
   return HDFS_CRC32C_OK;
 }
 
 // Wait for a sequence number a kernel publishes to pinned memory as its last
 // memory operation; after 200 ms the stream synchronisation reports a fault.
-int poll_seq(DevCtx &c, const uint32_t *word, uint32_t seq, const char *what) {
+int poll_seq(const uint32_t *word, uint32_t seq, const char *what, hipStream_t st) {
   using clk = std::chrono::steady_clock;
   const auto t0 = clk::now();
   for (uint32_t spin = 1; __atomic_load_n(word, __ATOMIC_ACQUIRE) != seq; spin++) {
     if ((spin & 4095u) == 0 && clk::now() - t0 > std::chrono::milliseconds(200)) {
-      HIPCHK(hipStreamSynchronize(c.stream));
+      HIPCHK(hipStreamSynchronize(st));
       if (__atomic_load_n(word, __ATOMIC_ACQUIRE) != seq) return fail(HDFS_CRC32C_EHIP, "%s: no completion word", what);
       break;
     }
@@ -755,18 +755,30 @@ int poll_seq(DevCtx &c, const uint32_t *word, uint32_t seq, const char *what) {
   return HDFS_CRC32C_OK;
 }
 
-int spec_pass(DevCtx &c, const uint8_t *d, uint64_t len, uint64_t pos, uint32_t max_count, int proto, uint32_t cs,
-              int ctype, const CopyOut &co, uint64_t done_b, uint8_t *bm, uint32_t *fb, hdfs_crc32c_packet *dst,
-              SpecResult &res) {
-  res = SpecResult{};
-  int rc = spec_alloc(c);
+// One speculative launch in flight on slot S: what collecting it needs.
+struct SpecLaunch {
+  uint32_t seq = 0;
+  int grid = 0;
+  uint64_t pos = 0;
+  uint8_t *bm = nullptr;
+  hipStream_t st = nullptr;
+  std::chrono::steady_clock::time_point t0, t1;  // launch call (diagnostic trace)
+};
+
+int spec_launch(DevCtx &c, SpecSlot &S, hipStream_t st, const uint8_t *d, uint64_t len, uint64_t pos,
+                uint32_t max_count, int proto, uint32_t cs, int ctype, const CopyOut &co, uint64_t done_b, uint8_t *bm,
+                uint32_t *fb, SpecLaunch &L) {
+  int rc = spec_alloc(c, S);
   if (rc) return rc;
   const uint64_t left = len - pos;
   const uint64_t want = (left / kRoundBytes + 63) / 64;  // >= 4 rounds per wave (launch_verify_dyn)
-  const int grid = int(std::max<uint64_t>(1, std::min<uint64_t>(want, uint64_t(c.bulk_cus()))));
-  const uint32_t seq = next_grid_seq(c);
-  auto *early = reinterpret_cast<SpecEarly *>(c.spec_h);
-  auto *fin = reinterpret_cast<SpecFinal *>(c.spec_h + sizeof(SpecEarly));
+  L.grid = int(std::max<uint64_t>(1, std::min<uint64_t>(want, uint64_t(c.bulk_cus()))));
+  L.seq = next_grid_seq(c);
+  L.pos = pos;
+  L.bm = bm;
+  L.st = st;
+  auto *early = reinterpret_cast<SpecEarly *>(S.h);
+  auto *fin = reinterpret_cast<SpecFinal *>(S.h + sizeof(SpecEarly));
   __atomic_store_n(&early->seq, 0u, __ATOMIC_RELEASE);
   __atomic_store_n(&fin->seq, 0u, __ATOMIC_RELEASE);
   SpecArgs a{};
@@ -785,25 +797,41 @@ int spec_pass(DevCtx &c, const uint8_t *d, uint64_t len, uint64_t pos, uint32_t 
   a.copy_cap = co.dst ? co.cap - done_b : 0u;
   a.gtab = c.d_tab_main_t[ctype == HDFS_CRC32C_CSUM_CRC32 ? 1 : 0];
   a.fb = fb;
-  a.ctl = c.spec_ctl;
-  a.exc = c.spec_exc;
-  a.parity = uint32_t(c.spec_n & 1u);
-  a.seq = seq;
+  a.ctl = S.ctl;
+  a.exc = S.exc;
+  a.parity = uint32_t(S.n & 1u);
+  a.seq = L.seq;
   a.tune = tile_tune() | (g_spec_pool_min << 16);
-  a.hout = c.spec_hd;
-  a.tabs = c.spec_tabs;
+  a.hout = S.hd;
+  a.tabs = S.tabs;
   a.stamps = kDiag ? g_diag : nullptr;
-  using clk = std::chrono::steady_clock;
-  const auto t0 = clk::now();
-  HIPCHK(launch_spec_verify(a, grid, co.dst ? 1 : 0, c.stream));
-  c.spec_n++;
+  L.t0 = std::chrono::steady_clock::now();
+  HIPCHK(launch_spec_verify(a, L.grid, co.dst ? 1 : 0, st));
+  S.n++;
   if (kDiag) g_spec_stats[0]++;
-  const auto t1 = clk::now();
-  if ((rc = poll_seq(c, &early->seq, seq, "speculative verify"))) return rc;
+  L.t1 = std::chrono::steady_clock::now();
+  return HDFS_CRC32C_OK;
+}
+
+// The host side of a speculative launch: packet 0's record and the run's
+// records predicted from it (filled while the kernel verifies), then the
+// final block: exceptions, verdicts, what follows the run.  Not taken
+// (res.taken false) when packet 0 starts no run or a header left the
+// prediction -- the caller frames the run the regular way.
+int spec_collect(DevCtx &c, SpecSlot &S, const SpecLaunch &L, const CopyOut &co, hdfs_crc32c_packet *dst,
+                 SpecResult &res) {
+  (void)c;
+  res = SpecResult{};
+  using clk = std::chrono::steady_clock;
+  auto *early = reinterpret_cast<SpecEarly *>(S.h);
+  auto *fin = reinterpret_cast<SpecFinal *>(S.h + sizeof(SpecEarly));
+  const uint64_t pos = L.pos;
+  int rc;
+  if ((rc = poll_seq(&early->seq, L.seq, "speculative verify", L.st))) return rc;
   const auto t2 = clk::now();
   SpecEarly E;
   std::memcpy(&E, early, sizeof(E));
-  if (!E.eligible) return HDFS_CRC32C_OK;  // every workgroup has returned; the regular pass queues behind them
+  if (!E.eligible) return HDFS_CRC32C_OK;  // every workgroup returns at once; work queued behind it runs next
   if (kDiag) g_spec_stats[1]++;
   hdfs_crc32c_packet r0;
   std::memcpy(&r0, E.r0, sizeof(r0));
@@ -816,11 +844,11 @@ int spec_pass(DevCtx &c, const uint8_t *d, uint64_t len, uint64_t pos, uint32_t 
     r.seqno = r0.seqno + int64_t(k);
   }
   const auto t3 = clk::now();
-  if ((rc = poll_seq(c, &fin->seq, seq, "speculative verify"))) return rc;
+  if ((rc = poll_seq(&fin->seq, L.seq, "speculative verify", L.st))) return rc;
   if (g_dstream_trace) {  // diagnostic: where a speculative launch spends its time (us)
     auto us = [](clk::time_point x, clk::time_point y) { return std::chrono::duration<double, std::micro>(y - x).count(); };
-    std::fprintf(stderr, "dstream spec grid=%d count=%u launch_us=%.1f early_us=%.1f fill_us=%.1f final_us=%.1f\n", grid,
-                 E.count, us(t0, t1), us(t1, t2), us(t2, t3), us(t3, clk::now()));
+    std::fprintf(stderr, "dstream spec grid=%d count=%u launch_us=%.1f early_us=%.1f fill_us=%.1f final_us=%.1f\n", L.grid,
+                 E.count, us(L.t0, L.t1), us(L.t1, t2), us(t2, t3), us(t3, clk::now()));
   }
   SpecFinal F;
   std::memcpy(&F, fin, sizeof(F));
@@ -831,7 +859,7 @@ int spec_pass(DevCtx &c, const uint8_t *d, uint64_t len, uint64_t pos, uint32_t 
   res.taken = true;
   if (kDiag) g_spec_stats[2]++;
   // same-size packets whose headers left the prediction: their own records
-  const auto *hx = reinterpret_cast<const SpecExc *>(c.spec_h + 256);
+  const auto *hx = reinterpret_cast<const SpecExc *>(S.h + 256);
   for (uint32_t j = 0; j < F.nexc; j++) {  // (more than kSpecExcMax raised exc)
     SpecExc x;
     std::memcpy(&x, hx + j, sizeof(x));
@@ -845,8 +873,8 @@ int spec_pass(DevCtx &c, const uint8_t *d, uint64_t len, uint64_t pos, uint32_t 
     // behind it, has run)
     const uint32_t nch = uint32_t(r0.crc_len) / 4u, nb = (nch + 7u) / 8u;
     std::vector<uint8_t> bmh(size_t(E.count) * nb);
-    HIPCHK(hipMemcpyAsync(bmh.data(), bm, bmh.size(), hipMemcpyDeviceToHost, c.stream));
-    HIPCHK(hipStreamSynchronize(c.stream));
+    HIPCHK(hipMemcpyAsync(bmh.data(), L.bm, bmh.size(), hipMemcpyDeviceToHost, L.st));
+    HIPCHK(hipStreamSynchronize(L.st));
     for (uint32_t k = 0; k < E.count; k++) {
       const uint8_t *b = bmh.data() + size_t(k) * nb;
       uint32_t bad = 0;
@@ -884,6 +912,17 @@ int spec_pass(DevCtx &c, const uint8_t *d, uint64_t len, uint64_t pos, uint32_t 
   return HDFS_CRC32C_OK;
 }
 
+// A synchronous speculative pass on the engine stream.
+int spec_pass(DevCtx &c, const uint8_t *d, uint64_t len, uint64_t pos, uint32_t max_count, int proto, uint32_t cs,
+              int ctype, const CopyOut &co, uint64_t done_b, uint8_t *bm, uint32_t *fb, hdfs_crc32c_packet *dst,
+              SpecResult &res) {
+  res = SpecResult{};
+  SpecLaunch L;
+  int rc = spec_launch(c, c.spec, c.stream, d, len, pos, max_count, proto, cs, ctype, co, done_b, bm, fb, L);
+  if (rc) return rc;
+  return spec_collect(c, c.spec, L, co, dst, res);
+}
+
 // A client read is decided by a packet that ends apply_read_window's walk
 // -- an empty packet, a lastPacketInBlock packet, or one that starts past
 // the read (UNEXPECTED_READ_OFFSET) -- so once a pass holds one, no later
@@ -915,7 +954,7 @@ bool read_window_over(const hdfs_crc32c_packet *p, size_t n, const CopyOut &co, 
 
 int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs, int ctype, size_t max_pkts,
               bool verify, const CopyOut &co, hdfs_crc32c_packet *dst, size_t *nout, uint64_t *consumed,
-              uint64_t *payload_out) {
+              uint64_t *payload_out, bool allow_spec = true) {
   *nout = 0;
   *consumed = 0;
   verify = verify && ctype != HDFS_CRC32C_CSUM_NULL;
@@ -957,7 +996,7 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
   // meets a header off its prediction (an irregular stream: later passes
   // frame); last_spec = the call's last command was a taken speculative
   // launch, whose completion word the host has seen
-  bool try_spec = verify && g_spec, last_spec = false;
+  bool try_spec = verify && g_spec && allow_spec, last_spec = false;
   using clk = std::chrono::steady_clock;
   const auto t0 = clk::now();
   double t_enq = 0, t_sync = 0, t_fill = 0;
@@ -1419,6 +1458,150 @@ int verify_packets_impl(const uint8_t *stream, uint64_t len, int proto, uint32_t
   if (npkts) *npkts = recs.size();
   if (consumed) *consumed = used;
   return first_error(recs.data(), recs.size());
+}
+
+// ---- asynchronous verify jobs (hdfs_crc32c_verify_packets_submit / _wait) ----
+// A device-resident run's speculative launch goes out on a job slot's own
+// stream at submit; the wait collects it and, when the launch did not take
+// the whole stream (another packet size follows, more packets than one pass,
+// or no run at all), frames and verifies the rest synchronously -- so the
+// result is hdfs_crc32c_verify_packets' in every case.  Jobs on different
+// slots overlap on the GPU: one launch's ramp and tail under another's
+// steady state (a datanode verifying a stream of blocks).
+}  // namespace
+}  // namespace hdfs_crc32c
+
+struct hdfs_crc32c_job {
+  int dev = -1, slot = -1;
+  const uint8_t *d = nullptr;
+  uint64_t len = 0;
+  int proto = 0, ctype = 0;
+  uint32_t cs = 0;
+  size_t max_pkts = 0;
+  bool launched = false;
+  hdfs_crc32c::SpecLaunch L;
+};
+
+namespace hdfs_crc32c {
+namespace {
+
+int job_submit(const uint8_t *d, uint64_t len, int proto, uint32_t cs, int ctype, size_t max_pkts,
+               hdfs_crc32c_job **out) {
+  const int dev = stream_device(d);
+  if (dev < 0) return fail(HDFS_CRC32C_EINVAL, "asynchronous verify takes device-resident streams");
+  DevCtx *cp = nullptr;
+  int rc;
+  if ((rc = ctx_init(dev, &cp))) return rc;
+  DevCtx &c = *cp;
+  DeviceGuard g(c.dev);
+  std::lock_guard<std::mutex> lk(c.mu);
+  int slot = -1;
+  for (int i = 0; i < kMaxJobs; i++)
+    if (!c.job_busy[i]) {
+      slot = i;
+      break;
+    }
+  if (slot < 0) return fail(HDFS_CRC32C_EINVAL, "%d verify jobs already in flight on device %d", kMaxJobs, dev);
+  auto *j = new (std::nothrow) hdfs_crc32c_job;
+  if (!j) return fail(HDFS_CRC32C_ENOMEM, "job");
+  j->dev = dev;
+  j->slot = slot;
+  j->d = d;
+  j->len = len;
+  j->proto = proto;
+  j->ctype = ctype;
+  j->cs = cs;
+  j->max_pkts = max_pkts;
+  // the speculative launch when the stream can hold a run it takes; else
+  // the wait does the whole call
+  const bool spec = ctype != HDFS_CRC32C_CSUM_NULL && g_spec && max_pkts >= 2 && len > kSmallRunBytes;
+  if (spec) {
+    SpecSlot &S = c.job_slot[slot];
+    if (!S.stream) {
+      if (hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking) != hipSuccess) {
+        (void)hipGetLastError();
+        delete j;
+        return fail(HDFS_CRC32C_EHIP, "job stream");
+      }
+    }
+    const uint32_t count = uint32_t(std::min<uint64_t>({uint64_t(max_pkts), kGridMaxCount, len / 6 + 1}));
+    const uint64_t bm_cap = align_up(len / 32 + count + 64, 256), need = bm_cap + uint64_t(count) * 4u + 256u;
+    if (need > S.scratch_cap) {
+      if (S.scratch) (void)hipFree(S.scratch);
+      S.scratch = nullptr;
+      S.scratch_cap = 0;
+      if (hipMalloc(&S.scratch, need) != hipSuccess) {
+        (void)hipGetLastError();
+        delete j;
+        return fail(HDFS_CRC32C_ENOMEM, "job scratch of %llu bytes", (unsigned long long)need);
+      }
+      S.scratch_cap = need;
+    }
+    rc = spec_launch(c, S, S.stream, d, len, 0, count, proto, cs, ctype, CopyOut{}, 0, S.scratch,
+                     reinterpret_cast<uint32_t *>(S.scratch + bm_cap), j->L);
+    if (rc) {
+      delete j;
+      return rc;
+    }
+    j->launched = true;
+  }
+  c.job_busy[slot] = true;
+  *out = j;
+  return HDFS_CRC32C_OK;
+}
+
+int job_wait(hdfs_crc32c_job *j, hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts, uint64_t *consumed) {
+  DevCtx *cp = nullptr;
+  int rc;
+  if ((rc = ctx_init(j->dev, &cp))) return rc;
+  DevCtx &c = *cp;
+  DeviceGuard g(c.dev);
+  std::lock_guard<std::mutex> lk(c.mu);
+  struct Release {  // the slot is free again on every return path
+    DevCtx &c;
+    hdfs_crc32c_job *j;
+    ~Release() {
+      c.job_busy[j->slot] = false;
+      delete j;
+    }
+  } rel{c, j};
+  const size_t cap = std::min(max_pkts, j->max_pkts);
+  size_t n = 0;
+  uint64_t used = 0, from = 0;
+  bool done = false, allow_spec = true;
+  if (j->launched) {
+    SpecResult sr;
+    std::vector<hdfs_crc32c_packet> recs(std::max<size_t>(1, std::min<uint64_t>(j->max_pkts, kGridMaxCount) + 1));
+    if ((rc = spec_collect(c, c.job_slot[j->slot], j->L, CopyOut{}, recs.data(), sr))) return rc;
+    if (sr.taken) {
+      if (sr.recorded > cap) return fail(HDFS_CRC32C_EINVAL, "wait: %zu records, room for %zu", size_t(sr.recorded), cap);
+      std::memcpy(pkts, recs.data(), size_t(sr.recorded) * sizeof(hdfs_crc32c_packet));
+      n = sr.recorded;
+      used = sr.consumed;
+      from = sr.next;
+      done = sr.end || n >= cap;
+    } else {
+      allow_spec = false;  // this stream has no run the launch takes: frame it
+    }
+  }
+  if (!done && from < j->len) {
+    // the rest (or all) of the stream, synchronously on the engine stream
+    size_t n2 = 0;
+    uint64_t used2 = 0;
+    rc = grid_walk(c, j->d + from, j->len - from, j->proto, j->cs, j->ctype, cap - n, true, CopyOut{}, pkts + n, &n2,
+                   &used2, nullptr, allow_spec);
+    if (kDiag) {
+      const int r2 = device_checks("verify job");
+      if (r2) return r2;
+    }
+    if (rc) return rc;
+    for (size_t k = 0; k < n2; k++) pkts[n + k].stream_off += from;
+    n += n2;
+    if (n2 || used2) used = from + used2;
+  }
+  *npkts = n;
+  *consumed = used;
+  return first_error(pkts, n);
 }
 
 // ---- client reads into host memory (hdfs_crc32c_read_packets, host iovecs) ----
@@ -1908,6 +2091,31 @@ int hdfs_crc32c_read_packets(const void *stream, uint64_t len, int proto, uint32
     rl -= int64_t(got);
     if (n_all >= max_pkts && i + 1 < iovcnt) return rc;  // no room for more records: the caller resumes
   }
+  return rc;
+}
+
+int hdfs_crc32c_verify_packets_submit(const void *stream, uint64_t len, int proto, uint32_t chunk_size, int ctype,
+                                      size_t max_pkts, hdfs_crc32c_job **job) {
+  if (!job) return fail(HDFS_CRC32C_EINVAL, "null job");
+  *job = nullptr;
+  int rc = check_framing_args(proto, chunk_size, ctype, g_err, sizeof(g_err));
+  if (rc) return rc;
+  if (!stream || !len) return fail(HDFS_CRC32C_EINVAL, "empty stream");
+  return job_submit(static_cast<const uint8_t *>(stream), len, proto, chunk_size, ctype, max_pkts, job);
+}
+
+int hdfs_crc32c_job_wait(hdfs_crc32c_job *job, hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts,
+                         uint64_t *consumed) {
+  if (npkts) *npkts = 0;
+  if (consumed) *consumed = 0;
+  if (!job) return fail(HDFS_CRC32C_EINVAL, "null job");
+  if (max_pkts && !pkts) return fail(HDFS_CRC32C_EINVAL, "null packet array");
+  size_t n = 0;
+  uint64_t used = 0;
+  const int rc = job_wait(job, pkts, max_pkts, &n, &used);
+  if (rc < 0) return rc;
+  if (npkts) *npkts = n;
+  if (consumed) *consumed = used;
   return rc;
 }
 

@@ -70,8 +70,11 @@ uint32_t _hdfs_sw_crc32c(uint32_t crc, const void *buf, unsigned len);
  * hdfs_crc32c_abi_version() with the version they were written for.
  *   3: round 3 (unversioned exports)
  *   4: hdfs_crc32c_verify_packets_copy -> hdfs_crc32c_read_packets (iovecs,
- *      resumable reads); versioned exports */
-#define HDFS_CRC32C_ABI_VERSION 4
+ *      resumable reads); versioned exports
+ *   5: hdfs_crc32c_read_packets: a client read ends at its first error (bad
+ *      CRCs included), host-memory iovecs and streams; asynchronous verify
+ *      jobs (hdfs_crc32c_verify_packets_submit / hdfs_crc32c_job_wait) */
+#define HDFS_CRC32C_ABI_VERSION 5
 int hdfs_crc32c_abi_version(void);
 
 const char *hdfs_crc32c_last_error(void);
@@ -233,8 +236,8 @@ int hdfs_crc32c_verify_packets(const void *stream, uint64_t len, int proto, uint
  *     (the host pipeline of hdfs_crc32c_verify_packets), then their bytes
  *     memcpy()ed into the iovecs as the reference does (:2516);
  *   - host stream, device buffers: EINVAL.
- * (Host buffers since round 5; the signature and symbol are unchanged, a
- * round-4 library refuses them with EINVAL.)
+ * (Host buffers since ABI 5; the signature is unchanged, a version-4
+ * library refuses them with EINVAL.)
  *
  * iov / iovcnt: the destination, buffers filled in order (the reference's
  * iovec array, :2509-2537), all device memory of the stream's device or all
@@ -298,6 +301,25 @@ typedef struct hdfs_crc32c_iovec {
 int hdfs_crc32c_read_packets(const void *stream, uint64_t len, int proto, uint32_t chunk_size, int ctype,
     int64_t client_offset, int64_t read_len, const hdfs_crc32c_iovec *iov, int iovcnt,
     hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts, uint64_t *consumed, uint64_t *delivered);
+
+/* Asynchronous hdfs_crc32c_verify_packets of a DEVICE-resident stream (a
+ * datanode verifying a stream of received blocks): submit launches the
+ * verify and returns; hdfs_crc32c_job_wait returns exactly what
+ * hdfs_crc32c_verify_packets would (records, consumed, first error) and
+ * releases the job.  Up to 4 jobs per device are in flight at once (a fifth
+ * submit is EINVAL); jobs overlap on the GPU, so one block's launch ramp and
+ * tail run under another's steady state.  A run of equal packets is
+ * verified by the speculative launch at submit; whatever it does not take
+ * (another packet size, more than 65 536 packets, no run at all) is framed
+ * and verified inside the wait.  The stream's bytes must stay unchanged, and
+ * written before the submit (synchronise whatever wrote them), until the
+ * wait returns; every submitted job must be waited for.  max_pkts at the
+ * wait must be at least the submit's. */
+typedef struct hdfs_crc32c_job hdfs_crc32c_job;
+int hdfs_crc32c_verify_packets_submit(const void *stream, uint64_t len, int proto, uint32_t chunk_size, int ctype,
+    size_t max_pkts, hdfs_crc32c_job **job);
+int hdfs_crc32c_job_wait(hdfs_crc32c_job *job, hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts,
+    uint64_t *consumed);
 
 /* ---- write path: outgoing data packets ---------------------------------- */
 /* One outgoing data packet, as _send_packet sizes it and

@@ -1,0 +1,114 @@
+"""Asynchronous verify jobs (round 5): hdfs_crc32c_verify_packets_submit /
+hdfs_crc32c_job_wait on device-resident packet streams.  Every job's result
+equals the oracle's verify (oracle_verify_packets: src/datanode.c:2345-2494,
+2931-2963) -- records, verdicts, consumed bytes, status -- whether the
+speculative launch at submit took the run, handed it back (a header off the
+run), was never tried (no run of whole-chunk packets, a short stream), or
+took only part of it (more packets than one pass, another size after it);
+with four jobs in flight at once, waited in any order, and with synchronous
+calls in between."""
+import numpy as np
+import pytest
+
+from packet_stream import CSUM_CRC32, CSUM_CRC32C, build_stream
+
+BAD = 29
+
+
+def _dev(engine, s, shift=0):
+    buf = engine.DeviceBuffer(len(s) + shift + 64)
+    buf.fill(0)
+    buf.upload(np.frombuffer(s, np.uint8), offset=shift)
+    engine.device_sync()
+    return buf, buf.ptr + shift
+
+
+def _cases(oracle):
+    out = []
+    rng = np.random.default_rng(41)
+
+    def add(name, proto, cs, ctype, dl, **kw):
+        corrupt = sorted({(int(k), int(rng.integers(0, max(1, dl[k] // cs)))) for k in rng.integers(0, len(dl), 4)})
+        s, _ = build_stream(oracle.crc32c, proto, cs, ctype, dl, seed=len(dl) + cs, corrupt=corrupt, **kw)
+        out.append((name, proto, cs, ctype, s))
+
+    add("v2_block", 2, 512, CSUM_CRC32C, [65536] * 128)
+    add("v1_crc32", 1, 512, CSUM_CRC32, [65536] * 100, last_empty=False)
+    add("v2_size_break", 2, 512, CSUM_CRC32C, [65536] * 60 + [30000] + [65536] * 40)
+    add("v2_other_size_after_run", 2, 512, CSUM_CRC32C, [65536] * 80 + [4096] * 30)
+    add("v2_many_exceptions", 2, 512, CSUM_CRC32C, [65536] * 100, seqnos=[3 * k for k in range(100)])
+    add("v2_partial_chunks_not_eligible", 2, 512, CSUM_CRC32C, [40000] * 200)
+    add("v2_short_stream", 2, 512, CSUM_CRC32C, [65536] * 20)
+    add("v2_cs4096", 2, 4096, CSUM_CRC32C, [65536] * 100)
+    s, _ = build_stream(oracle.crc32c, 2, 512, CSUM_CRC32C, [65536] * 90, seed=9)
+    w = oracle.verify_packets(s)[1]
+    out.append(("v2_cut_in_next", 2, 512, CSUM_CRC32C, s[:w[-1]["stream_off"] - 1000]))
+    bad_tail = bytearray(s)
+    e = w[-1]["stream_off"]
+    bad_tail[e:e + 4] = (0x7FFFFFFF).to_bytes(4, "big")  # plen > 1 GiB: PACKET_SIZE
+    out.append(("v2_framing_error_tail", 2, 512, CSUM_CRC32C, bytes(bad_tail)))
+    return out
+
+
+@pytest.mark.gpu
+def test_gpu_jobs_vs_oracle(engine, oracle):
+    """Four jobs in flight, waited in reverse order, then the next four: each
+    equals the oracle's verify and the synchronous call's."""
+    cases = _cases(oracle)
+    bufs = [_dev(engine, c[4], i % 3) for i, c in enumerate(cases)]
+    want = [oracle.verify_packets(c[4], c[1], c[2], c[3]) for c in cases]
+    for i0 in range(0, len(cases), 4):
+        idx = list(range(i0, min(i0 + 4, len(cases))))
+        jobs = {i: engine.VerifyJob(bufs[i][1], len(cases[i][4]), cases[i][1], cases[i][2], cases[i][3]) for i in idx}
+        for i in reversed(idx):
+            got = jobs[i].wait()
+            assert got == want[i], cases[i][0]
+            assert engine.verify_packets(None, cases[i][1], cases[i][2], cases[i][3], dptr=bufs[i][1],
+                                         nbytes=len(cases[i][4])) == want[i], cases[i][0]
+    for b, _ in bufs:
+        b.free()
+
+
+@pytest.mark.gpu
+def test_gpu_jobs_many_passes(engine, oracle):
+    """70 000 packets of 2 KiB: the launch at submit takes the first 65 536,
+    the wait verifies the rest (a second speculative launch) and the 1 000-B
+    tail packet; corruption on both sides of the pass edge."""
+    dl = [2048] * 70000 + [1000]
+    s, _ = build_stream(oracle.crc32c, 2, 512, CSUM_CRC32C, dl, seed=77,
+                        corrupt=[(5, 0), (65535, 3), (65536, 2), (69999, 1)])
+    mp = len(dl) + 2
+    want = oracle.verify_packets(s, max_pkts=mp)
+    keep, p = _dev(engine, s)
+    assert engine.VerifyJob(p, len(s), max_pkts=mp).wait() == want
+    # max_pkts inside the first pass: the records stop there, as the synchronous call's
+    w2 = oracle.verify_packets(s, max_pkts=1000)
+    assert engine.VerifyJob(p, len(s), max_pkts=1000).wait() == w2
+    keep.free()
+
+
+@pytest.mark.gpu
+def test_gpu_jobs_limit_and_interleaving(engine, oracle):
+    """A fifth job while four are in flight is refused (and the four still
+    complete correctly); synchronous verifies and reads run between a submit
+    and its wait; a waited slot takes a new job."""
+    dl = [65536] * 100
+    s, _ = build_stream(oracle.crc32c, 2, 512, CSUM_CRC32C, dl, seed=3, corrupt=[(50, 7)])
+    want = oracle.verify_packets(s)
+    bufs = [_dev(engine, s, i) for i in range(5)]
+    jobs = [engine.VerifyJob(p, len(s)) for _, p in bufs[:4]]
+    with pytest.raises(engine.CRC32CError):
+        engine.VerifyJob(bufs[4][1], len(s))
+    # synchronous calls while the jobs are in flight
+    assert engine.verify_packets(None, dptr=bufs[4][1], nbytes=len(s)) == want
+    dst = engine.DeviceBuffer(sum(dl))
+    rd = engine.read_packets(bufs[4][1], len(s), dst.ptr, sum(dl), client_offset=0, read_len=sum(dl))
+    wr = oracle.read_packets(s, 0, sum(dl))
+    assert rd[:3] == wr[:3] and dst.download(rd[3]).tobytes() == wr[3]
+    assert jobs[1].wait() == want
+    j5 = engine.VerifyJob(bufs[4][1], len(s))
+    for j in (jobs[0], jobs[2], jobs[3], j5):
+        assert j.wait() == want
+    dst.free()
+    for b, _ in bufs:
+        b.free()

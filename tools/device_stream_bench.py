@@ -224,6 +224,60 @@ def resumed_reads(ptr, n, npk, payload, reps=3):
     return res
 
 
+def pipelined_blocks(blk, nblk, payload, nblocks=16, inflight=4, reps=3):
+    """A datanode verifying a stream of received blocks: nblocks device-
+    resident 128 MiB block transfers verified back to back, synchronously
+    (hdfs_crc32c_verify_packets per block) and as asynchronous jobs with up to
+    `inflight` in flight (hdfs_crc32c_verify_packets_submit / _job_wait: one
+    block's launch ramp and tail overlap another's steady state).  Best of
+    reps; per-block time and aggregate GiB/s of payload."""
+    devs = []
+    for _ in range(nblocks):
+        d = h.DeviceBuffer(blk.nbytes + 64)
+        d.upload(blk)
+        devs.append(d)
+    h.device_sync()
+    n = blk.nbytes
+    arrs = [(h.abi.Packet * (nblk + 8))() for _ in range(inflight)]
+    cnt, used = ctypes.c_size_t(0), ctypes.c_uint64(0)
+
+    def sync_all():
+        for d in devs:
+            rc = lib.hdfs_crc32c_verify_packets(d.ptr, n, h.PROTO_V2, 512, h.CSUM_CRC32C, arrs[0], nblk + 8,
+                                                ctypes.byref(cnt), ctypes.byref(used))
+            assert rc == 0 and cnt.value == nblk, (rc, cnt.value)
+
+    def jobs_all():
+        q = []
+        for i, d in enumerate(devs):
+            if len(q) == inflight:
+                j, a = q.pop(0)
+                rc = lib.hdfs_crc32c_job_wait(j, a, nblk + 8, ctypes.byref(cnt), ctypes.byref(used))
+                assert rc == 0 and cnt.value == nblk and used.value == n, (rc, cnt.value)
+            j = ctypes.c_void_p()
+            rc = lib.hdfs_crc32c_verify_packets_submit(d.ptr, n, h.PROTO_V2, 512, h.CSUM_CRC32C, nblk + 8,
+                                                       ctypes.byref(j))
+            assert rc == 0, rc
+            q.append((j, arrs[i % inflight]))
+        for j, a in q:
+            rc = lib.hdfs_crc32c_job_wait(j, a, nblk + 8, ctypes.byref(cnt), ctypes.byref(used))
+            assert rc == 0 and cnt.value == nblk and used.value == n, (rc, cnt.value)
+
+    res = {"blocks": nblocks, "inflight": inflight}
+    for name, fn in (("sync", sync_all), ("jobs", jobs_all)):
+        fn()
+        best = 1e9
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fn()
+            best = min(best, time.perf_counter() - t0)
+        res[name] = {"us_per_block": round(best / nblocks * 1e6, 1),
+                     "GiBps": round(nblocks * payload / best / 2**30, 1)}
+    for d in devs:
+        d.free()
+    return res
+
+
 def block_and_run(plan_GiBps=None):
     """bench.py's extra.device_stream: the 1 GiB run and one 128 MiB block,
     end to end per call, beside a verify plan over the same packets (same
@@ -243,9 +297,13 @@ def block_and_run(plan_GiBps=None):
     dev = run_size(out, "block_128MiB", blk, 2048, nblk, 10)
     out["block_128MiB"]["client_reads"] = resumed_reads(dev.ptr, blk.nbytes, nblk, 2048 * 65536)
     dev.free()
+    out["block_128MiB"]["stream_of_blocks"] = pipelined_blocks(blk, nblk, 2048 * 65536)
     if plan_GiBps:
         for k in ("run_1GiB", "block_128MiB"):
             out[k]["frac_of_headline"] = round(out[k]["GiBps"] / plan_GiBps, 3)
+        for k in ("sync", "jobs"):
+            sb = out["block_128MiB"]["stream_of_blocks"][k]
+            sb["frac_of_headline"] = round(sb["GiBps"] / plan_GiBps, 3)
     out["note"] = ("hdfs_crc32c_verify_packets on v2 packet runs resident in HBM (64 KiB packets, 512 B chunks, "
                    "CRC32C), C call, records to host, best of N; plan_* = a verify plan over the same packets' "
                    "segments (table given), frac_of_plan = plan time / call time at the same size; "
@@ -321,6 +379,7 @@ def main():
     dev = run_size(out, "block_128MiB", blk, 2048, nblk, 10)
     out["block_128MiB"]["client_reads"] = resumed_reads(dev.ptr, blk.nbytes, nblk, 2048 * 65536)
     dev.free()
+    out["block_128MiB"]["stream_of_blocks"] = pipelined_blocks(blk, nblk, 2048 * 65536)
     print(json.dumps(out))
 
 
