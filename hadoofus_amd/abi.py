@@ -142,6 +142,10 @@ def bind_product(lib):
           [_vp, _u64, _int, _u32, _int, _sz, ctypes.POINTER(_vp)])
     _bind(lib, "hdfs_crc32c_job_wait", _int,
           [_vp, ctypes.POINTER(Packet), _sz, ctypes.POINTER(_sz), ctypes.POINTER(_u64)])
+    _bind(lib, "hdfs_crc32c_verify_blocks_submit", _int,
+          [ctypes.POINTER(_vp), ctypes.POINTER(_u64), _sz, _int, _u32, _int, _sz, ctypes.POINTER(_vp)])
+    _bind(lib, "hdfs_crc32c_job_wait_blocks", _int,
+          [_vp, ctypes.POINTER(Packet), _sz, ctypes.POINTER(_sz), ctypes.POINTER(_u64), ctypes.POINTER(_int)])
     _bind(lib, "hdfs_crc32c_abi_version", _int, [])
     _bind(lib, "hdfs_crc32c_session_create", _int, [ctypes.POINTER(_vp), _int, _u32, _int, _u64, _sz])
     _bind(lib, "hdfs_crc32c_session_buffer", _int, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_u64)])
@@ -441,6 +445,35 @@ class VerifyJob:
         if rc < 0:
             _check(rc, self.lib)
         return rc, [arr[i].as_dict() for i in range(npk.value)], used.value
+
+
+class VerifyBlocksJob:
+    """Up to 16 device-resident block streams verified in one launch
+    (hdfs_crc32c_verify_blocks_submit); wait() -> (rc, [(rc_b, [packet
+    dicts], consumed_b) per block]), each block's entry exactly
+    verify_packets' result for it."""
+
+    def __init__(self, blocks, proto=PROTO_V2, chunk_size=512, ctype=CSUM_CRC32C, max_pkts=None, lib=None):
+        """blocks: [(dptr, nbytes), ...]"""
+        self.lib = lib or load()
+        self.n = len(blocks)
+        big = max(n for _, n in blocks)
+        self.max_pkts = big // (25 if proto == PROTO_V1 else 6) + 1 if max_pkts is None else max_pkts
+        ptrs = (_vp * self.n)(*[p for p, _ in blocks])
+        lens = (_u64 * self.n)(*[n for _, n in blocks])
+        self.job = _vp()
+        _check(self.lib.hdfs_crc32c_verify_blocks_submit(ptrs, lens, self.n, proto, chunk_size, ctype, self.max_pkts,
+                                                          ctypes.byref(self.job)), self.lib)
+
+    def wait(self):
+        arr = (Packet * max(1, self.max_pkts * self.n))()
+        npk, used, rcs = (_sz * self.n)(), (_u64 * self.n)(), (_int * self.n)()
+        job, self.job = self.job, None
+        rc = self.lib.hdfs_crc32c_job_wait_blocks(job, arr, self.max_pkts, npk, used, rcs)
+        if rc < 0:
+            _check(rc, self.lib)
+        out = [(rcs[b], [arr[b * self.max_pkts + i].as_dict() for i in range(npk[b])], used[b]) for b in range(self.n)]
+        return rc, out
 
 
 def compose_packets(data, offset_in_block=0, seqno=0, proto=PROTO_V2, ctype=CSUM_CRC32C, finish=False,

@@ -132,6 +132,7 @@ struct PieceSlot {
 struct SpecSlot {
   SpecCtl *ctl = nullptr;
   SpecExc *exc = nullptr;
+  SpecRunTail *xtail = nullptr;  // [2][kSpecRunsMax]: what follows runs 1.. of a batch
   SpecTabData *tabs = nullptr;
   uint8_t *h = nullptr, *hd = nullptr;
   uint64_t n = 0;

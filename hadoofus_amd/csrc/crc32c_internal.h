@@ -186,15 +186,40 @@ struct SpecFinal {
   uint32_t pad[10];
 };
 static_assert(sizeof(SpecEarly) == 128 && sizeof(SpecFinal) == 128, "spec host blocks");
-constexpr size_t kSpecHostBytes = 256 + size_t(kSpecExcMax) * sizeof(SpecExc);
+// A BATCH launch verifies up to kSpecRunsMax runs (one block transfer each,
+// separate streams) of one packet layout in one grid: one launch's fixed cost
+// for the batch.  Run r's packet 0 record and packet count (early, written
+// by workgroup 0 with the early block) and what follows the run (final,
+// copied by the last workgroup) land in the host area after the exceptions.
+constexpr uint32_t kSpecRunsMax = 16;
+struct SpecRunEarly {
+  uint64_t r0[7];           // the run's packet 0 record (stream_off relative to the run's stream)
+  uint32_t count, pad;      // packets of the run this launch verifies
+};
+struct SpecRunTail {        // what follows run r (r >= 1; run 0's is in SpecCtl / SpecFinal)
+  uint64_t rec[7];
+  uint64_t total;
+  uint32_t status, pad;
+};
+static_assert(sizeof(SpecRunEarly) == 64 && sizeof(SpecRunTail) == 72, "spec run blocks");
+constexpr size_t kSpecRunEarlyOff = 256 + size_t(kSpecExcMax) * sizeof(SpecExc);
+constexpr size_t kSpecRunTailOff = kSpecRunEarlyOff + size_t(kSpecRunsMax) * sizeof(SpecRunEarly);
+constexpr size_t kSpecHostBytes = kSpecRunTailOff + size_t(kSpecRunsMax) * sizeof(SpecRunTail);
 // Parameters of the closed-form segment table (SpecTab, crc32c_kernels.hip).
+// A batch of runs of `per` packets each: packet k (global) is packet k - r *
+// per of run r = k / per (a multiply-high by um = floor(2^64 / per) + 1,
+// exact for k < 2^32), whose CRCs start at crc0r[r] + (k - r * per) *
+// stride; one run: nruns 1.
 struct SpecTabData {
   const uint8_t *crc0;          // packet 0's CRCs
   uint8_t *bm0, *copy_base;
   uint64_t stride, copy_cap;
-  uint32_t nch, cs, cb0, pad;   // dataLen = nch * cs (whole chunks), crc_len = 4 * nch
+  uint32_t nch, cs, cb0, nruns; // dataLen = nch * cs (whole chunks), crc_len = 4 * nch
+  uint64_t um;
+  uint32_t per, pad;
+  const uint8_t *crc0r[kSpecRunsMax];
 };
-static_assert(sizeof(SpecTabData) == 56, "SpecTabData");
+static_assert(sizeof(SpecTabData) == 56 + 16 + 128, "SpecTabData");
 struct SpecArgs {
   const uint8_t *s;
   uint64_t len, base;
@@ -217,6 +242,12 @@ struct SpecArgs {
   // stamps of the work loop at [3 * wave], and per-workgroup phase stamps at
   // [kSpecStampOff + 8 * block + phase] (s_memrealtime, 100 MHz)
   unsigned long long *stamps;
+  // batch: runs 1 .. nruns - 1 (run 0 is s + base, len - base), verify only
+  // (no read window, no copy-out); max_count caps each run
+  uint32_t nruns;
+  const uint8_t *xs[kSpecRunsMax];
+  uint64_t xlen[kSpecRunsMax];
+  SpecRunTail *xtail;       // [2][kSpecRunsMax] by ring slot (device)
 };
 constexpr size_t kSpecStampOff = 98304;
 constexpr uint64_t kSpecMaxStride = uint64_t(1) << 26;  // per-lane header offsets within a wave fit 32 bits

@@ -169,7 +169,10 @@ DEV SegHot seg_hot(SegP segs, uint32_t s) {
 // after decoding packet 0) and are read, like a SegDev, with scalar loads
 // through the constant address space: carried in SGPRs across the work
 // loop they pushed the kernel past the SGPR budget and into spills.
-struct SpecTab {
+// BATCH: the table of a batch of equal runs (spec_verify_kernel<0, 1>); the
+// single-run kernels keep the plain closed form in their hot loop.
+template <bool BATCH>
+struct SpecTabT {
   const CAS SpecTabData *p;
   DEV SegDev operator[](uint32_t k) const {
     SegDev d;
@@ -183,7 +186,13 @@ struct SpecTab {
     q.cs = p->cs;
     q.cb0 = p->cb0;
     const uint32_t T = (q.nch + kTileChunks - 1u) / kTileChunks, dlen = q.nch * q.cs;
-    const uint8_t *c = q.crc0 + static_cast<uint64_t>(k) * q.stride;
+    const uint8_t *c;
+    if constexpr (BATCH) {  // a batch of equal runs: packet k is packet k - r * per of run r = k / per (uniform)
+      const uint32_t r = static_cast<uint32_t>(__umul64hi(static_cast<uint64_t>(k), p->um));
+      c = p->crc0r[r] + static_cast<uint64_t>(k - r * p->per) * q.stride;
+    } else {
+      c = q.crc0 + static_cast<uint64_t>(k) * q.stride;
+    }
     d.data = c + 4u * q.nch;
     d.crcs = reinterpret_cast<uint32_t *>(const_cast<uint8_t *>(c));
     d.bitmap = q.bm0 + static_cast<uint64_t>(k) * T;
@@ -208,7 +217,9 @@ struct SpecTab {
     return d;
   }
 };
-DEV SegHot seg_hot(const SpecTab &t, uint32_t k) {
+using SpecTab = SpecTabT<false>;
+template <bool BATCH>
+DEV SegHot seg_hot(const SpecTabT<BATCH> &t, uint32_t k) {
   const SegDev d = t[k];
   return SegHot{d.data, d.crcs, d.bitmap, d.mtile_start, d.chunk_size, d.flags, d.nchunks, d.main_tiles};
 }
@@ -2869,19 +2880,28 @@ struct SpecRun {
 
 constexpr uint32_t kSpecHdrBytes = 48;  // header bytes compared per packet (canonical headers: <= 33)
 
-template <int COPY>
+template <int COPY, int BATCH>
 __global__ __launch_bounds__(1024) void spec_verify_kernel(SpecArgs a) {
+  static_assert(!(COPY && BATCH), "a batch is verify only");
   __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsWords + 2 + 2 * kSlots];
-  __shared__ __attribute__((aligned(16))) uint8_t win[2][kHdrWin];  // packet 0, the point after the run
+  // packet 0 of run r in win[r]; after the decode win[r + 1] takes the point
+  // after run r (the tails: win[0] stays the header template)
+  __shared__ __attribute__((aligned(16))) uint8_t win[kSpecRunsMax + 1][kHdrWin];
   __shared__ SpecRun run;
-  __shared__ uint64_t run_r0[7];  // packet 0's record, for the early block
+  __shared__ uint64_t run_r0[kSpecRunsMax][7];  // each run's packet 0 record, for the early blocks
   __shared__ uint64_t run_total;
+  // run r: packets at rS[r] + rP[r] + k * stride, k < rcount[r], records'
+  // stream_off relative to rS[r] (run 0: the call's stream and base)
+  __shared__ const uint8_t *rS[kSpecRunsMax];
+  __shared__ uint64_t rN[kSpecRunsMax], rP[kSpecRunsMax], roff0[kSpecRunsMax], rseq0[kSpecRunsMax];
+  __shared__ uint32_t rcount[kSpecRunsMax], rprefix[kSpecRunsMax + 1], gprefix[kSpecRunsMax + 1];
   // what the epilogue needs, parked in LDS: kept in SGPRs across the work
   // loop they pushed it past the SGPR budget (spills)
   __shared__ SpecCtl *ep_ctl;
   __shared__ SpecExc *ep_exc;
   __shared__ uint8_t *ep_hout;
-  __shared__ uint32_t ep_seq;
+  __shared__ SpecRunTail *ep_xtail;
+  __shared__ uint32_t ep_seq, ep_nruns;
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
   // diagnostic build: phase stamps of this workgroup (0 entry, 1 tables +
   // packet 0 decoded + closed-form table written, 2 work loop entered, 3
@@ -2891,83 +2911,169 @@ __global__ __launch_bounds__(1024) void spec_verify_kernel(SpecArgs a) {
     if (kDiag && ps && t == 0) ps[ph] = __builtin_amdgcn_s_memrealtime();
   };
   stamp(0);
+  const uint32_t nruns = !BATCH || a.nruns < 1u ? 1u : (a.nruns > kSpecRunsMax ? kSpecRunsMax : a.nruns);
   if (t == 0) {
     ep_ctl = a.ctl + a.parity;
     ep_exc = a.exc + a.parity * kSpecExcMax;
     ep_hout = a.hout;
+    ep_xtail = a.xtail ? a.xtail + a.parity * kSpecRunsMax : nullptr;
     ep_seq = a.seq;
+    ep_nruns = nruns;
   }
   SpecCtl *const ctl = a.ctl + a.parity;
   const uint64_t rem = a.len > a.base ? a.len - a.base : 0u;
+  // run r's stream, length and packet 0 position (per lane: a select over
+  // the argument slots, no dynamic index into the kernel arguments)
+  auto run_of = [&](uint32_t r, const uint8_t *&S, uint64_t &N, uint64_t &P) {
+    S = a.s;
+    N = a.len;
+    P = rem ? a.base : 0u;
+#pragma unroll
+    for (uint32_t i = 1; i < kSpecRunsMax; i++)
+      if (r == i) {
+        S = a.xs[i];
+        N = a.xlen[i];
+        P = 0u;
+      }
+  };
   if (wv == 0) {
-    // packet 0's first kHdrWin bytes (zeros past the stream) -> win[0]
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t *>(a.s + (rem ? a.base : 0u)), 0, static_cast<int>(rem < kHdrWin ? rem : kHdrWin),
-        0x00020000);
-    if (lane < kHdrWin / 16)
-      *reinterpret_cast<u32x4 *>(&win[0][16 * lane]) =
-          __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 16u * lane, 0, 0));
+    // packet 0's first kHdrWin bytes of each run (zeros past its stream) ->
+    // win[r]: lane 4 r + q loads bytes [16 q, 16 q + 16) of run r
+    const uint32_t r = lane >> 2, q = lane & 3u;
+    if (r < nruns) {
+      const uint8_t *S;
+      uint64_t N, P;
+      run_of(r, S, N, P);
+      const uint64_t left = N > P ? N - P : 0u;
+      if (r == 0) {  // one uniform descriptor: buffer loads clamp at the stream's end
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint8_t *>(a.s + (rem ? a.base : 0u)), 0, static_cast<int>(rem < kHdrWin ? rem : kHdrWin),
+            0x00020000);
+        *reinterpret_cast<u32x4 *>(&win[0][16 * q]) =
+            __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 16u * q, 0, 0));
+      } else {
+        uint32_t wd[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (uint32_t i = 0; i < 16; i++)
+          if (16u * q + i < left) wd[i / 4] |= uint32_t(S[P + 16u * q + i]) << (8u * (i % 4));
+        *reinterpret_cast<u32x4 *>(&win[r][16 * q]) = u32x4{wd[0], wd[1], wd[2], wd[3]};
+      }
+    }
   }
   fill_tables<1024, 0>(lds, a.gtab);
-  if (wv == 0 && lane == 0) {
-    // The critical path of every workgroup: packet 0's decode and this
-    // workgroup's copy of the closed-form table (written with vector stores,
-    // acknowledged before the barrier; read back with scalar loads in the
-    // work loop).  What only the host or the epilogue needs -- the point
-    // after the run, the early block, the next launch's control slot -- is
-    // left to one wave of workgroup 0 after the barrier.
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");  // the window's LDS stores, this wave's own
+  if (wv == 0) {
+    // The critical path of every workgroup: each run's packet 0 decoded
+    // (lane r: run r), the batch's layout checked, and this workgroup's copy
+    // of the closed-form table (written with vector stores, acknowledged
+    // before the barrier; read back with scalar loads in the work loop).
+    // What only the host or the epilogue needs -- the points after the runs,
+    // the early blocks, the next launch's control slot -- is left to one
+    // wave of workgroup 0 after the barrier.
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");  // the windows' LDS stores, this wave's own
+    const uint32_t r = lane;
     SpecRun d{};
-    hdfs_crc32c_packet r{};
+    hdfs_crc32c_packet rr{};
     uint64_t total = 0;
-    const uint32_t hl = a.proto == HDFS_CRC32C_PROTO_V2 ? 6u + ((uint32_t(win[0][4]) << 8) | win[0][5]) : 25u;
-    const bool fits = rem >= 6u && hl <= kHdrWin;
-    const int st = fits ? frame::frame_step(win[0], rem, a.base, a.proto, a.cs, a.ctype, r, total) : frame::kStepMore;
-    uint32_t cb0 = 0;
-    const uint32_t avail0 = st == frame::kStepNext ? frame::read_avail(r, a.rwin != 0, a.client_offset, cb0) : 0u;
-    bool ok = st == frame::kStepNext && !r.error && !r.last && r.crc_len > 0 && r.data_len > 0 &&
-              a.cs % kRoundBytes == 0 && uint32_t(r.data_len) % a.cs == 0 && total < kSpecMaxStride &&
-              spec_canonical(win[0], a.proto, hl) && avail0 > 0u;
+    bool ok = false;
     uint32_t count = 0;
-    if (ok) {
-      const uint64_t by_len = rem / total;
-      uint64_t cnt = min<uint64_t>(by_len, a.max_count);
-      // a client read takes the packets up to the one that completes it
-      if (a.rwin && a.copy_cap > avail0)
-        cnt = min<uint64_t>(cnt, 1u + (a.copy_cap - avail0 + uint64_t(r.data_len) - 1u) / uint64_t(r.data_len));
-      else if (a.rwin)
-        cnt = 1u;
-      count = static_cast<uint32_t>(cnt);
-      ok = count >= 2u;
-      d.stride = total;
-      d.hl = r.header_len;
-      d.crc_len = uint32_t(r.crc_len);
-      d.dlen = uint32_t(r.data_len);
-      d.nch = uint32_t(r.crc_len) / 4u;
-      d.T = (d.nch + kTileChunks - 1u) / kTileChunks;
-      d.cb0 = cb0;
-      d.v1 = a.proto == HDFS_CRC32C_PROTO_V1 ? 1u : 0u;
-      d.off0 = uint64_t(r.offset_in_block);
-      d.seq0 = uint64_t(r.seqno);
+    const uint8_t *S = a.s;
+    uint64_t N = 0, P = 0;
+    if (r < nruns) {
+      run_of(r, S, N, P);
+      const uint64_t left = N > P ? N - P : 0u;
+      const uint32_t hl = a.proto == HDFS_CRC32C_PROTO_V2 ? 6u + ((uint32_t(win[r][4]) << 8) | win[r][5]) : 25u;
+      const bool fits = left >= 6u && hl <= kHdrWin;
+      const int st = fits ? frame::frame_step(win[r], left, P, a.proto, a.cs, a.ctype, rr, total) : frame::kStepMore;
+      uint32_t cb0 = 0;
+      const bool rwin = a.rwin != 0 && nruns == 1u;
+      const uint32_t avail0 = st == frame::kStepNext ? frame::read_avail(rr, rwin, a.client_offset, cb0) : 0u;
+      ok = st == frame::kStepNext && !rr.error && !rr.last && rr.crc_len > 0 && rr.data_len > 0 &&
+           a.cs % kRoundBytes == 0 && uint32_t(rr.data_len) % a.cs == 0 && total < kSpecMaxStride &&
+           spec_canonical(win[r], a.proto, hl) && avail0 > 0u;
+      if (ok) {
+        const uint64_t by_len = left / total;
+        uint64_t cnt = min<uint64_t>(by_len, a.max_count);
+        // a client read takes the packets up to the one that completes it
+        if (rwin && a.copy_cap > avail0)
+          cnt = min<uint64_t>(cnt, 1u + (a.copy_cap - avail0 + uint64_t(rr.data_len) - 1u) / uint64_t(rr.data_len));
+        else if (rwin)
+          cnt = 1u;
+        count = static_cast<uint32_t>(cnt);
+        ok = count >= 2u;
+        d.stride = total;
+        d.hl = rr.header_len;
+        d.crc_len = uint32_t(rr.crc_len);
+        d.dlen = uint32_t(rr.data_len);
+        d.nch = uint32_t(rr.crc_len) / 4u;
+        d.T = (d.nch + kTileChunks - 1u) / kTileChunks;
+        d.cb0 = cb0;
+        d.v1 = a.proto == HDFS_CRC32C_PROTO_V1 ? 1u : 0u;
+        d.off0 = uint64_t(rr.offset_in_block);
+        d.seq0 = uint64_t(rr.seqno);
+      }
     }
-    d.eligible = ok ? 1u : 0u;
-    d.count = count;
-    run = d;
-    const uint64_t *x = reinterpret_cast<const uint64_t *>(&r);
+    // the batch takes its layout from run 0; every run must share it
+    const uint32_t hl0 = __builtin_amdgcn_readlane(d.hl, 0), cl0 = __builtin_amdgcn_readlane(d.crc_len, 0),
+                   dl0 = __builtin_amdgcn_readlane(d.dlen, 0);
+    const uint64_t st0 = (uint64_t(__builtin_amdgcn_readlane(static_cast<uint32_t>(total >> 32), 0)) << 32) |
+                         __builtin_amdgcn_readlane(static_cast<uint32_t>(total), 0);
+    // (and, for a batch, its packet count: the table maps packet k to run k / count)
+    const uint32_t cnt0 = __builtin_amdgcn_readlane(count, 0);
+    const bool bad = r < nruns && !(ok && d.hl == hl0 && d.crc_len == cl0 && d.dlen == dl0 && total == st0 &&
+                                    (nruns == 1u || count == cnt0));
+    const bool all_ok = __builtin_amdgcn_ballot_w64(bad) == 0ull;
+    // prefixes of the runs' packets and of their 64-packet header groups
+    uint32_t pre = 0, tot = 0, gpre = 0, gtot = 0;
 #pragma unroll
-    for (int q = 0; q < 7; q++) run_r0[q] = x[q];
-    run_total = total;
-    if (ok) {
+    for (uint32_t i = 0; i < kSpecRunsMax; i++) {
+      const uint32_t ci = __builtin_amdgcn_readlane(count, i);
+      if (i < nruns) {
+        if (i < r) {
+          pre += ci;
+          gpre += (ci + 63u) / 64u;
+        }
+        tot += ci;
+        gtot += (ci + 63u) / 64u;
+      }
+    }
+    if (r < nruns) {
+      rS[r] = S;
+      rN[r] = N;
+      rP[r] = P;
+      roff0[r] = d.off0;
+      rseq0[r] = d.seq0;
+      rcount[r] = count;
+      rprefix[r] = pre;
+      gprefix[r] = gpre;
+      const uint64_t *x = reinterpret_cast<const uint64_t *>(&rr);
+#pragma unroll
+      for (int q = 0; q < 7; q++) run_r0[r][q] = x[q];
+    }
+    if (r == 0) {
+      rprefix[nruns] = tot;
+      gprefix[nruns] = gtot;
+      d.eligible = all_ok ? 1u : 0u;
+      d.count = tot;
+      run = d;
+      run_total = total;
+    }
+    if (all_ok) {
       SpecTabData *q = a.tabs + blockIdx.x;
-      q->crc0 = a.s + a.base + d.hl;
-      q->bm0 = a.bm;
-      q->copy_base = COPY ? a.copy_base : nullptr;
-      q->stride = d.stride;
-      q->copy_cap = COPY ? a.copy_cap : 0u;
-      q->nch = d.nch;
-      q->cs = a.cs;
-      q->cb0 = COPY ? d.cb0 : 0u;
-      q->pad = 0u;
+      if (r < nruns) q->crc0r[r] = S + P + d.hl;
+      if (r == 0) {
+        q->crc0 = S + P + d.hl;
+        q->bm0 = a.bm;
+        q->copy_base = COPY ? a.copy_base : nullptr;
+        q->stride = d.stride;
+        q->copy_cap = COPY ? a.copy_cap : 0u;
+        q->nch = d.nch;
+        q->cs = a.cs;
+        q->cb0 = COPY ? d.cb0 : 0u;
+        q->nruns = nruns;
+        q->per = count;
+        q->um = count ? ~0ull / count + 1ull : 0ull;
+        q->pad = 0u;
+      }
       stores_done();
     }
   }
@@ -2988,98 +3094,131 @@ __global__ __launch_bounds__(1024) void spec_verify_kernel(SpecArgs a) {
   d.stride = rfl64(run.stride);
   d.off0 = rfl64(run.off0);
   d.seq0 = rfl64(run.seq0);
-  // Workgroup 0, last wave, lane 0: the point after the run (where the walk
-  // goes on, or what ends it) into the control slot, the next launch's slot
-  // zeroed, and the early block to the host (which fills the run's records
-  // while the kernel verifies it).  This wave joins the work loop after it;
-  // the other waves take the workgroup's tiles meanwhile (LDS tickets).
-  if (blockIdx.x == 0 && wv == 15u && lane == 0) {
-    if (d.eligible) {
+  // Workgroup 0, last wave: the next launch's control slot zeroed and the
+  // early block to the host (which fills the runs' records while the kernel
+  // verifies them); then lane 0 the point after each run (where its walk
+  // goes on, or what ends it) into its control slot, one run at a time
+  // (stage_header's descriptor is uniform).  This wave joins the work loop
+  // after it; the other waves take the workgroup's tiles meanwhile.
+  if (blockIdx.x == 0 && wv == 15u) {
+    if (lane < nruns && nruns > 1u) {  // the batch's per-run early records
+      auto *er = reinterpret_cast<SpecRunEarly *>(a.hout + kSpecRunEarlyOff) + lane;
+#pragma unroll
+      for (int q = 0; q < 7; q++) er->r0[q] = run_r0[lane][q];
+      er->count = rcount[lane];
+    }
+    if (lane == 0) {
+      // the next launch's control slot starts at zero (this launch's was
+      // zeroed by the one before)
+      SpecCtl *nx = a.ctl + (a.parity ^ 1u);
+      nx->mism = 0ull;
+      nx->gctr = 0u;
+      nx->done = 0u;
+      nx->exc = 0u;
+      nx->nexc = 0u;
+      auto *e = reinterpret_cast<SpecEarly *>(a.hout);
+#pragma unroll
+      for (int q = 0; q < 7; q++) e->r0[q] = run_r0[0][q];
+      e->stride = run_total;
+      e->eligible = d.eligible;
+      e->count = d.count;
+    }
+    stores_done();
+    __threadfence_system();
+    if (lane == 0) __hip_atomic_store(&reinterpret_cast<SpecEarly *>(a.hout)->seq, a.seq, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_SYSTEM);
+    for (uint32_t r = 0; lane == 0 && d.eligible && r < nruns; r++) {
+      const uint8_t *S = rS[r];
+      const uint64_t N = rN[r], P = rP[r], cnt = rcount[r];
       uint32_t ts = kGridOn;
       uint64_t ttot = 0;
       hdfs_crc32c_packet tr{};
-      const uint64_t by_len = rem / d.stride;
+      const uint64_t by_len = (N - P) / d.stride;
       // (the caller's record array holds count + 1 records only when the
-      // pass was not cut at max_count)
-      if (d.count == by_len && d.count < a.max_count) {  // the run ends with the stream's whole strides
-        const uint64_t pt = a.base + uint64_t(d.count) * d.stride;
-        if (pt >= a.len) {
+      // run was not cut at max_count)
+      if (cnt == by_len && cnt < a.max_count) {  // the run ends with the stream's whole strides
+        const uint64_t pt = P + cnt * d.stride;
+        if (pt >= N) {
           ts = kGridMore;
         } else {
-          stage_header(a.s, a.len, pt, 0u, win[1]);
-          const int tst = grid_frame(a.s, a.len, pt, win[1], a.proto, a.cs, a.ctype, tr, ttot);
+          stage_header(S, N, pt, 0u, win[r + 1]);
+          const int tst = grid_frame(S, N, pt, win[r + 1], a.proto, a.cs, a.ctype, tr, ttot);
           ts = tst == frame::kStepMore ? kGridMore : tst == frame::kStepStop ? kGridStop : kGridOff;
         }
       }
       const uint64_t *x = reinterpret_cast<const uint64_t *>(&tr);
+      if (r == 0) {
 #pragma unroll
-      for (int q = 0; q < 7; q++) at_st(&ctl->tail[q], x[q]);
-      at_st(&ctl->tail_total, ttot);
-      at_st32(&ctl->tail_status, ts);
+        for (int q = 0; q < 7; q++) at_st(&ctl->tail[q], x[q]);
+        at_st(&ctl->tail_total, ttot);
+        at_st32(&ctl->tail_status, ts);
+      } else if (a.xtail) {
+        SpecRunTail *y = a.xtail + a.parity * kSpecRunsMax + r;
+#pragma unroll
+        for (int q = 0; q < 7; q++) at_st(&y->rec[q], x[q]);
+        at_st(&y->total, ttot);
+        at_st32(&y->status, ts);
+      }
     }
-    // the next launch's control slot starts at zero (this launch's was
-    // zeroed by the one before)
-    SpecCtl *nx = a.ctl + (a.parity ^ 1u);
-    nx->mism = 0ull;
-    nx->gctr = 0u;
-    nx->done = 0u;
-    nx->exc = 0u;
-    nx->nexc = 0u;
-    stores_done();
-    auto *e = reinterpret_cast<SpecEarly *>(a.hout);
-#pragma unroll
-    for (int q = 0; q < 7; q++) e->r0[q] = run_r0[q];
-    e->stride = run_total;
-    e->eligible = d.eligible;
-    e->count = d.count;
-    __threadfence_system();
-    __hip_atomic_store(&e->seq, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   if (!d.eligible) return;
   const bool v1 = d.v1 != 0u;
-  // header checks: runs of 64 packets, run j on wave (j / G) % 16 of
-  // workgroup j % G; lane l compares packet 64 j + l (packet 0 is the
-  // prediction itself).  A wave's first run is loaded here and compared after
-  // the verify loop: its loads ride ahead of the loop's first rounds instead
-  // of holding every wave of the workgroup at the barrier for a round trip
-  // (a 1 GiB run has one run per workgroup; longer runs load the rest later)
+  // header checks: groups of 64 packets of a run, group g (over the runs in
+  // order) on wave (g / G) % 16 of workgroup g % G; lane l compares packet
+  // 64 j + l of the group's run (packet 0 of a run is its prediction
+  // itself).  A wave's first group is loaded here and compared after the
+  // verify loop: its loads ride ahead of the loop's first rounds instead of
+  // holding every wave of the workgroup at the barrier for a round trip (a
+  // 1 GiB run has one group per workgroup; longer runs load the rest later)
   const uint32_t G = gridDim.x;
   const uint32_t j0 = wv * G + blockIdx.x;
-  auto hdr_rsrc = [&](uint32_t j) {
-    const uint64_t p0 = a.base + uint64_t(64u * j) * d.stride;
-    const uint64_t span = a.len - p0;
+  const uint32_t ngroups = rfl(gprefix[nruns]);
+  auto group_run = [&](uint32_t g) {
+    uint32_t r = 0;
+#pragma unroll
+    for (uint32_t i = 1; i < kSpecRunsMax; i++) r += (i < nruns && g >= gprefix[i]) ? 1u : 0u;
+    return rfl(r);
+  };
+  // group g: its run, the group's first packet position in the run's stream
+  auto hdr_rsrc = [&](uint32_t r, uint32_t jr) {
+    const uint64_t p0 = rfl64(rP[r]) + uint64_t(64u * jr) * d.stride;
+    const uint64_t n = rfl64(rN[r]);
+    const uint64_t span = n > p0 ? n - p0 : 0u;
     return __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<uint8_t *>(rfl64(reinterpret_cast<uint64_t>(a.s + p0))), 0,
+        reinterpret_cast<uint8_t *>(rfl64(reinterpret_cast<uint64_t>(rS[r] + p0))), 0,
         static_cast<int>(rfl(span > 0xFFFFFFFFull ? 0xFFFFFFFFu : static_cast<uint32_t>(span))), 0x00020000);
   };
   const uint32_t vo = lane * static_cast<uint32_t>(d.stride);
   u32x4 h0[kSpecHdrBytes / 16];
-  if (64u * j0 < d.count) {
-    const __amdgpu_buffer_rsrc_t rs = hdr_rsrc(j0);
+  if (j0 < ngroups) {
+    const uint32_t r = group_run(j0);
+    const __amdgpu_buffer_rsrc_t rs = hdr_rsrc(r, j0 - rfl(gprefix[r]));
 #pragma unroll
     for (int q = 0; q < int(kSpecHdrBytes / 16); q++)
       h0[q] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 16u * q, 0, 0));
   }
   stamp(2);
-  const SpecTab tab{(const CAS SpecTabData *)(a.tabs + blockIdx.x)};
+  const SpecTabT<BATCH != 0> tab{(const CAS SpecTabData *)(a.tabs + blockIdx.x)};
   const uint64_t tiles = uint64_t(d.count) * d.T;
   tiles_run<kModeVerify, 3, 1, 3, 1, 1024, 1, COPY, 1, 0>(lds, tab, nullptr, d.count, tiles * (a.cs / kRoundBytes),
                                                           tiles, a.fb, &ctl->mism, kDiag ? a.stamps : nullptr, a.tune,
                                                           &ctl->gctr, nullptr, d.T, false);
-  for (uint32_t j = j0; 64u * j < d.count; j += 16u * G) {
+  for (uint32_t j = j0; j < ngroups; j += 16u * G) {
+    const uint32_t r = group_run(j), jr = j - rfl(gprefix[r]);
     u32x4 h[kSpecHdrBytes / 16];
     if (j == j0) {
 #pragma unroll
       for (int q = 0; q < int(kSpecHdrBytes / 16); q++) h[q] = h0[q];
     } else {
-      const __amdgpu_buffer_rsrc_t rs = hdr_rsrc(j);
+      const __amdgpu_buffer_rsrc_t rs = hdr_rsrc(r, jr);
 #pragma unroll
       for (int q = 0; q < int(kSpecHdrBytes / 16); q++)
         h[q] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 16u * q, 0, 0));
     }
-    const uint64_t p0 = a.base + uint64_t(64u * j) * d.stride;
-    const uint32_t k = 64u * j + lane;
-    const uint64_t off = d.off0 + uint64_t(k) * d.dlen, sq = d.seq0 + k;
+    const uint64_t p0 = rfl64(rP[r]) + uint64_t(64u * jr) * d.stride;
+    const uint32_t kr = 64u * jr + lane;
+    const uint32_t cnt_r = rfl(rcount[r]);
+    const uint64_t off = rfl64(roff0[r]) + uint64_t(kr) * d.dlen, sq = rfl64(rseq0[r]) + kr;
     uint32_t e[kSpecHdrBytes / 4];
     e[0] = spec_hdr_word<0>(win[0], v1, off, sq);
     e[1] = spec_hdr_word<1>(win[0], v1, off, sq);
@@ -3100,28 +3239,30 @@ __global__ __launch_bounds__(1024) void spec_verify_kernel(SpecArgs a) {
       const uint32_t m = 4u * w >= d.hl ? 0u : 4u * w + 4u <= d.hl ? 0xFFFFFFFFu : (1u << (8u * (d.hl - 4u * w))) - 1u;
       diff |= (h[w / 4][w % 4] ^ e[w]) & m;
     }
-    if (k < d.count && diff != 0u) {
+    if (kr < cnt_r && diff != 0u) {
       // rare: frame the packet as frame_build_kernel would.  Clean and in
       // the run's layout -- same header length, dataLen and CRC length, so
       // its CRCs and data sit where the closed-form table puts them (the
       // same wire size alone is not enough: a 27-B syncBlock header with
       // dataLen cut by 2 has packet 0's stride) -- an exception with its own
       // record; anything else voids the launch
-      hdfs_crc32c_packet r{};
+      hdfs_crc32c_packet rec{};
       uint64_t tot = 0;
       const uint64_t pos = p0 + vo;
-      const int st = frame::frame_step(a.s + pos, a.len - pos, pos, a.proto, a.cs, a.ctype, r, tot);
-      bool keep = st == frame::kStepNext && !r.error && tot == d.stride && r.header_len == d.hl &&
-                  static_cast<uint32_t>(r.data_len) == d.dlen && static_cast<uint32_t>(r.crc_len) == d.crc_len &&
-                  (!a.rwin || static_cast<uint64_t>(r.offset_in_block) == off);
+      const uint8_t *S = rS[r];
+      const uint64_t N = rfl64(rN[r]);
+      const int st = frame::frame_step(S + pos, N - pos, pos, a.proto, a.cs, a.ctype, rec, tot);
+      bool keep = st == frame::kStepNext && !rec.error && tot == d.stride && rec.header_len == d.hl &&
+                  static_cast<uint32_t>(rec.data_len) == d.dlen && static_cast<uint32_t>(rec.crc_len) == d.crc_len &&
+                  (!a.rwin || static_cast<uint64_t>(rec.offset_in_block) == off);
       if (keep) {
         const uint32_t slot = __hip_atomic_fetch_add(&ctl->nexc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (slot < kSpecExcMax) {
           SpecExc *x = a.exc + a.parity * kSpecExcMax + slot;
-          const uint64_t *w = reinterpret_cast<const uint64_t *>(&r);
+          const uint64_t *w = reinterpret_cast<const uint64_t *>(&rec);
 #pragma unroll
           for (int q = 0; q < 7; q++) at_st(&x->rec[q], w[q]);
-          at_st32(&x->k, k);
+          at_st32(&x->k, rfl(rprefix[r]) + kr);  // global packet index over the runs
         } else {
           keep = false;
         }
@@ -3157,6 +3298,15 @@ __global__ __launch_bounds__(1024) void spec_verify_kernel(SpecArgs a) {
         for (int q = 0; q < 7; q++) hx[j].rec[q] = at_ld(&x[j].rec[q]);
         hx[j].k = static_cast<uint32_t>(__hip_atomic_load(&x[j].k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
       }
+      const SpecRunTail *xt = ep_xtail;
+      auto *ht = reinterpret_cast<SpecRunTail *>(ep_hout + kSpecRunTailOff);
+      for (uint32_t r = 1; xt && r < ep_nruns; r++) {
+#pragma unroll
+        for (int q = 0; q < 7; q++) ht[r].rec[q] = at_ld(&xt[r].rec[q]);
+        ht[r].total = at_ld(&xt[r].total);
+        ht[r].status =
+            static_cast<uint32_t>(__hip_atomic_load(&xt[r].status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      }
       __threadfence_system();
       __hip_atomic_store(&f->seq, ep_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       stamp(4);
@@ -3166,8 +3316,10 @@ __global__ __launch_bounds__(1024) void spec_verify_kernel(SpecArgs a) {
 
 hipError_t launch_spec_verify(const SpecArgs &a, int grid, int copy, hipStream_t stream) {
   if (grid < 1 || !a.seq || !a.ctl || !a.exc || !a.hout || !a.tabs || a.parity > 1u) return hipErrorInvalidValue;
-  if (copy) hipLaunchKernelGGL(spec_verify_kernel<1>, dim3(grid), dim3(1024), 0, stream, a);
-  else hipLaunchKernelGGL(spec_verify_kernel<0>, dim3(grid), dim3(1024), 0, stream, a);
+  if (a.nruns > 1u && (copy || a.rwin || a.nruns > kSpecRunsMax || !a.xtail)) return hipErrorInvalidValue;
+  if (a.nruns > 1u) hipLaunchKernelGGL((spec_verify_kernel<0, 1>), dim3(grid), dim3(1024), 0, stream, a);
+  else if (copy) hipLaunchKernelGGL((spec_verify_kernel<1, 0>), dim3(grid), dim3(1024), 0, stream, a);
+  else hipLaunchKernelGGL((spec_verify_kernel<0, 0>), dim3(grid), dim3(1024), 0, stream, a);
   return hipGetLastError();
 }
 

@@ -710,11 +710,13 @@ int spec_alloc(DevCtx &c, SpecSlot &S) {
   if (S.ctl) return HDFS_CRC32C_OK;
   SpecCtl *ctl = nullptr;
   SpecExc *exc = nullptr;
+  SpecRunTail *xtail = nullptr;
   SpecTabData *tabs = nullptr;
   uint8_t *h = nullptr, *hd = nullptr;
   hipError_t e = hipMalloc(&ctl, 2 * sizeof(SpecCtl));
   if (e == hipSuccess) e = hipMemset(ctl, 0, 2 * sizeof(SpecCtl));  // the ring starts at zero
   if (e == hipSuccess) e = hipMalloc(&exc, 2 * kSpecExcMax * sizeof(SpecExc));
+  if (e == hipSuccess) e = hipMalloc(&xtail, 2 * kSpecRunsMax * sizeof(SpecRunTail));
   if (e == hipSuccess) e = hipMalloc(&tabs, size_t(std::max(c.num_cu, 1)) * sizeof(SpecTabData));
   if (e == hipSuccess) e = hipHostMalloc(&h, kSpecHostBytes, hipHostMallocCoherent | hipHostMallocMapped);
   if (e == hipSuccess) {
@@ -724,11 +726,13 @@ int spec_alloc(DevCtx &c, SpecSlot &S) {
   if (e != hipSuccess) {
     if (ctl) (void)hipFree(ctl);
     if (exc) (void)hipFree(exc);
+    if (xtail) (void)hipFree(xtail);
     if (tabs) (void)hipFree(tabs);
     if (h) (void)hipHostFree(h);
     return fail(HDFS_CRC32C_EHIP, "speculative verify buffers: %s", hipGetErrorString(e));
   }
   S.exc = exc;
+  S.xtail = xtail;
   S.tabs = tabs;
   S.h = h;
   S.hd = hd;
@@ -765,12 +769,16 @@ struct SpecLaunch {
   std::chrono::steady_clock::time_point t0, t1;  // launch call (diagnostic trace)
 };
 
+// nruns > 1: a batch -- runs 1 .. nruns - 1 at xs[r] (xlen[r] bytes) beside
+// run 0 at d + pos, all verified in this launch (no read window, no copy)
 int spec_launch(DevCtx &c, SpecSlot &S, hipStream_t st, const uint8_t *d, uint64_t len, uint64_t pos,
                 uint32_t max_count, int proto, uint32_t cs, int ctype, const CopyOut &co, uint64_t done_b, uint8_t *bm,
-                uint32_t *fb, SpecLaunch &L) {
+                uint32_t *fb, SpecLaunch &L, uint32_t nruns = 1, const uint8_t *const *xs = nullptr,
+                const uint64_t *xlen = nullptr) {
   int rc = spec_alloc(c, S);
   if (rc) return rc;
-  const uint64_t left = len - pos;
+  uint64_t left = len - pos;
+  for (uint32_t r = 1; r < nruns; r++) left += xlen[r];
   const uint64_t want = (left / kRoundBytes + 63) / 64;  // >= 4 rounds per wave (launch_verify_dyn)
   L.grid = int(std::max<uint64_t>(1, std::min<uint64_t>(want, uint64_t(c.bulk_cus()))));
   L.seq = next_grid_seq(c);
@@ -805,6 +813,12 @@ int spec_launch(DevCtx &c, SpecSlot &S, hipStream_t st, const uint8_t *d, uint64
   a.hout = S.hd;
   a.tabs = S.tabs;
   a.stamps = kDiag ? g_diag : nullptr;
+  a.nruns = nruns;
+  for (uint32_t r = 1; r < nruns; r++) {
+    a.xs[r] = xs[r];
+    a.xlen[r] = xlen[r];
+  }
+  a.xtail = S.xtail;
   L.t0 = std::chrono::steady_clock::now();
   HIPCHK(launch_spec_verify(a, L.grid, co.dst ? 1 : 0, st));
   S.n++;
@@ -909,6 +923,121 @@ int spec_collect(DevCtx &c, SpecSlot &S, const SpecLaunch &L, const CopyOut &co,
   } else if (F.tail_status == kGridMore) {  // the stream ends inside the next packet
     res.end = true;
   }  // kGridOff (another size) / kGridOn (the pass was cut): the walk goes on at run_end
+  return HDFS_CRC32C_OK;
+}
+
+// The host side of a BATCH launch (nruns runs, run r's packet 0 at pos0[r]
+// of its stream): each run's records predicted from its own packet 0 into
+// dst[r], then exceptions (global packet index -> run), verdicts and what
+// follows each run.  All runs taken or none (a header off the prediction in
+// any run voids the launch).
+struct SpecRunResult {
+  bool taken = false, end = false;
+  uint32_t recorded = 0;
+  uint64_t consumed = 0, next = 0;
+};
+int spec_collect_batch(SpecSlot &S, const SpecLaunch &L, uint32_t nruns, const uint64_t *pos0,
+                       hdfs_crc32c_packet *const *dst, std::vector<SpecRunResult> &res) {
+  res.assign(nruns, SpecRunResult{});
+  auto *early = reinterpret_cast<SpecEarly *>(S.h);
+  auto *fin = reinterpret_cast<SpecFinal *>(S.h + sizeof(SpecEarly));
+  int rc;
+  if ((rc = poll_seq(&early->seq, L.seq, "speculative batch verify", L.st))) return rc;
+  SpecEarly E;
+  std::memcpy(&E, early, sizeof(E));
+  if (!E.eligible) return HDFS_CRC32C_OK;
+  if (kDiag) g_spec_stats[1]++;
+  std::vector<SpecRunEarly> er(nruns);
+  std::memcpy(er.data(), S.h + kSpecRunEarlyOff, nruns * sizeof(SpecRunEarly));
+  std::vector<uint32_t> prefix(nruns + 1, 0);
+  std::vector<hdfs_crc32c_packet> r0(nruns);
+  for (uint32_t r = 0; r < nruns; r++) {
+    std::memcpy(&r0[r], er[r].r0, sizeof(hdfs_crc32c_packet));
+    prefix[r + 1] = prefix[r] + er[r].count;
+    for (uint32_t k = 0; k < er[r].count; k++) {
+      hdfs_crc32c_packet &q = dst[r][k];
+      q = r0[r];
+      q.stream_off = pos0[r] + uint64_t(k) * E.stride;
+      q.offset_in_block = r0[r].offset_in_block + int64_t(k) * r0[r].data_len;
+      q.seqno = r0[r].seqno + int64_t(k);
+    }
+  }
+  if (prefix[nruns] != E.count) return fail(HDFS_CRC32C_EHIP, "speculative batch: %u packets, runs hold %u", E.count,
+                                            prefix[nruns]);
+  if ((rc = poll_seq(&fin->seq, L.seq, "speculative batch verify", L.st))) return rc;
+  SpecFinal F;
+  std::memcpy(&F, fin, sizeof(F));
+  if (F.exc) {
+    if (kDiag) g_spec_stats[3]++;
+    return HDFS_CRC32C_OK;
+  }
+  if (kDiag) g_spec_stats[2]++;
+  auto run_of = [&](uint32_t k) {
+    return uint32_t(std::upper_bound(prefix.begin(), prefix.end(), k) - prefix.begin()) - 1u;
+  };
+  const auto *hx = reinterpret_cast<const SpecExc *>(S.h + 256);
+  for (uint32_t j = 0; j < F.nexc; j++) {
+    SpecExc x;
+    std::memcpy(&x, hx + j, sizeof(x));
+    if (x.k >= E.count) return fail(HDFS_CRC32C_EHIP, "speculative batch: exception record %u of %u", x.k, E.count);
+    const uint32_t r = run_of(x.k);
+    std::memcpy(&dst[r][x.k - prefix[r]], x.rec, sizeof(hdfs_crc32c_packet));
+  }
+  if (F.mism) {  // first bad chunk and count from the bitmap (global packet index)
+    const uint32_t nch = uint32_t(r0[0].crc_len) / 4u, nb = (nch + 7u) / 8u;
+    std::vector<uint8_t> bmh(size_t(E.count) * nb);
+    HIPCHK(hipMemcpyAsync(bmh.data(), L.bm, bmh.size(), hipMemcpyDeviceToHost, L.st));
+    HIPCHK(hipStreamSynchronize(L.st));
+    for (uint32_t k = 0; k < E.count; k++) {
+      const uint8_t *b = bmh.data() + size_t(k) * nb;
+      uint32_t bad = 0;
+      int32_t first = -1;
+      for (uint32_t j = 0; j < nb; j++) {
+        uint32_t byte = b[j];
+        if (j == nch / 8u) byte &= (1u << (nch % 8u)) - 1u;
+        if (!byte) continue;
+        if (first < 0) first = int32_t(8u * j + uint32_t(__builtin_ctz(byte)));
+        bad += uint32_t(__builtin_popcount(byte));
+      }
+      if (bad) {
+        const uint32_t r = run_of(k);
+        hdfs_crc32c_packet &q = dst[r][k - prefix[r]];
+        q.error = HDFS_CRC32C_ERR_DATANODE_BAD_CHECKSUM;
+        q.first_bad = first;
+        q.bad_chunks = bad;
+      }
+    }
+  }
+  std::vector<SpecRunTail> tails(nruns);
+  std::memcpy(tails.data(), S.h + kSpecRunTailOff, nruns * sizeof(SpecRunTail));
+  for (uint32_t r = 0; r < nruns; r++) {
+    uint32_t status;
+    uint64_t total;
+    const uint64_t *rec;
+    if (r == 0) {
+      status = F.tail_status;
+      total = F.tail_total;
+      rec = F.tail;
+    } else {
+      status = tails[r].status;
+      total = tails[r].total;
+      rec = tails[r].rec;
+    }
+    SpecRunResult &o = res[r];
+    o.taken = true;
+    o.recorded = er[r].count;
+    const uint64_t run_end = pos0[r] + uint64_t(er[r].count) * E.stride;
+    o.consumed = o.next = run_end;
+    if (status == kGridStop) {
+      hdfs_crc32c_packet &t = dst[r][er[r].count];
+      std::memcpy(&t, rec, sizeof(t));
+      if (!t.error) o.consumed = run_end + total;
+      o.recorded++;
+      o.end = true;
+    } else if (status == kGridMore) {
+      o.end = true;
+    }
+  }
   return HDFS_CRC32C_OK;
 }
 
@@ -1473,8 +1602,9 @@ int verify_packets_impl(const uint8_t *stream, uint64_t len, int proto, uint32_t
 
 struct hdfs_crc32c_job {
   int dev = -1, slot = -1;
-  const uint8_t *d = nullptr;
-  uint64_t len = 0;
+  std::vector<const uint8_t *> runs;  // the block streams (one for hdfs_crc32c_verify_packets_submit)
+  std::vector<uint64_t> lens;
+  bool batch = false;                 // hdfs_crc32c_verify_blocks_submit
   int proto = 0, ctype = 0;
   uint32_t cs = 0;
   size_t max_pkts = 0;
@@ -1485,10 +1615,12 @@ struct hdfs_crc32c_job {
 namespace hdfs_crc32c {
 namespace {
 
-int job_submit(const uint8_t *d, uint64_t len, int proto, uint32_t cs, int ctype, size_t max_pkts,
-               hdfs_crc32c_job **out) {
-  const int dev = stream_device(d);
+int job_submit(const uint8_t *const *runs, const uint64_t *lens, size_t n, bool batch, int proto, uint32_t cs,
+               int ctype, size_t max_pkts, hdfs_crc32c_job **out) {
+  const int dev = stream_device(runs[0]);
   if (dev < 0) return fail(HDFS_CRC32C_EINVAL, "asynchronous verify takes device-resident streams");
+  for (size_t r = 1; r < n; r++)
+    if (stream_device(runs[r]) != dev) return fail(HDFS_CRC32C_EINVAL, "block %zu: not on device %d", r, dev);
   DevCtx *cp = nullptr;
   int rc;
   if ((rc = ctx_init(dev, &cp))) return rc;
@@ -1506,15 +1638,17 @@ int job_submit(const uint8_t *d, uint64_t len, int proto, uint32_t cs, int ctype
   if (!j) return fail(HDFS_CRC32C_ENOMEM, "job");
   j->dev = dev;
   j->slot = slot;
-  j->d = d;
-  j->len = len;
+  j->runs.assign(runs, runs + n);
+  j->lens.assign(lens, lens + n);
+  j->batch = batch;
   j->proto = proto;
   j->ctype = ctype;
   j->cs = cs;
   j->max_pkts = max_pkts;
-  // the speculative launch when the stream can hold a run it takes; else
+  // the speculative launch when every stream can hold a run it takes; else
   // the wait does the whole call
-  const bool spec = ctype != HDFS_CRC32C_CSUM_NULL && g_spec && max_pkts >= 2 && len > kSmallRunBytes;
+  bool spec = ctype != HDFS_CRC32C_CSUM_NULL && g_spec && max_pkts >= 2;
+  for (size_t r = 0; r < n; r++) spec = spec && lens[r] > kSmallRunBytes;
   if (spec) {
     SpecSlot &S = c.job_slot[slot];
     if (!S.stream) {
@@ -1524,8 +1658,17 @@ int job_submit(const uint8_t *d, uint64_t len, int proto, uint32_t cs, int ctype
         return fail(HDFS_CRC32C_EHIP, "job stream");
       }
     }
-    const uint32_t count = uint32_t(std::min<uint64_t>({uint64_t(max_pkts), kGridMaxCount, len / 6 + 1}));
-    const uint64_t bm_cap = align_up(len / 32 + count + 64, 256), need = bm_cap + uint64_t(count) * 4u + 256u;
+    // per run at most max_count packets; the bitmap takes ceil(chunks / 8)
+    // bytes per packet (<= len / 32 + 1), first-bad one word per packet
+    const uint32_t count = uint32_t(std::min<uint64_t>(uint64_t(max_pkts), kGridMaxCount));
+    uint64_t bm_cap = 64, fbw = 0;
+    for (size_t r = 0; r < n; r++) {
+      const uint64_t cr = std::min<uint64_t>(count, lens[r] / 6 + 1);
+      bm_cap += lens[r] / 32 + cr;
+      fbw += cr;
+    }
+    bm_cap = align_up(bm_cap, 256);
+    const uint64_t need = bm_cap + fbw * 4u + 256u;
     if (need > S.scratch_cap) {
       if (S.scratch) (void)hipFree(S.scratch);
       S.scratch = nullptr;
@@ -1537,8 +1680,8 @@ int job_submit(const uint8_t *d, uint64_t len, int proto, uint32_t cs, int ctype
       }
       S.scratch_cap = need;
     }
-    rc = spec_launch(c, S, S.stream, d, len, 0, count, proto, cs, ctype, CopyOut{}, 0, S.scratch,
-                     reinterpret_cast<uint32_t *>(S.scratch + bm_cap), j->L);
+    rc = spec_launch(c, S, S.stream, runs[0], lens[0], 0, count, proto, cs, ctype, CopyOut{}, 0, S.scratch,
+                     reinterpret_cast<uint32_t *>(S.scratch + bm_cap), j->L, uint32_t(n), runs, lens);
     if (rc) {
       delete j;
       return rc;
@@ -1550,7 +1693,11 @@ int job_submit(const uint8_t *d, uint64_t len, int proto, uint32_t cs, int ctype
   return HDFS_CRC32C_OK;
 }
 
-int job_wait(hdfs_crc32c_job *j, hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts, uint64_t *consumed) {
+// Block b of a job: its records at pkts + b * max_pkts.  rcs[b] = what
+// hdfs_crc32c_verify_packets returns for it; the call returns the first
+// negative status, else the first nonzero rcs[b] in block order, else 0.
+int job_wait(hdfs_crc32c_job *j, hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts, uint64_t *consumed,
+             int *rcs) {
   DevCtx *cp = nullptr;
   int rc;
   if ((rc = ctx_init(j->dev, &cp))) return rc;
@@ -1565,43 +1712,64 @@ int job_wait(hdfs_crc32c_job *j, hdfs_crc32c_packet *pkts, size_t max_pkts, size
       delete j;
     }
   } rel{c, j};
+  const size_t n = j->runs.size();
   const size_t cap = std::min(max_pkts, j->max_pkts);
-  size_t n = 0;
-  uint64_t used = 0, from = 0;
-  bool done = false, allow_spec = true;
+  std::vector<SpecRunResult> res(n);
+  bool allow_spec = true;
   if (j->launched) {
-    SpecResult sr;
-    std::vector<hdfs_crc32c_packet> recs(std::max<size_t>(1, std::min<uint64_t>(j->max_pkts, kGridMaxCount) + 1));
-    if ((rc = spec_collect(c, c.job_slot[j->slot], j->L, CopyOut{}, recs.data(), sr))) return rc;
-    if (sr.taken) {
-      if (sr.recorded > cap) return fail(HDFS_CRC32C_EINVAL, "wait: %zu records, room for %zu", size_t(sr.recorded), cap);
-      std::memcpy(pkts, recs.data(), size_t(sr.recorded) * sizeof(hdfs_crc32c_packet));
-      n = sr.recorded;
-      used = sr.consumed;
-      from = sr.next;
-      done = sr.end || n >= cap;
+    // the launch's records land in per-run scratch (count + 1 records each),
+    // then in the caller's array
+    const size_t per = std::max<size_t>(1, std::min<uint64_t>(j->max_pkts, kGridMaxCount) + 1);
+    std::vector<hdfs_crc32c_packet> recs(per * n);
+    std::vector<hdfs_crc32c_packet *> dst(n);
+    std::vector<uint64_t> pos0(n, 0);
+    for (size_t r = 0; r < n; r++) dst[r] = recs.data() + r * per;
+    if (n == 1) {
+      SpecResult sr;
+      if ((rc = spec_collect(c, c.job_slot[j->slot], j->L, CopyOut{}, dst[0], sr))) return rc;
+      res[0].taken = sr.taken;
+      res[0].end = sr.end;
+      res[0].recorded = sr.recorded;
+      res[0].consumed = sr.consumed;
+      res[0].next = sr.next;
+      if (!sr.taken) allow_spec = false;  // this stream has no run the launch takes: frame it
     } else {
-      allow_spec = false;  // this stream has no run the launch takes: frame it
+      if ((rc = spec_collect_batch(c.job_slot[j->slot], j->L, uint32_t(n), pos0.data(), dst.data(), res))) return rc;
+    }
+    for (size_t r = 0; r < n; r++) {
+      if (!res[r].taken) continue;
+      if (res[r].recorded > cap)
+        return fail(HDFS_CRC32C_EINVAL, "wait: %u records, room for %zu", res[r].recorded, cap);
+      std::memcpy(pkts + r * max_pkts, dst[r], size_t(res[r].recorded) * sizeof(hdfs_crc32c_packet));
     }
   }
-  if (!done && from < j->len) {
-    // the rest (or all) of the stream, synchronously on the engine stream
-    size_t n2 = 0;
-    uint64_t used2 = 0;
-    rc = grid_walk(c, j->d + from, j->len - from, j->proto, j->cs, j->ctype, cap - n, true, CopyOut{}, pkts + n, &n2,
-                   &used2, nullptr, allow_spec);
-    if (kDiag) {
-      const int r2 = device_checks("verify job");
-      if (r2) return r2;
+  int first = HDFS_CRC32C_OK;
+  for (size_t r = 0; r < n; r++) {
+    hdfs_crc32c_packet *out = pkts + r * max_pkts;
+    size_t k = res[r].taken ? res[r].recorded : 0;
+    uint64_t used = res[r].taken ? res[r].consumed : 0, from = res[r].taken ? res[r].next : 0;
+    const bool done = res[r].taken && (res[r].end || k >= cap);
+    if (!done && from < j->lens[r]) {
+      // the rest (or all) of the block, synchronously on the engine stream
+      size_t n2 = 0;
+      uint64_t used2 = 0;
+      rc = grid_walk(c, j->runs[r] + from, j->lens[r] - from, j->proto, j->cs, j->ctype, cap - k, true, CopyOut{},
+                     out + k, &n2, &used2, nullptr, allow_spec);
+      if (kDiag) {
+        const int r2 = device_checks("verify job");
+        if (r2) return r2;
+      }
+      if (rc) return rc;
+      for (size_t q = 0; q < n2; q++) out[k + q].stream_off += from;
+      k += n2;
+      if (n2 || used2) used = from + used2;
     }
-    if (rc) return rc;
-    for (size_t k = 0; k < n2; k++) pkts[n + k].stream_off += from;
-    n += n2;
-    if (n2 || used2) used = from + used2;
+    npkts[r] = k;
+    consumed[r] = used;
+    rcs[r] = first_error(out, k);
+    if (!first) first = rcs[r];
   }
-  *npkts = n;
-  *consumed = used;
-  return first_error(pkts, n);
+  return first;
 }
 
 // ---- client reads into host memory (hdfs_crc32c_read_packets, host iovecs) ----
@@ -2101,7 +2269,22 @@ int hdfs_crc32c_verify_packets_submit(const void *stream, uint64_t len, int prot
   int rc = check_framing_args(proto, chunk_size, ctype, g_err, sizeof(g_err));
   if (rc) return rc;
   if (!stream || !len) return fail(HDFS_CRC32C_EINVAL, "empty stream");
-  return job_submit(static_cast<const uint8_t *>(stream), len, proto, chunk_size, ctype, max_pkts, job);
+  const uint8_t *s = static_cast<const uint8_t *>(stream);
+  return job_submit(&s, &len, 1, false, proto, chunk_size, ctype, max_pkts, job);
+}
+
+int hdfs_crc32c_verify_blocks_submit(const void *const *streams, const uint64_t *lens, size_t nblocks, int proto,
+                                     uint32_t chunk_size, int ctype, size_t max_pkts, hdfs_crc32c_job **job) {
+  if (!job) return fail(HDFS_CRC32C_EINVAL, "null job");
+  *job = nullptr;
+  int rc = check_framing_args(proto, chunk_size, ctype, g_err, sizeof(g_err));
+  if (rc) return rc;
+  if (!streams || !lens || nblocks < 1 || nblocks > kSpecRunsMax)
+    return fail(HDFS_CRC32C_EINVAL, "blocks: 1 to %u streams (%zu given)", kSpecRunsMax, nblocks);
+  for (size_t b = 0; b < nblocks; b++)
+    if (!streams[b] || !lens[b]) return fail(HDFS_CRC32C_EINVAL, "block %zu: empty stream", b);
+  return job_submit(reinterpret_cast<const uint8_t *const *>(streams), lens, nblocks, true, proto, chunk_size, ctype,
+                    max_pkts, job);
 }
 
 int hdfs_crc32c_job_wait(hdfs_crc32c_job *job, hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts,
@@ -2109,14 +2292,30 @@ int hdfs_crc32c_job_wait(hdfs_crc32c_job *job, hdfs_crc32c_packet *pkts, size_t 
   if (npkts) *npkts = 0;
   if (consumed) *consumed = 0;
   if (!job) return fail(HDFS_CRC32C_EINVAL, "null job");
+  if (job->batch) return fail(HDFS_CRC32C_EINVAL, "a job of blocks: hdfs_crc32c_job_wait_blocks");
   if (max_pkts && !pkts) return fail(HDFS_CRC32C_EINVAL, "null packet array");
   size_t n = 0;
   uint64_t used = 0;
-  const int rc = job_wait(job, pkts, max_pkts, &n, &used);
+  int rcb = 0;
+  const int rc = job_wait(job, pkts, max_pkts, &n, &used, &rcb);
   if (rc < 0) return rc;
   if (npkts) *npkts = n;
   if (consumed) *consumed = used;
   return rc;
+}
+
+int hdfs_crc32c_job_wait_blocks(hdfs_crc32c_job *job, hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts,
+                                uint64_t *consumed, int *rcs) {
+  if (!job) return fail(HDFS_CRC32C_EINVAL, "null job");
+  const size_t n = job->runs.size();
+  if (!npkts || !consumed || !rcs || (max_pkts && !pkts))
+    return fail(HDFS_CRC32C_EINVAL, "null output arrays (%zu blocks)", n);
+  for (size_t b = 0; b < n; b++) {
+    npkts[b] = 0;
+    consumed[b] = 0;
+    rcs[b] = 0;
+  }
+  return job_wait(job, pkts, max_pkts, npkts, consumed, rcs);
 }
 
 #ifdef HDFS_CRC32C_DIAG

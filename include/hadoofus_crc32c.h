@@ -73,7 +73,9 @@ uint32_t _hdfs_sw_crc32c(uint32_t crc, const void *buf, unsigned len);
  *      resumable reads); versioned exports
  *   5: hdfs_crc32c_read_packets: a client read ends at its first error (bad
  *      CRCs included), host-memory iovecs and streams; asynchronous verify
- *      jobs (hdfs_crc32c_verify_packets_submit / hdfs_crc32c_job_wait) */
+ *      jobs (hdfs_crc32c_verify_packets_submit / hdfs_crc32c_job_wait) and
+ *      batches of blocks (hdfs_crc32c_verify_blocks_submit /
+ *      hdfs_crc32c_job_wait_blocks) */
 #define HDFS_CRC32C_ABI_VERSION 5
 int hdfs_crc32c_abi_version(void);
 
@@ -320,6 +322,18 @@ int hdfs_crc32c_verify_packets_submit(const void *stream, uint64_t len, int prot
     size_t max_pkts, hdfs_crc32c_job **job);
 int hdfs_crc32c_job_wait(hdfs_crc32c_job *job, hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts,
     uint64_t *consumed);
+/* A job of up to 16 BLOCKS (separate device-resident streams, one block
+ * transfer each) verified in ONE launch when their packets share one layout
+ * (packet size and header length; each block's own offsets and seqnos): the
+ * launch's fixed cost is paid once per batch.  Blocks the launch cannot take
+ * are verified one by one inside the wait.  hdfs_crc32c_job_wait_blocks:
+ * block b's records at pkts + b * max_pkts, npkts[b], consumed[b], and
+ * rcs[b] = what hdfs_crc32c_verify_packets returns for block b; returns the
+ * first negative status, else the first nonzero rcs[b], else 0. */
+int hdfs_crc32c_verify_blocks_submit(const void *const *streams, const uint64_t *lens, size_t nblocks, int proto,
+    uint32_t chunk_size, int ctype, size_t max_pkts, hdfs_crc32c_job **job);
+int hdfs_crc32c_job_wait_blocks(hdfs_crc32c_job *job, hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts,
+    uint64_t *consumed, int *rcs);
 
 /* ---- write path: outgoing data packets ---------------------------------- */
 /* One outgoing data packet, as _send_packet sizes it and

@@ -112,3 +112,71 @@ def test_gpu_jobs_limit_and_interleaving(engine, oracle):
     dst.free()
     for b, _ in bufs:
         b.free()
+
+
+# --- batches of blocks in one launch (hdfs_crc32c_verify_blocks_submit) -------
+def _block(oracle, k, dl=None, proto=2, ctype=CSUM_CRC32C, corrupt=(), **kw):
+    """Block k of a file: 64 KiB packets from offsetInBlock 0, the empty last
+    packet, its own data."""
+    dl = dl or [65536] * 100
+    s, _ = build_stream(oracle.crc32c, proto, 512, ctype, dl, seed=100 + k, corrupt=corrupt, **kw)
+    return s
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["equal", "corrupt_and_exceptions", "unequal_counts", "one_irregular",
+                                  "v1_crc32", "single", "sixteen"])
+def test_gpu_blocks_vs_oracle(engine, oracle, case):
+    """Each block's records, verdicts, consumed bytes and status equal the
+    oracle's verify of that block, whether the batch launch took every block
+    (equal layouts and counts), or none (a block of another packet count or
+    size, an irregular block: each then verified on its own in the wait)."""
+    kw = {}
+    if case == "equal":
+        streams = [_block(oracle, k) for k in range(4)]
+    elif case == "corrupt_and_exceptions":
+        streams = [_block(oracle, 0, corrupt=[(3, 1), (99, 127)]), _block(oracle, 1),
+                   _block(oracle, 2, seqnos=[k + (5 if k > 40 else 0) for k in range(100)], corrupt=[(64, 0)]),
+                   _block(oracle, 3, offset_skew={10: 512})]
+    elif case == "unequal_counts":
+        streams = [_block(oracle, 0), _block(oracle, 1, dl=[65536] * 90), _block(oracle, 2)]
+    elif case == "one_irregular":
+        streams = [_block(oracle, 0), _block(oracle, 1, dl=[65536] * 50 + [30000] + [65536] * 49),
+                   _block(oracle, 2)]
+    elif case == "v1_crc32":
+        streams = [_block(oracle, k, proto=1, ctype=CSUM_CRC32, last_empty=False) for k in range(3)]
+        kw = {"proto": 1, "ctype": CSUM_CRC32}
+    elif case == "single":
+        streams = [_block(oracle, 0, corrupt=[(7, 7)])]
+    else:
+        streams = [_block(oracle, k, corrupt=[(k, k)] if k % 5 == 0 else []) for k in range(16)]
+    proto, ctype = kw.get("proto", 2), kw.get("ctype", CSUM_CRC32C)
+    bufs = [_dev(engine, st, k % 3) for k, st in enumerate(streams)]
+    want = [oracle.verify_packets(st, proto, 512, ctype) for st in streams]
+    job = engine.VerifyBlocksJob([(p, len(st)) for (_, p), st in zip(bufs, streams)], proto, 512, ctype)
+    rc, got = job.wait()
+    for b in range(len(streams)):
+        assert got[b] == want[b], (case, b)
+    first = next((w[0] for w in want if w[0]), 0)
+    assert rc == first
+    for bb, _ in bufs:
+        bb.free()
+
+
+@pytest.mark.gpu
+def test_gpu_blocks_taken_in_one_launch(engine, oracle):
+    """The diagnostic build's counters: a batch of four equal blocks is one
+    speculative launch, eligible and taken."""
+    import ctypes
+    from hadoofus_amd import abi, build
+    diag = abi.bind_diag(abi.bind_product(ctypes.CDLL(build.DIAG_LIB)))
+    streams = [_block(oracle, k, corrupt=[(k, 0)]) for k in range(4)]
+    bufs = [_dev(engine, st) for st in streams]
+    out = (ctypes.c_uint64 * 4)()
+    diag.hdfs_crc32c_diag_spec_stats(out, 1)
+    rc, got = engine.VerifyBlocksJob([(p, len(st)) for (_, p), st in zip(bufs, streams)], lib=diag).wait()
+    assert diag.hdfs_crc32c_diag_spec_stats(out, 1) == 0
+    assert tuple(out) == (1, 1, 1, 0), tuple(out)
+    assert [g for g in got] == [oracle.verify_packets(st) for st in streams]
+    for bb, _ in bufs:
+        bb.free()

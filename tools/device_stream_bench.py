@@ -227,9 +227,11 @@ def resumed_reads(ptr, n, npk, payload, reps=3):
 def pipelined_blocks(blk, nblk, payload, nblocks=16, inflight=4, reps=3):
     """A datanode verifying a stream of received blocks: nblocks device-
     resident 128 MiB block transfers verified back to back, synchronously
-    (hdfs_crc32c_verify_packets per block) and as asynchronous jobs with up to
+    (hdfs_crc32c_verify_packets per block), as asynchronous jobs with up to
     `inflight` in flight (hdfs_crc32c_verify_packets_submit / _job_wait: one
-    block's launch ramp and tail overlap another's steady state).  Best of
+    block's launch ramp and tail overlap another's steady state), and as
+    batches of 4 / 8 / 16 blocks verified in one launch each
+    (hdfs_crc32c_verify_blocks_submit, two batches in flight).  Best of
     reps; per-block time and aggregate GiB/s of payload."""
     devs = []
     for _ in range(nblocks):
@@ -263,8 +265,32 @@ def pipelined_blocks(blk, nblk, payload, nblocks=16, inflight=4, reps=3):
             rc = lib.hdfs_crc32c_job_wait(j, a, nblk + 8, ctypes.byref(cnt), ctypes.byref(used))
             assert rc == 0 and cnt.value == nblk and used.value == n, (rc, cnt.value)
 
+    def batch_all(per):
+        # jobs of `per` blocks each, verified in one launch per job (two jobs in flight)
+        arr = (h.abi.Packet * ((nblk + 8) * per))()
+        npk, usd, rcs = (ctypes.c_size_t * per)(), (ctypes.c_uint64 * per)(), (ctypes.c_int * per)()
+        q = []
+
+        def wait_one(j):
+            rc = lib.hdfs_crc32c_job_wait_blocks(j, arr, nblk + 8, npk, usd, rcs)
+            assert rc == 0 and all(npk[b] == nblk and usd[b] == n for b in range(per)), (rc, list(npk))
+
+        for b0 in range(0, nblocks, per):
+            if len(q) == 2:
+                wait_one(q.pop(0))
+            ptrs = (ctypes.c_void_p * per)(*[d.ptr for d in devs[b0:b0 + per]])
+            lens = (ctypes.c_uint64 * per)(*([n] * per))
+            j = ctypes.c_void_p()
+            rc = lib.hdfs_crc32c_verify_blocks_submit(ptrs, lens, per, h.PROTO_V2, 512, h.CSUM_CRC32C, nblk + 8,
+                                                      ctypes.byref(j))
+            assert rc == 0, rc
+            q.append(j)
+        for j in q:
+            wait_one(j)
+
     res = {"blocks": nblocks, "inflight": inflight}
-    for name, fn in (("sync", sync_all), ("jobs", jobs_all)):
+    for name, fn in (("sync", sync_all), ("jobs", jobs_all), ("batch4", lambda: batch_all(4)),
+                     ("batch8", lambda: batch_all(8)), ("batch16", lambda: batch_all(16))):
         fn()
         best = 1e9
         for _ in range(reps):
@@ -301,7 +327,7 @@ def block_and_run(plan_GiBps=None):
     if plan_GiBps:
         for k in ("run_1GiB", "block_128MiB"):
             out[k]["frac_of_headline"] = round(out[k]["GiBps"] / plan_GiBps, 3)
-        for k in ("sync", "jobs"):
+        for k in ("sync", "jobs", "batch4", "batch8", "batch16"):
             sb = out["block_128MiB"]["stream_of_blocks"][k]
             sb["frac_of_headline"] = round(sb["GiBps"] / plan_GiBps, 3)
     out["note"] = ("hdfs_crc32c_verify_packets on v2 packet runs resident in HBM (64 KiB packets, 512 B chunks, "
