@@ -1605,6 +1605,7 @@ struct hdfs_crc32c_job {
   std::vector<const uint8_t *> runs;  // the block streams (one for hdfs_crc32c_verify_packets_submit)
   std::vector<uint64_t> lens;
   bool batch = false;                 // hdfs_crc32c_verify_blocks_submit
+  std::vector<size_t> sel;            // the blocks the launch covers (its runs, in order)
   int proto = 0, ctype = 0;
   uint32_t cs = 0;
   size_t max_pkts = 0;
@@ -1645,11 +1646,30 @@ int job_submit(const uint8_t *const *runs, const uint64_t *lens, size_t n, bool 
   j->ctype = ctype;
   j->cs = cs;
   j->max_pkts = max_pkts;
-  // the speculative launch when every stream can hold a run it takes; else
-  // the wait does the whole call
-  bool spec = ctype != HDFS_CRC32C_CSUM_NULL && g_spec && max_pkts >= 2;
-  for (size_t r = 0; r < n; r++) spec = spec && lens[r] > kSmallRunBytes;
+  // The launch covers the largest group of blocks of one length (the first
+  // such group on a tie): blocks of one layout and length hold the same
+  // number of packets, which a batch launch needs (its table maps packet k
+  // to run k / count); the others -- a file's short last block, say -- are
+  // verified one by one in the wait.  A stream too short for a run the
+  // launch would take is left to the wait too.
+  for (size_t b = 0; b < n; b++) {
+    if (lens[b] <= kSmallRunBytes) continue;
+    size_t same = 0;
+    for (size_t q = 0; q < n; q++) same += lens[q] == lens[b] ? 1u : 0u;
+    if (j->sel.empty() || same > j->sel.size()) {
+      j->sel.clear();
+      for (size_t q = 0; q < n; q++)
+        if (lens[q] == lens[b]) j->sel.push_back(q);
+    }
+  }
+  const bool spec = ctype != HDFS_CRC32C_CSUM_NULL && g_spec && max_pkts >= 2 && !j->sel.empty();
   if (spec) {
+    std::vector<const uint8_t *> sruns;
+    std::vector<uint64_t> slens;
+    for (size_t b : j->sel) {
+      sruns.push_back(runs[b]);
+      slens.push_back(lens[b]);
+    }
     SpecSlot &S = c.job_slot[slot];
     if (!S.stream) {
       if (hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking) != hipSuccess) {
@@ -1662,9 +1682,9 @@ int job_submit(const uint8_t *const *runs, const uint64_t *lens, size_t n, bool 
     // bytes per packet (<= len / 32 + 1), first-bad one word per packet
     const uint32_t count = uint32_t(std::min<uint64_t>(uint64_t(max_pkts), kGridMaxCount));
     uint64_t bm_cap = 64, fbw = 0;
-    for (size_t r = 0; r < n; r++) {
-      const uint64_t cr = std::min<uint64_t>(count, lens[r] / 6 + 1);
-      bm_cap += lens[r] / 32 + cr;
+    for (uint64_t l : slens) {
+      const uint64_t cr = std::min<uint64_t>(count, l / 6 + 1);
+      bm_cap += l / 32 + cr;
       fbw += cr;
     }
     bm_cap = align_up(bm_cap, 256);
@@ -1680,8 +1700,9 @@ int job_submit(const uint8_t *const *runs, const uint64_t *lens, size_t n, bool 
       }
       S.scratch_cap = need;
     }
-    rc = spec_launch(c, S, S.stream, runs[0], lens[0], 0, count, proto, cs, ctype, CopyOut{}, 0, S.scratch,
-                     reinterpret_cast<uint32_t *>(S.scratch + bm_cap), j->L, uint32_t(n), runs, lens);
+    rc = spec_launch(c, S, S.stream, sruns[0], slens[0], 0, count, proto, cs, ctype, CopyOut{}, 0, S.scratch,
+                     reinterpret_cast<uint32_t *>(S.scratch + bm_cap), j->L, uint32_t(sruns.size()), sruns.data(),
+                     slens.data());
     if (rc) {
       delete j;
       return rc;
@@ -1718,29 +1739,32 @@ int job_wait(hdfs_crc32c_job *j, hdfs_crc32c_packet *pkts, size_t max_pkts, size
   bool allow_spec = true;
   if (j->launched) {
     // the launch's records land in per-run scratch (count + 1 records each),
-    // then in the caller's array
+    // then in the caller's array at the run's block
+    const size_t m = j->sel.size();
     const size_t per = std::max<size_t>(1, std::min<uint64_t>(j->max_pkts, kGridMaxCount) + 1);
-    std::vector<hdfs_crc32c_packet> recs(per * n);
-    std::vector<hdfs_crc32c_packet *> dst(n);
-    std::vector<uint64_t> pos0(n, 0);
-    for (size_t r = 0; r < n; r++) dst[r] = recs.data() + r * per;
-    if (n == 1) {
+    std::vector<hdfs_crc32c_packet> recs(per * m);
+    std::vector<hdfs_crc32c_packet *> dst(m);
+    std::vector<uint64_t> pos0(m, 0);
+    std::vector<SpecRunResult> rr(m);
+    for (size_t r = 0; r < m; r++) dst[r] = recs.data() + r * per;
+    if (m == 1) {
       SpecResult sr;
       if ((rc = spec_collect(c, c.job_slot[j->slot], j->L, CopyOut{}, dst[0], sr))) return rc;
-      res[0].taken = sr.taken;
-      res[0].end = sr.end;
-      res[0].recorded = sr.recorded;
-      res[0].consumed = sr.consumed;
-      res[0].next = sr.next;
-      if (!sr.taken) allow_spec = false;  // this stream has no run the launch takes: frame it
+      rr[0].taken = sr.taken;
+      rr[0].end = sr.end;
+      rr[0].recorded = sr.recorded;
+      rr[0].consumed = sr.consumed;
+      rr[0].next = sr.next;
+      if (!sr.taken && n == 1) allow_spec = false;  // this stream has no run the launch takes: frame it
     } else {
-      if ((rc = spec_collect_batch(c.job_slot[j->slot], j->L, uint32_t(n), pos0.data(), dst.data(), res))) return rc;
+      if ((rc = spec_collect_batch(c.job_slot[j->slot], j->L, uint32_t(m), pos0.data(), dst.data(), rr))) return rc;
     }
-    for (size_t r = 0; r < n; r++) {
-      if (!res[r].taken) continue;
-      if (res[r].recorded > cap)
-        return fail(HDFS_CRC32C_EINVAL, "wait: %u records, room for %zu", res[r].recorded, cap);
-      std::memcpy(pkts + r * max_pkts, dst[r], size_t(res[r].recorded) * sizeof(hdfs_crc32c_packet));
+    for (size_t r = 0; r < m; r++) {
+      const size_t b = j->sel[r];
+      res[b] = rr[r];
+      if (!rr[r].taken) continue;
+      if (rr[r].recorded > cap) return fail(HDFS_CRC32C_EINVAL, "wait: %u records, room for %zu", rr[r].recorded, cap);
+      std::memcpy(pkts + b * max_pkts, dst[r], size_t(rr[r].recorded) * sizeof(hdfs_crc32c_packet));
     }
   }
   int first = HDFS_CRC32C_OK;

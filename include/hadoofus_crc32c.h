@@ -325,8 +325,10 @@ int hdfs_crc32c_job_wait(hdfs_crc32c_job *job, hdfs_crc32c_packet *pkts, size_t 
 /* A job of up to 16 BLOCKS (separate device-resident streams, one block
  * transfer each) verified in ONE launch when their packets share one layout
  * (packet size and header length; each block's own offsets and seqnos): the
- * launch's fixed cost is paid once per batch.  Blocks the launch cannot take
- * are verified one by one inside the wait.  hdfs_crc32c_job_wait_blocks:
+ * launch's fixed cost is paid once per batch.  The launch covers the largest
+ * group of blocks of one length (blocks of one layout and length hold the
+ * same number of packets); the other blocks -- a file's short last block --
+ * and any the launch cannot take are verified one by one inside the wait.  hdfs_crc32c_job_wait_blocks:
  * block b's records at pkts + b * max_pkts, npkts[b], consumed[b], and
  * rcs[b] = what hdfs_crc32c_verify_packets returns for block b; returns the
  * first negative status, else the first nonzero rcs[b], else 0. */

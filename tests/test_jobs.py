@@ -124,8 +124,8 @@ def _block(oracle, k, dl=None, proto=2, ctype=CSUM_CRC32C, corrupt=(), **kw):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["equal", "corrupt_and_exceptions", "unequal_counts", "one_irregular",
-                                  "v1_crc32", "single", "sixteen"])
+@pytest.mark.parametrize("case", ["equal", "corrupt_and_exceptions", "unequal_counts", "short_last_block",
+                                  "one_irregular", "v1_crc32", "single", "sixteen"])
 def test_gpu_blocks_vs_oracle(engine, oracle, case):
     """Each block's records, verdicts, consumed bytes and status equal the
     oracle's verify of that block, whether the batch launch took every block
@@ -138,8 +138,10 @@ def test_gpu_blocks_vs_oracle(engine, oracle, case):
         streams = [_block(oracle, 0, corrupt=[(3, 1), (99, 127)]), _block(oracle, 1),
                    _block(oracle, 2, seqnos=[k + (5 if k > 40 else 0) for k in range(100)], corrupt=[(64, 0)]),
                    _block(oracle, 3, offset_skew={10: 512})]
-    elif case == "unequal_counts":
+    elif case == "unequal_counts":  # the launch takes blocks 0 and 2 (one length), block 1 in the wait
         streams = [_block(oracle, 0), _block(oracle, 1, dl=[65536] * 90), _block(oracle, 2)]
+    elif case == "short_last_block":
+        streams = [_block(oracle, k) for k in range(5)] + [_block(oracle, 5, dl=[65536] * 7 + [1000])]
     elif case == "one_irregular":
         streams = [_block(oracle, 0), _block(oracle, 1, dl=[65536] * 50 + [30000] + [65536] * 49),
                    _block(oracle, 2)]
@@ -178,5 +180,15 @@ def test_gpu_blocks_taken_in_one_launch(engine, oracle):
     assert diag.hdfs_crc32c_diag_spec_stats(out, 1) == 0
     assert tuple(out) == (1, 1, 1, 0), tuple(out)
     assert [g for g in got] == [oracle.verify_packets(st) for st in streams]
+    # a short last block: the launch still takes the four equal ones
+    last = _block(oracle, 9, dl=[65536] * 5 + [777])
+    lb = _dev(engine, last)
+    diag.hdfs_crc32c_diag_spec_stats(out, 1)
+    rc, got = engine.VerifyBlocksJob([(p, len(st)) for (_, p), st in zip(bufs, streams)] + [(lb[1], len(last))],
+                                     lib=diag).wait()
+    diag.hdfs_crc32c_diag_spec_stats(out, 1)
+    assert tuple(out)[:3] == (1, 1, 1), tuple(out)
+    assert got == [oracle.verify_packets(st) for st in streams + [last]]
+    lb[0].free()
     for bb, _ in bufs:
         bb.free()
