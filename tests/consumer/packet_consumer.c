@@ -11,7 +11,10 @@
  * copy-out (hdfs_crc32c_read_packets: c_begin, remains_tot,
  * src/datanode.c:2478-2549), once into one buffer and once resumed over a
  * scatter list of small buffers (HDFS_CRC32C_AGAIN); (5) maps an engine failure the way a datanode
- * must -- an I/O error, never a checksum error.
+ * must -- an I/O error, never a checksum error;
+ * (6) reads into host memory from the host and the device stream; (7)
+ * verifies three device-resident blocks as asynchronous jobs and as one
+ * batch (ABI 5).
  * Prints "0 failures" on success.  Test infrastructure (tests/test_abi.py
  * links it on CPU, tests/test_packets.py runs it on the GPU).
  */
@@ -258,15 +261,79 @@ int main(void)
 		free(back);
 	}
 
-	/* (5) an engine failure (here: a host buffer where device memory is
-	 * required) is an I/O error for the datanode, not a checksum error */
+	/* (5) an engine failure (here: a host-resident stream into a device
+	 * buffer, which the engine refuses) is an I/O error for the datanode,
+	 * not a checksum error */
 	{
 		uint64_t delivered = 0;
-		hdfs_crc32c_iovec hv = {data, DLEN};
-		rc = hdfs_crc32c_read_packets(s, total, HDFS_CRC32C_PROTO_V2, CS, HDFS_CRC32C_CSUM_CRC32C, 0,
-		    HDFS_CRC32C_READ_ALL, &hv, 1, rec, NPK + 1, &n, &used, &delivered);
+		void *dbuf = NULL;
+		check(hdfs_crc32c_dev_alloc(&dbuf, DLEN) == 0, "dev_alloc");
+		hdfs_crc32c_iovec dv = {dbuf, DLEN};
+		rc = hdfs_crc32c_read_packets(s, total, HDFS_CRC32C_PROTO_V2, CS, HDFS_CRC32C_CSUM_CRC32C, 0, DLEN, &dv, 1,
+		    rec, NPK + 1, &n, &used, &delivered);
 		const struct dn_error e = map_engine_rc(rc);
 		check(rc == HDFS_CRC32C_EINVAL && e.kind == 2 && e.num == EIO, "engine failure -> EIO");
+		hdfs_crc32c_dev_free(dbuf);
+	}
+	/* (6) a host-memory datanode (ABI 5): the same client read from the
+	 * host stream into the user's host iovecs in one call -- framed on the
+	 * host, verified on the GPU, copied as src/datanode.c:2516 does -- and
+	 * from the device stream into host memory */
+	{
+		uint64_t delivered = 0;
+		uint8_t *u0 = malloc(DLEN), *u1 = malloc(2 * DLEN);
+		hdfs_crc32c_iovec hv[2] = {{u0, DLEN}, {u1, 2 * DLEN}};
+		rc = hdfs_crc32c_read_packets(s + 8 * pk, total - 8 * pk, HDFS_CRC32C_PROTO_V2, CS, HDFS_CRC32C_CSUM_CRC32C,
+		    8 * (int64_t)DLEN + 5, 2 * (int64_t)DLEN, hv, 2, rec, NPK + 1, &n, &used, &delivered);
+		check(rc == 0 && n == 3 && delivered == 2 * DLEN && used == 3 * pk, "host read: records");
+		check(memcmp(u0, s + 8 * pk + 31 + crclen + 5, DLEN - 5) == 0 &&
+		    memcmp(u0 + DLEN - 5, s + 9 * pk + 31 + crclen, 5) == 0 &&
+		    memcmp(u1, s + 9 * pk + 31 + crclen + 5, DLEN - 5) == 0 &&
+		    memcmp(u1 + DLEN - 5, s + 10 * pk + 31 + crclen, 5) == 0, "host read: bytes");
+		/* the bad packet ends the read there, as on the device */
+		rc = hdfs_crc32c_read_packets(s + 3 * pk, total - 3 * pk, HDFS_CRC32C_PROTO_V2, CS, HDFS_CRC32C_CSUM_CRC32C,
+		    3 * (int64_t)DLEN + 1000, 5 * (int64_t)DLEN + 777, hv, 2, rec, NPK + 1, &n, &used, &delivered);
+		check(rc == HDFS_CRC32C_AGAIN && n == 3 && delivered == 3 * DLEN, "host read: buffers fill before the bad packet");
+		void *dstream = NULL;
+		check(hdfs_crc32c_dev_alloc(&dstream, total) == 0 && hdfs_crc32c_memcpy(dstream, s, total, 0) == 0, "upload");
+		memset(u0, 0, DLEN);
+		memset(u1, 0, 2 * DLEN);
+		rc = hdfs_crc32c_read_packets((uint8_t *)dstream + 8 * pk, total - 8 * pk, HDFS_CRC32C_PROTO_V2, CS,
+		    HDFS_CRC32C_CSUM_CRC32C, 8 * (int64_t)DLEN + 5, 2 * (int64_t)DLEN, hv, 2, rec, NPK + 1, &n, &used,
+		    &delivered);
+		check(rc == 0 && delivered == 2 * DLEN && memcmp(u1 + DLEN - 5, s + 10 * pk + 31 + crclen, 5) == 0,
+		    "device stream into host memory");
+		/* (7) three received blocks in HBM: asynchronous jobs, and one batch */
+		void *blk[3] = {dstream, NULL, NULL};
+		uint64_t blen[3] = {total, total, total};
+		for (int b = 1; b < 3; b++)
+			check(hdfs_crc32c_dev_alloc(&blk[b], total) == 0 && hdfs_crc32c_memcpy(blk[b], s, total, 0) == 0,
+			    "upload block");
+		hdfs_crc32c_job *job[3];
+		for (int b = 0; b < 3; b++)
+			check(hdfs_crc32c_verify_packets_submit(blk[b], total, HDFS_CRC32C_PROTO_V2, CS, HDFS_CRC32C_CSUM_CRC32C,
+			    NPK + 1, &job[b]) == 0, "submit");
+		for (int b = 2; b >= 0; b--) {
+			rc = hdfs_crc32c_job_wait(job[b], rec, NPK + 1, &n, &used);
+			check(rc == HDFS_CRC32C_ERR_DATANODE_BAD_CHECKSUM && n == NPK + 1 && used == total &&
+			    rec[7].first_bad == 3, "job wait");
+		}
+		hdfs_crc32c_packet *brec = calloc(3 * (NPK + 1), sizeof(*brec));
+		size_t bn[3];
+		uint64_t bused[3];
+		int brc[3];
+		check(hdfs_crc32c_verify_blocks_submit((const void *const *)blk, blen, 3, HDFS_CRC32C_PROTO_V2, CS,
+		    HDFS_CRC32C_CSUM_CRC32C, NPK + 1, &job[0]) == 0, "blocks submit");
+		rc = hdfs_crc32c_job_wait_blocks(job[0], brec, NPK + 1, bn, bused, brc);
+		check(rc == HDFS_CRC32C_ERR_DATANODE_BAD_CHECKSUM, "blocks wait rc");
+		for (int b = 0; b < 3; b++)
+			check(brc[b] == HDFS_CRC32C_ERR_DATANODE_BAD_CHECKSUM && bn[b] == NPK + 1 && bused[b] == total &&
+			    brec[b * (NPK + 1) + 7].first_bad == 3 && brec[b * (NPK + 1) + NPK].last, "blocks wait records");
+		free(brec);
+		for (int b = 0; b < 3; b++)
+			hdfs_crc32c_dev_free(blk[b]);
+		free(u0);
+		free(u1);
 	}
 	printf("%d failures\n", failures);
 	free(s);
