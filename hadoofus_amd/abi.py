@@ -146,6 +146,12 @@ def bind_product(lib):
           [ctypes.POINTER(_vp), ctypes.POINTER(_u64), _sz, _int, _u32, _int, _sz, ctypes.POINTER(_vp)])
     _bind(lib, "hdfs_crc32c_job_wait_blocks", _int,
           [_vp, ctypes.POINTER(Packet), _sz, ctypes.POINTER(_sz), ctypes.POINTER(_u64), ctypes.POINTER(_int)])
+    _bind(lib, "hdfs_crc32c_reader_open", _int,
+          [_vp, _u64, _int, _u32, _int, ctypes.c_int64, ctypes.c_int64, _sz, ctypes.POINTER(_vp)])
+    _bind(lib, "hdfs_crc32c_reader_next", _int,
+          [_vp, ctypes.POINTER(IoVec), _int, ctypes.POINTER(Packet), _sz, ctypes.POINTER(_sz), ctypes.POINTER(_u64),
+           ctypes.POINTER(_u64)])
+    _bind(lib, "hdfs_crc32c_reader_close", None, [_vp])
     _bind(lib, "hdfs_crc32c_abi_version", _int, [])
     _bind(lib, "hdfs_crc32c_session_create", _int, [ctypes.POINTER(_vp), _int, _u32, _int, _u64, _sz])
     _bind(lib, "hdfs_crc32c_session_buffer", _int, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_u64)])
@@ -423,6 +429,35 @@ def read_packets(dptr, nbytes, dst, dst_cap, proto=PROTO_V2, chunk_size=512, cty
     if rc < 0:
         _check(rc, lib)
     return rc, [arr[i].as_dict() for i in range(npk.value)], used.value, got.value
+
+
+class Reader:
+    """hdfs_crc32c_reader_*: a client read of a device-resident stream
+    verified once (open), delivered piece by piece (next)."""
+
+    def __init__(self, dptr, nbytes, client_offset, read_len, proto=PROTO_V2, chunk_size=512, ctype=CSUM_CRC32C,
+                 max_pkts=None, lib=None):
+        self.lib = lib or load()
+        self.max_pkts = nbytes // (25 if proto == PROTO_V1 else 6) + 1 if max_pkts is None else max_pkts
+        self.rd = _vp()
+        _check(self.lib.hdfs_crc32c_reader_open(dptr, nbytes, proto, chunk_size, ctype, client_offset, read_len,
+                                                 self.max_pkts, ctypes.byref(self.rd)), self.lib)
+        self.arr = (Packet * max(1, min(self.max_pkts, 1 << 16)))()
+
+    def next(self, iov):
+        """iov = [(ptr, len), ...] -> (rc, [packet dicts], consumed, delivered)."""
+        vec = (IoVec * max(1, len(iov)))(*[IoVec(p, n) for p, n in iov])
+        npk, used, got = _sz(0), _u64(0), _u64(0)
+        rc = self.lib.hdfs_crc32c_reader_next(self.rd, vec, len(iov), self.arr, len(self.arr), ctypes.byref(npk),
+                                              ctypes.byref(used), ctypes.byref(got))
+        if rc < 0:
+            _check(rc, self.lib)
+        return rc, [self.arr[i].as_dict() for i in range(npk.value)], used.value, got.value
+
+    def close(self):
+        if self.rd:
+            self.lib.hdfs_crc32c_reader_close(self.rd)
+            self.rd = None
 
 
 class VerifyJob:

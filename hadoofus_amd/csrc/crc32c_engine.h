@@ -60,6 +60,9 @@ hipError_t launch_header_window(const uint8_t *s, uint64_t len, uint64_t base, u
 // Copy-out (copy_dst non-null): each packet delivers frame::read_avail bytes
 // (win: the client read window from client_offset; else whole payloads),
 // placed by frame::read_place within copy_cap bytes of copy_dst.
+// A verified read's next bytes to device buffers (copy_pieces_kernel), grid
+// workgroups of 256 threads, <= kCopyBlocksMax.
+hipError_t launch_copy_pieces(const CopyPieces &a, int grid, hipStream_t stream);
 hipError_t launch_small_run(const uint8_t *s, uint64_t len, uint32_t count, int proto, uint32_t cs, int ctype,
                             int verify, const uint32_t *tab, const uint32_t *pow2, uint8_t *copy_dst,
                             uint64_t copy_cap, int win, int64_t client_offset, uint8_t *hout, uint32_t seq,

@@ -312,6 +312,28 @@ constexpr uint32_t kGridGroups = kGridMaxCount / 64 / 64;  // frame_build_kernel
 // per grid point: the record (56 B), then u32 {status | unsupported << 8,
 // first bad chunk, bad chunks, seq} -- seq written last.
 constexpr uint32_t kSmallRunMax = 64;
+// Delivery of an already verified client read (hdfs_crc32c_reader_next):
+// up to kCopyPiecesMax pieces (packet payload bytes at any alignment -> the
+// caller's device buffer) in one launch of copy_pieces_kernel.  A piece is
+// cut into units, the 16-B aligned blocks of its destination it touches
+// (whole ones stored as one dwordx4, its first and last byte by byte); the
+// last workgroup to finish (a device counter) publishes the call's sequence
+// number to one pinned word.
+constexpr uint32_t kCopyPiecesMax = 32;
+constexpr uint32_t kCopyBlocksMax = 512;
+struct CopyPieces {
+  const uint8_t *src[kCopyPiecesMax];
+  uint8_t *dst[kCopyPiecesMax];
+  uint32_t len[kCopyPiecesMax];
+  uint32_t uend[kCopyPiecesMax];  // cumulative units: piece i covers units [uend[i - 1], uend[i])
+  uint32_t n, seq;
+  uint32_t *done;                 // pinned, device address: the completion word
+  uint32_t *count;                // device: workgroups finished (the last one resets it)
+};
+// Units of a piece whose destination starts at d and holds len bytes.
+inline uint32_t copy_units(uintptr_t d, uint64_t len) {
+  return len ? uint32_t(((d + len + 15u) & ~uintptr_t(15)) - (d & ~uintptr_t(15))) / 16u : 0u;
+}
 constexpr uint32_t kSrSlot = 128;
 constexpr uint32_t kSrHostBytes = kSmallRunMax * kSrSlot;
 constexpr uint64_t kSmallRunBytes = uint64_t(kSmallRunMax) * (65536 + 4096);  // streams up to this try it

@@ -3534,6 +3534,87 @@ __global__ __launch_bounds__(1024) void small_run_kernel(const uint8_t *__restri
   }
 }
 
+// Copy of a verified read's next bytes.  Thread u of the grid (strided when
+// the call has more units than threads) takes unit u: the 16-B aligned
+// destination block D of piece i = the first with uend[i] > u (the piece
+// table is staged in LDS).  A whole unit reads the dword-aligned window
+// around its 16 source bytes and funnel-shifts it into place (packet payloads
+// sit at any byte offset of the wire stream), one dwordx4 store; the piece's
+// first and last unit go byte by byte.  Consecutive lanes take consecutive
+// units: loads and stores coalesce.  Stores are sc1 (written through the
+// XCD's L2 to memory, so no L2 write-back is needed for another XCD or a
+// later kernel to read them); every wave waits for its stores, and after the
+// workgroup barrier one lane counts the workgroup done (agent atomic); the
+// last one resets the counter and publishes the sequence number to the host
+// (one pinned word: no stream synchronisation).
+DEV void store16_sc1(uint8_t *p, u32x4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+DEV void store8_sc1(uint8_t *p, uint32_t v) {
+  asm volatile("global_store_byte %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+
+__global__ __launch_bounds__(256) void copy_pieces_kernel(CopyPieces a) {
+  __shared__ const uint8_t *lsrc[kCopyPiecesMax];
+  __shared__ uintptr_t ldst[kCopyPiecesMax], lend[kCopyPiecesMax];
+  __shared__ uint32_t luend[kCopyPiecesMax + 1];
+  const uint32_t n = a.n;
+  if (threadIdx.x < n) {
+    const uint32_t t = threadIdx.x;
+    lsrc[t] = a.src[t];
+    ldst[t] = reinterpret_cast<uintptr_t>(a.dst[t]);
+    lend[t] = reinterpret_cast<uintptr_t>(a.dst[t]) + a.len[t];
+    luend[t + 1u] = a.uend[t];
+  }
+  if (threadIdx.x == 0) luend[0] = 0u;
+  __syncthreads();
+  const uint32_t total = luend[n];
+  for (uint32_t u = blockIdx.x * 256u + threadIdx.x; u < total; u += gridDim.x * 256u) {
+    uint32_t lo = 0, hi = n - 1u;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (luend[mid + 1u] > u) hi = mid; else lo = mid + 1u;
+    }
+    const uintptr_t d = ldst[lo], e = lend[lo];
+    const uintptr_t D = (d & ~uintptr_t(15)) + 16u * uintptr_t(u - luend[lo]);
+    const uint8_t *src = lsrc[lo];
+    if (D >= d && D + 16u <= e) {
+      const uintptr_t sa = reinterpret_cast<uintptr_t>(src) + (D - d);
+      const uint32_t sh = uint32_t(sa & 3u);
+      const uint8_t *a0 = reinterpret_cast<const uint8_t *>(sa - sh);
+      uint32_t w[5];
+#pragma unroll
+      for (int k = 0; k < 4; k++) w[k] = gload32(a0 + 4 * k);
+      w[4] = sh ? gload32(a0 + 16) : 0u;  // only when it holds one of the bytes
+      u32x4 v;
+      v.x = align_word(w[1], w[0], sh);
+      v.y = align_word(w[2], w[1], sh);
+      v.z = align_word(w[3], w[2], sh);
+      v.w = align_word(w[4], w[3], sh);
+      store16_sc1(reinterpret_cast<uint8_t *>(D), v);
+    } else {
+      const uintptr_t x0 = D > d ? D : d, x1 = D + 16u < e ? D + 16u : e;
+      for (uintptr_t x = x0; x < x1; x++) store8_sc1(reinterpret_cast<uint8_t *>(x), gload8(src + (x - d)));
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t prev = __hip_atomic_fetch_add(a.count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev + 1u == gridDim.x) {
+      __hip_atomic_store(a.count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(a.done, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+hipError_t launch_copy_pieces(const CopyPieces &a, int grid, hipStream_t stream) {
+  if (!a.n || a.n > kCopyPiecesMax || grid < 1 || grid > int(kCopyBlocksMax) || !a.done || !a.count)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(copy_pieces_kernel, dim3(grid), dim3(256), 0, stream, a);
+  return hipGetLastError();
+}
+
 hipError_t launch_small_run(const uint8_t *s, uint64_t len, uint32_t count, int proto, uint32_t cs, int ctype,
                             int verify, const uint32_t *tab, const uint32_t *pow2, uint8_t *copy_dst,
                             uint64_t copy_cap, int win, int64_t client_offset, uint8_t *hout, uint32_t seq,

@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <memory>
 #include <thread>
 #include <vector>
 
@@ -1462,7 +1463,8 @@ int apply_read_window(hdfs_crc32c_packet *p, size_t &n, uint64_t &consumed, cons
 
 int verify_packets_dev_impl(int dev, const uint8_t *stream, uint64_t len, int proto, uint32_t cs, int ctype,
                             hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts, uint64_t *consumed,
-                            bool verify, const CopyOut &co = CopyOut{}, uint64_t *delivered = nullptr) {
+                            bool verify, const CopyOut &co = CopyOut{}, uint64_t *delivered = nullptr,
+                            Pieces *pieces = nullptr) {
   DevCtx *cp = nullptr;
   int rc;
   if ((rc = ctx_init(dev, &cp))) return rc;
@@ -1479,7 +1481,7 @@ int verify_packets_dev_impl(int dev, const uint8_t *stream, uint64_t len, int pr
   if (rc) return rc;
   int again = 0;
   if (co.win) {
-    again = apply_read_window(pkts, n, used, co, delivered);
+    again = apply_read_window(pkts, n, used, co, delivered, pieces);
   } else if (delivered) {  // what the reference copies out before its loop returns an error (src/datanode.c:2470-2486)
     uint64_t b = 0;
     for (size_t i = 0; i < n; i++) {
@@ -1969,6 +1971,197 @@ int read_host_to_host(const uint8_t *s, uint64_t len, int proto, uint32_t cs, in
   return rc ? rc : again ? HDFS_CRC32C_AGAIN : HDFS_CRC32C_OK;
 }
 
+// ---- verified reads delivered piece by piece (hdfs_crc32c_reader_*) ----
+}  // namespace
+}  // namespace hdfs_crc32c
+
+struct hdfs_crc32c_reader {
+  int dev = -1;
+  const uint8_t *s = nullptr;
+  std::vector<hdfs_crc32c_packet> recs;  // the read's records (the one that ended it last)
+  hdfs_crc32c::Pieces pieces;            // its bytes: (stream offset, length) in delivery order
+  std::vector<uint64_t> rec_done;        // records[k] is complete once this many bytes are delivered
+  int status = 0;                        // what the read returns once delivered (0 or the error)
+  uint64_t total = 0, done = 0, consumed = 0;
+  size_t piece = 0, rec_next = 0;
+  uint64_t piece_off = 0;
+  uint32_t *hdone = nullptr, *ddone = nullptr;  // pinned completion word of the copy kernel
+  uint32_t *count = nullptr;                    // device: its workgroup counter
+  uint32_t seq = 0;
+};
+
+namespace hdfs_crc32c {
+namespace {
+
+int reader_open(const uint8_t *s, uint64_t len, int proto, uint32_t cs, int ctype, int64_t client_offset,
+                int64_t read_len, size_t max_pkts, hdfs_crc32c_reader **out) {
+  const int dev = stream_device(s);
+  if (dev < 0) return fail(HDFS_CRC32C_EINVAL, "a reader takes a device-resident stream");
+  auto *rd = new (std::nothrow) hdfs_crc32c_reader;
+  if (!rd) return fail(HDFS_CRC32C_ENOMEM, "reader");
+  std::unique_ptr<hdfs_crc32c_reader, void (*)(hdfs_crc32c_reader *)> guard(rd, [](hdfs_crc32c_reader *r) {
+    if (r->hdone) (void)hipHostFree(r->hdone);
+    if (r->count) (void)hipFree(r->count);
+    delete r;
+  });
+  rd->dev = dev;
+  rd->s = s;
+  rd->recs.resize(std::max<size_t>(1, max_pkts));
+  CopyOut co;  // the window only: no copy now, the bytes go out with each next
+  co.win = true;
+  co.client_offset = client_offset;
+  co.want = co.cap = uint64_t(read_len);
+  size_t n = 0;
+  uint64_t used = 0, got = 0;
+  int rc = verify_packets_dev_impl(dev, s, len, proto, cs, ctype, rd->recs.data(), max_pkts, &n, &used, true, co, &got,
+                                   &rd->pieces);
+  if (rc < 0) return rc;
+  rd->recs.resize(n);
+  rd->status = rc == HDFS_CRC32C_AGAIN ? HDFS_CRC32C_OK : rc;  // (the window is the whole read: no AGAIN)
+  rd->total = got;
+  rd->consumed = used;
+  // a record is complete once every byte before the end of its data is out
+  rd->rec_done.resize(n);
+  {
+    size_t pi = 0;
+    uint64_t cum = 0;
+    for (size_t k = 0; k < n; k++) {
+      const hdfs_crc32c_packet &r = rd->recs[k];
+      const uint64_t d0 = wire_begin(r) + uint64_t(r.crc_len > 0 ? r.crc_len : 0);
+      const uint64_t d1 = d0 + uint64_t(r.data_len > 0 ? r.data_len : 0);
+      while (pi < rd->pieces.size() && rd->pieces[pi].first >= d0 && rd->pieces[pi].first < d1) {
+        cum += rd->pieces[pi].second;
+        pi++;
+      }
+      rd->rec_done[k] = k + 1 == n ? got : cum;  // the last record (an error, or the read's end) goes with the end
+    }
+  }
+  {
+    DeviceGuard g(dev);
+    if (hipHostMalloc(&rd->hdone, sizeof(uint32_t), hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
+      (void)hipGetLastError();
+      rd->hdone = nullptr;
+      return fail(HDFS_CRC32C_ENOMEM, "reader completion word");
+    }
+    *rd->hdone = 0;
+    HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&rd->ddone), rd->hdone, 0));
+    if (hipMalloc(&rd->count, sizeof(uint32_t)) != hipSuccess) {
+      (void)hipGetLastError();
+      rd->count = nullptr;
+      return fail(HDFS_CRC32C_ENOMEM, "reader counter");
+    }
+    HIPCHK(hipMemset(rd->count, 0, sizeof(uint32_t)));
+  }
+  *out = guard.release();
+  return HDFS_CRC32C_OK;
+}
+
+int reader_next(hdfs_crc32c_reader *rd, const hdfs_crc32c_iovec *iov, int iovcnt, hdfs_crc32c_packet *pkts,
+                size_t max_pkts, size_t *npkts, uint64_t *consumed, uint64_t *delivered) {
+  DevCtx *cp = nullptr;
+  int rc;
+  if ((rc = ctx_init(rd->dev, &cp))) return rc;
+  DevCtx &c = *cp;
+  DeviceGuard g(c.dev);
+  bool any_host = false, any_dev = false;
+  uint64_t cap = 0;
+  for (int i = 0; i < iovcnt; i++) {
+    if (!iov[i].len) continue;
+    if (!iov[i].base) return fail(HDFS_CRC32C_EINVAL, "iovec %d: null base", i);
+    const int d = stream_device(iov[i].base);
+    if (d < 0) any_host = true;
+    else if (d == rd->dev) any_dev = true;
+    else return fail(HDFS_CRC32C_EINVAL, "iovec %d: memory of device %d, the stream is on %d", i, d, rd->dev);
+    cap += iov[i].len;
+  }
+  if (any_host && any_dev) return fail(HDFS_CRC32C_EINVAL, "iovecs mix host and device memory");
+  const uint64_t want = std::min(cap, rd->total - rd->done);
+  // the call's copy jobs: the next `want` bytes of the pieces, laid over the iovecs
+  Pieces mine;
+  {
+    uint64_t left = want;
+    size_t pi = rd->piece;
+    uint64_t po = rd->piece_off;
+    while (left) {
+      const uint64_t take = std::min(left, rd->pieces[pi].second - po);
+      mine.push_back({rd->pieces[pi].first + po, take});
+      left -= take;
+      po += take;
+      if (po == rd->pieces[pi].second) {
+        pi++;
+        po = 0;
+      }
+    }
+    rd->piece = pi;
+    rd->piece_off = po;
+  }
+  std::vector<CopyJob> jobs;
+  scatter_jobs(rd->s, mine, iov, iovcnt, jobs);
+  if (!jobs.empty()) {
+    std::lock_guard<std::mutex> lk(c.mu);
+    if (any_host) {
+      for (const auto &j : jobs) HIPCHK(hipMemcpyAsync(j.dst, j.src, j.len, hipMemcpyDeviceToHost, c.stream));
+      HIPCHK(hipStreamSynchronize(c.stream));
+    } else {
+      // launches of up to kCopyPiecesMax pieces of < 1 GiB (a longer job is cut)
+      size_t j = 0;
+      uint64_t jo = 0;
+      while (j < jobs.size()) {
+        CopyPieces a{};
+        uint32_t units = 0;
+        while (j < jobs.size() && a.n < kCopyPiecesMax) {
+          const uint64_t take = std::min<uint64_t>(jobs[j].len - jo, 1ull << 30);
+          a.src[a.n] = jobs[j].src + jo;
+          a.dst[a.n] = jobs[j].dst + jo;
+          a.len[a.n] = uint32_t(take);
+          const uint32_t u = copy_units(reinterpret_cast<uintptr_t>(a.dst[a.n]), take);
+          if (uint64_t(units) + u > 0xF0000000ull) break;
+          units += u;
+          a.uend[a.n++] = units;
+          jo += take;
+          if (jo == jobs[j].len) {
+            j++;
+            jo = 0;
+          }
+        }
+        if (++rd->seq == 0) ++rd->seq;
+        a.seq = rd->seq;
+        a.done = rd->ddone;
+        a.count = rd->count;
+        // one unit per thread up to kCopyBlocksMax workgroups (2 MiB), strided beyond
+        const int grid = int(std::min<uint64_t>(kCopyBlocksMax, (uint64_t(units) + 255u) / 256u));
+        HIPCHK(launch_copy_pieces(a, std::max(grid, 1), c.stream));
+        if ((rc = poll_seq(rd->hdone, a.seq, "read delivery", c.stream))) return rc;
+      }
+    }
+  }
+  rd->done += want;
+  // records completed by this call; the read's last one (and status) once all is out
+  size_t k = 0;
+  while (rd->rec_next < rd->recs.size() && rd->rec_done[rd->rec_next] <= rd->done &&
+         (rd->done == rd->total || rd->rec_next + 1 < rd->recs.size())) {
+    if (k < max_pkts) pkts[k] = rd->recs[rd->rec_next];
+    k++;
+    rd->rec_next++;
+  }
+  if (k > max_pkts) return fail(HDFS_CRC32C_EINVAL, "next: %zu records, room for %zu", k, max_pkts);
+  *npkts = k;
+  *delivered = want;
+  // consumed: the end of the last complete packet so far, the read's own at its end
+  if (rd->done == rd->total) {
+    *consumed = rd->consumed;
+    return rd->status;
+  }
+  uint64_t at = 0;
+  for (size_t q = rd->rec_next; q-- > 0;) {
+    const hdfs_crc32c_packet &r = rd->recs[q];
+    at = wire_begin(r) + uint64_t(r.crc_len > 0 ? r.crc_len : 0) + uint64_t(r.data_len > 0 ? r.data_len : 0);
+    break;
+  }
+  *consumed = at;
+  return HDFS_CRC32C_AGAIN;
+}
+
 }  // namespace
 }  // namespace hdfs_crc32c
 
@@ -2284,6 +2477,45 @@ int hdfs_crc32c_read_packets(const void *stream, uint64_t len, int proto, uint32
     if (n_all >= max_pkts && i + 1 < iovcnt) return rc;  // no room for more records: the caller resumes
   }
   return rc;
+}
+
+int hdfs_crc32c_reader_open(const void *stream, uint64_t len, int proto, uint32_t chunk_size, int ctype,
+                            int64_t client_offset, int64_t read_len, size_t max_pkts, hdfs_crc32c_reader **rd) {
+  if (!rd) return fail(HDFS_CRC32C_EINVAL, "null reader");
+  *rd = nullptr;
+  int rc = check_framing_args(proto, chunk_size, ctype, g_err, sizeof(g_err));
+  if (rc) return rc;
+  if (ctype == HDFS_CRC32C_CSUM_NULL) return fail(HDFS_CRC32C_EINVAL, "a verified read needs CRC32 or CRC32C");
+  if (!stream || !len) return fail(HDFS_CRC32C_EINVAL, "empty stream");
+  if (read_len <= 0 || client_offset < 0)
+    return fail(HDFS_CRC32C_EINVAL, "read window: offset %lld, length %lld", (long long)client_offset,
+                (long long)read_len);
+  if (!max_pkts) return fail(HDFS_CRC32C_EINVAL, "no room for records");
+  return reader_open(static_cast<const uint8_t *>(stream), len, proto, chunk_size, ctype, client_offset, read_len,
+                     max_pkts, rd);
+}
+
+int hdfs_crc32c_reader_next(hdfs_crc32c_reader *rd, const hdfs_crc32c_iovec *iov, int iovcnt, hdfs_crc32c_packet *pkts,
+                            size_t max_pkts, size_t *npkts, uint64_t *consumed, uint64_t *delivered) {
+  if (npkts) *npkts = 0;
+  if (delivered) *delivered = 0;
+  if (!rd) return fail(HDFS_CRC32C_EINVAL, "null reader");
+  if (iovcnt < 0 || (iovcnt && !iov)) return fail(HDFS_CRC32C_EINVAL, "iovecs");
+  if (max_pkts && !pkts) return fail(HDFS_CRC32C_EINVAL, "null packet array");
+  size_t n = 0;
+  uint64_t used = 0, got = 0;
+  const int rc = reader_next(rd, iov, iovcnt, pkts, max_pkts, &n, &used, &got);
+  if (rc < 0) return rc;
+  if (npkts) *npkts = n;
+  if (consumed) *consumed = used;
+  if (delivered) *delivered = got;
+  return rc;
+}
+
+void hdfs_crc32c_reader_close(hdfs_crc32c_reader *rd) {
+  if (!rd) return;
+  if (rd->hdone) (void)hipHostFree(rd->hdone);
+  delete rd;
 }
 
 int hdfs_crc32c_verify_packets_submit(const void *stream, uint64_t len, int proto, uint32_t chunk_size, int ctype,

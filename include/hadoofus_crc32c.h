@@ -73,9 +73,10 @@ uint32_t _hdfs_sw_crc32c(uint32_t crc, const void *buf, unsigned len);
  *      resumable reads); versioned exports
  *   5: hdfs_crc32c_read_packets: a client read ends at its first error (bad
  *      CRCs included), host-memory iovecs and streams; asynchronous verify
- *      jobs (hdfs_crc32c_verify_packets_submit / hdfs_crc32c_job_wait) and
+ *      jobs (hdfs_crc32c_verify_packets_submit / hdfs_crc32c_job_wait),
  *      batches of blocks (hdfs_crc32c_verify_blocks_submit /
- *      hdfs_crc32c_job_wait_blocks) */
+ *      hdfs_crc32c_job_wait_blocks), verified reads delivered piece by
+ *      piece (hdfs_crc32c_reader_*) */
 #define HDFS_CRC32C_ABI_VERSION 5
 int hdfs_crc32c_abi_version(void);
 
@@ -336,6 +337,27 @@ int hdfs_crc32c_verify_blocks_submit(const void *const *streams, const uint64_t 
     uint32_t chunk_size, int ctype, size_t max_pkts, hdfs_crc32c_job **job);
 int hdfs_crc32c_job_wait_blocks(hdfs_crc32c_job *job, hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts,
     uint64_t *consumed, int *rcs);
+
+/* A client read VERIFIED ONCE and then delivered piece by piece -- the
+ * reference's read re-entered with remains_pkt > 0 (src/datanode.c:2356-2361,
+ * 2547-2549) for a caller whose buffer is smaller than the read, without
+ * framing or verifying any packet again.  open frames and verifies the
+ * packets of the read [client_offset, client_offset + read_len) of a
+ * DEVICE-resident stream under hdfs_crc32c_read_packets' rules (the read
+ * ends at its first error; max_pkts: room for its records) and keeps their
+ * records; each next delivers the following bytes into iov (device memory
+ * of the stream's device: one copy launch; or host memory: D2H per iovec),
+ * *delivered = bytes this call, *consumed = the stream bytes of the packets
+ * delivered so far (the read's own consumed at its end), the records of the
+ * packets it completed into pkts, and returns HDFS_CRC32C_AGAIN while bytes
+ * remain, then the read's status (0, or the error that ended it, whose
+ * record comes last).  The stream must stay unchanged until close. */
+typedef struct hdfs_crc32c_reader hdfs_crc32c_reader;
+int hdfs_crc32c_reader_open(const void *stream, uint64_t len, int proto, uint32_t chunk_size, int ctype,
+    int64_t client_offset, int64_t read_len, size_t max_pkts, hdfs_crc32c_reader **rd);
+int hdfs_crc32c_reader_next(hdfs_crc32c_reader *rd, const hdfs_crc32c_iovec *iov, int iovcnt,
+    hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts, uint64_t *consumed, uint64_t *delivered);
+void hdfs_crc32c_reader_close(hdfs_crc32c_reader *rd);
 
 /* ---- write path: outgoing data packets ---------------------------------- */
 /* One outgoing data packet, as _send_packet sizes it and

@@ -1,0 +1,105 @@
+"""Verified reads delivered piece by piece (round 5): hdfs_crc32c_reader_open
+verifies the packets of a client read once; hdfs_crc32c_reader_next then
+only copies -- the reference's read re-entered with remains_pkt > 0
+(src/datanode.c:2356-2361, 2547-2549) without reading any CRC again.  The
+pieces, concatenated, equal the oracle's single read loop (oracle_read_packets:
+src/datanode.c:1476-1481, 2428-2549): the bytes, the records in order, the
+final status and consumed bytes; every call but the last fills its buffer
+and returns AGAIN; nothing is written past a buffer."""
+import numpy as np
+import pytest
+
+from packet_stream import CSUM_CRC32, CSUM_CRC32C, build_stream
+
+AGAIN = 1000
+
+
+def _dev(engine, s, shift=0):
+    buf = engine.DeviceBuffer(len(s) + shift + 64)
+    buf.fill(0)
+    buf.upload(np.frombuffer(s, np.uint8), offset=shift)
+    engine.device_sync()
+    return buf, buf.ptr + shift
+
+
+def _read_through(engine, rd, piece, total_cap, host):
+    """All of a reader's bytes through buffers of `piece` bytes (a fresh
+    buffer region each call, a 16-B guard after it)."""
+    if host:
+        arena = np.full(total_cap + 64 * 1024, 0xA5, np.uint8)
+        base = arena.ctypes.data
+    else:
+        dbuf = engine.DeviceBuffer(total_cap + 64 * 1024)
+        dbuf.fill(0xA5)
+        base = dbuf.ptr
+    at, data, recs, calls = 0, b"", [], 0
+    while True:
+        rc, pk, used, got = rd.next([(base + at, piece)])
+        calls += 1
+        recs += pk
+        if got:
+            if host:
+                data += arena[at:at + got].tobytes()
+                guard = arena[at + piece:at + piece + 16].tobytes()
+            else:
+                data += dbuf.download(got, offset=at).tobytes()
+                guard = dbuf.download(16, offset=at + piece).tobytes()
+            assert guard == b"\xa5" * 16
+        at += piece + 16
+        if rc != AGAIN:
+            break
+        assert got == piece and calls < 100000
+    if not host:
+        dbuf.free()
+    return rc, recs, used, data, calls
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("proto,ctype,sizes", [
+    (2, CSUM_CRC32C, "regular"),
+    (1, CSUM_CRC32, "regular"),
+    (2, CSUM_CRC32C, "mixed"),
+])
+def test_gpu_reader_vs_oracle(engine, oracle, proto, ctype, sizes):
+    rng = np.random.default_rng(len(sizes) + proto)
+    if sizes == "regular":
+        dl = [65536] * 120 + [12345]
+    else:
+        dl = [int(x) for x in np.repeat(rng.choice([4096, 61440, 30000, 65536], 25), rng.integers(1, 6, 25))]
+    base = 2 * 65536
+    s, _ = build_stream(oracle.crc32c, proto, 512, ctype, dl, seed=len(dl) + 3, corrupt=[(len(dl) - 6, 2)],
+                        offset0=base)
+    total = sum(dl)
+    cases = [(base + 1000, total // 3), (base + 7, total), (base + total // 2, total), (base, 1)]
+    for ci, (co, rl) in enumerate(cases):
+        want = oracle.read_packets(s, co, rl, proto, 512, ctype)
+        keep, p = _dev(engine, s, ci % 3)
+        for piece, host in ((4099, False), (65536, False), (100003, True), (1 << 20, False)):
+            rd = engine.Reader(p, len(s), co, rl, proto, 512, ctype)
+            try:
+                rc, recs, used, data, calls = _read_through(engine, rd, piece, len(want[3]) + piece * 2, host)
+            finally:
+                rd.close()
+            assert (rc, recs, used) == want[:3], (co - base, rl, piece)
+            assert data == want[3], (co - base, rl, piece)
+        keep.free()
+
+
+@pytest.mark.gpu
+def test_gpu_reader_errors_first(engine, oracle):
+    """A read whose first packet has bad CRCs delivers nothing and returns
+    the error on the first call; a read past the block's end ends with
+    BAD_LASTPACKET after its bytes; a read that starts past the stream's
+    first packet is UNEXPECTED_READ_OFFSET."""
+    dl = [65536] * 10
+    s, _ = build_stream(oracle.crc32c, 2, 512, CSUM_CRC32C, dl, seed=5, corrupt=[(0, 3)])
+    s2, _ = build_stream(oracle.crc32c, 2, 512, CSUM_CRC32C, dl, seed=6)
+    for st, co, rl in ((s, 10, 1000), (s2, 100, 11 * 65536), (s2, 3 * 65536, 100)):
+        want = oracle.read_packets(st, co, rl)
+        keep, p = _dev(engine, st)
+        rd = engine.Reader(p, len(st), co, rl)
+        rc, recs, used, data, calls = _read_through(engine, rd, 65536, len(want[3]) + 2 * 65536, False)
+        rd.close()
+        assert (rc, recs, used) == want[:3] and data == want[3]
+        assert rc != 0
+        keep.free()

@@ -165,7 +165,9 @@ def resumed_reads(ptr, n, npk, payload, reps=3):
     2547-2549): one call into one buffer; resumed call by call (AGAIN)
     through 64 KiB and 1 MiB buffers (stream + consumed, client_offset +
     delivered, read_len - delivered); one call over a 64-entry scatter list;
-    one call into pinned and into pageable host memory.  Best of reps, GiB/s
+    one call into pinned and into pageable host memory; the resumed reads
+    through a reader (hdfs_crc32c_reader_*: verified once, then copies only).
+    Best of reps, GiB/s
     of delivered payload, calls per read, and the rate as a fraction of the
     single call's."""
     arr = (h.abi.Packet * (npk + 8))()
@@ -205,6 +207,29 @@ def resumed_reads(ptr, n, npk, payload, reps=3):
     res["single_call"] = {"GiBps": round(payload / t1 / 2**30, 1), "us": round(t1 * 1e6, 1), "calls": 1}
     for name, piece in (("resumed_64KiB", 64 << 10), ("resumed_1MiB", 1 << 20)):
         t, calls = best(lambda: read(piece))
+        res[name] = {"GiBps": round(payload / t / 2**30, 2), "us": round(t * 1e6, 1), "calls": calls,
+                     "us_per_call": round(t * 1e6 / calls, 2), "frac_of_single_call": round(t1 / t, 4)}
+    # the same resumed reads through a reader: verified once at open, then copies only
+    def reader(piece):
+        rd = ctypes.c_void_p()
+        rc = lib.hdfs_crc32c_reader_open(ptr, n, h.PROTO_V2, 512, h.CSUM_CRC32C, 0, payload, npk + 8, ctypes.byref(rd))
+        assert rc == 0, rc
+        tot, calls = 0, 0
+        try:
+            while True:
+                vec = (h.abi.IoVec * 1)(h.abi.IoVec(dst.ptr + tot, min(piece, payload - tot)))
+                rc = lib.hdfs_crc32c_reader_next(rd, vec, 1, arr, npk + 8, ctypes.byref(cnt), ctypes.byref(used),
+                                                 ctypes.byref(got))
+                calls += 1
+                tot += got.value
+                if rc != h.AGAIN:
+                    assert rc == 0 and tot == payload, (rc, tot)
+                    return calls
+        finally:
+            lib.hdfs_crc32c_reader_close(rd)
+
+    for name, piece in (("reader_64KiB", 64 << 10), ("reader_1MiB", 1 << 20)):
+        t, calls = best(lambda: reader(piece))
         res[name] = {"GiBps": round(payload / t / 2**30, 2), "us": round(t * 1e6, 1), "calls": calls,
                      "us_per_call": round(t * 1e6 / calls, 2), "frac_of_single_call": round(t1 / t, 4)}
     sl = payload // 64
