@@ -132,6 +132,17 @@ struct PieceSlot {
 // the pinned landing area (SpecEarly | SpecFinal | exceptions) and the number
 // of launches so far (its parity picks the ring slot).  Asynchronous job
 // slots also own a stream and the run's bitmap / first-bad scratch.
+// Launches of copy_pieces_kernel (a reader's own, or a device context's):
+// the pinned completion word and its sequence number, the device workgroup
+// counter, and the pinned entry table of table launches (grown on demand;
+// only rewritten once the previous launch has completed).
+struct CopyCtl {
+  uint32_t *hdone = nullptr, *ddone = nullptr, *count = nullptr;
+  uint32_t seq = 0;
+  uint8_t *htab = nullptr, *dtab = nullptr;
+  size_t tab_cap = 0;
+};
+
 struct SpecSlot {
   SpecCtl *ctl = nullptr;
   SpecExc *exc = nullptr;
@@ -256,6 +267,9 @@ struct DevCtx {
   std::mutex rd_mu;
   uint8_t *rd_stage = nullptr;
   uint64_t rd_stage_cap = 0;
+  // client reads over several device iovecs: the copy kernel's completion
+  // word and table (guarded by mu)
+  CopyCtl cp;
   // opt-in resident mailbox (guarded by mu): pinned request line ([0..3]
   // seq, len, chunk_size | flags, register) and status word ([16])
   bool mb_on = false, mb_alive = false;

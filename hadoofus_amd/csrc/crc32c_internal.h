@@ -313,14 +313,24 @@ constexpr uint32_t kGridGroups = kGridMaxCount / 64 / 64;  // frame_build_kernel
 // first bad chunk, bad chunks, seq} -- seq written last.
 constexpr uint32_t kSmallRunMax = 64;
 // Delivery of an already verified client read (hdfs_crc32c_reader_next):
-// up to kCopyPiecesMax pieces (packet payload bytes at any alignment -> the
-// caller's device buffer) in one launch of copy_pieces_kernel.  A piece is
-// cut into units, the 16-B aligned blocks of its destination it touches
-// (whole ones stored as one dwordx4, its first and last byte by byte); the
-// last workgroup to finish (a device counter) publishes the call's sequence
-// number to one pinned word.
+// pieces (packet payload bytes at any alignment -> the caller's device
+// buffers) in one launch of copy_pieces_kernel.  A piece is cut into units,
+// the 16-B aligned blocks of its destination it touches (whole ones stored as
+// one dwordx4, its first and last byte by byte); the last workgroup to
+// finish (a device counter) publishes the call's sequence number to one
+// pinned word.  Up to kCopyPiecesMax pieces travel in the kernel arguments;
+// more go in a table of CopyEntry in pinned memory (the kernel reads it over
+// the bus), each workgroup taking `per` consecutive units from the entry
+// wg0[blockIdx.x] on.
 constexpr uint32_t kCopyPiecesMax = 32;
-constexpr uint32_t kCopyBlocksMax = 512;
+constexpr uint32_t kCopyBlocksMax = 512;    // kernel-argument launches
+constexpr uint32_t kCopyTabBlocks = 4096;   // table launches
+constexpr uint32_t kCopyTabStage = 64;      // table entries a workgroup stages in LDS at a time
+struct CopyEntry {
+  const uint8_t *src;
+  uint8_t *dst;
+  uint32_t len, uend;  // uend: cumulative units, as CopyPieces::uend
+};
 struct CopyPieces {
   const uint8_t *src[kCopyPiecesMax];
   uint8_t *dst[kCopyPiecesMax];
@@ -329,6 +339,9 @@ struct CopyPieces {
   uint32_t n, seq;
   uint32_t *done;                 // pinned, device address: the completion word
   uint32_t *count;                // device: workgroups finished (the last one resets it)
+  const CopyEntry *tab;           // table launches: n entries (pinned, device address), then
+  const uint32_t *wg0;            //   the first entry of each workgroup
+  uint32_t per, total;            //   units per workgroup, all units
 };
 // Units of a piece whose destination starts at d and holds len bytes.
 inline uint32_t copy_units(uintptr_t d, uint64_t len) {

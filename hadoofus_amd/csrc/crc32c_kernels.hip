@@ -3554,52 +3554,128 @@ DEV void store8_sc1(uint8_t *p, uint32_t v) {
   asm volatile("global_store_byte %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
 }
 
-__global__ __launch_bounds__(256) void copy_pieces_kernel(CopyPieces a) {
-  __shared__ const uint8_t *lsrc[kCopyPiecesMax];
-  __shared__ uintptr_t ldst[kCopyPiecesMax], lend[kCopyPiecesMax];
-  __shared__ uint32_t luend[kCopyPiecesMax + 1];
-  const uint32_t n = a.n;
-  if (threadIdx.x < n) {
-    const uint32_t t = threadIdx.x;
-    lsrc[t] = a.src[t];
-    ldst[t] = reinterpret_cast<uintptr_t>(a.dst[t]);
-    lend[t] = reinterpret_cast<uintptr_t>(a.dst[t]) + a.len[t];
-    luend[t + 1u] = a.uend[t];
-  }
-  if (threadIdx.x == 0) luend[0] = 0u;
-  __syncthreads();
-  const uint32_t total = luend[n];
-  for (uint32_t u = blockIdx.x * 256u + threadIdx.x; u < total; u += gridDim.x * 256u) {
-    uint32_t lo = 0, hi = n - 1u;
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (luend[mid + 1u] > u) hi = mid; else lo = mid + 1u;
-    }
-    const uintptr_t d = ldst[lo], e = lend[lo];
-    const uintptr_t D = (d & ~uintptr_t(15)) + 16u * uintptr_t(u - luend[lo]);
-    const uint8_t *src = lsrc[lo];
-    if (D >= d && D + 16u <= e) {
-      const uintptr_t sa = reinterpret_cast<uintptr_t>(src) + (D - d);
-      const uint32_t sh = uint32_t(sa & 3u);
-      const uint8_t *a0 = reinterpret_cast<const uint8_t *>(sa - sh);
-      uint32_t w[5];
+// One unit: the 16-B destination block at D of a piece [d, e) whose byte d
+// comes from src.
+DEV void copy_unit(const uint8_t *src, uintptr_t d, uintptr_t e, uintptr_t D) {
+  if (D >= d && D + 16u <= e) {
+    const uintptr_t sa = reinterpret_cast<uintptr_t>(src) + (D - d);
+    const uint32_t sh = uint32_t(sa & 3u);
+    const uint8_t *a0 = reinterpret_cast<const uint8_t *>(sa - sh);
+    uint32_t w[5];
 #pragma unroll
-      for (int k = 0; k < 4; k++) w[k] = gload32(a0 + 4 * k);
-      w[4] = sh ? gload32(a0 + 16) : 0u;  // only when it holds one of the bytes
-      u32x4 v;
-      v.x = align_word(w[1], w[0], sh);
-      v.y = align_word(w[2], w[1], sh);
-      v.z = align_word(w[3], w[2], sh);
-      v.w = align_word(w[4], w[3], sh);
-      store16_sc1(reinterpret_cast<uint8_t *>(D), v);
-    } else {
-      const uintptr_t x0 = D > d ? D : d, x1 = D + 16u < e ? D + 16u : e;
-      for (uintptr_t x = x0; x < x1; x++) store8_sc1(reinterpret_cast<uint8_t *>(x), gload8(src + (x - d)));
+    for (int k = 0; k < 4; k++) w[k] = gload32(a0 + 4 * k);
+    w[4] = sh ? gload32(a0 + 16) : 0u;  // only when it holds one of the bytes
+    u32x4 v;
+    v.x = align_word(w[1], w[0], sh);
+    v.y = align_word(w[2], w[1], sh);
+    v.z = align_word(w[3], w[2], sh);
+    v.w = align_word(w[4], w[3], sh);
+    store16_sc1(reinterpret_cast<uint8_t *>(D), v);
+  } else {
+    const uintptr_t x0 = D > d ? D : d, x1 = D + 16u < e ? D + 16u : e;
+    for (uintptr_t x = x0; x < x1; x++) store8_sc1(reinterpret_cast<uint8_t *>(x), gload8(src + (x - d)));
+  }
+}
+
+// Units ucur, ucur + step, ... < uend of the staged pieces 0 .. cnt - 1
+// (luend[k] = the first unit of staged piece k, luend[cnt] its end), four
+// per thread at a time: every load of the four is issued before the first
+// store, so a wave keeps 4 x 16 B per lane in flight.
+DEV uint32_t staged_piece(const uint32_t *luend, uint32_t cnt, uint32_t u) {
+  uint32_t lo = 0, hi = cnt - 1u;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (luend[mid + 1u] > u) hi = mid; else lo = mid + 1u;
+  }
+  return lo;
+}
+
+DEV void copy_staged(const uint8_t *const *lsrc, const uintptr_t *ldst, const uintptr_t *lend, const uint32_t *luend,
+                     uint32_t cnt, uint32_t ucur, uint32_t uend, uint32_t step) {
+  for (uint32_t ub = ucur; ub < uend; ub += 4u * step) {
+    uint32_t w[4][5], sh[4], pk[4], mode[4];
+    uintptr_t D[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t u = ub + uint32_t(k) * step;
+      mode[k] = 0u;
+      if (u < uend) {
+        const uint32_t p = staged_piece(luend, cnt, u);
+        const uintptr_t d = ldst[p], e = lend[p];
+        pk[k] = p;
+        D[k] = (d & ~uintptr_t(15)) + 16u * uintptr_t(u - luend[p]);
+        mode[k] = (D[k] >= d && D[k] + 16u <= e) ? 1u : 2u;
+        if (mode[k] == 1u) {
+          const uintptr_t sa = reinterpret_cast<uintptr_t>(lsrc[p]) + (D[k] - d);
+          sh[k] = uint32_t(sa & 3u);
+          const uint8_t *a0 = reinterpret_cast<const uint8_t *>(sa - sh[k]);
+#pragma unroll
+          for (int q = 0; q < 4; q++) w[k][q] = gload32(a0 + 4 * q);
+          w[k][4] = sh[k] ? gload32(a0 + 16) : 0u;  // only when it holds one of the bytes
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      if (mode[k] == 1u) {
+        u32x4 v;
+        v.x = align_word(w[k][1], w[k][0], sh[k]);
+        v.y = align_word(w[k][2], w[k][1], sh[k]);
+        v.z = align_word(w[k][3], w[k][2], sh[k]);
+        v.w = align_word(w[k][4], w[k][3], sh[k]);
+        store16_sc1(reinterpret_cast<uint8_t *>(D[k]), v);
+      } else if (mode[k] == 2u) {
+        copy_unit(lsrc[pk[k]], ldst[pk[k]], lend[pk[k]], D[k]);
+      }
+    }
+  }
+}
+
+template <bool TAB>
+__global__ __launch_bounds__(256) void copy_pieces_kernel(CopyPieces a) {
+  constexpr uint32_t kStage = TAB ? kCopyTabStage : kCopyPiecesMax;
+  __shared__ const uint8_t *lsrc[kStage];
+  __shared__ uintptr_t ldst[kStage], lend[kStage];
+  __shared__ uint32_t luend[kStage + 1];
+  const uint32_t n = a.n, tid = threadIdx.x;
+  if (!TAB) {
+    if (tid < n) {
+      lsrc[tid] = a.src[tid];
+      ldst[tid] = reinterpret_cast<uintptr_t>(a.dst[tid]);
+      lend[tid] = reinterpret_cast<uintptr_t>(a.dst[tid]) + a.len[tid];
+      luend[tid + 1u] = a.uend[tid];
+    }
+    if (tid == 0) luend[0] = 0u;
+    __syncthreads();
+    const uint32_t total = luend[n];
+    copy_staged(lsrc, ldst, lend, luend, n, blockIdx.x * 256u + tid, total, gridDim.x * 256u);
+  } else {
+    // this workgroup's units [u0, u1), from entry e on: staged kStage entries
+    // at a time (the entries are read over the bus once per workgroup)
+    const uint32_t u0 = blockIdx.x * a.per, u1 = min(a.total, u0 + a.per);
+    uint32_t e = __builtin_amdgcn_readfirstlane(a.wg0[blockIdx.x]);
+    uint32_t ucur = u0;
+    while (ucur < u1) {
+      const uint32_t cnt = min(kStage, n - e);
+      if (tid < cnt) {
+        const CopyEntry x = a.tab[e + tid];
+        lsrc[tid] = x.src;
+        ldst[tid] = reinterpret_cast<uintptr_t>(x.dst);
+        lend[tid] = reinterpret_cast<uintptr_t>(x.dst) + x.len;
+        luend[tid + 1u] = x.uend;
+      }
+      if (tid == 0) luend[0] = e ? a.tab[e - 1u].uend : 0u;
+      __syncthreads();
+      const uint32_t cend = min(u1, luend[cnt]);
+      copy_staged(lsrc, ldst, lend, luend, cnt, ucur + tid, cend, 256u);
+      ucur = cend;
+      e += cnt;
+      __syncthreads();  // the stage is rewritten
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (tid == 0) {
     const uint32_t prev = __hip_atomic_fetch_add(a.count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (prev + 1u == gridDim.x) {
       __hip_atomic_store(a.count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -3609,9 +3685,15 @@ __global__ __launch_bounds__(256) void copy_pieces_kernel(CopyPieces a) {
 }
 
 hipError_t launch_copy_pieces(const CopyPieces &a, int grid, hipStream_t stream) {
-  if (!a.n || a.n > kCopyPiecesMax || grid < 1 || grid > int(kCopyBlocksMax) || !a.done || !a.count)
-    return hipErrorInvalidValue;
-  hipLaunchKernelGGL(copy_pieces_kernel, dim3(grid), dim3(256), 0, stream, a);
+  if (!a.n || grid < 1 || !a.done || !a.count) return hipErrorInvalidValue;
+  if (a.tab) {
+    if (grid > int(kCopyTabBlocks) || !a.wg0 || !a.per || uint64_t(a.per) * uint32_t(grid) < a.total)
+      return hipErrorInvalidValue;
+    hipLaunchKernelGGL(copy_pieces_kernel<true>, dim3(grid), dim3(256), 0, stream, a);
+  } else {
+    if (a.n > kCopyPiecesMax || grid > int(kCopyBlocksMax)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(copy_pieces_kernel<false>, dim3(grid), dim3(256), 0, stream, a);
+  }
   return hipGetLastError();
 }
 

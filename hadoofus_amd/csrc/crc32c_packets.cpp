@@ -803,7 +803,9 @@ int spec_launch(DevCtx &c, SpecSlot &S, hipStream_t st, const uint8_t *d, uint64
   a.client_offset = co.client_offset;
   a.bm = bm;
   a.copy_base = co.dst ? co.dst + done_b : nullptr;
-  a.copy_cap = co.dst ? co.cap - done_b : 0u;
+  // (a client read with no copy in the pass -- a reader, a scatter read --
+  // still sizes the run by what is left of its capacity)
+  a.copy_cap = (co.dst || co.win) ? co.cap - done_b : 0u;
   a.gtab = c.d_tab_main_t[ctype == HDFS_CRC32C_CSUM_CRC32 ? 1 : 0];
   a.fb = fb;
   a.ctl = S.ctl;
@@ -1971,6 +1973,158 @@ int read_host_to_host(const uint8_t *s, uint64_t len, int proto, uint32_t cs, in
   return rc ? rc : again ? HDFS_CRC32C_AGAIN : HDFS_CRC32C_OK;
 }
 
+// ---- device-to-device delivery of verified bytes (copy_pieces_kernel) ----
+int copyctl_init(CopyCtl &k) {
+  if (k.hdone) return HDFS_CRC32C_OK;
+  if (hipHostMalloc(&k.hdone, sizeof(uint32_t), hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
+    (void)hipGetLastError();
+    k.hdone = nullptr;
+    return fail(HDFS_CRC32C_ENOMEM, "copy completion word");
+  }
+  *k.hdone = 0;
+  HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&k.ddone), k.hdone, 0));
+  if (hipMalloc(&k.count, sizeof(uint32_t)) != hipSuccess) {
+    (void)hipGetLastError();
+    k.count = nullptr;
+    (void)hipHostFree(k.hdone);
+    k.hdone = nullptr;
+    return fail(HDFS_CRC32C_ENOMEM, "copy counter");
+  }
+  HIPCHK(hipMemset(k.count, 0, sizeof(uint32_t)));
+  return HDFS_CRC32C_OK;
+}
+
+void copyctl_free(CopyCtl &k) {
+  if (k.hdone) (void)hipHostFree(k.hdone);
+  if (k.count) (void)hipFree(k.count);
+  if (k.htab) (void)hipHostFree(k.htab);
+  k = CopyCtl{};
+}
+
+// The jobs (device source -> device destination) in launches of
+// copy_pieces_kernel on st, each waited for on the completion word: up to
+// kCopyPiecesMax pieces in the kernel arguments, more through the pinned
+// table (one launch for up to 2^31 units, 32 GiB).  Caller holds the lock
+// that serialises st and k.
+int copy_jobs_dev(CopyCtl &k, hipStream_t st, const std::vector<CopyJob> &jobs_in) {
+  int rc;
+  if ((rc = copyctl_init(k))) return rc;
+  std::vector<CopyJob> jobs;  // pieces of < 1 GiB (32-bit lengths)
+  jobs.reserve(jobs_in.size());
+  for (const auto &j : jobs_in)
+    for (uint64_t o = 0; o < j.len; o += 1ull << 30) jobs.push_back({j.src + o, j.dst + o, std::min<uint64_t>(j.len - o, 1ull << 30)});
+  auto next_seq = [&]() {
+    if (++k.seq == 0) ++k.seq;
+    return k.seq;
+  };
+  size_t j = 0;
+  while (j < jobs.size()) {
+    CopyPieces a{};
+    a.done = k.ddone;
+    a.count = k.count;
+    if (jobs.size() - j <= kCopyPiecesMax) {
+      uint32_t units = 0;
+      for (; j < jobs.size(); j++) {
+        a.src[a.n] = jobs[j].src;
+        a.dst[a.n] = jobs[j].dst;
+        a.len[a.n] = uint32_t(jobs[j].len);
+        units += copy_units(reinterpret_cast<uintptr_t>(jobs[j].dst), jobs[j].len);
+        a.uend[a.n++] = units;
+      }
+      a.seq = next_seq();
+      // one unit per thread up to kCopyBlocksMax workgroups (2 MiB), strided beyond
+      const int grid = int(std::min<uint64_t>(kCopyBlocksMax, std::max<uint64_t>(1, (uint64_t(units) + 255u) / 256u)));
+      HIPCHK(launch_copy_pieces(a, grid, st));
+    } else {
+      // as many jobs as fit 2^31 units
+      size_t j1 = j;
+      uint64_t units = 0;
+      while (j1 < jobs.size()) {
+        const uint32_t u = copy_units(reinterpret_cast<uintptr_t>(jobs[j1].dst), jobs[j1].len);
+        if (units + u > (1ull << 31)) break;
+        units += u;
+        j1++;
+      }
+      const uint32_t n = uint32_t(j1 - j);
+      // workgroups of >= 1024 units (4 per thread), at most kCopyTabBlocks
+      const uint32_t grid = uint32_t(std::min<uint64_t>(kCopyTabBlocks, std::max<uint64_t>(1, (units + 1023u) / 1024u)));
+      const uint32_t per = uint32_t((units + grid - 1u) / grid);
+      const size_t wg_off = align_up(size_t(n) * sizeof(CopyEntry), size_t(256));
+      const size_t need = wg_off + size_t(grid) * sizeof(uint32_t);
+      if (need > k.tab_cap) {
+        if (k.htab) HIPCHK(hipHostFree(k.htab));
+        k.htab = k.dtab = nullptr;
+        k.tab_cap = 0;
+        const size_t want = align_up(need, size_t(1) << 16);
+        if (hipHostMalloc(&k.htab, want, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
+          (void)hipGetLastError();
+          k.htab = nullptr;
+          return fail(HDFS_CRC32C_ENOMEM, "copy table of %zu bytes", want);
+        }
+        HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&k.dtab), k.htab, 0));
+        k.tab_cap = want;
+      }
+      auto *ent = reinterpret_cast<CopyEntry *>(k.htab);
+      auto *wg0 = reinterpret_cast<uint32_t *>(k.htab + wg_off);
+      uint32_t cum = 0, b = 0;
+      for (uint32_t i = 0; i < n; i++) {
+        const CopyJob &x = jobs[j + i];
+        cum += copy_units(reinterpret_cast<uintptr_t>(x.dst), x.len);
+        ent[i] = CopyEntry{x.src, x.dst, uint32_t(x.len), cum};
+        // workgroups whose first unit lies in entry i
+        for (; b < grid && uint64_t(b) * per < cum; b++) wg0[b] = i;
+      }
+      for (; b < grid; b++) wg0[b] = n - 1u;  // (past the end: no units)
+      a.n = n;
+      a.tab = reinterpret_cast<const CopyEntry *>(k.dtab);
+      a.wg0 = reinterpret_cast<const uint32_t *>(k.dtab + wg_off);
+      a.per = per;
+      a.total = uint32_t(units);
+      a.seq = next_seq();
+      HIPCHK(launch_copy_pieces(a, int(grid), st));
+      j = j1;
+    }
+    if ((rc = poll_seq(k.hdone, a.seq, "read delivery", st))) return rc;
+  }
+  return HDFS_CRC32C_OK;
+}
+
+// Device-resident stream, several device iovecs: the read verified ONCE with
+// the whole capacity (no copy-out in the pass; its delivered byte ranges
+// kept), then all its bytes laid over the iovecs by one copy launch -- the
+// same result as one pass per buffer, each resuming where the last stopped.
+int read_dev_scatter(int dev, const uint8_t *s, uint64_t len, int proto, uint32_t cs, int ctype, int64_t client_offset,
+                     int64_t read_len, const hdfs_crc32c_iovec *iov, int iovcnt, uint64_t total,
+                     hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts, uint64_t *consumed,
+                     uint64_t *delivered) {
+  DevCtx *cp = nullptr;
+  int rc;
+  if ((rc = ctx_init(dev, &cp))) return rc;
+  DevCtx &c = *cp;
+  DeviceGuard g(c.dev);
+  CopyOut co;  // the window only: no copy in the pass
+  co.win = true;
+  co.client_offset = client_offset;
+  co.want = uint64_t(read_len);
+  co.cap = std::min<uint64_t>(total, uint64_t(read_len));
+  size_t n = 0;
+  uint64_t used = 0, got = 0;
+  Pieces pieces;
+  rc = verify_packets_dev_impl(dev, s, len, proto, cs, ctype, pkts, max_pkts, &n, &used, true, co, &got, &pieces);
+  if (rc < 0) return rc;
+  std::vector<CopyJob> jobs;
+  scatter_jobs(s, pieces, iov, iovcnt, jobs);
+  if (!jobs.empty()) {
+    std::lock_guard<std::mutex> lk(c.mu);
+    int r2 = copy_jobs_dev(c.cp, c.stream, jobs);
+    if (r2) return r2;
+  }
+  *npkts = n;
+  *consumed = used;
+  *delivered = got;
+  return rc;
+}
+
 // ---- verified reads delivered piece by piece (hdfs_crc32c_reader_*) ----
 }  // namespace
 }  // namespace hdfs_crc32c
@@ -1985,9 +2139,7 @@ struct hdfs_crc32c_reader {
   uint64_t total = 0, done = 0, consumed = 0;
   size_t piece = 0, rec_next = 0;
   uint64_t piece_off = 0;
-  uint32_t *hdone = nullptr, *ddone = nullptr;  // pinned completion word of the copy kernel
-  uint32_t *count = nullptr;                    // device: its workgroup counter
-  uint32_t seq = 0;
+  hdfs_crc32c::CopyCtl cc;               // its copy launches
 };
 
 namespace hdfs_crc32c {
@@ -2000,8 +2152,7 @@ int reader_open(const uint8_t *s, uint64_t len, int proto, uint32_t cs, int ctyp
   auto *rd = new (std::nothrow) hdfs_crc32c_reader;
   if (!rd) return fail(HDFS_CRC32C_ENOMEM, "reader");
   std::unique_ptr<hdfs_crc32c_reader, void (*)(hdfs_crc32c_reader *)> guard(rd, [](hdfs_crc32c_reader *r) {
-    if (r->hdone) (void)hipHostFree(r->hdone);
-    if (r->count) (void)hipFree(r->count);
+    copyctl_free(r->cc);
     delete r;
   });
   rd->dev = dev;
@@ -2038,19 +2189,7 @@ int reader_open(const uint8_t *s, uint64_t len, int proto, uint32_t cs, int ctyp
   }
   {
     DeviceGuard g(dev);
-    if (hipHostMalloc(&rd->hdone, sizeof(uint32_t), hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
-      (void)hipGetLastError();
-      rd->hdone = nullptr;
-      return fail(HDFS_CRC32C_ENOMEM, "reader completion word");
-    }
-    *rd->hdone = 0;
-    HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&rd->ddone), rd->hdone, 0));
-    if (hipMalloc(&rd->count, sizeof(uint32_t)) != hipSuccess) {
-      (void)hipGetLastError();
-      rd->count = nullptr;
-      return fail(HDFS_CRC32C_ENOMEM, "reader counter");
-    }
-    HIPCHK(hipMemset(rd->count, 0, sizeof(uint32_t)));
+    if ((rc = copyctl_init(rd->cc))) return rc;
   }
   *out = guard.release();
   return HDFS_CRC32C_OK;
@@ -2103,36 +2242,7 @@ int reader_next(hdfs_crc32c_reader *rd, const hdfs_crc32c_iovec *iov, int iovcnt
       for (const auto &j : jobs) HIPCHK(hipMemcpyAsync(j.dst, j.src, j.len, hipMemcpyDeviceToHost, c.stream));
       HIPCHK(hipStreamSynchronize(c.stream));
     } else {
-      // launches of up to kCopyPiecesMax pieces of < 1 GiB (a longer job is cut)
-      size_t j = 0;
-      uint64_t jo = 0;
-      while (j < jobs.size()) {
-        CopyPieces a{};
-        uint32_t units = 0;
-        while (j < jobs.size() && a.n < kCopyPiecesMax) {
-          const uint64_t take = std::min<uint64_t>(jobs[j].len - jo, 1ull << 30);
-          a.src[a.n] = jobs[j].src + jo;
-          a.dst[a.n] = jobs[j].dst + jo;
-          a.len[a.n] = uint32_t(take);
-          const uint32_t u = copy_units(reinterpret_cast<uintptr_t>(a.dst[a.n]), take);
-          if (uint64_t(units) + u > 0xF0000000ull) break;
-          units += u;
-          a.uend[a.n++] = units;
-          jo += take;
-          if (jo == jobs[j].len) {
-            j++;
-            jo = 0;
-          }
-        }
-        if (++rd->seq == 0) ++rd->seq;
-        a.seq = rd->seq;
-        a.done = rd->ddone;
-        a.count = rd->count;
-        // one unit per thread up to kCopyBlocksMax workgroups (2 MiB), strided beyond
-        const int grid = int(std::min<uint64_t>(kCopyBlocksMax, (uint64_t(units) + 255u) / 256u));
-        HIPCHK(launch_copy_pieces(a, std::max(grid, 1), c.stream));
-        if ((rc = poll_seq(rd->hdone, a.seq, "read delivery", c.stream))) return rc;
-      }
+      if ((rc = copy_jobs_dev(rd->cc, c.stream, jobs))) return rc;
     }
   }
   rd->done += want;
@@ -2414,6 +2524,7 @@ int hdfs_crc32c_read_packets(const void *stream, uint64_t len, int proto, uint32
   // de-framing copy), or all host memory
   bool any_host = false, any_dev = false;
   uint64_t total = 0;
+  int nbuf = 0;
   for (int i = 0; i < iovcnt; i++) {
     if (!iov[i].len) continue;
     if (!iov[i].base) return fail(HDFS_CRC32C_EINVAL, "iovec %d: null base", i);
@@ -2422,6 +2533,7 @@ int hdfs_crc32c_read_packets(const void *stream, uint64_t len, int proto, uint32
     else if (d == dev) any_dev = true;
     else return fail(HDFS_CRC32C_EINVAL, "iovec %d: memory of device %d, the stream is on %d", i, d, dev);
     total += iov[i].len;
+    nbuf++;
   }
   if (any_host && any_dev) return fail(HDFS_CRC32C_EINVAL, "iovecs mix host and device memory");
   if (!total) return HDFS_CRC32C_OK;
@@ -2439,7 +2551,19 @@ int hdfs_crc32c_read_packets(const void *stream, uint64_t len, int proto, uint32
     if (delivered) *delivered = got;
     return rc;
   }
-  // One pass per buffer: each delivers into its buffer and stops with AGAIN
+  if (nbuf > 1) {  // (a client read: READ_ALL takes one buffer)
+    size_t n = 0;
+    uint64_t used = 0, got = 0;
+    rc = read_dev_scatter(dev, static_cast<const uint8_t *>(stream), len, proto, chunk_size, ctype, client_offset,
+                          read_len, iov, iovcnt, total, pkts, max_pkts, &n, &used, &got);
+    if (rc < 0) return rc;
+    if (npkts) *npkts = n;
+    if (consumed) *consumed = used;
+    if (delivered) *delivered = got;
+    return rc;
+  }
+  // One buffer: the fused verify + copy-out.  (Kept general: one pass per
+  // buffer, each delivers into its buffer and stops with AGAIN
   // when the buffer is full, and the next resumes where the read stands
   // (the stream from the packet it stopped in, the client offset advanced
   // by what was delivered) -- the reference's re-entry with remains_pkt > 0.
@@ -2514,7 +2638,7 @@ int hdfs_crc32c_reader_next(hdfs_crc32c_reader *rd, const hdfs_crc32c_iovec *iov
 
 void hdfs_crc32c_reader_close(hdfs_crc32c_reader *rd) {
   if (!rd) return;
-  if (rd->hdone) (void)hipHostFree(rd->hdone);
+  copyctl_free(rd->cc);
   delete rd;
 }
 

@@ -74,7 +74,8 @@ def test_gpu_reader_vs_oracle(engine, oracle, proto, ctype, sizes):
     for ci, (co, rl) in enumerate(cases):
         want = oracle.read_packets(s, co, rl, proto, 512, ctype)
         keep, p = _dev(engine, s, ci % 3)
-        for piece, host in ((4099, False), (65536, False), (100003, True), (1 << 20, False)):
+        # (3 MiB + 5: more pieces than one launch's arguments take -- the table launch)
+        for piece, host in ((4099, False), (65536, False), (100003, True), (1 << 20, False), ((3 << 20) + 5, False)):
             rd = engine.Reader(p, len(s), co, rl, proto, 512, ctype)
             try:
                 rc, recs, used, data, calls = _read_through(engine, rd, piece, len(want[3]) + piece * 2, host)
@@ -103,3 +104,43 @@ def test_gpu_reader_errors_first(engine, oracle):
         assert (rc, recs, used) == want[:3] and data == want[3]
         assert rc != 0
         keep.free()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nbuf,lo,hi", [(2000, 1, 300), (300, 1000, 40000), (40, 1, 17)])
+def test_gpu_scatter_many_buffers(engine, oracle, nbuf, lo, hi):
+    """One hdfs_crc32c_read_packets call over many device buffers (the
+    reference's iovec array, src/datanode.c:2509-2537): the read is verified
+    once and its bytes laid over the buffers by one copy launch -- from a
+    table of thousands of pieces (tiny buffers: a workgroup stages several
+    rounds of entries), or from the launch's own arguments.  Bytes, records,
+    consumed and status equal the oracle's single read; a 16-B guard after
+    every buffer is untouched."""
+    rng = np.random.default_rng(nbuf + lo)
+    dl = [65536] * 40 + [777]
+    s, _ = build_stream(oracle.crc32c, 2, 512, CSUM_CRC32C, dl, seed=nbuf, corrupt=[(30, 2)])
+    keep, p = _dev(engine, s, 1)
+    sizes = [int(x) for x in rng.integers(lo, hi + 1, nbuf)]
+    iov, off = [], 0
+    for n in sizes:
+        iov.append((off, n))
+        off += n + 16 + int(rng.integers(0, 16))
+    cap = sum(sizes)
+    for co in (0, 5 * 65536 + 333):
+        rl = min(cap + 5000, sum(dl) - co)  # more than the buffers hold: AGAIN
+        want = oracle.read_packets(s, co, rl, cap=cap)
+        big = engine.DeviceBuffer(off + 64)
+        big.fill(0xA5)
+        rc, recs, used, got = engine.read_packets(p, len(s), None, 0, client_offset=co, read_len=rl,
+                                                  iov=[(big.ptr + a, n) for a, n in iov])
+        assert (rc, recs, used) == want[:3], (nbuf, co)
+        flat = big.download(off).tobytes()
+        data, left = b"", got
+        for a, n in iov:
+            take = min(n, left)
+            data += flat[a:a + take]
+            left -= take
+            assert flat[a + n:a + n + 16] == b"\xa5" * 16
+        assert data == want[3], (nbuf, co)
+        big.free()
+    keep.free()
