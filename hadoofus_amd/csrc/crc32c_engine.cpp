@@ -86,6 +86,14 @@ uint32_t g_xcd_major = uint32_t(HDFS_KNOB("HDFS_CRC32C_XCD", 1)) & 3u;
 // launch keeps the last 8 % of its tiles in the global pool (schedule 3's
 // two-phase split; the plan kernels use 32).
 uint32_t g_spec_pool_min = uint32_t(HDFS_KNOB("HDFS_CRC32C_SPEC_POOL", 32)) & 255u;
+// Table launches of copy_pieces_kernel: fewest units per workgroup, and
+// whether the piece table is copied to device memory first (1) or read
+// over the bus from pinned memory (0).
+uint32_t g_copy_wg_units = uint32_t(HDFS_KNOB("HDFS_CRC32C_COPY_WG_UNITS", 1024));
+int g_copy_dev_tab = HDFS_KNOB("HDFS_CRC32C_COPY_DEV_TAB", 1);
+// (r05 reader_sizes: the resident block copies ~16 GB/s; 64 KiB 7.4 us per
+// delivery against 10.5 launched, 256 KiB 19 against 10.6)
+uint64_t g_mb_copy_max = uint64_t(HDFS_KNOB("HDFS_CRC32C_MB_COPY_MAX", 96 << 10));
 // Compute-mode CRC stores: 2 (product) schedule 3 with the LDS group gather
 // (one 256-B store per 8-tile group); diagnostic build only: 1 schedule 4
 // on tables of whole groups, 0 one 32-B store per tile
@@ -455,6 +463,8 @@ void mb_post(DevCtx &c, uint32_t seq, uint32_t len, uint32_t csf, uint32_t reg0,
 
 bool mb_exited(const DevCtx &c) { return __atomic_load_n(&c.h_mb[16], __ATOMIC_ACQUIRE) == (c.mb_epoch << 1); }
 
+int mb_wait(DevCtx &c, uint32_t seq, std::chrono::steady_clock::time_point t0);
+
 int mailbox_call(DevCtx &c, int mode, uint32_t len, uint32_t cs, uint32_t reg0, bool be, int ctype,
                  const uint8_t *dsrc, const uint8_t *hsrc, const uint8_t *hcrc, uint32_t crc_bytes) {
   const uint32_t seq = ++c.small_seq;
@@ -476,22 +486,47 @@ int mailbox_call(DevCtx &c, int mode, uint32_t len, uint32_t cs, uint32_t reg0, 
                        (ctype ? kMbCrc32Flag : 0u) | (dsrc ? kMbDevFlag : 0u);
   mb_post(c, seq, len, csf, reg0, dsrc);
   const auto t0 = std::chrono::steady_clock::now();
+  const int rc = mb_wait(c, seq, t0);
+  if (rc) return rc;
+  if (g_small_trace) {  // diagnostic: host staging / wait, kernel phases (diag build, 10 ns ticks)
+    const auto t1 = std::chrono::steady_clock::now();
+    const uint32_t *m = c.h_small_out;
+    std::fprintf(stderr, "mailbox len=%u cs=%u stage_us=%.2f wait_us=%.2f load_us=%.2f comp_us=%.2f\n", len, cs,
+                 std::chrono::duration<double, std::micro>(t0 - ta).count(),
+                 std::chrono::duration<double, std::micro>(t1 - t0).count(), (m[5] - m[4]) / 100.0,
+                 (m[6] - m[5]) / 100.0);
+  }
+  // a single chunk's CRC came with the completion word (one store)
+  if (mode != kModeVerify && len <= cs) c.h_small_out[kSmallMeta] = c.h_small_out[3];
+  return HDFS_CRC32C_OK;
+}
+
+// A reader's delivery through the open mailbox: n <= kCopyPiecesMax pieces
+// staged at the start of the input stage, one request line, the completion
+// line awaited as for a small call.  Caller holds c.mu and has checked
+// c.mb_on.
+int mailbox_copy(DevCtx &c, const CopyEntry *e, uint32_t n) {
+  if (!n || n > kCopyPiecesMax) return fail(HDFS_CRC32C_EINVAL, "mailbox copy of %u pieces", n);
+  const uint32_t seq = ++c.small_seq;
+  if (c.mb_alive && mb_exited(c)) c.mb_alive = false;
+  if (!c.mb_alive) {
+    const int rc = mb_launch(c, c.mb_posted);
+    if (rc) return rc;
+  }
+  std::memcpy(c.h_small_in, e, size_t(n) * sizeof(CopyEntry));
+  mb_post(c, seq, n, kMbCopyFlag, 0u, nullptr);
+  return mb_wait(c, seq, std::chrono::steady_clock::now());
+}
+
+// Waits for request seq's completion line; relaunches a mailbox that idled
+// out before it saw the request.
+int mb_wait(DevCtx &c, uint32_t seq, std::chrono::steady_clock::time_point t0) {
   for (uint32_t spin = 1;; spin++) {
     if (__atomic_load_n(&c.h_small_out[2], __ATOMIC_ACQUIRE) == seq) {
       // the completion line is the resident kernel's last memory operation
       // for a request; a fault while serving it ends the kernel before it
       // (caught by the stream query below after 200 ms)
       c.mb_calls++;
-      if (g_small_trace) {  // diagnostic: host staging / wait, kernel phases (diag build, 10 ns ticks)
-        const auto t1 = std::chrono::steady_clock::now();
-        const uint32_t *m = c.h_small_out;
-        std::fprintf(stderr, "mailbox len=%u cs=%u stage_us=%.2f wait_us=%.2f load_us=%.2f comp_us=%.2f\n", len, cs,
-                     std::chrono::duration<double, std::micro>(t0 - ta).count(),
-                     std::chrono::duration<double, std::micro>(t1 - t0).count(), (m[5] - m[4]) / 100.0,
-                     (m[6] - m[5]) / 100.0);
-      }
-      // a single chunk's CRC came with the completion word (one store)
-      if (mode != kModeVerify && len <= cs) c.h_small_out[kSmallMeta] = c.h_small_out[3];
       return HDFS_CRC32C_OK;
     }
     if ((spin & 255u) == 0 && mb_exited(c)) {

@@ -141,6 +141,8 @@ struct CopyCtl {
   uint32_t seq = 0;
   uint8_t *htab = nullptr, *dtab = nullptr;
   size_t tab_cap = 0;
+  uint8_t *vtab = nullptr;  // device-memory copy of the table (g_copy_dev_tab)
+  size_t vtab_cap = 0;
 };
 
 struct SpecSlot {
@@ -270,6 +272,9 @@ struct DevCtx {
   // client reads over several device iovecs: the copy kernel's completion
   // word and table (guarded by mu)
   CopyCtl cp;
+  // readers' copy state, kept for the next reader (a free would synchronise
+  // the device, which waits for an open mailbox to idle out)
+  std::vector<CopyCtl> cp_pool;
   // opt-in resident mailbox (guarded by mu): pinned request line ([0..3]
   // seq, len, chunk_size | flags, register) and status word ([16])
   bool mb_on = false, mb_alive = false;
@@ -287,8 +292,13 @@ struct DevCtx {
   // not serialise with the NULL stream, so device_sync with a mailbox open
   // synchronises each of them)
   std::vector<hipStream_t> user_streams;
-  // CUs the bulk (one-workgroup-per-CU) kernels may use
-  int bulk_cus() const { return num_cu - (mb_on ? 1 : 0); }
+  // Workgroups of the bulk (one-workgroup-per-CU) kernels.  With the mailbox
+  // resident, one CU per XCD is left out, not one in all: workgroups are dealt
+  // to the XCDs round-robin, so a grid of num_cu - 1 still gives the
+  // mailbox's XCD one workgroup per CU, and the one that lands after the
+  // others waits for the mailbox to idle out (round 5: a reader's open
+  // stalled by the idle limit on every read).  32 CUs per XCD on gfx950.
+  int bulk_cus() const { return num_cu - (mb_on ? std::max(1, num_cu / 32) : 0); }
   std::mutex mu;
 };
 
@@ -340,10 +350,20 @@ uint32_t tile_tune();
 // spec_verify_kernel: rounds per wave from which the global pool is used
 // (tune bits 23:16 of the tiled kernel; 0 there means 32)
 extern uint32_t g_spec_pool_min;
+// copy_pieces_kernel table launches: fewest units per workgroup; piece table
+// in device memory (1) or read from pinned memory (0)
+extern uint32_t g_copy_wg_units;
+extern int g_copy_dev_tab;
 // Any segment whose data is not 4-B aligned (selects the realigning kernel).
 bool any_unaligned(const SegDev *segs, size_t n);
 // Copy / compute streams, events and the small pipeline buffers.
 int pipe_reserve(DevCtx &c, size_t piece, uint32_t cs, size_t npieces);
+// A reader's delivery of n <= kCopyPiecesMax pieces through the open mailbox
+// (caller holds c.mu, c.mb_on).
+int mailbox_copy(DevCtx &c, const CopyEntry *e, uint32_t n);
+// Deliveries up to this many bytes go to the open mailbox (one CU copies;
+// larger ones launch copy_pieces_kernel).
+extern uint64_t g_mb_copy_max;
 
 // One-launch path for synchronous calls on <= kSmallMax bytes
 // (small_chunks_kernel or the open mailbox; caller holds c.mu and has staged

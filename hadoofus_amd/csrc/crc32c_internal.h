@@ -319,18 +319,20 @@ constexpr uint32_t kSmallRunMax = 64;
 // one dwordx4, its first and last byte by byte); the last workgroup to
 // finish (a device counter) publishes the call's sequence number to one
 // pinned word.  Up to kCopyPiecesMax pieces travel in the kernel arguments;
-// more go in a table of CopyEntry in pinned memory (the kernel reads it over
-// the bus), each workgroup taking `per` consecutive units from the entry
-// wg0[blockIdx.x] on.
+// more go in a table of CopyEntry, written in pinned memory and copied to
+// device memory ahead of the launch on the same stream, each workgroup
+// taking `per` consecutive units from the entry wg0[blockIdx.x] on.
 constexpr uint32_t kCopyPiecesMax = 32;
 constexpr uint32_t kCopyBlocksMax = 512;    // kernel-argument launches
-constexpr uint32_t kCopyTabBlocks = 4096;   // table launches
+constexpr uint32_t kCopyTabBlocks = 4096;   // table launches: the kernel's limit
+constexpr uint32_t kCopyTabGrid = 1024;     //   and the host's choice
 constexpr uint32_t kCopyTabStage = 64;      // table entries a workgroup stages in LDS at a time
 struct CopyEntry {
   const uint8_t *src;
   uint8_t *dst;
   uint32_t len, uend;  // uend: cumulative units, as CopyPieces::uend
 };
+static_assert(sizeof(CopyEntry) == 24, "CopyEntry layout (the mailbox reads it as 6 words)");
 struct CopyPieces {
   const uint8_t *src[kCopyPiecesMax];
   uint8_t *dst[kCopyPiecesMax];
@@ -342,7 +344,9 @@ struct CopyPieces {
   const CopyEntry *tab;           // table launches: n entries (pinned, device address), then
   const uint32_t *wg0;            //   the first entry of each workgroup
   uint32_t per, total;            //   units per workgroup, all units
+  unsigned long long *stamps;     // diagnostic build: [kCopyStampOff + 4 * block + phase]
 };
+constexpr size_t kCopyStampOff = 110592;
 // Units of a piece whose destination starts at d and holds len bytes.
 inline uint32_t copy_units(uintptr_t d, uint64_t len) {
   return len ? uint32_t(((d + len + 15u) & ~uintptr_t(15)) - (d & ~uintptr_t(15))) / 16u : 0u;
@@ -360,6 +364,9 @@ constexpr uint32_t kSmallMaxChunks = 2048;
 constexpr uint32_t kMbVerifyFlag = 1u << 24, kMbBeFlag = 1u << 25, kMbCrc32Flag = 1u << 26, kMbQuitFlag = 1u << 27;
 // device-memory source: its 64-bit address is the word pair after the line
 constexpr uint32_t kMbDevFlag = 1u << 28;
+// a reader's delivery (hdfs_crc32c_reader_next): word 1 = n <= kCopyPiecesMax
+// CopyEntry records staged at the start of the input stage
+constexpr uint32_t kMbCopyFlag = 1u << 29;
 
 
 constexpr uint32_t kRoundBytes = 512;  // sub-chunk handled by 8 lanes per round

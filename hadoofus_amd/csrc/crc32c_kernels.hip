@@ -1672,7 +1672,7 @@ __global__ __launch_bounds__(1024) void small_chunks_kernel(const uint8_t *__res
                                                              uint32_t *__restrict__ crcs, uint32_t seq) {
   __shared__ uint32_t tt[1024];                             // t0..t3
   __shared__ uint32_t dat[kSmallMax / 4 + kSmallMax / 64];  // one pad word per 16
-  __shared__ uint32_t acc[kSmallMaxChunks];
+  __shared__ __attribute__((aligned(16))) uint32_t acc[kSmallMaxChunks];  // (a copy request: its staged pieces)
   __shared__ uint32_t res[2];
   const uint32_t tid = threadIdx.x;
   // piece size: 16, 32 or 64 B, the smallest that keeps the pieces within
@@ -1817,6 +1817,125 @@ __global__ __launch_bounds__(1024) void small_chunks_kernel(const uint8_t *__res
   }
 }
 
+// Funnel shift: bytes [sh, sh + 4) of the 8-B value hi:lo.
+DEV uint32_t align_word(uint32_t hi, uint32_t lo, uint32_t sh) {
+  return __builtin_amdgcn_alignbyte(hi, lo, sh);
+}
+
+// Copy of a verified read's next bytes.  Thread u of the grid (strided when
+// the call has more units than threads) takes unit u: the 16-B aligned
+// destination block D of piece i = the first with uend[i] > u (the piece
+// table is staged in LDS).  A whole unit reads the dword-aligned window
+// around its 16 source bytes and funnel-shifts it into place (packet payloads
+// sit at any byte offset of the wire stream), one dwordx4 store; the piece's
+// first and last unit go byte by byte.  Consecutive lanes take consecutive
+// units: loads and stores coalesce.  Stores are sc1 (written through the
+// XCD's L2 to memory, so no L2 write-back is needed for another XCD or a
+// later kernel to read them); every wave waits for its stores, and after the
+// workgroup barrier one lane counts the workgroup done (agent atomic); the
+// last one resets the counter and publishes the sequence number to the host
+// (one pinned word: no stream synchronisation).
+DEV void store16_sc1(uint8_t *p, u32x4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+DEV void store8_sc1(uint8_t *p, uint32_t v) {
+  asm volatile("global_store_byte %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+
+// One unit: the 16-B destination block at D of a piece [d, e) whose byte d
+// comes from src.
+DEV void copy_unit(const uint8_t *src, uintptr_t d, uintptr_t e, uintptr_t D) {
+  if (D >= d && D + 16u <= e) {
+    const uintptr_t sa = reinterpret_cast<uintptr_t>(src) + (D - d);
+    const uint32_t sh = uint32_t(sa & 3u);
+    const uint8_t *a0 = reinterpret_cast<const uint8_t *>(sa - sh);
+    uint32_t w[5];
+#pragma unroll
+    for (int k = 0; k < 4; k++) w[k] = gload32(a0 + 4 * k);
+    w[4] = sh ? gload32(a0 + 16) : 0u;  // only when it holds one of the bytes
+    u32x4 v;
+    v.x = align_word(w[1], w[0], sh);
+    v.y = align_word(w[2], w[1], sh);
+    v.z = align_word(w[3], w[2], sh);
+    v.w = align_word(w[4], w[3], sh);
+    store16_sc1(reinterpret_cast<uint8_t *>(D), v);
+  } else {
+    const uintptr_t x0 = D > d ? D : d, x1 = D + 16u < e ? D + 16u : e;
+    for (uintptr_t x = x0; x < x1; x++) store8_sc1(reinterpret_cast<uint8_t *>(x), gload8(src + (x - d)));
+  }
+}
+
+// The staged piece (0 .. cnt - 1) that holds unit u: luend[k] = the first
+// unit of staged piece k, luend[cnt] the end of the last.
+DEV uint32_t staged_piece(const uint32_t *luend, uint32_t cnt, uint32_t u) {
+  uint32_t lo = 0, hi = cnt - 1u;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (luend[mid + 1u] > u) hi = mid; else lo = mid + 1u;
+  }
+  return lo;
+}
+
+// A unit's loads (the issue half) and its store (the other half).
+struct CopyLd {
+  uint32_t w[5], sh, pk, mode;  // mode 0: none, 1: whole 16 B, 2: byte by byte at the store
+  uintptr_t D;
+};
+
+DEV void copy_issue(CopyLd &x, const uint8_t *const *lsrc, const uintptr_t *ldst, const uintptr_t *lend,
+                    const uint32_t *luend, uint32_t cnt, uint32_t u, uint32_t uend) {
+  x.mode = 0u;
+  if (u >= uend) return;
+  const uint32_t p = staged_piece(luend, cnt, u);
+  const uintptr_t d = ldst[p], e = lend[p];
+  x.pk = p;
+  x.D = (d & ~uintptr_t(15)) + 16u * uintptr_t(u - luend[p]);
+  x.mode = (x.D >= d && x.D + 16u <= e) ? 1u : 2u;
+  if (x.mode == 1u) {
+    const uintptr_t sa = reinterpret_cast<uintptr_t>(lsrc[p]) + (x.D - d);
+    x.sh = uint32_t(sa & 3u);
+    const uint8_t *a0 = reinterpret_cast<const uint8_t *>(sa - x.sh);
+#pragma unroll
+    for (int q = 0; q < 4; q++) x.w[q] = gload32(a0 + 4 * q);
+    x.w[4] = x.sh ? gload32(a0 + 16) : 0u;  // only when it holds one of the bytes
+  }
+}
+
+DEV void copy_finish(const CopyLd &x, const uint8_t *const *lsrc, const uintptr_t *ldst, const uintptr_t *lend) {
+  if (x.mode == 1u) {
+    u32x4 v;
+    v.x = align_word(x.w[1], x.w[0], x.sh);
+    v.y = align_word(x.w[2], x.w[1], x.sh);
+    v.z = align_word(x.w[3], x.w[2], x.sh);
+    v.w = align_word(x.w[4], x.w[3], x.sh);
+    store16_sc1(reinterpret_cast<uint8_t *>(x.D), v);
+  } else if (x.mode == 2u) {
+    copy_unit(lsrc[x.pk], ldst[x.pk], lend[x.pk], x.D);
+  }
+}
+
+// Units ucur, ucur + step, ... < uend of the staged pieces, U per thread at
+// a time and software-pipelined: the next U units' loads are issued before
+// this U's stores, so a lane has up to 2U x 16 B in flight and the loads
+// never wait behind the write-through stores' acknowledgements (one in-order
+// counter covers both on gfx950).
+template <int U = 4>
+DEV void copy_staged(const uint8_t *const *lsrc, const uintptr_t *ldst, const uintptr_t *lend, const uint32_t *luend,
+                     uint32_t cnt, uint32_t ucur, uint32_t uend, uint32_t step) {
+  CopyLd cur[U], nxt[U];
+#pragma unroll
+  for (int k = 0; k < U; k++) copy_issue(cur[k], lsrc, ldst, lend, luend, cnt, ucur + uint32_t(k) * step, uend);
+  for (uint32_t ub = ucur; ub < uend; ub += uint32_t(U) * step) {
+#pragma unroll
+    for (int k = 0; k < U; k++)
+      copy_issue(nxt[k], lsrc, ldst, lend, luend, cnt, ub + uint32_t(U + k) * step, uend);
+#pragma unroll
+    for (int k = 0; k < U; k++) copy_finish(cur[k], lsrc, ldst, lend);
+#pragma unroll
+    for (int k = 0; k < U; k++) cur[k] = nxt[k];
+  }
+}
+
 // Resident "mailbox" variant of small_chunks_kernel (opt-in,
 // hdfs_crc32c_mailbox_create): ONE workgroup stays on one CU and serves the
 // synchronous small calls (_hdfs_crc32c and aliases, verify_crcdata,
@@ -1866,6 +1985,33 @@ DEV void fill_ztree(uint32_t *zt, const uint32_t *__restrict__ gtab, uint32_t ti
   for (uint32_t s = 0; s < 3; s++) zt[s * 1024u + tid] = gtab[kTabSliceWords + ((1u << s) - 1u) * 1024u + tid];
 }
 
+// A copy request served by the mailbox: n CopyEntry records at the start of
+// the input stage (read system-coherent: the host wrote them just before the
+// request line) staged in LDS, then every unit by the block's 1 024 threads,
+// write-through stores as copy_pieces_kernel's; returns once every wave's
+// stores are acknowledged.
+DEV void mb_copy(const __amdgpu_buffer_rsrc_t rin, uint32_t n, uint32_t *lds, uint32_t tid) {
+  auto *lsrc = reinterpret_cast<const uint8_t **>(lds);
+  auto *ldst = reinterpret_cast<uintptr_t *>(lds + 2u * kCopyPiecesMax);
+  auto *lend = reinterpret_cast<uintptr_t *>(lds + 4u * kCopyPiecesMax);
+  uint32_t *luend = lds + 6u * kCopyPiecesMax;
+  if (tid < n) {
+    uint32_t w[6];
+#pragma unroll
+    for (uint32_t q = 0; q < 6; q++) w[q] = __builtin_amdgcn_raw_buffer_load_b32(rin, 24u * tid + 4u * q, 0, 17);
+    const uintptr_t src = (uintptr_t(w[1]) << 32) | w[0], dst = (uintptr_t(w[3]) << 32) | w[2];
+    lsrc[tid] = reinterpret_cast<const uint8_t *>(src);
+    ldst[tid] = dst;
+    lend[tid] = dst + w[4];
+    luend[tid + 1u] = w[5];
+  }
+  if (tid == 0) luend[0] = 0u;
+  __syncthreads();
+  copy_staged<2>(lsrc, ldst, lend, luend, n, tid, luend[n], 1024u);  // (the CRC path's registers: no spills)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
 __global__ __launch_bounds__(1024) void mailbox_kernel(const uint32_t *__restrict__ req, const uint8_t *__restrict__ in,
                                                        uint32_t *__restrict__ meta, uint32_t *__restrict__ crcs,
                                                        const uint32_t *__restrict__ tab0, const uint32_t *__restrict__ tab1,
@@ -1881,7 +2027,7 @@ __global__ __launch_bounds__(1024) void mailbox_kernel(const uint32_t *__restric
   __shared__ uint32_t kx[2 * kTabKxWords];
   __shared__ uint32_t zt[3 * 1024];                 // Z_64, Z_128, Z_256 of the current type
   __shared__ uint32_t slot[2 * (kSmallMax / 512)];  // tree mode: 512-B group partials {crc, j | m << 16}
-  __shared__ uint32_t acc[kSmallMaxChunks];
+  __shared__ __attribute__((aligned(16))) uint32_t acc[kSmallMaxChunks];  // (a copy request: its staged pieces)
   __shared__ uint32_t res[2];
   __shared__ uint32_t ctl[6];
   __shared__ uint32_t tailacc;
@@ -1936,6 +2082,14 @@ __global__ __launch_bounds__(1024) void mailbox_kernel(const uint32_t *__restric
     const uint32_t seq = rfl(ctl[0]), len = rfl(ctl[1]), csf = rfl(ctl[2]), reg0 = rfl(ctl[3]);
     const bool dev = (csf & kMbDevFlag) != 0u;
     if (csf & kMbQuitFlag) break;  // uniform: every wave leaves here
+    if (csf & kMbCopyFlag) {       // uniform: a reader's delivery, len = pieces
+      mb_copy(rin, len, acc, tid);
+      if (tid == 0) *(volatile GAS u32x4 *)(GAS uint8_t *)meta = u32x4{0xFFFFFFFFu, 0u, seq, 0u};
+      last = seq;
+      t_idle = __builtin_amdgcn_s_memrealtime();
+      __syncthreads();  // the stage in acc is rewritten by the next request
+      continue;
+    }
     const uint32_t cs = csf & 0x1FFFFu, ct = (csf & kMbCrc32Flag) ? 1u : 0u;
     const bool verify = (csf & kMbVerifyFlag) != 0u, be = (csf & kMbBeFlag) != 0u;
     const uint32_t nch = (len + cs - 1u) / cs;
@@ -2242,9 +2396,6 @@ __global__ __launch_bounds__(256) void corrupt_kernel(uint8_t *__restrict__ data
 // so each lane reads the dword-aligned window around its 16 output bytes and
 // funnel-shifts it into place (v_alignbyte_b32); stores are 16-B aligned.
 // The slice also moves its share of the packet's BE CRC words.
-DEV uint32_t align_word(uint32_t hi, uint32_t lo, uint32_t sh) {
-  return __builtin_amdgcn_alignbyte(hi, lo, sh);
-}
 
 __global__ __launch_bounds__(256) void packet_gather_kernel(const uint8_t *__restrict__ raw,
                                                              const PktDesc *__restrict__ descs, uint32_t npk,
@@ -3534,103 +3685,6 @@ __global__ __launch_bounds__(1024) void small_run_kernel(const uint8_t *__restri
   }
 }
 
-// Copy of a verified read's next bytes.  Thread u of the grid (strided when
-// the call has more units than threads) takes unit u: the 16-B aligned
-// destination block D of piece i = the first with uend[i] > u (the piece
-// table is staged in LDS).  A whole unit reads the dword-aligned window
-// around its 16 source bytes and funnel-shifts it into place (packet payloads
-// sit at any byte offset of the wire stream), one dwordx4 store; the piece's
-// first and last unit go byte by byte.  Consecutive lanes take consecutive
-// units: loads and stores coalesce.  Stores are sc1 (written through the
-// XCD's L2 to memory, so no L2 write-back is needed for another XCD or a
-// later kernel to read them); every wave waits for its stores, and after the
-// workgroup barrier one lane counts the workgroup done (agent atomic); the
-// last one resets the counter and publishes the sequence number to the host
-// (one pinned word: no stream synchronisation).
-DEV void store16_sc1(uint8_t *p, u32x4 v) {
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
-}
-DEV void store8_sc1(uint8_t *p, uint32_t v) {
-  asm volatile("global_store_byte %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
-}
-
-// One unit: the 16-B destination block at D of a piece [d, e) whose byte d
-// comes from src.
-DEV void copy_unit(const uint8_t *src, uintptr_t d, uintptr_t e, uintptr_t D) {
-  if (D >= d && D + 16u <= e) {
-    const uintptr_t sa = reinterpret_cast<uintptr_t>(src) + (D - d);
-    const uint32_t sh = uint32_t(sa & 3u);
-    const uint8_t *a0 = reinterpret_cast<const uint8_t *>(sa - sh);
-    uint32_t w[5];
-#pragma unroll
-    for (int k = 0; k < 4; k++) w[k] = gload32(a0 + 4 * k);
-    w[4] = sh ? gload32(a0 + 16) : 0u;  // only when it holds one of the bytes
-    u32x4 v;
-    v.x = align_word(w[1], w[0], sh);
-    v.y = align_word(w[2], w[1], sh);
-    v.z = align_word(w[3], w[2], sh);
-    v.w = align_word(w[4], w[3], sh);
-    store16_sc1(reinterpret_cast<uint8_t *>(D), v);
-  } else {
-    const uintptr_t x0 = D > d ? D : d, x1 = D + 16u < e ? D + 16u : e;
-    for (uintptr_t x = x0; x < x1; x++) store8_sc1(reinterpret_cast<uint8_t *>(x), gload8(src + (x - d)));
-  }
-}
-
-// Units ucur, ucur + step, ... < uend of the staged pieces 0 .. cnt - 1
-// (luend[k] = the first unit of staged piece k, luend[cnt] its end), four
-// per thread at a time: every load of the four is issued before the first
-// store, so a wave keeps 4 x 16 B per lane in flight.
-DEV uint32_t staged_piece(const uint32_t *luend, uint32_t cnt, uint32_t u) {
-  uint32_t lo = 0, hi = cnt - 1u;
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (luend[mid + 1u] > u) hi = mid; else lo = mid + 1u;
-  }
-  return lo;
-}
-
-DEV void copy_staged(const uint8_t *const *lsrc, const uintptr_t *ldst, const uintptr_t *lend, const uint32_t *luend,
-                     uint32_t cnt, uint32_t ucur, uint32_t uend, uint32_t step) {
-  for (uint32_t ub = ucur; ub < uend; ub += 4u * step) {
-    uint32_t w[4][5], sh[4], pk[4], mode[4];
-    uintptr_t D[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const uint32_t u = ub + uint32_t(k) * step;
-      mode[k] = 0u;
-      if (u < uend) {
-        const uint32_t p = staged_piece(luend, cnt, u);
-        const uintptr_t d = ldst[p], e = lend[p];
-        pk[k] = p;
-        D[k] = (d & ~uintptr_t(15)) + 16u * uintptr_t(u - luend[p]);
-        mode[k] = (D[k] >= d && D[k] + 16u <= e) ? 1u : 2u;
-        if (mode[k] == 1u) {
-          const uintptr_t sa = reinterpret_cast<uintptr_t>(lsrc[p]) + (D[k] - d);
-          sh[k] = uint32_t(sa & 3u);
-          const uint8_t *a0 = reinterpret_cast<const uint8_t *>(sa - sh[k]);
-#pragma unroll
-          for (int q = 0; q < 4; q++) w[k][q] = gload32(a0 + 4 * q);
-          w[k][4] = sh[k] ? gload32(a0 + 16) : 0u;  // only when it holds one of the bytes
-        }
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      if (mode[k] == 1u) {
-        u32x4 v;
-        v.x = align_word(w[k][1], w[k][0], sh[k]);
-        v.y = align_word(w[k][2], w[k][1], sh[k]);
-        v.z = align_word(w[k][3], w[k][2], sh[k]);
-        v.w = align_word(w[k][4], w[k][3], sh[k]);
-        store16_sc1(reinterpret_cast<uint8_t *>(D[k]), v);
-      } else if (mode[k] == 2u) {
-        copy_unit(lsrc[pk[k]], ldst[pk[k]], lend[pk[k]], D[k]);
-      }
-    }
-  }
-}
-
 template <bool TAB>
 __global__ __launch_bounds__(256) void copy_pieces_kernel(CopyPieces a) {
   constexpr uint32_t kStage = TAB ? kCopyTabStage : kCopyPiecesMax;
@@ -3638,6 +3692,13 @@ __global__ __launch_bounds__(256) void copy_pieces_kernel(CopyPieces a) {
   __shared__ uintptr_t ldst[kStage], lend[kStage];
   __shared__ uint32_t luend[kStage + 1];
   const uint32_t n = a.n, tid = threadIdx.x;
+  // diagnostic phase stamps (100 MHz): 0 entry, 1 first entries staged, 2
+  // stores acknowledged, 3 counted done
+  unsigned long long *const ps = kDiag && a.stamps ? a.stamps + kCopyStampOff + 4u * blockIdx.x : nullptr;
+  auto stamp = [&](uint32_t ph) {
+    if (kDiag && ps && tid == 0) ps[ph] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
   if (!TAB) {
     if (tid < n) {
       lsrc[tid] = a.src[tid];
@@ -3651,7 +3712,7 @@ __global__ __launch_bounds__(256) void copy_pieces_kernel(CopyPieces a) {
     copy_staged(lsrc, ldst, lend, luend, n, blockIdx.x * 256u + tid, total, gridDim.x * 256u);
   } else {
     // this workgroup's units [u0, u1), from entry e on: staged kStage entries
-    // at a time (the entries are read over the bus once per workgroup)
+    // at a time (each entry is read by the workgroups it spans)
     const uint32_t u0 = blockIdx.x * a.per, u1 = min(a.total, u0 + a.per);
     uint32_t e = __builtin_amdgcn_readfirstlane(a.wg0[blockIdx.x]);
     uint32_t ucur = u0;
@@ -3666,6 +3727,7 @@ __global__ __launch_bounds__(256) void copy_pieces_kernel(CopyPieces a) {
       }
       if (tid == 0) luend[0] = e ? a.tab[e - 1u].uend : 0u;
       __syncthreads();
+      if (ucur == u0) stamp(1);
       const uint32_t cend = min(u1, luend[cnt]);
       copy_staged(lsrc, ldst, lend, luend, cnt, ucur + tid, cend, 256u);
       ucur = cend;
@@ -3675,6 +3737,7 @@ __global__ __launch_bounds__(256) void copy_pieces_kernel(CopyPieces a) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  stamp(2);
   if (tid == 0) {
     const uint32_t prev = __hip_atomic_fetch_add(a.count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (prev + 1u == gridDim.x) {
@@ -3682,6 +3745,7 @@ __global__ __launch_bounds__(256) void copy_pieces_kernel(CopyPieces a) {
       __hip_atomic_store(a.done, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
+  stamp(3);
 }
 
 hipError_t launch_copy_pieces(const CopyPieces &a, int grid, hipStream_t stream) {

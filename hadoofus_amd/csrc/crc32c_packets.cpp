@@ -1994,10 +1994,27 @@ int copyctl_init(CopyCtl &k) {
   return HDFS_CRC32C_OK;
 }
 
+// A reader's copy state from the device's pool (caller holds c.mu), and back.
+CopyCtl copyctl_take(DevCtx &c) {
+  if (c.cp_pool.empty()) return CopyCtl{};
+  CopyCtl k = c.cp_pool.back();
+  c.cp_pool.pop_back();
+  return k;
+}
+
+void copyctl_give(int dev, CopyCtl &k) {
+  DevCtx *cp = nullptr;
+  if (!k.hdone || ctx_init(dev, &cp)) return;
+  std::lock_guard<std::mutex> lk(cp->mu);
+  cp->cp_pool.push_back(k);
+  k = CopyCtl{};
+}
+
 void copyctl_free(CopyCtl &k) {
   if (k.hdone) (void)hipHostFree(k.hdone);
   if (k.count) (void)hipFree(k.count);
   if (k.htab) (void)hipHostFree(k.htab);
+  if (k.vtab) (void)hipFree(k.vtab);
   k = CopyCtl{};
 }
 
@@ -2006,8 +2023,22 @@ void copyctl_free(CopyCtl &k) {
 // kCopyPiecesMax pieces in the kernel arguments, more through the pinned
 // table (one launch for up to 2^31 units, 32 GiB).  Caller holds the lock
 // that serialises st and k.
-int copy_jobs_dev(CopyCtl &k, hipStream_t st, const std::vector<CopyJob> &jobs_in) {
+int copy_jobs_dev(CopyCtl &k, hipStream_t st, const std::vector<CopyJob> &jobs_in, DevCtx *mb = nullptr) {
   int rc;
+  if (mb && mb->mb_on && !jobs_in.empty() && jobs_in.size() <= kCopyPiecesMax) {
+    // a small delivery with the latency mode open: the resident kernel copies
+    uint64_t bytes = 0;
+    for (const auto &j : jobs_in) bytes += j.len;
+    if (bytes <= g_mb_copy_max) {
+      CopyEntry e[kCopyPiecesMax];
+      uint32_t units = 0, n = 0;
+      for (const auto &j : jobs_in) {
+        units += copy_units(reinterpret_cast<uintptr_t>(j.dst), j.len);
+        e[n++] = CopyEntry{j.src, j.dst, uint32_t(j.len), units};
+      }
+      return mailbox_copy(*mb, e, n);
+    }
+  }
   if ((rc = copyctl_init(k))) return rc;
   std::vector<CopyJob> jobs;  // pieces of < 1 GiB (32-bit lengths)
   jobs.reserve(jobs_in.size());
@@ -2020,6 +2051,7 @@ int copy_jobs_dev(CopyCtl &k, hipStream_t st, const std::vector<CopyJob> &jobs_i
   size_t j = 0;
   while (j < jobs.size()) {
     CopyPieces a{};
+    a.stamps = kDiag ? g_diag : nullptr;
     a.done = k.ddone;
     a.count = k.count;
     if (jobs.size() - j <= kCopyPiecesMax) {
@@ -2046,8 +2078,12 @@ int copy_jobs_dev(CopyCtl &k, hipStream_t st, const std::vector<CopyJob> &jobs_i
         j1++;
       }
       const uint32_t n = uint32_t(j1 - j);
-      // workgroups of >= 1024 units (4 per thread), at most kCopyTabBlocks
-      const uint32_t grid = uint32_t(std::min<uint64_t>(kCopyTabBlocks, std::max<uint64_t>(1, (units + 1023u) / 1024u)));
+      // workgroups of >= g_copy_wg_units units (1024), at most 1024 of them
+      // (about what is resident at once: a workgroup stages its first
+      // entries once, then streams; r05 copy_sweep: 1 024 workgroups of 8 192
+      // units 53 us for 128 MiB, 4 096 of 2 048 units 67 us)
+      const uint64_t wgu = std::max<uint32_t>(256u, g_copy_wg_units);
+      const uint32_t grid = uint32_t(std::min<uint64_t>(kCopyTabGrid, std::max<uint64_t>(1, (units + wgu - 1u) / wgu)));
       const uint32_t per = uint32_t((units + grid - 1u) / grid);
       const size_t wg_off = align_up(size_t(n) * sizeof(CopyEntry), size_t(256));
       const size_t need = wg_off + size_t(grid) * sizeof(uint32_t);
@@ -2076,8 +2112,24 @@ int copy_jobs_dev(CopyCtl &k, hipStream_t st, const std::vector<CopyJob> &jobs_i
       }
       for (; b < grid; b++) wg0[b] = n - 1u;  // (past the end: no units)
       a.n = n;
-      a.tab = reinterpret_cast<const CopyEntry *>(k.dtab);
-      a.wg0 = reinterpret_cast<const uint32_t *>(k.dtab + wg_off);
+      const uint8_t *tab = k.dtab;
+      if (g_copy_dev_tab) {
+        if (need > k.vtab_cap) {
+          if (k.vtab) HIPCHK(hipFree(k.vtab));
+          k.vtab = nullptr;
+          k.vtab_cap = 0;
+          if (hipMalloc(&k.vtab, k.tab_cap) != hipSuccess) {
+            (void)hipGetLastError();
+            k.vtab = nullptr;
+            return fail(HDFS_CRC32C_ENOMEM, "copy table");
+          }
+          k.vtab_cap = k.tab_cap;
+        }
+        HIPCHK(hipMemcpyAsync(k.vtab, k.htab, need, hipMemcpyHostToDevice, st));
+        tab = k.vtab;
+      }
+      a.tab = reinterpret_cast<const CopyEntry *>(tab);
+      a.wg0 = reinterpret_cast<const uint32_t *>(tab + wg_off);
       a.per = per;
       a.total = uint32_t(units);
       a.seq = next_seq();
@@ -2116,7 +2168,7 @@ int read_dev_scatter(int dev, const uint8_t *s, uint64_t len, int proto, uint32_
   scatter_jobs(s, pieces, iov, iovcnt, jobs);
   if (!jobs.empty()) {
     std::lock_guard<std::mutex> lk(c.mu);
-    int r2 = copy_jobs_dev(c.cp, c.stream, jobs);
+    int r2 = copy_jobs_dev(c.cp, c.stream, jobs, &c);
     if (r2) return r2;
   }
   *npkts = n;
@@ -2152,7 +2204,7 @@ int reader_open(const uint8_t *s, uint64_t len, int proto, uint32_t cs, int ctyp
   auto *rd = new (std::nothrow) hdfs_crc32c_reader;
   if (!rd) return fail(HDFS_CRC32C_ENOMEM, "reader");
   std::unique_ptr<hdfs_crc32c_reader, void (*)(hdfs_crc32c_reader *)> guard(rd, [](hdfs_crc32c_reader *r) {
-    copyctl_free(r->cc);
+    copyctl_give(r->dev, r->cc);
     delete r;
   });
   rd->dev = dev;
@@ -2189,6 +2241,12 @@ int reader_open(const uint8_t *s, uint64_t len, int proto, uint32_t cs, int ctyp
   }
   {
     DeviceGuard g(dev);
+    {
+      DevCtx *cp = nullptr;
+      if ((rc = ctx_init(dev, &cp))) return rc;
+      std::lock_guard<std::mutex> lk(cp->mu);
+      rd->cc = copyctl_take(*cp);
+    }
     if ((rc = copyctl_init(rd->cc))) return rc;
   }
   *out = guard.release();
@@ -2242,7 +2300,7 @@ int reader_next(hdfs_crc32c_reader *rd, const hdfs_crc32c_iovec *iov, int iovcnt
       for (const auto &j : jobs) HIPCHK(hipMemcpyAsync(j.dst, j.src, j.len, hipMemcpyDeviceToHost, c.stream));
       HIPCHK(hipStreamSynchronize(c.stream));
     } else {
-      if ((rc = copy_jobs_dev(rd->cc, c.stream, jobs))) return rc;
+      if ((rc = copy_jobs_dev(rd->cc, c.stream, jobs, &c))) return rc;
     }
   }
   rd->done += want;
@@ -2638,7 +2696,7 @@ int hdfs_crc32c_reader_next(hdfs_crc32c_reader *rd, const hdfs_crc32c_iovec *iov
 
 void hdfs_crc32c_reader_close(hdfs_crc32c_reader *rd) {
   if (!rd) return;
-  copyctl_free(rd->cc);
+  copyctl_give(rd->dev, rd->cc);  // (kept for the next reader: no device synchronisation here)
   delete rd;
 }
 

@@ -276,7 +276,8 @@ int hdfs_crc32c_verify_packets(const void *stream, uint64_t len, int proto, uint
  *   not returned.  *delivered = the bytes the reference copies to the
  *   caller before its loop returns (a BAD_LASTPACKET packet's own bytes
  *   included).  Records, *consumed, *delivered and the status do not depend
- *   on how the destination is split.
+ *   on how the destination is split.  (Several device buffers: the read is
+ *   verified once and its bytes laid over them by one copy launch.)
  *   A destination smaller than the rest of the read is RESUMABLE, as the
  *   reference's read is (`rlen == 0 && remains_tot > 0` -> HDFS_AGAIN,
  *   :2547-2549, re-entered with remains_pkt > 0, :2356-2361): once the

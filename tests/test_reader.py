@@ -144,3 +144,57 @@ def test_gpu_scatter_many_buffers(engine, oracle, nbuf, lo, hi):
         assert data == want[3], (nbuf, co)
         big.free()
     keep.free()
+
+
+@pytest.mark.gpu
+def test_gpu_reader_through_mailbox(engine, oracle):
+    """With the latency mode open (hdfs_crc32c_mailbox_create) a delivery of
+    <= 32 pieces and <= 96 KiB is copied by the resident kernel instead of a
+    launch: the same bytes, records and status as the oracle's read, guard
+    bytes untouched; larger deliveries keep the launch; a small scatter read
+    goes the same way; an idled-out mailbox is relaunched by the next call."""
+    dl = [65536] * 60 + [4321]
+    s, _ = build_stream(oracle.crc32c, 2, 512, CSUM_CRC32C, dl, seed=44, corrupt=[(50, 3)])
+    keep, p = _dev(engine, s, 2)
+    co, rl = 1234, sum(dl) - 2000
+    want = oracle.read_packets(s, co, rl)
+    with engine.Mailbox(idle_ms=50) as mb:
+        for piece in (4099, 65536, 98304, (1 << 20) + 17, (3 << 20) + 5):
+            c0 = mb.stats()[0]
+            rd = engine.Reader(p, len(s), co, rl)
+            try:
+                rc, recs, used, data, calls = _read_through(engine, rd, piece, len(want[3]) + piece * 2, False)
+            finally:
+                rd.close()
+            assert (rc, recs, used) == want[:3], piece
+            assert data == want[3], piece
+            served = mb.stats()[0] - c0
+            if piece <= 98304:
+                assert served >= calls - 1, (piece, served, calls)
+            else:  # full deliveries launch; only the short last one may be served
+                assert served <= 1, (piece, served)
+        # a small scatter read: three buffers, one delivery through the mailbox
+        c0 = mb.stats()[0]
+        big = engine.DeviceBuffer(300000)
+        big.fill(0xA5)
+        iov = [(0, 40000), (40016, 1000), (41032, 50000)]
+        w2 = oracle.read_packets(s, co, rl, cap=91000)
+        r2 = engine.read_packets(p, len(s), None, 0, client_offset=co, read_len=rl,
+                                 iov=[(big.ptr + a, n) for a, n in iov])
+        assert r2[:3] == w2[:3]
+        flat = big.download(300000).tobytes()
+        assert flat[0:40000] + flat[40016:41016] + flat[41032:91032] == w2[3]
+        for a, n in iov:
+            assert flat[a + n:a + n + 16] == b"\xa5" * 16
+        assert mb.stats()[0] - c0 == 1
+        big.free()
+        # idle out, then a reader call relaunches the resident kernel
+        import time
+        time.sleep(0.2)
+        l0 = mb.stats()[1]
+        rd = engine.Reader(p, len(s), co, rl)
+        rc, recs, used, data, calls = _read_through(engine, rd, 65536, len(want[3]) + 2 * 65536, False)
+        rd.close()
+        assert (rc, recs, used) == want[:3] and data == want[3]
+        assert mb.stats()[1] > l0
+    keep.free()

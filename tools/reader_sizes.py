@@ -1,8 +1,10 @@
 """Per-call cost of hdfs_crc32c_reader_next by piece size (GPU box): a
 128 MiB block of 64 KiB packets in device memory, one reader per pass, the
-whole read delivered in pieces of 16 KiB .. 8 MiB into a device buffer;
-and the same read in ONE hdfs_crc32c_read_packets call over 64 buffers.
-Prints one JSON line {piece: {"us_per_call", "GiBps", "calls"}}; run it under
+whole read delivered in pieces of 16 KiB .. 8 MiB into a device buffer, by
+launches and with the mailbox (latency mode) open; and the same read in ONE
+hdfs_crc32c_read_packets call over 64 buffers.  Prints one JSON line
+{"launch"|"mailbox": {piece: {"us_per_call", "GiBps", "calls"}}, "scatter_64"};
+run it under
 rocprofv3 --kernel-trace --stats to split the call into copy_pieces_kernel
 time and the rest.
 
@@ -32,6 +34,30 @@ def main():
     arr = (h.abi.Packet * (npk + 8))()
     cnt, used, got = ctypes.c_size_t(0), ctypes.c_uint64(0), ctypes.c_uint64(0)
     out = {}
+    out["launch"] = sweep(lib, d, img, npk, payload, dst, arr, cnt, used, got)
+    with h.Mailbox():  # the latency mode: deliveries <= 1 MiB copied by the resident kernel
+        out["mailbox"] = sweep(lib, d, img, npk, payload, dst, arr, cnt, used, got)
+    # one call over 64 device buffers (the verify once + one table copy launch)
+    sl = payload // 64
+    vec = (h.abi.IoVec * 64)(*[h.abi.IoVec(dst.ptr + k * sl, sl) for k in range(64)])
+    best = 1e9
+    for rep in range(6):
+        t0 = time.perf_counter()
+        rc = lib.hdfs_crc32c_read_packets(d.ptr, img.nbytes, h.PROTO_V2, 512, h.CSUM_CRC32C, 0, payload, vec, 64, arr,
+                                          npk + 8, ctypes.byref(cnt), ctypes.byref(used), ctypes.byref(got))
+        t = time.perf_counter() - t0
+        assert rc == 0 and got.value == payload, (rc, got.value)
+        if rep:
+            best = min(best, t)
+    out["scatter_64"] = {"us": round(best * 1e6, 1), "GiBps": round(payload / best / 2**30, 2)}
+    js = json.dumps(out)
+    print(js)
+    if len(sys.argv) > 1:
+        open(sys.argv[1], "w").write(js + "\n")
+
+
+def sweep(lib, d, img, npk, payload, dst, arr, cnt, used, got):
+    out = {}
     for piece in (16 << 10, 64 << 10, 256 << 10, 1 << 20, 4 << 20, 8 << 20):
         best = 1e9
         for rep in range(4):
@@ -55,23 +81,7 @@ def main():
                 best = min(best, t)
         out[piece] = {"us_per_call": round(best * 1e6 / calls, 2), "GiBps": round(payload / best / 2**30, 2),
                       "calls": calls}
-    # one call over 64 device buffers (the verify once + one table copy launch)
-    sl = payload // 64
-    vec = (h.abi.IoVec * 64)(*[h.abi.IoVec(dst.ptr + k * sl, sl) for k in range(64)])
-    best = 1e9
-    for rep in range(6):
-        t0 = time.perf_counter()
-        rc = lib.hdfs_crc32c_read_packets(d.ptr, img.nbytes, h.PROTO_V2, 512, h.CSUM_CRC32C, 0, payload, vec, 64, arr,
-                                          npk + 8, ctypes.byref(cnt), ctypes.byref(used), ctypes.byref(got))
-        t = time.perf_counter() - t0
-        assert rc == 0 and got.value == payload, (rc, got.value)
-        if rep:
-            best = min(best, t)
-    out["scatter_64"] = {"us": round(best * 1e6, 1), "GiBps": round(payload / best / 2**30, 2)}
-    js = json.dumps(out)
-    print(js)
-    if len(sys.argv) > 1:
-        open(sys.argv[1], "w").write(js + "\n")
+    return out
 
 
 if __name__ == "__main__":

@@ -99,9 +99,10 @@ def measure(nbytes, reps=6):
     return {"payload_bytes": nbytes, "packets": npk, "wire_bytes": int(img.nbytes), "runs": runs}
 
 
-out = {"block_128MiB": measure(128 << 20), "run_1GiB": measure(1 << 30)}
-js = json.dumps(out)
-print(js)
-if len(sys.argv) > 1:
-    with open(sys.argv[1], "w") as fh:
-        fh.write(js + "\n")
+if __name__ == "__main__":
+    out = {"block_128MiB": measure(128 << 20), "run_1GiB": measure(1 << 30)}
+    js = json.dumps(out)
+    print(js)
+    if len(sys.argv) > 1:
+        with open(sys.argv[1], "w") as fh:
+            fh.write(js + "\n")
