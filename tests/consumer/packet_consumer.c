@@ -330,6 +330,32 @@ int main(void)
 			check(brc[b] == HDFS_CRC32C_ERR_DATANODE_BAD_CHECKSUM && bn[b] == NPK + 1 && bused[b] == total &&
 			    brec[b * (NPK + 1) + 7].first_bad == 3 && brec[b * (NPK + 1) + NPK].last, "blocks wait records");
 		free(brec);
+		/* (8) the clean client read once more through a reader (ABI 5):
+		 * verified once at open, then delivered piece by piece into host
+		 * memory, each piece ending inside a packet (src/datanode.c:2547-2549) */
+		{
+			hdfs_crc32c_reader *rdr = NULL;
+			check(hdfs_crc32c_reader_open((uint8_t *)blk[0] + 8 * pk, total - 8 * pk, HDFS_CRC32C_PROTO_V2, CS,
+			    HDFS_CRC32C_CSUM_CRC32C, 8 * (int64_t)DLEN + 5, 2 * (int64_t)DLEN, NPK + 1, &rdr) == 0, "reader open");
+			const uint64_t piece = DLEN / 2 + 3;
+			uint64_t got_tot = 0;
+			size_t nrec = 0;
+			int calls = 0;
+			memset(u1, 0, 2 * DLEN);
+			do {
+				const uint64_t left = 2 * DLEN - got_tot;
+				hdfs_crc32c_iovec iv = {u1 + got_tot, left < piece ? left : piece};
+				rc = hdfs_crc32c_reader_next(rdr, &iv, 1, rec + nrec, NPK + 1 - nrec, &n, &used, &delivered);
+				nrec += n;
+				got_tot += delivered;
+				calls++;
+			} while (rc == HDFS_CRC32C_AGAIN && calls < 16);
+			hdfs_crc32c_reader_close(rdr);
+			check(rc == 0 && got_tot == 2 * DLEN && nrec == 3 && used == 3 * pk && calls == 4, "reader: pieces");
+			check(memcmp(u1, s + 8 * pk + 31 + crclen + 5, DLEN - 5) == 0 &&
+			    memcmp(u1 + DLEN - 5, s + 9 * pk + 31 + crclen, DLEN) == 0 &&
+			    memcmp(u1 + 2 * DLEN - 5, s + 10 * pk + 31 + crclen, 5) == 0, "reader: bytes");
+		}
 		for (int b = 0; b < 3; b++)
 			hdfs_crc32c_dev_free(blk[b]);
 		free(u0);
