@@ -1853,6 +1853,22 @@ void run_host_jobs(const std::vector<CopyJob> &jobs) {
   for (auto &x : th) x.join();
 }
 
+// The device staging area of reads into host memory, at least cap bytes
+// (caller holds c.rd_mu).
+int rd_stage_reserve(DevCtx &c, uint64_t cap) {
+  if (cap <= c.rd_stage_cap) return HDFS_CRC32C_OK;
+  if (c.rd_stage) HIPCHK(hipFree(c.rd_stage));
+  c.rd_stage = nullptr;
+  c.rd_stage_cap = 0;
+  const uint64_t want = align_up(cap, uint64_t(1) << 20);
+  if (hipMalloc(&c.rd_stage, want) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(HDFS_CRC32C_ENOMEM, "read staging of %llu bytes", (unsigned long long)want);
+  }
+  c.rd_stage_cap = want;
+  return HDFS_CRC32C_OK;
+}
+
 // Device-resident stream, host destination: the fused verify + copy-out into
 // a device staging area (one pass, the whole capacity), then D2H per iovec.
 int read_dev_to_host(int dev, const uint8_t *s, uint64_t len, int proto, uint32_t cs, int ctype, int64_t client_offset,
@@ -1867,17 +1883,7 @@ int read_dev_to_host(int dev, const uint8_t *s, uint64_t len, int proto, uint32_
   std::lock_guard<std::mutex> lk(c.rd_mu);
   const bool win = read_len != HDFS_CRC32C_READ_ALL;
   const uint64_t cap = win ? std::min<uint64_t>(total, uint64_t(read_len)) : total;
-  if (cap > c.rd_stage_cap) {
-    if (c.rd_stage) HIPCHK(hipFree(c.rd_stage));
-    c.rd_stage = nullptr;
-    c.rd_stage_cap = 0;
-    const uint64_t want = align_up(cap, uint64_t(1) << 20);
-    if (hipMalloc(&c.rd_stage, want) != hipSuccess) {
-      (void)hipGetLastError();
-      return fail(HDFS_CRC32C_ENOMEM, "read staging of %llu bytes", (unsigned long long)want);
-    }
-    c.rd_stage_cap = want;
-  }
+  if ((rc = rd_stage_reserve(c, cap))) return rc;
   CopyOut co;
   co.dst = c.rd_stage;
   co.cap = cap;
@@ -2294,7 +2300,20 @@ int reader_next(hdfs_crc32c_reader *rd, const hdfs_crc32c_iovec *iov, int iovcnt
   }
   std::vector<CopyJob> jobs;
   scatter_jobs(rd->s, mine, iov, iovcnt, jobs);
-  if (!jobs.empty()) {
+  if (!jobs.empty() && any_host && mine.size() > 2) {
+    // many pieces into host memory: gathered contiguous in the device
+    // staging area by one copy, then one D2H per iovec (not one per piece)
+    std::lock_guard<std::mutex> lk0(c.rd_mu);
+    if ((rc = rd_stage_reserve(c, want))) return rc;
+    std::lock_guard<std::mutex> lk(c.mu);
+    std::vector<CopyJob> gather;
+    const hdfs_crc32c_iovec sv{c.rd_stage, want};
+    scatter_jobs(rd->s, mine, &sv, 1, gather);
+    if ((rc = copy_jobs_dev(rd->cc, c.stream, gather, &c))) return rc;
+    scatter_jobs(c.rd_stage, Pieces{{0, want}}, iov, iovcnt, jobs);
+    for (const auto &j : jobs) HIPCHK(hipMemcpyAsync(j.dst, j.src, j.len, hipMemcpyDeviceToHost, c.stream));
+    HIPCHK(hipStreamSynchronize(c.stream));
+  } else if (!jobs.empty()) {
     std::lock_guard<std::mutex> lk(c.mu);
     if (any_host) {
       for (const auto &j : jobs) HIPCHK(hipMemcpyAsync(j.dst, j.src, j.len, hipMemcpyDeviceToHost, c.stream));

@@ -75,7 +75,9 @@ def test_gpu_reader_vs_oracle(engine, oracle, proto, ctype, sizes):
         want = oracle.read_packets(s, co, rl, proto, 512, ctype)
         keep, p = _dev(engine, s, ci % 3)
         # (3 MiB + 5: more pieces than one launch's arguments take -- the table launch)
-        for piece, host in ((4099, False), (65536, False), (100003, True), (1 << 20, False), ((3 << 20) + 5, False)):
+        # (host 1 MiB + 7: many pieces gathered through the device staging area, one D2H)
+        for piece, host in ((4099, False), (65536, False), (100003, True), (1 << 20, False), ((3 << 20) + 5, False),
+                            ((1 << 20) + 7, True)):
             rd = engine.Reader(p, len(s), co, rl, proto, 512, ctype)
             try:
                 rc, recs, used, data, calls = _read_through(engine, rd, piece, len(want[3]) + piece * 2, host)
