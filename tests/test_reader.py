@@ -200,3 +200,28 @@ def test_gpu_reader_through_mailbox(engine, oracle):
         assert (rc, recs, used) == want[:3] and data == want[3]
         assert mb.stats()[1] > l0
     keep.free()
+
+
+@pytest.mark.gpu
+def test_gpu_reader_records_or_stream_run_out(engine, oracle):
+    """A read the reader cannot complete -- its record array (max_pkts) or
+    the stream ends first -- delivers what the oracle's read loop delivers
+    (src/datanode.c:1476-1481 stops at the same packet) and ends with the same
+    status, records and consumed bytes: the caller resumes at stream +
+    consumed with client_offset + delivered."""
+    dl = [65536] * 30 + [5000]
+    s, _ = build_stream(oracle.crc32c, 2, 512, CSUM_CRC32C, dl, seed=91)
+    whole = oracle.verify_packets(s)[1]
+    cut = s[:whole[20]["stream_off"] + 1000]  # ends inside packet 20
+    for st, mp in ((s, 7), (cut, None), (cut, 3)):
+        co, rl = 777, sum(dl) - 1000
+        want = oracle.read_packets(st, co, rl, max_pkts=mp) if mp else oracle.read_packets(st, co, rl)
+        keep, p = _dev(engine, st)
+        rd = engine.Reader(p, len(st), co, rl, max_pkts=mp)
+        try:
+            rc, recs, used, data, calls = _read_through(engine, rd, 65536, len(want[3]) + 2 * 65536, False)
+        finally:
+            rd.close()
+        assert (rc, recs, used) == want[:3], mp
+        assert data == want[3], mp
+        keep.free()
