@@ -1909,6 +1909,33 @@ int read_dev_to_host(int dev, const uint8_t *s, uint64_t len, int proto, uint32_
   return rc;
 }
 
+// A client read of a host-resident stream, planned: the window is a function
+// of the headers (which packets the read takes), so the stream is framed on
+// the host, only the packets the window walk looked at are verified on the
+// GPU (hdfs_crc32c_verify_packets' host pipeline), and the window applied
+// to their verdicts -> records, delivered byte ranges, consumed, delivered,
+// again.  Returns a negative status or 0.
+int host_window_plan(const uint8_t *s, uint64_t len, int proto, uint32_t cs, int ctype, const CopyOut &co,
+                     size_t max_pkts, std::vector<hdfs_crc32c_packet> &recs, Pieces &pieces, uint64_t *used,
+                     uint64_t *got, int *again) {
+  int rc;
+  *used = 0;
+  if ((rc = parse_packet_stream(s, len, proto, cs, ctype, max_pkts, recs, used, g_err, sizeof(g_err)))) return rc;
+  size_t nh = recs.size(), seen = 0;
+  uint64_t ch = *used;
+  (void)apply_read_window(recs.data(), nh, ch, co, nullptr, nullptr, &seen);
+  // verified: up to the start of the first packet the walk did not look at
+  const uint64_t vlen = seen < recs.size() ? recs[seen].stream_off : len;
+  recs.assign(seen, hdfs_crc32c_packet{});
+  size_t nv = 0;
+  rc = verify_packets_impl(s, vlen, proto, cs, ctype, recs.data(), recs.size(), &nv, used, true);
+  if (rc < 0) return rc;
+  recs.resize(nv);
+  *again = apply_read_window(recs.data(), nv, *used, co, got, &pieces);
+  recs.resize(nv);
+  return HDFS_CRC32C_OK;
+}
+
 // Host-resident stream, host destination: framed on the host, the packets
 // the read takes verified on the GPU (hdfs_crc32c_verify_packets' host
 // pipeline), then their delivered bytes copied.
@@ -1930,19 +1957,9 @@ int read_host_to_host(const uint8_t *s, uint64_t len, int proto, uint32_t cs, in
     co.client_offset = client_offset;
     co.want = uint64_t(read_len);
     co.cap = std::min<uint64_t>(total, uint64_t(read_len));
-    // the window is a function of the headers: which packets the read takes
-    if ((rc = parse_packet_stream(s, len, proto, cs, ctype, max_pkts, recs, &used, g_err, sizeof(g_err)))) return rc;
-    size_t nh = recs.size(), seen = 0;
-    uint64_t ch = used;
-    (void)apply_read_window(recs.data(), nh, ch, co, nullptr, nullptr, &seen);
-    // verified: up to the start of the first packet the walk did not look at
-    const uint64_t vlen = seen < recs.size() ? recs[seen].stream_off : len;
-    recs.assign(seen, hdfs_crc32c_packet{});
-    size_t nv = 0;
-    rc = verify_packets_impl(s, vlen, proto, cs, ctype, recs.data(), recs.size(), &nv, &used, true);
-    if (rc < 0) return rc;
-    n = nv;
-    again = apply_read_window(recs.data(), n, used, co, &got, &pieces);
+    if ((rc = host_window_plan(s, len, proto, cs, ctype, co, max_pkts, recs, pieces, &used, &got, &again)) < 0)
+      return rc;
+    n = recs.size();
   } else {
     // straight into the caller's records (max_pkts of them)
     size_t nv = 0;
@@ -2206,7 +2223,6 @@ namespace {
 int reader_open(const uint8_t *s, uint64_t len, int proto, uint32_t cs, int ctype, int64_t client_offset,
                 int64_t read_len, size_t max_pkts, hdfs_crc32c_reader **out) {
   const int dev = stream_device(s);
-  if (dev < 0) return fail(HDFS_CRC32C_EINVAL, "a reader takes a device-resident stream");
   auto *rd = new (std::nothrow) hdfs_crc32c_reader;
   if (!rd) return fail(HDFS_CRC32C_ENOMEM, "reader");
   std::unique_ptr<hdfs_crc32c_reader, void (*)(hdfs_crc32c_reader *)> guard(rd, [](hdfs_crc32c_reader *r) {
@@ -2222,10 +2238,20 @@ int reader_open(const uint8_t *s, uint64_t len, int proto, uint32_t cs, int ctyp
   co.want = co.cap = uint64_t(read_len);
   size_t n = 0;
   uint64_t used = 0, got = 0;
-  int rc = verify_packets_dev_impl(dev, s, len, proto, cs, ctype, rd->recs.data(), max_pkts, &n, &used, true, co, &got,
-                                   &rd->pieces);
-  if (rc < 0) return rc;
-  rd->recs.resize(n);
+  int rc;
+  if (dev >= 0) {
+    rc = verify_packets_dev_impl(dev, s, len, proto, cs, ctype, rd->recs.data(), max_pkts, &n, &used, true, co, &got,
+                                 &rd->pieces);
+    if (rc < 0) return rc;
+    rd->recs.resize(n);
+  } else {  // a host-resident stream: framed on the host, the read's packets verified on the GPU
+    int again = 0;
+    if ((rc = host_window_plan(s, len, proto, cs, ctype, co, max_pkts, rd->recs, rd->pieces, &used, &got, &again)) < 0)
+      return rc;
+    n = rd->recs.size();
+    rc = first_error(rd->recs.data(), n);
+    if (!rc && again) rc = HDFS_CRC32C_AGAIN;
+  }
   rd->status = rc == HDFS_CRC32C_AGAIN ? HDFS_CRC32C_OK : rc;  // (the window is the whole read: no AGAIN)
   rd->total = got;
   rd->consumed = used;
@@ -2245,7 +2271,7 @@ int reader_open(const uint8_t *s, uint64_t len, int proto, uint32_t cs, int ctyp
       rd->rec_done[k] = k + 1 == n ? got : cum;  // the last record (an error, or the read's end) goes with the end
     }
   }
-  {
+  if (dev >= 0) {
     DeviceGuard g(dev);
     {
       DevCtx *cp = nullptr;
@@ -2261,11 +2287,7 @@ int reader_open(const uint8_t *s, uint64_t len, int proto, uint32_t cs, int ctyp
 
 int reader_next(hdfs_crc32c_reader *rd, const hdfs_crc32c_iovec *iov, int iovcnt, hdfs_crc32c_packet *pkts,
                 size_t max_pkts, size_t *npkts, uint64_t *consumed, uint64_t *delivered) {
-  DevCtx *cp = nullptr;
   int rc;
-  if ((rc = ctx_init(rd->dev, &cp))) return rc;
-  DevCtx &c = *cp;
-  DeviceGuard g(c.dev);
   bool any_host = false, any_dev = false;
   uint64_t cap = 0;
   for (int i = 0; i < iovcnt; i++) {
@@ -2274,10 +2296,15 @@ int reader_next(hdfs_crc32c_reader *rd, const hdfs_crc32c_iovec *iov, int iovcnt
     const int d = stream_device(iov[i].base);
     if (d < 0) any_host = true;
     else if (d == rd->dev) any_dev = true;
+    else if (rd->dev < 0) return fail(HDFS_CRC32C_EINVAL, "iovec %d: a host-resident stream copies out to host memory", i);
     else return fail(HDFS_CRC32C_EINVAL, "iovec %d: memory of device %d, the stream is on %d", i, d, rd->dev);
     cap += iov[i].len;
   }
   if (any_host && any_dev) return fail(HDFS_CRC32C_EINVAL, "iovecs mix host and device memory");
+  DevCtx *cp = nullptr;
+  if ((rc = ctx_init(rd->dev, &cp))) return rc;  // (a host stream: the default device's, unused)
+  DevCtx &c = *cp;
+  DeviceGuard g(c.dev);
   const uint64_t want = std::min(cap, rd->total - rd->done);
   // the call's copy jobs: the next `want` bytes of the pieces, laid over the iovecs
   Pieces mine;
@@ -2300,7 +2327,9 @@ int reader_next(hdfs_crc32c_reader *rd, const hdfs_crc32c_iovec *iov, int iovcnt
   }
   std::vector<CopyJob> jobs;
   scatter_jobs(rd->s, mine, iov, iovcnt, jobs);
-  if (!jobs.empty() && any_host && mine.size() > 2) {
+  if (rd->dev < 0) {
+    run_host_jobs(jobs);  // host stream to host memory: the reference's memcpy (src/datanode.c:2516)
+  } else if (!jobs.empty() && any_host && mine.size() > 2) {
     // many pieces into host memory: gathered contiguous in the device
     // staging area by one copy, then one D2H per iovec (not one per piece)
     std::lock_guard<std::mutex> lk0(c.rd_mu);

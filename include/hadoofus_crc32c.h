@@ -343,11 +343,14 @@ int hdfs_crc32c_job_wait_blocks(hdfs_crc32c_job *job, hdfs_crc32c_packet *pkts, 
  * reference's read re-entered with remains_pkt > 0 (src/datanode.c:2356-2361,
  * 2547-2549) for a caller whose buffer is smaller than the read, without
  * framing or verifying any packet again.  open frames and verifies the
- * packets of the read [client_offset, client_offset + read_len) of a
- * DEVICE-resident stream under hdfs_crc32c_read_packets' rules (the read
- * ends at its first error; max_pkts: room for its records) and keeps their
- * records; each next delivers the following bytes into iov (device memory
- * of the stream's device: one copy launch; or host memory: D2H per iovec),
+ * packets of the read [client_offset, client_offset + read_len) under
+ * hdfs_crc32c_read_packets' rules (the read ends at its first error;
+ * max_pkts: room for its records) and keeps their records; each next
+ * delivers the following bytes into iov -- from a DEVICE-resident stream
+ * into device memory of its device (one copy launch, or a request to the
+ * open mailbox for <= 96 KiB) or host memory (D2H); from a HOST-resident
+ * stream (framed on the host, its read's packets verified on the GPU at
+ * open) into host memory only (memcpy, src/datanode.c:2516) --
  * *delivered = bytes this call, *consumed = the stream bytes of the packets
  * delivered so far (the read's own consumed at its end), the records of the
  * packets it completed into pkts, and returns HDFS_CRC32C_AGAIN while bytes

@@ -225,3 +225,31 @@ def test_gpu_reader_records_or_stream_run_out(engine, oracle):
         assert (rc, recs, used) == want[:3], mp
         assert data == want[3], mp
         keep.free()
+
+
+@pytest.mark.gpu
+def test_gpu_reader_host_stream(engine, oracle):
+    """A reader over a HOST-resident stream (a host-memory datanode's
+    receive buffer): framed on the host, the read's packets verified on the
+    GPU once at open, each next a memcpy into the caller's host buffer
+    (src/datanode.c:2516) -- equal to the oracle's read; device buffers are
+    refused for a host stream, as hdfs_crc32c_read_packets refuses them."""
+    dl = [65536] * 50 + [3333]
+    s, _ = build_stream(oracle.crc32c, 2, 512, CSUM_CRC32C, dl, seed=17, corrupt=[(44, 5)])
+    hs = np.frombuffer(s, np.uint8).copy()
+    for co, rl in ((1000, sum(dl) // 2), (5, sum(dl))):
+        want = oracle.read_packets(s, co, rl)
+        for piece in (4099, 65536, (1 << 20) + 3):
+            rd = engine.Reader(hs.ctypes.data, len(s), co, rl)
+            try:
+                rc, recs, used, data, calls = _read_through(engine, rd, piece, len(want[3]) + 2 * piece, True)
+            finally:
+                rd.close()
+            assert (rc, recs, used) == want[:3], (co, rl, piece)
+            assert data == want[3], (co, rl, piece)
+    dbuf = engine.DeviceBuffer(65536)
+    rd = engine.Reader(hs.ctypes.data, len(s), 0, 100000)
+    with pytest.raises(engine.CRC32CError):
+        rd.next([(dbuf.ptr, 65536)])
+    rd.close()
+    dbuf.free()

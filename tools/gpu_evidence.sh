@@ -7,7 +7,9 @@
 # rocprofv3 with its trace-vs-line comparison), p (PMC + torchrun +
 # C4), d (device-stream + small-call benches), q (SQ/TA/TCP counters of the
 # compute and verify kernels, tools/pmc_sq.py), s (phase stamps of the
-# speculative verify, tools/spec_phases.py); default tbpd, one call.
+# speculative verify, tools/spec_phases.py), r (reader / copy costs:
+# tools/reader_sizes.py, reader_calls.py, copy_phases.py); default tbpd,
+# one call.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
@@ -42,4 +44,7 @@ has q && step pmc_sq timeout -k 10 900 python tools/pmc_sq.py ${O}_pmc_sq.json >
 has q && cat ${O}_pmc_sq.json
 has s && step spec_phases timeout -k 10 300 python tools/spec_phases.py ${O}_spec_phases.json > /dev/null 2> ${O}_spec_phases.err
 has s && cat ${O}_spec_phases.json
+has r && step reader_sizes timeout -k 10 300 python tools/reader_sizes.py ${O}_reader_sizes.json > /dev/null 2> ${O}_reader_sizes.err
+has r && step reader_calls timeout -k 10 300 python tools/reader_calls.py ${O}_reader_calls.json > /dev/null 2> ${O}_reader_calls.err
+has r && step copy_phases timeout -k 10 300 python tools/copy_phases.py ${O}_copy_phases.json > /dev/null 2> ${O}_copy_phases.err
 exit 0
