@@ -5,7 +5,9 @@ only copies -- the reference's read re-entered with remains_pkt > 0
 pieces, concatenated, equal the oracle's single read loop (oracle_read_packets:
 src/datanode.c:1476-1481, 2428-2549): the bytes, the records in order, the
 final status and consumed bytes; every call but the last fills its buffer
-and returns AGAIN; nothing is written past a buffer."""
+and returns AGAIN; nothing is written past a buffer.  Call by call, each
+return (status, the records it completes, consumed, delivered) equals
+_reader_model's, derived from the oracle's read."""
 import numpy as np
 import pytest
 
@@ -22,9 +24,48 @@ def _dev(engine, s, shift=0):
     return buf, buf.ptr + shift
 
 
-def _read_through(engine, rd, piece, total_cap, host):
+ERR_BAD_LASTPACKET = 32
+
+
+def _reader_model(want, co, rl, piece):
+    """What each hdfs_crc32c_reader_next call returns for the oracle's read
+    `want` = (rc, records, consumed, bytes) of [co, co + rl) through buffers
+    of `piece` bytes: (rc, records completed, consumed, delivered) per call.
+    A record is complete once every byte it delivers is out (the read's last
+    record -- its error, or the packet that completes it -- with the last
+    call); consumed = the end of the last complete packet, the read's own
+    at its end; AGAIN until then (src/datanode.c:2547-2549)."""
+    rc_f, recs, used_f, data = want
+    total = len(data)
+    cum, done_at = 0, []
+    for r in recs:
+        gives = 0
+        if not r["error"] or r["error"] == ERR_BAD_LASTPACKET:
+            off, dl = r["offset_in_block"], r["data_len"]
+            gives = max(0, min(off + dl, co + rl) - max(off, co))
+        cum += gives
+        done_at.append(cum)
+    if done_at:
+        done_at[-1] = total
+    calls, done, nxt = [], 0, 0
+    while True:
+        got = min(piece, total - done)
+        done += got
+        k0 = nxt
+        while nxt < len(recs) and done_at[nxt] <= done and (done == total or nxt + 1 < len(recs)):
+            nxt += 1
+        if done == total:
+            calls.append((rc_f, recs[k0:nxt], used_f, got))
+            return calls
+        r = recs[nxt - 1] if nxt else None
+        consumed = r["stream_off"] + r["header_len"] + r["crc_len"] + r["data_len"] if r else 0
+        calls.append((AGAIN, recs[k0:nxt], consumed, got))
+
+
+def _read_through(engine, rd, piece, total_cap, host, model=None):
     """All of a reader's bytes through buffers of `piece` bytes (a fresh
-    buffer region each call, a 16-B guard after it)."""
+    buffer region each call, a 16-B guard after it); model: each call's
+    expected (rc, records, consumed, delivered) (_reader_model)."""
     if host:
         arena = np.full(total_cap + 64 * 1024, 0xA5, np.uint8)
         base = arena.ctypes.data
@@ -35,6 +76,8 @@ def _read_through(engine, rd, piece, total_cap, host):
     at, data, recs, calls = 0, b"", [], 0
     while True:
         rc, pk, used, got = rd.next([(base + at, piece)])
+        if model is not None:
+            assert calls < len(model) and (rc, pk, used, got) == model[calls], (piece, calls)
         calls += 1
         recs += pk
         if got:
@@ -51,6 +94,8 @@ def _read_through(engine, rd, piece, total_cap, host):
         assert got == piece and calls < 100000
     if not host:
         dbuf.free()
+    if model is not None:
+        assert calls == len(model), (piece, calls, len(model))
     return rc, recs, used, data, calls
 
 
@@ -80,7 +125,8 @@ def test_gpu_reader_vs_oracle(engine, oracle, proto, ctype, sizes):
                             ((1 << 20) + 7, True)):
             rd = engine.Reader(p, len(s), co, rl, proto, 512, ctype)
             try:
-                rc, recs, used, data, calls = _read_through(engine, rd, piece, len(want[3]) + piece * 2, host)
+                rc, recs, used, data, calls = _read_through(engine, rd, piece, len(want[3]) + piece * 2, host,
+                                                            model=_reader_model(want, co, rl, piece))
             finally:
                 rd.close()
             assert (rc, recs, used) == want[:3], (co - base, rl, piece)
@@ -101,7 +147,8 @@ def test_gpu_reader_errors_first(engine, oracle):
         want = oracle.read_packets(st, co, rl)
         keep, p = _dev(engine, st)
         rd = engine.Reader(p, len(st), co, rl)
-        rc, recs, used, data, calls = _read_through(engine, rd, 65536, len(want[3]) + 2 * 65536, False)
+        rc, recs, used, data, calls = _read_through(engine, rd, 65536, len(want[3]) + 2 * 65536, False,
+                                                    model=_reader_model(want, co, rl, 65536))
         rd.close()
         assert (rc, recs, used) == want[:3] and data == want[3]
         assert rc != 0
@@ -165,7 +212,8 @@ def test_gpu_reader_through_mailbox(engine, oracle):
             c0 = mb.stats()[0]
             rd = engine.Reader(p, len(s), co, rl)
             try:
-                rc, recs, used, data, calls = _read_through(engine, rd, piece, len(want[3]) + piece * 2, False)
+                rc, recs, used, data, calls = _read_through(engine, rd, piece, len(want[3]) + piece * 2, False,
+                                                            model=_reader_model(want, co, rl, piece))
             finally:
                 rd.close()
             assert (rc, recs, used) == want[:3], piece
@@ -219,7 +267,8 @@ def test_gpu_reader_records_or_stream_run_out(engine, oracle):
         keep, p = _dev(engine, st)
         rd = engine.Reader(p, len(st), co, rl, max_pkts=mp)
         try:
-            rc, recs, used, data, calls = _read_through(engine, rd, 65536, len(want[3]) + 2 * 65536, False)
+            rc, recs, used, data, calls = _read_through(engine, rd, 65536, len(want[3]) + 2 * 65536, False,
+                                                        model=_reader_model(want, co, rl, 65536))
         finally:
             rd.close()
         assert (rc, recs, used) == want[:3], mp
@@ -242,7 +291,8 @@ def test_gpu_reader_host_stream(engine, oracle):
         for piece in (4099, 65536, (1 << 20) + 3):
             rd = engine.Reader(hs.ctypes.data, len(s), co, rl)
             try:
-                rc, recs, used, data, calls = _read_through(engine, rd, piece, len(want[3]) + 2 * piece, True)
+                rc, recs, used, data, calls = _read_through(engine, rd, piece, len(want[3]) + 2 * piece, True,
+                                                            model=_reader_model(want, co, rl, piece))
             finally:
                 rd.close()
             assert (rc, recs, used) == want[:3], (co, rl, piece)
@@ -253,3 +303,68 @@ def test_gpu_reader_host_stream(engine, oracle):
         rd.next([(dbuf.ptr, 65536)])
     rd.close()
     dbuf.free()
+
+
+def test_reader_model_concatenates_to_the_oracle_read(oracle):
+    """CPU: the per-call model (_reader_model) adds up to the oracle's single
+    read -- every record once and in order, the bytes, consumed at the end --
+    for clean, bad-CRC, BAD_LASTPACKET and UNEXPECTED_READ_OFFSET reads and
+    buffer sizes around the packet size."""
+    dl = [65536] * 12 + [1000]
+    s, _ = build_stream(oracle.crc32c, 2, 512, CSUM_CRC32C, dl, seed=3, corrupt=[(9, 4)])
+    s2, _ = build_stream(oracle.crc32c, 2, 512, CSUM_CRC32C, dl, seed=4)
+    for st, co, rl in ((s, 100, 5 * 65536), (s, 70000, 20 * 65536), (s2, 3, sum(dl) + 500), (s2, 0, 1),
+                       (s2, 5 * 65536 + 7, 3 * 65536)):
+        want = oracle.read_packets(st, co, rl)
+        for piece in (1, 4099, 65536, 65537, 1 << 20):
+            if len(want[3]) // piece > 5000:
+                continue
+            m = _reader_model(want, co, rl, piece)
+            assert [r for c in m for r in c[1]] == want[1]
+            assert sum(c[3] for c in m) == len(want[3])
+            assert m[-1][0] == want[0] and m[-1][2] == want[2]
+            assert all(c[0] == AGAIN and c[3] == piece for c in m[:-1])
+
+
+@pytest.mark.gpu
+def test_gpu_reader_random(engine, oracle):
+    """Seeded random reads: stream shapes (packet sizes mixed and regular, a
+    corrupt chunk or none, v1/v2, CRC32/CRC32C), read windows anywhere in the
+    block, buffer sizes from 1 B to 2 MiB, device or host buffers, the
+    mailbox open or not -- every call equal to _reader_model of the oracle's
+    read."""
+    rng = np.random.default_rng(2024)
+    for case in range(24):
+        proto = int(rng.choice([1, 2]))
+        ctype = int(rng.choice([CSUM_CRC32, CSUM_CRC32C]))
+        npk = int(rng.integers(2, 40))
+        if rng.random() < 0.5:
+            dl = [65536] * npk + [int(rng.integers(1, 65536))]
+        else:
+            dl = [int(x) for x in rng.choice([512, 4096, 30000, 61440, 65536], npk)]
+        corrupt = [(int(rng.integers(0, len(dl))), 0)] if rng.random() < 0.4 else []
+        s, _ = build_stream(oracle.crc32c, proto, 512, ctype, dl, seed=case, corrupt=corrupt,
+                            last_empty=proto == 2)
+        total = sum(dl)
+        co = int(rng.integers(0, total))
+        rl = int(rng.integers(1, total - co + 2000))
+        want = oracle.read_packets(s, co, rl, proto, 512, ctype)
+        piece = int(rng.choice([1, 777, 4096, 65536, 100000, 1 << 21]))
+        if len(want[3]) // piece > 2000:
+            piece = max(piece, len(want[3]) // 2000 + 1)
+        host = bool(rng.random() < 0.3)
+        keep, p = _dev(engine, s, case % 4)
+        box = engine.Mailbox() if rng.random() < 0.3 else None
+        try:
+            rd = engine.Reader(p, len(s), co, rl, proto, 512, ctype)
+            try:
+                rc, recs, used, data, calls = _read_through(engine, rd, piece, len(want[3]) + 2 * piece, host,
+                                                            model=_reader_model(want, co, rl, piece))
+            finally:
+                rd.close()
+        finally:
+            if box:
+                box.close()
+            keep.free()
+        assert (rc, recs, used) == want[:3], case
+        assert data == want[3], case
