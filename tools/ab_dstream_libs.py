@@ -1,6 +1,6 @@
 """Same-process A/B of two builds of the engine on device-resident packet runs
 (GPU box): a 1 GiB run and one 128 MiB block through hdfs_crc32c_verify_packets
-of each library, interleaved, best of N per round, 3 rounds.  Only the
+of each library, interleaved, best of N per round, 3 rounds (AB_ROUNDS).  Only the
 round-4-stable entry points are bound, so any two builds compare.
 
     python tools/ab_dstream_libs.py BASE_LIB NEW_LIB [out.json]"""
@@ -56,7 +56,7 @@ def main():
         d.upload(im)
         devs.append((name, d, im.nbytes, npk))
     h.device_sync()
-    for _ in range(3):
+    for _ in range(int(os.environ.get("AB_ROUNDS", "3"))):
         r = {}
         for name, d, n, npk in devs:
             for tag, lib in (("base", base), ("new", new)):
