@@ -368,3 +368,54 @@ def test_gpu_reader_random(engine, oracle):
             keep.free()
         assert (rc, recs, used) == want[:3], case
         assert data == want[3], case
+
+
+@pytest.mark.gpu
+def test_gpu_readers_threads(engine, oracle):
+    """Readers used from several threads at once (ctypes releases the GIL:
+    the engine's calls really interleave), beside verify jobs and scatter
+    reads on other threads, with the mailbox open: every reader's calls
+    still equal the per-call model of the oracle's read."""
+    import threading
+    dl = [65536] * 24 + [2222]
+    streams = [build_stream(oracle.crc32c, 2, 512, CSUM_CRC32C, dl, seed=200 + i,
+                            corrupt=[(20, 1)] if i % 2 else [])[0] for i in range(4)]
+    bufs = [_dev(engine, st, i) for i, st in enumerate(streams)]
+    errors = []
+
+    def reader_worker(i):
+        try:
+            st, (_, p) = streams[i], bufs[i]
+            for rep, (co, rl, piece) in enumerate(((100, 20 * 65536, 65536), (7, sum(dl), 30001),
+                                                   (65536 * 3, 5 * 65536, 1 << 20))):
+                want = oracle.read_packets(st, co, rl)
+                rd = engine.Reader(p, len(st), co, rl)
+                try:
+                    got = _read_through(engine, rd, piece, len(want[3]) + 2 * piece, rep == 1,
+                                        model=_reader_model(want, co, rl, piece))
+                finally:
+                    rd.close()
+                assert got[:3] == want[:3] and got[3] == want[3]
+        except Exception as e:  # noqa: BLE001 -- reported by the main thread
+            errors.append((i, repr(e)))
+
+    def job_worker():
+        try:
+            for _ in range(3):
+                jobs = [engine.VerifyJob(p, len(st)) for st, (_, p) in zip(streams, bufs)]
+                for j, st in zip(jobs, streams):
+                    assert j.wait() == oracle.verify_packets(st)
+        except Exception as e:  # noqa: BLE001
+            errors.append(("jobs", repr(e)))
+
+    with engine.Mailbox():
+        th = [threading.Thread(target=reader_worker, args=(i,)) for i in range(4)]
+        th.append(threading.Thread(target=job_worker))
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=240)
+        assert not any(t.is_alive() for t in th)
+    assert not errors, errors
+    for b, _ in bufs:
+        b.free()
