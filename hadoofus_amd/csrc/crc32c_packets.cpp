@@ -2092,6 +2092,7 @@ int copy_jobs_dev(CopyCtl &k, hipStream_t st, const std::vector<CopyJob> &jobs_i
       HIPCHK(launch_copy_pieces(a, grid, st));
     } else {
       // as many jobs as fit 2^31 units
+      const auto tb = std::chrono::steady_clock::now();
       size_t j1 = j;
       uint64_t units = 0;
       while (j1 < jobs.size()) {
@@ -2156,7 +2157,17 @@ int copy_jobs_dev(CopyCtl &k, hipStream_t st, const std::vector<CopyJob> &jobs_i
       a.per = per;
       a.total = uint32_t(units);
       a.seq = next_seq();
+      const auto tl = std::chrono::steady_clock::now();
       HIPCHK(launch_copy_pieces(a, int(grid), st));
+      if (g_dstream_trace) {
+        const auto tw = std::chrono::steady_clock::now();
+        if ((rc = poll_seq(k.hdone, a.seq, "read delivery", st))) return rc;
+        auto us = [](std::chrono::steady_clock::time_point x, std::chrono::steady_clock::time_point y) {
+          return std::chrono::duration<double, std::micro>(y - x).count();
+        };
+        std::fprintf(stderr, "dstream copy table n=%u grid=%u build_us=%.1f launch_us=%.1f wait_us=%.1f\n", n, grid,
+                     us(tb, tl), us(tl, tw), us(tw, std::chrono::steady_clock::now()));
+      }
       j = j1;
     }
     if ((rc = poll_seq(k.hdone, a.seq, "read delivery", st))) return rc;
@@ -2185,14 +2196,23 @@ int read_dev_scatter(int dev, const uint8_t *s, uint64_t len, int proto, uint32_
   size_t n = 0;
   uint64_t used = 0, got = 0;
   Pieces pieces;
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
   rc = verify_packets_dev_impl(dev, s, len, proto, cs, ctype, pkts, max_pkts, &n, &used, true, co, &got, &pieces);
   if (rc < 0) return rc;
+  const auto t1 = clk::now();
   std::vector<CopyJob> jobs;
   scatter_jobs(s, pieces, iov, iovcnt, jobs);
+  const auto t2 = clk::now();
   if (!jobs.empty()) {
     std::lock_guard<std::mutex> lk(c.mu);
     int r2 = copy_jobs_dev(c.cp, c.stream, jobs, &c);
     if (r2) return r2;
+  }
+  if (g_dstream_trace) {  // diagnostic: where a scatter read spends its time (us)
+    auto us = [](clk::time_point x, clk::time_point y) { return std::chrono::duration<double, std::micro>(y - x).count(); };
+    std::fprintf(stderr, "dstream scatter pieces=%zu jobs=%zu verify_us=%.1f jobs_us=%.1f copy_us=%.1f\n",
+                 pieces.size(), jobs.size(), us(t0, t1), us(t1, t2), us(t2, clk::now()));
   }
   *npkts = n;
   *consumed = used;
