@@ -351,11 +351,16 @@ int hdfs_crc32c_job_wait_blocks(hdfs_crc32c_job *job, hdfs_crc32c_packet *pkts, 
  * open mailbox for <= 96 KiB) or host memory (D2H); from a HOST-resident
  * stream (framed on the host, its read's packets verified on the GPU at
  * open) into host memory only (memcpy, src/datanode.c:2516) --
- * *delivered = bytes this call, *consumed = the stream bytes of the packets
- * delivered so far (the read's own consumed at its end), the records of the
- * packets it completed into pkts, and returns HDFS_CRC32C_AGAIN while bytes
- * remain, then the read's status (0, or the error that ended it, whose
- * record comes last).  The stream must stay unchanged until close. */
+ * *delivered = bytes this call, *consumed = the end of the last packet
+ * delivered whole so far (the read's own consumed at its end), into pkts
+ * the records of the packets whose last byte this call delivered (the
+ * read's last record with the last call), and returns HDFS_CRC32C_AGAIN
+ * while bytes remain, then the read's status: 0, or the error that ended
+ * it, whose record comes last.  A read the stream or max_pkts cannot
+ * complete ends with 0 and fewer bytes than read_len, as
+ * hdfs_crc32c_read_packets' does: resume at stream + consumed.  The stream
+ * must stay unchanged until close; calls after the last return the status
+ * again and deliver nothing. */
 typedef struct hdfs_crc32c_reader hdfs_crc32c_reader;
 int hdfs_crc32c_reader_open(const void *stream, uint64_t len, int proto, uint32_t chunk_size, int ctype,
     int64_t client_offset, int64_t read_len, size_t max_pkts, hdfs_crc32c_reader **rd);
