@@ -3685,6 +3685,11 @@ __global__ __launch_bounds__(1024) void small_run_kernel(const uint8_t *__restri
   }
 }
 
+// The delivery of verified bytes (the unit, store and completion protocol:
+// "Copy of a verified read's next bytes" above the mailbox kernel, which
+// serves small deliveries with the same unit code).  !TAB: the pieces in the
+// kernel arguments, staged in LDS, units strided over the grid.  TAB: the
+// device table, each workgroup a contiguous unit range from its first entry.
 template <bool TAB>
 __global__ __launch_bounds__(256) void copy_pieces_kernel(CopyPieces a) {
   constexpr uint32_t kStage = TAB ? kCopyTabStage : kCopyPiecesMax;
