@@ -93,6 +93,9 @@ uint32_t g_copy_wg_units = uint32_t(HDFS_KNOB("HDFS_CRC32C_COPY_WG_UNITS", 1024)
 int g_copy_dev_tab = HDFS_KNOB("HDFS_CRC32C_COPY_DEV_TAB", 1);
 // (r05 reader_sizes: the resident block copies ~16 GB/s; 64 KiB 7.4 us per
 // delivery against 10.5 launched, 256 KiB 19 against 10.6)
+// What follows a taken run, when short, in one short-run launch (1) or a
+// framing pass (0, diagnostic A/B).
+int g_tail_small = HDFS_KNOB("HDFS_CRC32C_TAIL_SMALL", 1);
 uint64_t g_mb_copy_max = uint64_t(HDFS_KNOB("HDFS_CRC32C_MB_COPY_MAX", 96 << 10));
 // Compute-mode CRC stores: 2 (product) schedule 3 with the LDS group gather
 // (one 256-B store per 8-tile group); diagnostic build only: 1 schedule 4

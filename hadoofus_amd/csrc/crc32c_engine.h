@@ -63,6 +63,9 @@ hipError_t launch_header_window(const uint8_t *s, uint64_t len, uint64_t base, u
 // A verified read's next bytes to device buffers (copy_pieces_kernel), grid
 // workgroups of 256 threads, <= kCopyBlocksMax.
 hipError_t launch_copy_pieces(const CopyPieces &a, int grid, hipStream_t stream);
+// The same from a device table, beside a running verify (no LDS, one
+// workgroup per CU next to a verify workgroup).
+hipError_t launch_copy_beside(const CopyPieces &a, int grid, hipStream_t stream);
 hipError_t launch_small_run(const uint8_t *s, uint64_t len, uint32_t count, int proto, uint32_t cs, int ctype,
                             int verify, const uint32_t *tab, const uint32_t *pow2, uint8_t *copy_dst,
                             uint64_t copy_cap, int win, int64_t client_offset, uint8_t *hout, uint32_t seq,
@@ -272,6 +275,10 @@ struct DevCtx {
   // client reads over several device iovecs: the copy kernel's completion
   // word and table (guarded by mu)
   CopyCtl cp;
+  // the copy a scatter read starts beside its verify (copy_beside_kernel)
+  // and its stream (guarded by mu)
+  CopyCtl cp_beside;
+  hipStream_t cp_stream = nullptr;
   // readers' copy state, kept for the next reader (a free would synchronise
   // the device, which waits for an open mailbox to idle out)
   std::vector<CopyCtl> cp_pool;
@@ -364,6 +371,8 @@ int mailbox_copy(DevCtx &c, const CopyEntry *e, uint32_t n);
 // Deliveries up to this many bytes go to the open mailbox (one CU copies;
 // larger ones launch copy_pieces_kernel).
 extern uint64_t g_mb_copy_max;
+// the short rest of a stream after a taken run: one short-run launch
+extern int g_tail_small;
 
 // One-launch path for synchronous calls on <= kSmallMax bytes
 // (small_chunks_kernel or the open mailbox; caller holds c.mu and has staged

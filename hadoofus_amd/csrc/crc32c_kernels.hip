@@ -3753,6 +3753,93 @@ __global__ __launch_bounds__(256) void copy_pieces_kernel(CopyPieces a) {
   stamp(3);
 }
 
+// The same delivery BESIDE a running verify (read_dev_scatter starts it
+// from the packets predicted at the speculative launch's early block): no
+// LDS -- the verify's workgroups hold each CU's -- and few enough VGPRs that
+// one workgroup fits next to a verify workgroup on every CU, so the copy
+// streams while the verify does.  Table launches only; a thread walks its
+// units (strided by 256) with its own entry cursor; a
+// piece's edge blocks go byte by byte on the spot.  Four units in flight
+// per lane; more workgroups than fit beside the verify, so the rest start as
+// its workgroups retire.
+struct CopyLdG {
+  uint32_t w[5], sh, ok;
+  uintptr_t D;
+};
+
+DEV void copyg_issue(CopyLdG &x, const CopyEntry *__restrict__ tab, uint32_t &ec, uint32_t &us, uint32_t &ue,
+                     uint32_t u, uint32_t u1) {
+  x.ok = 0u;
+  if (u >= u1) return;
+  while (u >= ue) {
+    ec++;
+    us = ue;
+    ue = tab[ec].uend;
+  }
+  const CopyEntry xe = tab[ec];
+  const uintptr_t d = reinterpret_cast<uintptr_t>(xe.dst), e = d + xe.len;
+  const uintptr_t D = (d & ~uintptr_t(15)) + 16u * uintptr_t(u - us);
+  if (D >= d && D + 16u <= e) {
+    const uintptr_t sa = reinterpret_cast<uintptr_t>(xe.src) + (D - d);
+    x.sh = uint32_t(sa & 3u);
+    const uint8_t *a0 = reinterpret_cast<const uint8_t *>(sa - x.sh);
+#pragma unroll
+    for (int q = 0; q < 4; q++) x.w[q] = gload32(a0 + 4 * q);
+    x.w[4] = x.sh ? gload32(a0 + 16) : 0u;
+    x.D = D;
+    x.ok = 1u;
+  } else {
+    copy_unit(xe.src, d, e, D);
+  }
+}
+
+DEV void copyg_finish(const CopyLdG &x) {
+  if (!x.ok) return;
+  u32x4 v;
+  v.x = align_word(x.w[1], x.w[0], x.sh);
+  v.y = align_word(x.w[2], x.w[1], x.sh);
+  v.z = align_word(x.w[3], x.w[2], x.sh);
+  v.w = align_word(x.w[4], x.w[3], x.sh);
+  store16_sc1(reinterpret_cast<uint8_t *>(x.D), v);
+}
+
+__global__ __launch_bounds__(256) void copy_beside_kernel(CopyPieces a) {
+  const uint32_t tid = threadIdx.x;
+  const uint32_t u0 = blockIdx.x * a.per, u1 = min(a.total, u0 + a.per);
+  const CopyEntry *__restrict__ tab = a.tab;
+  uint32_t ec = __builtin_amdgcn_readfirstlane(a.wg0[blockIdx.x]);
+  uint32_t us = ec ? tab[ec - 1u].uend : 0u, ue = tab[ec].uend;
+  constexpr int U = 4;
+  CopyLdG cur[U], nxt[U];
+#pragma unroll
+  for (int k = 0; k < U; k++) copyg_issue(cur[k], tab, ec, us, ue, u0 + tid + 256u * uint32_t(k), u1);
+  for (uint32_t ub = u0 + tid; ub < u1; ub += 256u * U) {
+#pragma unroll
+    for (int k = 0; k < U; k++) copyg_issue(nxt[k], tab, ec, us, ue, ub + 256u * uint32_t(U + k), u1);
+#pragma unroll
+    for (int k = 0; k < U; k++) copyg_finish(cur[k]);
+#pragma unroll
+    for (int k = 0; k < U; k++) cur[k] = nxt[k];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const uint32_t prev = __hip_atomic_fetch_add(a.count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev + 1u == gridDim.x) {
+      __hip_atomic_store(a.count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(a.done, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+hipError_t launch_copy_beside(const CopyPieces &a, int grid, hipStream_t stream) {
+  if (!a.n || grid < 1 || grid > int(kCopyTabBlocks) || !a.done || !a.count || !a.tab || !a.wg0 || !a.per ||
+      uint64_t(a.per) * uint32_t(grid) < a.total)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(copy_beside_kernel, dim3(grid), dim3(256), 0, stream, a);
+  return hipGetLastError();
+}
+
 hipError_t launch_copy_pieces(const CopyPieces &a, int grid, hipStream_t stream) {
   if (!a.n || grid < 1 || !a.done || !a.count) return hipErrorInvalidValue;
   if (a.tab) {

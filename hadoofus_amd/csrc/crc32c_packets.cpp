@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <functional>
 #include <memory>
 #include <thread>
 #include <vector>
@@ -835,6 +836,15 @@ int spec_launch(DevCtx &c, SpecSlot &S, hipStream_t st, const uint8_t *d, uint64
 // final block: exceptions, verdicts, what follows the run.  Not taken
 // (res.taken false) when packet 0 starts no run or a header left the
 // prediction -- the caller frames the run the regular way.
+// Called by the first speculative pass of a call (stream offset 0) once the
+// run's records are predicted from the early block, while the kernel still
+// verifies: a scatter read starts its copy there (read_dev_scatter).  Set
+// for the duration of one call on the calling thread.
+struct EarlyHook {
+  std::function<void(const hdfs_crc32c_packet *recs, uint32_t count)> fn;
+};
+thread_local const EarlyHook *t_early_hook = nullptr;
+
 int spec_collect(DevCtx &c, SpecSlot &S, const SpecLaunch &L, const CopyOut &co, hdfs_crc32c_packet *dst,
                  SpecResult &res) {
   (void)c;
@@ -860,6 +870,7 @@ int spec_collect(DevCtx &c, SpecSlot &S, const SpecLaunch &L, const CopyOut &co,
     r.offset_in_block = r0.offset_in_block + int64_t(k) * r0.data_len;
     r.seqno = r0.seqno + int64_t(k);
   }
+  if (t_early_hook && pos == 0) t_early_hook->fn(dst, E.count);
   const auto t3 = clk::now();
   if ((rc = poll_seq(&fin->seq, L.seq, "speculative verify", L.st))) return rc;
   if (g_dstream_trace) {  // diagnostic: where a speculative launch spends its time (us)
@@ -1167,6 +1178,38 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
     // copy-out: this pass fills the destination from what earlier passes
     // delivered on, within what is left of it
     const uint64_t done_b = std::min(payload, co.cap);
+    if (pos > 0 && left <= kSmallRunBytes && g_tail_small) {
+      // what follows a taken run -- a block's short last packet, the empty
+      // end packet -- in ONE short-run launch instead of a framing pass and
+      // its verify (three launches); it hands back (0) unless the walk ends
+      // inside it, and the regular pass takes over
+      CopyOut co2 = co;
+      if (co.dst) {
+        co2.dst = co.dst + done_b;
+        co2.cap = co.cap - done_b;
+      }
+      size_t nr = 0;
+      uint64_t used_r = 0, pay_r = 0;
+      const int r = small_run(c, d + pos, left, proto, cs, ctype, verify, co2, max_pkts - n, dst + n, &nr, &used_r,
+                              &pay_r);
+      if (r < 0) {
+        rc = r;
+        break;
+      }
+      if (r == 1) {
+        for (size_t k = 0; k < nr; k++) dst[n + k].stream_off += pos;
+        if (co.dst && !co.win && payload + pay_r > co.cap) {
+          rc = fail(HDFS_CRC32C_EINVAL, "copy-out buffer of %llu bytes is too small (%llu needed so far)",
+                    (unsigned long long)co.cap, (unsigned long long)(payload + pay_r));
+          break;
+        }
+        n += nr;
+        payload += pay_r;
+        *consumed = pos + used_r;
+        last_spec = true;  // (its completion words were seen: the call's last command has run)
+        break;
+      }
+    }
     if (try_spec && left > kSmallRunBytes) {
       SpecResult sr;
       if ((rc = spec_pass(c, d, len, pos, count, proto, cs, ctype, co, done_b, dg + L.bm,
@@ -2041,6 +2084,62 @@ void copyctl_free(CopyCtl &k) {
   k = CopyCtl{};
 }
 
+// The device table of a table launch: entries n jobs (< 2^31 units in all),
+// each workgroup's first entry, written in pinned memory and (g_copy_dev_tab)
+// copied to device memory on st; fills a's table fields.
+int copy_table(CopyCtl &k, hipStream_t st, const CopyJob *jobs, uint32_t n, uint64_t units, uint32_t grid,
+               CopyPieces &a) {
+  const uint32_t per = uint32_t((units + grid - 1u) / grid);
+  const size_t wg_off = align_up(size_t(n) * sizeof(CopyEntry), size_t(256));
+  const size_t need = wg_off + size_t(grid) * sizeof(uint32_t);
+  if (need > k.tab_cap) {
+    if (k.htab) HIPCHK(hipHostFree(k.htab));
+    k.htab = k.dtab = nullptr;
+    k.tab_cap = 0;
+    const size_t want = align_up(need, size_t(1) << 16);
+    if (hipHostMalloc(&k.htab, want, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
+      (void)hipGetLastError();
+      k.htab = nullptr;
+      return fail(HDFS_CRC32C_ENOMEM, "copy table of %zu bytes", want);
+    }
+    HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&k.dtab), k.htab, 0));
+    k.tab_cap = want;
+  }
+  auto *ent = reinterpret_cast<CopyEntry *>(k.htab);
+  auto *wg0 = reinterpret_cast<uint32_t *>(k.htab + wg_off);
+  uint32_t cum = 0, b = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    const CopyJob &x = jobs[i];
+    cum += copy_units(reinterpret_cast<uintptr_t>(x.dst), x.len);
+    ent[i] = CopyEntry{x.src, x.dst, uint32_t(x.len), cum};
+    // workgroups whose first unit lies in entry i
+    for (; b < grid && uint64_t(b) * per < cum; b++) wg0[b] = i;
+  }
+  for (; b < grid; b++) wg0[b] = n - 1u;  // (past the end: no units)
+  a.n = n;
+  const uint8_t *tab = k.dtab;
+  if (g_copy_dev_tab) {
+    if (need > k.vtab_cap) {
+      if (k.vtab) HIPCHK(hipFree(k.vtab));
+      k.vtab = nullptr;
+      k.vtab_cap = 0;
+      if (hipMalloc(&k.vtab, k.tab_cap) != hipSuccess) {
+        (void)hipGetLastError();
+        k.vtab = nullptr;
+        return fail(HDFS_CRC32C_ENOMEM, "copy table");
+      }
+      k.vtab_cap = k.tab_cap;
+    }
+    HIPCHK(hipMemcpyAsync(k.vtab, k.htab, need, hipMemcpyHostToDevice, st));
+    tab = k.vtab;
+  }
+  a.tab = reinterpret_cast<const CopyEntry *>(tab);
+  a.wg0 = reinterpret_cast<const uint32_t *>(tab + wg_off);
+  a.per = per;
+  a.total = uint32_t(units);
+  return HDFS_CRC32C_OK;
+}
+
 // The jobs (device source -> device destination) in launches of
 // copy_pieces_kernel on st, each waited for on the completion word: up to
 // kCopyPiecesMax pieces in the kernel arguments, more through the pinned
@@ -2108,54 +2207,7 @@ int copy_jobs_dev(CopyCtl &k, hipStream_t st, const std::vector<CopyJob> &jobs_i
       // units 53 us for 128 MiB, 4 096 of 2 048 units 67 us)
       const uint64_t wgu = std::max<uint32_t>(256u, g_copy_wg_units);
       const uint32_t grid = uint32_t(std::min<uint64_t>(kCopyTabGrid, std::max<uint64_t>(1, (units + wgu - 1u) / wgu)));
-      const uint32_t per = uint32_t((units + grid - 1u) / grid);
-      const size_t wg_off = align_up(size_t(n) * sizeof(CopyEntry), size_t(256));
-      const size_t need = wg_off + size_t(grid) * sizeof(uint32_t);
-      if (need > k.tab_cap) {
-        if (k.htab) HIPCHK(hipHostFree(k.htab));
-        k.htab = k.dtab = nullptr;
-        k.tab_cap = 0;
-        const size_t want = align_up(need, size_t(1) << 16);
-        if (hipHostMalloc(&k.htab, want, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
-          (void)hipGetLastError();
-          k.htab = nullptr;
-          return fail(HDFS_CRC32C_ENOMEM, "copy table of %zu bytes", want);
-        }
-        HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&k.dtab), k.htab, 0));
-        k.tab_cap = want;
-      }
-      auto *ent = reinterpret_cast<CopyEntry *>(k.htab);
-      auto *wg0 = reinterpret_cast<uint32_t *>(k.htab + wg_off);
-      uint32_t cum = 0, b = 0;
-      for (uint32_t i = 0; i < n; i++) {
-        const CopyJob &x = jobs[j + i];
-        cum += copy_units(reinterpret_cast<uintptr_t>(x.dst), x.len);
-        ent[i] = CopyEntry{x.src, x.dst, uint32_t(x.len), cum};
-        // workgroups whose first unit lies in entry i
-        for (; b < grid && uint64_t(b) * per < cum; b++) wg0[b] = i;
-      }
-      for (; b < grid; b++) wg0[b] = n - 1u;  // (past the end: no units)
-      a.n = n;
-      const uint8_t *tab = k.dtab;
-      if (g_copy_dev_tab) {
-        if (need > k.vtab_cap) {
-          if (k.vtab) HIPCHK(hipFree(k.vtab));
-          k.vtab = nullptr;
-          k.vtab_cap = 0;
-          if (hipMalloc(&k.vtab, k.tab_cap) != hipSuccess) {
-            (void)hipGetLastError();
-            k.vtab = nullptr;
-            return fail(HDFS_CRC32C_ENOMEM, "copy table");
-          }
-          k.vtab_cap = k.tab_cap;
-        }
-        HIPCHK(hipMemcpyAsync(k.vtab, k.htab, need, hipMemcpyHostToDevice, st));
-        tab = k.vtab;
-      }
-      a.tab = reinterpret_cast<const CopyEntry *>(tab);
-      a.wg0 = reinterpret_cast<const uint32_t *>(tab + wg_off);
-      a.per = per;
-      a.total = uint32_t(units);
+      if ((rc = copy_table(k, st, jobs.data() + j, n, units, grid, a))) return rc;
       a.seq = next_seq();
       const auto tl = std::chrono::steady_clock::now();
       HIPCHK(launch_copy_pieces(a, int(grid), st));
@@ -2173,6 +2225,56 @@ int copy_jobs_dev(CopyCtl &k, hipStream_t st, const std::vector<CopyJob> &jobs_i
     if ((rc = poll_seq(k.hdone, a.seq, "read delivery", st))) return rc;
   }
   return HDFS_CRC32C_OK;
+}
+
+// Runs shorter than this (packets) are not copied beside their verify: the
+// copy could only start when a short verify has ended (the host prepares it
+// from the early block in 10-30 us), and alone the LDS-staged copy kernel is
+// the faster one.
+constexpr uint32_t kBesideMinPackets = 1024;
+
+// The jobs launched beside a running verify on the context's copy stream
+// (copy_beside_kernel, one workgroup per CU next to the verify's); *seq: the
+// completion word's value to wait for.  Returns 1 when the jobs do not fit
+// one launch (nothing launched).  Caller holds c.mu.
+int copy_launch_beside(DevCtx &c, const std::vector<CopyJob> &jobs_in, uint32_t *seq) {
+  int rc;
+  if ((rc = copyctl_init(c.cp_beside))) return rc;
+  if (!c.cp_stream) HIPCHK(hipStreamCreateWithFlags(&c.cp_stream, hipStreamNonBlocking));
+  std::vector<CopyJob> jobs;
+  uint64_t units = 0;
+  for (const auto &j : jobs_in)
+    for (uint64_t o = 0; o < j.len; o += 1ull << 30) {
+      jobs.push_back({j.src + o, j.dst + o, std::min<uint64_t>(j.len - o, 1ull << 30)});
+      units += copy_units(reinterpret_cast<uintptr_t>(j.dst + o), jobs.back().len);
+    }
+  if (jobs.empty() || units > (1ull << 31)) return 1;
+  // (one workgroup per CU fits beside the verify; the others start as its
+  // workgroups retire)
+  const uint32_t grid = uint32_t(std::min<uint64_t>(kCopyTabGrid, std::max<uint64_t>(1, (units + 2047u) / 2048u)));
+  CopyPieces a{};
+  a.done = c.cp_beside.ddone;
+  a.count = c.cp_beside.count;
+  if ((rc = copy_table(c.cp_beside, c.cp_stream, jobs.data(), uint32_t(jobs.size()), units, grid, a))) return rc;
+  if (++c.cp_beside.seq == 0) ++c.cp_beside.seq;
+  a.seq = c.cp_beside.seq;
+  HIPCHK(launch_copy_beside(a, int(grid), c.cp_stream));
+  *seq = a.seq;
+  return HDFS_CRC32C_OK;
+}
+
+// iov with its first `skip` bytes dropped.
+std::vector<hdfs_crc32c_iovec> iov_after(const hdfs_crc32c_iovec *iov, int iovcnt, uint64_t skip) {
+  std::vector<hdfs_crc32c_iovec> out;
+  for (int i = 0; i < iovcnt; i++) {
+    if (skip >= iov[i].len) {
+      skip -= iov[i].len;
+      continue;
+    }
+    out.push_back({static_cast<uint8_t *>(iov[i].base) + skip, iov[i].len - skip});
+    skip = 0;
+  }
+  return out;
 }
 
 // Device-resident stream, several device iovecs: the read verified ONCE with
@@ -2198,11 +2300,53 @@ int read_dev_scatter(int dev, const uint8_t *s, uint64_t len, int proto, uint32_
   Pieces pieces;
   using clk = std::chrono::steady_clock;
   const auto t0 = clk::now();
+  // The copy starts under the verify: when the speculative launch's early
+  // block predicts the run's records, their window pieces are copied by
+  // copy_beside_kernel while the kernel verifies (bytes past what the read
+  // delivers are unspecified, as in the fused copy).  The verdicts then
+  // decide what was delivered; pieces the prediction missed (the packets
+  // after the run) are copied after, and a run whose headers left the
+  // prediction is copied again from the actual pieces.
+  Pieces pred;
+  uint32_t pred_seq = 0;
+  int pred_rc = 0;
+  EarlyHook hook{[&](const hdfs_crc32c_packet *recs, uint32_t count) {
+    if (count < kBesideMinPackets || pred_seq) return;
+    std::vector<hdfs_crc32c_packet> tmp(recs, recs + count);
+    size_t nn = count;
+    uint64_t u = 0, gp = 0;
+    (void)apply_read_window(tmp.data(), nn, u, co, &gp, &pred);
+    std::vector<CopyJob> pj;
+    scatter_jobs(s, pred, iov, iovcnt, pj);
+    if (pj.empty()) return;
+    const int r = copy_launch_beside(c, pj, &pred_seq);  // (c.mu is held by the verify)
+    if (r < 0) pred_rc = r;
+    if (r) pred_seq = 0;
+  }};
+  t_early_hook = &hook;
   rc = verify_packets_dev_impl(dev, s, len, proto, cs, ctype, pkts, max_pkts, &n, &used, true, co, &got, &pieces);
-  if (rc < 0) return rc;
+  t_early_hook = nullptr;
   const auto t1 = clk::now();
+  // the copy started under the verify is waited for on every path
+  if (pred_seq) {
+    const int r = poll_seq(c.cp_beside.hdone, pred_seq, "read delivery beside the verify", c.cp_stream);
+    if (r) return r;
+  }
+  if (rc < 0) return rc;
+  if (pred_rc < 0) return pred_rc;
+  // what the prediction copied: the pieces both agree on, in order
+  size_t same = 0;
+  uint64_t off = 0;
+  if (pred_seq) {
+    while (same < pieces.size() && same < pred.size() && pieces[same] == pred[same]) off += pieces[same++].second;
+    if (same < pieces.size() && same < pred.size()) same = 0, off = 0;  // left the prediction: copy it all again
+  }
   std::vector<CopyJob> jobs;
-  scatter_jobs(s, pieces, iov, iovcnt, jobs);
+  if (same < pieces.size()) {
+    const Pieces rest(pieces.begin() + long(same), pieces.end());
+    const std::vector<hdfs_crc32c_iovec> iv = iov_after(iov, iovcnt, off);
+    scatter_jobs(s, rest, iv.data(), int(iv.size()), jobs);
+  }
   const auto t2 = clk::now();
   if (!jobs.empty()) {
     std::lock_guard<std::mutex> lk(c.mu);
@@ -2211,8 +2355,10 @@ int read_dev_scatter(int dev, const uint8_t *s, uint64_t len, int proto, uint32_
   }
   if (g_dstream_trace) {  // diagnostic: where a scatter read spends its time (us)
     auto us = [](clk::time_point x, clk::time_point y) { return std::chrono::duration<double, std::micro>(y - x).count(); };
-    std::fprintf(stderr, "dstream scatter pieces=%zu jobs=%zu verify_us=%.1f jobs_us=%.1f copy_us=%.1f\n",
-                 pieces.size(), jobs.size(), us(t0, t1), us(t1, t2), us(t2, clk::now()));
+    std::fprintf(stderr,
+                 "dstream scatter pieces=%zu predicted=%zu kept=%zu jobs_after=%zu verify_us=%.1f jobs_us=%.1f "
+                 "copy_after_us=%.1f\n",
+                 pieces.size(), pred.size(), same, jobs.size(), us(t0, t1), us(t1, t2), us(t2, clk::now()));
   }
   *npkts = n;
   *consumed = used;

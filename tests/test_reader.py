@@ -156,6 +156,52 @@ def test_gpu_reader_errors_first(engine, oracle):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["clean", "seqno_jumps", "offset_skew", "offset_skew_early", "corrupt"])
+def test_gpu_scatter_copy_beside_verify(engine, oracle, kind):
+    """A scatter read of a run of >= 64 equal packets starts its copy under
+    the verify, from the packets predicted at the early block: when the
+    verdicts or the actual headers disagree with the prediction (a corrupt
+    packet ends the read early; a skewed offsetInBlock moves the window, or
+    only a record, as a seqno jump does) the result still equals the oracle's
+    read -- bytes, records, consumed, status -- and no guard byte moves."""
+    dl = [65536] * 1100 + [9999]  # (a run of >= 1 024 packets is copied beside its verify)
+    kw = {}
+    if kind == "seqno_jumps":
+        kw["seqnos"] = [k + (3 if k >= 900 else 0) for k in range(len(dl))]
+    elif kind == "offset_skew":
+        kw["offset_skew"] = {700: 4096}
+    elif kind == "offset_skew_early":  # packet 1 claims packet 0's offset: a read from 777 takes it from 777 too
+        kw["offset_skew"] = {1: -65536}
+    elif kind == "corrupt":
+        kw["corrupt"] = [(800, 2)]
+    s, _ = build_stream(oracle.crc32c, 2, 512, CSUM_CRC32C, dl, seed=31, **kw)
+    keep, p = _dev(engine, s, 3)
+    sizes = [8 << 20] * 8 + [123457] * 3
+    iov, off = [], 0
+    for n in sizes:
+        iov.append((off, n))
+        off += n + 16
+    cap = sum(sizes)
+    for co, rl in ((0, cap + 100000), (777, sum(dl) - 777), (5 * 65536 + 3, 1000 * 65536)):
+        want = oracle.read_packets(s, co, rl, cap=cap)
+        big = engine.DeviceBuffer(off + 64)
+        big.fill(0xA5)
+        rc, recs, used, got = engine.read_packets(p, len(s), None, 0, client_offset=co, read_len=rl,
+                                                  iov=[(big.ptr + a, n) for a, n in iov])
+        assert (rc, recs, used) == want[:3], (kind, co)
+        flat = big.download(off).tobytes()
+        data, left = b"", got
+        for a, n in iov:
+            take = min(n, left)
+            data += flat[a:a + take]
+            left -= take
+            assert flat[a + n:a + n + 16] == b"\xa5" * 16
+        assert data == want[3], (kind, co)
+        big.free()
+    keep.free()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("nbuf,lo,hi", [(2000, 1, 300), (300, 1000, 40000), (40, 1, 17)])
 def test_gpu_scatter_many_buffers(engine, oracle, nbuf, lo, hi):
     """One hdfs_crc32c_read_packets call over many device buffers (the
