@@ -257,6 +257,7 @@ struct DevCtx {
   uint32_t grid_seq = 0;
   // short device runs (small_run_kernel): device scratch + pinned host area
   uint8_t *sr_h = nullptr, *sr_hd = nullptr;
+  uint8_t *sr2_h = nullptr, *sr2_hd = nullptr;  // the rest of a stream, launched under a speculative verify
   hipStream_t r_stream = nullptr;  // device framing: record copies of runs with many exceptions
   std::vector<GridSlot> grid;
   // speculative one-launch verify (spec_verify_kernel; guarded by mu): the

@@ -590,20 +590,53 @@ int reserve_grid(DevCtx &c, size_t si, const GridLayout &L) {
 // resolved only when the read is decided inside what was framed -- the
 // destination fills there, or a packet ends the read (read_stopper).
 bool read_window_over(const hdfs_crc32c_packet *p, size_t n, const CopyOut &co, const uint32_t *idx, size_t nidx);
+// One short-run launch in flight: its pinned slot set (the synchronous
+// calls' c.sr_h, or c.sr2_h for the rest of a stream launched under a
+// speculative verify), sequence number, grid points and the epoch read
+// before the launch.
+struct SrLaunch {
+  uint8_t *h = nullptr;
+  uint32_t seq = 0, count = 0;
+  uint64_t epoch = 0;
+};
+
+int sr_launch(DevCtx &c, bool second, const uint8_t *d, uint64_t len, int proto, uint32_t cs, int ctype, bool verify,
+              const CopyOut &co, size_t max_pkts, SrLaunch &L) {
+  uint8_t *&h = second ? c.sr2_h : c.sr_h;
+  uint8_t *&hd = second ? c.sr2_hd : c.sr_hd;
+  if (!h) {
+    HIPCHK(hipHostMalloc(&h, kSrHostBytes, hipHostMallocCoherent | hipHostMallocMapped));
+    std::memset(h, 0, kSrHostBytes);
+    HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&hd), h, 0));
+  }
+  L.h = h;
+  L.count = uint32_t(std::min<uint64_t>({uint64_t(kSmallRunMax), uint64_t(max_pkts), len / 6 + 1}));
+  L.seq = next_grid_seq(c);
+  const int tset = ctype == HDFS_CRC32C_CSUM_CRC32 ? 1 : 0;
+  L.epoch = c.queued_epoch.load(std::memory_order_acquire);  // before the launch
+  HIPCHK(launch_small_run(d, len, L.count, proto, cs, ctype, verify ? 1 : 0, c.d_tab_main_t[tset], c.d_tab_pow2_t[tset],
+                          co.dst, co.cap, co.win ? 1 : 0, co.client_offset, hd, L.seq, c.stream));
+  return HDFS_CRC32C_OK;
+}
+
+// Waits for a short-run launch and turns its slots into records; 0 when the
+// walk does not end inside it (the caller frames the stream instead).
+int sr_collect(DevCtx &c, const SrLaunch &L, uint64_t len, const CopyOut &co, size_t max_pkts,
+               hdfs_crc32c_packet *dst, size_t *nout, uint64_t *consumed, uint64_t *payload, bool truncated = false);
+
 int small_run(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs, int ctype, bool verify,
               const CopyOut &co, size_t max_pkts, hdfs_crc32c_packet *dst, size_t *nout, uint64_t *consumed,
               uint64_t *payload, bool truncated = false) {
-  if (!c.sr_h) {
-    HIPCHK(hipHostMalloc(&c.sr_h, kSrHostBytes, hipHostMallocCoherent | hipHostMallocMapped));
-    std::memset(c.sr_h, 0, kSrHostBytes);
-    HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&c.sr_hd), c.sr_h, 0));
-  }
-  const uint32_t count = uint32_t(std::min<uint64_t>({uint64_t(kSmallRunMax), uint64_t(max_pkts), len / 6 + 1}));
-  const uint32_t seq = next_grid_seq(c);
-  const int tset = ctype == HDFS_CRC32C_CSUM_CRC32 ? 1 : 0;
-  const uint64_t epoch = c.queued_epoch.load(std::memory_order_acquire);  // before the launch
-  HIPCHK(launch_small_run(d, len, count, proto, cs, ctype, verify ? 1 : 0, c.d_tab_main_t[tset], c.d_tab_pow2_t[tset],
-                          co.dst, co.cap, co.win ? 1 : 0, co.client_offset, c.sr_hd, seq, c.stream));
+  SrLaunch L;
+  const int rc = sr_launch(c, false, d, len, proto, cs, ctype, verify, co, max_pkts, L);
+  if (rc) return rc;
+  return sr_collect(c, L, len, co, max_pkts, dst, nout, consumed, payload, truncated);
+}
+
+int sr_collect(DevCtx &c, const SrLaunch &L, uint64_t len, const CopyOut &co, size_t max_pkts,
+               hdfs_crc32c_packet *dst, size_t *nout, uint64_t *consumed, uint64_t *payload, bool truncated) {
+  const uint32_t count = L.count, seq = L.seq;
+  const uint64_t epoch = L.epoch;
   // a fault of earlier work on the stream is this call's error, not the next
   // caller's: queried while the kernel is in flight when unconfirmed work
   // is queued before it (as small_call)
@@ -613,7 +646,7 @@ int small_run(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
       return fail(HDFS_CRC32C_EHIP, "earlier work on the stream: %s", hipGetErrorString(q));
   }
   auto word = [&](uint32_t k, int i) -> const uint32_t * {
-    return reinterpret_cast<const uint32_t *>(c.sr_h + size_t(k) * kSrSlot + kGridRecBytes) + i;
+    return reinterpret_cast<const uint32_t *>(L.h + size_t(k) * kSrSlot + kGridRecBytes) + i;
   };
   using clk = std::chrono::steady_clock;
   const auto t0 = clk::now();
@@ -636,7 +669,7 @@ int small_run(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
   // the run: grid points up to the first that is not On (grid_build_kernel's rule)
   auto rec = [&](uint32_t k) {
     hdfs_crc32c_packet r;
-    std::memcpy(&r, c.sr_h + size_t(k) * kSrSlot, sizeof(r));
+    std::memcpy(&r, L.h + size_t(k) * kSrSlot, sizeof(r));
     return r;
   };
   uint32_t fbk = count, unsup = 0;
@@ -844,6 +877,9 @@ struct EarlyHook {
   std::function<void(const hdfs_crc32c_packet *recs, uint32_t count)> fn;
 };
 thread_local const EarlyHook *t_early_hook = nullptr;
+// grid_walk's own: the short rest of a verified stream launched at the early
+// block (E.count, E.stride), queued behind the speculative kernel
+thread_local const std::function<void(uint32_t count, uint64_t stride)> *t_tail_hook = nullptr;
 
 int spec_collect(DevCtx &c, SpecSlot &S, const SpecLaunch &L, const CopyOut &co, hdfs_crc32c_packet *dst,
                  SpecResult &res) {
@@ -871,6 +907,7 @@ int spec_collect(DevCtx &c, SpecSlot &S, const SpecLaunch &L, const CopyOut &co,
     r.seqno = r0.seqno + int64_t(k);
   }
   if (t_early_hook && pos == 0) t_early_hook->fn(dst, E.count);
+  if (t_tail_hook) (*t_tail_hook)(E.count, E.stride);
   const auto t3 = clk::now();
   if ((rc = poll_seq(&fin->seq, L.seq, "speculative verify", L.st))) return rc;
   if (g_dstream_trace) {  // diagnostic: where a speculative launch spends its time (us)
@@ -1212,9 +1249,42 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
     }
     if (try_spec && left > kSmallRunBytes) {
       SpecResult sr;
-      if ((rc = spec_pass(c, d, len, pos, count, proto, cs, ctype, co, done_b, dg + L.bm,
-                          reinterpret_cast<uint32_t *>(dg + L.fb), dst + n, sr)))
-        break;
+      // a verify (no read window, no copy): when the stream's rest after the
+      // run is short -- a block's short last packet and the empty end packet
+      // -- its short-run launch is queued behind the speculative kernel as
+      // soon as the early block sizes the run, so it runs without a host
+      // round trip in between
+      SrLaunch tl;
+      uint64_t tail_at = 0;
+      const std::function<void(uint32_t, uint64_t)> tail_fn = [&](uint32_t cnt, uint64_t stride) {
+        const uint64_t at = pos + uint64_t(cnt) * stride;
+        const size_t room = max_pkts - n > cnt ? max_pkts - n - cnt : 0;
+        if (at >= len || len - at > kSmallRunBytes || !room || !g_tail_small) return;
+        if (sr_launch(c, true, d + at, len - at, proto, cs, ctype, verify, CopyOut{}, room, tl) == 0) tail_at = at;
+      };
+      if (!co.dst && !co.win) t_tail_hook = &tail_fn;
+      rc = spec_pass(c, d, len, pos, count, proto, cs, ctype, co, done_b, dg + L.bm,
+                     reinterpret_cast<uint32_t *>(dg + L.fb), dst + n, sr);
+      t_tail_hook = nullptr;
+      // the queued rest: taken when the walk goes on exactly there, else
+      // waited for and dropped
+      size_t nt = 0;
+      uint64_t used_t = 0, pay_t = 0;
+      int got_tail = 0;
+      if (tail_at) {
+        const bool usable = !rc && sr.taken && !sr.end && sr.next == tail_at;
+        std::vector<hdfs_crc32c_packet> scratch;
+        hdfs_crc32c_packet *to = dst + n + sr.recorded;
+        if (!usable) {
+          scratch.resize(tl.count);
+          to = scratch.data();
+        }
+        const size_t room = usable ? max_pkts - n - sr.recorded : tl.count;
+        const int r2 = sr_collect(c, tl, len - tail_at, CopyOut{}, room, to, &nt, &used_t, &pay_t);
+        if (r2 < 0 && !rc) rc = r2;
+        got_tail = usable && r2 == 1 ? 1 : 0;
+      }
+      if (rc) break;
       if (sr.taken) {
         if (co.dst && !co.win && payload + sr.payload > co.cap) {
           rc = fail(HDFS_CRC32C_EINVAL, "copy-out buffer of %llu bytes is too small (%llu needed so far)",
@@ -1228,6 +1298,13 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
         *consumed = sr.consumed;
         last_spec = true;
         if (sr.end || read_over) break;
+        if (got_tail) {  // the rest, verified behind the run
+          for (size_t k = 0; k < nt; k++) dst[n + k].stream_off += tail_at;
+          n += nt;
+          payload += pay_t;
+          *consumed = tail_at + used_t;
+          break;
+        }
         pos = sr.next;
         continue;
       }
