@@ -280,6 +280,11 @@ struct DevCtx {
   // and its stream (guarded by mu)
   CopyCtl cp_beside;
   hipStream_t cp_stream = nullptr;
+  // held by a scatter read from before its verify until its copy beside the
+  // verify has completed (one such copy in flight per device: its table and
+  // completion word are rewritten by the next); taken before mu, try-locked
+  // (a concurrent scatter read copies after its verify instead)
+  std::mutex beside_mu;
   // readers' copy state, kept for the next reader (a free would synchronise
   // the device, which waits for an open mailbox to idle out)
   std::vector<CopyCtl> cp_pool;

@@ -2387,8 +2387,9 @@ int read_dev_scatter(int dev, const uint8_t *s, uint64_t len, int proto, uint32_
   Pieces pred;
   uint32_t pred_seq = 0;
   int pred_rc = 0;
+  std::unique_lock<std::mutex> beside(c.beside_mu, std::try_to_lock);
   EarlyHook hook{[&](const hdfs_crc32c_packet *recs, uint32_t count) {
-    if (count < kBesideMinPackets || pred_seq) return;
+    if (count < kBesideMinPackets || pred_seq || !beside.owns_lock()) return;
     std::vector<hdfs_crc32c_packet> tmp(recs, recs + count);
     size_t nn = count;
     uint64_t u = 0, gp = 0;
@@ -2409,6 +2410,7 @@ int read_dev_scatter(int dev, const uint8_t *s, uint64_t len, int proto, uint32_
     const int r = poll_seq(c.cp_beside.hdone, pred_seq, "read delivery beside the verify", c.cp_stream);
     if (r) return r;
   }
+  if (beside.owns_lock()) beside.unlock();
   if (rc < 0) return rc;
   if (pred_rc < 0) return pred_rc;
   // what the prediction copied: the pieces both agree on, in order

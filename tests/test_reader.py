@@ -465,3 +465,54 @@ def test_gpu_readers_threads(engine, oracle):
     assert not errors, errors
     for b, _ in bufs:
         b.free()
+
+
+@pytest.mark.gpu
+def test_gpu_scatter_threads(engine, oracle):
+    """Scatter reads of long runs from three threads at once: one copy
+    beside a verify is in flight per device (the others copy after their
+    verify), and every read equals the oracle's."""
+    import threading
+    dl = [65536] * 1100 + [4321]
+    streams = [build_stream(oracle.crc32c, 2, 512, CSUM_CRC32C, dl, seed=300 + i,
+                            corrupt=[(900, 1)] if i == 1 else [])[0] for i in range(3)]
+    bufs = [_dev(engine, st, i) for i, st in enumerate(streams)]
+    sizes = [16 << 20] * 4 + [54321] * 5
+    cap = sum(sizes)
+    errors = []
+
+    def worker(i):
+        try:
+            st, (_, p) = streams[i], bufs[i]
+            for co in (0, 1234567):
+                rl = sum(dl) - co
+                want = oracle.read_packets(st, co, rl, cap=cap)
+                iov, off = [], 0
+                for n in sizes:
+                    iov.append((off, n))
+                    off += n + 16
+                big = engine.DeviceBuffer(off + 64)
+                big.fill(0xA5)
+                rc, recs, used, got = engine.read_packets(p, len(st), None, 0, client_offset=co, read_len=rl,
+                                                          iov=[(big.ptr + a, n) for a, n in iov])
+                flat = big.download(off).tobytes()
+                big.free()
+                data, left = b"", got
+                for a, n in iov:
+                    take = min(n, left)
+                    data += flat[a:a + take]
+                    left -= take
+                    assert flat[a + n:a + n + 16] == b"\xa5" * 16
+                assert (rc, recs, used) == want[:3] and data == want[3], (i, co)
+        except Exception as e:  # noqa: BLE001 -- reported by the main thread
+            errors.append((i, repr(e)))
+
+    th = [threading.Thread(target=worker, args=(i,)) for i in range(3)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=240)
+    assert not any(t.is_alive() for t in th)
+    assert not errors, errors
+    for b, _ in bufs:
+        b.free()
