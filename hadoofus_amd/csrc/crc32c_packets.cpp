@@ -1259,7 +1259,9 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
       const std::function<void(uint32_t, uint64_t)> tail_fn = [&](uint32_t cnt, uint64_t stride) {
         const uint64_t at = pos + uint64_t(cnt) * stride;
         const size_t room = max_pkts - n > cnt ? max_pkts - n - cnt : 0;
-        if (at >= len || len - at > kSmallRunBytes || !room || !g_tail_small) return;
+        // (a rest within one header window is one packet the kernel frames
+        // itself -- the empty end packet of a block -- and needs no launch)
+        if (at >= len || len - at <= kHdrWin || len - at > kSmallRunBytes || !room || !g_tail_small) return;
         if (sr_launch(c, true, d + at, len - at, proto, cs, ctype, verify, CopyOut{}, room, tl) == 0) tail_at = at;
       };
       if (!co.dst && !co.win) t_tail_hook = &tail_fn;
