@@ -3,9 +3,11 @@ diagnostic build): copy_pieces_kernel stamps s_memrealtime (100 MHz) per
 workgroup -- 0 entry, 1 first piece-table entries staged (table launches),
 2 its stores acknowledged, 3 counted done -- when a stamp buffer is set
 (Diag.set_tuning(2, ptr)).  Runs a 128 MiB block of 64 KiB packets in device
-memory read in ONE hdfs_crc32c_read_packets call over 64 device buffers (the
-verify, then one table launch of ~2 100 pieces), and prints per phase
-[min, median, max] microseconds from the earliest workgroup's entry.
+memory through a reader (verified at open) delivered by ONE
+hdfs_crc32c_reader_next into one device buffer: one table launch of 2 048
+pieces (a scatter read copies beside its verify with copy_beside_kernel
+instead, which has no stamps).  Prints per phase [min, median, max]
+microseconds from the earliest workgroup's entry.
 
     python tools/copy_phases.py [out.json]"""
 import ctypes
@@ -38,17 +40,20 @@ def main():
     st = h.DeviceBuffer((OFF + NBLK * 4) * 8)
     arr = (h.abi.Packet * (npk + 8))()
     cnt, used, got = ctypes.c_size_t(0), ctypes.c_uint64(0), ctypes.c_uint64(0)
-    sl = payload // 64
-    vec = (h.abi.IoVec * 64)(*[h.abi.IoVec(dst.ptr + k * sl, sl) for k in range(64)])
+    vec = (h.abi.IoVec * 1)(h.abi.IoVec(dst.ptr, payload))
     runs = []
     for rep in range(5):
+        rd = ctypes.c_void_p()
+        assert lib.hdfs_crc32c_reader_open(d.ptr, img.nbytes, h.PROTO_V2, 512, h.CSUM_CRC32C, 0, payload, npk + 8,
+                                           ctypes.byref(rd)) == 0
         st.fill(0)
         h.device_sync()
         D.set_tuning(2, st.ptr if rep else None)
         t = time.perf_counter()
-        rc = lib.hdfs_crc32c_read_packets(d.ptr, img.nbytes, h.PROTO_V2, 512, h.CSUM_CRC32C, 0, payload, vec, 64,
-                                          arr, npk + 8, ctypes.byref(cnt), ctypes.byref(used), ctypes.byref(got))
+        rc = lib.hdfs_crc32c_reader_next(rd, vec, 1, arr, npk + 8, ctypes.byref(cnt), ctypes.byref(used),
+                                         ctypes.byref(got))
         wall = (time.perf_counter() - t) * 1e6
+        lib.hdfs_crc32c_reader_close(rd)
         assert rc >= 0 and got.value == payload, (rc, got.value)
         h.device_sync()
         if not rep:
