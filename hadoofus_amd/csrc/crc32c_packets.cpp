@@ -1249,11 +1249,11 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
     }
     if (try_spec && left > kSmallRunBytes) {
       SpecResult sr;
-      // a verify (no read window, no copy): when the stream's rest after the
-      // run is short -- a block's short last packet and the empty end packet
-      // -- its short-run launch is queued behind the speculative kernel as
-      // soon as the early block sizes the run, so it runs without a host
-      // round trip in between
+      // a verify (no copy-out; a read window is applied to the records
+      // afterwards): when the stream's rest after the run is short -- a
+      // block's short last packet and the empty end packet -- its short-run
+      // launch is queued behind the speculative kernel as soon as the early
+      // block sizes the run, so it runs without a host round trip in between
       SrLaunch tl;
       uint64_t tail_at = 0;
       const std::function<void(uint32_t, uint64_t)> tail_fn = [&](uint32_t cnt, uint64_t stride) {
@@ -1264,7 +1264,7 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
         if (at >= len || len - at <= kHdrWin || len - at > kSmallRunBytes || !room || !g_tail_small) return;
         if (sr_launch(c, true, d + at, len - at, proto, cs, ctype, verify, CopyOut{}, room, tl) == 0) tail_at = at;
       };
-      if (!co.dst && !co.win) t_tail_hook = &tail_fn;
+      if (!co.dst) t_tail_hook = &tail_fn;  // (a window without copy-out: the host applies it to the records after)
       rc = spec_pass(c, d, len, pos, count, proto, cs, ctype, co, done_b, dg + L.bm,
                      reinterpret_cast<uint32_t *>(dg + L.fb), dst + n, sr);
       t_tail_hook = nullptr;
