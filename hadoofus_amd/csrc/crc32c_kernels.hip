@@ -3427,39 +3427,46 @@ __global__ __launch_bounds__(1024) void spec_verify_kernel(SpecArgs a) {
   stores_done();
   __syncthreads();
   stamp(3);
-  if (t == 0) {
+  if (t < 64u) {
+    // wave 0: lane 0 counts the workgroup done; in the last workgroup the
+    // wave copies the counters, exceptions and run tails to the host area one
+    // dword per lane -- every load in flight at once instead of a chain of
+    // dependent agent-scope round trips (~2.6 us of the block's end) -- and
+    // lane 0 publishes the sequence number after the wave's stores
     SpecCtl *const c = ep_ctl;
-    const uint32_t n = __hip_atomic_fetch_add(&c->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t n = 0;
+    if (lane == 0) n = __hip_atomic_fetch_add(&c->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    n = static_cast<uint32_t>(__shfl(static_cast<int>(n), 0));
     if (n == gridDim.x - 1u) {
-      auto *f = reinterpret_cast<SpecFinal *>(ep_hout + sizeof(SpecEarly));
-      f->mism = at_ld(reinterpret_cast<const uint64_t *>(&c->mism));
-      f->exc = static_cast<uint32_t>(__hip_atomic_load(&c->exc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      f->tail_status =
-          static_cast<uint32_t>(__hip_atomic_load(&c->tail_status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      f->tail_total = at_ld(&c->tail_total);
-#pragma unroll
-      for (int q = 0; q < 7; q++) f->tail[q] = at_ld(&c->tail[q]);
-      const uint32_t nexc =
-          static_cast<uint32_t>(__hip_atomic_load(&c->nexc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      f->nexc = nexc;
-      const SpecExc *x = ep_exc;
-      SpecExc *hx = reinterpret_cast<SpecExc *>(ep_hout + 256);
-      for (uint32_t j = 0; j < min(nexc, kSpecExcMax); j++) {
-#pragma unroll
-        for (int q = 0; q < 7; q++) hx[j].rec[q] = at_ld(&x[j].rec[q]);
-        hx[j].k = static_cast<uint32_t>(__hip_atomic_load(&x[j].k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      }
-      const SpecRunTail *xt = ep_xtail;
-      auto *ht = reinterpret_cast<SpecRunTail *>(ep_hout + kSpecRunTailOff);
-      for (uint32_t r = 1; xt && r < ep_nruns; r++) {
-#pragma unroll
-        for (int q = 0; q < 7; q++) ht[r].rec[q] = at_ld(&xt[r].rec[q]);
-        ht[r].total = at_ld(&xt[r].total);
-        ht[r].status =
-            static_cast<uint32_t>(__hip_atomic_load(&xt[r].status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      // SpecFinal dword j <- SpecCtl dword: mism 0-1, exc 4, tail_status 5,
+      // tail_total 6-7, tail 8-21, nexc 22 (dword 20 is the sequence number)
+      static_assert(offsetof(SpecCtl, exc) == 16 && offsetof(SpecCtl, tail_total) == 24 &&
+                        offsetof(SpecCtl, tail) == 32 && offsetof(SpecCtl, nexc) == 88 &&
+                        offsetof(SpecFinal, exc) == 8 && offsetof(SpecFinal, tail_total) == 16 &&
+                        offsetof(SpecFinal, tail) == 24 && offsetof(SpecFinal, seq) == 80 &&
+                        offsetof(SpecFinal, nexc) == 84,
+                    "the final block's dword map");
+      const uint32_t src = lane < 2u ? lane : lane < 20u ? lane + 2u : 22u;
+      uint32_t v = 0;
+      if (lane < 22u && lane != 20u)
+        v = __hip_atomic_load(reinterpret_cast<const uint32_t *>(c) + src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      auto *f = reinterpret_cast<uint32_t *>(ep_hout + sizeof(SpecEarly));
+      if (lane < 22u && lane != 20u) f[lane] = v;
+      const uint32_t nexc = static_cast<uint32_t>(__shfl(static_cast<int>(v), 21));
+      const uint32_t nxd = min(nexc, kSpecExcMax) * uint32_t(sizeof(SpecExc) / 4u);
+      const auto *xs = reinterpret_cast<const uint32_t *>(ep_exc);
+      auto *xd = reinterpret_cast<uint32_t *>(ep_hout + 256);
+      for (uint32_t q = lane; q < nxd; q += 64u)
+        xd[q] = __hip_atomic_load(xs + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (ep_xtail) {  // run r >= 1's tail (SpecRunTail r)
+        constexpr uint32_t kW = uint32_t(sizeof(SpecRunTail) / 4u);
+        const auto *ts = reinterpret_cast<const uint32_t *>(ep_xtail);
+        auto *td = reinterpret_cast<uint32_t *>(ep_hout + kSpecRunTailOff);
+        for (uint32_t q = kW + lane; q < kW * ep_nruns; q += 64u)
+          td[q] = __hip_atomic_load(ts + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       __threadfence_system();
-      __hip_atomic_store(&f->seq, ep_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (lane == 0) __hip_atomic_store(&f[20], ep_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       stamp(4);
     }
   }
