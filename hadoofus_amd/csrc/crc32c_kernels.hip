@@ -311,7 +311,10 @@ constexpr uint32_t kSlots = 8;  // LDS slots for published units
 #endif
 static_assert((HDFS_GATHER_SLOTS & (HDFS_GATHER_SLOTS - 1)) == 0, "gather slots: a power of two");
 constexpr uint32_t kGatherSlots = HDFS_GATHER_SLOTS, kGatherWords = kGatherSlots * 65;
-constexpr uint64_t kPhase1Num = 23, kPhase1Den = 25;  // 92 % static
+#ifndef HDFS_PHASE1_NUM  // A/B builds only (-DHDFS_PHASE1_NUM=n)
+#define HDFS_PHASE1_NUM 23
+#endif
+constexpr uint64_t kPhase1Num = HDFS_PHASE1_NUM, kPhase1Den = 25;  // 92 % static
 
 struct Sched {
   uint64_t r1;       // ORDER 0: end of the wave's round slice
