@@ -112,6 +112,11 @@ int g_spec = HDFS_KNOB("HDFS_CRC32C_SPEC", 1);
 int g_stage_vram = HDFS_KNOB("HDFS_CRC32C_MB_STAGE", 1);
 // Mailbox timing experiments (diagnostic build only; see mailbox_kernel).
 int g_mb_exp = HDFS_KNOB("HDFS_CRC32C_MB_EXP", 0);
+// The resident kernel's stream: 1 a high-priority stream (a hardware queue
+// of its own), 0 a normal one (diagnostic: it then shares one of the
+// process's GPU_MAX_HW_QUEUES queues with other streams, and every dispatch
+// queued behind it there waits for its idle exit)
+int g_mb_queue = HDFS_KNOB("HDFS_CRC32C_MB_QUEUE", 1);
 // Diagnostic per-wave timestamps (device buffer, 3 x u64 per wave) or null.
 unsigned long long *g_diag = nullptr;
 
@@ -1502,7 +1507,21 @@ int hdfs_crc32c_mailbox_create(hdfs_crc32c_mailbox **mb, uint32_t idle_ms) {
     }
     c->mb_posted = 0;
   }
-  if (!c->mb_stream) HIPCHK(hipStreamCreateWithFlags(&c->mb_stream, hipStreamNonBlocking));
+  if (!c->mb_stream) {
+    // A persistent kernel must not share a hardware queue: the runtime maps
+    // a process's normal-priority streams onto at most GPU_MAX_HW_QUEUES
+    // (4) queues, and a dispatch queued behind the resident kernel on its
+    // queue -- a verify on c.stream, say -- waits for its idle exit (50 ms:
+    // measured as a 50 ms stall per reader in some processes).  High-priority
+    // streams come from a queue pool of their own, where the mailbox is the
+    // only one.
+    int lo = 0, hi = 0;
+    if (g_mb_queue && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess && hi != lo) {
+      HIPCHK(hipStreamCreateWithPriority(&c->mb_stream, hipStreamNonBlocking, hi));
+    } else {
+      HIPCHK(hipStreamCreateWithFlags(&c->mb_stream, hipStreamNonBlocking));
+    }
+  }
   const uint64_t ms = idle_ms ? idle_ms : 50u;
   c->mb_idle_ticks = uint32_t(std::min<uint64_t>(ms * 100000u, 0xFFFFFFFFu));  // s_memrealtime: 100 MHz
   c->mb_calls = c->mb_launches = 0;
