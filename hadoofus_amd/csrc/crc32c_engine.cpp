@@ -96,6 +96,9 @@ int g_copy_dev_tab = HDFS_KNOB("HDFS_CRC32C_COPY_DEV_TAB", 1);
 // What follows a taken run, when short, in one short-run launch (1) or a
 // framing pass (0, diagnostic A/B).
 int g_tail_small = HDFS_KNOB("HDFS_CRC32C_TAIL_SMALL", 1);
+// the rest queued under a speculative verify: on its own stream (1) or
+// behind the kernel on the call's stream (0)
+int g_tail_stream = HDFS_KNOB("HDFS_CRC32C_TAIL_STREAM", 1);
 uint64_t g_mb_copy_max = uint64_t(HDFS_KNOB("HDFS_CRC32C_MB_COPY_MAX", 96 << 10));
 // Compute-mode CRC stores: 2 (product) schedule 3 with the LDS group gather
 // (one 256-B store per 8-tile group); diagnostic build only: 1 schedule 4
@@ -183,6 +186,13 @@ int ctx_init(int device, DevCtx **out) {
   // Blocking stream: it serialises with the legacy NULL stream, so the
   // synchronous helpers (hipMemcpy/hipMemset) see prior plan work.
   HIPCHK(hipStreamCreate(&c.stream));
+  // the short rest of a verified stream runs beside the speculative kernel
+  // on t_stream.  Created right after c.stream: the runtime spreads a
+  // process's streams over at most GPU_MAX_HW_QUEUES hardware queues, and two
+  // streams created one after the other land on different ones (created
+  // later, it shared c.stream's queue in a process with more streams and
+  // waited behind the kernel again)
+  HIPCHK(hipStreamCreateWithFlags(&c.t_stream, hipStreamNonBlocking));
   HIPCHK(hipHostMalloc(&c.h_stage, kStageCap, hipHostMallocDefault));
   HIPCHK(hipMalloc(&c.d_stage, kStageCap));
   HIPCHK(hipMalloc(&c.d_seg, sizeof(SegDev)));

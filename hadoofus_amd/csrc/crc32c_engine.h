@@ -258,6 +258,9 @@ struct DevCtx {
   // short device runs (small_run_kernel): device scratch + pinned host area
   uint8_t *sr_h = nullptr, *sr_hd = nullptr;
   uint8_t *sr2_h = nullptr, *sr2_hd = nullptr;  // the rest of a stream, launched under a speculative verify
+  // its stream: beside the speculative kernel, so it starts on the first CU
+  // that kernel frees instead of after its last workgroup
+  hipStream_t t_stream = nullptr;
   hipStream_t r_stream = nullptr;  // device framing: record copies of runs with many exceptions
   std::vector<GridSlot> grid;
   // speculative one-launch verify (spec_verify_kernel; guarded by mu): the
@@ -379,6 +382,7 @@ int mailbox_copy(DevCtx &c, const CopyEntry *e, uint32_t n);
 extern uint64_t g_mb_copy_max;
 // the short rest of a stream after a taken run: one short-run launch
 extern int g_tail_small;
+extern int g_tail_stream;
 
 // One-launch path for synchronous calls on <= kSmallMax bytes
 // (small_chunks_kernel or the open mailbox; caller holds c.mu and has staged

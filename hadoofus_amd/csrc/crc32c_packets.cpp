@@ -598,10 +598,11 @@ struct SrLaunch {
   uint8_t *h = nullptr;
   uint32_t seq = 0, count = 0;
   uint64_t epoch = 0;
+  hipStream_t st = nullptr;  // the stream it was queued on
 };
 
 int sr_launch(DevCtx &c, bool second, const uint8_t *d, uint64_t len, int proto, uint32_t cs, int ctype, bool verify,
-              const CopyOut &co, size_t max_pkts, SrLaunch &L) {
+              const CopyOut &co, size_t max_pkts, SrLaunch &L, hipStream_t st = nullptr) {
   uint8_t *&h = second ? c.sr2_h : c.sr_h;
   uint8_t *&hd = second ? c.sr2_hd : c.sr_hd;
   if (!h) {
@@ -614,8 +615,9 @@ int sr_launch(DevCtx &c, bool second, const uint8_t *d, uint64_t len, int proto,
   L.seq = next_grid_seq(c);
   const int tset = ctype == HDFS_CRC32C_CSUM_CRC32 ? 1 : 0;
   L.epoch = c.queued_epoch.load(std::memory_order_acquire);  // before the launch
+  L.st = st ? st : c.stream;
   HIPCHK(launch_small_run(d, len, L.count, proto, cs, ctype, verify ? 1 : 0, c.d_tab_main_t[tset], c.d_tab_pow2_t[tset],
-                          co.dst, co.cap, co.win ? 1 : 0, co.client_offset, hd, L.seq, c.stream));
+                          co.dst, co.cap, co.win ? 1 : 0, co.client_offset, hd, L.seq, L.st));
   return HDFS_CRC32C_OK;
 }
 
@@ -653,7 +655,7 @@ int sr_collect(DevCtx &c, const SrLaunch &L, uint64_t len, const CopyOut &co, si
   for (uint32_t k = 0; k < count; k++) {
     for (uint32_t spin = 1; __atomic_load_n(word(k, 3), __ATOMIC_ACQUIRE) != seq; spin++) {
       if ((spin & 4095u) == 0 && clk::now() - t0 > std::chrono::milliseconds(200)) {
-        HIPCHK(hipStreamSynchronize(c.stream));
+        HIPCHK(hipStreamSynchronize(L.st));
         if (__atomic_load_n(word(k, 3), __ATOMIC_ACQUIRE) != seq) return fail(HDFS_CRC32C_EHIP, "short-run kernel");
         break;
       }
@@ -664,8 +666,8 @@ int sr_collect(DevCtx &c, const SrLaunch &L, uint64_t len, const CopyOut &co, si
   }
   // every slot is published (each workgroup's sequence word is its last
   // memory operation, so a fault of this launch cannot be followed by it;
-  // and everything queued before the launch has completed)
-  c.confirm(epoch);
+  // and, on c.stream, everything queued before the launch has completed)
+  if (L.st == c.stream) c.confirm(epoch);
   // the run: grid points up to the first that is not On (grid_build_kernel's rule)
   auto rec = [&](uint32_t k) {
     hdfs_crc32c_packet r;
@@ -1279,7 +1281,11 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
         // (a rest within one header window is one packet the kernel frames
         // itself -- the empty end packet of a block -- and needs no launch)
         if (at >= len || len - at <= kHdrWin || len - at > kSmallRunBytes || !room || !g_tail_small) return;
-        if (sr_launch(c, true, d + at, len - at, proto, cs, ctype, verify, CopyOut{}, room, tl) == 0) tail_at = at;
+        // (on its own stream: the kernel's early block means every command
+        // queued before it has run, so the rest's bytes are as ready as the
+        // run's; it starts on the first CU the speculative kernel frees)
+        hipStream_t ts = g_tail_stream ? c.t_stream : nullptr;
+        if (sr_launch(c, true, d + at, len - at, proto, cs, ctype, verify, CopyOut{}, room, tl, ts) == 0) tail_at = at;
       };
       if (!co.dst) t_tail_hook = &tail_fn;  // (a window without copy-out: the host applies it to the records after)
       rc = spec_pass(c, d, len, pos, count, proto, cs, ctype, co, done_b, dg + L.bm,

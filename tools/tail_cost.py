@@ -36,7 +36,8 @@ def main():
     H = pk[0]["hdr_len"]
     tail = np.concatenate([hb[:H], data[:12345], hb[H:]])
     blk_e, nblk = dsb.wire_image(128 << 20, 9, empty_last=True)
-    out = {"tail_small": os.environ.get("HDFS_CRC32C_TAIL_SMALL", "1")}
+    out = {"tail_small": os.environ.get("HDFS_CRC32C_TAIL_SMALL", "1"),
+           "tail_stream": os.environ.get("HDFS_CRC32C_TAIL_STREAM", "1")}
     for name, im in (("block_empty_end", blk_e), ("block_short_last_packet", np.concatenate([img, tail]))):
         dev = h.DeviceBuffer(im.nbytes + 64)
         dev.upload(im)
