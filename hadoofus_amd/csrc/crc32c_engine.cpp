@@ -193,6 +193,8 @@ int ctx_init(int device, DevCtx **out) {
   // later, it shared c.stream's queue in a process with more streams and
   // waited behind the kernel again)
   HIPCHK(hipStreamCreateWithFlags(&c.t_stream, hipStreamNonBlocking));
+  // (and a scatter read's copy beside the same kernel, for the same reason)
+  HIPCHK(hipStreamCreateWithFlags(&c.cp_stream, hipStreamNonBlocking));
   HIPCHK(hipHostMalloc(&c.h_stage, kStageCap, hipHostMallocDefault));
   HIPCHK(hipMalloc(&c.d_stage, kStageCap));
   HIPCHK(hipMalloc(&c.d_seg, sizeof(SegDev)));
