@@ -462,8 +462,10 @@ int hdfs_crc32c_host_free(void *p);
  * line in pinned memory -- no kernel launch per call.  Other calls keep
  * their one-launch path.  The resident kernel exits on its own after idle_ms
  * without a request (0: 50 ms; the next call relaunches it) and on destroy.
- * While a mailbox is open the engine's bulk kernels use one CU fewer, and a
- * device-wide synchronisation (hipDeviceSynchronize, torch.cuda.synchronize)
+ * While a mailbox is open the engine's bulk kernels leave one CU per XCD to
+ * it.  The resident kernel runs on a high-priority stream, a hardware queue
+ * of its own (on a queue shared with other streams, work queued behind it
+ * would wait for its idle exit).  A device-wide synchronisation (hipDeviceSynchronize, torch.cuda.synchronize)
  * waits for the resident kernel's idle exit: synchronise streams instead.
  * The same holds for calls that free or re-allocate device or pinned memory
  * (hdfs_crc32c_dev_free, hdfs_crc32c_host_free, and an engine call whose
