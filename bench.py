@@ -11,6 +11,12 @@ src/datanode.c:2931-2963, over every chunk of every block).
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3|C4]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
 
+`python bench.py --gpus N` (N > 1) outside torchrun starts
+torch.distributed.run with N ranks as a child process (before any GPU
+call) and exits with its code; under torchrun, --gpus must equal
+WORLD_SIZE or the run is refused.  At N > 1 the C3 line is weak scaling
+(1024 blocks per GPU) and extra.c4_strong times BASELINE's C4 split.
+
 --config C3 (default, the headline): 1024 blocks (128 GiB) per GPU, weak
 scaling.  --config C4: 512 blocks (64 GiB) for the whole node split evenly
 over the ranks (BASELINE.json configs[3]), strong scaling.  Ranks shard
@@ -41,6 +47,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+METRIC = "CRC32C verify GiB/s (device-resident), 512B chunks over 128MiB HDFS blocks"
 BLOCK = 128 << 20
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 MOD, BITMUL = 65537, 7919  # SURVEY.md 8d corruption pattern
@@ -50,9 +57,13 @@ DIGESTS = os.path.join(ROOT, "tests", "golden", "block_digests_all.npz")
 PINNED = {(0, 512): 0xF2590C08}
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks, one per GPU (default: WORLD_SIZE under torchrun, else 1); without torchrun, "
+                         "N > 1 starts torch.distributed.run as a child process")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="rank plumbing only: gloo, no device work (the launcher's CPU test)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", choices=("C3", "C4"), default="C3")
@@ -62,7 +73,63 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-extra", action="store_true", help="skip C2/C5/ceiling side measurements")
     ap.add_argument("--cpu-gib", type=float, default=4.0, help="CPU baseline sample size (GiB)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` without torchrun: run N ranks, one per GPU, as
+    `python -m torch.distributed.run --nproc-per-node N bench.py <argv>` in a
+    CHILD process (never exec: the caller may be a profiler's process) and
+    return its exit code.  Called before anything imports torch or touches a
+    GPU; the ranks' stdout (rank 0's JSON line) is this process's stdout."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this driver
+    return subprocess.call(cmd, env=env)
+
+
+def resolve_world(args, torchrun):
+    """-> the rank count this process belongs to, validating --gpus against
+    torchrun's WORLD_SIZE (a mismatch would print an N-GPU line measured on
+    a different number of GPUs)."""
+    world = int(os.environ.get("WORLD_SIZE", "1")) if torchrun else 1
+    if args.gpus is None:
+        return world
+    if args.gpus < 1:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} must be >= 1")
+    if torchrun and args.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but torchrun started WORLD_SIZE={world} ranks")
+    return args.gpus
+
+
+def dry_run(args):
+    """The launcher's rank plumbing with no device work: gloo collective, one
+    gathered record per rank, the same aggregation and line shape as the real
+    run (value is meaningless and says so)."""
+    from hadoofus_amd import shard
+    d = shard.Collective("gloo") if shard.launched_by_torchrun() else shard.Local()
+    infos = d.gather({"rank": d.rank, "local_rank": d.local, "pid": os.getpid(), "host": socket.gethostname(),
+                      "pci_bus_id": f"dry-run:{d.local}"})
+    shard.check_distinct_devices(infos)
+    scaling, g0, B = shard.workload_blocks(args.config, d.rank, d.world, args.blocks)
+    d.barrier()
+    tot_bytes, _, ok, t_max = d.aggregate(B * BLOCK, 0, True, 1.0)
+    if d.rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "GiB/s", "n_gpus": d.world, "dry_run": True,
+                          "scaling": scaling, "ranks": [i["rank"] for i in infos],
+                          "pids": [i["pid"] for i in infos], "all_ranks_ok": ok == d.world,
+                          "bytes_per_step": tot_bytes, "config": {"workload": args.config}}), flush=True)
+    d.close()
 
 
 def pmc_traffic(kernel, nbytes, chunk):
@@ -240,10 +307,16 @@ def bitmap_matches(bm_host, nbits_per_block, bad_local):
 
 def main():
     args = parse()
-    from hadoofus_amd import shard
+    from hadoofus_amd import shard  # no torch, no HIP: safe before the launch decision
+    torchrun = shard.launched_by_torchrun()
+    n_req = resolve_world(args, torchrun)
+    if n_req > 1 and not torchrun:
+        sys.exit(launch_ranks(n_req, sys.argv[1:]))
+    if args.dry_run:
+        return dry_run(args)
     # torch (and with it the HIP runtime it ships) is imported before the
     # engine library only when launched as ranks.
-    d = shard.Collective("nccl") if shard.launched_by_torchrun() else shard.Local()
+    d = shard.Collective("nccl") if torchrun else shard.Local()
     import hadoofus_amd as h
 
     h.load()
@@ -444,8 +517,38 @@ def main():
             extra["c4_speedup_bound"] = {f"{g}gpu": round(shard_ms[512] / shard_ms[512 // g], 3)
                                          for g in (2, 4, 8) if 512 // g in shard_ms}
 
+    # C4 strong scaling beside the weak-scaled headline when N > 1
+    # (BASELINE.json configs[3]: 64 GiB for the whole node, split evenly):
+    # each rank verifies its 512 / N share, taken from the front of its
+    # resident blocks, timed between barriers, max over ranks.
+    c4 = None
+    if d.world > 1 and args.config == "C3" and not args.no_extra:
+        nb4 = min(shard.split_blocks(512, d.rank, d.world)[1], B)
+        sp = h.Plan(h.MODE_VERIFY, segs(lambda g: cs, crcs.ptr, bms.ptr)[:nb4])
+        sp.execute(stream)
+        h.stream_sync(stream)
+        k4 = max(2, args.steps)
+        d.barrier()
+        h.stream_sync(stream)
+        t4 = time.perf_counter()
+        for _ in range(k4):
+            sp.execute(stream)
+        h.stream_sync(stream)
+        d.barrier()
+        t4 = time.perf_counter() - t4
+        _, m4 = sp.results(stream)
+        sp.destroy()
+        want4 = sum(1 for b, _c in bad_local if b < nb4)
+        b4, mm4, ok4, tmax4 = d.aggregate(nb4 * BLOCK * k4, m4, m4 == want4, t4)
+        c4 = {"workload": "C4 strong: 512 x 128MiB blocks (64 GiB) split evenly over the GPUs, verify, 512B chunks",
+              "GiBps": round(b4 / tmax4 / (1 << 30), 1), "total_bytes_per_step": int(b4 / k4),
+              "blocks_rank0": nb4, "ms_per_step": round(tmax4 / k4 * 1e3, 3), "steps": k4,
+              "mismatches": int(mm4), "all_ranks_ok": ok4 == d.world}
+
     tot_bytes, tot_mism, ok, t_max = d.aggregate(B * BLOCK * args.steps, m, parity_ok, elapsed)
     n = d.world
+    if c4:
+        extra["c4_strong"] = c4
 
     if d.rank == 0:
         gib_s = tot_bytes / t_max / (1 << 30)
@@ -465,13 +568,15 @@ def main():
                 f"{extra.get('ceiling_source', '')}) reaches the verify kernel's own {round(achieved, 1)} GB/s, "
                 "so no empirical peak is reported; frac is against the 8 TB/s spec only")
         if args.config == "C3":
-            workload = ("C3 verify: 1024 x 128MiB HDFS blocks per GPU of splitmix64 data, 512B chunks, BE wire CRCs, "
-                        "1/65537 chunks corrupted, bitmap + first-bad out")
+            workload = (f"C3 verify: {B} x 128MiB HDFS blocks per GPU of splitmix64 data, 512B chunks, BE wire CRCs, "
+                        "1/65537 chunks corrupted, bitmap + first-bad out"
+                        + (f"; weak scaling over {n} GPUs ({n * B} blocks in all)" if n > 1 else ""))
         else:
             workload = ("C4 verify: 64GiB (512 x 128MiB blocks) split evenly over the GPUs, 512B chunks, BE wire CRCs, "
-                        "1/65537 chunks corrupted, bitmap + first-bad out")
+                        "1/65537 chunks corrupted, bitmap + first-bad out"
+                        + (f"; strong scaling over {n} GPUs" if n > 1 else ""))
         line = {
-            "metric": "CRC32C verify GiB/s (device-resident), 512B chunks over 128MiB HDFS blocks",
+            "metric": METRIC,
             "value": round(gib_s, 1),
             "unit": "GiB/s",
             "n_gpus": n,
