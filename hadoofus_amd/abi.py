@@ -444,11 +444,13 @@ class Reader:
                                                  self.max_pkts, ctypes.byref(self.rd)), self.lib)
         self.arr = (Packet * max(1, min(self.max_pkts, 1 << 16)))()
 
-    def next(self, iov):
-        """iov = [(ptr, len), ...] -> (rc, [packet dicts], consumed, delivered)."""
+    def next(self, iov, room=None):
+        """iov = [(ptr, len), ...] -> (rc, [packet dicts], consumed, delivered);
+        room: the record array's capacity passed as max_pkts (default: all)."""
         vec = (IoVec * max(1, len(iov)))(*[IoVec(p, n) for p, n in iov])
         npk, used, got = _sz(0), _u64(0), _u64(0)
-        rc = self.lib.hdfs_crc32c_reader_next(self.rd, vec, len(iov), self.arr, len(self.arr), ctypes.byref(npk),
+        room = len(self.arr) if room is None else min(room, len(self.arr))
+        rc = self.lib.hdfs_crc32c_reader_next(self.rd, vec, len(iov), self.arr, room, ctypes.byref(npk),
                                               ctypes.byref(used), ctypes.byref(got))
         if rc < 0:
             _check(rc, self.lib)

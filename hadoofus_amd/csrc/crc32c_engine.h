@@ -168,6 +168,7 @@ struct DevCtx {
   std::atomic<bool> ready{false};
   int dev = -1;
   int num_cu = 0;
+  int num_xcd = 8;  // gfx950 (MI355X): 8 XCDs of 32 CUs; workgroups dealt round-robin
   char arch[64] = "";
   // table sets per checksum type: [0] CRC32C, [1] CRC32 (zlib polynomial)
   uint32_t *d_tab_main_t[2] = {nullptr, nullptr};
@@ -313,8 +314,9 @@ struct DevCtx {
   // to the XCDs round-robin, so a grid of num_cu - 1 still gives the
   // mailbox's XCD one workgroup per CU, and the one that lands after the
   // others waits for the mailbox to idle out (round 5: a reader's open
-  // stalled by the idle limit on every read).  32 CUs per XCD on gfx950.
-  int bulk_cus() const { return num_cu - (mb_on ? std::max(1, num_cu / 32) : 0); }
+  // stalled by the idle limit on every read).  num_xcd is the gfx950 part's
+  // XCD count (ctx_init admits gfx950 only), not derived from num_cu.
+  int bulk_cus() const { return num_cu - (mb_on ? num_xcd : 0); }
   std::mutex mu;
 };
 

@@ -1529,6 +1529,8 @@ int grid_walk(DevCtx &c, const uint8_t *d, uint64_t len, int proto, uint32_t cs,
 //   - a framing error (:2439-2446) or bad CRCs (:2470-2475: bad_crcs, the
 //     loop breaks at :1478 and the call returns BAD_CHECKSUM, :1500-1505):
 //     the packet is recorded, delivers nothing and is not consumed;
+//   - a framing error is not consumed, except an empty packet not flagged
+//     last (PACKET_SIZE, :2450-2455: its header is);
 //   - an empty last packet while the read wants bytes is BAD_LASTPACKET
 //     (:2450-2456; its header is consumed);
 //   - a packet that starts past the read (c_begin >= dataLen) is
@@ -1568,7 +1570,10 @@ int apply_read_window(hdfs_crc32c_packet *p, size_t &n, uint64_t &consumed, cons
     if (examined) *examined = k + 1;
     if (r.error) {  // framing error or bad CRCs
       n = k + 1;
-      consumed = r.stream_off;
+      // an empty packet not flagged last fails with its header consumed
+      // (src/datanode.c:2450-2455); no other framing error consumes anything
+      const bool empty_not_last = r.error == HDFS_CRC32C_ERR_DATANODE_PACKET_SIZE && r.data_len == 0 && r.crc_len == 0;
+      consumed = r.stream_off + (empty_not_last ? r.header_len : 0);
       break;
     }
     if (r.data_len == 0) {  // the empty last packet (a non-last one is a framing error)
@@ -2049,7 +2054,9 @@ int read_dev_to_host(int dev, const uint8_t *s, uint64_t len, int proto, uint32_
   DeviceGuard g(c.dev);
   std::lock_guard<std::mutex> lk(c.rd_mu);
   const bool win = read_len != HDFS_CRC32C_READ_ALL;
-  const uint64_t cap = win ? std::min<uint64_t>(total, uint64_t(read_len)) : total;
+  // the delivered payload never exceeds the stream's own bytes: a host buffer
+  // larger than the stream does not size (and pin) a larger staging area
+  const uint64_t cap = std::min<uint64_t>(win ? std::min<uint64_t>(total, uint64_t(read_len)) : total, len);
   if ((rc = rd_stage_reserve(c, cap))) return rc;
   CopyOut co;
   co.dst = c.rd_stage;
@@ -2644,19 +2651,17 @@ int reader_next(hdfs_crc32c_reader *rd, const hdfs_crc32c_iovec *iov, int iovcnt
     }
   }
   rd->done += want;
-  // records completed by this call; the read's last one (and status) once all is out
+  // records completed so far, at most max_pkts of them; the rest wait for the
+  // next call (which may deliver no bytes); the read's last record (and its
+  // status) once all bytes are out
   size_t k = 0;
-  while (rd->rec_next < rd->recs.size() && rd->rec_done[rd->rec_next] <= rd->done &&
-         (rd->done == rd->total || rd->rec_next + 1 < rd->recs.size())) {
-    if (k < max_pkts) pkts[k] = rd->recs[rd->rec_next];
-    k++;
-    rd->rec_next++;
-  }
-  if (k > max_pkts) return fail(HDFS_CRC32C_EINVAL, "next: %zu records, room for %zu", k, max_pkts);
+  while (k < max_pkts && rd->rec_next < rd->recs.size() && rd->rec_done[rd->rec_next] <= rd->done &&
+         (rd->done == rd->total || rd->rec_next + 1 < rd->recs.size()))
+    pkts[k++] = rd->recs[rd->rec_next++];
   *npkts = k;
   *delivered = want;
   // consumed: the end of the last complete packet so far, the read's own at its end
-  if (rd->done == rd->total) {
+  if (rd->done == rd->total && rd->rec_next == rd->recs.size()) {
     *consumed = rd->consumed;
     return rd->status;
   }

@@ -354,8 +354,10 @@ int hdfs_crc32c_job_wait_blocks(hdfs_crc32c_job *job, hdfs_crc32c_packet *pkts, 
  * *delivered = bytes this call, *consumed = the end of the last packet
  * delivered whole so far (the read's own consumed at its end), into pkts
  * the records of the packets whose last byte this call delivered (the
- * read's last record with the last call), and returns HDFS_CRC32C_AGAIN
- * while bytes remain, then the read's status: 0, or the error that ended
+ * read's last record with the last call) -- at most max_pkts of them; the
+ * rest come with the following calls, which may deliver no bytes -- and
+ * returns HDFS_CRC32C_AGAIN while bytes or records remain, then the read's
+ * status: 0, or the error that ended
  * it, whose record comes last.  A read the stream or max_pkts cannot
  * complete ends with 0 and fewer bytes than read_len, as
  * hdfs_crc32c_read_packets' does: resume at stream + consumed.  The stream

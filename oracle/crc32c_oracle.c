@@ -671,7 +671,9 @@ int oracle_verify_packets(const uint8_t *s, uint64_t len, int proto, uint32_t cs
  * (src/datanode.c:2428-2549) for the block bytes [client_offset,
  * client_offset + read_len), into a destination of cap bytes
  * (UINT64_MAX: as large as the read).  Per packet, in the reference's order:
- *   - a framing error ends the read (:2439-2446);
+ *   - a framing error ends the read (:2439-2446), not consumed -- except an
+ *     empty packet not flagged last (PACKET_SIZE), whose header is consumed
+ *     (:2450-2455);
  *   - an empty last packet while bytes are still wanted is BAD_LASTPACKET
  *     (:2450-2456; its header is consumed, :2455);
  *   - bad CRCs end the read (:2470-2475 set bad_crcs, the loop breaks on it
@@ -714,6 +716,9 @@ int oracle_read_packets(const uint8_t *s, uint64_t len, int proto, uint32_t cs, 
 		if (st == 1) {
 			if (!k.error) { /* the empty last packet: the read wanted more */
 				k.error = ORACLE_ERR_BAD_LASTPACKET;
+				*consumed = pos + total;
+			} else if (total) { /* an empty packet not flagged last: PACKET_SIZE with its
+			                       header consumed (src/datanode.c:2451-2455) */
 				*consumed = pos + total;
 			}
 			out[n++] = k;

@@ -7,11 +7,12 @@ GPU: hdfs_crc32c_verify_packets against the fixtures and, on large
 generated streams, against the oracle."""
 import json
 import os
+import struct
 
 import numpy as np
 import pytest
 
-from packet_stream import CSUM_CRC32, CSUM_CRC32C, assemble, build_stream
+from packet_stream import CSUM_CRC32, CSUM_CRC32C, assemble, build_stream, frame_v2, header_v2
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "packet_cases.json")
 BAD = 29
@@ -512,14 +513,30 @@ def _read_cases(oracle):
     out.append(("bad_crc_mid", s3, 40, 4 * 65536 + 9, BAD, 3, p3[40:]))
     # bad CRCs in the packet the read starts in: nothing delivered
     out.append(("bad_crc_first", s3[w3[2]["stream_off"]:], 2 * 65536 + 5, 1000, BAD, 1, b""))
+    # framing errors end the read after the packets before them (src/datanode.c:2439-2456):
+    # an empty packet NOT flagged last after packet 2 -- PACKET_SIZE, its header consumed
+    # (:2450-2455) -- and packet 2 framed with a plen 4 short -- CRC_LEN, not consumed
+    s4, _ = build_stream(oracle.crc32c, 2, cs, CSUM_CRC32C, [65536] * 5, seed=4, last_empty=False)
+    w4 = oracle.verify_packets(s4)[1]
+    cut = w4[3]["stream_off"]
+    empty = frame_v2(header_v2(3 * 65536, 3, False, 0), b"", b"")
+    p4 = b"".join(_payload_of(s4, w4, k) for k in range(3))
+    out.append(("empty_not_last", s4[:cut] + empty + s4[cut:], 5, 4 * 65536, ERR_PACKET_SIZE, 4, p4[5:]))
+    a2 = w4[2]["stream_off"]
+    bad2 = struct.pack(">i", struct.unpack(">i", s4[a2:a2 + 4])[0] - 4) + s4[a2 + 4:]
+    out.append(("crc_len_mid", s4[:a2] + bad2, 5, 4 * 65536, ERR_CRC_LEN, 3, p4[5:2 * 65536]))
     return out
 
 
 def _read_consumed(pk):
     """Where a read that ended with record pk stands in the stream: a packet
-    whose header, CRCs or read offset raised the error is not consumed
-    (src/datanode.c:2445-2446, 2472-2475, 2483-2486); any other is."""
-    if pk["error"] in (BAD, ERR_UNEXPECTED_READ_OFFSET):
+    whose framing, CRCs or read offset raised the error is not consumed
+    (src/datanode.c:2445-2446, 2472-2475, 2483-2486), except the empty packet
+    not flagged last, whose header is (PACKET_SIZE, :2450-2455); any other
+    packet is consumed whole."""
+    if pk["error"] == ERR_PACKET_SIZE and pk["data_len"] == 0 and pk["crc_len"] == 0:
+        return pk["stream_off"] + pk["header_len"]
+    if pk["error"] and pk["error"] != ERR_BAD_LASTPACKET:
         return pk["stream_off"]
     return pk["stream_off"] + pk["header_len"] + pk["crc_len"] + pk["data_len"]
 
@@ -566,6 +583,7 @@ AGAIN = 1000
 
 
 ERR_UNEXPECTED_READ_OFFSET, ERR_BAD_LASTPACKET = 28, 32
+ERR_PACKET_SIZE, ERR_CRC_LEN = 25, 26
 
 
 def _dev_read(engine, s, shift, co, rl, proto=2, cs=512, ctype=CSUM_CRC32C, cap=None, mp=None):

@@ -323,6 +323,48 @@ def test_gpu_reader_records_or_stream_run_out(engine, oracle):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("room", [0, 1, 2])
+def test_gpu_reader_small_record_array(engine, oracle, room):
+    """next with room for fewer records than the call completes (max_pkts 0,
+    1 or 2) loses nothing: the records it has no room for come with the
+    following calls (bytes first, then record-only calls that deliver 0
+    bytes), in order, and the read's status and consumed come with its last
+    record -- the concatenation equals the oracle's single read.  With room
+    0, a call completes no record, so consumed never moves past 0 before the
+    draining calls."""
+    dl = [4096] * 40 + [777]
+    s, _ = build_stream(oracle.crc32c, 2, 512, CSUM_CRC32C, dl, seed=23, corrupt=[(33, 1)])
+    co, rl = 100, sum(dl)
+    want = oracle.read_packets(s, co, rl)
+    keep, p = _dev(engine, s)
+    dbuf = engine.DeviceBuffer(len(want[3]) + 65536)
+    rd = engine.Reader(p, len(s), co, rl)
+    try:
+        data, recs, at, calls, last_used = b"", [], 0, 0, 0
+        while True:
+            piece = 65536
+            rc, pk, used, got = rd.next([(dbuf.ptr + at, piece)], room=room if data != want[3] else max(room, 1))
+            calls += 1
+            assert len(pk) <= max(room, 1 if data == want[3] else room)
+            assert used >= last_used
+            last_used = used
+            recs += pk
+            data += dbuf.download(got, offset=at).tobytes() if got else b""
+            at += got
+            if rc != AGAIN:
+                break
+            assert calls < 1000
+        assert (rc, recs, used) == want[:3]
+        assert data == want[3]
+        # after the last call: the status again, nothing delivered
+        assert rd.next([(dbuf.ptr, 4096)], room=room)[0] == rc
+    finally:
+        rd.close()
+        dbuf.free()
+        keep.free()
+
+
+@pytest.mark.gpu
 def test_gpu_reader_host_stream(engine, oracle):
     """A reader over a HOST-resident stream (a host-memory datanode's
     receive buffer): framed on the host, the read's packets verified on the
