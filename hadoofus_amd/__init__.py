@@ -14,7 +14,7 @@ from .abi import (  # noqa: F401
     CRC32CError, DeviceBuffer, Mailbox, Plan, Segment, Session, crc32c, compose_crcs, compose_packets,
     composite_crcs, compute_host, verify_host, PinnedBuffer, corrupt, fill_splitmix64, stream_create,
     stream_sync, device_info, init, bound_device, device_sync, load, stream_crc_dev, stream_ex,
-    verify_crcdata, VerifyJob, VerifyBlocksJob, Reader,
+    verify_crcdata, VerifyJob, VerifyBlocksJob, Reader, read_packets_fd, EIO,
 )
 
 __all__ = [n for n in dir() if not n.startswith("_")]

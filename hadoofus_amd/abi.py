@@ -26,6 +26,7 @@ ERR_UNEXPECTED_CRC_LEN = 27
 ERR_UNEXPECTED_READ_OFFSET = 28
 ERR_BAD_CHECKSUM = 29
 ERR_BAD_LASTPACKET = 32
+EIO = -5       # hdfs_crc32c_read_packets_fd: a write to the fd failed
 READ_ALL = -1  # read_packets: whole payloads, no client read window
 AGAIN = 1000   # read_packets: the destination filled before the read completed (resumable)
 ABI_VERSION = 5  # include/hadoofus_crc32c.h HDFS_CRC32C_ABI_VERSION these bindings are written for
@@ -152,6 +153,9 @@ def bind_product(lib):
           [_vp, ctypes.POINTER(IoVec), _int, ctypes.POINTER(Packet), _sz, ctypes.POINTER(_sz), ctypes.POINTER(_u64),
            ctypes.POINTER(_u64)])
     _bind(lib, "hdfs_crc32c_reader_close", None, [_vp])
+    _bind(lib, "hdfs_crc32c_read_packets_fd", _int,
+          [_vp, _u64, _int, _u32, _int, ctypes.c_int64, ctypes.c_int64, _int, ctypes.c_int64,
+           ctypes.POINTER(Packet), _sz, ctypes.POINTER(_sz), ctypes.POINTER(_u64), ctypes.POINTER(_u64)])
     _bind(lib, "hdfs_crc32c_abi_version", _int, [])
     _bind(lib, "hdfs_crc32c_session_create", _int, [ctypes.POINTER(_vp), _int, _u32, _int, _u64, _sz])
     _bind(lib, "hdfs_crc32c_session_buffer", _int, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_u64)])
@@ -199,6 +203,7 @@ def bind_diag(lib):
     _bind(lib, "hdfs_crc32c_set_runs", _int, [_int])
     _bind(lib, "hdfs_crc32c_diag_device_checks", _int, [ctypes.POINTER(_u32), _int])
     _bind(lib, "hdfs_crc32c_set_speculation", _int, [_int])
+    _bind(lib, "hdfs_crc32c_set_job_coalesce", _int, [_int])
     _bind(lib, "hdfs_crc32c_diag_spec_stats", _int, [ctypes.POINTER(_u64), _int])
     _bind(lib, "hdfs_crc32c_diag_stream_queries", _int, [ctypes.POINTER(_u64)])
     return lib
@@ -427,6 +432,26 @@ def read_packets(dptr, nbytes, dst, dst_cap, proto=PROTO_V2, chunk_size=512, cty
     rc = lib.hdfs_crc32c_read_packets(dptr, nbytes, proto, chunk_size, ctype, client_offset, read_len, vec, len(iov),
                                       arr, max_pkts, ctypes.byref(npk), ctypes.byref(used), ctypes.byref(got))
     if rc < 0:
+        _check(rc, lib)
+    return rc, [arr[i].as_dict() for i in range(npk.value)], used.value, got.value
+
+
+def read_packets_fd(dptr, nbytes, fd, fd_offset, client_offset, read_len, proto=PROTO_V2, chunk_size=512,
+                    ctype=CSUM_CRC32C, max_pkts=None, lib=None, check=True):
+    """hdfs_crc32c_read_packets_fd: the client read [client_offset,
+    client_offset + read_len) of a stream (device- or host-resident), its
+    bytes pwrite()n to fd at fd_offset (hdfs_datanode_read_file,
+    src/datanode.c:2531-2541).  -> (rc, [packet dicts], consumed, delivered);
+    check=False returns a negative rc instead of raising."""
+    if max_pkts is None:
+        max_pkts = nbytes // (25 if proto == PROTO_V1 else 6) + 1
+    arr = (Packet * max(1, max_pkts))()
+    npk, used, got = _sz(0), _u64(0), _u64(0)
+    lib = lib or load()
+    rc = lib.hdfs_crc32c_read_packets_fd(dptr, nbytes, proto, chunk_size, ctype, client_offset, read_len, fd,
+                                         fd_offset, arr, max_pkts, ctypes.byref(npk), ctypes.byref(used),
+                                         ctypes.byref(got))
+    if rc < 0 and check:
         _check(rc, lib)
     return rc, [arr[i].as_dict() for i in range(npk.value)], used.value, got.value
 

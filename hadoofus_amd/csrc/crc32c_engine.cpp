@@ -110,6 +110,12 @@ int g_runs = HDFS_KNOB("HDFS_CRC32C_RUNS", 2);
 // (spec_verify_kernel; 1, the product) or always frame the run (0,
 // diagnostic build only: the A/B of round 4).
 int g_spec = HDFS_KNOB("HDFS_CRC32C_SPEC", 1);
+// Asynchronous jobs (hdfs_crc32c_verify_packets_submit): 1 (the product)
+// queue a job submitted while a launch runs and send the queue out as one
+// batch launch; 0 (diagnostic A/B) launch every job at its submit, as round
+// 5 did; 2 (diagnostic, deterministic tests) queue even on an idle GPU --
+// the queue goes out only when a wait needs it, when full, or on a key change.
+int g_job_coalesce = HDFS_KNOB("HDFS_CRC32C_JOB_COALESCE", 1);
 // Small-call input stage: 1 fine-grained VRAM written through the BAR when
 // the device is large-BAR, else (and 0) pinned host memory.
 int g_stage_vram = HDFS_KNOB("HDFS_CRC32C_MB_STAGE", 1);
@@ -1601,6 +1607,12 @@ int hdfs_crc32c_diag_stream_queries(uint64_t *out) {
 int hdfs_crc32c_set_speculation(int on) {
   if (on != 0 && on != 1) return fail(HDFS_CRC32C_EINVAL, "speculation 0 or 1");
   g_spec = on;
+  return HDFS_CRC32C_OK;
+}
+
+int hdfs_crc32c_set_job_coalesce(int mode) {
+  if (mode < 0 || mode > 2) return fail(HDFS_CRC32C_EINVAL, "job coalescing 0 (off), 1 (product) or 2 (hold)");
+  g_job_coalesce = mode;
   return HDFS_CRC32C_OK;
 }
 

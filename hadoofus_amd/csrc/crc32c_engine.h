@@ -80,6 +80,8 @@ hipError_t launch_spec_verify(const SpecArgs &a, int grid, int copy, hipStream_t
 // device-resident packet runs: try spec_verify_kernel first (diagnostic
 // build: hdfs_crc32c_set_speculation)
 extern int g_spec;
+// asynchronous jobs: queue and batch (1), launch at submit (0), hold (2)
+extern int g_job_coalesce;
 // diagnostic build: per-wave / per-block s_memrealtime stamps (set_tuning)
 extern unsigned long long *g_diag;
 // frame_build_kernel's stamps sit after the tiled kernel's per-wave words
@@ -159,8 +161,11 @@ struct SpecSlot {
   uint8_t *scratch = nullptr;
   uint64_t scratch_cap = 0;
 };
-// asynchronous verify jobs in flight per device
+// asynchronous verify jobs: launches in flight per device (job slots), and
+// jobs submitted and not yet waited for per device
 constexpr int kMaxJobs = 4;
+constexpr size_t kMaxJobsOut = 64;
+struct JobQueue;
 
 struct DevCtx {
   // published with release after every field below is set up; the unlocked
@@ -270,7 +275,10 @@ struct DevCtx {
   // bitmap / first-bad scratch
   SpecSlot spec;
   SpecSlot job_slot[kMaxJobs];
-  bool job_busy[kMaxJobs] = {};
+  bool job_busy[kMaxJobs] = {};  // the slot holds a launch not yet collected
+  // asynchronous jobs: submitted runs waiting to share one launch, launches
+  // in flight (crc32c_packets.cpp; guarded by mu, created on first use)
+  JobQueue *jobq = nullptr;
   // client reads into host memory (hdfs_crc32c_read_packets with host
   // iovecs): the device staging the fused copy-out fills before the D2H
   // scatter; rd_mu is held across the verify and the scatter (taken before mu)

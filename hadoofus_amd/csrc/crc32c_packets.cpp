@@ -7,6 +7,7 @@
 #include "crc32c_packets.h"
 
 #include <algorithm>
+#include <cerrno>
 #include <cstdio>
 #include <chrono>
 #include <cstdlib>
@@ -16,6 +17,8 @@
 #include <memory>
 #include <thread>
 #include <vector>
+
+#include <unistd.h>
 
 #include "crc32c_engine.h"
 
@@ -1766,18 +1769,56 @@ int verify_packets_impl(const uint8_t *stream, uint64_t len, int proto, uint32_t
 }
 
 // ---- asynchronous verify jobs (hdfs_crc32c_verify_packets_submit / _wait) ----
-// A device-resident run's speculative launch goes out on a job slot's own
-// stream at submit; the wait collects it and, when the launch did not take
-// the whole stream (another packet size follows, more packets than one pass,
-// or no run at all), frames and verifies the rest synchronously -- so the
-// result is hdfs_crc32c_verify_packets' in every case.  Jobs on different
-// slots overlap on the GPU: one launch's ramp and tail under another's
-// steady state (a datanode verifying a stream of blocks).
+// A device-resident run is verified by a speculative launch on a job slot's
+// own stream; the wait collects it and, when the launch did not take the
+// whole stream (another packet size follows, more packets than one pass, or
+// no run at all), frames and verifies the rest synchronously -- so the result
+// is hdfs_crc32c_verify_packets' in every case.
+// Coalescing (a datanode verifying a stream of received blocks, one job per
+// block): a launch carries a fixed cost of ~13 us whatever its size, so runs
+// submitted while an earlier launch is still running are not launched one by
+// one: they queue (runs of one layout key: protocol, chunk size, checksum
+// type, length, record room) and go out together as ONE batch launch of up to
+// kSpecRunsMax runs (spec_verify_kernel<..., 1>, the path of
+// hdfs_crc32c_verify_blocks_submit) when
+//   - a submit finds no launch running (the GPU would idle),
+//   - a wait needs a queued job, or would block on a running launch (the
+//     queue goes out first, so the GPU has it behind the running one),
+//   - the queue holds kSpecRunsMax runs, or a run of another key arrives.
+// The results are per job exactly as before.  A launch's results are copied
+// out of its slot when it is collected (by the first wait of one of its
+// jobs, or to free the slot for a new launch), so its jobs may be waited in
+// any order.
+struct JobGroup {
+  int slot = -1;
+  SpecLaunch L;
+  uint32_t m = 0;                          // runs in the launch
+  size_t per = 0;                          // records per run in recs
+  bool collected = false, single_not_taken = false;
+  int rc = 0;                              // the collection's status
+  std::vector<hdfs_crc32c_packet> recs;    // [m][per]
+  std::vector<SpecRunResult> rr;           // [m]
+  int refs = 0;                            // jobs not yet waited for
+};
 }  // namespace
+struct JobQueue {
+  std::vector<hdfs_crc32c_job *> pending;  // queued runs, in submit order
+  struct Key {
+    int proto, ctype;
+    uint32_t cs;
+    uint64_t len;
+    size_t max_pkts;
+    bool operator==(const Key &o) const {
+      return proto == o.proto && ctype == o.ctype && cs == o.cs && len == o.len && max_pkts == o.max_pkts;
+    }
+  } key{};
+  std::vector<JobGroup *> running;         // launched, not collected (oldest first)
+  size_t outstanding = 0;                  // jobs submitted and not yet waited for
+};
 }  // namespace hdfs_crc32c
 
 struct hdfs_crc32c_job {
-  int dev = -1, slot = -1;
+  int dev = -1;
   std::vector<const uint8_t *> runs;  // the block streams (one for hdfs_crc32c_verify_packets_submit)
   std::vector<uint64_t> lens;
   bool batch = false;                 // hdfs_crc32c_verify_blocks_submit
@@ -1785,12 +1826,156 @@ struct hdfs_crc32c_job {
   int proto = 0, ctype = 0;
   uint32_t cs = 0;
   size_t max_pkts = 0;
-  bool launched = false;
-  hdfs_crc32c::SpecLaunch L;
+  bool queued = false;                // waiting in the device's queue for a launch
+  hdfs_crc32c::JobGroup *grp = nullptr;  // its launch (runs grp_run .. grp_run + sel.size() - 1)
+  uint32_t grp_run = 0;
 };
 
 namespace hdfs_crc32c {
 namespace {
+
+JobQueue &jobq(DevCtx &c) {
+  if (!c.jobq) c.jobq = new JobQueue;
+  return *c.jobq;
+}
+
+// A launch is done once its early block says the run was not taken (every
+// workgroup returns at once) or its final block is published.
+bool group_done(DevCtx &c, const JobGroup &g) {
+  const SpecSlot &S = c.job_slot[g.slot];
+  const auto *early = reinterpret_cast<const SpecEarly *>(S.h);
+  const auto *fin = reinterpret_cast<const SpecFinal *>(S.h + sizeof(SpecEarly));
+  if (__atomic_load_n(&early->seq, __ATOMIC_ACQUIRE) != g.L.seq) return false;
+  if (!__atomic_load_n(&early->eligible, __ATOMIC_RELAXED)) return true;
+  return __atomic_load_n(&fin->seq, __ATOMIC_ACQUIRE) == g.L.seq;
+}
+
+// Copy a launch's results out of its slot and free the slot.
+int group_collect(DevCtx &c, JobQueue &q, JobGroup *g) {
+  if (g->collected) return g->rc;
+  SpecSlot &S = c.job_slot[g->slot];
+  g->recs.assign(g->per * g->m, hdfs_crc32c_packet{});
+  g->rr.assign(g->m, SpecRunResult{});
+  int rc;
+  if (g->m == 1) {
+    SpecResult sr;
+    rc = spec_collect(c, S, g->L, CopyOut{}, g->recs.data(), sr);
+    g->rr[0].taken = sr.taken;
+    g->rr[0].end = sr.end;
+    g->rr[0].recorded = sr.recorded;
+    g->rr[0].consumed = sr.consumed;
+    g->rr[0].next = sr.next;
+    g->single_not_taken = !sr.taken;
+  } else {
+    std::vector<hdfs_crc32c_packet *> dst(g->m);
+    std::vector<uint64_t> pos0(g->m, 0);
+    for (uint32_t r = 0; r < g->m; r++) dst[r] = g->recs.data() + r * g->per;
+    rc = spec_collect_batch(S, g->L, g->m, pos0.data(), dst.data(), g->rr);
+  }
+  g->collected = true;
+  g->rc = rc;
+  c.job_busy[g->slot] = false;
+  q.running.erase(std::remove(q.running.begin(), q.running.end(), g), q.running.end());
+  return rc;
+}
+
+// Launch runs (streams[r], lens[r]) of one layout key as one speculative
+// launch on a free job slot -- collecting the oldest running launch first
+// when all slots are busy.  -> the group (refs 0), or null with rc set.
+JobGroup *group_launch(DevCtx &c, JobQueue &q, const uint8_t *const *streams, const uint64_t *lens, uint32_t m,
+                       int proto, uint32_t cs, int ctype, size_t max_pkts, int *rcp) {
+  int slot = -1;
+  for (;;) {
+    for (int i = 0; i < kMaxJobs && slot < 0; i++)
+      if (!c.job_busy[i]) slot = i;
+    if (slot >= 0 || q.running.empty()) break;
+    (void)group_collect(c, q, q.running.front());  // (its status stays with its jobs)
+  }
+  if (slot < 0) {
+    *rcp = fail(HDFS_CRC32C_EHIP, "no free job slot");
+    return nullptr;
+  }
+  SpecSlot &S = c.job_slot[slot];
+  if (!S.stream && hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking) != hipSuccess) {
+    (void)hipGetLastError();
+    S.stream = nullptr;
+    *rcp = fail(HDFS_CRC32C_EHIP, "job stream");
+    return nullptr;
+  }
+  // per run at most `count` packets; the bitmap takes ceil(chunks / 8) bytes
+  // per packet (<= len / 32 + 1), first-bad one word per packet
+  const uint32_t count = uint32_t(std::min<uint64_t>(uint64_t(max_pkts), kGridMaxCount));
+  uint64_t bm_cap = 64, fbw = 0;
+  for (uint32_t r = 0; r < m; r++) {
+    const uint64_t cr = std::min<uint64_t>(count, lens[r] / 6 + 1);
+    bm_cap += lens[r] / 32 + cr;
+    fbw += cr;
+  }
+  bm_cap = align_up(bm_cap, 256);
+  const uint64_t need = bm_cap + fbw * 4u + 256u;
+  if (need > S.scratch_cap) {
+    if (S.scratch) (void)hipFree(S.scratch);
+    S.scratch = nullptr;
+    S.scratch_cap = 0;
+    if (hipMalloc(&S.scratch, need) != hipSuccess) {
+      (void)hipGetLastError();
+      *rcp = fail(HDFS_CRC32C_ENOMEM, "job scratch of %llu bytes", (unsigned long long)need);
+      return nullptr;
+    }
+    S.scratch_cap = need;
+  }
+  auto *g = new (std::nothrow) JobGroup;
+  if (!g) {
+    *rcp = fail(HDFS_CRC32C_ENOMEM, "job launch");
+    return nullptr;
+  }
+  g->slot = slot;
+  g->m = m;
+  g->per = size_t(count) + 1;
+  int rc = spec_launch(c, S, S.stream, streams[0], lens[0], 0, count, proto, cs, ctype, CopyOut{}, 0, S.scratch,
+                       reinterpret_cast<uint32_t *>(S.scratch + bm_cap), g->L, m, streams, lens);
+  if (rc) {
+    delete g;
+    *rcp = rc;
+    return nullptr;
+  }
+  c.job_busy[slot] = true;
+  q.running.push_back(g);
+  *rcp = HDFS_CRC32C_OK;
+  return g;
+}
+
+// The queue goes out as one launch.  If the launch fails, its jobs are
+// verified synchronously in their waits instead (the wait reports an error
+// that persists).
+void queue_flush(DevCtx &c, JobQueue &q) {
+  if (q.pending.empty()) return;
+  std::vector<const uint8_t *> s;
+  std::vector<uint64_t> l;
+  for (hdfs_crc32c_job *j : q.pending) {
+    s.push_back(j->runs[0]);
+    l.push_back(j->lens[0]);
+  }
+  int rc = 0;
+  JobGroup *g = group_launch(c, q, s.data(), l.data(), uint32_t(s.size()), q.key.proto, q.key.cs, q.key.ctype,
+                             q.key.max_pkts, &rc);
+  for (size_t r = 0; r < q.pending.size(); r++) {
+    hdfs_crc32c_job *j = q.pending[r];
+    j->queued = false;
+    if (g) {
+      j->grp = g;
+      j->grp_run = uint32_t(r);
+      g->refs++;
+    }
+  }
+  q.pending.clear();
+}
+
+bool any_running(DevCtx &c, JobQueue &q) {
+  for (JobGroup *g : q.running)
+    if (!group_done(c, *g)) return true;
+  return false;
+}
 
 int job_submit(const uint8_t *const *runs, const uint64_t *lens, size_t n, bool batch, int proto, uint32_t cs,
                int ctype, size_t max_pkts, hdfs_crc32c_job **out) {
@@ -1804,17 +1989,12 @@ int job_submit(const uint8_t *const *runs, const uint64_t *lens, size_t n, bool 
   DevCtx &c = *cp;
   DeviceGuard g(c.dev);
   std::lock_guard<std::mutex> lk(c.mu);
-  int slot = -1;
-  for (int i = 0; i < kMaxJobs; i++)
-    if (!c.job_busy[i]) {
-      slot = i;
-      break;
-    }
-  if (slot < 0) return fail(HDFS_CRC32C_EINVAL, "%d verify jobs already in flight on device %d", kMaxJobs, dev);
+  JobQueue &q = jobq(c);
+  if (q.outstanding >= kMaxJobsOut)
+    return fail(HDFS_CRC32C_EINVAL, "%zu verify jobs already outstanding on device %d", kMaxJobsOut, dev);
   auto *j = new (std::nothrow) hdfs_crc32c_job;
   if (!j) return fail(HDFS_CRC32C_ENOMEM, "job");
   j->dev = dev;
-  j->slot = slot;
   j->runs.assign(runs, runs + n);
   j->lens.assign(lens, lens + n);
   j->batch = batch;
@@ -1831,62 +2011,38 @@ int job_submit(const uint8_t *const *runs, const uint64_t *lens, size_t n, bool 
   for (size_t b = 0; b < n; b++) {
     if (lens[b] <= kSmallRunBytes) continue;
     size_t same = 0;
-    for (size_t q = 0; q < n; q++) same += lens[q] == lens[b] ? 1u : 0u;
+    for (size_t q2 = 0; q2 < n; q2++) same += lens[q2] == lens[b] ? 1u : 0u;
     if (j->sel.empty() || same > j->sel.size()) {
       j->sel.clear();
-      for (size_t q = 0; q < n; q++)
-        if (lens[q] == lens[b]) j->sel.push_back(q);
+      for (size_t q2 = 0; q2 < n; q2++)
+        if (lens[q2] == lens[b]) j->sel.push_back(q2);
     }
   }
-  const bool spec = ctype != HDFS_CRC32C_CSUM_NULL && g_spec && max_pkts >= 2 && !j->sel.empty();
-  if (spec) {
-    std::vector<const uint8_t *> sruns;
-    std::vector<uint64_t> slens;
-    for (size_t b : j->sel) {
-      sruns.push_back(runs[b]);
-      slens.push_back(lens[b]);
-    }
-    SpecSlot &S = c.job_slot[slot];
-    if (!S.stream) {
-      if (hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking) != hipSuccess) {
-        (void)hipGetLastError();
-        delete j;
-        return fail(HDFS_CRC32C_EHIP, "job stream");
-      }
-    }
-    // per run at most max_count packets; the bitmap takes ceil(chunks / 8)
-    // bytes per packet (<= len / 32 + 1), first-bad one word per packet
-    const uint32_t count = uint32_t(std::min<uint64_t>(uint64_t(max_pkts), kGridMaxCount));
-    uint64_t bm_cap = 64, fbw = 0;
-    for (uint64_t l : slens) {
-      const uint64_t cr = std::min<uint64_t>(count, l / 6 + 1);
-      bm_cap += l / 32 + cr;
-      fbw += cr;
-    }
-    bm_cap = align_up(bm_cap, 256);
-    const uint64_t need = bm_cap + fbw * 4u + 256u;
-    if (need > S.scratch_cap) {
-      if (S.scratch) (void)hipFree(S.scratch);
-      S.scratch = nullptr;
-      S.scratch_cap = 0;
-      if (hipMalloc(&S.scratch, need) != hipSuccess) {
-        (void)hipGetLastError();
-        delete j;
-        return fail(HDFS_CRC32C_ENOMEM, "job scratch of %llu bytes", (unsigned long long)need);
-      }
-      S.scratch_cap = need;
-    }
-    rc = spec_launch(c, S, S.stream, sruns[0], slens[0], 0, count, proto, cs, ctype, CopyOut{}, 0, S.scratch,
-                     reinterpret_cast<uint32_t *>(S.scratch + bm_cap), j->L, uint32_t(sruns.size()), sruns.data(),
-                     slens.data());
-    if (rc) {
-      delete j;
-      return rc;
-    }
-    j->launched = true;
-  }
-  c.job_busy[slot] = true;
+  q.outstanding++;
   *out = j;
+  const bool spec = ctype != HDFS_CRC32C_CSUM_NULL && g_spec && max_pkts >= 2 && !j->sel.empty();
+  if (!spec) return HDFS_CRC32C_OK;  // all of it in the wait
+  if (batch) {  // a job of blocks: its own launch now
+    std::vector<const uint8_t *> s;
+    std::vector<uint64_t> l;
+    for (size_t b : j->sel) {
+      s.push_back(runs[b]);
+      l.push_back(lens[b]);
+    }
+    JobGroup *grp = group_launch(c, q, s.data(), l.data(), uint32_t(s.size()), proto, cs, ctype, max_pkts, &rc);
+    if (grp) {
+      j->grp = grp;
+      grp->refs = 1;
+    }
+    return HDFS_CRC32C_OK;  // (a failed launch: the blocks are verified in the wait)
+  }
+  const JobQueue::Key key{proto, ctype, cs, lens[0], max_pkts};
+  if (!q.pending.empty() && !(q.key == key)) queue_flush(c, q);
+  q.key = key;
+  j->queued = true;
+  q.pending.push_back(j);
+  if (q.pending.size() >= kSpecRunsMax || g_job_coalesce == 0 || (g_job_coalesce == 1 && !any_running(c, q)))
+    queue_flush(c, q);
   return HDFS_CRC32C_OK;
 }
 
@@ -1901,47 +2057,40 @@ int job_wait(hdfs_crc32c_job *j, hdfs_crc32c_packet *pkts, size_t max_pkts, size
   DevCtx &c = *cp;
   DeviceGuard g(c.dev);
   std::lock_guard<std::mutex> lk(c.mu);
-  struct Release {  // the slot is free again on every return path
-    DevCtx &c;
+  JobQueue &q = jobq(c);
+  struct Release {  // the job (and its launch's results, after its last job) on every return path
+    JobQueue &q;
     hdfs_crc32c_job *j;
     ~Release() {
-      c.job_busy[j->slot] = false;
+      q.outstanding--;
+      if (j->grp && --j->grp->refs == 0) delete j->grp;
       delete j;
     }
-  } rel{c, j};
+  } rel{q, j};
+  if (j->queued) queue_flush(c, q);  // this job's run goes out now, with every queued one
+  JobGroup *grp = j->grp;
+  if (grp && !grp->collected) {
+    if (!q.pending.empty() && !group_done(c, *grp)) queue_flush(c, q);  // queued behind the running launch
+    group_collect(c, q, grp);
+  }
+  if (grp && grp->rc) return grp->rc;
   const size_t n = j->runs.size();
   const size_t cap = std::min(max_pkts, j->max_pkts);
   std::vector<SpecRunResult> res(n);
   bool allow_spec = true;
-  if (j->launched) {
-    // the launch's records land in per-run scratch (count + 1 records each),
-    // then in the caller's array at the run's block
-    const size_t m = j->sel.size();
-    const size_t per = std::max<size_t>(1, std::min<uint64_t>(j->max_pkts, kGridMaxCount) + 1);
-    std::vector<hdfs_crc32c_packet> recs(per * m);
-    std::vector<hdfs_crc32c_packet *> dst(m);
-    std::vector<uint64_t> pos0(m, 0);
-    std::vector<SpecRunResult> rr(m);
-    for (size_t r = 0; r < m; r++) dst[r] = recs.data() + r * per;
-    if (m == 1) {
-      SpecResult sr;
-      if ((rc = spec_collect(c, c.job_slot[j->slot], j->L, CopyOut{}, dst[0], sr))) return rc;
-      rr[0].taken = sr.taken;
-      rr[0].end = sr.end;
-      rr[0].recorded = sr.recorded;
-      rr[0].consumed = sr.consumed;
-      rr[0].next = sr.next;
-      if (!sr.taken && n == 1) allow_spec = false;  // this stream has no run the launch takes: frame it
-    } else {
-      if ((rc = spec_collect_batch(c.job_slot[j->slot], j->L, uint32_t(m), pos0.data(), dst.data(), rr))) return rc;
-    }
-    for (size_t r = 0; r < m; r++) {
+  if (grp) {
+    // the launch's records (count + 1 per run), into the caller's array at
+    // the run's block
+    for (size_t r = 0; r < j->sel.size(); r++) {
       const size_t b = j->sel[r];
-      res[b] = rr[r];
-      if (!rr[r].taken) continue;
-      if (rr[r].recorded > cap) return fail(HDFS_CRC32C_EINVAL, "wait: %u records, room for %zu", rr[r].recorded, cap);
-      std::memcpy(pkts + b * max_pkts, dst[r], size_t(rr[r].recorded) * sizeof(hdfs_crc32c_packet));
+      const SpecRunResult &rr = grp->rr[j->grp_run + r];
+      res[b] = rr;
+      if (!rr.taken) continue;
+      if (rr.recorded > cap) return fail(HDFS_CRC32C_EINVAL, "wait: %u records, room for %zu", rr.recorded, cap);
+      std::memcpy(pkts + b * max_pkts, grp->recs.data() + (j->grp_run + r) * grp->per,
+                  size_t(rr.recorded) * sizeof(hdfs_crc32c_packet));
     }
+    if (grp->single_not_taken && n == 1) allow_spec = false;  // this stream has no run the launch takes: frame it
   }
   int first = HDFS_CRC32C_OK;
   for (size_t r = 0; r < n; r++) {
@@ -1960,7 +2109,7 @@ int job_wait(hdfs_crc32c_job *j, hdfs_crc32c_packet *pkts, size_t max_pkts, size
         if (r2) return r2;
       }
       if (rc) return rc;
-      for (size_t q = 0; q < n2; q++) out[k + q].stream_off += from;
+      for (size_t q2 = 0; q2 < n2; q2++) out[k + q2].stream_off += from;
       k += n2;
       if (n2 || used2) used = from + used2;
     }
@@ -3043,6 +3192,64 @@ void hdfs_crc32c_reader_close(hdfs_crc32c_reader *rd) {
   if (!rd) return;
   copyctl_give(rd->dev, rd->cc);  // (kept for the next reader: no device synchronisation here)
   delete rd;
+}
+
+// hdfs_datanode_read_file's copy-out (src/datanode.c:2531-2541): a reader
+// verifies the read once, each next delivers the following bytes into a
+// host staging buffer, and they are pwrite()n at the fd offset -- retried
+// until complete, as _hdfs_pwrite_all does (src/net.c:290-313).
+int hdfs_crc32c_read_packets_fd(const void *stream, uint64_t len, int proto, uint32_t chunk_size, int ctype,
+                                int64_t client_offset, int64_t read_len, int fd, int64_t fd_offset,
+                                hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts, uint64_t *consumed,
+                                uint64_t *delivered) {
+  if (npkts) *npkts = 0;
+  if (consumed) *consumed = 0;
+  if (delivered) *delivered = 0;
+  if (fd < 0 || fd_offset < 0) return fail(HDFS_CRC32C_EINVAL, "fd %d at offset %lld", fd, (long long)fd_offset);
+  if (read_len <= 0 || client_offset < 0)  // a client read (src/datanode.c:870-878: bloff, len)
+    return fail(HDFS_CRC32C_EINVAL, "read window: offset %lld, length %lld", (long long)client_offset,
+                (long long)read_len);
+  if (max_pkts && !pkts) return fail(HDFS_CRC32C_EINVAL, "null packet array");
+  if (!len) return HDFS_CRC32C_OK;
+  hdfs_crc32c_reader *rd = nullptr;
+  int rc = hdfs_crc32c_reader_open(stream, len, proto, chunk_size, ctype, client_offset, read_len, max_pkts, &rd);
+  if (rc < 0) return rc;
+  constexpr uint64_t kStage = uint64_t(4) << 20;
+  std::vector<uint8_t> buf(size_t(std::min<uint64_t>(uint64_t(read_len), kStage)));
+  size_t n_all = 0;
+  uint64_t got_all = 0, used = 0;
+  for (;;) {
+    const hdfs_crc32c_iovec iov{buf.data(), buf.size()};
+    size_t n = 0;
+    uint64_t u = 0, got = 0;
+    rc = hdfs_crc32c_reader_next(rd, &iov, 1, pkts ? pkts + n_all : nullptr, max_pkts - n_all, &n, &u, &got);
+    if (rc < 0) break;
+    n_all += n;
+    used = u;
+    for (uint64_t w = 0; w < got;) {
+      const ssize_t k = pwrite(fd, buf.data() + w, size_t(got - w), off_t(fd_offset + int64_t(got_all + w)));
+      if (k < 0 && errno == EINTR) continue;
+      if (k <= 0) {
+        const int e = k < 0 ? errno : 0;
+        got_all += w;
+        hdfs_crc32c_reader_close(rd);
+        if (npkts) *npkts = n_all;
+        if (consumed) *consumed = used;
+        if (delivered) *delivered = got_all;
+        return fail(HDFS_CRC32C_EIO, "pwrite to fd %d at %lld: %s", fd, (long long)(fd_offset + int64_t(got_all)),
+                    e ? std::strerror(e) : "wrote nothing (end of file)");
+      }
+      w += uint64_t(k);
+    }
+    got_all += got;
+    if (rc != HDFS_CRC32C_AGAIN) break;
+  }
+  hdfs_crc32c_reader_close(rd);
+  if (rc < 0) return rc;
+  if (npkts) *npkts = n_all;
+  if (consumed) *consumed = used;
+  if (delivered) *delivered = got_all;
+  return rc;
 }
 
 int hdfs_crc32c_verify_packets_submit(const void *stream, uint64_t len, int proto, uint32_t chunk_size, int ctype,

@@ -46,6 +46,7 @@ uint32_t _hdfs_sw_crc32c(uint32_t crc, const void *buf, unsigned len);
 #define HDFS_CRC32C_ENODEV (-2)   /* no usable gfx950 device / HIP runtime */
 #define HDFS_CRC32C_ENOMEM (-3)   /* device or pinned allocation failed */
 #define HDFS_CRC32C_EHIP (-4)     /* HIP runtime error (see last_error) */
+#define HDFS_CRC32C_EIO (-5)      /* writing a read's bytes to a file descriptor failed (errno in last_error) */
 /* Datanode-level results reuse the reference's enum hdfs_error_numeric
  * values (include/objects.h:21-113; checked by compiling that header). */
 #define HDFS_CRC32C_ERR_DATANODE_UNSUPPORTED_CHECKSUM 8
@@ -310,10 +311,15 @@ int hdfs_crc32c_read_packets(const void *stream, uint64_t len, int proto, uint32
  * datanode verifying a stream of received blocks): submit launches the
  * verify and returns; hdfs_crc32c_job_wait returns exactly what
  * hdfs_crc32c_verify_packets would (records, consumed, first error) and
- * releases the job.  Up to 4 jobs per device are in flight at once (a fifth
- * submit is EINVAL); jobs overlap on the GPU, so one block's launch ramp and
- * tail run under another's steady state.  A run of equal packets is
- * verified by the speculative launch at submit; whatever it does not take
+ * releases the job.  Up to 64 jobs per device may be outstanding (submitted,
+ * not yet waited for; one more is EINVAL).  Jobs submitted while an earlier
+ * launch is still running queue and go out together as ONE batch launch
+ * (as hdfs_crc32c_verify_blocks_submit's) -- when a submit finds the GPU
+ * idle, when a wait needs a queued job or would block on a running launch,
+ * or at 16 queued runs or a run of another length or layout -- so a stream
+ * of blocks pays the launch's fixed cost once per batch; up to 4 launches
+ * run at once (a submit or wait may first collect the oldest).  A run of
+ * equal packets is verified by the speculative launch; whatever it does not take
  * (another packet size, more than 65 536 packets, no run at all) is framed
  * and verified inside the wait.  The stream's bytes must stay unchanged, and
  * written before the submit (synchronise whatever wrote them), until the
@@ -369,6 +375,23 @@ int hdfs_crc32c_reader_open(const void *stream, uint64_t len, int proto, uint32_
 int hdfs_crc32c_reader_next(hdfs_crc32c_reader *rd, const hdfs_crc32c_iovec *iov, int iovcnt,
     hdfs_crc32c_packet *pkts, size_t max_pkts, size_t *npkts, uint64_t *consumed, uint64_t *delivered);
 void hdfs_crc32c_reader_close(hdfs_crc32c_reader *rd);
+
+/* A client read whose bytes go to a FILE DESCRIPTOR (the reference's
+ * hdfs_datanode_read_file: _recv_packet_copy_data pwrite()s each verified
+ * packet's bytes at fdoffset and advances it, src/datanode.c:2531-2541,
+ * src/net.c:290-313): the read [client_offset, client_offset + read_len) of
+ * the stream under hdfs_crc32c_read_packets' rules -- records, status,
+ * consumed as that call returns them with a destination of read_len bytes --
+ * with the delivered bytes written to fd at fd_offset, fd_offset +
+ * *delivered ... (pwrite, retried until complete; the fd may be a regular
+ * file, a pipe is not seekable and fails).  The stream is verified once; the
+ * bytes leave through a bounded host staging buffer (device streams: D2H)
+ * in stream order, so a failing write leaves exactly the bytes before it
+ * written: HDFS_CRC32C_EIO, *delivered = the bytes written, errno's text in
+ * hdfs_crc32c_last_error().  read_len > 0 (a window; no READ_ALL). */
+int hdfs_crc32c_read_packets_fd(const void *stream, uint64_t len, int proto, uint32_t chunk_size, int ctype,
+    int64_t client_offset, int64_t read_len, int fd, int64_t fd_offset, hdfs_crc32c_packet *pkts, size_t max_pkts,
+    size_t *npkts, uint64_t *consumed, uint64_t *delivered);
 
 /* ---- write path: outgoing data packets ---------------------------------- */
 /* One outgoing data packet, as _send_packet sizes it and

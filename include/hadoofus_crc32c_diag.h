@@ -80,6 +80,13 @@ int hdfs_crc32c_set_runs(int on);
  * of a run of equal packets first, 0 always frames the run on the device
  * first (the round-3 path) -- for same-process A/Bs.  Env HDFS_CRC32C_SPEC. */
 int hdfs_crc32c_set_speculation(int on);
+/* Asynchronous jobs (hdfs_crc32c_verify_packets_submit): 1 (default, the
+ * product) queues a job submitted while a launch runs and sends the queue
+ * out as one batch launch; 0 launches every job at its submit (the round-5
+ * path, for same-process A/Bs); 2 queues even on an idle GPU (the queue goes
+ * out only when a wait needs it, at 16 runs or on a key change: launch
+ * counts a test can predict).  Env HDFS_CRC32C_JOB_COALESCE. */
+int hdfs_crc32c_set_job_coalesce(int mode);
 /* Speculative one-launch verifies since the last reset: out4 = {launches,
  * eligible (packet 0 starts a run of equal packets), taken (no header off
  * the prediction), header exceptions}; reset != 0 clears them. */

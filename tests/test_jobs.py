@@ -6,7 +6,9 @@ speculative launch at submit took the run, handed it back (a header off the
 run), was never tried (no run of whole-chunk packets, a short stream), or
 took only part of it (more packets than one pass, another size after it);
 with four jobs in flight at once, waited in any order, and with synchronous
-calls in between."""
+calls in between.  Jobs submitted while a launch runs share one batch
+launch (round 6): a stream of 16 blocks, one job each, is verified in a
+few launches, every job's result still the oracle's."""
 import numpy as np
 import pytest
 
@@ -89,16 +91,19 @@ def test_gpu_jobs_many_passes(engine, oracle):
 
 @pytest.mark.gpu
 def test_gpu_jobs_limit_and_interleaving(engine, oracle):
-    """A fifth job while four are in flight is refused (and the four still
+    """A 65th job while 64 are outstanding is refused (and the 64 still
     complete correctly); synchronous verifies and reads run between a submit
-    and its wait; a waited slot takes a new job."""
+    and its wait; a waited job makes room for a new one."""
     dl = [65536] * 100
     s, _ = build_stream(oracle.crc32c, 2, 512, CSUM_CRC32C, dl, seed=3, corrupt=[(50, 7)])
     want = oracle.verify_packets(s)
     bufs = [_dev(engine, s, i) for i in range(5)]
-    jobs = [engine.VerifyJob(p, len(s)) for _, p in bufs[:4]]
+    jobs = [engine.VerifyJob(bufs[i % 4][1], len(s)) for i in range(64)]
     with pytest.raises(engine.CRC32CError):
         engine.VerifyJob(bufs[4][1], len(s))
+    for j in jobs[4:]:
+        assert j.wait() == want
+    jobs = jobs[:4]
     # synchronous calls while the jobs are in flight
     assert engine.verify_packets(None, dptr=bufs[4][1], nbytes=len(s)) == want
     dst = engine.DeviceBuffer(sum(dl))
@@ -190,5 +195,138 @@ def test_gpu_blocks_taken_in_one_launch(engine, oracle):
     assert tuple(out)[:3] == (1, 1, 1), tuple(out)
     assert got == [oracle.verify_packets(st) for st in streams + [last]]
     lb[0].free()
+    for bb, _ in bufs:
+        bb.free()
+
+
+def _diag():
+    import ctypes
+    from hadoofus_amd import abi, build
+    return abi.bind_diag(abi.bind_product(ctypes.CDLL(build.DIAG_LIB)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("order", ["in_order", "reverse", "window4"])
+def test_gpu_jobs_coalesce_stream_of_blocks(engine, oracle, order):
+    """A datanode's stream of 16 received blocks, one job per block, with a
+    bad packet in block 9 (and an irregular header in block 12, which voids
+    the batch launch it lands in: those blocks are verified one by one in
+    their waits): every job equals the oracle's verify of its block.  Jobs
+    submitted while a launch runs go out together, so 16 jobs submitted back
+    to back take at most 3 launches (the first alone, the rest as batches)."""
+    diag = _diag()
+    streams = [_block(oracle, k, corrupt=[(61, 5)] if k == 9 else [],
+                      **({"seqnos": [k2 + (3 if k2 > 70 else 0) for k2 in range(100)]} if k == 12 else {}))
+               for k in range(16)]
+    bufs = [_dev(engine, st, k % 2) for k, st in enumerate(streams)]
+    want = [oracle.verify_packets(st) for st in streams]
+    assert want[9][0] == BAD and want[12][0] == 0
+    out = (__import__("ctypes").c_uint64 * 4)()
+    diag.hdfs_crc32c_diag_spec_stats(out, 1)
+    got = {}
+    if order == "window4":  # at most 4 outstanding: wait for the oldest before the next submit
+        q = []
+        for k, ((_, p), st) in enumerate(zip(bufs, streams)):
+            if len(q) == 4:
+                k0, j0 = q.pop(0)
+                got[k0] = j0.wait()
+            q.append((k, engine.VerifyJob(p, len(st), lib=diag)))
+        for k0, j0 in q:
+            got[k0] = j0.wait()
+    else:
+        jobs = [engine.VerifyJob(p, len(st), lib=diag) for (_, p), st in zip(bufs, streams)]
+        for k in (range(16) if order == "in_order" else reversed(range(16))):
+            got[k] = jobs[k].wait()
+    diag.hdfs_crc32c_diag_spec_stats(out, 1)
+    for k in range(16):
+        assert got[k] == want[k], (order, k)
+    launches = out[0]
+    if order != "window4":
+        # the first job alone, the other 15 in one batch -- plus the single
+        # passes of the blocks of a batch that block 12 voided
+        assert launches <= 2 + 15, tuple(out)
+        assert out[2] >= 1, tuple(out)  # a launch was taken
+    for bb, _ in bufs:
+        bb.free()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,want_launches", [(2, 1), (0, 16)])
+def test_gpu_jobs_coalesce_counts_launches(engine, oracle, mode, want_launches):
+    """16 clean equal blocks submitted back to back (diagnostic build).  Hold
+    mode (2: queue even on an idle GPU, so the count does not depend on how
+    fast the host submits): the 16th submit fills the queue and all 16 go out
+    as ONE batch launch, taken.  Mode 0 (the round-5 path): one launch per
+    job.  Every result the oracle's either way."""
+    diag = _diag()
+    streams = [_block(oracle, k) for k in range(16)]
+    bufs = [_dev(engine, st) for st in streams]
+    want = [oracle.verify_packets(st) for st in streams]
+    out = (__import__("ctypes").c_uint64 * 4)()
+    assert diag.hdfs_crc32c_set_job_coalesce(mode) == 0
+    try:
+        diag.hdfs_crc32c_diag_spec_stats(out, 1)
+        jobs = [engine.VerifyJob(p, len(st), lib=diag) for (_, p), st in zip(bufs, streams)]
+        got = [j.wait() for j in jobs]
+        diag.hdfs_crc32c_diag_spec_stats(out, 1)
+    finally:
+        diag.hdfs_crc32c_set_job_coalesce(1)
+    assert got == want
+    assert tuple(out)[:3] == (want_launches,) * 3, tuple(out)
+    for bb, _ in bufs:
+        bb.free()
+
+
+@pytest.mark.gpu
+def test_gpu_jobs_hold_flushes_at_wait(engine, oracle):
+    """Hold mode, 5 jobs queued: the first wait sends all 5 out as one launch,
+    whichever job it is for; then 3 more jobs of another length (a key
+    change sends nothing out by itself while the queue is empty) go out at
+    their first wait."""
+    diag = _diag()
+    a = [_block(oracle, k, corrupt=[(k, 1)]) for k in range(5)]
+    b = [_block(oracle, 10 + k, dl=[65536] * 80) for k in range(3)]  # (> 64 packets: not a short run)
+    bufs = [_dev(engine, st) for st in a + b]
+    want = [oracle.verify_packets(st) for st in a + b]
+    out = (__import__("ctypes").c_uint64 * 4)()
+    assert diag.hdfs_crc32c_set_job_coalesce(2) == 0
+    try:
+        diag.hdfs_crc32c_diag_spec_stats(out, 1)
+        ja = [engine.VerifyJob(p, len(st), lib=diag) for (_, p), st in zip(bufs[:5], a)]
+        assert ja[3].wait() == want[3]
+        diag.hdfs_crc32c_diag_spec_stats(out, 0)
+        assert out[0] == 1, tuple(out)
+        jb = [engine.VerifyJob(p, len(st), lib=diag) for (_, p), st in zip(bufs[5:], b)]
+        for k in (0, 1, 2, 4):
+            assert ja[k].wait() == want[k], k
+        for k in (2, 0, 1):
+            assert jb[k].wait() == want[5 + k], k
+        diag.hdfs_crc32c_diag_spec_stats(out, 1)
+    finally:
+        diag.hdfs_crc32c_set_job_coalesce(1)
+    assert tuple(out)[:3] == (2, 2, 2), tuple(out)
+    for bb, _ in bufs:
+        bb.free()
+
+
+@pytest.mark.gpu
+def test_gpu_jobs_coalesce_mixed_keys(engine, oracle):
+    """Jobs of alternating lengths and chunk sizes (each key change sends the
+    queue out), a short last block and a CRC32 v1 block among them, waited
+    out of order: each equals the oracle's verify."""
+    specs = []
+    for k in range(12):
+        if k % 4 == 3:
+            specs.append((_block(oracle, k, dl=[65536] * 7 + [1000]), 2, 512, CSUM_CRC32C))
+        elif k % 4 == 2:
+            specs.append((_block(oracle, k, proto=1, ctype=CSUM_CRC32, last_empty=False, corrupt=[(3, 3)]),
+                          1, 512, CSUM_CRC32))
+        else:
+            specs.append((_block(oracle, k, dl=[65536] * (100 if k % 2 else 80)), 2, 512, CSUM_CRC32C))
+    bufs = [_dev(engine, st, k % 3) for k, (st, *_r) in enumerate(specs)]
+    want = [oracle.verify_packets(st, pr, cs, ct) for st, pr, cs, ct in specs]
+    jobs = [engine.VerifyJob(p, len(st), pr, cs, ct) for (_, p), (st, pr, cs, ct) in zip(bufs, specs)]
+    for k in [5, 0, 11, 3, 1, 2, 4, 6, 10, 9, 8, 7]:
+        assert jobs[k].wait() == want[k], k
     for bb, _ in bufs:
         bb.free()
