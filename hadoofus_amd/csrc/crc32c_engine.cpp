@@ -114,7 +114,9 @@ int g_spec = HDFS_KNOB("HDFS_CRC32C_SPEC", 1);
 // queue a job submitted while a launch runs and send the queue out as one
 // batch launch; 0 (diagnostic A/B) launch every job at its submit, as round
 // 5 did; 2 (diagnostic, deterministic tests) queue even on an idle GPU --
-// the queue goes out only when a wait needs it, when full, or on a key change.
+// the queue goes out only when a wait needs it, when full, or on a key change;
+// 3 (diagnostic A/B) as 1, but a wait that blocks on a running launch sends
+// the queue out behind it only if it holds two runs or more.
 int g_job_coalesce = HDFS_KNOB("HDFS_CRC32C_JOB_COALESCE", 1);
 // Small-call input stage: 1 fine-grained VRAM written through the BAR when
 // the device is large-BAR, else (and 0) pinned host memory.
@@ -1534,7 +1536,11 @@ int hdfs_crc32c_mailbox_create(hdfs_crc32c_mailbox **mb, uint32_t idle_ms) {
     // streams come from a queue pool of their own, where the mailbox is the
     // only one.
     int lo = 0, hi = 0;
-    if (g_mb_queue && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess && hi != lo) {
+    if (g_mb_queue == 2) {  // diagnostic: a CU-masked stream (all CUs), which the runtime never pools
+      std::vector<uint32_t> mask(size_t((c->num_cu + 31) / 32), 0u);
+      for (int cu = 0; cu < c->num_cu; cu++) mask[size_t(cu / 32)] |= 1u << (cu % 32);
+      HIPCHK(hipExtStreamCreateWithCUMask(&c->mb_stream, uint32_t(mask.size()), mask.data()));
+    } else if (g_mb_queue && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess && hi != lo) {
       HIPCHK(hipStreamCreateWithPriority(&c->mb_stream, hipStreamNonBlocking, hi));
     } else {
       HIPCHK(hipStreamCreateWithFlags(&c->mb_stream, hipStreamNonBlocking));
@@ -1611,7 +1617,8 @@ int hdfs_crc32c_set_speculation(int on) {
 }
 
 int hdfs_crc32c_set_job_coalesce(int mode) {
-  if (mode < 0 || mode > 2) return fail(HDFS_CRC32C_EINVAL, "job coalescing 0 (off), 1 (product) or 2 (hold)");
+  if (mode < 0 || mode > 3)
+    return fail(HDFS_CRC32C_EINVAL, "job coalescing 0 (off), 1 (product), 2 (hold) or 3 (no lone run behind a launch)");
   g_job_coalesce = mode;
   return HDFS_CRC32C_OK;
 }

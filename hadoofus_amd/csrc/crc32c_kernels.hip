@@ -1955,9 +1955,25 @@ DEV void copy_staged(const uint8_t *const *lsrc, const uintptr_t *ldst, const ui
 // x^(8 dd) mod P (VALU, no table levels).  Results go to the same pinned
 // output block as small_chunks_kernel, its completion sequence number last.
 // Requests must have chunk_size % 64 == 0 or a single chunk (else the host
-// launches small_chunks_kernel).  Exit: a quit request, or idle_ticks
-// (100 MHz s_memrealtime) without a request -- every wave leaves through the
-// same barrier-synchronised test; status[0] = (epoch << 1) | alive.
+// launches small_chunks_kernel).  Exit: a quit request, idle_ticks (100 MHz
+// s_memrealtime) without a request, or another packet written to the
+// kernel's own hardware queue (below) -- every wave leaves through the same
+// barrier-synchronised test; status[0] = (epoch << 1) | alive.
+// Yield: a persistent kernel holds up every packet queued behind it on its
+// hardware queue, and the runtime shares a process's queues among its
+// streams (at most GPU_MAX_HW_QUEUES per priority level: a host process with
+// that many high-priority streams of its own shares one with the mailbox's;
+// tools/mb_queue_share.py measured such a stream's work waiting the whole
+// 50 ms idle exit).  While idle, wave 0 also polls the write index of the
+// AQL queue it was dispatched from (amd_queue_t.write_dispatch_id, through
+// the queue pointer the CP passes in SGPRs): once anything is written behind
+// it, the kernel leaves as on an idle exit, and the next call relaunches it
+// behind that work.
+constexpr unsigned kAqlWriteIdOff = 56;  // offsetof(amd_queue_t, write_dispatch_id) (hsa/amd_hsa_queue.h)
+DEV uint64_t aql_write_index() {
+  const char *q = (const char *)(unsigned long long)(__builtin_amdgcn_queue_ptr());
+  return *(const volatile uint64_t *)(q + kAqlWriteIdOff);  // system-coherent (sc0 sc1)
+}
 
 DEV u32x4 sysload16(const __amdgpu_buffer_rsrc_t r, uint32_t off) {
   // sc0 sc1: system-coherent, never served from a stale cache line
@@ -2047,17 +2063,18 @@ __global__ __launch_bounds__(1024) void mailbox_kernel(const uint32_t *__restric
   const uint32_t hsel = (lane >> 3) & 1u, loff = 16u * (4u * (lane & 7u) + (lane >> 4));
   uint32_t last = seq0;
   uint64_t t_idle = __builtin_amdgcn_s_memrealtime();
+  const uint64_t qw0 = tid == 0 ? aql_write_index() : 0u;  // the queue's write index at our start
   for (;;) {
     if (tid == 0) {
       u32x4 v;
-      for (;;) {
+      for (uint32_t spin = 0;; spin++) {
         // volatile: a plain (or buffer-intrinsic) load is hoisted out of the
         // loop by the compiler, which then spins on a stale value; volatile
         // global loads are also system-coherent (sc0 sc1) on gfx950
         v = *(const volatile GAS u32x4 *)(const GAS uint8_t *)req;
         if (v.x != last) break;
-        if (__builtin_amdgcn_s_memrealtime() - t_idle > idle_ticks) {
-          v = u32x4{last, 0u, kMbQuitFlag, 0u};
+        if (__builtin_amdgcn_s_memrealtime() - t_idle > idle_ticks || ((spin & 15u) == 15u && aql_write_index() != qw0)) {
+          v = u32x4{last, 0u, kMbQuitFlag, 0u};  // idle, or work queued behind us: leave
           break;
         }
         __builtin_amdgcn_s_sleep(1);

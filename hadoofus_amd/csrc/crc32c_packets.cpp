@@ -1796,7 +1796,9 @@ struct JobGroup {
   size_t per = 0;                          // records per run in recs
   bool collected = false, single_not_taken = false;
   int rc = 0;                              // the collection's status
-  std::vector<hdfs_crc32c_packet> recs;    // [m][per]
+  // [m][per], not zero-filled: per is max_pkts-sized (up to 65 537) and
+  // only the records a run produces are written and read
+  std::unique_ptr<hdfs_crc32c_packet[]> recs;
   std::vector<SpecRunResult> rr;           // [m]
   int refs = 0;                            // jobs not yet waited for
 };
@@ -1854,12 +1856,21 @@ bool group_done(DevCtx &c, const JobGroup &g) {
 int group_collect(DevCtx &c, JobQueue &q, JobGroup *g) {
   if (g->collected) return g->rc;
   SpecSlot &S = c.job_slot[g->slot];
-  g->recs.assign(g->per * g->m, hdfs_crc32c_packet{});
+  g->recs.reset(new (std::nothrow) hdfs_crc32c_packet[g->per * g->m]);
   g->rr.assign(g->m, SpecRunResult{});
+  if (!g->recs) {
+    g->collected = true;
+    g->rc = fail(HDFS_CRC32C_ENOMEM, "records of %u runs", g->m);
+    // the launch still owns its slot until it has run: wait for it first
+    (void)hipStreamSynchronize(S.stream);
+    c.job_busy[g->slot] = false;
+    q.running.erase(std::remove(q.running.begin(), q.running.end(), g), q.running.end());
+    return g->rc;
+  }
   int rc;
   if (g->m == 1) {
     SpecResult sr;
-    rc = spec_collect(c, S, g->L, CopyOut{}, g->recs.data(), sr);
+    rc = spec_collect(c, S, g->L, CopyOut{}, g->recs.get(), sr);
     g->rr[0].taken = sr.taken;
     g->rr[0].end = sr.end;
     g->rr[0].recorded = sr.recorded;
@@ -1869,7 +1880,7 @@ int group_collect(DevCtx &c, JobQueue &q, JobGroup *g) {
   } else {
     std::vector<hdfs_crc32c_packet *> dst(g->m);
     std::vector<uint64_t> pos0(g->m, 0);
-    for (uint32_t r = 0; r < g->m; r++) dst[r] = g->recs.data() + r * g->per;
+    for (uint32_t r = 0; r < g->m; r++) dst[r] = g->recs.get() + r * g->per;
     rc = spec_collect_batch(S, g->L, g->m, pos0.data(), dst.data(), g->rr);
   }
   g->collected = true;
@@ -2041,7 +2052,7 @@ int job_submit(const uint8_t *const *runs, const uint64_t *lens, size_t n, bool 
   q.key = key;
   j->queued = true;
   q.pending.push_back(j);
-  if (q.pending.size() >= kSpecRunsMax || g_job_coalesce == 0 || (g_job_coalesce == 1 && !any_running(c, q)))
+  if (q.pending.size() >= kSpecRunsMax || g_job_coalesce == 0 || (g_job_coalesce != 2 && !any_running(c, q)))
     queue_flush(c, q);
   return HDFS_CRC32C_OK;
 }
@@ -2070,7 +2081,10 @@ int job_wait(hdfs_crc32c_job *j, hdfs_crc32c_packet *pkts, size_t max_pkts, size
   if (j->queued) queue_flush(c, q);  // this job's run goes out now, with every queued one
   JobGroup *grp = j->grp;
   if (grp && !grp->collected) {
-    if (!q.pending.empty() && !group_done(c, *grp)) queue_flush(c, q);  // queued behind the running launch
+    // the queue goes out behind the running launch (diagnostic mode 3: only
+    // two runs or more; a single one waits for the next submit or wait)
+    if (!q.pending.empty() && (g_job_coalesce != 3 || q.pending.size() >= 2) && !group_done(c, *grp))
+      queue_flush(c, q);
     group_collect(c, q, grp);
   }
   if (grp && grp->rc) return grp->rc;
@@ -2087,7 +2101,7 @@ int job_wait(hdfs_crc32c_job *j, hdfs_crc32c_packet *pkts, size_t max_pkts, size
       res[b] = rr;
       if (!rr.taken) continue;
       if (rr.recorded > cap) return fail(HDFS_CRC32C_EINVAL, "wait: %u records, room for %zu", rr.recorded, cap);
-      std::memcpy(pkts + b * max_pkts, grp->recs.data() + (j->grp_run + r) * grp->per,
+      std::memcpy(pkts + b * max_pkts, grp->recs.get() + (j->grp_run + r) * grp->per,
                   size_t(rr.recorded) * sizeof(hdfs_crc32c_packet));
     }
     if (grp->single_not_taken && n == 1) allow_spec = false;  // this stream has no run the launch takes: frame it

@@ -85,7 +85,9 @@ int hdfs_crc32c_set_speculation(int on);
  * out as one batch launch; 0 launches every job at its submit (the round-5
  * path, for same-process A/Bs); 2 queues even on an idle GPU (the queue goes
  * out only when a wait needs it, at 16 runs or on a key change: launch
- * counts a test can predict).  Env HDFS_CRC32C_JOB_COALESCE. */
+ * counts a test can predict); 3 as 1, but a wait blocking on a running
+ * launch sends the queue out behind it only if it holds two runs or more.
+ * Env HDFS_CRC32C_JOB_COALESCE. */
 int hdfs_crc32c_set_job_coalesce(int mode);
 /* Speculative one-launch verifies since the last reset: out4 = {launches,
  * eligible (packet 0 starts a run of equal packets), taken (no header off

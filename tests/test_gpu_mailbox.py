@@ -163,6 +163,55 @@ def test_mailbox_keeps_its_own_queue(engine, oracle):
             b.free()
 
 
+@pytest.mark.parametrize("nhi", [4, 8])
+def test_mailbox_yields_on_a_shared_queue(engine, oracle, nhi):
+    """A host process that already holds GPU_MAX_HW_QUEUES (4) or more
+    high-priority streams of its own leaves the mailbox's high-priority
+    stream no queue to itself: one of those streams shares its hardware
+    queue, and before round 6 its work waited the kernel's whole 50 ms idle
+    exit (tools/mb_queue_share.py: 47.8 ms).  The resident kernel now watches
+    its queue's write index and leaves as soon as anything is queued behind
+    it: every stream's work completes within a few ms, and the next mailbox
+    call relaunches it and is served correctly."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    vp = ctypes.c_void_p
+    hip.hipStreamCreateWithPriority.argtypes = [ctypes.POINTER(vp), ctypes.c_uint, ctypes.c_int]
+    hip.hipDeviceGetStreamPriorityRange.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
+    hip.hipMemsetAsync.argtypes = [vp, ctypes.c_int, ctypes.c_size_t, vp]
+    hip.hipStreamSynchronize.argtypes = [vp]
+    hip.hipStreamDestroy.argtypes = [vp]
+    lo, hi = ctypes.c_int(0), ctypes.c_int(0)
+    assert hip.hipDeviceGetStreamPriorityRange(ctypes.byref(lo), ctypes.byref(hi)) == 0
+    scratch = engine.DeviceBuffer(4096)
+    streams = []
+    small = np.arange(2048, dtype=np.uint32).astype(np.uint8)
+    try:
+        for _ in range(nhi):
+            s = vp()
+            assert hip.hipStreamCreateWithPriority(ctypes.byref(s), 1, hi.value) == 0
+            assert hip.hipMemsetAsync(scratch.ptr, 0, 64, s) == 0
+            assert hip.hipStreamSynchronize(s) == 0
+            streams.append(s)
+        with engine.Mailbox() as mb:
+            for rep in range(2):
+                assert engine.crc32c(0, small) == oracle.crc32c(0, small)  # served (launched, or relaunched)
+                time.sleep(0.002)
+                for k, s in enumerate(streams):
+                    t0 = time.perf_counter()
+                    assert hip.hipMemsetAsync(scratch.ptr, 1, 64, s) == 0
+                    assert hip.hipStreamSynchronize(s) == 0
+                    dt = time.perf_counter() - t0
+                    assert dt < 0.01, (nhi, rep, k, dt)
+            assert engine.crc32c(0, small) == oracle.crc32c(0, small)
+            calls, launches = mb.stats()
+            assert calls == 3 and 1 <= launches <= 3, (calls, launches)
+    finally:
+        for s in streams:
+            hip.hipStreamDestroy(s)
+        scratch.free()
+
+
 def test_mailbox_one_per_device(engine):
     with engine.Mailbox():
         with pytest.raises(engine.CRC32CError):

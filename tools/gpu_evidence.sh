@@ -8,8 +8,9 @@
 # C4), d (device-stream + small-call benches), q (SQ/TA/TCP counters of the
 # compute and verify kernels, tools/pmc_sq.py), s (phase stamps of the
 # speculative verify, tools/spec_phases.py), r (reader / copy costs:
-# tools/reader_sizes.py, reader_calls.py, copy_phases.py); default tbpd,
-# one call.
+# tools/reader_sizes.py, reader_calls.py, copy_phases.py), j (job
+# coalescing on/off, tools/jobs_coalesce_ab.py), m (streams sharing the
+# mailbox's hardware queue, tools/mb_queue_share.py); default tbpd, one call.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
@@ -47,4 +48,8 @@ has s && cat ${O}_spec_phases.json
 has r && step reader_sizes timeout -k 10 300 python tools/reader_sizes.py ${O}_reader_sizes.json > /dev/null 2> ${O}_reader_sizes.err
 has r && step reader_calls timeout -k 10 300 python tools/reader_calls.py ${O}_reader_calls.json > /dev/null 2> ${O}_reader_calls.err
 has r && step copy_phases timeout -k 10 300 python tools/copy_phases.py ${O}_copy_phases.json > /dev/null 2> ${O}_copy_phases.err
+has j && step jobs_ab timeout -k 10 300 python tools/jobs_coalesce_ab.py ${O}_jobs_ab.json > /dev/null 2> ${O}_jobs_ab.err
+has j && cat ${O}_jobs_ab.json | tail -3
+has m && step mb_share timeout -k 10 300 python tools/mb_queue_share.py ${O}_mb_share.json > ${O}_mb_share.log 2>&1
+has m && cat ${O}_mb_share.log
 exit 0

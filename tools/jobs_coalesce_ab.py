@@ -24,7 +24,7 @@ def main():
     rounds = []
     for r in range(3):
         one = {}
-        for mode in ((1, 0) if r % 2 else (0, 1)):
+        for mode in ((1, 3, 0) if r % 2 else (0, 3, 1)):
             assert dsb.lib.hdfs_crc32c_set_job_coalesce(mode) == 0
             one[f"coalesce{mode}"] = dsb.pipelined_blocks(blk, nblk, 2048 * 65536)
             print(json.dumps({"round": r, "mode": mode, "jobs": one[f"coalesce{mode}"]["jobs"]}), flush=True)
@@ -32,10 +32,11 @@ def main():
     dsb.lib.hdfs_crc32c_set_job_coalesce(1)
     keys = ("sync", "jobs", "jobs_inflight8", "jobs_inflight16", "batch4", "batch8", "batch16")
     best = {f"coalesce{m}": {k: min(rd[f"coalesce{m}"][k]["us_per_block"] for rd in rounds) for k in keys}
-            for m in (0, 1)}
+            for m in (0, 1, 3)}
     res = {"rounds": rounds, "best_us_per_block": best,
            "note": "diagnostic build; us per 128 MiB block, best of 3 interleaved rounds (each itself best of 3); "
-                   "coalesce1 = the product policy, coalesce0 = every job launched at its submit (round 5)"}
+                   "coalesce1 = the product policy, coalesce0 = every job launched at its submit (round 5), "
+                   "coalesce3 = as 1 but no lone run sent out behind a running launch"}
     with open(out_path, "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(best))
