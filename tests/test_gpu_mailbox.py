@@ -172,7 +172,9 @@ def test_mailbox_yields_on_a_shared_queue(engine, oracle, nhi):
     exit (tools/mb_queue_share.py: 47.8 ms).  The resident kernel now watches
     its queue's write index and leaves as soon as anything is queued behind
     it: every stream's work completes within a few ms, and the next mailbox
-    call relaunches it and is served correctly."""
+    call relaunches it and is served correctly.  tools/probes/queue_ids.hip
+    showed the write index moving while the read index stays at the running
+    dispatch (profiles/r06/r6d_queue_ids.txt)."""
     import ctypes
     hip = ctypes.CDLL("libamdhip64.so")
     vp = ctypes.c_void_p
@@ -206,6 +208,15 @@ def test_mailbox_yields_on_a_shared_queue(engine, oracle, nhi):
             assert engine.crc32c(0, small) == oracle.crc32c(0, small)
             calls, launches = mb.stats()
             assert calls == 3 and 1 <= launches <= 3, (calls, launches)
+            # a device-wide synchronisation and a free (which implies one) no
+            # longer wait for the idle exit either: the runtime queues a marker
+            # behind the kernel, which then leaves
+            t0 = time.perf_counter()
+            engine.device_sync()
+            buf = engine.DeviceBuffer(1 << 20)
+            buf.free()
+            assert time.perf_counter() - t0 < 0.01
+            assert engine.crc32c(0, small) == oracle.crc32c(0, small)
     finally:
         for s in streams:
             hip.hipStreamDestroy(s)
