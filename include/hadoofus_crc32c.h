@@ -488,19 +488,18 @@ int hdfs_crc32c_host_free(void *p);
  * their one-launch path.  The resident kernel exits on its own after idle_ms
  * without a request (0: 50 ms; the next call relaunches it) and on destroy.
  * While a mailbox is open the engine's bulk kernels leave one CU per XCD to
- * it.  The resident kernel runs on a high-priority stream, a hardware queue
- * of its own (on a queue shared with other streams, work queued behind it
- * would wait for its idle exit).  A device-wide synchronisation (hipDeviceSynchronize, torch.cuda.synchronize)
- * waits for the resident kernel's idle exit: synchronise streams instead.
- * The same holds for calls that free or re-allocate device or pinned memory
- * (hdfs_crc32c_dev_free, hdfs_crc32c_host_free, and an engine call whose
- * internal scratch has to grow): the runtime may wait for every stream of
- * the device there, i.e. up to idle_ms for the resident kernel.  Allocate
- * before opening a mailbox, or close it around re-allocations.
+ * it.  The resident kernel runs on a high-priority stream, usually a
+ * hardware queue of its own; a process with GPU_MAX_HW_QUEUES or more
+ * high-priority streams shares one with it.  Anything queued behind the
+ * kernel on its queue -- another stream's work there, the marker a NULL-
+ * stream copy, a free or a device-wide synchronisation puts on it -- makes it
+ * leave at once (it watches its AQL queue's write index), and the next call
+ * relaunches it: such work waits microseconds, not idle_ms (round 5's
+ * 50 ms stalls, profiles/r06/r6c_mb_share.json vs r6e_mb_share.json).
  * One mailbox per device (EBUSY-style HDFS_CRC32C_EINVAL for a second). */
 typedef struct hdfs_crc32c_mailbox hdfs_crc32c_mailbox;
 int hdfs_crc32c_mailbox_create(hdfs_crc32c_mailbox **mb, uint32_t idle_ms);
-/* Calls served by the resident kernel and kernel launches (first + relaunches after idle exits). */
+/* Calls served by the resident kernel and kernel launches (first + relaunches after idle exits and yields). */
 int hdfs_crc32c_mailbox_stats(const hdfs_crc32c_mailbox *mb, uint64_t *calls, uint64_t *launches);
 int hdfs_crc32c_mailbox_destroy(hdfs_crc32c_mailbox *mb);
 
