@@ -4,7 +4,7 @@
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 NAME=$1; shift
-OUT=$ROOT/build/ab/$NAME
+OUT=${AB_OUT:-$ROOT/build/ab}/$NAME
 mkdir -p "$OUT"
 C=$ROOT/hadoofus_amd/csrc
 # same flags as hadoofus_amd/build.py (pass extra ones after NAME)
