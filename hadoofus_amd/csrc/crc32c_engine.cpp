@@ -132,6 +132,45 @@ int g_mb_queue = HDFS_KNOB("HDFS_CRC32C_MB_QUEUE", 1);
 unsigned long long *g_diag = nullptr;
 
 
+// The AQL queue a stream's dispatches land on (one tiny dispatch, waited for).
+int stream_queue(hipStream_t s, uint64_t *dq, uint64_t *q) {
+  HIPCHK(launch_queue_probe(dq, s));
+  HIPCHK(hipMemcpyAsync(q, dq, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  return HDFS_CRC32C_OK;
+}
+
+// The streams beside the speculative kernel (t_stream: the short rest of a
+// block; cp_stream: a scatter read's copy) must not share c.stream's
+// hardware queue, or their work waits behind the kernel it was meant to run
+// beside.  The runtime spreads a process's streams over at most
+// GPU_MAX_HW_QUEUES queues per priority level (least used first), so which
+// queue a stream gets depends on what the host process created before: it
+// is probed here (queue_probe_kernel reports the queue a dispatch ran from)
+// and a stream on c.stream's queue is replaced by a CU-masked one over every
+// CU, which the runtime never pools -- a queue of its own (measured:
+// tools/mb_queue_share.py, mailbox stream variant 2).
+int queue_probe_streams(DevCtx &c) {
+  uint64_t *dq = nullptr;
+  HIPCHK(hipMalloc(&dq, sizeof(uint64_t)));
+  int rc = stream_queue(c.stream, dq, &c.q_main);
+  for (int k = 0; k < 2 && !rc; k++) {
+    hipStream_t &s = k == 0 ? c.t_stream : c.cp_stream;
+    uint64_t &q = k == 0 ? c.q_tail : c.q_copy;
+    if ((rc = stream_queue(s, dq, &q))) break;
+    if (q != c.q_main) continue;
+    HIPCHK(hipStreamDestroy(s));
+    s = nullptr;
+    std::vector<uint32_t> mask(size_t((c.num_cu + 31) / 32), 0u);
+    for (int cu = 0; cu < c.num_cu; cu++) mask[size_t(cu / 32)] |= 1u << (cu % 32);
+    HIPCHK(hipExtStreamCreateWithCUMask(&s, uint32_t(mask.size()), mask.data()));
+    if ((rc = stream_queue(s, dq, &q))) break;
+    if (q == c.q_main) rc = fail(HDFS_CRC32C_EHIP, "stream %d shares the engine stream's hardware queue", k);
+  }
+  (void)hipFree(dq);
+  return rc;
+}
+
 int ctx_init(int device, DevCtx **out) {
   int ndev = 0;
   hipError_t e = hipGetDeviceCount(&ndev);
@@ -195,11 +234,9 @@ int ctx_init(int device, DevCtx **out) {
   // synchronous helpers (hipMemcpy/hipMemset) see prior plan work.
   HIPCHK(hipStreamCreate(&c.stream));
   // the short rest of a verified stream runs beside the speculative kernel
-  // on t_stream.  Created right after c.stream: the runtime spreads a
-  // process's streams over at most GPU_MAX_HW_QUEUES hardware queues, and two
-  // streams created one after the other land on different ones (created
-  // later, it shared c.stream's queue in a process with more streams and
-  // waited behind the kernel again)
+  // on t_stream, which must not share c.stream's hardware queue (created
+  // later, it shared it in a process with more streams and waited behind
+  // the kernel again): its queue is probed below (queue_probe_streams)
   HIPCHK(hipStreamCreateWithFlags(&c.t_stream, hipStreamNonBlocking));
   // (and a scatter read's copy beside the same kernel, for the same reason)
   HIPCHK(hipStreamCreateWithFlags(&c.cp_stream, hipStreamNonBlocking));
@@ -207,6 +244,7 @@ int ctx_init(int device, DevCtx **out) {
   HIPCHK(hipMalloc(&c.d_stage, kStageCap));
   HIPCHK(hipMalloc(&c.d_seg, sizeof(SegDev)));
   HIPCHK(hipMalloc(&c.d_small, 64));  // [0] acc [1] first_bad [2..3] mism [8] pool counter
+  if (const int rq = queue_probe_streams(c)) return rq;
   // Small-call input stage.  Large-BAR devices: fine-grained VRAM the host
   // writes through the BAR (64 KiB in ~1.3 us), which the kernels then read
   // from HBM instead of across PCIe; otherwise pinned host memory.
@@ -1546,6 +1584,13 @@ int hdfs_crc32c_mailbox_create(hdfs_crc32c_mailbox **mb, uint32_t idle_ms) {
       HIPCHK(hipStreamCreateWithFlags(&c->mb_stream, hipStreamNonBlocking));
     }
   }
+  if (!c->q_mb) {  // (diagnostics: the queue the resident kernel lands on)
+    uint64_t *dq = nullptr;
+    HIPCHK(hipMalloc(&dq, sizeof(uint64_t)));
+    rc = stream_queue(c->mb_stream, dq, &c->q_mb);
+    (void)hipFree(dq);
+    if (rc) return rc;
+  }
   const uint64_t ms = idle_ms ? idle_ms : 50u;
   c->mb_idle_ticks = uint32_t(std::min<uint64_t>(ms * 100000u, 0xFFFFFFFFu));  // s_memrealtime: 100 MHz
   c->mb_calls = c->mb_launches = 0;
@@ -1607,6 +1652,18 @@ int hdfs_crc32c_diag_stream_queries(uint64_t *out) {
   if (rc) return rc;
   if (!out) return fail(HDFS_CRC32C_EINVAL, "null out");
   *out = c->stream_queries;
+  return HDFS_CRC32C_OK;
+}
+
+int hdfs_crc32c_diag_stream_queues(uint64_t *out4) {
+  DevCtx *c = nullptr;
+  int rc = ctx_init(-1, &c);
+  if (rc) return rc;
+  if (!out4) return fail(HDFS_CRC32C_EINVAL, "null out");
+  out4[0] = c->q_main;
+  out4[1] = c->q_tail;
+  out4[2] = c->q_copy;
+  out4[3] = c->q_mb;
   return HDFS_CRC32C_OK;
 }
 

@@ -40,6 +40,10 @@ hipError_t launch_small_chunks(int mode, const uint8_t *p, uint32_t len, uint32_
                                uint32_t be, const uint32_t *expect, const uint32_t *tab, const uint32_t *kx,
                                uint32_t poly, uint32_t *meta, uint32_t *crcs, uint32_t seq, hipStream_t stream);
 hipError_t launch_prep(uint32_t *fb, uint32_t nfb, unsigned long long *mism, uint32_t *gctr, hipStream_t stream);
+// The hardware queue a stream's dispatches land on: the AQL queue pointer the
+// CP passes the kernel, written to *out (device memory).
+hipError_t launch_queue_probe(uint64_t *out, hipStream_t stream);
+int stream_queue(hipStream_t s, uint64_t *dq, uint64_t *q);
 // Resident mailbox kernel (one workgroup; exits on a quit request or after
 // idle_ticks of 10 ns without one; status[0] = (epoch << 1) | alive).
 hipError_t launch_mailbox(const uint32_t *req, const uint8_t *in, uint32_t *meta, uint32_t *crcs, const uint32_t *tab0,
@@ -267,6 +271,10 @@ struct DevCtx {
   // its stream: beside the speculative kernel, so it starts on the first CU
   // that kernel frees instead of after its last workgroup
   hipStream_t t_stream = nullptr;
+  // AQL queues (amd_queue_t addresses) of stream, t_stream and cp_stream as
+  // probed at init: the streams beside the speculative kernel must not share
+  // its queue (queue_probe_streams)
+  uint64_t q_main = 0, q_tail = 0, q_copy = 0, q_mb = 0;  // (q_mb: the mailbox stream's, once created)
   hipStream_t r_stream = nullptr;  // device framing: record copies of runs with many exceptions
   std::vector<GridSlot> grid;
   // speculative one-launch verify (spec_verify_kernel; guarded by mu): the

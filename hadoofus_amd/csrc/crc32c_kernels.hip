@@ -3991,6 +3991,15 @@ hipError_t read_device_checks(uint32_t out[3], int reset) {
 #endif
 }
 
+__global__ void queue_probe_kernel(uint64_t *out) {
+  if (threadIdx.x == 0) *out = (uint64_t)(unsigned long long)(__builtin_amdgcn_queue_ptr());
+}
+
+hipError_t launch_queue_probe(uint64_t *out, hipStream_t stream) {
+  hipLaunchKernelGGL(queue_probe_kernel, dim3(1), dim3(64), 0, stream, out);
+  return hipGetLastError();
+}
+
 hipError_t launch_header_window(const uint8_t *s, uint64_t len, uint64_t base, uint64_t stride, uint32_t count,
                                 int proto, uint8_t *out, uint64_t *stride_out, hipStream_t stream) {
   if (!count) return hipSuccess;

@@ -97,6 +97,11 @@ int hdfs_crc32c_diag_spec_stats(uint64_t *out4, int reset);
  * earlier work on the engine stream, made only while work no call has seen
  * complete -- an asynchronous plan execute -- is queued before them). */
 int hdfs_crc32c_diag_stream_queries(uint64_t *out);
+/* The hardware (AQL) queues the engine's streams landed on, as probed: out4 =
+ * {engine stream, short-rest stream, copy-beside stream, mailbox stream (0
+ * until a mailbox was created)}.  The two beside streams never share the
+ * engine stream's queue (replaced by a CU-masked stream at init if they did). */
+int hdfs_crc32c_diag_stream_queues(uint64_t *out4);
 /* Device checks: the framing kernels (frame_build, header_window, small_run,
  * grid_finalize) test, in this build, the invariants
  * behind each address they touch (a record slot inside its pass, a packet's bytes inside
