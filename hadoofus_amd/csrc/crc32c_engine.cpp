@@ -150,6 +150,8 @@ int stream_queue(hipStream_t s, uint64_t *dq, uint64_t *q) {
 // and a stream on c.stream's queue is replaced by a CU-masked one over every
 // CU, which the runtime never pools -- a queue of its own (measured:
 // tools/mb_queue_share.py, mailbox stream variant 2).
+// A replacement that cannot be made leaves the stream as it was (slower
+// beside-work, never a failed init).
 int queue_probe_streams(DevCtx &c) {
   uint64_t *dq = nullptr;
   HIPCHK(hipMalloc(&dq, sizeof(uint64_t)));
@@ -159,13 +161,22 @@ int queue_probe_streams(DevCtx &c) {
     uint64_t &q = k == 0 ? c.q_tail : c.q_copy;
     if ((rc = stream_queue(s, dq, &q))) break;
     if (q != c.q_main) continue;
-    HIPCHK(hipStreamDestroy(s));
-    s = nullptr;
     std::vector<uint32_t> mask(size_t((c.num_cu + 31) / 32), 0u);
     for (int cu = 0; cu < c.num_cu; cu++) mask[size_t(cu / 32)] |= 1u << (cu % 32);
-    HIPCHK(hipExtStreamCreateWithCUMask(&s, uint32_t(mask.size()), mask.data()));
-    if ((rc = stream_queue(s, dq, &q))) break;
-    if (q == c.q_main) rc = fail(HDFS_CRC32C_EHIP, "stream %d shares the engine stream's hardware queue", k);
+    hipStream_t own = nullptr;
+    uint64_t q2 = 0;
+    if (hipExtStreamCreateWithCUMask(&own, uint32_t(mask.size()), mask.data()) != hipSuccess) {
+      (void)hipGetLastError();
+      continue;
+    }
+    if ((rc = stream_queue(own, dq, &q2))) break;
+    if (q2 == c.q_main) {
+      (void)hipStreamDestroy(own);
+      continue;
+    }
+    (void)hipStreamDestroy(s);
+    s = own;
+    q = q2;
   }
   (void)hipFree(dq);
   return rc;
