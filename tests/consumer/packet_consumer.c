@@ -14,7 +14,8 @@
  * must -- an I/O error, never a checksum error;
  * (6) reads into host memory from the host and the device stream; (7)
  * verifies three device-resident blocks as asynchronous jobs and as one
- * batch (ABI 5).
+ * batch (ABI 5); (8) reads through a reader; (9) writes a read to a file
+ * descriptor (hdfs_crc32c_read_packets_fd).
  * Prints "0 failures" on success.  Test infrastructure (tests/test_abi.py
  * links it on CPU, tests/test_packets.py runs it on the GPU).
  */
@@ -23,6 +24,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include "hadoofus_crc32c.h"
 
@@ -355,6 +357,30 @@ int main(void)
 			check(memcmp(u1, s + 8 * pk + 31 + crclen + 5, DLEN - 5) == 0 &&
 			    memcmp(u1 + DLEN - 5, s + 9 * pk + 31 + crclen, DLEN) == 0 &&
 			    memcmp(u1 + 2 * DLEN - 5, s + 10 * pk + 31 + crclen, 5) == 0, "reader: bytes");
+		}
+		/* (9) the same client read written to a file descriptor, as
+		 * hdfs_datanode_read_file does (pwrite at fdoffset,
+		 * src/datanode.c:2531-2541), at file offset 100 */
+		{
+			char path[] = "/tmp/hdfs_crc32c_fd_XXXXXX";
+			const int fd = mkstemp(path);
+			check(fd >= 0, "mkstemp");
+			rc = hdfs_crc32c_read_packets_fd((uint8_t *)blk[0] + 8 * pk, total - 8 * pk, HDFS_CRC32C_PROTO_V2, CS,
+			    HDFS_CRC32C_CSUM_CRC32C, 8 * (int64_t)DLEN + 5, 2 * (int64_t)DLEN, fd, 100, rec, NPK + 1, &n, &used,
+			    &delivered);
+			check(rc == 0 && n == 3 && used == 3 * pk && delivered == 2 * DLEN, "fd read: records");
+			memset(u1, 0, 2 * DLEN);
+			check(pread(fd, u1, 2 * DLEN, 100) == (ssize_t)(2 * DLEN), "fd read: pread");
+			check(memcmp(u1, s + 8 * pk + 31 + crclen + 5, DLEN - 5) == 0 &&
+			    memcmp(u1 + 2 * DLEN - 5, s + 10 * pk + 31 + crclen, 5) == 0, "fd read: bytes");
+			/* the read across the bad packet: the bytes before it, then its error */
+			rc = hdfs_crc32c_read_packets_fd((uint8_t *)blk[0] + 3 * pk, total - 3 * pk, HDFS_CRC32C_PROTO_V2, CS,
+			    HDFS_CRC32C_CSUM_CRC32C, 3 * (int64_t)DLEN + 1000, 5 * (int64_t)DLEN, fd, 0, rec, NPK + 1, &n, &used,
+			    &delivered);
+			check(rc == HDFS_CRC32C_ERR_DATANODE_BAD_CHECKSUM && n == 5 && delivered == 4 * DLEN - 1000,
+			    "fd read: ends at the bad packet");
+			close(fd);
+			unlink(path);
 		}
 		for (int b = 0; b < 3; b++)
 			hdfs_crc32c_dev_free(blk[b]);
