@@ -207,6 +207,7 @@ def bind_diag(lib):
     _bind(lib, "hdfs_crc32c_diag_spec_stats", _int, [ctypes.POINTER(_u64), _int])
     _bind(lib, "hdfs_crc32c_diag_stream_queries", _int, [ctypes.POINTER(_u64)])
     _bind(lib, "hdfs_crc32c_diag_stream_queues", _int, [ctypes.POINTER(_u64)])
+    _bind(lib, "hdfs_crc32c_diag_job_queues", _int, [ctypes.POINTER(_u64)])
     return lib
 
 

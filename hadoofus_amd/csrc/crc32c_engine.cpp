@@ -118,6 +118,11 @@ int g_spec = HDFS_KNOB("HDFS_CRC32C_SPEC", 1);
 // 3 (diagnostic A/B) as 1, but a wait that blocks on a running launch sends
 // the queue out behind it only if it holds two runs or more.
 int g_job_coalesce = HDFS_KNOB("HDFS_CRC32C_JOB_COALESCE", 1);
+// Job slot streams: 1 (the product) each on a hardware queue of its own
+// (none of the engine stream's or another slot's: two launches on one queue
+// run back to back, never side by side); 0 (diagnostic A/B) as the runtime
+// places them.
+int g_job_queues = HDFS_KNOB("HDFS_CRC32C_JOB_QUEUES", 1);
 // Small-call input stage: 1 fine-grained VRAM written through the BAR when
 // the device is large-BAR, else (and 0) pinned host memory.
 int g_stage_vram = HDFS_KNOB("HDFS_CRC32C_MB_STAGE", 1);
@@ -150,6 +155,40 @@ int stream_queue(hipStream_t s, uint64_t *dq, uint64_t *q) {
 // and a stream on c.stream's queue is replaced by a CU-masked one over every
 // CU, which the runtime never pools -- a queue of its own (measured:
 // tools/mb_queue_share.py, mailbox stream variant 2).
+int stream_on_own_queue(DevCtx &c, hipStream_t *s, uint64_t *q, const uint64_t *avoid, int n) {
+  *s = nullptr;
+  *q = 0;
+  uint64_t *dq = nullptr;
+  HIPCHK(hipMalloc(&dq, sizeof(uint64_t)));
+  auto shared = [&](uint64_t x) {
+    for (int i = 0; i < n; i++)
+      if (avoid[i] && avoid[i] == x) return true;
+    return false;
+  };
+  int rc = HDFS_CRC32C_OK;
+  if (hipStreamCreateWithFlags(s, hipStreamNonBlocking) != hipSuccess) {
+    (void)hipGetLastError();
+    *s = nullptr;
+    rc = fail(HDFS_CRC32C_EHIP, "stream");
+  } else if (!(rc = stream_queue(*s, dq, q)) && g_job_queues && shared(*q)) {
+    std::vector<uint32_t> mask(size_t((c.num_cu + 31) / 32), 0u);
+    for (int cu = 0; cu < c.num_cu; cu++) mask[size_t(cu / 32)] |= 1u << (cu % 32);
+    hipStream_t own = nullptr;
+    uint64_t q2 = 0;
+    if (hipExtStreamCreateWithCUMask(&own, uint32_t(mask.size()), mask.data()) != hipSuccess) {
+      (void)hipGetLastError();
+    } else if (!stream_queue(own, dq, &q2) && !shared(q2)) {
+      (void)hipStreamDestroy(*s);
+      *s = own;
+      *q = q2;
+    } else {
+      (void)hipStreamDestroy(own);
+    }
+  }
+  (void)hipFree(dq);
+  return rc;
+}
+
 // A replacement that cannot be made leaves the stream as it was (slower
 // beside-work, never a failed init).
 int queue_probe_streams(DevCtx &c) {
@@ -1681,6 +1720,16 @@ int hdfs_crc32c_diag_stream_queues(uint64_t *out4) {
 int hdfs_crc32c_set_speculation(int on) {
   if (on != 0 && on != 1) return fail(HDFS_CRC32C_EINVAL, "speculation 0 or 1");
   g_spec = on;
+  return HDFS_CRC32C_OK;
+}
+
+int hdfs_crc32c_diag_job_queues(uint64_t *out4) {
+  DevCtx *c = nullptr;
+  int rc = ctx_init(-1, &c);
+  if (rc) return rc;
+  if (!out4) return fail(HDFS_CRC32C_EINVAL, "null out");
+  std::lock_guard<std::mutex> lk(c->mu);
+  for (int i = 0; i < kMaxJobs; i++) out4[i] = c->job_slot[i].q;
   return HDFS_CRC32C_OK;
 }
 

@@ -86,6 +86,8 @@ hipError_t launch_spec_verify(const SpecArgs &a, int grid, int copy, hipStream_t
 extern int g_spec;
 // asynchronous jobs: queue and batch (1), launch at submit (0), hold (2)
 extern int g_job_coalesce;
+// job slot streams on hardware queues of their own (1) or as placed (0)
+extern int g_job_queues;
 // diagnostic build: per-wave / per-block s_memrealtime stamps (set_tuning)
 extern unsigned long long *g_diag;
 // frame_build_kernel's stamps sit after the tiled kernel's per-wave words
@@ -162,6 +164,7 @@ struct SpecSlot {
   uint8_t *h = nullptr, *hd = nullptr;
   uint64_t n = 0;
   hipStream_t stream = nullptr;
+  uint64_t q = 0;  // the hardware queue `stream` landed on (job slots: probed when made)
   uint8_t *scratch = nullptr;
   uint64_t scratch_cap = 0;
 };
@@ -337,6 +340,10 @@ struct DevCtx {
 };
 
 extern DevCtx g_ctx[kMaxDev];
+// A non-blocking stream whose hardware queue is none of avoid[0..n): a plain
+// one if the runtime placed it so, else (g_job_queues) a CU-masked one,
+// which the runtime never pools; *q its queue.
+int stream_on_own_queue(DevCtx &c, hipStream_t *s, uint64_t *q, const uint64_t *avoid, int n);
 
 struct DeviceGuard {
   int prev = -1;

@@ -1907,11 +1907,14 @@ JobGroup *group_launch(DevCtx &c, JobQueue &q, const uint8_t *const *streams, co
     return nullptr;
   }
   SpecSlot &S = c.job_slot[slot];
-  if (!S.stream && hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking) != hipSuccess) {
-    (void)hipGetLastError();
-    S.stream = nullptr;
-    *rcp = fail(HDFS_CRC32C_EHIP, "job stream");
-    return nullptr;
+  if (!S.stream) {  // on a hardware queue of its own: launches of different slots overlap
+    uint64_t avoid[kMaxJobs + 1] = {c.q_main};
+    for (int i = 0; i < kMaxJobs; i++) avoid[i + 1] = c.job_slot[i].q;
+    int rq;
+    if ((rq = stream_on_own_queue(c, &S.stream, &S.q, avoid, kMaxJobs + 1))) {
+      *rcp = rq;
+      return nullptr;
+    }
   }
   // per run at most `count` packets; the bitmap takes ceil(chunks / 8) bytes
   // per packet (<= len / 32 + 1), first-bad one word per packet

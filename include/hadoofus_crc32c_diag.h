@@ -102,6 +102,11 @@ int hdfs_crc32c_diag_stream_queries(uint64_t *out);
  * until a mailbox was created)}.  The two beside streams never share the
  * engine stream's queue (replaced by a CU-masked stream at init if they did). */
 int hdfs_crc32c_diag_stream_queues(uint64_t *out4);
+/* The hardware queues of the 4 asynchronous-job slot streams (0: not made
+ * yet).  With HDFS_CRC32C_JOB_QUEUES=1 (default) each is none of the engine
+ * stream's or another slot's: two job launches run side by side, never
+ * back to back on one queue.  Env HDFS_CRC32C_JOB_QUEUES=0: as placed. */
+int hdfs_crc32c_diag_job_queues(uint64_t *out4);
 /* Device checks: the framing kernels (frame_build, header_window, small_run,
  * grid_finalize) test, in this build, the invariants
  * behind each address they touch (a record slot inside its pass, a packet's bytes inside
