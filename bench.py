@@ -617,6 +617,19 @@ def main():
                 extra["device_stream"] = device_stream_bench.block_and_run(plan_GiBps=gib_s)
             except Exception as e:  # reported, never fatal to the headline line
                 extra["device_stream_error"] = repr(e)[:300]
+            # the same stream of blocks from a C caller (a datanode's view,
+            # no Python between the calls): tools/probes/jobs_bench.c
+            exe = os.path.join(ROOT, "tools", "probes", "jobs_bench")
+            if os.path.exists(exe) and "device_stream" in extra:
+                try:
+                    import subprocess
+                    r = subprocess.run([exe], capture_output=True, text=True, timeout=180)
+                    c = json.loads(r.stdout.strip().splitlines()[-1])
+                    for k, us in c["us_per_block"].items():
+                        c.setdefault("frac_of_headline", {})[k] = round((2048 * 65536) / (us * 1e-6) / (1 << 30) / gib_s, 3)
+                    extra["device_stream"]["block_128MiB"]["stream_of_blocks_c"] = c
+                except Exception as e:  # reported, never fatal to the headline line
+                    extra["device_stream"]["stream_of_blocks_c_error"] = repr(e)[:300]
             try:
                 import h2d_bench
                 hr = h2d_bench.measure(8 << 30, (64,), 3)
