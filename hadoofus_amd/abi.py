@@ -204,6 +204,8 @@ def bind_diag(lib):
     _bind(lib, "hdfs_crc32c_diag_device_checks", _int, [ctypes.POINTER(_u32), _int])
     _bind(lib, "hdfs_crc32c_set_speculation", _int, [_int])
     _bind(lib, "hdfs_crc32c_set_job_coalesce", _int, [_int])
+    _bind(lib, "hdfs_crc32c_set_job_early", _int, [_int])
+    _bind(lib, "hdfs_crc32c_diag_job_early", _int, [ctypes.POINTER(_u64), _int])
     _bind(lib, "hdfs_crc32c_diag_spec_stats", _int, [ctypes.POINTER(_u64), _int])
     _bind(lib, "hdfs_crc32c_diag_stream_queries", _int, [ctypes.POINTER(_u64)])
     _bind(lib, "hdfs_crc32c_diag_stream_queues", _int, [ctypes.POINTER(_u64)])

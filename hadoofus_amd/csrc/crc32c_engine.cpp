@@ -118,6 +118,12 @@ int g_spec = HDFS_KNOB("HDFS_CRC32C_SPEC", 1);
 // 3 (diagnostic A/B) as 1, but a wait that blocks on a running launch sends
 // the queue out behind it only if it holds two runs or more.
 int g_job_coalesce = HDFS_KNOB("HDFS_CRC32C_JOB_COALESCE", 1);
+// Coalesced batches: 1 (the product) publish each run's completion and
+// return a job once its own run is done (a clean run in the prediction); 0
+// (diagnostic A/B) jobs return when the whole launch has.
+int g_job_early = HDFS_KNOB("HDFS_CRC32C_JOB_EARLY", 1);
+// jobs of coalesced batches returned {at their run's completion, at the launch's end}
+std::atomic<uint64_t> g_job_early_stats[2];
 // Job slot streams: 1 (the product) each on a hardware queue of its own
 // (none of the engine stream's or another slot's: two launches on one queue
 // run back to back, never side by side); 0 (diagnostic A/B) as the runtime
@@ -1030,13 +1036,13 @@ int chunk_crcs_to_host(const void *data, uint64_t len, uint32_t cs, int ctype, u
 int device_checks(const char *call) {
   if (!kDiag) return HDFS_CRC32C_OK;
   static const char *const kName[] = {"check self-test", "frame_build_kernel (framing)", "frame_build_kernel (table)", "header_window_kernel",
-                                      "small_run_kernel", "grid_finalize_kernel"};
+                                      "small_run_kernel", "grid_finalize_kernel", "spec_verify_kernel (per-run completion)"};
   uint32_t v[3];
   const hipError_t e = read_device_checks(v, 1);
   if (e != hipSuccess) return fail(HDFS_CRC32C_EHIP, "%s: reading the device checks: %s", call, hipGetErrorString(e));
   if (!v[2]) return HDFS_CRC32C_OK;
   return fail(HDFS_CRC32C_EHIP, "%s: device check failed in %s at crc32c_kernels.hip:%u (%u violations)", call,
-              kName[v[0] < 6 ? v[0] : 0], v[1], v[2]);
+              kName[v[0] < 7 ? v[0] : 0], v[1], v[2]);
 }
 
 }  // namespace hdfs_crc32c
@@ -1737,6 +1743,18 @@ int hdfs_crc32c_set_job_coalesce(int mode) {
   if (mode < 0 || mode > 3)
     return fail(HDFS_CRC32C_EINVAL, "job coalescing 0 (off), 1 (product), 2 (hold) or 3 (no lone run behind a launch)");
   g_job_coalesce = mode;
+  return HDFS_CRC32C_OK;
+}
+
+int hdfs_crc32c_set_job_early(int on) {
+  if (on < 0 || on > 1) return fail(HDFS_CRC32C_EINVAL, "per-run completion 0 (off) or 1 (product)");
+  g_job_early = on;
+  return HDFS_CRC32C_OK;
+}
+
+int hdfs_crc32c_diag_job_early(uint64_t *out2, int reset) {
+  if (!out2) return fail(HDFS_CRC32C_EINVAL, "null out");
+  for (int i = 0; i < 2; i++) out2[i] = reset ? g_job_early_stats[i].exchange(0) : g_job_early_stats[i].load();
   return HDFS_CRC32C_OK;
 }
 

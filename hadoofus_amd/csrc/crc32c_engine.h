@@ -86,6 +86,8 @@ hipError_t launch_spec_verify(const SpecArgs &a, int grid, int copy, hipStream_t
 extern int g_spec;
 // asynchronous jobs: queue and batch (1), launch at submit (0), hold (2)
 extern int g_job_coalesce;
+extern int g_job_early;
+extern std::atomic<uint64_t> g_job_early_stats[2];
 // job slot streams on hardware queues of their own (1) or as placed (0)
 extern int g_job_queues;
 // diagnostic build: per-wave / per-block s_memrealtime stamps (set_tuning)

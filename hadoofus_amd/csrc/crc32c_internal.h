@@ -26,6 +26,7 @@ enum DevCheckKernel : uint32_t {
   kDkHeaderWindow = 3,
   kDkSmallRun = 4,
   kDkFinalize = 5,
+  kDkSpecEarly = 6,  // spec_verify_kernel<0, 1>: a workgroup's tiles of a run != what it was said to own
 };
 
 // Segment flags (also mirrored as HDFS_CRC32C_SEG_* in the public header).
@@ -161,7 +162,13 @@ struct SpecCtl {
   uint64_t tail_total;      // its wire size when kGridStop
   uint64_t tail[7];         // its record (hdfs_crc32c_packet) when kGridStop
   uint32_t nexc, pad0;      // exceptions found (entries past kSpecExcMax are not kept: exc is raised)
-  uint64_t pad[20];
+  // a coalesced batch's per-run completion (SpecArgs::early): run r is done
+  // once every workgroup has verified its tiles of r and every header group
+  // of r is checked -- run_done[r] counts both; bit r of run_bad: a header of
+  // run r left the prediction
+  uint32_t run_done[16];
+  uint32_t run_mism[16];    // mismatching chunks of run r
+  uint32_t run_bad, pad1[7];
 };
 static_assert(sizeof(SpecCtl) == 256, "SpecCtl");
 // Pinned host area of one speculative launch: [0, 128) early block, written
@@ -194,17 +201,28 @@ static_assert(sizeof(SpecEarly) == 128 && sizeof(SpecFinal) == 128, "spec host b
 constexpr uint32_t kSpecRunsMax = 16;
 struct SpecRunEarly {
   uint64_t r0[7];           // the run's packet 0 record (stream_off relative to the run's stream)
-  uint32_t count, pad;      // packets of the run this launch verifies
+  uint32_t count;           // packets of the run this launch verifies
+  uint32_t early;           // 1: the run's completion is published (SpecRunDone; no pool tiles in it)
 };
-struct SpecRunTail {        // what follows run r (r >= 1; run 0's is in SpecCtl / SpecFinal)
+static_assert(kSpecRunsMax == 16, "SpecCtl's per-run words");
+struct SpecRunTail {        // what follows run r (the host area's entry 0 only for per-run completion)
   uint64_t rec[7];
   uint64_t total;
-  uint32_t status, pad;
+  uint32_t status, seq;     // seq: the launch's, once the entry is in the host area (per-run completion)
 };
-static_assert(sizeof(SpecRunEarly) == 64 && sizeof(SpecRunTail) == 72, "spec run blocks");
+// Per-run completion of a coalesced batch (SpecArgs::early): the workgroup
+// that completes run r (SpecCtl::run_done) publishes its verdict, sequence
+// number last.  The host returns a job whose run is done, clean (no
+// mismatch) and in the prediction (no header off it) without waiting for
+// the rest of the launch.
+struct SpecRunDone {
+  uint32_t seq, mism, bad, pad;
+};
+static_assert(sizeof(SpecRunEarly) == 64 && sizeof(SpecRunTail) == 72 && sizeof(SpecRunDone) == 16, "spec run blocks");
 constexpr size_t kSpecRunEarlyOff = 256 + size_t(kSpecExcMax) * sizeof(SpecExc);
 constexpr size_t kSpecRunTailOff = kSpecRunEarlyOff + size_t(kSpecRunsMax) * sizeof(SpecRunEarly);
-constexpr size_t kSpecHostBytes = kSpecRunTailOff + size_t(kSpecRunsMax) * sizeof(SpecRunTail);
+constexpr size_t kSpecRunDoneOff = kSpecRunTailOff + size_t(kSpecRunsMax) * sizeof(SpecRunTail);
+constexpr size_t kSpecHostBytes = kSpecRunDoneOff + size_t(kSpecRunsMax) * sizeof(SpecRunDone);
 // Parameters of the closed-form segment table (SpecTab, crc32c_kernels.hip).
 // A batch of runs of `per` packets each: packet k (global) is packet k - r *
 // per of run r = k / per (a multiply-high by um = floor(2^64 / per) + 1,
@@ -218,8 +236,12 @@ struct SpecTabData {
   uint64_t um;
   uint32_t per, pad;
   const uint8_t *crc0r[kSpecRunsMax];
+  // per-run completion (a BATCH launch with SpecArgs::early)
+  SpecCtl *ctl;
+  uint8_t *hdone;               // host area: SpecRunDone[kSpecRunsMax]
+  uint32_t seq, pad1;
 };
-static_assert(sizeof(SpecTabData) == 56 + 16 + 128, "SpecTabData");
+static_assert(sizeof(SpecTabData) == 56 + 16 + 128 + 24, "SpecTabData");
 struct SpecArgs {
   const uint8_t *s;
   uint64_t len, base;
@@ -245,6 +267,7 @@ struct SpecArgs {
   // batch: runs 1 .. nruns - 1 (run 0 is s + base, len - base), verify only
   // (no read window, no copy-out); max_count caps each run
   uint32_t nruns;
+  uint32_t early;           // batch: publish each run's completion (SpecRunDone)
   const uint8_t *xs[kSpecRunsMax];
   uint64_t xlen[kSpecRunsMax];
   SpecRunTail *xtail;       // [2][kSpecRunsMax] by ring slot (device)

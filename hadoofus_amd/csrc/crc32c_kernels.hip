@@ -171,9 +171,56 @@ DEV SegHot seg_hot(SegP segs, uint32_t s) {
 // loop they pushed the kernel past the SGPR budget and into spills.
 // BATCH: the table of a batch of equal runs (spec_verify_kernel<0, 1>); the
 // single-run kernels keep the plain closed form in their hot loop.
+// Per-run completion of a coalesced batch (SpecArgs::early): one more of
+// run r's count -- a workgroup done with its tiles of r, or a header group of
+// r checked.  What it depends on (the run's mismatch count, its header mark)
+// are agent-scope atomics the contributor has waited for (vmcnt) before it
+// counts: relaxed atomics and no fences here -- an agent-scope release /
+// acquire is an L2 write-back and invalidate, once per workgroup and run.
+// The contribution that reaches the run's target publishes the run's
+// verdict to the host as ONE 16-B store {seq, mism, bad} (no fence).
+DEV void spec_run_contribute(SpecCtl *ctl, uint8_t *hdone, uint32_t seq, uint32_t target, uint32_t r) {
+  const uint32_t n = __hip_atomic_fetch_add(&ctl->run_done[r], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (n + 1u != target) return;
+  const uint32_t mism = __hip_atomic_load(&ctl->run_mism[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t bad = (__hip_atomic_load(&ctl->run_bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> r) & 1u;
+  *(volatile GAS u32x4 *)(GAS uint8_t *)(hdone + sizeof(SpecRunDone) * r) = u32x4{seq, mism, bad, 0u};
+}
+
+// LDS words of the per-run completion (BATCH): [0, 16) tiles of run r this
+// workgroup has verified, [16, 32) tiles of run r it owns (kEarlyOff: r has
+// pool tiles, not published), [32, 48) run r's target (workgroups + header
+// groups), [48] the owned tiles' sum, [49] per-run completion on
+constexpr uint32_t kEarlyWords = 50, kEarlyOff = 0xFFFFFFFFu;
+
 template <bool BATCH>
 struct SpecTabT {
   const CAS SpecTabData *p;
+  uint32_t *e;  // BATCH: the per-run completion words (LDS, kEarlyWords)
+  // per-run completion on for this wave: the owned tiles the prologue
+  // restated from the schedule add up to the wave's own static tickets
+  DEV uint32_t early_ok(uint32_t nk) const {
+    if constexpr (BATCH) return rfl(e[49] != 0u && e[48] == nk ? 1u : 0u);
+    return 0u;
+  }
+  // the tile of packet k verified (its last round; byte = its mismatch bits):
+  // counted for its run, and the workgroup's last tile of the run contributes
+  DEV void tile_done(uint32_t k, uint32_t byte, uint32_t lane) const {
+    if constexpr (BATCH) {
+      const uint32_t r = rfl(static_cast<uint32_t>(__umul64hi(static_cast<uint64_t>(k), p->um)));
+      SpecCtl *const ctl = p->ctl;
+      if (byte) {  // rare: the run's mismatches, acknowledged before the tile counts
+        if (lane == 0)
+          __hip_atomic_fetch_add(&ctl->run_mism[r], static_cast<uint32_t>(__builtin_popcount(byte)), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+      }
+      uint32_t old = 0;
+      if (lane == 0) old = __hip_atomic_fetch_add(&e[r], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      old = __builtin_amdgcn_readlane(old, 0);
+      if (old + 1u == rfl(e[16u + r]) && lane == 0) spec_run_contribute(ctl, p->hdone, p->seq, e[32u + r], r);
+    }
+  }
   DEV SegDev operator[](uint32_t k) const {
     SegDev d;
     SpecTabData q;
@@ -218,6 +265,14 @@ struct SpecTabT {
   }
 };
 using SpecTab = SpecTabT<false>;
+template <class Tab>
+struct TabEarly {
+  static constexpr bool value = false;
+};
+template <>
+struct TabEarly<SpecTabT<true>> {
+  static constexpr bool value = true;
+};
 template <bool BATCH>
 DEV SegHot seg_hot(const SpecTabT<BATCH> &t, uint32_t k) {
   const SegDev d = t[k];
@@ -475,6 +530,7 @@ struct LaneConst {
   // the diagnostic build's store-policy experiment (EP::policy); 0 in the
   // release build, where no hook reads it
   uint32_t store_policy;
+  uint32_t early;    // a coalesced batch's per-run completion (TabEarly tables)
 };
 
 // Store / load sites of the tiled kernel's epilogue.  The product kernels
@@ -911,6 +967,8 @@ DEV void finish(const uint32_t *lds, uint32_t exp, const Cursor c, Tab segs, uin
       atomicMin(&first_bad[c.seg], c.tile * kTileChunks + __builtin_ctz(byte));
       atomicAdd(mism, static_cast<unsigned long long>(__builtin_popcount(byte)));
     }
+    if constexpr (TabEarly<Tab>::value)
+      if (last && L.early) segs.tile_done(c.seg, byte, L.lane);
   }
 }
 
@@ -1281,6 +1339,7 @@ DEV void tiles_run(uint32_t *lds, const Tab sg, const SegDev *__restrict__ segs,
   L.ntiles = total_tiles;
   L.gslot = &lds[kLdsWords + 2 + 2 * kSlots];
   L.rmask = 7u;
+  L.early = 0u;
 
   constexpr uint32_t wpb = BLOCK / 64;
   const uint32_t wave = rfl(blockIdx.x * wpb + (threadIdx.x >> 6));
@@ -1360,6 +1419,7 @@ DEV void tiles_run(uint32_t *lds, const Tab sg, const SegDev *__restrict__ segs,
       w.p2first = tile_at_round(sg, nseg, r_static, total_tiles);
     }
     w.ntiles = total_tiles;
+    if constexpr (TabEarly<Tab>::value) L.early = sg.early_ok(w.nk);
     {
       const uint64_t per = (total_tiles - w.p2first) / (4ull * gridDim.x);
       w.ushift = per >= (1ull << kUnitMaxShift) ? kUnitMaxShift
@@ -3073,6 +3133,7 @@ __global__ __launch_bounds__(1024) void spec_verify_kernel(SpecArgs a) {
   __shared__ uint8_t *ep_hout;
   __shared__ SpecRunTail *ep_xtail;
   __shared__ uint32_t ep_seq, ep_nruns;
+  __shared__ uint32_t ecnt[kEarlyWords];  // BATCH: per-run completion (SpecTabT::e)
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
   // diagnostic build: phase stamps of this workgroup (0 entry, 1 tables +
   // packet 0 decoded + closed-form table written, 2 work loop entered, 3
@@ -3244,9 +3305,13 @@ __global__ __launch_bounds__(1024) void spec_verify_kernel(SpecArgs a) {
         q->per = count;
         q->um = count ? ~0ull / count + 1ull : 0ull;
         q->pad = 0u;
+        q->ctl = ctl;
+        q->hdone = a.hout + kSpecRunDoneOff;
+        q->seq = a.seq;
       }
       stores_done();
     }
+    if (BATCH && r < kSpecRunsMax) ecnt[r] = 0u;  // per-run completion: tiles counted per run
   }
   __syncthreads();
   stamp(1);
@@ -3265,6 +3330,59 @@ __global__ __launch_bounds__(1024) void spec_verify_kernel(SpecArgs a) {
   d.stride = rfl64(run.stride);
   d.off0 = rfl64(run.off0);
   d.seq0 = rfl64(run.seq0);
+  if (BATCH && d.eligible) {
+    // Per-run completion (a coalesced batch, a.early): the tiles this
+    // workgroup owns of each run -- tiles_run's schedule 3 dealing restated
+    // (static groups of 2^gshift tiles, gfirst + i * gstride; the pool takes
+    // tiles from p2first on) -- each run's target, and the runs with pool
+    // tiles, which are not published.  Every wave writes the same words
+    // (lane r: run r) before its own tiles; tiles_run checks the
+    // restatement against the wave's own static tickets (early_ok) before
+    // any tile counts.  32-bit: a batch has < 2^31 tiles.
+    const uint32_t cnt0 = rfl(rcount[0]);
+    const uint32_t per_t = cnt0 * d.T, ntl = per_t * nruns;
+    const uint32_t G = gridDim.x, b = blockIdx.x, pmin = (a.tune >> 16) & 0xffu;
+    const bool pool = uint64_t(ntl) * (a.cs / kRoundBytes) >= uint64_t(pmin ? pmin : 32u) * G * 16u;
+    const uint32_t gsh = (a.tune >> 8) & 15u, xm = (a.tune >> 12) & 3u;
+    const uint32_t ng = static_cast<uint32_t>((pool ? uint64_t(ntl) * kPhase1Num / kPhase1Den : ntl) >> gsh);
+    uint32_t gf, gst, nkg, p2;
+    if (xm == 2u && (G % 8u) == 0 && ng >= 8u * (G / 8u)) {
+      const uint32_t ngx = ng / 8u, G8 = G / 8u, l = b / 8u;
+      gf = (b % 8u) * ngx + l;
+      gst = G8;
+      nkg = (ngx - 1u - l) / G8 + 1u;
+      p2 = (ngx * 8u) << gsh;
+    } else {
+      gf = xm != 0u && (G % 8u) == 0 ? (b % 8u) * (G / 8u) + b / 8u : b;
+      gst = G;
+      nkg = ng > gf ? (ng - 1u - gf) / G + 1u : 0u;
+      p2 = ng << gsh;
+    }
+    auto below = [&](uint32_t x) -> uint32_t {  // this workgroup's static groups under group x
+      return x > gf ? min(nkg, (x - gf + gst - 1u) / gst) : 0u;
+    };
+    const bool on = a.early != 0u && nruns > 1u && (per_t & ((1u << gsh) - 1u)) == 0u &&
+                    uint64_t(cnt0) * d.T * nruns < (1ull << 31);
+    const uint32_t r = lane;
+    uint32_t owned = 0, dis = 1;
+    if (r < nruns) {
+      owned = (below(((r + 1u) * per_t) >> gsh) - below((r * per_t) >> gsh)) << gsh;
+      dis = (r + 1u) * per_t > p2 ? 1u : 0u;
+      ecnt[16u + r] = dis ? kEarlyOff : owned;
+      ecnt[32u + r] = G + (rcount[r] + 63u) / 64u;
+    }
+    uint32_t sum = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kSpecRunsMax; i++) sum += __builtin_amdgcn_readlane(owned, i);
+    if (r == 0) {
+      ecnt[48] = sum;
+      ecnt[49] = on ? 1u : 0u;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");  // (this wave's reads of them follow)
+    // a workgroup that owns none of a run's tiles is done with it now
+    if (wv == 0 && on && r < nruns && !dis && owned == 0u)
+      spec_run_contribute(ctl, a.hout + kSpecRunDoneOff, a.seq, G + (rcount[r] + 63u) / 64u, r);
+  }
   // Workgroup 0, last wave: the next launch's control slot zeroed and the
   // early block to the host (which fills the runs' records while the kernel
   // verifies them); then lane 0 the point after each run (where its walk
@@ -3277,6 +3395,16 @@ __global__ __launch_bounds__(1024) void spec_verify_kernel(SpecArgs a) {
 #pragma unroll
       for (int q = 0; q < 7; q++) er->r0[q] = run_r0[lane][q];
       er->count = rcount[lane];
+      er->early = BATCH && ecnt[49] != 0u &&
+                          ecnt[16u + lane] != kEarlyOff ? 1u : 0u;
+    }
+    if (lane < kSpecRunsMax) {
+      // the next launch's per-run words start at zero too -- from every
+      // kernel of the ring, batch or not: the next launch may be a batch
+      SpecCtl *nx = a.ctl + (a.parity ^ 1u);
+      nx->run_done[lane] = 0u;
+      nx->run_mism[lane] = 0u;
+      if (lane == 0) nx->run_bad = 0u;
     }
     if (lane == 0) {
       // the next launch's control slot starts at zero (this launch's was
@@ -3329,6 +3457,18 @@ __global__ __launch_bounds__(1024) void spec_verify_kernel(SpecArgs a) {
         for (int q = 0; q < 7; q++) at_st(&y->rec[q], x[q]);
         at_st(&y->total, ttot);
         at_st32(&y->status, ts);
+        at_st32(&y->seq, a.seq);  // (the final block's copy of the entry keeps the host's sequence number)
+      }
+      if (BATCH && ecnt[49]) {
+        // per-run completion: what follows run r in the host area now, for
+        // a job that returns before the launch ends
+        auto *ht = reinterpret_cast<SpecRunTail *>(a.hout + kSpecRunTailOff) + r;
+#pragma unroll
+        for (int q = 0; q < 7; q++) ht->rec[q] = x[q];
+        ht->total = ttot;
+        ht->status = ts;
+        __threadfence_system();
+        __hip_atomic_store(&ht->seq, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
   }
@@ -3369,23 +3509,11 @@ __global__ __launch_bounds__(1024) void spec_verify_kernel(SpecArgs a) {
       h0[q] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 16u * q, 0, 0));
   }
   stamp(2);
-  const SpecTabT<BATCH != 0> tab{(const CAS SpecTabData *)(a.tabs + blockIdx.x)};
-  const uint64_t tiles = uint64_t(d.count) * d.T;
-  tiles_run<kModeVerify, 3, 1, 3, 1, 1024, 1, COPY, 1, 0>(lds, tab, nullptr, d.count, tiles * (a.cs / kRoundBytes),
-                                                          tiles, a.fb, &ctl->mism, kDiag ? a.stamps : nullptr, a.tune,
-                                                          &ctl->gctr, nullptr, d.T, false);
-  for (uint32_t j = j0; j < ngroups; j += 16u * G) {
+  // a coalesced batch with per-run completion checks a wave's first header
+  // group before its tiles: a run is published only once its headers are
+  const bool hdr_first = BATCH && rfl(ecnt[49]) != 0u;
+  auto check = [&](uint32_t j, const u32x4 (&h)[kSpecHdrBytes / 16]) {
     const uint32_t r = group_run(j), jr = j - rfl(gprefix[r]);
-    u32x4 h[kSpecHdrBytes / 16];
-    if (j == j0) {
-#pragma unroll
-      for (int q = 0; q < int(kSpecHdrBytes / 16); q++) h[q] = h0[q];
-    } else {
-      const __amdgpu_buffer_rsrc_t rs = hdr_rsrc(r, jr);
-#pragma unroll
-      for (int q = 0; q < int(kSpecHdrBytes / 16); q++)
-        h[q] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 16u * q, 0, 0));
-    }
     const uint64_t p0 = rfl64(rP[r]) + uint64_t(64u * jr) * d.stride;
     const uint32_t kr = 64u * jr + lane;
     const uint32_t cnt_r = rfl(rcount[r]);
@@ -3440,6 +3568,34 @@ __global__ __launch_bounds__(1024) void spec_verify_kernel(SpecArgs a) {
       }
       if (!keep) __hip_atomic_fetch_or(&ctl->exc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    if (hdr_first) {
+      // the group's part of its run: a header off the prediction marks the
+      // run (never published), then the group counts (after the mark)
+      if (__ballot(kr < cnt_r && diff != 0u) != 0ull) {  // rare
+        if (lane == 0) __hip_atomic_fetch_or(&ctl->run_bad, 1u << r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        stores_done();
+      }
+      if (lane == 0) spec_run_contribute(ctl, a.hout + kSpecRunDoneOff, a.seq, ecnt[32u + r], r);
+    }
+  };
+  if (hdr_first && j0 < ngroups) check(j0, h0);
+  const SpecTabT<BATCH != 0> tab{(const CAS SpecTabData *)(a.tabs + blockIdx.x), ecnt};
+  const uint64_t tiles = uint64_t(d.count) * d.T;
+  tiles_run<kModeVerify, 3, 1, 3, 1, 1024, 1, COPY, 1, 0>(lds, tab, nullptr, d.count, tiles * (a.cs / kRoundBytes),
+                                                          tiles, a.fb, &ctl->mism, kDiag ? a.stamps : nullptr, a.tune,
+                                                          &ctl->gctr, nullptr, d.T, false);
+  for (uint32_t j = j0; j < ngroups; j += 16u * G) {
+    if (j == j0) {
+      if (!hdr_first) check(j, h0);
+      continue;
+    }
+    u32x4 h[kSpecHdrBytes / 16];
+    const uint32_t r = group_run(j), jr = j - rfl(gprefix[r]);
+    const __amdgpu_buffer_rsrc_t rs = hdr_rsrc(r, jr);
+#pragma unroll
+    for (int q = 0; q < int(kSpecHdrBytes / 16); q++)
+      h[q] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 16u * q, 0, 0));
+    check(j, h);
   }
   // every wave's stores and atomics (mismatch count, exception flag) are
   // acknowledged before its workgroup counts itself done; the last
@@ -3447,6 +3603,11 @@ __global__ __launch_bounds__(1024) void spec_verify_kernel(SpecArgs a) {
   stores_done();
   __syncthreads();
   stamp(3);
+  // diagnostic build: every tile this workgroup verified of a published run
+  // counted, and the count is the prologue's restatement of what it owns
+  // (an owned count too low would publish a run before its last tiles)
+  if (kDiag && BATCH && wv == 0 && lane < nruns && ecnt[49] && ecnt[16u + lane] != kEarlyOff)
+    (void)DCHK(ecnt[lane] == ecnt[16u + lane], kDkSpecEarly);
   if (t < 64u) {
     // wave 0: lane 0 counts the workgroup done; in the last workgroup the
     // wave copies the counters, exceptions and run tails to the host area one

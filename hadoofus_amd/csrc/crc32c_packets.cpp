@@ -815,7 +815,7 @@ struct SpecLaunch {
 int spec_launch(DevCtx &c, SpecSlot &S, hipStream_t st, const uint8_t *d, uint64_t len, uint64_t pos,
                 uint32_t max_count, int proto, uint32_t cs, int ctype, const CopyOut &co, uint64_t done_b, uint8_t *bm,
                 uint32_t *fb, SpecLaunch &L, uint32_t nruns = 1, const uint8_t *const *xs = nullptr,
-                const uint64_t *xlen = nullptr) {
+                const uint64_t *xlen = nullptr, bool per_run = false) {
   int rc = spec_alloc(c, S);
   if (rc) return rc;
   uint64_t left = len - pos;
@@ -857,6 +857,7 @@ int spec_launch(DevCtx &c, SpecSlot &S, hipStream_t st, const uint8_t *d, uint64
   a.tabs = S.tabs;
   a.stamps = kDiag ? g_diag : nullptr;
   a.nruns = nruns;
+  a.early = per_run && nruns > 1 ? 1u : 0u;
   for (uint32_t r = 1; r < nruns; r++) {
     a.xs[r] = xs[r];
     a.xlen[r] = xlen[r];
@@ -997,6 +998,36 @@ struct SpecRunResult {
   uint32_t recorded = 0;
   uint64_t consumed = 0, next = 0;
 };
+// A run's records predicted from its packet 0 (stream offsets from pos0).
+void predict_run(const hdfs_crc32c_packet &r0, uint32_t count, uint64_t stride, uint64_t pos0, hdfs_crc32c_packet *dst) {
+  for (uint32_t k = 0; k < count; k++) {
+    hdfs_crc32c_packet &q = dst[k];
+    q = r0;
+    q.stream_off = pos0 + uint64_t(k) * stride;
+    q.offset_in_block = r0.offset_in_block + int64_t(k) * r0.data_len;
+    q.seqno = r0.seqno + int64_t(k);
+  }
+}
+// What follows a run of `count` packets (the point after it: status, wire
+// size, record) -> its result, and the record that ends the walk at
+// dst[count] when there is one.
+void run_tail(uint32_t count, uint64_t stride, uint64_t pos0, uint32_t status, uint64_t total, const uint64_t *rec,
+              hdfs_crc32c_packet *dst, SpecRunResult &o) {
+  o.taken = true;
+  o.recorded = count;
+  const uint64_t run_end = pos0 + uint64_t(count) * stride;
+  o.consumed = o.next = run_end;
+  if (status == kGridStop) {  // the empty last packet or a framing error ends the walk
+    hdfs_crc32c_packet &t = dst[count];
+    std::memcpy(&t, rec, sizeof(t));
+    if (!t.error) o.consumed = run_end + total;
+    o.recorded++;
+    o.end = true;
+  } else if (status == kGridMore) {  // the stream ends inside the next packet
+    o.end = true;
+  }  // kGridOff (another size) / kGridOn (the pass was cut): the walk goes on at run_end
+}
+
 int spec_collect_batch(SpecSlot &S, const SpecLaunch &L, uint32_t nruns, const uint64_t *pos0,
                        hdfs_crc32c_packet *const *dst, std::vector<SpecRunResult> &res) {
   res.assign(nruns, SpecRunResult{});
@@ -1015,13 +1046,7 @@ int spec_collect_batch(SpecSlot &S, const SpecLaunch &L, uint32_t nruns, const u
   for (uint32_t r = 0; r < nruns; r++) {
     std::memcpy(&r0[r], er[r].r0, sizeof(hdfs_crc32c_packet));
     prefix[r + 1] = prefix[r] + er[r].count;
-    for (uint32_t k = 0; k < er[r].count; k++) {
-      hdfs_crc32c_packet &q = dst[r][k];
-      q = r0[r];
-      q.stream_off = pos0[r] + uint64_t(k) * E.stride;
-      q.offset_in_block = r0[r].offset_in_block + int64_t(k) * r0[r].data_len;
-      q.seqno = r0[r].seqno + int64_t(k);
-    }
+    predict_run(r0[r], er[r].count, E.stride, pos0[r], dst[r]);
   }
   if (prefix[nruns] != E.count) return fail(HDFS_CRC32C_EHIP, "speculative batch: %u packets, runs hold %u", E.count,
                                             prefix[nruns]);
@@ -1084,22 +1109,40 @@ int spec_collect_batch(SpecSlot &S, const SpecLaunch &L, uint32_t nruns, const u
       total = tails[r].total;
       rec = tails[r].rec;
     }
-    SpecRunResult &o = res[r];
-    o.taken = true;
-    o.recorded = er[r].count;
-    const uint64_t run_end = pos0[r] + uint64_t(er[r].count) * E.stride;
-    o.consumed = o.next = run_end;
-    if (status == kGridStop) {
-      hdfs_crc32c_packet &t = dst[r][er[r].count];
-      std::memcpy(&t, rec, sizeof(t));
-      if (!t.error) o.consumed = run_end + total;
-      o.recorded++;
-      o.end = true;
-    } else if (status == kGridMore) {
-      o.end = true;
-    }
+    run_tail(er[r].count, E.stride, pos0[r], status, total, rec, dst[r], res[r]);
   }
   return HDFS_CRC32C_OK;
+}
+
+// Per-run completion of a coalesced batch (SpecArgs::early): run i's
+// results before the launch ends, when its completion is published, clean
+// (no mismatch) and in the prediction (no header off it), and what follows
+// it is in the host area.  1: results in dst / o; 0: not yet; -1: not for
+// this run (mismatches, exceptions, pool tiles, more records than `cap`, or
+// the launch took no run) -- the launch's final block decides it.
+int spec_run_early(const SpecSlot &S, const SpecLaunch &L, uint32_t i, size_t cap, hdfs_crc32c_packet *dst,
+                   SpecRunResult &o) {
+  const auto *early = reinterpret_cast<const SpecEarly *>(S.h);
+  if (__atomic_load_n(&early->seq, __ATOMIC_ACQUIRE) != L.seq) return 0;
+  if (!early->eligible) return -1;
+  const auto *er = reinterpret_cast<const SpecRunEarly *>(S.h + kSpecRunEarlyOff) + i;
+  if (!er->early) return -1;
+  const auto *f = reinterpret_cast<const SpecRunDone *>(S.h + kSpecRunDoneOff) + i;
+  if (__atomic_load_n(&f->seq, __ATOMIC_ACQUIRE) != L.seq) return 0;
+  if (f->mism || f->bad) return -1;
+  const auto *tl = reinterpret_cast<const SpecRunTail *>(S.h + kSpecRunTailOff) + i;
+  if (__atomic_load_n(&tl->seq, __ATOMIC_ACQUIRE) != L.seq) return 0;
+  SpecRunEarly e;
+  SpecRunTail t;
+  std::memcpy(&e, er, sizeof(e));
+  std::memcpy(&t, tl, sizeof(t));
+  if (size_t(e.count) + (t.status == kGridStop ? 1u : 0u) > cap) return -1;
+  hdfs_crc32c_packet r0;
+  std::memcpy(&r0, e.r0, sizeof(r0));
+  predict_run(r0, e.count, early->stride, 0, dst);
+  o = SpecRunResult{};
+  run_tail(e.count, early->stride, 0, t.status, t.total, t.rec, dst, o);
+  return 1;
 }
 
 // A synchronous speculative pass on the engine stream.
@@ -1894,13 +1937,15 @@ int group_collect(DevCtx &c, JobQueue &q, JobGroup *g) {
 // launch on a free job slot -- collecting the oldest running launch first
 // when all slots are busy.  -> the group (refs 0), or null with rc set.
 JobGroup *group_launch(DevCtx &c, JobQueue &q, const uint8_t *const *streams, const uint64_t *lens, uint32_t m,
-                       int proto, uint32_t cs, int ctype, size_t max_pkts, int *rcp) {
+                       int proto, uint32_t cs, int ctype, size_t max_pkts, int *rcp, bool early) {
   int slot = -1;
   for (;;) {
     for (int i = 0; i < kMaxJobs && slot < 0; i++)
       if (!c.job_busy[i]) slot = i;
     if (slot >= 0 || q.running.empty()) break;
-    (void)group_collect(c, q, q.running.front());  // (its status stays with its jobs)
+    JobGroup *old = q.running.front();
+    (void)group_collect(c, q, old);  // (its status stays with its jobs)
+    if (old->refs == 0) delete old;  // every job of it returned before the launch ended
   }
   if (slot < 0) {
     *rcp = fail(HDFS_CRC32C_EHIP, "no free job slot");
@@ -1947,7 +1992,7 @@ JobGroup *group_launch(DevCtx &c, JobQueue &q, const uint8_t *const *streams, co
   g->m = m;
   g->per = size_t(count) + 1;
   int rc = spec_launch(c, S, S.stream, streams[0], lens[0], 0, count, proto, cs, ctype, CopyOut{}, 0, S.scratch,
-                       reinterpret_cast<uint32_t *>(S.scratch + bm_cap), g->L, m, streams, lens);
+                       reinterpret_cast<uint32_t *>(S.scratch + bm_cap), g->L, m, streams, lens, early);
   if (rc) {
     delete g;
     *rcp = rc;
@@ -1972,7 +2017,7 @@ void queue_flush(DevCtx &c, JobQueue &q) {
   }
   int rc = 0;
   JobGroup *g = group_launch(c, q, s.data(), l.data(), uint32_t(s.size()), q.key.proto, q.key.cs, q.key.ctype,
-                             q.key.max_pkts, &rc);
+                             q.key.max_pkts, &rc, g_job_early != 0);
   for (size_t r = 0; r < q.pending.size(); r++) {
     hdfs_crc32c_job *j = q.pending[r];
     j->queued = false;
@@ -2043,7 +2088,7 @@ int job_submit(const uint8_t *const *runs, const uint64_t *lens, size_t n, bool 
       s.push_back(runs[b]);
       l.push_back(lens[b]);
     }
-    JobGroup *grp = group_launch(c, q, s.data(), l.data(), uint32_t(s.size()), proto, cs, ctype, max_pkts, &rc);
+    JobGroup *grp = group_launch(c, q, s.data(), l.data(), uint32_t(s.size()), proto, cs, ctype, max_pkts, &rc, false);
     if (grp) {
       j->grp = grp;
       grp->refs = 1;
@@ -2077,25 +2122,57 @@ int job_wait(hdfs_crc32c_job *j, hdfs_crc32c_packet *pkts, size_t max_pkts, size
     hdfs_crc32c_job *j;
     ~Release() {
       q.outstanding--;
-      if (j->grp && --j->grp->refs == 0) delete j->grp;
+      // (a launch still running when its last job returns early is deleted
+      // once collected: group_launch)
+      if (j->grp && --j->grp->refs == 0 && j->grp->collected) delete j->grp;
       delete j;
     }
   } rel{q, j};
   if (j->queued) queue_flush(c, q);  // this job's run goes out now, with every queued one
   JobGroup *grp = j->grp;
-  if (grp && !grp->collected) {
-    // the queue goes out behind the running launch (diagnostic mode 3: only
-    // two runs or more; a single one waits for the next submit or wait)
-    if (!q.pending.empty() && (g_job_coalesce != 3 || q.pending.size() >= 2) && !group_done(c, *grp))
-      queue_flush(c, q);
-    group_collect(c, q, grp);
-  }
-  if (grp && grp->rc) return grp->rc;
   const size_t n = j->runs.size();
   const size_t cap = std::min(max_pkts, j->max_pkts);
   std::vector<SpecRunResult> res(n);
+  bool early_done = false;
+  if (grp && !grp->collected) {
+    // the queue goes out behind the running launch (diagnostic mode 3: only
+    // two runs or more; a single one waits for the next submit or wait)
+    auto flush = [&] {
+      if (!q.pending.empty() && (g_job_coalesce != 3 || q.pending.size() >= 2) && !grp->collected && !group_done(c, *grp))
+        queue_flush(c, q);
+    };
+    if (g_job_early && j->grp_run + 1 < grp->m && !j->batch && j->sel.size() == 1) {
+      // Per-run completion: the job of a run before the launch's last
+      // returns once its own run is published, while the launch verifies
+      // the runs after it.  The queue goes out when the wait is on the
+      // launch's last run (the caller submits the jobs the earlier returns
+      // make room for meanwhile: they go out together), which also collects
+      // the launch, or on a run that will not be published.
+      const uint32_t i = j->grp_run;
+      hdfs_crc32c_packet *dst = pkts + j->sel[0] * max_pkts;
+      const auto t0 = std::chrono::steady_clock::now();
+      for (uint32_t spin = 0; !grp->collected && !group_done(c, *grp); spin++) {
+        const int e = spec_run_early(c.job_slot[grp->slot], grp->L, i, cap, dst, res[j->sel[0]]);
+        if (e > 0) {
+          early_done = true;
+          break;
+        }
+        if (e < 0) break;
+        if ((spin & 255u) == 255u && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
+#if defined(__x86_64__) || defined(__i386__)
+        __builtin_ia32_pause();
+#endif
+      }
+      g_job_early_stats[early_done ? 0 : 1]++;
+    }
+    if (!early_done) {
+      flush();
+      if (!grp->collected) group_collect(c, q, grp);
+    }
+  }
+  if (grp && grp->rc && !early_done) return grp->rc;
   bool allow_spec = true;
-  if (grp) {
+  if (grp && !early_done) {
     // the launch's records (count + 1 per run), into the caller's array at
     // the run's block
     for (size_t r = 0; r < j->sel.size(); r++) {

@@ -318,7 +318,11 @@ int hdfs_crc32c_read_packets(const void *stream, uint64_t len, int proto, uint32
  * idle, when a wait needs a queued job or would block on a running launch,
  * or at 16 queued runs or a run of another length or layout -- so a stream
  * of blocks pays the launch's fixed cost once per batch; up to 4 launches
- * run at once (a submit or wait may first collect the oldest).  A run of
+ * run at once (a submit or wait may first collect the oldest).  The wait
+ * on a job of such a batch returns as soon as its own block is verified --
+ * clean, its headers the predicted ones -- while the launch verifies the
+ * blocks after it (the wait on the batch's last block, or on a block with a
+ * bad chunk or an irregular header, returns with the launch).  A run of
  * equal packets is verified by the speculative launch; whatever it does not take
  * (another packet size, more than 65 536 packets, no run at all) is framed
  * and verified inside the wait.  The stream's bytes must stay unchanged, and

@@ -89,6 +89,16 @@ int hdfs_crc32c_set_speculation(int on);
  * launch sends the queue out behind it only if it holds two runs or more.
  * Env HDFS_CRC32C_JOB_COALESCE. */
 int hdfs_crc32c_set_job_coalesce(int mode);
+/* Per-run completion of coalesced batches: 1 (default, the product) a job
+ * whose run is done -- verified clean, its headers in the prediction --
+ * returns while the batch launch verifies the runs after it; 0 every job
+ * waits for its whole launch (for same-process A/Bs).  Env
+ * HDFS_CRC32C_JOB_EARLY. */
+int hdfs_crc32c_set_job_early(int on);
+/* Waits on jobs of coalesced batches (with per-run completion on): out2 =
+ * {returned at their run's completion, returned at the launch's end};
+ * reset != 0 clears them. */
+int hdfs_crc32c_diag_job_early(uint64_t *out2, int reset);
 /* Speculative one-launch verifies since the last reset: out4 = {launches,
  * eligible (packet 0 starts a run of equal packets), taken (no header off
  * the prediction), header exceptions}; reset != 0 clears them. */
