@@ -3584,17 +3584,18 @@ __global__ __launch_bounds__(1024) void spec_verify_kernel(SpecArgs a) {
   tiles_run<kModeVerify, 3, 1, 3, 1, 1024, 1, COPY, 1, 0>(lds, tab, nullptr, d.count, tiles * (a.cs / kRoundBytes),
                                                           tiles, a.fb, &ctl->mism, kDiag ? a.stamps : nullptr, a.tune,
                                                           &ctl->gctr, nullptr, d.T, false);
-  for (uint32_t j = j0; j < ngroups; j += 16u * G) {
-    if (j == j0) {
-      if (!hdr_first) check(j, h0);
-      continue;
-    }
+  for (uint32_t j = hdr_first ? j0 + 16u * G : j0; j < ngroups; j += 16u * G) {
     u32x4 h[kSpecHdrBytes / 16];
-    const uint32_t r = group_run(j), jr = j - rfl(gprefix[r]);
-    const __amdgpu_buffer_rsrc_t rs = hdr_rsrc(r, jr);
+    if (j == j0) {
 #pragma unroll
-    for (int q = 0; q < int(kSpecHdrBytes / 16); q++)
-      h[q] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 16u * q, 0, 0));
+      for (int q = 0; q < int(kSpecHdrBytes / 16); q++) h[q] = h0[q];
+    } else {
+      const uint32_t r = group_run(j), jr = j - rfl(gprefix[r]);
+      const __amdgpu_buffer_rsrc_t rs = hdr_rsrc(r, jr);
+#pragma unroll
+      for (int q = 0; q < int(kSpecHdrBytes / 16); q++)
+        h[q] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 16u * q, 0, 0));
+    }
     check(j, h);
   }
   // every wave's stores and atomics (mismatch count, exception flag) are
