@@ -27,7 +27,7 @@ import sys
 import numpy as np
 import pytest
 
-from packet_stream import CSUM_CRC32C, build_stream
+from packet_stream import CSUM_CRC32, CSUM_CRC32C, build_stream
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -100,6 +100,35 @@ def test_gpu_jobs_per_run_dealings(engine, oracle, xcd, gshift):
         assert got[k] == want[k], (xcd, gshift, k)
     assert checks == (0, 0, 0), checks
     assert sum(early) <= 5, early  # (the last run's wait collects the launch)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("proto,cs,ctype,last_empty", [(2, 4096, CSUM_CRC32C, True), (2, 1024, CSUM_CRC32, True),
+                                                       (1, 512, CSUM_CRC32, False), (2, 2048, CSUM_CRC32C, True)])
+def test_gpu_jobs_per_run_layouts(engine, oracle, proto, cs, ctype, last_empty):
+    """Other layouts in one batch (tiles of several rounds at 1-4 KiB chunks,
+    CRC32, the v1 protocol): bad chunks at the last tile of block 1 and the
+    first of block 3; every job the oracle's, no device check."""
+    diag = _diag()
+    nch = 65536 // cs
+    streams = [build_stream(oracle.crc32c, proto, cs, ctype, [65536] * 100, seed=500 + k, last_empty=last_empty,
+                            corrupt=[(99, nch - 1)] if k == 1 else [(0, 0)] if k == 3 else [])[0] for k in range(5)]
+    want = [oracle.verify_packets(s, proto=proto, chunk_size=cs, ctype=ctype) for s in streams]
+    assert want[1][0] != 0 and want[3][0] != 0 and want[0][0] == 0
+    bufs = [_dev(engine, s) for s in streams]
+    assert diag.hdfs_crc32c_set_job_coalesce(2) == 0
+    try:
+        _checks(diag)
+        jobs = [engine.VerifyJob(b.ptr, len(s), proto=proto, chunk_size=cs, ctype=ctype, lib=diag)
+                for b, s in zip(bufs, streams)]
+        got = [j.wait() for j in jobs]
+        checks = _checks(diag)
+    finally:
+        diag.hdfs_crc32c_set_job_coalesce(1)
+    for b in bufs:
+        b.free()
+    assert got == want
+    assert checks == (0, 0, 0), checks
 
 
 @pytest.mark.gpu
@@ -179,7 +208,7 @@ import diaglib
 import hadoofus_amd as h
 lib = h.abi.bind_diag(h.load(diaglib.DIAG_LIB_PATH))
 from oracle import Oracle
-from packet_stream import CSUM_CRC32C, build_stream
+from packet_stream import CSUM_CRC32, CSUM_CRC32C, build_stream
 o = Oracle()
 streams = [build_stream(o.crc32c, 2, 512, CSUM_CRC32C, [65536] * 100, seed=400 + k,
                         corrupt=[(99, 127)] if k == 6 else [])[0] for k in range(8)]
