@@ -243,3 +243,50 @@ def test_gpu_jobs_per_run_with_pool():
     assert out["same"], out
     assert out["checks"] == [0, 0, 0], out
     assert sum(out["early"]) >= 1, out
+
+
+@pytest.mark.gpu
+def test_gpu_jobs_threads(engine, oracle):
+    """A datanode's receiver threads: 4 threads, each verifying its own 6
+    blocks as jobs with 2 outstanding (their jobs share batch launches and
+    per-run completions), while a fifth makes synchronous calls on other
+    blocks: every result the oracle's, no device check."""
+    import threading
+    diag = _diag()
+    streams = [_block(oracle, k, corrupt=[(99, 127)] if k % 5 == 2 else []) for k in range(28)]
+    want = [oracle.verify_packets(s) for s in streams]
+    bufs = [_dev(engine, s) for s in streams]
+    got, errs = {}, []
+
+    def receiver(ks):
+        try:
+            q = []
+            for k in ks:
+                if len(q) == 2:
+                    k0, j0 = q.pop(0)
+                    got[k0] = j0.wait()
+                q.append((k, engine.VerifyJob(bufs[k].ptr, len(streams[k]), lib=diag)))
+            for k0, j0 in q:
+                got[k0] = j0.wait()
+        except Exception as e:  # reported below
+            errs.append(repr(e))
+
+    def sync_caller(ks):
+        try:
+            for k in ks:
+                got[k] = engine.verify_packets(None, dptr=bufs[k].ptr, nbytes=len(streams[k]), lib=diag)
+        except Exception as e:
+            errs.append(repr(e))
+
+    _checks(diag)
+    th = [threading.Thread(target=receiver, args=(range(6 * t, 6 * t + 6),)) for t in range(4)]
+    th.append(threading.Thread(target=sync_caller, args=(range(24, 28),)))
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    for b in bufs:
+        b.free()
+    assert not errs, errs
+    assert [got[k] for k in range(28)] == want
+    assert _checks(diag) == (0, 0, 0)
