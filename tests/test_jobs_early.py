@@ -290,3 +290,29 @@ def test_gpu_jobs_threads(engine, oracle):
     assert not errs, errs
     assert [got[k] for k in range(28)] == want
     assert _checks(diag) == (0, 0, 0)
+
+
+@pytest.mark.gpu
+def test_gpu_jobs_per_run_wait_room(engine, oracle):
+    """A wait whose record array is smaller than the run (less room than at
+    the submit) fails with EINVAL whether or not the run completed early --
+    as without per-run completion -- and the batch's other jobs are
+    unaffected."""
+    diag = _diag()
+    streams = [_block(oracle, k) for k in range(4)]
+    want = [oracle.verify_packets(s) for s in streams]
+    bufs = [_dev(engine, s) for s in streams]
+    assert diag.hdfs_crc32c_set_job_coalesce(2) == 0
+    try:
+        jobs = [engine.VerifyJob(b.ptr, len(s), lib=diag) for b, s in zip(bufs, streams)]
+        small = (engine.Packet * 50)()
+        n, used = ctypes.c_size_t(0), ctypes.c_uint64(0)
+        job, jobs[1].job = jobs[1].job, None
+        rc = diag.hdfs_crc32c_job_wait(job, small, 50, ctypes.byref(n), ctypes.byref(used))
+        got = {k: jobs[k].wait() for k in (0, 2, 3)}
+    finally:
+        diag.hdfs_crc32c_set_job_coalesce(1)
+    for b in bufs:
+        b.free()
+    assert rc == -1, rc  # HDFS_CRC32C_EINVAL
+    assert all(got[k] == want[k] for k in (0, 2, 3))
