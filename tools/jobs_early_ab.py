@@ -4,7 +4,11 @@ blocks as jobs (4 / 8 / 16 outstanding) and as batches, each setting in
 fresh processes, alternated over `rounds`; the jobs that returned at their
 run's completion / at the launch's end reported per process.
 
-    python tools/jobs_early_ab.py OUT.json [rounds]"""
+    python tools/jobs_early_ab.py OUT.json [rounds] [VAR=a,b]
+
+VAR=a,b: the same stream A/B over another environment knob of the
+diagnostic build instead (e.g. HDFS_CRC32C_SPEC_POOL=32,16: the rounds per
+wave from which the speculative kernels use the global pool)."""
 import ctypes
 import json
 import os
@@ -35,10 +39,14 @@ def main():
         return
     out_path = sys.argv[1]
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 3
-    res = {"0": [], "1": []}
+    var, vals = "HDFS_CRC32C_JOB_EARLY", ("0", "1")
+    if len(sys.argv) > 3:
+        var, v = sys.argv[3].split("=")
+        vals = tuple(v.split(","))
+    res = {v: [] for v in vals}
     for r in range(rounds):
-        for v in (("0", "1") if r % 2 == 0 else ("1", "0")):
-            env = dict(os.environ, HDFS_CRC32C_JOB_EARLY=v)
+        for v in (vals if r % 2 == 0 else vals[::-1]):
+            env = dict(os.environ, **{var: v})
             p = subprocess.run([sys.executable, os.path.abspath(__file__), "--case"], env=env, capture_output=True,
                                text=True, timeout=200)
             if p.returncode:
@@ -46,8 +54,8 @@ def main():
                 sys.exit(p.returncode)
             o = json.loads(p.stdout.strip().splitlines()[-1])
             res[v].append(o)
-            print(json.dumps({"round": r, "job_early": v, **o}), flush=True)
-    keys = res["0"][0]["us_per_block"].keys()
+            print(json.dumps({"round": r, var: v, **o}), flush=True)
+    keys = res[vals[0]][0]["us_per_block"].keys()
     summary = {v: {k: round(statistics.median(o["us_per_block"][k] for o in res[v]), 1) for k in keys} for v in res}
     with open(out_path, "w") as f:
         json.dump({"summary_median_us_per_block": summary, "runs": res}, f, indent=1)
