@@ -620,16 +620,19 @@ def main():
             # the same stream of blocks from a C caller (a datanode's view,
             # no Python between the calls): tools/probes/jobs_bench.c
             exe = os.path.join(ROOT, "tools", "probes", "jobs_bench")
+            # (16 blocks, as the Python stream above; and 64, where a stream's
+            # first and last lone launches weigh a quarter as much)
             if os.path.exists(exe) and "device_stream" in extra:
-                try:
-                    import subprocess
-                    r = subprocess.run([exe], capture_output=True, text=True, timeout=180)
-                    c = json.loads(r.stdout.strip().splitlines()[-1])
-                    for k, us in c["us_per_block"].items():
-                        c.setdefault("frac_of_headline", {})[k] = round((2048 * 65536) / (us * 1e-6) / (1 << 30) / gib_s, 3)
-                    extra["device_stream"]["block_128MiB"]["stream_of_blocks_c"] = c
-                except Exception as e:  # reported, never fatal to the headline line
-                    extra["device_stream"]["stream_of_blocks_c_error"] = repr(e)[:300]
+                for nb, key in ((16, "stream_of_blocks_c"), (64, "stream_of_64_blocks_c")):
+                    try:
+                        import subprocess
+                        r = subprocess.run([exe, str(nb)], capture_output=True, text=True, timeout=180)
+                        c = json.loads(r.stdout.strip().splitlines()[-1])
+                        for k, us in c["us_per_block"].items():
+                            c.setdefault("frac_of_headline", {})[k] = round((2048 * 65536) / (us * 1e-6) / (1 << 30) / gib_s, 3)
+                        extra["device_stream"]["block_128MiB"][key] = c
+                    except Exception as e:  # reported, never fatal to the headline line
+                        extra["device_stream"][key + "_error"] = repr(e)[:300]
             try:
                 import h2d_bench
                 hr = h2d_bench.measure(8 << 30, (64,), 3)

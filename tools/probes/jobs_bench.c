@@ -1,5 +1,6 @@
 /*
- * A datanode's stream of received blocks in C (GPU box): 16 device-resident
+ * A datanode's stream of received blocks in C (GPU box): NB (argv[1], 16 by
+ * default, at most 64) device-resident
  * 128 MiB block transfers (2 048 v2 packets of 64 KiB + the empty last one,
  * composed by hdfs_crc32c_compose_packets from device-filled data), verified
  *   - synchronously, one hdfs_crc32c_verify_packets per block;
@@ -19,7 +20,7 @@
 
 #include "hadoofus_crc32c.h"
 
-#define NB 16
+#define NBMAX 64
 #define BLOCK (128ull << 20)
 
 static double now_us(void)
@@ -31,8 +32,10 @@ static double now_us(void)
 
 #define CHK(x) do { int rc_ = (x); if (rc_ < 0) { fprintf(stderr, "%s: %d %s\n", #x, rc_, hdfs_crc32c_last_error()); exit(1); } } while (0)
 
-int main(void)
+int main(int argc, char **argv)
 {
+	const int NB = argc > 1 ? atoi(argv[1]) : 16;
+	if (NB < 8 || NB > NBMAX || NB % 8) { fprintf(stderr, "blocks: a multiple of 8 in [8, %d]\n", NBMAX); return 1; }
 	/* one block's wire image, built on the host from composed headers */
 	void *ddata = NULL;
 	CHK(hdfs_crc32c_dev_alloc(&ddata, BLOCK));
@@ -57,8 +60,8 @@ int main(void)
 		memcpy(wire + w, data + op[i].data_off, (size_t)op[i].data_len);
 		w += (uint64_t)op[i].data_len;
 	}
-	void *blk[NB];
-	uint64_t blen[NB];
+	void *blk[NBMAX];
+	uint64_t blen[NBMAX];
 	for (int b = 0; b < NB; b++) {
 		CHK(hdfs_crc32c_dev_alloc(&blk[b], wlen));
 		CHK(hdfs_crc32c_memcpy(blk[b], wire, wlen, 0));
@@ -67,9 +70,9 @@ int main(void)
 	CHK(hdfs_crc32c_device_sync());
 	const size_t maxpk = npk + 8;
 	hdfs_crc32c_packet *rec = calloc(NB * maxpk, sizeof(*rec));
-	size_t n = 0, bn[NB];
-	uint64_t used = 0, bused[NB];
-	int brc[NB];
+	size_t n = 0, bn[NBMAX];
+	uint64_t used = 0, bused[NBMAX];
+	int brc[NBMAX];
 	double best[6] = {1e18, 1e18, 1e18, 1e18, 1e18, 1e18};
 	for (int rep = 0; rep < 6; rep++) {
 		double t0 = now_us();
@@ -103,12 +106,17 @@ int main(void)
 			if (rep && t < best[1 + k]) best[1 + k] = t;
 		}
 		t0 = now_us();
-		{
-			hdfs_crc32c_job *bj[2];
-			for (int g = 0; g < 2; g++)
+		{  /* batches of 8 blocks, two in flight */
+			hdfs_crc32c_job *bj[NBMAX / 8];
+			for (int g = 0; g < NB / 8; g++) {
+				if (g >= 2) {
+					int rc = hdfs_crc32c_job_wait_blocks(bj[g - 2], rec, maxpk, bn, bused, brc);
+					if (rc != 0 || bn[0] != npk) { fprintf(stderr, "blocks %d\n", rc); return 1; }
+				}
 				CHK(hdfs_crc32c_verify_blocks_submit((const void *const *)(blk + 8 * g), blen + 8 * g, 8,
 				    HDFS_CRC32C_PROTO_V2, 512, HDFS_CRC32C_CSUM_CRC32C, maxpk, &bj[g]));
-			for (int g = 0; g < 2; g++) {
+			}
+			for (int g = NB / 8 - 2; g < NB / 8; g++) {
 				int rc = hdfs_crc32c_job_wait_blocks(bj[g], rec, maxpk, bn, bused, brc);
 				if (rc != 0 || bn[0] != npk) { fprintf(stderr, "blocks %d\n", rc); return 1; }
 			}
