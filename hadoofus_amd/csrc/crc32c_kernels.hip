@@ -3312,6 +3312,7 @@ __global__ __launch_bounds__(1024) void spec_verify_kernel(SpecArgs a) {
       stores_done();
     }
     if (BATCH && r < kSpecRunsMax) ecnt[r] = 0u;  // per-run completion: tiles counted per run
+    if (BATCH && r == 0) ecnt[49] = 0u;           // (off until every wave has restated the dealing)
   }
   __syncthreads();
   stamp(1);
